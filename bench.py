@@ -1,0 +1,246 @@
+"""Benchmark: multi-cam frames/sec (7-cam -> 480x1440 BEV) on MI355X.
+
+Workload = BASELINE.json configs[1]: Wildtrack-shaped 7 cameras x 3 x 1080 x
+1920 fp32 images -> ResNet-50 (timm features_only, out_index=2, stride 8) ->
+1x1 proj to C=64 -> IPM warp onto the 480x1440 ground grid -> mean fusion
+over views.  One step = one batch of B frames through that whole hot path
+(CNNEncoder.forward + GeometryTransformer.forward_fused), inputs resident in
+HBM, random-init weights of that architecture, synthetic images, the fixed
+Appendix-B camera rig.
+
+Multi-GPU (torchrun, one process per GPU): frames are independent, so each
+rank runs its own B frames with no data-path collective (weak scaling); only
+the timing barrier and a MAX-reduction of the elapsed time cross ranks.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a
+`roofline` object for the dominant kernel family (backbone convs on fp32
+MFMA), `roofline_warp` for the IPM warp kernel (HBM-bound), and a
+`cpu_baseline` (the reference's torch-CPU composition, timed on this host on
+a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "vision-based-spatio-temporal-analysis_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bev_rig  # noqa: E402
+
+BOUNDS = (-24.0, 24.0, -7.2, 7.2)
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_F32_MFMA_TF = 157.3  # MI355X fp32 matrix spec (= vector peak)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step")
+    ap.add_argument("--views", type=int, default=7)
+    ap.add_argument("--channels", type=int, default=64)
+    ap.add_argument("--backbone", default="resnet50")
+    ap.add_argument("--img", type=int, nargs=2, default=(1080, 1920))
+    ap.add_argument("--bev", type=int, nargs=2, default=(480, 1440))
+    ap.add_argument("--cpu-iters", type=int, default=2, help="frames timed for the CPU baseline (0 = skip)")
+    ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
+    return ap.parse_args()
+
+
+def backbone_flops(enc, H, W):
+    """2 * MACs of every conv executed per image (stem..out_index + proj)."""
+    import torch.nn as nn
+    net = enc.backbone
+    total = 0
+
+    def conv(c: nn.Conv2d, h, w):
+        ho = (h + 2 * c.padding[0] - c.kernel_size[0]) // c.stride[0] + 1
+        wo = (w + 2 * c.padding[1] - c.kernel_size[1]) // c.stride[1] + 1
+        return 2 * ho * wo * c.out_channels * c.in_channels * c.kernel_size[0] * c.kernel_size[1], ho, wo
+
+    if not enc._use_timm:
+        f0, h, w = conv(net[0], H, W)
+        f1, h, w = conv(net[2], h, w)
+        return f0 + f1
+    f, h, w = conv(net.conv1, H, W)
+    total += f
+    h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1
+    for li, layer in enumerate((net.layer1, net.layer2, net.layer3, net.layer4), start=1):
+        if li > enc.out_index:
+            break
+        for blk in layer:
+            hi, wi = h, w
+            for c, _, _ in blk.convs():
+                f, h, w = conv(c, h, w)
+                total += f
+            if blk.downsample is not None:
+                total += conv(blk.downsample[0], hi, wi)[0]
+    total += 2 * h * w * enc.proj.in_channels * enc.proj.out_channels
+    return total
+
+
+def warp_alg_bytes(geom, H, feats_shape, img, B, V):
+    """out bytes + distinct touched source bytes, counted from the real taps."""
+    import bev_native as nat
+    _, _, C, Hf, Wf = feats_shape
+    xs, ys = geom._device_axes(H.device)
+    x0y0, _, valid = nat.taps(H, xs, ys, Hf, Wf, img)
+    touched = 0
+    for n in range(H.shape[0]):
+        m = torch.zeros(Hf + 1, Wf + 1, dtype=torch.bool, device=H.device)
+        v = valid[n].to(torch.int32)
+        x0 = x0y0[n, ..., 0].long()
+        y0 = x0y0[n, ..., 1].long()
+        for bit, dx, dy in ((1, 0, 0), (2, 1, 0), (4, 0, 1), (8, 1, 1)):
+            sel = (v & bit) > 0
+            m[(y0 + dy)[sel], (x0 + dx)[sel]] = True
+        touched += int(m.sum().item())
+    out_bytes = 4 * C * geom.bev_h * geom.bev_w * B
+    return out_bytes + 4 * C * touched, out_bytes, touched
+
+
+def cpu_baseline(enc, args, K, Rt):
+    """The reference's CPU path (timm-style ResNet on torch CPU + geometry.py grid_sample loop + mean),
+    timed on this host on `cpu_iters` frames (median)."""
+    import backbone_ref
+    from oracle import reference_composition_cpu
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    enc_cpu = enc.to("cpu")
+    H, W = args.img
+    gen = torch.Generator().manual_seed(1)
+    times = []
+    for _ in range(args.cpu_iters):
+        imgs = torch.randn(1, args.views, 3, H, W, generator=gen)
+        t0 = time.perf_counter()
+        feats = backbone_ref.encoder_forward(enc_cpu, imgs)
+        reference_composition_cpu(feats, torch.from_numpy(K[:1]), torch.from_numpy(Rt[:1]), (H, W), args.bev[0],
+                                  args.bev[1], BOUNDS)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": round(1.0 / t, 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_iters} frame(s) of the same workload ({args.views}x3x{H}x{W} -> {args.backbone} "
+                      f"layer2 + proj C={args.channels} -> grid_sample warp -> mean), median {t:.2f} s/frame, "
+                      "torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from models.encoders.cnn_encoder import CNNEncoder
+    from models.fusion.geometry import GeometryTransformer
+
+    B, V, C = args.batch, args.views, args.channels
+    H, W = args.img
+    torch.manual_seed(1234 + rank)
+    enc = CNNEncoder(out_channels=C, backbone=args.backbone, pretrained=False).eval().to(dev)
+    geom = GeometryTransformer(args.bev[0], args.bev[1], BOUNDS)
+    K, Rt = bev_rig.rig(V, H, W, B)
+    Kd, Rtd = torch.from_numpy(K).to(dev), torch.from_numpy(Rt).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(rank)
+    images = torch.randn(B, V, 3, H, W, device=dev, generator=gen)
+
+    stream = torch.cuda.current_stream(dev)
+    ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], warp [t1,t2]
+
+    def step(record):
+        with torch.no_grad():
+            e0 = e1 = e2 = None
+            if record:
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record(stream)
+            if args.warp_only:
+                feats = step.feats
+            else:
+                feats = enc(images)
+            if record:
+                e1.record(stream)
+            bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean")
+            if record:
+                e2.record(stream)
+                ev.append((e0, e1, e2))
+            return feats, bev
+
+    step.feats = None
+    feats, bev = step(False)
+    step.feats = feats
+    for _ in range(args.warmup):
+        step(False)
+
+    def barrier():
+        if dist:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    bb_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    wp_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    frames = world * B * args.steps
+    value = frames / elapsed
+
+    if rank == 0:
+        flops = backbone_flops(enc, H, W) * V * B
+        Hm = geom.homographies(Kd, Rtd, B, V, dev)
+        alg, out_b, touched = warp_alg_bytes(geom, Hm, feats.shape, (H, W), B, V)
+        roof_bb = None if args.warp_only else {
+            "kernel": "k_conv (fp32 MFMA implicit GEMM, every backbone conv launch of one step)",
+            "bound": "mfma", "achieved": round(flops / (bb_ms * 1e-3) / 1e12, 3), "peak": PEAK_F32_MFMA_TF,
+            "unit": "TFLOP/s", "frac": round(flops / (bb_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TF, 4), "traffic": None,
+            "flops_per_step": flops, "avg_ms": round(bb_ms, 4)}
+        ach = alg / (wp_ms * 1e-3) / 1e9
+        roof_wp = {"kernel": "k_warp_fuse (IPM warp + mean, fused)", "bound": "hbm", "achieved": round(ach, 1),
+                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                   "alg_bytes_per_launch": alg, "out_bytes": out_b, "touched_src_pixels": touched,
+                   "avg_us": round(wp_ms * 1e3, 2)}
+        line = {
+            "metric": "multi-cam frames/sec (7-cam→480×1440 BEV)",
+            "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{V}-cam {H}x{W} -> {args.backbone}(layer2)+proj C={C} -> IPM warp -> mean "
+                                   f"-> {args.bev[0]}x{args.bev[1]} BEV (BASELINE configs[1])",
+                       "frames_per_gpu_per_step": B, "cameras": V, "bev": list(args.bev), "channels": C,
+                       "parallelism": f"frame-sharded x{world} (no collective)"},
+            "roofline": roof_bb if roof_bb else roof_wp,
+            "roofline_warp": roof_wp,
+        }
+        if args.warp_only:
+            line["metric"] = "IPM warp+mean launches/sec (warp-only profiling mode)"
+        if world == 1 and args.cpu_iters > 0 and not args.warp_only:
+            line["cpu_baseline"] = cpu_baseline(enc, args, K, Rt)
+        print(json.dumps(line), flush=True)
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

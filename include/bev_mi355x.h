@@ -1,0 +1,142 @@
+/*
+ * bev_mi355x.h -- C ABI of the MI355X-native multi-view -> BEV hot path.
+ *
+ * One shared library, libbev_mi355x.so (built from
+ * vision-based-spatio-temporal-analysis_amd/csrc/ for gfx950), exports these
+ * entry points.  Plain pointers and sizes only: no torch / HIP types appear in
+ * the signatures (`stream` is a hipStream_t passed as void*, NULL = the null
+ * stream).  All tensor pointers are DEVICE pointers unless the parameter says
+ * "host".  Memory is caller-owned; no entry point allocates, frees or
+ * synchronises, so every call is stream-ordered and hipGraph-capturable.
+ * Return value: 0 on success, otherwise a hipError_t (as int) or
+ * BEV_ERR_ARGS (-1) for an argument the kernel cannot take.
+ *
+ * Each function cites the reference interface it replaces
+ * (sea-sky-web/Vision-based-Spatio-Temporal-Analysis @ 2025-11-14, paths
+ * relative to project/).  The reference is pure Python/torch, so "replaces"
+ * means: the torch op sequence at that file:line, which its modules call on
+ * the hot path.  INTEGRATION.md shows the ctypes binding a maintainer adds.
+ */
+#ifndef BEV_MI355X_H
+#define BEV_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BEV_ERR_ARGS (-1)
+
+/* fusion modes (fusion.py:11-22; AttentionFusion fusion.py:25-36 == MEAN) */
+#define BEV_FUSE_SUM 0
+#define BEV_FUSE_MEAN 1
+#define BEV_FUSE_MAX 2
+
+/* ABI version (bumped on any signature change). */
+int bev_abi_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Geometry helpers
+ * ------------------------------------------------------------------------- */
+
+/* host: BEV cell-centre axis, bit-identical to torch.linspace on the CPU.
+ * Replaces geometry.py:26-27 (torch.linspace(min+0.5res, max-0.5res, n)). */
+int bev_linspace_f32(double lo, double hi, int n, float *out_host);
+
+/* device: H[n][3][3] = K[n][3][3] @ G[n][3][3], G = [r1 r2 t], with the
+ * reference CPU's rounding (MKL AVX-512 3-term dot).
+ * Replaces geometry.py:60-63 (`H = K @ G` inside _compute_homography); the
+ * shape-tolerance branches geometry.py:35-59 are resolved by the host into
+ * (K, G) before the call. */
+int bev_homography_f32(const float *K, const float *G, int n, float *H, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * IPM warp (GeometryTransformer, grid_sample branch)
+ *
+ * feats: N = B*V feature maps of C x Hf x Wf fp32, addressed with element
+ *   strides (sN, sC, sH, sW) so NCHW and channels-last (NHWC) both work.
+ * Hmat: [N][9] world->image homographies (bev_homography_f32 output).
+ * xs [Wb], ys [Hb]: BEV cell-centre axes (bev_linspace_f32 output).
+ * sx = (float)(Wf / (double)W_img), sy = (float)(Hf / (double)H_img).
+ * ------------------------------------------------------------------------- */
+
+/* Per-view warp: out [N][C][Hb][Wb] contiguous.  Bit-identical to
+ * geometry.py:142-162 (grid build + F.grid_sample(bilinear, zeros,
+ * align_corners=False) + bev_out[b,v] = sampled) for every (b,v). */
+int bev_ipm_warp_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                     const float *xs, const float *ys, int N, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                     int Wb, float *out, void *stream);
+
+/* Fused warp + view reduction: out [B][C][Hb][Wb] contiguous, mode one of
+ * BEV_FUSE_*.  Bit-identical to SimpleFusion(mode)(GeometryTransformer(...))
+ * i.e. geometry.py:120-162 followed by fusion.py:17-22, without materialising
+ * the [B,V,C,Hb,Wb] intermediate.  Feature map b*V+v is view v of frame b. */
+int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                          const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                          int Hb, int Wb, int mode, float *out, void *stream);
+
+/* Bilinear corners for index-exactness checks: x0y0 [N][Hb][Wb][2] int32
+ * (0 when both taps of an axis are out of range), wts [N][Hb][Wb][4] (nw, ne,
+ * sw, se), valid [N][Hb][Wb] uint8 bitmask (1 nw, 2 ne, 4 sw, 8 se).  The
+ * integer indices torch's grid_sampler_2d derives at geometry.py:161. */
+int bev_ipm_taps_f32(const float *Hmat, const float *xs, const float *ys, int N, int Hf, int Wf, float sx, float sy,
+                     int Hb, int Wb, int32_t *x0y0, float *wts, uint8_t *valid, void *stream);
+
+/* Backward of bev_ipm_warp_f32 w.r.t. feats (the grid is constant: calibration
+ * carries no gradient).  gfeats [N][C][Hf][Wf] contiguous is OVERWRITTEN.
+ * gout [N][C][Hb][Wb] contiguous.  Float atomics: the summation order, and
+ * therefore the last bits, may vary run to run.  Replaces autograd through
+ * geometry.py:161 (grid_sampler_2d_backward, input grad only). */
+int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C, int Hf,
+                         int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, void *stream);
+
+/* Backward of bev_ipm_warp_fuse_f32 for mode SUM / MEAN: gout [B][C][Hb][Wb],
+ * gfeats [B*V][C][Hf][Wf] contiguous, OVERWRITTEN. */
+int bev_ipm_warp_fuse_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int B, int V,
+                              int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode, float *gfeats,
+                              void *stream);
+
+/* ---------------------------------------------------------------------------
+ * View fusion on materialised per-view maps (SimpleFusion / AttentionFusion)
+ * x [B][V][M] contiguous -> out [B][M].  Replaces fusion.py:19-22
+ * (bev_maps.sum(1) / .mean(1) / .max(1).values; AttentionFusion fusion.py:36).
+ * ------------------------------------------------------------------------- */
+int bev_view_fuse_f32(const float *x, int B, int V, int64_t M, int mode, float *out, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Backbone (CNNEncoder, cnn_encoder.py:39-70): convolutions on MFMA.
+ *
+ * Activations are channels-last (NHWC) fp32.  Weights are packed by
+ * bev_conv_pack_weights_f32 into [KH*KW*Ci (padded)][Co (padded)] panels.
+ * y = act( conv(x, w) + bias (+ residual) ),  act = ReLU if relu != 0.
+ * Batch-norm (eval) is folded into (w, bias) by the host.
+ * x may instead be NCHW (in_nchw = 1): the stem reads the caller's images
+ * [B*V,3,H,W] directly (cnn_encoder.py:66-67 view).
+ * ------------------------------------------------------------------------- */
+
+/* Size in floats of the packed weight panel for (Co, Ci, KH, KW). */
+int64_t bev_conv_packed_size(int Co, int Ci, int KH, int KW);
+
+/* device: w [Co][Ci][KH][KW] (torch OIHW) -> packed panel (see above). */
+int bev_conv_pack_weights_f32(const float *w, int Co, int Ci, int KH, int KW, float *packed, void *stream);
+
+/* device: NHWC (or NCHW input) implicit-GEMM convolution on fp32 MFMA.
+ * residual (NHWC, same shape as y) and bias may be NULL. */
+int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed, const float *bias,
+                   const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
+                   int Wo, void *stream);
+
+/* device: NHWC max-pool (timm ResNet stem: 3x3, stride 2, pad 1). */
+int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
+                           int Wo, void *stream);
+
+/* device: layout conversions between NCHW and NHWC. */
+int bev_nchw_to_nhwc_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
+int bev_nhwc_to_nchw_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BEV_MI355X_H */

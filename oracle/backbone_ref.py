@@ -1,0 +1,61 @@
+"""torch fp32 CPU reference of the backbone graphs (TEST INFRASTRUCTURE ONLY).
+
+Restates, with plain torch CPU ops, what timm's `features_only` ResNet
+computes up to feature index `out_index` (cnn_encoder.py:26,41-42) followed
+by the encoder's 1x1 projection (cnn_encoder.py:43-46), reading the weights
+of our timm-named module (models/encoders/resnet.py) so both sides use the
+same parameters.  BatchNorm runs unfused (F.batch_norm, eval statistics) --
+the HIP path folds it, so the comparison is tolerance-based (fp32 order of
+accumulation differs; rtol 1e-4 per SURVEY.md §8d).  Parity with timm itself
+is unpinned (timm is absent offline).
+
+Used by tests/ and by bench.py's cpu_baseline leg only.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _cbr(x, conv, bn, relu=True):
+    y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
+    if bn is not None:
+        y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+    return F.relu(y) if relu else y
+
+
+def resnet_features(net, x, out_index: int):
+    """features_only[out_index] of a timm-named ResNet `net` on NCHW x (any device; CPU in practice)."""
+    with torch.no_grad():
+        y = _cbr(x, net.conv1, net.bn1)
+        if out_index == 0:
+            return y
+        y = F.max_pool2d(y, 3, 2, 1)
+        for li, layer in enumerate((net.layer1, net.layer2, net.layer3, net.layer4), start=1):
+            for blk in layer:
+                sc = x_in = y
+                if blk.downsample is not None:
+                    sc = _cbr(x_in, blk.downsample[0], blk.downsample[1], relu=False)
+                chain = blk.convs()
+                z = x_in
+                for idx, (conv, bn, _) in enumerate(chain):
+                    last = idx == len(chain) - 1
+                    z = _cbr(z, conv, bn, relu=not last)
+                y = F.relu(z + sc)
+            if li == out_index:
+                return y
+        return y
+
+
+def encoder_forward(enc, images):
+    """CNNEncoder.forward restated on torch CPU ops: [B,V,3,H,W] -> [B,V,C,Hf,Wf] (contiguous)."""
+    B, V = images.shape[:2]
+    x = images.reshape(B * V, *images.shape[2:])
+    with torch.no_grad():
+        if enc._use_timm:
+            f = resnet_features(enc.backbone, x, enc.out_index)
+            y = F.conv2d(f, enc.proj.weight, enc.proj.bias)
+        else:
+            s = enc.backbone
+            y = F.relu(F.conv2d(F.relu(F.conv2d(x, s[0].weight, s[0].bias, 2, 1)), s[2].weight, s[2].bias, 2, 1))
+    return y.reshape(B, V, *y.shape[1:])

@@ -1,0 +1,269 @@
+"""ctypes binding of libbev_mi355x.so (include/bev_mi355x.h) for torch tensors.
+
+This is the only door from the Python module surface (models/) to the HIP
+kernels.  There is NO CPU or PyTorch fallback: if the library is missing or a
+tensor is not on a ROCm device, the call raises.  torch is imported before the
+library is loaded so its HIP runtime (soname libamdhip64.so.7) is the one the
+kernels bind to -- one runtime, one set of streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
+ABI_VERSION = 1
+
+FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_d = ctypes.c_double
+
+# name -> (restype, argtypes); must match include/bev_mi355x.h
+SIGNATURES = {
+    "bev_abi_version": (_i, []),
+    "bev_linspace_f32": (_i, [_d, _d, _i, _vp]),
+    "bev_homography_f32": (_i, [_vp, _vp, _i, _vp, _vp]),
+    "bev_ipm_warp_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
+    "bev_ipm_warp_fuse_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
+                                   _i, _vp, _vp]),
+    "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
+    "bev_ipm_warp_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
+    "bev_ipm_warp_fuse_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _vp]),
+    "bev_view_fuse_f32": (_i, [_vp, _i, _i, _i64, _i, _vp, _vp]),
+    "bev_conv_packed_size": (_i64, [_i, _i, _i, _i]),
+    "bev_conv_pack_weights_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+    "bev_conv2d_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+    "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+}
+
+
+def build(force: bool = False) -> str:
+    """Compile libbev_mi355x.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    cmd = ["make", "-s", "-C", HERE] + (["-B"] if force else [])
+    subprocess.check_call(cmd)
+    return LIB_PATH
+
+
+def lib():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libbev_mi355x.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = L.bev_abi_version()
+        if v != ABI_VERSION:
+            raise ImportError(f"libbev_mi355x.so ABI {v} != expected {ABI_VERSION}; rebuild")
+        _lib = L
+    return _lib
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def _check(rc: int, name: str):
+    if rc != 0:
+        if rc == -1:
+            raise HipError(f"{name}: invalid arguments (BEV_ERR_ARGS)")
+        raise HipError(f"{name}: hipError {rc}")
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _require_gpu(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise HipError("libbev_mi355x kernels need ROCm device tensors (got a CPU tensor); "
+                           "this package has no CPU fallback")
+        if t.dtype != torch.float32:
+            raise HipError(f"fp32 tensors expected, got {t.dtype}")
+
+
+# ---------------------------------------------------------------------------
+# geometry
+# ---------------------------------------------------------------------------
+def linspace(lo: float, hi: float, n: int) -> torch.Tensor:
+    out = torch.empty(max(n, 0), dtype=torch.float32)
+    _check(lib().bev_linspace_f32(lo, hi, n, _ptr(out)), "bev_linspace_f32")
+    return out
+
+
+def homography(K33: torch.Tensor, G33: torch.Tensor) -> torch.Tensor:
+    """K33, G33 [n,3,3] device fp32 -> H [n,9] (bit-identical to the reference CPU matmul)."""
+    K33 = K33.contiguous()
+    G33 = G33.contiguous()
+    _require_gpu(K33, G33)
+    n = K33.shape[0]
+    H = torch.empty(n, 9, device=K33.device, dtype=torch.float32)
+    _check(lib().bev_homography_f32(_ptr(K33), _ptr(G33), n, _ptr(H), _stream(K33)), "bev_homography_f32")
+    return H
+
+
+def _scales(Hf, Wf, img_hw):
+    return float(torch.tensor(Wf / float(img_hw[1]), dtype=torch.float32)), \
+        float(torch.tensor(Hf / float(img_hw[0]), dtype=torch.float32))
+
+
+def warp(feats: torch.Tensor, H: torch.Tensor, xs: torch.Tensor, ys: torch.Tensor, img_hw) -> torch.Tensor:
+    """feats [N,C,Hf,Wf] (any strides) -> out [N,C,Hb,Wb]."""
+    _require_gpu(feats, H, xs, ys)
+    N, C, Hf, Wf = feats.shape
+    Hb, Wb = ys.numel(), xs.numel()
+    sx, sy = _scales(Hf, Wf, img_hw)
+    out = torch.empty(N, C, Hb, Wb, device=feats.device, dtype=torch.float32)
+    s = feats.stride()
+    _check(lib().bev_ipm_warp_f32(_ptr(feats), s[0], s[1], s[2], s[3], _ptr(H), _ptr(xs), _ptr(ys), N, C, Hf, Wf, sx,
+                                  sy, Hb, Wb, _ptr(out), _stream(feats)), "bev_ipm_warp_f32")
+    return out
+
+
+def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, out: torch.Tensor = None):
+    """feats [B,V,C,Hf,Wf] (any strides within a map; maps b*V+v) -> out [B,C,Hb,Wb]."""
+    _require_gpu(feats, H, xs, ys)
+    B, V, C, Hf, Wf = feats.shape
+    if B * V > 0 and feats.stride(0) != V * feats.stride(1):
+        feats = feats.contiguous()
+    Hb, Wb = ys.numel(), xs.numel()
+    sx, sy = _scales(Hf, Wf, img_hw)
+    if out is None:
+        out = torch.empty(B, C, Hb, Wb, device=feats.device, dtype=torch.float32)
+    s = feats.stride()
+    _check(lib().bev_ipm_warp_fuse_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf,
+                                       Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _stream(feats)),
+           "bev_ipm_warp_fuse_f32")
+    return out
+
+
+def taps(H, xs, ys, Hf, Wf, img_hw):
+    _require_gpu(H, xs, ys)
+    N = H.shape[0]
+    Hb, Wb = ys.numel(), xs.numel()
+    sx, sy = _scales(Hf, Wf, img_hw)
+    dev = H.device
+    x0y0 = torch.empty(N, Hb, Wb, 2, device=dev, dtype=torch.int32)
+    wts = torch.empty(N, Hb, Wb, 4, device=dev, dtype=torch.float32)
+    valid = torch.empty(N, Hb, Wb, device=dev, dtype=torch.uint8)
+    _check(lib().bev_ipm_taps_f32(_ptr(H), _ptr(xs), _ptr(ys), N, Hf, Wf, sx, sy, Hb, Wb, _ptr(x0y0), _ptr(wts),
+                                  _ptr(valid), _stream(H)), "bev_ipm_taps_f32")
+    return x0y0, wts, valid
+
+
+def warp_bwd(gout, H, xs, ys, Hf, Wf, img_hw):
+    gout = gout.contiguous()
+    _require_gpu(gout, H, xs, ys)
+    N, C, Hb, Wb = gout.shape
+    sx, sy = _scales(Hf, Wf, img_hw)
+    g = torch.empty(N, C, Hf, Wf, device=gout.device, dtype=torch.float32)
+    _check(lib().bev_ipm_warp_bwd_f32(_ptr(gout), _ptr(H), _ptr(xs), _ptr(ys), N, C, Hf, Wf, sx, sy, Hb, Wb, _ptr(g),
+                                      _stream(gout)), "bev_ipm_warp_bwd_f32")
+    return g
+
+
+def warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode):
+    gout = gout.contiguous()
+    _require_gpu(gout, H, xs, ys)
+    B, C, Hb, Wb = gout.shape
+    sx, sy = _scales(Hf, Wf, img_hw)
+    g = torch.empty(B, V, C, Hf, Wf, device=gout.device, dtype=torch.float32)
+    _check(lib().bev_ipm_warp_fuse_bwd_f32(_ptr(gout), _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf, Wf, sx, sy, Hb, Wb,
+                                           FUSE_MODES[mode], _ptr(g), _stream(gout)), "bev_ipm_warp_fuse_bwd_f32")
+    return g
+
+
+def view_fuse(x: torch.Tensor, mode: str) -> torch.Tensor:
+    """x [B,V,...] -> [B,...] (SimpleFusion)."""
+    x = x.contiguous()
+    _require_gpu(x)
+    B, V = x.shape[:2]
+    M = x[0, 0].numel() if B * V > 0 else 0
+    out = torch.empty((B,) + tuple(x.shape[2:]), device=x.device, dtype=torch.float32)
+    _check(lib().bev_view_fuse_f32(_ptr(x), B, V, M, FUSE_MODES[mode], _ptr(out), _stream(x)), "bev_view_fuse_f32")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# backbone
+# ---------------------------------------------------------------------------
+def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
+    """OIHW fp32 (device) -> packed MFMA panel."""
+    w = w.detach().contiguous()
+    _require_gpu(w)
+    Co, Ci, KH, KW = w.shape
+    n = lib().bev_conv_packed_size(Co, Ci, KH, KW)
+    out = torch.empty(n, device=w.device, dtype=torch.float32)
+    _check(lib().bev_conv_pack_weights_f32(_ptr(w), Co, Ci, KH, KW, _ptr(out), _stream(w)), "bev_conv_pack_weights_f32")
+    return out
+
+
+def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
+                relu: bool, residual: torch.Tensor = None, in_nchw: bool = False, out: torch.Tensor = None):
+    """x: [N,H,W,Ci] NHWC (or [N,Ci,H,W] with in_nchw) -> y [N,Ho,Wo,Co] NHWC."""
+    x = x.contiguous()
+    _require_gpu(x, packed, bias, residual)
+    if in_nchw:
+        N, Ci, H, W = x.shape
+    else:
+        N, H, W, Ci = x.shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == out.shape
+    _check(lib().bev_conv2d_f32(_ptr(x), int(in_nchw), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co, KH,
+                                KW, stride, pad, int(relu), _ptr(out), Ho, Wo, _stream(x)), "bev_conv2d_f32")
+    return out
+
+
+def maxpool_nhwc(x: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tensor:
+    x = x.contiguous()
+    _require_gpu(x)
+    N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.float32)
+    _check(lib().bev_maxpool2d_nhwc_f32(_ptr(x), N, H, W, C, k, stride, pad, _ptr(y), Ho, Wo, _stream(x)),
+           "bev_maxpool2d_nhwc_f32")
+    return y
+
+
+def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    x = x.contiguous()
+    _require_gpu(x)
+    N, C, H, W = x.shape
+    y = torch.empty(N, H, W, C, device=x.device, dtype=torch.float32)
+    _check(lib().bev_nchw_to_nhwc_f32(_ptr(x), N, C, H, W, _ptr(y), _stream(x)), "bev_nchw_to_nhwc_f32")
+    return y
+
+
+def nhwc_to_nchw(x: torch.Tensor) -> torch.Tensor:
+    x = x.contiguous()
+    _require_gpu(x)
+    N, H, W, C = x.shape
+    y = torch.empty(N, C, H, W, device=x.device, dtype=torch.float32)
+    _check(lib().bev_nhwc_to_nchw_f32(_ptr(x), N, C, H, W, _ptr(y), _stream(x)), "bev_nhwc_to_nchw_f32")
+    return y

@@ -1,0 +1,405 @@
+// bev_conv.hip -- per-camera backbone convolutions for gfx950 (MI355X).
+//
+// Replaces the convolution stack the reference runs per camera in
+// CNNEncoder._encode_single (cnn_encoder.py:39-48): the timm ResNet
+// `features_only` graph (cnn_encoder.py:26,41-42) + the lazy 1x1 projection
+// (cnn_encoder.py:43-46), or the fallback 2-conv stack (cnn_encoder.py:31-37).
+//
+// Convolution = implicit GEMM on the exact-f32 MFMA (v_mfma_f32_32x32x2_f32,
+// 64 FLOP/clk/SIMD, bitwise an fmaf chain):
+//     y[m][n] = act( sum_k A[m][k] * W[k][n] + bias[n] (+ res[m][n]) )
+//     m = (image, oy, ox), n = output channel, k = (ky, kx, ci)
+// Activations are channels-last (NHWC) so that a 16-deep K step of a layer
+// with Ci % 16 == 0 is one contiguous 64-B run per output pixel.  The stem
+// (Ci = 3, images NCHW straight from the caller) uses a per-element loader.
+//
+// Tiling: 256 threads = 4 waves as WM x WN, each wave 64 x 64 outputs
+// (2 x 2 MFMA tiles of 32 x 32, 64 accumulator VGPRs).  K step BK = 16 staged
+// global -> registers -> LDS, double-buffered (issue the next step's global
+// loads before the MFMAs of this one, write them to the other LDS buffer
+// after; one barrier per step).  Inside a K step the MFMA's two k-slots are
+// mapped to k = 8*h + p (h = lane >> 5, p = 0..7) so each lane's eight A and
+// eight B operands are two contiguous ds_read_b128 from [row][k] images padded
+// to 80-B rows (conflict-free 16-lane groups).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+constexpr int BK = 16;       // K step
+constexpr int LROW = BK + 4; // LDS row stride in floats (80 B)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__host__ __device__ inline int64_t kpad(int K) { return (K + BK - 1) / BK * BK; }
+__host__ __device__ inline int64_t copad(int Co) { return (Co + 127) / 128 * 128; }
+
+// ---------------------------------------------------------------------------
+// weight packing: OIHW -> [Co_pad][K_pad], k = (ky*KW + kx)*Ci + ci
+// ---------------------------------------------------------------------------
+__global__ void k_pack(const float *__restrict__ w, int Co, int Ci, int KH, int KW, int64_t Kp, int64_t Cop,
+                       float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= Kp * Cop) return;
+    const int n = (int)(t / Kp);
+    const int k = (int)(t % Kp);
+    const int K = Ci * KH * KW;
+    float v = 0.0f;
+    if (n < Co && k < K) {
+        const int ci = k % Ci, r = k / Ci, kx = r % KW, ky = r / KW;
+        v = w[(((int64_t)n * Ci + ci) * KH + ky) * KW + kx];
+    }
+    out[t] = v;
+}
+
+struct ConvArgs {
+    const float *x;
+    const float *wp;
+    const float *bias;
+    const float *res;
+    float *y;
+    int N, H, W, Ci, Co, KH, KW, stride, pad, Ho, Wo;
+    int relu;
+    int in_nchw;  // generic loader only: input is NCHW instead of NHWC
+    int64_t M;
+    int K;
+    int Kp;
+};
+
+// A-tile loader, fast path: NHWC input with Ci % 16 == 0.  Each thread owns
+// ROWS rows of the tile (rows tid/4 + 64*r) and one 16-B quad of the K step.
+template <int ROWS>
+struct LoaderA16 {
+    int64_t pix[ROWS];  // base element offset of image n (n*H*W*Ci)
+    int iy0[ROWS], ix0[ROWS];
+    bool ok[ROWS];
+    int quad;
+
+    __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+        quad = tid & 3;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int64_t m = m0 + (tid >> 2) + 64 * r;
+            ok[r] = m < a.M;
+            const int64_t mm = ok[r] ? m : 0;
+            const int ox = (int)(mm % a.Wo);
+            const int64_t t = mm / a.Wo;
+            const int oy = (int)(t % a.Ho);
+            const int n = (int)(t / a.Ho);
+            pix[r] = (int64_t)n * a.H * a.W * a.Ci;
+            iy0[r] = oy * a.stride - a.pad;
+            ix0[r] = ox * a.stride - a.pad;
+        }
+    }
+    __device__ void load(const ConvArgs &a, int k0, float4 (&v)[ROWS]) const {
+        const int rr = k0 / a.Ci;          // (ky, kx) of this K step
+        const int ci = k0 - rr * a.Ci + quad * 4;
+        const int ky = rr / a.KW, kx = rr - (rr / a.KW) * a.KW;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int iy = iy0[r] + ky, ix = ix0[r] + kx;
+            const bool in = ok[r] && (k0 < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            v[r] = in ? *(const float4 *)(a.x + pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+};
+
+// A-tile loader, generic path: any Ci, NHWC or NCHW input, element-wise.
+template <int ROWS>
+struct LoaderAGen {
+    int64_t pix[ROWS];
+    int iy0[ROWS], ix0[ROWS];
+    bool ok[ROWS];
+    int quad;
+    bool nchw;
+
+    __device__ void init(const ConvArgs &a, int64_t m0, int tid, bool in_nchw) {
+        quad = tid & 3;
+        nchw = in_nchw;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int64_t m = m0 + (tid >> 2) + 64 * r;
+            ok[r] = m < a.M;
+            const int64_t mm = ok[r] ? m : 0;
+            const int ox = (int)(mm % a.Wo);
+            const int64_t t = mm / a.Wo;
+            const int oy = (int)(t % a.Ho);
+            const int n = (int)(t / a.Ho);
+            pix[r] = (int64_t)n * a.H * a.W * a.Ci;
+            iy0[r] = oy * a.stride - a.pad;
+            ix0[r] = ox * a.stride - a.pad;
+        }
+    }
+    __device__ void load(const ConvArgs &a, int k0, float4 (&v)[ROWS]) const {
+        float e[4][ROWS];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = k0 + quad * 4 + q;
+            const int ci = k % a.Ci, rr = k / a.Ci, kx = rr % a.KW, ky = rr / a.KW;
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) {
+                const int iy = iy0[r] + ky, ix = ix0[r] + kx;
+                const bool in = ok[r] && (k < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                const int64_t off = nchw ? pix[r] + ((int64_t)ci * a.H + iy) * a.W + ix
+                                         : pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci;
+                e[q][r] = in ? a.x[off] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) v[r] = make_float4(e[0][r], e[1][r], e[2][r], e[3][r]);
+    }
+};
+
+// WM x WN waves, each 64 x 64 outputs.
+template <int WM, int WN, bool FAST>
+__global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
+    constexpr int BM = WM * 64, BN = WN * 64;
+    constexpr int AROWS = BM / 64;  // rows per thread in the A loader
+    constexpr int BROWS = BN / 64;  // rows per thread in the B loader
+    __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LROW];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int n_tiles = (a.Co + BN - 1) / BN;
+    const int64_t m0 = (int64_t)(blockIdx.x / n_tiles) * BM;
+    const int n0 = (blockIdx.x % n_tiles) * BN;
+
+    // loaders
+    typename std::conditional<FAST, LoaderA16<AROWS>, LoaderAGen<AROWS>>::type la;
+    if constexpr (FAST) la.init(a, m0, tid);
+    else la.init(a, m0, tid, a.in_nchw != 0);
+    const int bq = tid & 3;
+    const float *wrow[BROWS];
+#pragma unroll
+    for (int r = 0; r < BROWS; ++r) wrow[r] = a.wp + (int64_t)(n0 + (tid >> 2) + 64 * r) * a.Kp + bq * 4;
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+
+    float4 ra[AROWS], rb[BROWS];
+    auto gload = [&](int k0) {
+        la.load(a, k0, ra);
+#pragma unroll
+        for (int r = 0; r < BROWS; ++r) rb[r] = *(const float4 *)(wrow[r] + k0);
+    };
+    auto swrite = [&](int buf) {
+        float *As = lds[buf];
+        float *Bs = lds[buf] + BM * LROW;
+#pragma unroll
+        for (int r = 0; r < AROWS; ++r) *(float4 *)(As + ((tid >> 2) + 64 * r) * LROW + bq * 4) = ra[r];
+#pragma unroll
+        for (int r = 0; r < BROWS; ++r) *(float4 *)(Bs + ((tid >> 2) + 64 * r) * LROW + bq * 4) = rb[r];
+    };
+
+    const int nk = a.Kp / BK;
+    gload(0);
+    swrite(0);
+    __syncthreads();
+    const int r32 = lane & 31, h = lane >> 5;
+    for (int ks = 0; ks < nk; ++ks) {
+        const int cur = ks & 1;
+        if (ks + 1 < nk) gload((ks + 1) * BK);
+        const float *As = lds[cur];
+        const float *Bs = lds[cur] + BM * LROW;
+        float4 fa[2][2], fb[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float *pa = As + (wm * 64 + i * 32 + r32) * LROW + h * 8;
+            fa[i][0] = *(const float4 *)pa;
+            fa[i][1] = *(const float4 *)(pa + 4);
+            const float *pb = Bs + (wn * 64 + i * 32 + r32) * LROW + h * 8;
+            fb[i][0] = *(const float4 *)pb;
+            fb[i][1] = *(const float4 *)(pb + 4);
+        }
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float av = ((const float *)&fa[i][p >> 2])[p & 3];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const float bv = ((const float *)&fb[j][p >> 2])[p & 3];
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        if (ks + 1 < nk) {
+            swrite(cur ^ 1);
+            __syncthreads();
+        }
+    }
+
+    // epilogue: D[row][col], col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 64 + j * 32 + r32;
+        if (n >= a.Co) continue;
+        const float bv = a.bias ? a.bias[n] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m >= a.M) continue;
+                float v = acc[i][j][r] + bv;
+                if (a.res) v += a.res[m * a.Co + n];
+                if (a.relu) v = v > 0.0f ? v : 0.0f;
+                a.y[m * a.Co + n] = v;
+            }
+        }
+    }
+}
+
+// NHWC max-pool (padding counts as -inf, as torch.nn.MaxPool2d)
+__global__ void k_maxpool(const float *__restrict__ x, int N, int H, int W, int C, int k, int s, int p,
+                          float *__restrict__ y, int Ho, int Wo) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)N * Ho * Wo * C;
+    if (t >= total) return;
+    const int c = (int)(t % C);
+    int64_t r = t / C;
+    const int ox = (int)(r % Wo);
+    r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int n = (int)(r / Ho);
+    float m = -__builtin_inff();
+    for (int ky = 0; ky < k; ++ky) {
+        const int iy = oy * s - p + ky;
+        if (iy < 0 || iy >= H) continue;
+        for (int kx = 0; kx < k; ++kx) {
+            const int ix = ox * s - p + kx;
+            if (ix < 0 || ix >= W) continue;
+            const float v = x[(((int64_t)n * H + iy) * W + ix) * C + c];
+            m = (v > m || v != v) ? v : m;
+        }
+    }
+    y[t] = m;
+}
+
+// 32x32 tiled transposes between [N][C][HW] and [N][HW][C]
+__global__ void k_transpose(const float *__restrict__ x, int R, int S, float *__restrict__ y) {
+    // x [N][R][S] -> y [N][S][R]
+    __shared__ float tile[32][33];
+    const int n = blockIdx.z;
+    const int s0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+    const float *xn = x + (int64_t)n * R * S;
+    float *yn = y + (int64_t)n * R * S;
+    for (int q = threadIdx.y; q < 32; q += 8) {
+        const int r = r0 + q, s = s0 + threadIdx.x;
+        if (r < R && s < S) tile[q][threadIdx.x] = xn[(int64_t)r * S + s];
+    }
+    __syncthreads();
+    for (int q = threadIdx.y; q < 32; q += 8) {
+        const int s = s0 + q, r = r0 + threadIdx.x;
+        if (r < R && s < S) yn[(int64_t)s * R + r] = tile[threadIdx.x][q];
+    }
+}
+
+inline int last() { return (int)hipGetLastError(); }
+
+template <int WM, int WN>
+int launch_conv(const ConvArgs &a, bool fast, hipStream_t st) {
+    constexpr int BM = WM * 64, BN = WN * 64;
+    const int64_t m_tiles = (a.M + BM - 1) / BM;
+    const int n_tiles = (a.Co + BN - 1) / BN;
+    const int64_t blocks = m_tiles * n_tiles;
+    if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
+    if (fast) hipLaunchKernelGGL((k_conv<WM, WN, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_conv<WM, WN, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return last();
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t bev_conv_packed_size(int Co, int Ci, int KH, int KW) {
+    if (Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return 0;
+    return copad(Co) * kpad(Ci * KH * KW);
+}
+
+int bev_conv_pack_weights_f32(const float *w, int Co, int Ci, int KH, int KW, float *packed, void *stream) {
+    if (!w || !packed || Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;
+    const int64_t Kp = kpad(Ci * KH * KW), Cop = copad(Co);
+    const int64_t total = Kp * Cop;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, Co, Ci,
+                       KH, KW, Kp, Cop, packed);
+    return last();
+}
+
+int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed, const float *bias,
+                   const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
+                   int Wo, void *stream) {
+    if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
+        stride <= 0 || pad < 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvArgs a;
+    a.x = x;
+    a.wp = packed;
+    a.bias = bias;
+    a.res = residual;
+    a.y = y;
+    a.N = N;
+    a.H = H;
+    a.W = W;
+    a.Ci = Ci;
+    a.Co = Co;
+    a.KH = KH;
+    a.KW = KW;
+    a.stride = stride;
+    a.pad = pad;
+    a.Ho = Ho;
+    a.Wo = Wo;
+    a.relu = relu;
+    a.M = (int64_t)N * Ho * Wo;
+    a.K = Ci * KH * KW;
+    a.Kp = (int)kpad(a.K);
+    a.in_nchw = in_nchw;
+    const bool fast = !in_nchw && (Ci % BK == 0);
+    hipStream_t st = (hipStream_t)stream;
+    if (Co <= 64) return launch_conv<4, 1>(a, fast, st);
+    return launch_conv<2, 2>(a, fast, st);
+}
+
+int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
+                           int Wo, void *stream) {
+    if (!x || !y || N < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || stride <= 0 || pad < 0) return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1) return BEV_ERR_ARGS;
+    const int64_t total = (int64_t)N * Ho * Wo * C;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_maxpool, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, N, H, W,
+                       C, k, stride, pad, y, Ho, Wo);
+    return last();
+}
+
+int bev_nchw_to_nhwc_f32(const float *x, int N, int C, int H, int W, float *y, void *stream) {
+    if (!x || !y || N < 0 || C <= 0 || H <= 0 || W <= 0) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    const int S = H * W;
+    hipLaunchKernelGGL(k_transpose, dim3((S + 31) / 32, (C + 31) / 32, N), dim3(32, 8), 0, (hipStream_t)stream, x, C,
+                       S, y);
+    return last();
+}
+
+int bev_nhwc_to_nchw_f32(const float *x, int N, int C, int H, int W, float *y, void *stream) {
+    if (!x || !y || N < 0 || C <= 0 || H <= 0 || W <= 0) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    const int S = H * W;
+    hipLaunchKernelGGL(k_transpose, dim3((C + 31) / 32, (S + 31) / 32, N), dim3(32, 8), 0, (hipStream_t)stream, x, S,
+                       C, y);
+    return last();
+}
+
+}  // extern "C"

@@ -1,0 +1,201 @@
+"""ResNet backbones (timm-compatible module names) executed by the HIP conv kernels.
+
+The reference builds its per-camera backbone with
+`timm.create_model(name, pretrained, features_only=True)` (cnn_encoder.py:26)
+and keeps `feats_list[out_index]` (cnn_encoder.py:41-42, out_index=2 ->
+the stride-8 `layer2` output).  timm is an unpinned third-party dependency
+absent from this image, so the graphs are restated here with timm's
+parameter names (conv1 / bn1 / layer1..4 / downsample.0/1), so that a timm
+state_dict loads unchanged.  Parity with timm itself is therefore UNPINNED;
+the conv kernels are pinned against a torch fp32 reference of the same
+weights (oracle/backbone_ref.py, tests/test_backbone_gpu.py).
+
+Execution (inference / eval mode): activations stay channels-last (NHWC) on
+the device; every conv+BN(+residual)(+ReLU) is ONE `bev_conv2d_f32` launch
+with batch-norm folded into the packed weights and bias; the stem reads the
+caller's NCHW images directly.  Stages past `out_index` are not executed:
+features_only returns them but CNNEncoder discards them, so skipping them
+leaves the output unchanged.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn as nn
+
+import bev_native as _nat
+
+__all__ = ["ResNet", "resnet18", "resnet34", "resnet50", "NATIVE_BACKBONES", "FoldedConv", "stage_of"]
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.act1 = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.act2 = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def convs(self):
+        """(conv, bn, relu, residual_from) chain for the native executor."""
+        return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, True)]
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        width = planes
+        outplanes = planes * self.expansion
+        self.conv1 = nn.Conv2d(inplanes, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.act1 = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)  # timm: stride on the 3x3
+        self.bn2 = nn.BatchNorm2d(width)
+        self.act2 = nn.ReLU(inplace=True)
+        self.conv3 = nn.Conv2d(width, outplanes, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(outplanes)
+        self.act3 = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def convs(self):
+        return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, True), (self.conv3, self.bn3, True)]
+
+
+class FoldedConv:
+    """conv (+ eval-mode BN) folded into a packed MFMA weight panel + bias, cached on device.
+
+    The cache is keyed on the parameters' storage and version counters, so an
+    optimizer step or load_state_dict triggers a re-pack on the next call.
+    """
+
+    def __init__(self, conv: nn.Conv2d, bn: nn.BatchNorm2d = None):
+        self.conv, self.bn = conv, bn
+        self._key = None
+        self.packed = self.bias = None
+
+    def _tensors(self):
+        ts = [self.conv.weight] + ([self.conv.bias] if self.conv.bias is not None else [])
+        if self.bn is not None:
+            ts += [self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var]
+        return ts
+
+    def prepare(self, device):
+        key = tuple((t.data_ptr(), t._version) for t in self._tensors()) + (str(device),)
+        if key == self._key:
+            return
+        with torch.no_grad():
+            w = self.conv.weight.detach().to(device=device, dtype=torch.float32)
+            b = (self.conv.bias.detach().to(device=device, dtype=torch.float32) if self.conv.bias is not None
+                 else torch.zeros(w.shape[0], device=device))
+            if self.bn is not None:
+                bn = self.bn
+                scale = bn.weight.detach().to(device) / torch.sqrt(bn.running_var.detach().to(device) + bn.eps)
+                w = w * scale.view(-1, 1, 1, 1)
+                b = bn.bias.detach().to(device) + (b - bn.running_mean.detach().to(device)) * scale
+            self.packed = _nat.pack_conv_weight(w.contiguous())
+            self.bias = b.contiguous().float()
+        self._key = key
+
+    def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False):
+        self.prepare(x.device)
+        c = self.conv
+        return _nat.conv2d_nhwc(x, self.packed, self.bias, c.out_channels, c.kernel_size[0], c.kernel_size[1],
+                                c.stride[0], c.padding[0], relu, residual=residual, in_nchw=in_nchw)
+
+
+def stage_of(out_index: int) -> int:
+    """features_only index -> number of residual stages to run (0: act1, 1: layer1, ...)."""
+    return max(0, out_index)
+
+
+class ResNet(nn.Module):
+    """timm-named ResNet trunk.  forward_features_nhwc(x, out_index) runs natively."""
+
+    def __init__(self, block, layers: List[int]):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.act1 = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._make_layer(block, 64, layers[0], 1)
+        self.layer2 = self._make_layer(block, 128, layers[1], 2)
+        self.layer3 = self._make_layer(block, 256, layers[2], 2)
+        self.layer4 = self._make_layer(block, 512, layers[3], 2)
+        self.feature_info = [64, 64 * block.expansion, 128 * block.expansion, 256 * block.expansion,
+                             512 * block.expansion]
+        for m in self.modules():  # timm's ResNet init
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        self._folded = {}
+
+    def _make_layer(self, block, planes, blocks, stride):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(nn.Conv2d(self.inplanes, planes * block.expansion, 1, stride, bias=False),
+                                       nn.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            layers.append(block(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def _fc(self, conv, bn):
+        k = id(conv)
+        if k not in self._folded:
+            self._folded[k] = FoldedConv(conv, bn)
+        return self._folded[k]
+
+    def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
+        """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC feature map of features_only[out_index]."""
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("native ResNet executes eval-mode (folded BN) inference only")
+        y = self._fc(self.conv1, self.bn1)(x, relu=True, in_nchw=True)  # act1: index 0
+        if out_index == 0:
+            return y
+        y = _nat.maxpool_nhwc(y, 3, 2, 1)
+        for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
+            for blk in layer:
+                y = self._block(blk, y)
+            if li == out_index:
+                return y
+        return y
+
+    def _block(self, blk, x):
+        sc = x
+        if blk.downsample is not None:
+            sc = self._fc(blk.downsample[0], blk.downsample[1])(x, relu=False)
+        chain = blk.convs()
+        y = x
+        for idx, (conv, bn, relu) in enumerate(chain):
+            last = idx == len(chain) - 1
+            y = self._fc(conv, bn)(y, relu=relu, residual=sc if last else None)
+        return y
+
+
+def resnet18():
+    return ResNet(BasicBlock, [2, 2, 2, 2])
+
+
+def resnet34():
+    return ResNet(BasicBlock, [3, 4, 6, 3])
+
+
+def resnet50():
+    return ResNet(Bottleneck, [3, 4, 6, 3])
+
+
+NATIVE_BACKBONES = {"resnet18": resnet18, "resnet34": resnet34, "resnet50": resnet50}
