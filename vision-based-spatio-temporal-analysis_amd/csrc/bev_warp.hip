@@ -25,6 +25,7 @@
 // that (tile, view).  Output is written once, non-temporally.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "bev_geometry.h"
 #include "../../include/bev_mi355x.h"
@@ -127,18 +128,25 @@ __global__ __launch_bounds__(NT) void k_warp(const float *__restrict__ feats, in
 // -------------------------------------------------------------------------
 // fused warp + reduce: out [B][C][Hb][Wb]
 // -------------------------------------------------------------------------
-// LDS image of one view's footprint for a chunk of CK channels:
-//   pixel p (row-major inside the bbox) at byte p*PSTRIDE, channels packed.
-// PSTRIDE = CK*4 + 16 keeps consecutive pixels on different 16-B bank slots
-// (stride in slots = CK/4 + 1, odd) so the 16-lane groups of ds_read_b128 hit
-// distinct slots; lanes sampling the same pixel broadcast.
-// One extra all-zero pixel at index npix serves every invalid tap.
-constexpr int LDS_BYTES = 40 * 1024;
+// Tile = FT_H x FT_W = 8 x 32 BEV cells, 256 threads, one cell per lane; wave
+// w owns rows 2w, 2w+1 (lanes 0-31 / 32-63), so each per-channel output store
+// is two full 128-B lines.
+//
+// LDS image of one view's source footprint for a chunk of CK channels:
+//   pixel p (row-major inside the tile's bbox) at byte p*PSTRIDE, CK channels
+//   packed.  PSTRIDE = CK*4 + 16 (odd number of 16-B slots) so distinct pixels
+//   of a 16-lane ds_read_b128 group sit on distinct bank slots; lanes sampling
+//   the same pixel broadcast.  Pixel index npix is an all-zero pixel that
+//   every out-of-range tap reads (zeros padding, no branch in the inner loop).
+// Per view: taps -> wave bbox (shuffles) -> [barrier] -> block bbox -> stage
+// (global float4 -> ds_write_b128) -> [barrier] -> 4 ds_read_b128 per 4
+// channels + bilinear + accumulate.  The bbox partials are double-buffered by
+// view parity, so two barriers per view suffice.
+constexpr int FT_W = 32, FT_H = 8, FT_NT = FT_W * FT_H;
 
 template <int CK>
 struct Stage {
     static constexpr int PSTRIDE = CK * 4 + 16;
-    static constexpr int MAXPIX = LDS_BYTES / PSTRIDE - 1;
 };
 
 __device__ __forceinline__ int wave_min(int v) {
@@ -152,20 +160,39 @@ __device__ __forceinline__ int wave_max(int v) {
     return v;
 }
 
-template <int CK, int MODE>
-__global__ __launch_bounds__(NT) void k_warp_fuse(const float *__restrict__ feats, int64_t sN, int64_t sC, int64_t sH,
-                                                  int64_t sW, const float *__restrict__ Hmat,
-                                                  const float *__restrict__ xs, const float *__restrict__ ys, int V,
-                                                  int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                                                  float *__restrict__ out) {
-    using S = Stage<CK>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int (*red)[TILE_H] = reinterpret_cast<int (*)[TILE_H]>(smem + LDS_BYTES);  // [4][TILE_H] bbox partials
+// exact p / d for 0 <= p < 2^22, 1 <= d < 2^22 (float estimate + one correction)
+__device__ __forceinline__ int fast_div(int p, int d, float inv_d) {
+    int q = (int)((float)p * inv_d);
+    const int r = p - q * d;
+    q += (r >= d) - (r < 0);
+    return q;
+}
 
-    const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * TILE_W + tx;
-    const int j = blockIdx.x * TILE_W + tx;
-    const int i = blockIdx.y * TILE_H + ty;
-    const int b = blockIdx.z;
+template <int CK, int MODE, bool VEC>
+__global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict__ feats, int64_t sN, int64_t sC,
+                                                        int64_t sH, int64_t sW, const float *__restrict__ Hmat,
+                                                        const float *__restrict__ xs, const float *__restrict__ ys,
+                                                        int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                                                        int Wb, float *__restrict__ out, int img_bytes) {
+    constexpr int PS = Stage<CK>::PSTRIDE;
+    constexpr int G4 = CK / 4;  // float4 groups per pixel
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int *red = reinterpret_cast<int *>(smem + img_bytes);  // [2 parity][4 values][4 waves]
+    const int maxpix = img_bytes / PS - 1;
+
+    // XCD-aware tile order: consecutive tiles (which share source pixels) are
+    // dealt to the same XCD (blocks b, b+8, ... share one); bijective remap.
+    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, nt = ntx * nty;
+    int tile = blockIdx.x;
+    {
+        const int q = nt / 8, r = nt % 8, x = tile % 8;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    const int tyb = tile / ntx, txb = tile - tyb * ntx;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i = tyb * FT_H + wave * 2 + (lane >> 5);
+    const int j = txb * FT_W + (lane & 31);
+    const int b = blockIdx.y;
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
@@ -183,7 +210,6 @@ __global__ __launch_bounds__(NT) void k_warp_fuse(const float *__restrict__ feat
             load_h(Hmat, n, h);
             Taps t = cell_taps(h, cx, cy, Hf, Wf, sx, sy);
             if (!inside) t.valid = 0;
-            // footprint bbox over valid taps of the workgroup
             int bx0 = 0x7fffffff, by0 = 0x7fffffff, bx1 = -1, by1 = -1;
             if (t.valid) {
                 bx0 = (t.valid & 5) ? t.x0 : t.x0 + 1;
@@ -191,27 +217,27 @@ __global__ __launch_bounds__(NT) void k_warp_fuse(const float *__restrict__ feat
                 by0 = (t.valid & 3) ? t.y0 : t.y0 + 1;
                 by1 = (t.valid & 12) ? t.y0 + 1 : t.y0;
             }
+            const bool wave_any = __ballot(t.valid != 0) != 0ull;
             bx0 = wave_min(bx0);
             by0 = wave_min(by0);
             bx1 = wave_max(bx1);
             by1 = wave_max(by1);
-            __syncthreads();  // previous view's LDS reads are done before red[] / smem reuse
-            if (tx == 0) {
-                red[0][ty] = bx0;
-                red[1][ty] = by0;
-                red[2][ty] = bx1;
-                red[3][ty] = by1;
+            int *rp = red + (v & 1) * 16;
+            if (lane == 0) {
+                rp[wave] = bx0;
+                rp[4 + wave] = by0;
+                rp[8 + wave] = bx1;
+                rp[12 + wave] = by1;
             }
-            __syncthreads();
+            __syncthreads();  // (A) bbox partials visible; previous view's LDS reads are done
 #pragma unroll
-            for (int w = 0; w < TILE_H; ++w) {
-                bx0 = min(bx0, red[0][w]);
-                by0 = min(by0, red[1][w]);
-                bx1 = max(bx1, red[2][w]);
-                by1 = max(by1, red[3][w]);
+            for (int w = 0; w < 4; ++w) {
+                bx0 = min(bx0, rp[w]);
+                by0 = min(by0, rp[4 + w]);
+                bx1 = max(bx1, rp[8 + w]);
+                by1 = max(by1, rp[12 + w]);
             }
-            if (bx1 < 0) {
-                // no cell of the tile sees this view: every sample is +0
+            if (bx1 < 0) {  // no cell of the tile sees this view: every sample is +0
                 if (MODE == BEV_FUSE_MAX) {
 #pragma unroll
                     for (int q = 0; q < CK; ++q) acc[q] = (v == 0) ? 0.0f : nan_max(acc[q], 0.0f);
@@ -219,58 +245,94 @@ __global__ __launch_bounds__(NT) void k_warp_fuse(const float *__restrict__ feat
                 continue;  // sum / mean: acc + (+0) == acc (acc is never -0 here)
             }
             const int bw = bx1 - bx0 + 1, bh = by1 - by0 + 1;
-            const int npix = bw * bh;
             const float *f = feats + (int64_t)n * sN + (int64_t)c0 * sC;
-            float smp[CK];
-            if (npix <= S::MAXPIX) {
-                // ---- stage the footprint: [pixel][channel] ------------------------
-                // element e -> (pixel p = e / ck, channel q = e % ck); consecutive lanes
-                // walk channels first (contiguous in NHWC, strided in NCHW).
-                const int total = npix * ck;
-                for (int e = tid; e < total; e += NT) {
-                    const int p = e / ck, q = e - p * ck;
-                    const int py = p / bw, px = p - py * bw;
-                    const float val = f[(int64_t)q * sC + (int64_t)(by0 + py) * sH + (int64_t)(bx0 + px) * sW];
-                    *(float *)(smem + p * S::PSTRIDE + q * 4) = val;
-                }
-                if (ck < CK) {  // zero the unused channel slots of every pixel
-                    for (int e = tid; e < npix * (CK - ck); e += NT) {
-                        const int p = e / (CK - ck), q = ck + e - p * (CK - ck);
-                        *(float *)(smem + p * S::PSTRIDE + q * 4) = 0.0f;
+            // Split the footprint into blocks that fit the LDS budget.  Blocks
+            // overlap by one pixel in x and y, so every lane's 2x2 tap quad lies
+            // inside the block it is assigned to; almost always there is one block.
+            int wb = bw, hb = bh, nbx = 1, nby = 1;
+            if (bw * bh > maxpix) {
+                wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                hb = min(bh, maxpix / wb);
+                nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+            }
+            const bool single = (nbx == 1) && (nby == 1);
+            int mkx = 0, mky = 0;
+            if (!single && t.valid) {
+                const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                mkx = (nbx == 1) ? 0 : min((xlo - bx0) / (wb - 1), nbx - 1);
+                mky = (nby == 1) ? 0 : min((ylo - by0) / (hb - 1), nby - 1);
+            }
+            if (!single && MODE == BEV_FUSE_MAX && !t.valid) {
+#pragma unroll
+                for (int q = 0; q < CK; ++q) acc[q] = (v == 0) ? 0.0f : nan_max(acc[q], 0.0f);
+            }
+            for (int ky = 0; ky < nby; ++ky) {
+                for (int kx = 0; kx < nbx; ++kx) {
+                    const int sx0 = bx0 + kx * (wb - 1), sy0 = by0 + ky * (hb - 1);
+                    const int sbw = min(wb, bx1 - sx0 + 1), sbh = min(hb, by1 - sy0 + 1);
+                    const int npix = sbw * sbh;
+                    if (!single) __syncthreads();  // previous block's LDS reads are done
+                    // ---- stage the block as [pixel][channel] ----------------------------
+                    const float inv_bw = 1.0f / (float)sbw;
+                    if (VEC) {  // channels contiguous (NHWC), ck % 4 == 0
+                        const int total = npix * G4;
+                        for (int e = tid; e < total; e += FT_NT) {
+                            const int p = e / G4, g = e - p * G4;
+                            const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
+                            float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+                            if (g * 4 < ck)
+                                val = *(const float4 *)(f + (int64_t)(sy0 + py) * sH + (int64_t)(sx0 + px) * sW + g * 4);
+                            *(float4 *)(smem + p * PS + g * 16) = val;
+                        }
+                    } else {  // generic strides
+                        const int total = npix * CK;
+                        for (int e = tid; e < total; e += FT_NT) {
+                            const int p = e / CK, q = e - p * CK;
+                            const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
+                            float val = 0.0f;
+                            if (q < ck) val = f[(int64_t)q * sC + (int64_t)(sy0 + py) * sH + (int64_t)(sx0 + px) * sW];
+                            *(float *)(smem + p * PS + q * 4) = val;
+                        }
+                    }
+                    if (tid < G4) *(float4 *)(smem + npix * PS + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+                    __syncthreads();  // (B) image ready
+                    // single block: every lane of an active wave samples (invalid taps
+                    // read the zero pixel -> +0, which is the reference's sample too).
+                    const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                    const bool go = single ? wave_any : (__ballot(mine) != 0ull);
+                    if (go) {
+                        const int pb = (t.y0 - sy0) * sbw + (t.x0 - sx0);
+                        const unsigned char *a0 = smem + ((mine && (t.valid & 1)) ? pb : npix) * PS;
+                        const unsigned char *a1 = smem + ((mine && (t.valid & 2)) ? pb + 1 : npix) * PS;
+                        const unsigned char *a2 = smem + ((mine && (t.valid & 4)) ? pb + sbw : npix) * PS;
+                        const unsigned char *a3 = smem + ((mine && (t.valid & 8)) ? pb + sbw + 1 : npix) * PS;
+#pragma unroll
+                        for (int g = 0; g < G4; ++g) {
+                            const float4 vnw = *(const float4 *)(a0 + g * 16);
+                            const float4 vne = *(const float4 *)(a1 + g * 16);
+                            const float4 vsw = *(const float4 *)(a2 + g * 16);
+                            const float4 vse = *(const float4 *)(a3 + g * 16);
+                            const float sm[4] = {bilerp(vnw.x, vne.x, vsw.x, vse.x, t.w),
+                                                 bilerp(vnw.y, vne.y, vsw.y, vse.y, t.w),
+                                                 bilerp(vnw.z, vne.z, vsw.z, vse.z, t.w),
+                                                 bilerp(vnw.w, vne.w, vsw.w, vse.w, t.w)};
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                float &a = acc[4 * g + u];
+                                float r;
+                                if (MODE == BEV_FUSE_MAX) r = (v == 0) ? sm[u] : nan_max(a, sm[u]);
+                                else r = a + sm[u];
+                                a = mine ? r : a;
+                            }
+                            // bound the LDS-read lookahead (registers): at most 4 groups in flight
+                            if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                        }
+                    } else if (single && MODE == BEV_FUSE_MAX) {
+#pragma unroll
+                        for (int q = 0; q < CK; ++q) acc[q] = (v == 0) ? 0.0f : nan_max(acc[q], 0.0f);
                     }
                 }
-                for (int q = tid; q < CK; q += NT) *(float *)(smem + npix * S::PSTRIDE + q * 4) = 0.0f;
-                __syncthreads();
-                // ---- gather from LDS ----------------------------------------------
-                const int lx = t.x0 - bx0, ly = t.y0 - by0;
-                const int pb = ly * bw + lx;
-                const int a0 = ((t.valid & 1) ? pb : npix) * S::PSTRIDE;
-                const int a1 = ((t.valid & 2) ? pb + 1 : npix) * S::PSTRIDE;
-                const int a2 = ((t.valid & 4) ? pb + bw : npix) * S::PSTRIDE;
-                const int a3 = ((t.valid & 8) ? pb + bw + 1 : npix) * S::PSTRIDE;
-#pragma unroll
-                for (int q = 0; q < CK; q += 4) {
-                    const float4 vnw = *(const float4 *)(smem + a0 + q * 4);
-                    const float4 vne = *(const float4 *)(smem + a1 + q * 4);
-                    const float4 vsw = *(const float4 *)(smem + a2 + q * 4);
-                    const float4 vse = *(const float4 *)(smem + a3 + q * 4);
-                    smp[q + 0] = bilerp(vnw.x, vne.x, vsw.x, vse.x, t.w);
-                    smp[q + 1] = bilerp(vnw.y, vne.y, vsw.y, vse.y, t.w);
-                    smp[q + 2] = bilerp(vnw.z, vne.z, vsw.z, vse.z, t.w);
-                    smp[q + 3] = bilerp(vnw.w, vne.w, vsw.w, vse.w, t.w);
-                }
-            } else {
-                // ---- footprint too large: direct global gathers -----------------------
-                const GOff g = global_offsets(t, sH, sW);
-#pragma unroll
-                for (int q = 0; q < CK; ++q) smp[q] = (q < ck) ? sample_global(f + (int64_t)q * sC, g, t) : 0.0f;
-            }
-            if (MODE == BEV_FUSE_MAX) {
-#pragma unroll
-                for (int q = 0; q < CK; ++q) acc[q] = (v == 0) ? smp[q] : nan_max(acc[q], smp[q]);
-            } else {
-#pragma unroll
-                for (int q = 0; q < CK; ++q) acc[q] = acc[q] + smp[q];
             }
         }
         if (inside) {
@@ -343,26 +405,52 @@ __global__ void k_view_fuse(const float *__restrict__ x, int V, int64_t M, float
 inline int err(hipError_t e) { return (int)e; }
 inline int last() { return (int)hipGetLastError(); }
 
-template <int CK>
+// LDS budget of the fused warp's footprint image (bytes); BEV_WARP_LDS_KB overrides.
+inline int warp_lds_bytes() {
+    static int v = [] {
+        const char *e = getenv("BEV_WARP_LDS_KB");
+        int kb = e ? atoi(e) : 60;
+        if (kb < 4) kb = 4;
+        if (kb > 150) kb = 150;
+        return kb * 1024;
+    }();
+    return v;
+}
+
+template <int CK, bool VEC>
 int launch_fuse(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                 const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
                 float *out, hipStream_t st) {
-    dim3 grid((Wb + TILE_W - 1) / TILE_W, (Hb + TILE_H - 1) / TILE_H, B), block(TILE_W, TILE_H);
-    const size_t lds = LDS_BYTES + 4 * TILE_H * sizeof(int);
+    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
+    dim3 grid(ntiles, B), block(FT_NT);
+    const int img = warp_lds_bytes();
+    const size_t lds = img + 32 * sizeof(int);
     switch (mode) {
         case BEV_FUSE_SUM:
-            hipLaunchKernelGGL((k_warp_fuse<CK, BEV_FUSE_SUM>), grid, block, lds, st, feats, sN, sC, sH, sW, Hmat, xs,
-                               ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out);
+            hipLaunchKernelGGL((k_warp_fuse<CK, BEV_FUSE_SUM, VEC>), grid, block, lds, st, feats, sN, sC, sH, sW, Hmat,
+                               xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, img);
             break;
         case BEV_FUSE_MEAN:
-            hipLaunchKernelGGL((k_warp_fuse<CK, BEV_FUSE_MEAN>), grid, block, lds, st, feats, sN, sC, sH, sW, Hmat,
-                               xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out);
+            hipLaunchKernelGGL((k_warp_fuse<CK, BEV_FUSE_MEAN, VEC>), grid, block, lds, st, feats, sN, sC, sH, sW,
+                               Hmat, xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, img);
             break;
         default:
-            hipLaunchKernelGGL((k_warp_fuse<CK, BEV_FUSE_MAX>), grid, block, lds, st, feats, sN, sC, sH, sW, Hmat, xs,
-                               ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out);
+            hipLaunchKernelGGL((k_warp_fuse<CK, BEV_FUSE_MAX, VEC>), grid, block, lds, st, feats, sN, sC, sH, sW, Hmat,
+                               xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, img);
     }
     return last();
+}
+
+template <int CK>
+int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                   const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                   int Wb, int mode, float *out, hipStream_t st) {
+    const bool vec = (sC == 1) && (C % 4 == 0) && (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) &&
+                     (sN % 4 == 0);
+    if (vec)
+        return launch_fuse<CK, true>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                     st);
+    return launch_fuse<CK, false>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
 }
 
 }  // namespace
@@ -418,12 +506,17 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                           int Hb, int Wb, int mode, float *out, void *stream) {
     if (B < 0 || V <= 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B > 65535) return BEV_ERR_ARGS;
+    if ((int64_t)Hf * Wf >= (1 << 22)) return BEV_ERR_ARGS;  // fast_div range of the footprint index
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
     if (B == 0 || C == 0 || Hb == 0 || Wb == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (C <= 4) return launch_fuse<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-    if (C <= 8) return launch_fuse<8>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-    return launch_fuse<16>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    if (C <= 4)
+        return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    if (C <= 16)
+        return launch_fuse_ck<16>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    if (C <= 32)
+        return launch_fuse_ck<32>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    return launch_fuse_ck<64>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
 }
 
 int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C, int Hf,
