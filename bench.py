@@ -168,7 +168,7 @@ def main():
             if record:
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                 e0.record(stream)
-            if args.warp_only:
+            if args.warp_only and step.feats is not None:
                 feats = step.feats
             else:
                 feats = enc(images)

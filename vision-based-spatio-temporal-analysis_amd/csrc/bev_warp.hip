@@ -349,6 +349,285 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
 }
 
 // -------------------------------------------------------------------------
+// fused warp + reduce, LDS-DMA pipelined (NHWC features, 64-channel chunks)
+// -------------------------------------------------------------------------
+// Same tile / lane mapping and arithmetic as k_warp_fuse, but the footprint
+// image of view v+1 is copied global -> LDS by global_load_lds_dwordx4 (no
+// registers, asynchronous) while view v is being sampled, so the copy latency
+// hides under compute and each view costs ONE workgroup barrier.
+//
+// Image layout: pixel p at byte p*272 = 17 slots of 16 B (16 channel groups +
+// 1 pad slot, the same conflict-free padded stride as the register path).  A
+// DMA wave-instruction writes 64 consecutive slots (1 KiB, lane-linear); the
+// pad is produced by giving each lane the GLOBAL source of its slot
+// (slot -> pixel slot/17, channel group slot%17), pad slots re-read group 0.
+// Images live in a ring inside the LDS pool: the next view's image is placed
+// after (or, wrapping, before) the current one; a footprint that does not fit
+// beside the current image is staged synchronously after the current view
+// (and split into overlapping blocks if it exceeds the whole pool).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+constexpr int DPS = 272;  // bytes per staged pixel
+
+__device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)p;
+}
+
+// Issue the DMA of footprint block (sx0, sy0, sbw x sbh) into LDS byte offset `off`.
+__device__ __forceinline__ void dma_block(const float *__restrict__ f, int64_t sH, int64_t sW, int sx0, int sy0,
+                                          int sbw, int npix, unsigned char *smem, int off, int wave, int lane) {
+    const int ninstr = (npix * 17 + 63) >> 6;
+    const float inv_bw = 1.0f / (float)sbw;
+    for (int k = wave; k < ninstr; k += FT_NT / 64) {
+        const int slot = k * 64 + lane;
+        const int p = slot / 17, sl = slot - p * 17;
+        const float *src = f;  // any valid address for the tail lanes
+        if (p < npix) {
+            const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
+            src = f + (int64_t)(sy0 + py) * sH + (int64_t)(sx0 + px) * sW + ((sl < 16) ? sl * 4 : 0);
+        }
+        // Inline asm on purpose: hipcc treats the builtin's LDS write as aliasing every
+        // later ds_read and drains vmcnt before them, which would serialise the
+        // prefetch.  Completion is waited for explicitly (vmcnt(0) + barrier) before
+        // the image is read.  M0 is saved/restored inside the statement.
+        const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_base(smem) + off + k * 1024));
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(dst)
+            : "memory");
+    }
+}
+
+// Footprint bbox of the workgroup for one view (wave partials -> red[] -> block).
+struct Box {
+    int x0, y0, x1, y1;
+};
+
+__device__ __forceinline__ Box wave_box(const Taps &t) {
+    Box b{0x7fffffff, 0x7fffffff, -1, -1};
+    if (t.valid) {
+        b.x0 = (t.valid & 5) ? t.x0 : t.x0 + 1;
+        b.x1 = (t.valid & 10) ? t.x0 + 1 : t.x0;
+        b.y0 = (t.valid & 3) ? t.y0 : t.y0 + 1;
+        b.y1 = (t.valid & 12) ? t.y0 + 1 : t.y0;
+    }
+    b.x0 = wave_min(b.x0);
+    b.y0 = wave_min(b.y0);
+    b.x1 = wave_max(b.x1);
+    b.y1 = wave_max(b.y1);
+    return b;
+}
+
+__device__ __forceinline__ void put_box(int *rp, const Box &b, int wave, int lane) {
+    if (lane == 0) {
+        rp[wave] = b.x0;
+        rp[4 + wave] = b.y0;
+        rp[8 + wave] = b.x1;
+        rp[12 + wave] = b.y1;
+    }
+}
+
+__device__ __forceinline__ Box get_box(const int *rp) {
+    Box b{rp[0], rp[4], rp[8], rp[12]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        b.x0 = min(b.x0, rp[w]);
+        b.y0 = min(b.y0, rp[4 + w]);
+        b.x1 = max(b.x1, rp[8 + w]);
+        b.y1 = max(b.y1, rp[12 + w]);
+    }
+    b.x0 = __builtin_amdgcn_readfirstlane(b.x0);
+    b.y0 = __builtin_amdgcn_readfirstlane(b.y0);
+    b.x1 = __builtin_amdgcn_readfirstlane(b.x1);
+    b.y1 = __builtin_amdgcn_readfirstlane(b.y1);
+    return b;
+}
+
+// Sample one view for the lanes with `mine` from an image at LDS byte offset
+// `ib` (origin sx0, sy0, width sbw); invalid taps read the zero pixel `zp`.
+template <int MODE>
+__device__ __forceinline__ void sample_view(float (&acc)[64], const Taps &t, bool mine, int v,
+                                            const unsigned char *smem, int ib, int sx0, int sy0, int sbw, int zp) {
+    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * DPS;
+    const unsigned char *a0 = smem + ((mine && (t.valid & 1)) ? pb : zp);
+    const unsigned char *a1 = smem + ((mine && (t.valid & 2)) ? pb + DPS : zp);
+    const unsigned char *a2 = smem + ((mine && (t.valid & 4)) ? pb + sbw * DPS : zp);
+    const unsigned char *a3 = smem + ((mine && (t.valid & 8)) ? pb + (sbw + 1) * DPS : zp);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+        const float4 vnw = *(const float4 *)(a0 + g * 16);
+        const float4 vne = *(const float4 *)(a1 + g * 16);
+        const float4 vsw = *(const float4 *)(a2 + g * 16);
+        const float4 vse = *(const float4 *)(a3 + g * 16);
+        const float sm[4] = {bilerp(vnw.x, vne.x, vsw.x, vse.x, t.w), bilerp(vnw.y, vne.y, vsw.y, vse.y, t.w),
+                             bilerp(vnw.z, vne.z, vsw.z, vse.z, t.w), bilerp(vnw.w, vne.w, vsw.w, vse.w, t.w)};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float &a = acc[4 * g + u];
+            const float r = (MODE == BEV_FUSE_MAX) ? ((v == 0) ? sm[u] : nan_max(a, sm[u])) : a + sm[u];
+            a = mine ? r : a;
+        }
+        if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ void zero_view(float (&acc)[64], int v) {
+    if (MODE == BEV_FUSE_MAX) {
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc[q] = (v == 0) ? 0.0f : nan_max(acc[q], 0.0f);
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                            int64_t sW, const float *__restrict__ Hmat,
+                                                            const float *__restrict__ xs,
+                                                            const float *__restrict__ ys, int V, int C, int Hf,
+                                                            int Wf, float sx, float sy, int Hb, int Wb,
+                                                            float *__restrict__ out, int pool) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int zp = pool;                                      // zero pixel (256 B)
+    int *red = reinterpret_cast<int *>(smem + pool + 256);    // [2 parity][16]
+    const int maxpix = pool / DPS - 4;                        // ~1 KiB DMA rounding slack
+
+    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, nt = ntx * nty;
+    int tile = blockIdx.x;
+    {
+        const int q = nt / 8, r = nt % 8, x = tile % 8;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    const int tyb = tile / ntx, txb = tile - tyb * ntx;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i = tyb * FT_H + wave * 2 + (lane >> 5);
+    const int j = txb * FT_W + (lane & 31);
+    const int b = blockIdx.y;
+    const bool inside = (i < Hb) && (j < Wb);
+    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
+    const size_t plane = (size_t)Hb * Wb;
+    float *o = out + (size_t)b * C * plane + (size_t)(inside ? i : 0) * Wb + (inside ? j : 0);
+    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    auto taps_of = [&](int v) {
+        float h[9];
+        load_h(Hmat, b * V + v, h);
+        Taps t = cell_taps(h, cx, cy, Hf, Wf, sx, sy);
+        if (!inside) t.valid = 0;
+        return t;
+    };
+
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        float acc[64];
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc[q] = 0.0f;
+
+        // prologue: plan + prefetch view 0
+        Taps tn = taps_of(0);
+        bool anyn = __ballot(tn.valid != 0) != 0ull;
+        put_box(red, wave_box(tn), wave, lane);
+        __syncthreads();
+        Box bn = get_box(red);
+        int offn = -1;
+        {
+            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+            if (bn.x1 >= 0 && npix <= maxpix) {
+                offn = 0;
+                dma_block(feats + (int64_t)(b * V) * sN + c0, sH, sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem,
+                          0, wave, lane);
+            }
+        }
+
+        for (int v = 0; v < V; ++v) {
+            const Taps t = tn;
+            const bool wave_any = anyn;
+            const Box bx = bn;
+            const int off = offn;
+            const bool empty = bx.x1 < 0;
+            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+            const float *f = feats + (int64_t)(b * V + v) * sN + c0;
+            bool done = empty;
+            if (!empty && off < 0) {
+                // ---- synchronous staging (did not fit beside the previous image) ----
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                    hb = min(bh, maxpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                int mkx = 0, mky = 0;
+                if (!single && t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
+                }
+                if (!single && !t.valid) zero_view<MODE>(acc, v);
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        __syncthreads();  // earlier LDS images are no longer read
+                        dma_block(f, sH, sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __syncthreads();
+                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
+                        if (go) sample_view<MODE>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        else if (single) zero_view<MODE>(acc, v);
+                    }
+                done = true;
+            }
+            // ---- look ahead: taps + bbox of view v+1 ----------------------------------
+            const bool more = v + 1 < V;
+            if (more) {
+                tn = taps_of(v + 1);
+                anyn = __ballot(tn.valid != 0) != 0ull;
+                put_box(red + ((v + 1) & 1) * 16, wave_box(tn), wave, lane);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v landed
+            __syncthreads();  // (X) all DMA of view v landed; bbox partials of v+1 visible
+            if (more) {
+                bn = get_box(red + ((v + 1) & 1) * 16);
+                offn = -1;
+                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+                if (bn.x1 >= 0 && npix <= maxpix) {
+                    const int need = ((npix * 17 + 63) >> 6) * 1024;
+                    // ring placement beside the live image of view v (if any)
+                    const int lo = (!done && off >= 0) ? off : 0;
+                    const int hi = (!done && off >= 0) ? off + (((bw * bh * 17 + 63) >> 6) * 1024) : 0;
+                    if (hi + need <= pool) offn = hi;
+                    else if (need <= lo) offn = 0;
+                    if (offn >= 0)
+                        dma_block(feats + (int64_t)(b * V + v + 1) * sN + c0, sH, sW, bn.x0, bn.y0,
+                                  bn.x1 - bn.x0 + 1, npix, smem, offn, wave, lane);
+                }
+            }
+            // ---- sample view v from its prefetched image ------------------------------
+            if (!done) {
+                if (wave_any) sample_view<MODE>(acc, t, true, v, smem, off, bx.x0, bx.y0, bw, zp);
+                else zero_view<MODE>(acc, v);
+            } else if (empty) {
+                zero_view<MODE>(acc, v);
+            }
+        }
+        if (inside) {
+            const float fv = (float)V;
+#pragma unroll
+            for (int q = 0; q < 64; ++q) {
+                const float r = (MODE == BEV_FUSE_MEAN) ? acc[q] / fv : acc[q];
+                __builtin_nontemporal_store(r, o + (size_t)(c0 + q) * plane);
+            }
+        }
+        __syncthreads();  // next chunk reuses red[] and the pool
+    }
+}
+
+// -------------------------------------------------------------------------
 // backward (grad w.r.t. feats): scatter-add with float atomics
 // -------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_warp_bwd(const float *__restrict__ gout, const float *__restrict__ Hmat,
@@ -441,6 +720,37 @@ int launch_fuse(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t 
     return last();
 }
 
+// LDS pool of the DMA-pipelined fused warp (bytes); BEV_WARP_POOL_KB overrides.
+inline int warp_pool_bytes() {
+    static int v = [] {
+        const char *e = getenv("BEV_WARP_POOL_KB");
+        int kb = e ? atoi(e) : 72;
+        if (kb < 8) kb = 8;
+        if (kb > 150) kb = 150;
+        return kb * 1024;
+    }();
+    return v;
+}
+
+inline int launch_fuse_dma(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
+                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                           int Hb, int Wb, int mode, float *out, hipStream_t st) {
+    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
+    dim3 grid(ntiles, B), block(FT_NT);
+    const int pool = warp_pool_bytes();
+    const size_t lds = pool + 256 + 32 * sizeof(int);
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL(k_warp_fuse_dma<BEV_FUSE_SUM>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
+                           C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL(k_warp_fuse_dma<BEV_FUSE_MEAN>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
+                           C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    else
+        hipLaunchKernelGGL(k_warp_fuse_dma<BEV_FUSE_MAX>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
+                           C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    return last();
+}
+
 template <int CK>
 int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
                    const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
@@ -510,6 +820,9 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
     if (B == 0 || C == 0 || Hb == 0 || Wb == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    const bool dma_ok = (sC == 1) && (C % 64 == 0) && (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) &&
+                        (sH % 4 == 0) && (sN % 4 == 0) && getenv("BEV_WARP_NO_DMA") == nullptr;
+    if (dma_ok) return launch_fuse_dma(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 16)
