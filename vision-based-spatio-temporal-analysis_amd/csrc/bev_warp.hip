@@ -375,18 +375,18 @@ __device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
 }
 
 // Issue the DMA of footprint block (sx0, sy0, sbw x sbh) into LDS byte offset `off`.
-__device__ __forceinline__ void dma_block(const float *__restrict__ f, int64_t sH, int64_t sW, int sx0, int sy0,
-                                          int sbw, int npix, unsigned char *smem, int off, int wave, int lane) {
+// Element offsets are 32-bit (the launcher checks that a feature map fits).
+__device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
+                                          int npix, unsigned char *smem, int off, int wave, int lane) {
     const int ninstr = (npix * 17 + 63) >> 6;
     const float inv_bw = 1.0f / (float)sbw;
+    const int base = sy0 * sH + sx0 * sW;
     for (int k = wave; k < ninstr; k += FT_NT / 64) {
         const int slot = k * 64 + lane;
         const int p = slot / 17, sl = slot - p * 17;
-        const float *src = f;  // any valid address for the tail lanes
-        if (p < npix) {
-            const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
-            src = f + (int64_t)(sy0 + py) * sH + (int64_t)(sx0 + px) * sW + ((sl < 16) ? sl * 4 : 0);
-        }
+        const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
+        const int eo = base + py * sH + px * sW + ((sl < 16) ? sl * 4 : 0);
+        const float *src = f + ((p < npix) ? eo : 0);  // tail lanes: any valid address
         // Inline asm on purpose: hipcc treats the builtin's LDS write as aliasing every
         // later ds_read and drains vmcnt before them, which would serialise the
         // prefetch.  Completion is waited for explicitly (vmcnt(0) + barrier) before
@@ -407,18 +407,38 @@ struct Box {
     int x0, y0, x1, y1;
 };
 
+// Packed (x, y) 16-bit pairs: min of (x0, y0) and min of (-x1, -y1) -> 2 shuffles per step.
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int pk_min(int a, int b) {
+    short2_t x = __builtin_bit_cast(short2_t, a), y = __builtin_bit_cast(short2_t, b);
+    return __builtin_bit_cast(int, __builtin_elementwise_min(x, y));
+}
+
+__device__ __forceinline__ int pk2(int lo, int hi) { return (lo & 0xffff) | (hi << 16); }
+__device__ __forceinline__ int pk_lo(int v) { return (int)(short)(v & 0xffff); }
+__device__ __forceinline__ int pk_hi(int v) { return v >> 16; }
+
 __device__ __forceinline__ Box wave_box(const Taps &t) {
-    Box b{0x7fffffff, 0x7fffffff, -1, -1};
+    // sentinels: x0/y0 -> 32767, -x1/-y1 -> 32767 (empty); coordinates are < 2^14
+    int mn = pk2(32767, 32767), mx = pk2(32767, 32767);
     if (t.valid) {
-        b.x0 = (t.valid & 5) ? t.x0 : t.x0 + 1;
-        b.x1 = (t.valid & 10) ? t.x0 + 1 : t.x0;
-        b.y0 = (t.valid & 3) ? t.y0 : t.y0 + 1;
-        b.y1 = (t.valid & 12) ? t.y0 + 1 : t.y0;
+        const int x0 = (t.valid & 5) ? t.x0 : t.x0 + 1, x1 = (t.valid & 10) ? t.x0 + 1 : t.x0;
+        const int y0 = (t.valid & 3) ? t.y0 : t.y0 + 1, y1 = (t.valid & 12) ? t.y0 + 1 : t.y0;
+        mn = pk2(x0, y0);
+        mx = pk2(-x1, -y1);
     }
-    b.x0 = wave_min(b.x0);
-    b.y0 = wave_min(b.y0);
-    b.x1 = wave_max(b.x1);
-    b.y1 = wave_max(b.y1);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mn = pk_min(mn, __shfl_xor(mn, o));
+        mx = pk_min(mx, __shfl_xor(mx, o));
+    }
+    Box b;
+    if (pk_lo(mn) == 32767) {
+        b = Box{0x7fffffff, 0x7fffffff, -1, -1};
+    } else {
+        b = Box{pk_lo(mn), pk_hi(mn), -pk_lo(mx), -pk_hi(mx)};
+    }
     return b;
 }
 
@@ -449,7 +469,7 @@ __device__ __forceinline__ Box get_box(const int *rp) {
 
 // Sample one view for the lanes with `mine` from an image at LDS byte offset
 // `ib` (origin sx0, sy0, width sbw); invalid taps read the zero pixel `zp`.
-template <int MODE>
+template <int MODE, int WIN>
 __device__ __forceinline__ void sample_view(float (&acc)[64], const Taps &t, bool mine, int v,
                                             const unsigned char *smem, int ib, int sx0, int sy0, int sbw, int zp) {
     const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * DPS;
@@ -468,10 +488,10 @@ __device__ __forceinline__ void sample_view(float (&acc)[64], const Taps &t, boo
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             float &a = acc[4 * g + u];
-            const float r = (MODE == BEV_FUSE_MAX) ? ((v == 0) ? sm[u] : nan_max(a, sm[u])) : a + sm[u];
+            const float r = (MODE == BEV_FUSE_MAX) ? nan_max(a, sm[u]) : a + sm[u];
             a = mine ? r : a;
         }
-        if ((g & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        if ((g % WIN) == WIN - 1) __builtin_amdgcn_sched_barrier(0);  // bound LDS-read lookahead
     }
 }
 
@@ -479,12 +499,12 @@ template <int MODE>
 __device__ __forceinline__ void zero_view(float (&acc)[64], int v) {
     if (MODE == BEV_FUSE_MAX) {
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = (v == 0) ? 0.0f : nan_max(acc[q], 0.0f);
+        for (int q = 0; q < 64; ++q) acc[q] = nan_max(acc[q], 0.0f);
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restrict__ feats, int64_t sN, int64_t sH,
+template <int MODE, int OCC>
+__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_dma(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                             int64_t sW, const float *__restrict__ Hmat,
                                                             const float *__restrict__ xs,
                                                             const float *__restrict__ ys, int V, int C, int Hf,
@@ -509,7 +529,6 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restr
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
-    float *o = out + (size_t)b * C * plane + (size_t)(inside ? i : 0) * Wb + (inside ? j : 0);
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
 
     auto taps_of = [&](int v) {
@@ -521,9 +540,10 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restr
     };
 
     for (int c0 = 0; c0 < C; c0 += 64) {
+        // max: -inf is the identity of the NaN-propagating max, so no first-view special case
         float acc[64];
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = 0.0f;
+        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
 
         // prologue: plan + prefetch view 0
         Taps tn = taps_of(0);
@@ -536,8 +556,8 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restr
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
             if (bn.x1 >= 0 && npix <= maxpix) {
                 offn = 0;
-                dma_block(feats + (int64_t)(b * V) * sN + c0, sH, sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem,
-                          0, wave, lane);
+                dma_block(feats + (int64_t)(b * V) * sN + c0, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1,
+                          npix, smem, 0, wave, lane);
             }
         }
 
@@ -572,12 +592,12 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restr
                         const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
                         const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
                         __syncthreads();  // earlier LDS images are no longer read
-                        dma_block(f, sH, sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane);
+                        dma_block(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane);
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
                         const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
                         const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        if (go) sample_view<MODE, (OCC >= 4 ? 1 : 4)>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
                         else if (single) zero_view<MODE>(acc, v);
                     }
                 done = true;
@@ -603,13 +623,13 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restr
                     if (hi + need <= pool) offn = hi;
                     else if (need <= lo) offn = 0;
                     if (offn >= 0)
-                        dma_block(feats + (int64_t)(b * V + v + 1) * sN + c0, sH, sW, bn.x0, bn.y0,
+                        dma_block(feats + (int64_t)(b * V + v + 1) * sN + c0, (int)sH, (int)sW, bn.x0, bn.y0,
                                   bn.x1 - bn.x0 + 1, npix, smem, offn, wave, lane);
                 }
             }
             // ---- sample view v from its prefetched image ------------------------------
             if (!done) {
-                if (wave_any) sample_view<MODE>(acc, t, true, v, smem, off, bx.x0, bx.y0, bw, zp);
+                if (wave_any) sample_view<MODE, (OCC >= 4 ? 1 : 4)>(acc, t, true, v, smem, off, bx.x0, bx.y0, bw, zp);
                 else zero_view<MODE>(acc, v);
             } else if (empty) {
                 zero_view<MODE>(acc, v);
@@ -617,13 +637,190 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse_dma(const float *__restr
         }
         if (inside) {
             const float fv = (float)V;
+            const int cell = i * Wb + j;
 #pragma unroll
             for (int q = 0; q < 64; ++q) {
                 const float r = (MODE == BEV_FUSE_MEAN) ? acc[q] / fv : acc[q];
-                __builtin_nontemporal_store(r, o + (size_t)(c0 + q) * plane);
+                float *oc = out + ((size_t)b * C + c0 + q) * plane;  // wave-uniform base
+                __builtin_nontemporal_store(r, oc + cell);
             }
         }
         __syncthreads();  // next chunk reuses red[] and the pool
+    }
+}
+
+// -------------------------------------------------------------------------
+// fused warp + reduce, one wave per workgroup, no barriers (default DMA path)
+// -------------------------------------------------------------------------
+// A workgroup is ONE wavefront owning a WT_H x WT_W = 4 x 16 tile of BEV cells
+// (lane = cell; each per-channel store is four 64-B row pieces).  The wave
+// computes its own footprint bbox (shuffles), copies the footprint image of
+// view v+1 into its private LDS ring by LDS-DMA (lane-masked to the exact
+// 272-B/pixel image) and samples view v meanwhile; LDS-DMA completion is
+// ordered for the issuing wave by its own vmcnt, so no workgroup barrier is
+// ever needed and waves run free.  Footprints that do not fit beside the live
+// image are copied after it (waited), larger-than-ring ones in overlapping
+// blocks (same decomposition as the register-staged kernel).
+constexpr int WT_W = 16, WT_H = 4;
+
+__device__ __forceinline__ void dma_wave(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
+                                         int npix, unsigned char *smem, int off, int lane) {
+    const int nslot = npix * 17;
+    const float inv_bw = 1.0f / (float)sbw;
+    const int base = sy0 * sH + sx0 * sW;
+    for (int k = 0; k * 64 < nslot; ++k) {
+        const int slot = k * 64 + lane;
+        const int p = slot / 17, sl = slot - p * 17;
+        const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
+        const float *src = f + base + py * sH + px * sW + ((sl < 16) ? sl * 4 : 0);
+        const unsigned dst = lds_base(smem) + off + k * 1024;
+        if (slot < nslot) {  // exec-masked tail: the image is exactly npix * 272 B
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(src), "s"(dst)
+                : "memory");
+        }
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64, 3) void k_warp_fuse_wave(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                          int64_t sW, const float *__restrict__ Hmat,
+                                                          const float *__restrict__ xs,
+                                                          const float *__restrict__ ys, int V, int C, int Hf, int Wf,
+                                                          float sx, float sy, int Hb, int Wb, float *__restrict__ out,
+                                                          int ring) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int ZP = 0, RB = 256;  // zero pixel, ring base
+    const int maxpix = ring / DPS;
+    const int ntx = (Wb + WT_W - 1) / WT_W, nty = (Hb + WT_H - 1) / WT_H, nt = ntx * nty;
+    int tile = blockIdx.x;
+    {
+        const int q = nt / 8, r = nt % 8, x = tile % 8;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    const int tyb = tile / ntx, txb = tile - tyb * ntx;
+    const int lane = threadIdx.x;
+    const int i = tyb * WT_H + (lane >> 4);
+    const int j = txb * WT_W + (lane & 15);
+    const int b = blockIdx.y;
+    const bool inside = (i < Hb) && (j < Wb);
+    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
+    const size_t plane = (size_t)Hb * Wb;
+    const int isH = (int)sH, isW = (int)sW;
+    if (lane < 16) *(float4 *)(smem + ZP + lane * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    auto taps_of = [&](int v) {
+        float h[9];
+        load_h(Hmat, b * V + v, h);
+        Taps t = cell_taps(h, cx, cy, Hf, Wf, sx, sy);
+        if (!inside) t.valid = 0;
+        return t;
+    };
+    auto uniform_box = [&](const Taps &t) {
+        Box bx = wave_box(t);
+        bx.x0 = __builtin_amdgcn_readfirstlane(bx.x0);
+        bx.y0 = __builtin_amdgcn_readfirstlane(bx.y0);
+        bx.x1 = __builtin_amdgcn_readfirstlane(bx.x1);
+        bx.y1 = __builtin_amdgcn_readfirstlane(bx.y1);
+        return bx;
+    };
+
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        float acc[64];
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        const float *fb = feats + (int64_t)(b * V) * sN + c0;
+
+        Taps tn = taps_of(0);
+        Box bn = uniform_box(tn);
+        int offn = -1;
+        {
+            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+            if (bn.x1 >= 0 && npix <= maxpix) {
+                offn = RB;
+                dma_wave(fb, isH, isW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, RB, lane);
+            }
+        }
+        for (int v = 0; v < V; ++v) {
+            const Taps t = tn;
+            const Box bx = bn;
+            const int off = offn;
+            const bool empty = bx.x1 < 0;
+            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+            const float *f = fb + (int64_t)v * sN;
+            bool done = empty;
+            if (!empty && off < 0) {
+                // ---- synchronous copy (and block split when larger than the ring) ----
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                    hb = min(bh, maxpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                int mkx = 0, mky = 0;
+                if (!single && t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
+                }
+                if (!single && !t.valid) zero_view<MODE>(acc, v);
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // ring free
+                        dma_wave(f, isH, isW, sx0, sy0, sbw, sbw * sbh, smem, RB, lane);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                        const bool go = __ballot(single ? (t.valid != 0) : mine) != 0ull;
+                        if (go) sample_view<MODE, 2>(acc, t, mine, v, smem, RB, sx0, sy0, sbw, ZP);
+                        else if (single) zero_view<MODE>(acc, v);
+                    }
+                done = true;
+            }
+            const bool more = v + 1 < V;
+            if (more) {
+                tn = taps_of(v + 1);
+                bn = uniform_box(tn);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image of view v landed (this wave's DMA)
+            if (more) {
+                offn = -1;
+                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+                if (bn.x1 >= 0 && npix <= maxpix) {
+                    const int need = npix * DPS;
+                    const bool live = !done && off >= 0;
+                    const int lo = live ? off : RB, hi = live ? off + bw * bh * DPS : RB;
+                    if (hi + need <= RB + ring) offn = hi;
+                    else if (RB + need <= lo) offn = RB;
+                    if (offn >= 0)
+                        dma_wave(fb + (int64_t)(v + 1) * sN, isH, isW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem,
+                                 offn, lane);
+                }
+            }
+            if (!done) {
+                if (__ballot(t.valid != 0) != 0ull) sample_view<MODE, 2>(acc, t, true, v, smem, off, bx.x0, bx.y0, bw, ZP);
+                else zero_view<MODE>(acc, v);
+            } else if (empty) {
+                zero_view<MODE>(acc, v);
+            }
+        }
+        if (inside) {
+            const float fv = (float)V;
+            const int cell = i * Wb + j;
+#pragma unroll
+            for (int q = 0; q < 64; ++q) {
+                const float r = (MODE == BEV_FUSE_MEAN) ? acc[q] / fv : acc[q];
+                float *oc = out + ((size_t)b * C + c0 + q) * plane;
+                __builtin_nontemporal_store(r, oc + cell);
+            }
+        }
     }
 }
 
@@ -732,23 +929,78 @@ inline int warp_pool_bytes() {
     return v;
 }
 
+// Waves per SIMD the DMA kernel is built for (2: 72 KB pool, <=256 VGPR;
+// 4: 36 KB pool, <=128 VGPR); BEV_WARP_OCC overrides.
+inline int warp_occ() {
+    static int v = [] {
+        const char *e = getenv("BEV_WARP_OCC");
+        return (e && atoi(e) == 2) ? 2 : 4;
+    }();
+    return v;
+}
+
+template <int OCC>
+int launch_fuse_dma_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
+                        int mode, float *out, hipStream_t st, int pool) {
+    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
+    dim3 grid(ntiles, B), block(FT_NT);
+    const size_t lds = pool + 256 + 32 * sizeof(int);
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL((k_warp_fuse_dma<BEV_FUSE_SUM, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
+                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL((k_warp_fuse_dma<BEV_FUSE_MEAN, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
+                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    else
+        hipLaunchKernelGGL((k_warp_fuse_dma<BEV_FUSE_MAX, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
+                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    return last();
+}
+
+// Per-wave LDS ring of the barrier-free kernel (bytes); BEV_WARP_RING_KB overrides.
+inline int warp_ring_bytes() {
+    static int v = [] {
+        const char *e = getenv("BEV_WARP_RING_KB");
+        int kb = e ? atoi(e) : 13;
+        if (kb < 2) kb = 2;
+        if (kb > 60) kb = 60;
+        return kb * 1024 - 256;
+    }();
+    return v;
+}
+
+inline int launch_fuse_wave(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
+                            const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                            int Hb, int Wb, int mode, float *out, hipStream_t st) {
+    const int ntiles = ((Wb + WT_W - 1) / WT_W) * ((Hb + WT_H - 1) / WT_H);
+    dim3 grid(ntiles, B), block(64);
+    const int ring = warp_ring_bytes();
+    const size_t lds = 256 + ring;
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL(k_warp_fuse_wave<BEV_FUSE_SUM>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
+                           C, Hf, Wf, sx, sy, Hb, Wb, out, ring);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL(k_warp_fuse_wave<BEV_FUSE_MEAN>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
+                           C, Hf, Wf, sx, sy, Hb, Wb, out, ring);
+    else
+        hipLaunchKernelGGL(k_warp_fuse_wave<BEV_FUSE_MAX>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
+                           C, Hf, Wf, sx, sy, Hb, Wb, out, ring);
+    return last();
+}
+
 inline int launch_fuse_dma(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
                            const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                            int Hb, int Wb, int mode, float *out, hipStream_t st) {
-    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
-    dim3 grid(ntiles, B), block(FT_NT);
-    const int pool = warp_pool_bytes();
-    const size_t lds = pool + 256 + 32 * sizeof(int);
-    if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL(k_warp_fuse_dma<BEV_FUSE_SUM>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
-                           C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL(k_warp_fuse_dma<BEV_FUSE_MEAN>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
-                           C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
-    else
-        hipLaunchKernelGGL(k_warp_fuse_dma<BEV_FUSE_MAX>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
-                           C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
-    return last();
+    const char *e = getenv("BEV_WARP_POOL_KB");
+    if (warp_occ() == 2) {
+        const int pool = e ? warp_pool_bytes() : 72 * 1024;
+        return launch_fuse_dma_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                      st, pool);
+    }
+    const int pool = e ? warp_pool_bytes() : 36 * 1024;
+    return launch_fuse_dma_occ<4>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                  pool);
 }
 
 template <int CK>
@@ -820,8 +1072,10 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
     if (B == 0 || C == 0 || Hb == 0 || Wb == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const bool dma_ok = (sC == 1) && (C % 64 == 0) && (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) &&
+    const bool dma_ok = (sC == 1) && (C % 64 == 0) && Hf < 16384 && Wf < 16384 && ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) && (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) &&
                         (sH % 4 == 0) && (sN % 4 == 0) && getenv("BEV_WARP_NO_DMA") == nullptr;
+    if (dma_ok && getenv("BEV_WARP_WAVE") != nullptr)
+        return launch_fuse_wave(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (dma_ok) return launch_fuse_dma(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
