@@ -30,8 +30,8 @@
 
 namespace {
 
-constexpr int BK = 16;       // K step
-constexpr int LROW = BK + 4; // LDS row stride in floats (80 B)
+constexpr int BK = 32;        // K step
+constexpr int LROW = BK + 4;  // LDS row stride in floats (144 B: 9 slots, odd -> conflict-free b128 rows)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -57,11 +57,11 @@ __global__ void k_pack(const float *__restrict__ w, int Co, int Ci, int KH, int 
 }
 
 struct ConvArgs {
-    const float *x;
-    const float *wp;
-    const float *bias;
-    const float *res;
-    float *y;
+    const float *__restrict__ x;
+    const float *__restrict__ wp;
+    const float *__restrict__ bias;
+    const float *__restrict__ res;
+    float *__restrict__ y;
     int N, H, W, Ci, Co, KH, KW, stride, pad, Ho, Wo;
     int relu;
     int in_nchw;  // generic loader only: input is NCHW instead of NHWC
@@ -70,20 +70,16 @@ struct ConvArgs {
     int Kp;
 };
 
-// A-tile loader, fast path: NHWC input with Ci % 16 == 0.  Each thread owns
-// ROWS rows of the tile (rows tid/4 + 64*r) and one 16-B quad of the K step.
+// Per-thread view of the A tile rows it loads: rows (tid >> 3) + 32 r, one 16-B quad.
 template <int ROWS>
-struct LoaderA16 {
-    int64_t pix[ROWS];  // base element offset of image n (n*H*W*Ci)
+struct RowsA {
+    int64_t pix[ROWS];  // element offset of the row's image
     int iy0[ROWS], ix0[ROWS];
     bool ok[ROWS];
-    int quad;
-
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
-        quad = tid & 3;
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
-            const int64_t m = m0 + (tid >> 2) + 64 * r;
+            const int64_t m = m0 + (tid >> 3) + 32 * r;
             ok[r] = m < a.M;
             const int64_t mm = ok[r] ? m : 0;
             const int ox = (int)(mm % a.Wo);
@@ -93,49 +89,56 @@ struct LoaderA16 {
             pix[r] = (int64_t)n * a.H * a.W * a.Ci;
             iy0[r] = oy * a.stride - a.pad;
             ix0[r] = ox * a.stride - a.pad;
-        }
-    }
-    __device__ void load(const ConvArgs &a, int k0, float4 (&v)[ROWS]) const {
-        const int rr = k0 / a.Ci;          // (ky, kx) of this K step
-        const int ci = k0 - rr * a.Ci + quad * 4;
-        const int ky = rr / a.KW, kx = rr - (rr / a.KW) * a.KW;
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            const int iy = iy0[r] + ky, ix = ix0[r] + kx;
-            const bool in = ok[r] && (k0 < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            v[r] = in ? *(const float4 *)(a.x + pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
 };
 
-// A-tile loader, generic path: any Ci, NHWC or NCHW input, element-wise.
+// A loader, fast path: NHWC, Ci % 32 == 0 -> a K step is one (ky, kx) and 32
+// consecutive channels, i.e. one contiguous 128-B run per output pixel.  The
+// (ky, kx, ci0) position advances incrementally (no divisions in the loop).
 template <int ROWS>
-struct LoaderAGen {
-    int64_t pix[ROWS];
-    int iy0[ROWS], ix0[ROWS];
-    bool ok[ROWS];
-    int quad;
-    bool nchw;
-
-    __device__ void init(const ConvArgs &a, int64_t m0, int tid, bool in_nchw) {
-        quad = tid & 3;
-        nchw = in_nchw;
+struct LoaderFast {
+    RowsA<ROWS> rows;
+    int quad, ky, kx, ci0;
+    __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+        rows.init(a, m0, tid);
+        quad = tid & 7;
+        ky = kx = ci0 = 0;
+    }
+    __device__ void load(const ConvArgs &a, float4 (&v)[ROWS]) const {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
-            const int64_t m = m0 + (tid >> 2) + 64 * r;
-            ok[r] = m < a.M;
-            const int64_t mm = ok[r] ? m : 0;
-            const int ox = (int)(mm % a.Wo);
-            const int64_t t = mm / a.Wo;
-            const int oy = (int)(t % a.Ho);
-            const int n = (int)(t / a.Ho);
-            pix[r] = (int64_t)n * a.H * a.W * a.Ci;
-            iy0[r] = oy * a.stride - a.pad;
-            ix0[r] = ox * a.stride - a.pad;
+            const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
+            const bool in = rows.ok[r] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            v[r] = in ? *(const float4 *)(a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    __device__ void load(const ConvArgs &a, int k0, float4 (&v)[ROWS]) const {
+    __device__ void advance(const ConvArgs &a) {
+        ci0 += BK;
+        if (ci0 == a.Ci) {
+            ci0 = 0;
+            if (++kx == a.KW) {
+                kx = 0;
+                ++ky;
+            }
+        }
+    }
+};
+
+// A loader, generic path: any Ci, NHWC or NCHW input, element-wise.
+template <int ROWS>
+struct LoaderGen {
+    RowsA<ROWS> rows;
+    int quad, k0;
+    bool nchw;
+    __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+        rows.init(a, m0, tid);
+        quad = tid & 7;
+        k0 = 0;
+        nchw = a.in_nchw != 0;
+    }
+    __device__ void load(const ConvArgs &a, float4 (&v)[ROWS]) const {
         float e[4][ROWS];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -143,25 +146,27 @@ struct LoaderAGen {
             const int ci = k % a.Ci, rr = k / a.Ci, kx = rr % a.KW, ky = rr / a.KW;
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
-                const int iy = iy0[r] + ky, ix = ix0[r] + kx;
-                const bool in = ok[r] && (k < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-                const int64_t off = nchw ? pix[r] + ((int64_t)ci * a.H + iy) * a.W + ix
-                                         : pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci;
+                const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
+                const bool in = rows.ok[r] && (k < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                const int64_t off = nchw ? rows.pix[r] + ((int64_t)ci * a.H + iy) * a.W + ix
+                                         : rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci;
                 e[q][r] = in ? a.x[off] : 0.0f;
             }
         }
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) v[r] = make_float4(e[0][r], e[1][r], e[2][r], e[3][r]);
     }
+    __device__ void advance(const ConvArgs &) { k0 += BK; }
 };
 
-// WM x WN waves, each 64 x 64 outputs.
-template <int WM, int WN, bool FAST>
+// Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
+template <int WM, int WN, int TM, int TN, bool FAST>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
-    constexpr int BM = WM * 64, BN = WN * 64;
-    constexpr int AROWS = BM / 64;  // rows per thread in the A loader
-    constexpr int BROWS = BN / 64;  // rows per thread in the B loader
-    __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LROW];
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int AROWS = BM / 32;  // A rows per thread (rows tid/8 + 32 r)
+    constexpr int BROWS = BN / 32;
+    constexpr int STAGE = (BM + BN) * LROW;
+    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -170,65 +175,72 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int64_t m0 = (int64_t)(blockIdx.x / n_tiles) * BM;
     const int n0 = (blockIdx.x % n_tiles) * BN;
 
-    // loaders
-    typename std::conditional<FAST, LoaderA16<AROWS>, LoaderAGen<AROWS>>::type la;
-    if constexpr (FAST) la.init(a, m0, tid);
-    else la.init(a, m0, tid, a.in_nchw != 0);
-    const int bq = tid & 3;
-    const float *wrow[BROWS];
-#pragma unroll
-    for (int r = 0; r < BROWS; ++r) wrow[r] = a.wp + (int64_t)(n0 + (tid >> 2) + 64 * r) * a.Kp + bq * 4;
+    typename std::conditional<FAST, LoaderFast<AROWS>, LoaderGen<AROWS>>::type la;
+    la.init(a, m0, tid);
+    const int bq = tid & 7;
+    const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
 
-    f32x16 acc[2][2];
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
     float4 ra[AROWS], rb[BROWS];
-    auto gload = [&](int k0) {
-        la.load(a, k0, ra);
+    int kb = 0;  // k offset of the B panel
+    auto gload = [&]() {
+        la.load(a, ra);
 #pragma unroll
-        for (int r = 0; r < BROWS; ++r) rb[r] = *(const float4 *)(wrow[r] + k0);
+        for (int r = 0; r < BROWS; ++r) rb[r] = *(const float4 *)(wrow + (int64_t)(32 * r) * a.Kp + kb);
+        la.advance(a);
+        kb += BK;
     };
     auto swrite = [&](int buf) {
-        float *As = lds[buf];
-        float *Bs = lds[buf] + BM * LROW;
+        float *As = lds + buf * STAGE;
+        float *Bs = As + BM * LROW;
 #pragma unroll
-        for (int r = 0; r < AROWS; ++r) *(float4 *)(As + ((tid >> 2) + 64 * r) * LROW + bq * 4) = ra[r];
+        for (int r = 0; r < AROWS; ++r) *(float4 *)(As + ((tid >> 3) + 32 * r) * LROW + bq * 4) = ra[r];
 #pragma unroll
-        for (int r = 0; r < BROWS; ++r) *(float4 *)(Bs + ((tid >> 2) + 64 * r) * LROW + bq * 4) = rb[r];
+        for (int r = 0; r < BROWS; ++r) *(float4 *)(Bs + ((tid >> 3) + 32 * r) * LROW + bq * 4) = rb[r];
     };
 
     const int nk = a.Kp / BK;
-    gload(0);
+    gload();
     swrite(0);
     __syncthreads();
     const int r32 = lane & 31, h = lane >> 5;
     for (int ks = 0; ks < nk; ++ks) {
         const int cur = ks & 1;
-        if (ks + 1 < nk) gload((ks + 1) * BK);
-        const float *As = lds[cur];
-        const float *Bs = lds[cur] + BM * LROW;
-        float4 fa[2][2], fb[2][2];
+        if (ks + 1 < nk) gload();
+        const float *As = lds + cur * STAGE;
+        const float *Bs = As + BM * LROW;
+        // MFMA k-slot h of step p reads k = 16 h + p (p = 0..15): per half of the
+        // step each lane reads two contiguous float4 of its row per operand tile.
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float *pa = As + (wm * 64 + i * 32 + r32) * LROW + h * 8;
-            fa[i][0] = *(const float4 *)pa;
-            fa[i][1] = *(const float4 *)(pa + 4);
-            const float *pb = Bs + (wn * 64 + i * 32 + r32) * LROW + h * 8;
-            fb[i][0] = *(const float4 *)pb;
-            fb[i][1] = *(const float4 *)(pb + 4);
-        }
+        for (int half = 0; half < 2; ++half) {
+            float4 fa[TM][2], fb[TN][2];
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
+            for (int i = 0; i < TM; ++i) {
+                const float *pa = As + (wm * TM * 32 + i * 32 + r32) * LROW + h * 16 + half * 8;
+                fa[i][0] = *(const float4 *)pa;
+                fa[i][1] = *(const float4 *)(pa + 4);
+            }
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float av = ((const float *)&fa[i][p >> 2])[p & 3];
+            for (int j = 0; j < TN; ++j) {
+                const float *pb = Bs + (wn * TN * 32 + j * 32 + r32) * LROW + h * 16 + half * 8;
+                fb[j][0] = *(const float4 *)pb;
+                fb[j][1] = *(const float4 *)(pb + 4);
+            }
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const float bv = ((const float *)&fb[j][p >> 2])[p & 3];
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+            for (int p = 0; p < 8; ++p) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const float av = ((const float *)&fa[i][p >> 2])[p & 3];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float bv = ((const float *)&fb[j][p >> 2])[p & 3];
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -238,22 +250,67 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         }
     }
 
-    // epilogue: D[row][col], col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
+    // ---- epilogue through LDS: 32x32 accumulator tile -> rows of float4 ----------
+    // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+    __syncthreads();  // every wave is done reading the staging buffers
+    float *E = lds + wave * (32 * LROW);
+    const bool vec = (a.Co & 3) == 0;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + j * 32 + r32;
-        if (n >= a.Co) continue;
-        const float bv = a.bias ? a.bias[n] : 0.0f;
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int j = 0; j < TN; ++j) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int64_t m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (m >= a.M) continue;
-                float v = acc[i][j][r] + bv;
-                if (a.res) v += a.res[m * a.Co + n];
-                if (a.relu) v = v > 0.0f ? v : 0.0f;
-                a.y[m * a.Co + n] = v;
+            for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * h) * LROW + r32] = acc[i][j][r];
+            // same-wave LDS ops complete in order: no barrier needed
+            const int c4 = lane & 7;
+            const int n = n0 + wn * TN * 32 + j * 32 + c4 * 4;
+            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.bias) {
+                if (vec && n + 3 < a.Co) bv = *(const float4 *)(a.bias + n);
+                else {
+                    bv.x = n < a.Co ? a.bias[n] : 0.f;
+                    bv.y = n + 1 < a.Co ? a.bias[n + 1] : 0.f;
+                    bv.z = n + 2 < a.Co ? a.bias[n + 2] : 0.f;
+                    bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
+                }
+            }
+            float4 v[4], rv[4];
+            int64_t mrow[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = (lane >> 3) + 8 * q;
+                mrow[q] = m0 + wm * TM * 32 + i * 32 + row;
+                v[q] = *(const float4 *)(E + row * LROW + c4 * 4);
+                rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (a.res && mrow[q] < a.M && vec && n + 3 < a.Co)
+                    rv[q] = *(const float4 *)(a.res + mrow[q] * a.Co + n);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (mrow[q] >= a.M) continue;
+                float o[4] = {v[q].x + bv.x, v[q].y + bv.y, v[q].z + bv.z, v[q].w + bv.w};
+                const float rr[4] = {rv[q].x, rv[q].y, rv[q].z, rv[q].w};
+                float *yp = a.y + mrow[q] * a.Co + n;
+                if (vec && n + 3 < a.Co) {
+                    if (a.res) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) o[u] += rr[u];
+                    }
+                    if (a.relu) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) o[u] = o[u] > 0.0f ? o[u] : 0.0f;
+                    }
+                    *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (n + u >= a.Co) break;
+                        float t = o[u];
+                        if (a.res) t += a.res[mrow[q] * a.Co + n + u];
+                        if (a.relu) t = t > 0.0f ? t : 0.0f;
+                        yp[u] = t;
+                    }
+                }
             }
         }
     }
@@ -306,15 +363,15 @@ __global__ void k_transpose(const float *__restrict__ x, int R, int S, float *__
 
 inline int last() { return (int)hipGetLastError(); }
 
-template <int WM, int WN>
+template <int WM, int WN, int TM, int TN>
 int launch_conv(const ConvArgs &a, bool fast, hipStream_t st) {
-    constexpr int BM = WM * 64, BN = WN * 64;
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t m_tiles = (a.M + BM - 1) / BM;
     const int n_tiles = (a.Co + BN - 1) / BN;
     const int64_t blocks = m_tiles * n_tiles;
     if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
-    if (fast) hipLaunchKernelGGL((k_conv<WM, WN, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_conv<WM, WN, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    if (fast) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     return last();
 }
 
@@ -369,8 +426,8 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     a.in_nchw = in_nchw;
     const bool fast = !in_nchw && (Ci % BK == 0);
     hipStream_t st = (hipStream_t)stream;
-    if (Co <= 64) return launch_conv<4, 1>(a, fast, st);
-    return launch_conv<2, 2>(a, fast, st);
+    if (Co <= 64) return launch_conv<4, 1, 1, 2>(a, fast, st);  // 128 x 64 tiles
+    return launch_conv<2, 2, 2, 2>(a, fast, st);                 // 128 x 128 tiles
 }
 
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
