@@ -126,8 +126,9 @@ struct LoaderFast {
     }
 };
 
-// A loader, generic path: any Ci, NHWC or NCHW input, element-wise.
-template <int ROWS>
+// A loader, generic path: any Ci, NHWC or NCHW input, element-wise.  CI / KW
+// > 0 bake the layer geometry in (constant divisors; the ResNet stem uses 3 / 7).
+template <int ROWS, int CI = 0, int KWc = 0>
 struct LoaderGen {
     RowsA<ROWS> rows;
     int quad, k0;
@@ -143,7 +144,8 @@ struct LoaderGen {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int k = k0 + quad * 4 + q;
-            const int ci = k % a.Ci, rr = k / a.Ci, kx = rr % a.KW, ky = rr / a.KW;
+            const int Ci = CI > 0 ? CI : a.Ci, KW = KWc > 0 ? KWc : a.KW;
+            const int ci = k % Ci, rr = k / Ci, kx = rr % KW, ky = rr / KW;
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) {
                 const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
@@ -160,7 +162,8 @@ struct LoaderGen {
 };
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
-template <int WM, int WN, int TM, int TN, bool FAST>
+// LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7)
+template <int WM, int WN, int TM, int TN, int LOADER>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int AROWS = BM / 32;  // A rows per thread (rows tid/8 + 32 r)
@@ -175,7 +178,9 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int64_t m0 = (int64_t)(blockIdx.x / n_tiles) * BM;
     const int n0 = (blockIdx.x % n_tiles) * BN;
 
-    typename std::conditional<FAST, LoaderFast<AROWS>, LoaderGen<AROWS>>::type la;
+    typename std::conditional<LOADER == 1, LoaderFast<AROWS>,
+                              typename std::conditional<LOADER == 2, LoaderGen<AROWS, 3, 7>,
+                                                        LoaderGen<AROWS>>::type>::type la;
     la.init(a, m0, tid);
     const int bq = tid & 7;
     const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
@@ -250,96 +255,116 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         }
     }
 
-    // ---- epilogue through LDS: 32x32 accumulator tile -> rows of float4 ----------
+    // ---- epilogue through LDS ---------------------------------------------------
+    // The wave's (TM*32) x (TN*32) accumulator tile goes to LDS, then every lane
+    // issues ALL its residual float4 loads at once (deep memory parallelism for
+    // the memory-bound 1x1 layers), combines and stores whole float4 row pieces.
     // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+    constexpr int WR = TM * 32, WC = TN * 32, ER = WC + 4;  // wave tile, LDS row stride
+    constexpr int C4 = WC / 4;                              // float4 per row
+    constexpr int RPI = 64 / C4;                            // rows per wave-instruction
+    constexpr int NQ = WR / RPI;                            // float4 per lane
+    static_assert(4 * WR * ER <= 2 * STAGE, "epilogue tile must fit the staging LDS");
     __syncthreads();  // every wave is done reading the staging buffers
-    float *E = lds + wave * (32 * LROW);
-    const bool vec = (a.Co & 3) == 0;
+    float *E = lds + wave * (WR * ER);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * h) * LROW + r32] = acc[i][j][r];
-            // same-wave LDS ops complete in order: no barrier needed
-            const int c4 = lane & 7;
-            const int n = n0 + wn * TN * 32 + j * 32 + c4 * 4;
-            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (a.bias) {
-                if (vec && n + 3 < a.Co) bv = *(const float4 *)(a.bias + n);
-                else {
-                    bv.x = n < a.Co ? a.bias[n] : 0.f;
-                    bv.y = n + 1 < a.Co ? a.bias[n + 1] : 0.f;
-                    bv.z = n + 2 < a.Co ? a.bias[n + 2] : 0.f;
-                    bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
-                }
+            for (int r = 0; r < 16; ++r) E[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
+    // same-wave LDS ops complete in order: no barrier needed
+    const int c4 = lane % C4, rq = lane / C4;
+    const int n = n0 + wn * WC + c4 * 4;
+    const bool nvec = ((a.Co & 3) == 0) && (n + 3 < a.Co);
+    const int64_t mbase = m0 + wm * WR;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.bias) {
+        if (nvec) bv = *(const float4 *)(a.bias + n);
+        else {
+            bv.x = n < a.Co ? a.bias[n] : 0.f;
+            bv.y = n + 1 < a.Co ? a.bias[n + 1] : 0.f;
+            bv.z = n + 2 < a.Co ? a.bias[n + 2] : 0.f;
+            bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
+        }
+    }
+    float4 rv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int64_t m = mbase + rq + RPI * q;
+        rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int row = rq + RPI * q;
+        const int64_t m = mbase + row;
+        if (m >= a.M) continue;
+        const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
+        float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
+        float *yp = a.y + m * a.Co + n;
+        if (nvec) {
+            if (a.res) {
+                o[0] += rv[q].x;
+                o[1] += rv[q].y;
+                o[2] += rv[q].z;
+                o[3] += rv[q].w;
             }
-            float4 v[4], rv[4];
-            int64_t mrow[4];
+            if (a.relu) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int row = (lane >> 3) + 8 * q;
-                mrow[q] = m0 + wm * TM * 32 + i * 32 + row;
-                v[q] = *(const float4 *)(E + row * LROW + c4 * 4);
-                rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (a.res && mrow[q] < a.M && vec && n + 3 < a.Co)
-                    rv[q] = *(const float4 *)(a.res + mrow[q] * a.Co + n);
+                for (int u = 0; u < 4; ++u) o[u] = o[u] > 0.0f ? o[u] : 0.0f;
             }
+            *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (mrow[q] >= a.M) continue;
-                float o[4] = {v[q].x + bv.x, v[q].y + bv.y, v[q].z + bv.z, v[q].w + bv.w};
-                const float rr[4] = {rv[q].x, rv[q].y, rv[q].z, rv[q].w};
-                float *yp = a.y + mrow[q] * a.Co + n;
-                if (vec && n + 3 < a.Co) {
-                    if (a.res) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) o[u] += rr[u];
-                    }
-                    if (a.relu) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) o[u] = o[u] > 0.0f ? o[u] : 0.0f;
-                    }
-                    *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (n + u >= a.Co) break;
-                        float t = o[u];
-                        if (a.res) t += a.res[mrow[q] * a.Co + n + u];
-                        if (a.relu) t = t > 0.0f ? t : 0.0f;
-                        yp[u] = t;
-                    }
-                }
+            for (int u = 0; u < 4; ++u) {
+                if (n + u >= a.Co) break;
+                float t = o[u];
+                if (a.res) t += a.res[m * a.Co + n + u];
+                if (a.relu) t = t > 0.0f ? t : 0.0f;
+                yp[u] = t;
             }
         }
     }
 }
 
-// NHWC max-pool (padding counts as -inf, as torch.nn.MaxPool2d)
+// NHWC max-pool (padding counts as -inf, as torch.nn.MaxPool2d); one float4
+// of channels per thread when C % 4 == 0.
+template <bool VEC>
 __global__ void k_maxpool(const float *__restrict__ x, int N, int H, int W, int C, int k, int s, int p,
                           float *__restrict__ y, int Ho, int Wo) {
+    const int CV = VEC ? C / 4 : C;
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)N * Ho * Wo * C;
+    const int64_t total = (int64_t)N * Ho * Wo * CV;
     if (t >= total) return;
-    const int c = (int)(t % C);
-    int64_t r = t / C;
+    const int c = (int)(t % CV);
+    int64_t r = t / CV;
     const int ox = (int)(r % Wo);
     r /= Wo;
     const int oy = (int)(r % Ho);
     const int n = (int)(r / Ho);
-    float m = -__builtin_inff();
+    const float ninf = -__builtin_inff();
+    float m[4] = {ninf, ninf, ninf, ninf};
     for (int ky = 0; ky < k; ++ky) {
         const int iy = oy * s - p + ky;
         if (iy < 0 || iy >= H) continue;
         for (int kx = 0; kx < k; ++kx) {
             const int ix = ox * s - p + kx;
             if (ix < 0 || ix >= W) continue;
-            const float v = x[(((int64_t)n * H + iy) * W + ix) * C + c];
-            m = (v > m || v != v) ? v : m;
+            const int64_t base = (((int64_t)n * H + iy) * W + ix) * C;
+            if (VEC) {
+                const float4 v = *(const float4 *)(x + base + 4 * c);
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) m[u] = (vv[u] > m[u] || vv[u] != vv[u]) ? vv[u] : m[u];
+            } else {
+                const float v = x[base + c];
+                m[0] = (v > m[0] || v != v) ? v : m[0];
+            }
         }
     }
-    y[t] = m;
+    if (VEC) *(float4 *)(y + t * 4) = make_float4(m[0], m[1], m[2], m[3]);
+    else y[t] = m[0];
 }
 
 // 32x32 tiled transposes between [N][C][HW] and [N][HW][C]
@@ -364,14 +389,16 @@ __global__ void k_transpose(const float *__restrict__ x, int R, int S, float *__
 inline int last() { return (int)hipGetLastError(); }
 
 template <int WM, int WN, int TM, int TN>
-int launch_conv(const ConvArgs &a, bool fast, hipStream_t st) {
+int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t m_tiles = (a.M + BM - 1) / BM;
     const int n_tiles = (a.Co + BN - 1) / BN;
     const int64_t blocks = m_tiles * n_tiles;
     if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
-    if (fast) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, true>), dim3((unsigned)blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, false>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    const dim3 g((unsigned)blocks), b(256);
+    if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1>), g, b, 0, st, a);
+    else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0>), g, b, 0, st, a);
     return last();
 }
 
@@ -424,20 +451,25 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     a.K = Ci * KH * KW;
     a.Kp = (int)kpad(a.K);
     a.in_nchw = in_nchw;
-    const bool fast = !in_nchw && (Ci % BK == 0);
+    const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : 0;
     hipStream_t st = (hipStream_t)stream;
-    if (Co <= 64) return launch_conv<4, 1, 1, 2>(a, fast, st);  // 128 x 64 tiles
-    return launch_conv<2, 2, 2, 2>(a, fast, st);                 // 128 x 128 tiles
+    if (Co <= 64) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
+    return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
 }
 
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
                            int Wo, void *stream) {
     if (!x || !y || N < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || stride <= 0 || pad < 0) return BEV_ERR_ARGS;
     if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1) return BEV_ERR_ARGS;
-    const int64_t total = (int64_t)N * Ho * Wo * C;
+    const bool vec = (C % 4 == 0) && (((uintptr_t)x & 15) == 0) && (((uintptr_t)y & 15) == 0);
+    const int64_t total = (int64_t)N * Ho * Wo * (vec ? C / 4 : C);
     if (total == 0) return 0;
-    hipLaunchKernelGGL(k_maxpool, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, N, H, W,
-                       C, k, stride, pad, y, Ho, Wo);
+    if (vec)
+        hipLaunchKernelGGL(k_maxpool<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           x, N, H, W, C, k, stride, pad, y, Ho, Wo);
+    else
+        hipLaunchKernelGGL(k_maxpool<false>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           x, N, H, W, C, k, stride, pad, y, Ho, Wo);
     return last();
 }
 
