@@ -1,0 +1,92 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the sharding logic.
+
+Frame sharding has no collective; camera sharding's single exchange is a
+reduce-scatter over BEV rows.  Partial per-rank BEV sums come from the CPU
+oracle here (test infrastructure); on the GPU they come from the fused HIP
+kernel in SUM mode (bev_dist.camera_sharded_forward).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, PKG
+
+ORACLE_DIR = os.path.join(os.path.dirname(GOLDEN), "..", "oracle")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, result_q):
+    import sys
+    for p in (PKG, os.path.abspath(ORACLE_DIR)):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bev_dist
+        from oracle import Oracle
+        o = Oracle()
+        d = np.load(os.path.join(GOLDEN, "warp_w3_v3.npz"))
+        B, V, C, Hf, Wf = (int(d[k]) for k in ("B", "V", "C", "Hf", "Wf"))
+        feats = np.random.default_rng(int(d["seed"])).standard_normal(size=(B, V, C, Hf, Wf), dtype=np.float32)
+        img = (int(d["img_h"]), int(d["img_w"]))
+        bounds = tuple(float(x) for x in d["bounds"])
+        per_view = o.geometry_forward(feats, d["K"], d["Rt"], img, int(d["bev_h"]), int(d["bev_w"]), bounds)
+        v0, v1 = bev_dist.camera_shard(V, rank, world)
+        out = {}
+        for mode in ("mean", "sum", "max"):
+            part = per_view[:, v0:v1]
+            partial = o.fuse(part, "max" if mode == "max" else "sum") if v1 > v0 else np.full(
+                (B, C) + per_view.shape[3:], -np.inf if mode == "max" else 0.0, np.float32)
+            full = bev_dist.reduce_partial_bev(torch.from_numpy(partial), V, mode, gather=True)
+            sl = bev_dist.reduce_partial_bev(torch.from_numpy(partial), V, mode, gather=False)
+            out[mode] = (full.numpy(), sl.numpy(), o.fuse(per_view, mode))
+        result_q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_shard_partitions():
+    import bev_dist
+    for n in (0, 1, 7, 8, 13, 64):
+        for world in (1, 2, 3, 8):
+            got = []
+            for r in range(world):
+                got.extend(bev_dist.frame_shard(n, r, world))
+            assert got == list(range(n))
+    assert bev_dist.camera_shard(16, 3, 8) == (6, 8)
+
+
+@pytest.mark.timeout(300)
+def test_camera_sharded_reduce_scatter_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        for mode, (full, sl, ref) in res[rank].items():
+            scale = max(np.abs(ref).max(), 1e-30)
+            if mode == "max":
+                assert np.array_equal(full, ref), mode  # max is order-independent
+            else:
+                assert np.abs(full - ref).max() <= 1e-5 * scale, mode
+            rows = ref.shape[2] // 2
+            np.testing.assert_array_equal(sl, full[:, :, rank * rows:(rank + 1) * rows])

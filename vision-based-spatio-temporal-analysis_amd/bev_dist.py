@@ -1,0 +1,78 @@
+"""Multi-GPU sharding of the multi-view -> BEV hot path.
+
+The reference is single-process (no torch.distributed anywhere).  Two ways to
+spread the path over the GPUs of a node, one process per GPU:
+
+* frame sharding (BASELINE configs 2/4, the benchmark): frames are
+  independent, each rank runs Backbone -> warp -> fusion on its own frames.
+  No data-path collective at all; `frame_shard` just splits the frame range.
+
+* camera sharding (BASELINE config 5, 16 cams at 4K, 2 cameras per GPU): each
+  rank warps ITS cameras with the fused kernel in SUM mode (a partial BEV sum
+  [B, C, Hb, Wb]), then ONE reduce-scatter over BEV rows gives every rank the
+  full sum for its slice of rows; mean divides by the global camera count.
+  This is the path's only exchange step (RCCL over xGMI; gloo in CPU tests).
+  The view-summation order differs from the reference's sequential v = 0..V-1
+  (partial sums are added across ranks), so this mode is tolerance-equal
+  (max|d| <= 1e-5 * max|x|), not bit-equal.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["frame_shard", "camera_shard", "reduce_partial_bev", "camera_sharded_forward"]
+
+
+def frame_shard(num_frames: int, rank: int, world: int) -> range:
+    """Contiguous block of frame indices owned by `rank` (sizes differ by at most one)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    q, r = divmod(num_frames, world)
+    start = rank * q + min(rank, r)
+    return range(start, start + q + (1 if rank < r else 0))
+
+
+def camera_shard(num_views: int, rank: int, world: int) -> Tuple[int, int]:
+    """[v0, v1) cameras owned by `rank`."""
+    rg = frame_shard(num_views, rank, world)
+    return rg.start, rg.stop
+
+
+def reduce_partial_bev(partial: torch.Tensor, num_views: int, mode: str = "mean",
+                       group: Optional[dist.ProcessGroup] = None, gather: bool = False) -> torch.Tensor:
+    """Combine per-rank partial BEV maps [B, C, Hb, Wb] into the fused result.
+
+    `partial` is this rank's SUM over its cameras (mode sum/mean) or MAX over
+    them (mode max).  Returns this rank's row slice [B, C, Hb/world, Wb] of the
+    fused map, or the whole map when `gather` (one extra all-gather).
+    Hb must be divisible by the group size.
+    """
+    world = dist.get_world_size(group)
+    B, C, Hb, Wb = partial.shape
+    if Hb % world:
+        raise ValueError(f"BEV rows {Hb} not divisible by world size {world}")
+    rpr = Hb // world
+    # rows-major chunks so that rank r's slice is the r-th contiguous chunk
+    x = partial.reshape(B, C, world, rpr, Wb).permute(2, 0, 1, 3, 4).contiguous()
+    out = torch.empty(B, C, rpr, Wb, dtype=partial.dtype, device=partial.device)
+    op = dist.ReduceOp.MAX if mode == "max" else dist.ReduceOp.SUM
+    dist.reduce_scatter_tensor(out, x.view(world * B, C, rpr, Wb), op=op, group=group)
+    if mode == "mean":
+        out = out / float(num_views)
+    if not gather:
+        return out
+    full = torch.empty(world, B, C, rpr, Wb, dtype=out.dtype, device=out.device)
+    dist.all_gather_into_tensor(full.view(world * B, C, rpr, Wb), out.contiguous(), group=group)
+    return full.permute(1, 2, 0, 3, 4).reshape(B, C, Hb, Wb)
+
+
+def camera_sharded_forward(geom, feats_local: torch.Tensor, K_local, Rt_local, img_size, num_views: int,
+                           mode: str = "mean", group: Optional[dist.ProcessGroup] = None,
+                           gather: bool = False) -> torch.Tensor:
+    """K5 path: this rank's cameras -> fused partial (HIP kernel) -> reduce-scatter over BEV rows."""
+    part_mode = "max" if mode == "max" else "sum"
+    partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
+    return reduce_partial_bev(partial, num_views, mode, group, gather)
