@@ -36,6 +36,12 @@ extern "C" {
 /* ABI version (bumped on any signature change). */
 int bev_abi_version(void);
 
+/* host: performance knobs (no effect on results).  knob BEV_TUNE_CONV_TILE:
+ * 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128 output tiles for
+ * bev_conv2d_f32.  Returns the previous value, or BEV_ERR_ARGS. */
+#define BEV_TUNE_CONV_TILE 1
+int bev_tune(int knob, int value);
+
 /* ---------------------------------------------------------------------------
  * Geometry helpers
  * ------------------------------------------------------------------------- */

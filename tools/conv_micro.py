@@ -1,0 +1,79 @@
+"""Micro-benchmark of single backbone conv layers (ResNet-50 at 7 x 1080x1920) on the HIP kernel.
+
+    python tools/conv_micro.py l1.0.c3 l2.1.c2 stem --iters 20
+
+Prints one line per layer: time per call (HIP events) and TFLOP/s.  Used with
+rocprofv3 --pmc to attribute counters to one layer shape at a time.
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "vision-based-spatio-temporal-analysis_amd"))
+
+import torch  # noqa: E402
+
+import bev_native as nat  # noqa: E402
+
+N = 7
+# name: (Ci, Co, k, stride, H_in, W_in, residual, nchw_in)
+LAYERS = {
+    "stem": (3, 64, 7, 2, 1080, 1920, False, True),
+    "l1.0.ds": (64, 256, 1, 1, 270, 480, False, False),
+    "l1.0.c1": (64, 64, 1, 1, 270, 480, False, False),
+    "l1.1.c1": (256, 64, 1, 1, 270, 480, False, False),
+    "l1.0.c2": (64, 64, 3, 1, 270, 480, False, False),
+    "l1.0.c3": (64, 256, 1, 1, 270, 480, True, False),
+    "l2.0.ds": (256, 512, 1, 2, 270, 480, False, False),
+    "l2.0.c1": (256, 128, 1, 1, 270, 480, False, False),
+    "l2.0.c2": (128, 128, 3, 2, 270, 480, False, False),
+    "l2.1.c1": (512, 128, 1, 1, 135, 240, False, False),
+    "l2.1.c2": (128, 128, 3, 1, 135, 240, False, False),
+    "l2.1.c3": (128, 512, 1, 1, 135, 240, True, False),
+    "proj": (512, 64, 1, 1, 135, 240, False, False),
+}
+
+
+def run(name, iters):
+    Ci, Co, k, s, H, W, res, nchw = LAYERS[name]
+    p = k // 2
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn((N, Ci, H, W) if nchw else (N, H, W, Ci), device=dev, generator=g)
+    w = torch.randn(Co, Ci, k, k, device=dev, generator=g) * (2.0 / (Ci * k * k)) ** 0.5
+    b = torch.randn(Co, device=dev, generator=g)
+    r = torch.randn(N, Ho, Wo, Co, device=dev, generator=g) if res else None
+    packed = nat.pack_conv_weight(w)
+    out = torch.empty(N, Ho, Wo, Co, device=dev)
+    for _ in range(3):
+        nat.conv2d_nhwc(x, packed, b, Co, k, k, s, p, True, residual=r, in_nchw=nchw, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        nat.conv2d_nhwc(x, packed, b, Co, k, k, s, p, True, residual=r, in_nchw=nchw, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2 * N * Ho * Wo * Co * Ci * k * k
+    byts = 4 * (x.numel() + out.numel() + (r.numel() if res else 0))
+    print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("layers", nargs="*", default=list(LAYERS))
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tiles", type=int, nargs="*", default=[0], help="BEV_TUNE_CONV_TILE values to A/B")
+    a = ap.parse_args()
+    for rnd in range(2):  # interleaved rounds, same process
+        for t in a.tiles:
+            nat.tune(nat.TUNE_CONV_TILE, t)
+            print(f"-- round {rnd} tile {t}")
+            for name in a.layers:
+                run(name, a.iters)
+
+
+if __name__ == "__main__":
+    main()

@@ -31,6 +31,7 @@ _d = ctypes.c_double
 # name -> (restype, argtypes); must match include/bev_mi355x.h
 SIGNATURES = {
     "bev_abi_version": (_i, []),
+    "bev_tune": (_i, [_i, _i]),
     "bev_linspace_f32": (_i, [_d, _d, _i, _vp]),
     "bev_homography_f32": (_i, [_vp, _vp, _i, _vp, _vp]),
     "bev_ipm_warp_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
@@ -72,6 +73,17 @@ def lib():
             raise ImportError(f"libbev_mi355x.so ABI {v} != expected {ABI_VERSION}; rebuild")
         _lib = L
     return _lib
+
+
+TUNE_CONV_TILE = 1
+
+
+def tune(knob: int, value: int) -> int:
+    """Set a performance knob (include/bev_mi355x.h BEV_TUNE_*); returns the previous value."""
+    rc = lib().bev_tune(knob, value)
+    if rc < 0:
+        raise ValueError(f"bad tuning knob/value {knob}/{value}")
+    return rc
 
 
 class HipError(RuntimeError):

@@ -34,6 +34,7 @@ constexpr int BK = 32;        // K step
 constexpr int LROW = BK + 4;  // LDS row stride in floats (144 B: 9 slots, odd -> conflict-free b128 rows)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector: promotes to VGPRs reliably
 
 __host__ __device__ inline int64_t kpad(int K) { return (K + BK - 1) / BK * BK; }
 __host__ __device__ inline int64_t copad(int Co) { return (Co + 127) / 128 * 128; }
@@ -105,13 +106,13 @@ struct LoaderFast {
         quad = tid & 7;
         ky = kx = ci0 = 0;
     }
-    __device__ void load(const ConvArgs &a, float4 (&v)[ROWS]) const {
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[ROWS]) const {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
             const bool in = rows.ok[r] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            v[r] = in ? *(const float4 *)(a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[r] = in ? *(const f32x4 *)(a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4)
+                      : (f32x4){0.f, 0.f, 0.f, 0.f};
         }
     }
     __device__ void advance(const ConvArgs &a) {
@@ -139,7 +140,7 @@ struct LoaderGen {
         k0 = 0;
         nchw = a.in_nchw != 0;
     }
-    __device__ void load(const ConvArgs &a, float4 (&v)[ROWS]) const {
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[ROWS]) const {
         float e[4][ROWS];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -156,10 +157,22 @@ struct LoaderGen {
             }
         }
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) v[r] = make_float4(e[0][r], e[1][r], e[2][r], e[3][r]);
+        for (int r = 0; r < ROWS; ++r) v[r] = (f32x4){e[0][r], e[1][r], e[2][r], e[3][r]};
     }
     __device__ void advance(const ConvArgs &) { k0 += BK; }
 };
+
+template <int R>
+__device__ __forceinline__ void load_rows(f32x4 (&v)[R], const float *__restrict__ p, int64_t ld, int k) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = *(const f32x4 *)(p + (int64_t)(32 * r) * ld + k);
+}
+
+template <int R>
+__device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) *(f32x4 *)(p + 32 * r * LROW) = v[r];
+}
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
 // LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7)
@@ -191,69 +204,70 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
-    float4 ra[AROWS], rb[BROWS];
+    // global -> register prefetch of one K step (helpers, not lambdas: register
+    // arrays captured by reference were address-taken and landed in scratch)
+    f32x4 ra[AROWS], rb[BROWS];
     int kb = 0;  // k offset of the B panel
-    auto gload = [&]() {
-        la.load(a, ra);
-#pragma unroll
-        for (int r = 0; r < BROWS; ++r) rb[r] = *(const float4 *)(wrow + (int64_t)(32 * r) * a.Kp + kb);
-        la.advance(a);
-        kb += BK;
-    };
-    auto swrite = [&](int buf) {
-        float *As = lds + buf * STAGE;
-        float *Bs = As + BM * LROW;
-#pragma unroll
-        for (int r = 0; r < AROWS; ++r) *(float4 *)(As + ((tid >> 3) + 32 * r) * LROW + bq * 4) = ra[r];
-#pragma unroll
-        for (int r = 0; r < BROWS; ++r) *(float4 *)(Bs + ((tid >> 3) + 32 * r) * LROW + bq * 4) = rb[r];
-    };
+#define BEV_GLOAD()                          \
+    do {                                     \
+        la.load(a, ra);                      \
+        load_rows<BROWS>(rb, wrow, a.Kp, kb); \
+        la.advance(a);                       \
+        kb += BK;                            \
+    } while (0)
+#define BEV_SWRITE(buf)                                                                   \
+    do {                                                                                  \
+        store_rows<AROWS>(lds + (buf) * STAGE + (tid >> 3) * LROW + bq * 4, ra);          \
+        store_rows<BROWS>(lds + (buf) * STAGE + (BM + (tid >> 3)) * LROW + bq * 4, rb);   \
+    } while (0)
 
     const int nk = a.Kp / BK;
-    gload();
-    swrite(0);
+    BEV_GLOAD();
+    BEV_SWRITE(0);
     __syncthreads();
     const int r32 = lane & 31, h = lane >> 5;
     for (int ks = 0; ks < nk; ++ks) {
         const int cur = ks & 1;
-        if (ks + 1 < nk) gload();
+        if (ks + 1 < nk) BEV_GLOAD();
         const float *As = lds + cur * STAGE;
         const float *Bs = As + BM * LROW;
         // MFMA k-slot h of step p reads k = 16 h + p (p = 0..15): per half of the
         // step each lane reads two contiguous float4 of its row per operand tile.
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-            float4 fa[TM][2], fb[TN][2];
+            f32x4 fa[TM][2], fb[TN][2];
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const float *pa = As + (wm * TM * 32 + i * 32 + r32) * LROW + h * 16 + half * 8;
-                fa[i][0] = *(const float4 *)pa;
-                fa[i][1] = *(const float4 *)(pa + 4);
+                fa[i][0] = *(const f32x4 *)pa;
+                fa[i][1] = *(const f32x4 *)(pa + 4);
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const float *pb = Bs + (wn * TN * 32 + j * 32 + r32) * LROW + h * 16 + half * 8;
-                fb[j][0] = *(const float4 *)pb;
-                fb[j][1] = *(const float4 *)(pb + 4);
+                fb[j][0] = *(const f32x4 *)pb;
+                fb[j][1] = *(const f32x4 *)(pb + 4);
             }
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
-                    const float av = ((const float *)&fa[i][p >> 2])[p & 3];
+                    const float av = fa[i][p >> 2][p & 3];
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        const float bv = ((const float *)&fb[j][p >> 2])[p & 3];
+                        const float bv = fb[j][p >> 2][p & 3];
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
                     }
                 }
             }
         }
         if (ks + 1 < nk) {
-            swrite(cur ^ 1);
+            BEV_SWRITE(cur ^ 1);
             __syncthreads();
         }
     }
+#undef BEV_GLOAD
+#undef BEV_SWRITE
 
     // ---- epilogue through LDS ---------------------------------------------------
     // The wave's (TM*32) x (TN*32) accumulator tile goes to LDS, then every lane
@@ -402,9 +416,21 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     return last();
 }
 
+int g_conv_tile = 0;
+
 }  // namespace
 
 extern "C" {
+
+int bev_tune(int knob, int value) {
+    if (knob == BEV_TUNE_CONV_TILE) {
+        if (value < 0 || value > 3) return BEV_ERR_ARGS;
+        const int old = g_conv_tile;
+        g_conv_tile = value;
+        return old;
+    }
+    return BEV_ERR_ARGS;
+}
 
 int64_t bev_conv_packed_size(int Co, int Ci, int KH, int KW) {
     if (Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return 0;
@@ -453,7 +479,10 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     a.in_nchw = in_nchw;
     const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : 0;
     hipStream_t st = (hipStream_t)stream;
-    if (Co <= 64) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
+    int tile = g_conv_tile;
+    if (tile == 0) tile = (Co <= 64) ? 2 : 1;
+    if (tile == 2) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
+    if (tile == 3) return launch_conv<2, 2, 1, 2>(a, loader, st);  // 64 x 128 tiles
     return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
 }
 
