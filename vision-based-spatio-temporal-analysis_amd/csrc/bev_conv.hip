@@ -101,12 +101,18 @@ template <int ROWS>
 struct LoaderFast {
     RowsA<ROWS> rows;
     int quad, ky, kx, ci0;
+    f32x4 v[ROWS];
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
         rows.init(a, m0, tid);
         quad = tid & 7;
         ky = kx = ci0 = 0;
     }
-    __device__ void load(const ConvArgs &a, f32x4 (&v)[ROWS]) const {
+    // A tile image: row (tid >> 3) + 32 r, k columns quad*4 .. +3
+    __device__ void store(float *As, int tid) const {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) *(f32x4 *)(As + ((tid >> 3) + 32 * r) * LROW + quad * 4) = v[r];
+    }
+    __device__ void load(const ConvArgs &a) {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
@@ -127,37 +133,53 @@ struct LoaderFast {
     }
 };
 
-// A loader, generic path: any Ci, NHWC or NCHW input, element-wise.  CI / KW
-// > 0 bake the layer geometry in (constant divisors; the ResNet stem uses 3 / 7).
-template <int ROWS, int CI = 0, int KWc = 0>
-struct LoaderGen {
-    RowsA<ROWS> rows;
-    int quad, k0;
-    bool nchw;
+// A loader, generic path (any Ci, NHWC or NCHW input), element-wise.  Each
+// thread owns ONE output pixel (row) of the tile and a contiguous run of KPT
+// k's, so for a given k the 64 lanes of a wave read 64 neighbouring output
+// pixels (coalesced) and the k -> (ky, kx, ci) decode is wave-uniform.
+// CI / KWc > 0 bake the geometry in (the ResNet stem: Ci = 3, 7 x 7, NCHW).
+template <int BM, int CI = 0, int KWc = 0>
+struct LoaderRow {
+    static constexpr int TPR = 256 / BM;  // threads per row
+    static constexpr int KPT = BK / TPR;  // k's per thread and K step
+    int64_t pix;
+    int iy0, ix0, row, kq, k0;
+    bool ok, nchw;
+    f32x4 v[KPT / 4];
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
-        rows.init(a, m0, tid);
-        quad = tid & 7;
+        row = tid % BM;
+        kq = tid / BM;
+        const int64_t m = m0 + row;
+        ok = m < a.M;
+        const int64_t mm = ok ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int n = (int)(t / a.Ho);
+        pix = (int64_t)n * a.H * a.W * a.Ci;
+        iy0 = oy * a.stride - a.pad;
+        ix0 = ox * a.stride - a.pad;
         k0 = 0;
         nchw = a.in_nchw != 0;
     }
-    __device__ void load(const ConvArgs &a, f32x4 (&v)[ROWS]) const {
-        float e[4][ROWS];
+    __device__ void store(float *As, int) const {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int k = k0 + quad * 4 + q;
-            const int Ci = CI > 0 ? CI : a.Ci, KW = KWc > 0 ? KWc : a.KW;
+        for (int i = 0; i < KPT / 4; ++i) *(f32x4 *)(As + row * LROW + kq * KPT + 4 * i) = v[i];
+    }
+    __device__ void load(const ConvArgs &a) {
+        const int Ci = CI > 0 ? CI : a.Ci, KW = KWc > 0 ? KWc : a.KW;
+        float e[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const int k = k0 + kq * KPT + j;  // uniform across the wave
             const int ci = k % Ci, rr = k / Ci, kx = rr % KW, ky = rr / KW;
-#pragma unroll
-            for (int r = 0; r < ROWS; ++r) {
-                const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
-                const bool in = rows.ok[r] && (k < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-                const int64_t off = nchw ? rows.pix[r] + ((int64_t)ci * a.H + iy) * a.W + ix
-                                         : rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci;
-                e[q][r] = in ? a.x[off] : 0.0f;
-            }
+            const int iy = iy0 + ky, ix = ix0 + kx;
+            const bool in = ok && (k < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const int64_t off = nchw ? pix + ((int64_t)ci * a.H + iy) * a.W + ix : pix + ((int64_t)iy * a.W + ix) * Ci + ci;
+            e[j] = in ? a.x[off] : 0.0f;
         }
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) v[r] = (f32x4){e[0][r], e[1][r], e[2][r], e[3][r]};
+        for (int i = 0; i < KPT / 4; ++i) v[i] = (f32x4){e[4 * i], e[4 * i + 1], e[4 * i + 2], e[4 * i + 3]};
     }
     __device__ void advance(const ConvArgs &) { k0 += BK; }
 };
@@ -192,8 +214,8 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int n0 = (blockIdx.x % n_tiles) * BN;
 
     typename std::conditional<LOADER == 1, LoaderFast<AROWS>,
-                              typename std::conditional<LOADER == 2, LoaderGen<AROWS, 3, 7>,
-                                                        LoaderGen<AROWS>>::type>::type la;
+                              typename std::conditional<LOADER == 2, LoaderRow<BM, 3, 7>,
+                                                        LoaderRow<BM>>::type>::type la;
     la.init(a, m0, tid);
     const int bq = tid & 7;
     const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
@@ -206,18 +228,18 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
 
     // global -> register prefetch of one K step (helpers, not lambdas: register
     // arrays captured by reference were address-taken and landed in scratch)
-    f32x4 ra[AROWS], rb[BROWS];
+    f32x4 rb[BROWS];
     int kb = 0;  // k offset of the B panel
 #define BEV_GLOAD()                          \
     do {                                     \
-        la.load(a, ra);                      \
+        la.load(a);                          \
         load_rows<BROWS>(rb, wrow, a.Kp, kb); \
         la.advance(a);                       \
         kb += BK;                            \
     } while (0)
 #define BEV_SWRITE(buf)                                                                   \
     do {                                                                                  \
-        store_rows<AROWS>(lds + (buf) * STAGE + (tid >> 3) * LROW + bq * 4, ra);          \
+        la.store(lds + (buf) * STAGE, tid);                                               \
         store_rows<BROWS>(lds + (buf) * STAGE + (BM + (tid >> 3)) * LROW + bq * 4, rb);   \
     } while (0)
 
@@ -480,7 +502,21 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : 0;
     hipStream_t st = (hipStream_t)stream;
     int tile = g_conv_tile;
-    if (tile == 0) tile = (Co <= 64) ? 2 : 1;
+    if (tile == 0) {
+        // Cost model (measured on MI355X, tools/conv_micro.py A/B): time ~ rounds of
+        // resident blocks (256 CUs x 2 blocks) x tile area; ties go to the larger
+        // tile (better operand reuse).  Candidates: 1 = 128x128, 3 = 64x128, 2 = 128x64.
+        const int64_t M = a.M;
+        auto cost = [&](int bm, int bn) {
+            const int64_t blocks = ((M + bm - 1) / bm) * ((Co + bn - 1) / bn);
+            return (double)((blocks + 511) / 512) * bm * bn;
+        };
+        const double c1 = cost(128, 128), c3 = cost(64, 128), c2 = cost(128, 64);
+        tile = 1;
+        double best = c1;
+        if (c3 < 0.95 * best) { tile = 3; best = c3; }
+        if (c2 < 0.95 * best) { tile = 2; best = c2; }
+    }
     if (tile == 2) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
     if (tile == 3) return launch_conv<2, 2, 1, 2>(a, loader, st);  // 64 x 128 tiles
     return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
