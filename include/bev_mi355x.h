@@ -114,7 +114,8 @@ int bev_view_fuse_f32(const float *x, int B, int V, int64_t M, int mode, float *
  * Backbone (CNNEncoder, cnn_encoder.py:39-70): convolutions on MFMA.
  *
  * Activations are channels-last (NHWC) fp32.  Weights are packed by
- * bev_conv_pack_weights_f32 into [KH*KW*Ci (padded)][Co (padded)] panels.
+ * bev_conv_pack_weights_f32 into a [Co padded to 128][K padded to 32] panel,
+ * K index k = (ky*KW + kx)*Ci + ci (the implicit-GEMM reduction order).
  * y = act( conv(x, w) + bias (+ residual) ),  act = ReLU if relu != 0.
  * Batch-norm (eval) is folded into (w, bias) by the host.
  * x may instead be NCHW (in_nchw = 1): the stem reads the caller's images
