@@ -134,6 +134,19 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
                    const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
                    int Wo, void *stream);
 
+/* device: bottleneck tail as ONE GEMM (NHWC, both 1x1):
+ *   y = act( x (*) W1  +  x2[:, ::s2, ::s2, :] (*) W2  + bias )
+ * x [N][Ho][Wo][Ci] is conv3's input, x2 [N][H2][W2][Ci2] the block input the
+ * downsample shortcut reads with stride s2 (Ho = (H2-1)/s2 + 1, same for W).
+ * packed = bev_conv_pack_weights_f32 of the concatenated [Co][Ci + Ci2][1][1]
+ * weight [W1 | W2] (BN folded), bias = b1 + b2.  Ci, Ci2 % 32 == 0.
+ * Replaces timm Bottleneck.forward's conv3 -> bn3 -> (+ downsample(shortcut):
+ * conv1x1/stride + BN) -> act3 inside the features_only trunk
+ * (cnn_encoder.py:26, 41-42): the shortcut tensor is never materialised. */
+int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const float *x2, int H2, int W2, int Ci2,
+                        int stride2, const float *packed, const float *bias, int Co, int relu, float *y,
+                        void *stream);
+
 /* device: NHWC max-pool (timm ResNet stem: 3x3, stride 2, pad 1). */
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
                            int Wo, void *stream);

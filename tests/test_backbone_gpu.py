@@ -58,6 +58,32 @@ def test_conv_vs_torch_fp32(case):
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
+DUAL_CASES = [
+    # N, Ci (conv3 input), Ci2 (block input), H2, W2, s2, Co
+    (2, 64, 64, 17, 23, 1, 256),     # layer1 block 0: conv3 64->256 + downsample 64->256
+    (1, 128, 256, 15, 21, 2, 512),   # layer2 block 0: conv3 128->512 + downsample 256->512, stride 2
+    (1, 32, 96, 9, 10, 3, 200),      # ragged Co, stride 3, odd sizes
+]
+
+
+@pytest.mark.parametrize("case", DUAL_CASES, ids=[f"ci{c[1]}+{c[2]}_s{c[5]}_co{c[6]}" for c in DUAL_CASES])
+def test_conv_dual_vs_torch_fp32(case):
+    """bev_conv2d_dual_f32 == relu(conv1x1(h, W1) + conv1x1(x, W2, stride) + b) (timm Bottleneck tail)."""
+    import bev_native as nat
+    N, Ci, Ci2, H2, W2, s2, Co = case
+    Ho, Wo = (H2 - 1) // s2 + 1, (W2 - 1) // s2 + 1
+    h = _rand((N, Ci, Ho, Wo), 11)
+    x = _rand((N, Ci2, H2, W2), 12)
+    w1 = _rand((Co, Ci, 1, 1), 13, scale=(2.0 / Ci) ** 0.5)
+    w2 = _rand((Co, Ci2, 1, 1), 14, scale=(2.0 / Ci2) ** 0.5)
+    b = _rand((Co,), 15)
+    ref = F.relu(F.conv2d(h, w1) + F.conv2d(x, w2, stride=s2) + b.view(1, -1, 1, 1))
+    packed = nat.pack_conv_weight(torch.cat([w1, w2], 1).to(DEV))
+    y = nat.conv2d_dual_nhwc(h.permute(0, 2, 3, 1).contiguous().to(DEV), x.permute(0, 2, 3, 1).contiguous().to(DEV),
+                             s2, packed, b.to(DEV), Co, relu=True)
+    np.testing.assert_allclose(y.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
 def test_maxpool_and_layouts_exact():
     import bev_native as nat
     x = _rand((2, 64, 31, 45), 5)

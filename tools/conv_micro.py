@@ -33,6 +33,36 @@ LAYERS = {
     "l2.1.c3": (128, 512, 1, 1, 135, 240, True, False),
     "proj": (512, 64, 1, 1, 135, 240, False, False),
 }
+# fused bottleneck tails (bev_conv2d_dual_f32): name: (Ci conv3 in, Ci2 block in, Co, s2, H2, W2)
+DUAL = {
+    "l1.0.tail": (64, 64, 256, 1, 270, 480),
+    "l2.0.tail": (128, 256, 512, 2, 270, 480),
+}
+
+
+def run_dual(name, iters):
+    Ci, Ci2, Co, s2, H2, W2 = DUAL[name]
+    Ho, Wo = (H2 - 1) // s2 + 1, (W2 - 1) // s2 + 1
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    h = torch.randn(N, Ho, Wo, Ci, device=dev, generator=g)
+    x = torch.randn(N, H2, W2, Ci2, device=dev, generator=g)
+    w = torch.randn(Co, Ci + Ci2, 1, 1, device=dev, generator=g) * (2.0 / (Ci + Ci2)) ** 0.5
+    b = torch.randn(Co, device=dev, generator=g)
+    packed = nat.pack_conv_weight(w)
+    out = torch.empty(N, Ho, Wo, Co, device=dev)
+    for _ in range(3):
+        nat.conv2d_dual_nhwc(h, x, s2, packed, b, Co, True, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        nat.conv2d_dual_nhwc(h, x, s2, packed, b, Co, True, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2 * N * Ho * Wo * Co * (Ci + Ci2)
+    byts = 4 * (h.numel() + N * Ho * Wo * Ci2 + out.numel())
+    print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
 
 
 def run(name, iters):
@@ -63,7 +93,7 @@ def run(name, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("layers", nargs="*", default=list(LAYERS))
+    ap.add_argument("layers", nargs="*", default=list(LAYERS) + list(DUAL))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tiles", type=int, nargs="*", default=[0], help="BEV_TUNE_CONV_TILE values to A/B")
     a = ap.parse_args()
@@ -72,7 +102,7 @@ def main():
             nat.tune(nat.TUNE_CONV_TILE, t)
             print(f"-- round {rnd} tile {t}")
             for name in a.layers:
-                run(name, a.iters)
+                (run_dual if name in DUAL else run)(name, a.iters)
 
 
 if __name__ == "__main__":

@@ -8,6 +8,7 @@ kernels bind to -- one runtime, one set of streams.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import subprocess
@@ -44,10 +45,45 @@ SIGNATURES = {
     "bev_conv_packed_size": (_i64, [_i, _i, _i, _i]),
     "bev_conv_pack_weights_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
 }
+
+
+# ---------------------------------------------------------------------------
+# launch timing: HIP events recorded on the launch stream around each kernel
+# launch of a class ("conv", "warp_fuse"), so a benchmark can price exactly
+# those kernels (bench.py roofline) without a profiler.  Off by default.
+# ---------------------------------------------------------------------------
+_SPANS = None  # dict name -> list of (start, end) events while recording
+
+
+def spans_start():
+    global _SPANS
+    _SPANS = {}
+
+
+def spans_stop() -> dict:
+    """Stop recording; returns name -> list of per-launch durations in ms (synchronises)."""
+    global _SPANS
+    spans, _SPANS = _SPANS or {}, None
+    torch.cuda.synchronize()
+    return {k: [a.elapsed_time(b) for a, b in v] for k, v in spans.items()}
+
+
+@contextlib.contextmanager
+def _span(name: str, t: torch.Tensor):
+    if _SPANS is None:
+        yield
+        return
+    st = torch.cuda.current_stream(t.device)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    yield
+    e1.record(st)
+    _SPANS.setdefault(name, []).append((e0, e1))
 
 
 def build(force: bool = False) -> str:
@@ -165,9 +201,10 @@ def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, o
     if out is None:
         out = torch.empty(B, C, Hb, Wb, device=feats.device, dtype=torch.float32)
     s = feats.stride()
-    _check(lib().bev_ipm_warp_fuse_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf,
-                                       Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _stream(feats)),
-           "bev_ipm_warp_fuse_f32")
+    with _span("warp_fuse", feats):
+        rc = lib().bev_ipm_warp_fuse_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C,
+                                         Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _stream(feats))
+    _check(rc, "bev_ipm_warp_fuse_f32")
     return out
 
 
@@ -247,8 +284,27 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
     if residual is not None:
         residual = residual.contiguous()
         assert residual.shape == out.shape
-    _check(lib().bev_conv2d_f32(_ptr(x), int(in_nchw), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co, KH,
-                                KW, stride, pad, int(relu), _ptr(out), Ho, Wo, _stream(x)), "bev_conv2d_f32")
+    with _span("conv", x):
+        rc = lib().bev_conv2d_f32(_ptr(x), int(in_nchw), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co,
+                                  KH, KW, stride, pad, int(relu), _ptr(out), Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_f32")
+    return out
+
+
+def conv2d_dual_nhwc(x: torch.Tensor, x2: torch.Tensor, stride2: int, packed: torch.Tensor, bias, Co: int,
+                     relu: bool, out: torch.Tensor = None):
+    """act(x (*) W1 + x2[:, ::s2, ::s2] (*) W2 + bias), both 1x1, NHWC: x [N,Ho,Wo,Ci], x2 [N,H2,W2,Ci2]."""
+    x = x.contiguous()
+    x2 = x2.contiguous()
+    _require_gpu(x, x2, packed, bias)
+    N, Ho, Wo, Ci = x.shape
+    _, H2, W2, Ci2 = x2.shape
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    with _span("conv", x):
+        rc = lib().bev_conv2d_dual_f32(_ptr(x), N, Ho, Wo, Ci, _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed),
+                                       _ptr(bias), Co, int(relu), _ptr(out), _stream(x))
+    _check(rc, "bev_conv2d_dual_f32")
     return out
 
 

@@ -69,6 +69,9 @@ struct ConvArgs {
     int64_t M;
     int K;
     int Kp;
+    // dual-source 1x1 (LOADER 3): k in [Ci, Ci + Ci2) reads x2 [N][H2][W2][Ci2] at (oy*s2, ox*s2)
+    const float *__restrict__ x2;
+    int Ci2, H2, W2, stride2;
 };
 
 // Per-thread view of the A tile rows it loads: rows (tid >> 3) + 32 r, one 16-B quad.
@@ -131,6 +134,48 @@ struct LoaderFast {
             }
         }
     }
+};
+
+// A loader, dual-source 1x1 (bottleneck conv3 + downsample shortcut in ONE GEMM):
+// K = [0, Ci) reads x [M][Ci] (the conv3 input, one pixel per output pixel),
+// K = [Ci, Ci + Ci2) reads x2 at the strided pixel (oy*s2, ox*s2) -- the
+// downsample's 1x1/stride-s2 input.  Ci, Ci2 % 32 == 0.
+template <int ROWS>
+struct LoaderDual {
+    int64_t p1[ROWS], p2[ROWS];
+    bool ok[ROWS];
+    int quad, k0;
+    f32x4 v[ROWS];
+    __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int64_t m = m0 + (tid >> 3) + 32 * r;
+            ok[r] = m < a.M;
+            const int64_t mm = ok[r] ? m : 0;
+            const int ox = (int)(mm % a.Wo);
+            const int64_t t = mm / a.Wo;
+            const int oy = (int)(t % a.Ho);
+            const int64_t n = t / a.Ho;
+            p1[r] = mm * a.Ci;
+            p2[r] = ((n * a.H2 + (int64_t)oy * a.stride2) * a.W2 + (int64_t)ox * a.stride2) * a.Ci2;
+        }
+        quad = tid & 7;
+        k0 = 0;
+    }
+    __device__ void store(float *As, int tid) const {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) *(f32x4 *)(As + ((tid >> 3) + 32 * r) * LROW + quad * 4) = v[r];
+    }
+    __device__ void load(const ConvArgs &a) {
+        const bool first = k0 < a.Ci;  // wave-uniform
+        const float *src = first ? a.x + k0 : a.x2 + (k0 - a.Ci);
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int64_t off = (first ? p1[r] : p2[r]) + quad * 4;
+            v[r] = ok[r] ? *(const f32x4 *)(src + off) : (f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    __device__ void advance(const ConvArgs &) { k0 += BK; }
 };
 
 // A loader, generic path (any Ci, NHWC or NCHW input), element-wise.  Each
@@ -197,7 +242,7 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
 }
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
-// LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7)
+// LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1
 template <int WM, int WN, int TM, int TN, int LOADER>
 __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -213,9 +258,11 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     const int64_t m0 = (int64_t)(blockIdx.x / n_tiles) * BM;
     const int n0 = (blockIdx.x % n_tiles) * BN;
 
-    typename std::conditional<LOADER == 1, LoaderFast<AROWS>,
-                              typename std::conditional<LOADER == 2, LoaderRow<BM, 3, 7>,
-                                                        LoaderRow<BM>>::type>::type la;
+    typename std::conditional<
+        LOADER == 1, LoaderFast<AROWS>,
+        typename std::conditional<LOADER == 2, LoaderRow<BM, 3, 7>,
+                                  typename std::conditional<LOADER == 3, LoaderDual<AROWS>,
+                                                            LoaderRow<BM>>::type>::type>::type la;
     la.init(a, m0, tid);
     const int bq = tid & 7;
     const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
@@ -434,11 +481,36 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     const dim3 g((unsigned)blocks), b(256);
     if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1>), g, b, 0, st, a);
     else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2>), g, b, 0, st, a);
+    else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0>), g, b, 0, st, a);
     return last();
 }
 
 int g_conv_tile = 0;
+
+// Tile choice + launch.  Cost model (measured on MI355X, tools/conv_micro.py
+// A/B): time ~ rounds of resident blocks (256 CUs x 2 blocks) x tile area; ties
+// go to the larger tile (better operand reuse).  Candidates: 1 = 128x128,
+// 3 = 64x128, 2 = 128x64.
+int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
+    int tile = g_conv_tile;
+    if (tile == 0) {
+        const int64_t M = a.M;
+        const int Co = a.Co;
+        auto cost = [&](int bm, int bn) {
+            const int64_t blocks = ((M + bm - 1) / bm) * ((Co + bn - 1) / bn);
+            return (double)((blocks + 511) / 512) * bm * bn;
+        };
+        const double c1 = cost(128, 128), c3 = cost(64, 128), c2 = cost(128, 64);
+        tile = 1;
+        double best = c1;
+        if (c3 < 0.95 * best) { tile = 3; best = c3; }
+        if (c2 < 0.95 * best) { tile = 2; best = c2; }
+    }
+    if (tile == 2) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
+    if (tile == 3) return launch_conv<2, 2, 1, 2>(a, loader, st);  // 64 x 128 tiles
+    return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
+}
 
 }  // namespace
 
@@ -500,26 +572,47 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     a.Kp = (int)kpad(a.K);
     a.in_nchw = in_nchw;
     const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : 0;
-    hipStream_t st = (hipStream_t)stream;
-    int tile = g_conv_tile;
-    if (tile == 0) {
-        // Cost model (measured on MI355X, tools/conv_micro.py A/B): time ~ rounds of
-        // resident blocks (256 CUs x 2 blocks) x tile area; ties go to the larger
-        // tile (better operand reuse).  Candidates: 1 = 128x128, 3 = 64x128, 2 = 128x64.
-        const int64_t M = a.M;
-        auto cost = [&](int bm, int bn) {
-            const int64_t blocks = ((M + bm - 1) / bm) * ((Co + bn - 1) / bn);
-            return (double)((blocks + 511) / 512) * bm * bn;
-        };
-        const double c1 = cost(128, 128), c3 = cost(64, 128), c2 = cost(128, 64);
-        tile = 1;
-        double best = c1;
-        if (c3 < 0.95 * best) { tile = 3; best = c3; }
-        if (c2 < 0.95 * best) { tile = 2; best = c2; }
-    }
-    if (tile == 2) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
-    if (tile == 3) return launch_conv<2, 2, 1, 2>(a, loader, st);  // 64 x 128 tiles
-    return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
+    a.x2 = nullptr;
+    a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    return launch_tiled(a, loader, (hipStream_t)stream);
+}
+
+int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const float *x2, int H2, int W2, int Ci2,
+                        int stride2, const float *packed, const float *bias, int Co, int relu, float *y,
+                        void *stream) {
+    if (!x || !x2 || !packed || !y || N < 0 || Ho <= 0 || Wo <= 0 || Ci <= 0 || Ci2 <= 0 || H2 <= 0 || W2 <= 0 ||
+        stride2 <= 0 || Co <= 0)
+        return BEV_ERR_ARGS;
+    if (Ci % BK != 0 || Ci2 % BK != 0) return BEV_ERR_ARGS;
+    if (Ho != (H2 - 1) / stride2 + 1 || Wo != (W2 - 1) / stride2 + 1) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvArgs a;
+    a.x = x;
+    a.wp = packed;
+    a.bias = bias;
+    a.res = nullptr;
+    a.y = y;
+    a.N = N;
+    a.H = Ho;
+    a.W = Wo;
+    a.Ci = Ci;
+    a.Co = Co;
+    a.KH = a.KW = 1;
+    a.stride = 1;
+    a.pad = 0;
+    a.Ho = Ho;
+    a.Wo = Wo;
+    a.relu = relu;
+    a.M = (int64_t)N * Ho * Wo;
+    a.K = Ci + Ci2;
+    a.Kp = (int)kpad(a.K);
+    a.in_nchw = 0;
+    a.x2 = x2;
+    a.Ci2 = Ci2;
+    a.H2 = H2;
+    a.W2 = W2;
+    a.stride2 = stride2;
+    return launch_tiled(a, 3, (hipStream_t)stream);
 }
 
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,

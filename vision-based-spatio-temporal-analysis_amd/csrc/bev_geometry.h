@@ -5,8 +5,10 @@
 //   geometry.py:144-149  uvw = H @ [x y 1]^T (MKL AVX-512 3-term dot), w_safe, u, v
 //   geometry.py:151-158  feature-space rescale and [-1,1] normalisation
 //   geometry.py:161      grid_sampler_2d unnormalise + floor + bilinear weights
-// Everything is plain IEEE fp32; FMAs are explicit (__builtin_fmaf) and the
-// library is compiled with -ffp-contract=off so no other contraction happens.
+// Everything is plain IEEE fp32 (divisions by launch constants are evaluated
+// through an exactly-equivalent double product, div_rcp); FMAs are explicit
+// (__builtin_fmaf) and the library is compiled with -ffp-contract=off so no
+// other contraction happens.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,6 +20,35 @@ __device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, fl
     return __builtin_fmaf(a2, b2, __builtin_fmaf(a1, b1, __builtin_fmaf(a0, b0, 0.0f)));
 }
 
+// a / b rounded to f32 exactly as IEEE division, for a divisor b that is fixed
+// per launch, given rb = 1.0 / (double)b.  Proof: the double product has
+// relative error < 2^-52 (two roundings to 53 bits), while the exact quotient
+// of two 24-bit-significand floats is never an f32 rounding midpoint and lies at
+// least 1 / (2^24 * 2^25) = 2^-49 (relative) away from every midpoint.  So the
+// product and a/b round to the same float (zeros, infinities, NaNs and f32
+// subnormal results included).  3 VALU instead of the 11-instruction f32
+// division sequence.
+__device__ __forceinline__ float div_rcp(float a, double rb) { return (float)((double)a * rb); }
+
+// A wave-uniform double held in SGPRs (the VALU double division that produced
+// it leaves it in VGPRs otherwise).
+__device__ __forceinline__ double uniform_d(double d) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, d);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double recip_uniform(int n) { return uniform_d(1.0 / (double)n); }
+
+// Per-launch constants of the feature-map grid.
+struct Grid {
+    float fWf, fHf;  // (float)Wf, (float)Hf
+    double rWf, rHf; // 1 / Wf, 1 / Hf in double (div_rcp)
+};
+__device__ __forceinline__ Grid make_grid(int Hf, int Wf) {
+    return Grid{(float)Wf, (float)Hf, recip_uniform(Wf), recip_uniform(Hf)};
+}
+
 // Bilinear taps of one BEV cell in one feature map.
 struct Taps {
     int x0, y0;       // top-left corner (only meaningful for valid taps)
@@ -26,7 +57,7 @@ struct Taps {
 };
 
 // h[9] = world->image homography, (x, y) = BEV cell centre on the ground plane.
-__device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, int Hf, int Wf, float sx, float sy) {
+__device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, const Grid &g, float sx, float sy) {
     // geometry.py:144-149
     const float u0 = dot3(h[0], h[1], h[2], x, y, 1.0f);
     const float u1 = dot3(h[3], h[4], h[5], x, y, 1.0f);
@@ -37,9 +68,9 @@ __device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, in
     // geometry.py:151-158
     const float fx = u * sx;
     const float fy = v * sy;
-    const float fWf = (float)Wf, fHf = (float)Hf;
-    const float gx = ((fx + 0.5f) / fWf) * 2.0f - 1.0f;
-    const float gy = ((fy + 0.5f) / fHf) * 2.0f - 1.0f;
+    const float fWf = g.fWf, fHf = g.fHf;
+    const float gx = div_rcp(fx + 0.5f, g.rWf) * 2.0f - 1.0f;  // ((fx + 0.5) / Wf) * 2 - 1
+    const float gy = div_rcp(fy + 0.5f, g.rHf) * 2.0f - 1.0f;
     // grid_sampler_2d (align_corners=False): ix = (gx + 1) * Wf/2 - 0.5 as one FMA
     const float ix = __builtin_fmaf(gx + 1.0f, fWf / 2.0f, -0.5f);
     const float iy = __builtin_fmaf(gy + 1.0f, fHf / 2.0f, -0.5f);

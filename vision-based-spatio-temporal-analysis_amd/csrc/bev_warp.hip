@@ -66,7 +66,8 @@ __global__ void k_taps(const float *__restrict__ Hmat, const float *__restrict__
     if (i >= Hb || j >= Wb) return;
     float h[9];
     load_h(Hmat, n, h);
-    const Taps t = cell_taps(h, xs[j], ys[i], Hf, Wf, sx, sy);
+    const Grid grid = make_grid(Hf, Wf);
+    const Taps t = cell_taps(h, xs[j], ys[i], grid, sx, sy);
     const size_t cell = ((size_t)n * Hb + i) * Wb + j;
     x0y0[2 * cell] = t.x0;
     x0y0[2 * cell + 1] = t.y0;
@@ -110,7 +111,8 @@ __global__ __launch_bounds__(NT) void k_warp(const float *__restrict__ feats, in
     if (i >= Hb || j >= Wb) return;
     float h[9];
     load_h(Hmat, n, h);
-    const Taps t = cell_taps(h, xs[j], ys[i], Hf, Wf, sx, sy);
+    const Grid grid = make_grid(Hf, Wf);
+    const Taps t = cell_taps(h, xs[j], ys[i], grid, sx, sy);
     const GOff g = global_offsets(t, sH, sW);
     const float *f = feats + (int64_t)n * sN;
     const size_t plane = (size_t)Hb * Wb;
@@ -196,6 +198,8 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
+    const Grid grid = make_grid(Hf, Wf);
+    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
     float *o = out + (size_t)b * C * plane + (size_t)(inside ? i : 0) * Wb + (inside ? j : 0);
 
     for (int c0 = 0; c0 < C; c0 += CK) {
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
             const int n = b * V + v;
             float h[9];
             load_h(Hmat, n, h);
-            Taps t = cell_taps(h, cx, cy, Hf, Wf, sx, sy);
+            Taps t = cell_taps(h, cx, cy, grid, sx, sy);
             if (!inside) t.valid = 0;
             int bx0 = 0x7fffffff, by0 = 0x7fffffff, bx1 = -1, by1 = -1;
             if (t.valid) {
@@ -336,11 +340,10 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
             }
         }
         if (inside) {
-            const float fv = (float)V;
 #pragma unroll
             for (int q = 0; q < CK; ++q) {
                 if (q < ck) {
-                    const float r = (MODE == BEV_FUSE_MEAN) ? acc[q] / fv : acc[q];
+                    const float r = (MODE == BEV_FUSE_MEAN) ? div_rcp(acc[q], rV) : acc[q];
                     __builtin_nontemporal_store(r, o + (size_t)(c0 + q) * plane);
                 }
             }
@@ -399,6 +402,25 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
             : "=&s"(keep)
             : "v"(src), "s"(dst)
             : "memory");
+    }
+}
+
+// Output stores of a 64-channel chunk through a buffer descriptor: SGPR base of
+// the chunk, per-lane byte offset of the cell, SGPR byte offset of the channel
+// plane -> no per-store address arithmetic.  The dispatcher guarantees the
+// chunk (64 planes) spans < 4 GiB.  aux 2 = nt (streaming, written once).
+__device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell, const float (&acc)[64], int mode,
+                                            double rV) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * 64 * sizeof(float)), 0x00020000);
+    const int voff = cell * (int)sizeof(float);
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+        float a = acc[q];
+        asm volatile("" : "+v"(a)::"memory");  // convert after the previous store (no hoisted doubles)
+        const float r = (mode == BEV_FUSE_MEAN) ? div_rcp(a, rV) : a;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
+                                              (int)(uint32_t)(q * plane * sizeof(float)), 2);
     }
 }
 
@@ -529,17 +551,25 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_dma(const float *__res
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
+    const Grid grid = make_grid(Hf, Wf);
+    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
 
+    float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
     auto taps_of = [&](int v) {
         float h[9];
         load_h(Hmat, b * V + v, h);
-        Taps t = cell_taps(h, cx, cy, Hf, Wf, sx, sy);
+        Taps t = cell_taps(h, ccx, ccy, grid, sx, sy);
         if (!inside) t.valid = 0;
         return t;
     };
 
     for (int c0 = 0; c0 < C; c0 += 64) {
+        // Taps are recomputed per chunk on purpose: without this the compiler hoists
+        // view 0's taps out of the chunk loop and spills them across it.
+        ccx = cx;
+        ccy = cy;
+        asm volatile("" : "+v"(ccx), "+v"(ccy));
         // max: -inf is the identity of the NaN-propagating max, so no first-view special case
         float acc[64];
 #pragma unroll
@@ -635,16 +665,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_dma(const float *__res
                 zero_view<MODE>(acc, v);
             }
         }
-        if (inside) {
-            const float fv = (float)V;
-            const int cell = i * Wb + j;
-#pragma unroll
-            for (int q = 0; q < 64; ++q) {
-                const float r = (MODE == BEV_FUSE_MEAN) ? acc[q] / fv : acc[q];
-                float *oc = out + ((size_t)b * C + c0 + q) * plane;  // wave-uniform base
-                __builtin_nontemporal_store(r, oc + cell);
-            }
-        }
+        if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
         __syncthreads();  // next chunk reuses red[] and the pool
     }
 }
@@ -710,13 +731,16 @@ __global__ __launch_bounds__(64, 3) void k_warp_fuse_wave(const float *__restric
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
+    const Grid grid = make_grid(Hf, Wf);
+    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
     const int isH = (int)sH, isW = (int)sW;
     if (lane < 16) *(float4 *)(smem + ZP + lane * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
 
+    float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
     auto taps_of = [&](int v) {
         float h[9];
         load_h(Hmat, b * V + v, h);
-        Taps t = cell_taps(h, cx, cy, Hf, Wf, sx, sy);
+        Taps t = cell_taps(h, ccx, ccy, grid, sx, sy);
         if (!inside) t.valid = 0;
         return t;
     };
@@ -730,6 +754,11 @@ __global__ __launch_bounds__(64, 3) void k_warp_fuse_wave(const float *__restric
     };
 
     for (int c0 = 0; c0 < C; c0 += 64) {
+        // Taps are recomputed per chunk on purpose: without this the compiler hoists
+        // view 0's taps out of the chunk loop and spills them across it.
+        ccx = cx;
+        ccy = cy;
+        asm volatile("" : "+v"(ccx), "+v"(ccy));
         float acc[64];
 #pragma unroll
         for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
@@ -811,16 +840,7 @@ __global__ __launch_bounds__(64, 3) void k_warp_fuse_wave(const float *__restric
                 zero_view<MODE>(acc, v);
             }
         }
-        if (inside) {
-            const float fv = (float)V;
-            const int cell = i * Wb + j;
-#pragma unroll
-            for (int q = 0; q < 64; ++q) {
-                const float r = (MODE == BEV_FUSE_MEAN) ? acc[q] / fv : acc[q];
-                float *oc = out + ((size_t)b * C + c0 + q) * plane;
-                __builtin_nontemporal_store(r, oc + cell);
-            }
-        }
+        if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
     }
 }
 
@@ -837,16 +857,18 @@ __global__ __launch_bounds__(NT) void k_warp_bwd(const float *__restrict__ gout,
     if (i >= Hb || j >= Wb) return;
     float h[9];
     load_h(Hmat, n, h);
-    const Taps t = cell_taps(h, xs[j], ys[i], Hf, Wf, sx, sy);
+    const Grid grid = make_grid(Hf, Wf);
+    const Taps t = cell_taps(h, xs[j], ys[i], grid, sx, sy);
     if (t.valid == 0) return;
     const size_t plane = (size_t)Hb * Wb, fplane = (size_t)Hf * Wf;
     const int src = per_view_gout ? n : n / V;
+    const double rscale = 1.0 / (double)scale;
     const float *g = gout + (size_t)src * C * plane + (size_t)i * Wb + j;
     float *gf = gfeats + (size_t)n * C * fplane;
     const size_t base = (size_t)t.y0 * Wf + t.x0;
     for (int c = 0; c < C; ++c) {
         float go = g[(size_t)c * plane];
-        if (scale != 1.0f) go = go / scale;  // mean backward: grad / V
+        if (scale != 1.0f) go = div_rcp(go, rscale);  // mean backward: grad / V
         float *p = gf + (size_t)c * fplane + base;
         if (t.valid & 1) atomicAdd(p, t.w[0] * go);
         if (t.valid & 2) atomicAdd(p + 1, t.w[1] * go);
@@ -863,7 +885,7 @@ __global__ void k_view_fuse(const float *__restrict__ x, int V, int64_t M, float
     const int b = blockIdx.y;
     const float *xb = x + (size_t)b * V * M;
     float *ob = out + (size_t)b * M;
-    const float fv = (float)V;
+    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
     for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
         float acc;
         if (MODE == BEV_FUSE_MAX) {
@@ -872,7 +894,7 @@ __global__ void k_view_fuse(const float *__restrict__ x, int V, int64_t M, float
         } else {
             acc = 0.0f;
             for (int v = 0; v < V; ++v) acc = acc + xb[(size_t)v * M + m];
-            if (MODE == BEV_FUSE_MEAN) acc = acc / fv;
+            if (MODE == BEV_FUSE_MEAN) acc = div_rcp(acc, rV);
         }
         ob[m] = acc;
     }
@@ -993,7 +1015,7 @@ inline int launch_fuse_dma(const float *feats, int64_t sN, int64_t sH, int64_t s
                            const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                            int Hb, int Wb, int mode, float *out, hipStream_t st) {
     const char *e = getenv("BEV_WARP_POOL_KB");
-    if (warp_occ() == 2) {
+    if (warp_occ() == 2 || mode == BEV_FUSE_MAX) {  // MAX's extra live state spills at 128 VGPRs
         const int pool = e ? warp_pool_bytes() : 72 * 1024;
         return launch_fuse_dma_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
                                       st, pool);
@@ -1073,7 +1095,9 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
     if (B == 0 || C == 0 || Hb == 0 || Wb == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const bool dma_ok = (sC == 1) && (C % 64 == 0) && Hf < 16384 && Wf < 16384 && ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) && (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) &&
-                        (sH % 4 == 0) && (sN % 4 == 0) && getenv("BEV_WARP_NO_DMA") == nullptr;
+                        (sH % 4 == 0) && (sN % 4 == 0) &&
+                        (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32) &&  // store_chunk descriptor
+                        getenv("BEV_WARP_NO_DMA") == nullptr;
     if (dma_ok && getenv("BEV_WARP_WAVE") != nullptr)
         return launch_fuse_wave(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (dma_ok) return launch_fuse_dma(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);

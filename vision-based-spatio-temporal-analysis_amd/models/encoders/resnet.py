@@ -93,6 +93,14 @@ class FoldedConv:
         key = tuple((t.data_ptr(), t._version) for t in self._tensors()) + (str(device),)
         if key == self._key:
             return
+        w, b = self.folded(device)
+        with torch.no_grad():
+            self.packed = _nat.pack_conv_weight(w.contiguous())
+            self.bias = b.contiguous().float()
+        self._key = key
+
+    def folded(self, device):
+        """(w OIHW, b) with eval BN folded in, on `device`."""
         with torch.no_grad():
             w = self.conv.weight.detach().to(device=device, dtype=torch.float32)
             b = (self.conv.bias.detach().to(device=device, dtype=torch.float32) if self.conv.bias is not None
@@ -102,15 +110,53 @@ class FoldedConv:
                 scale = bn.weight.detach().to(device) / torch.sqrt(bn.running_var.detach().to(device) + bn.eps)
                 w = w * scale.view(-1, 1, 1, 1)
                 b = bn.bias.detach().to(device) + (b - bn.running_mean.detach().to(device)) * scale
-            self.packed = _nat.pack_conv_weight(w.contiguous())
-            self.bias = b.contiguous().float()
-        self._key = key
+        return w, b
 
     def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False):
         self.prepare(x.device)
         c = self.conv
         return _nat.conv2d_nhwc(x, self.packed, self.bias, c.out_channels, c.kernel_size[0], c.kernel_size[1],
                                 c.stride[0], c.padding[0], relu, residual=residual, in_nchw=in_nchw)
+
+
+class FoldedTail:
+    """Bottleneck tail conv3/bn3 + downsample conv/bn (+ add + ReLU) as ONE dual-source 1x1 GEMM.
+
+    timm's Bottleneck.forward computes act3(bn3(conv3(h)) + bn_ds(conv_ds(x))); with both
+    BNs folded this is act(h (*) W3 + x[::s] (*) Wds + (b3 + bds)), a single GEMM over the
+    concatenated K = [h | x[::s]] -- the shortcut tensor is never written (bev_conv2d_dual_f32).
+    Summation order differs from conv-then-add: fp32-tolerance equal, not bitwise.
+    """
+
+    def __init__(self, main: FoldedConv, short: FoldedConv):
+        self.main, self.short = main, short
+        self._key = None
+        self.packed = self.bias = None
+
+    @staticmethod
+    def applies(blk) -> bool:
+        ds = blk.downsample
+        c3 = blk.conv3
+        return (ds is not None and isinstance(ds[0], nn.Conv2d) and ds[0].kernel_size == (1, 1)
+                and ds[0].padding == (0, 0) and c3.kernel_size == (1, 1) and c3.stride == (1, 1)
+                and c3.in_channels % 32 == 0 and ds[0].in_channels % 32 == 0 and ds[0].bias is None)
+
+    def prepare(self, device):
+        key = tuple((t.data_ptr(), t._version) for f in (self.main, self.short) for t in f._tensors()) + (str(device),)
+        if key == self._key:
+            return
+        w1, b1 = self.main.folded(device)
+        w2, b2 = self.short.folded(device)
+        with torch.no_grad():
+            w = torch.cat([w1.reshape(w1.shape[0], -1), w2.reshape(w2.shape[0], -1)], 1)
+            self.packed = _nat.pack_conv_weight(w.reshape(w.shape[0], w.shape[1], 1, 1).contiguous())
+            self.bias = (b1 + b2).contiguous().float()
+        self._key = key
+
+    def __call__(self, h, x):
+        self.prepare(h.device)
+        return _nat.conv2d_dual_nhwc(h, x, self.short.conv.stride[0], self.packed, self.bias,
+                                     self.main.conv.out_channels, relu=True)
 
 
 def stage_of(out_index: int) -> int:
@@ -141,6 +187,7 @@ class ResNet(nn.Module):
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         self._folded = {}
+        self.fuse_shortcut = True  # bottleneck conv3 + downsample as one dual-source GEMM
 
     def _make_layer(self, block, planes, blocks, stride):
         downsample = None
@@ -174,7 +221,17 @@ class ResNet(nn.Module):
                 return y
         return y
 
+    def _tail(self, blk):
+        k = ("tail", id(blk))
+        if k not in self._folded:
+            self._folded[k] = FoldedTail(self._fc(blk.conv3, blk.bn3), self._fc(blk.downsample[0], blk.downsample[1]))
+        return self._folded[k]
+
     def _block(self, blk, x):
+        if isinstance(blk, Bottleneck) and self.fuse_shortcut and FoldedTail.applies(blk):
+            h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
+            h = self._fc(blk.conv2, blk.bn2)(h, relu=True)
+            return self._tail(blk)(h, x)
         sc = x
         if blk.downsample is not None:
             sc = self._fc(blk.downsample[0], blk.downsample[1])(x, relu=False)
