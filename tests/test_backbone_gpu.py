@@ -24,7 +24,8 @@ def _rand(shape, seed, scale=1.0):
 
 CASES = [
     # N, Ci, H, W, Co, K, stride, pad, nchw_in, residual, relu
-    (2, 3, 37, 53, 64, 7, 2, 3, True, False, True),    # stem (generic NCHW loader)
+    (2, 3, 37, 53, 64, 7, 2, 3, True, False, True),    # stem (k_stem: LDS patch, even/odd planes)
+    (1, 3, 45, 301, 24, 7, 2, 3, True, False, False),  # stem, ragged Co / partial tiles, no relu
     (1, 16, 20, 30, 24, 3, 2, 1, False, False, True),   # fallback encoder 2nd conv
     (2, 64, 17, 23, 64, 3, 1, 1, False, True, True),    # layer1 3x3 + residual
     (2, 64, 17, 23, 256, 1, 1, 0, False, True, True),   # 1x1 expand + residual

@@ -102,20 +102,20 @@ struct RowsA {
 // (ky, kx, ci0) position advances incrementally (no divisions in the loop).
 template <int ROWS>
 struct LoaderFast {
+    static constexpr int NV = ROWS;  // float4 per thread and K step
     RowsA<ROWS> rows;
     int quad, ky, kx, ci0;
-    f32x4 v[ROWS];
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
         rows.init(a, m0, tid);
         quad = tid & 7;
         ky = kx = ci0 = 0;
     }
     // A tile image: row (tid >> 3) + 32 r, k columns quad*4 .. +3
-    __device__ void store(float *As, int tid) const {
+    __device__ void store(float *As, int tid, const f32x4 (&v)[NV]) const {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) *(f32x4 *)(As + ((tid >> 3) + 32 * r) * LROW + quad * 4) = v[r];
     }
-    __device__ void load(const ConvArgs &a) {
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[NV]) {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
@@ -142,10 +142,10 @@ struct LoaderFast {
 // downsample's 1x1/stride-s2 input.  Ci, Ci2 % 32 == 0.
 template <int ROWS>
 struct LoaderDual {
+    static constexpr int NV = ROWS;
     int64_t p1[ROWS], p2[ROWS];
     bool ok[ROWS];
     int quad, k0;
-    f32x4 v[ROWS];
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
@@ -162,11 +162,11 @@ struct LoaderDual {
         quad = tid & 7;
         k0 = 0;
     }
-    __device__ void store(float *As, int tid) const {
+    __device__ void store(float *As, int tid, const f32x4 (&v)[NV]) const {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) *(f32x4 *)(As + ((tid >> 3) + 32 * r) * LROW + quad * 4) = v[r];
     }
-    __device__ void load(const ConvArgs &a) {
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[NV]) {
         const bool first = k0 < a.Ci;  // wave-uniform
         const float *src = first ? a.x + k0 : a.x2 + (k0 - a.Ci);
 #pragma unroll
@@ -187,10 +187,10 @@ template <int BM, int CI = 0, int KWc = 0>
 struct LoaderRow {
     static constexpr int TPR = 256 / BM;  // threads per row
     static constexpr int KPT = BK / TPR;  // k's per thread and K step
+    static constexpr int NV = KPT / 4;
     int64_t pix;
     int iy0, ix0, row, kq, k0;
     bool ok, nchw;
-    f32x4 v[KPT / 4];
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
         row = tid % BM;
         kq = tid / BM;
@@ -207,11 +207,11 @@ struct LoaderRow {
         k0 = 0;
         nchw = a.in_nchw != 0;
     }
-    __device__ void store(float *As, int) const {
+    __device__ void store(float *As, int, const f32x4 (&v)[NV]) const {
 #pragma unroll
         for (int i = 0; i < KPT / 4; ++i) *(f32x4 *)(As + row * LROW + kq * KPT + 4 * i) = v[i];
     }
-    __device__ void load(const ConvArgs &a) {
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[NV]) {
         const int Ci = CI > 0 ? CI : a.Ci, KW = KWc > 0 ? KWc : a.KW;
         float e[KPT];
 #pragma unroll
@@ -273,31 +273,36 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
-    // global -> register prefetch of one K step (helpers, not lambdas: register
-    // arrays captured by reference were address-taken and landed in scratch)
-    f32x4 rb[BROWS];
+    // global -> register prefetch, TWO K steps ahead (helpers, not lambdas: register
+    // arrays captured by reference were address-taken and landed in scratch).
+    // Step ks: registers set 0 receive step ks+2 while the MFMAs consume LDS
+    // buffer ks&1; set 1 (step ks+1) is then written to the other LDS buffer.
+    constexpr int NV = decltype(la)::NV;
+    f32x4 va0[NV], va1[NV], rb0[BROWS], rb1[BROWS];
     int kb = 0;  // k offset of the B panel
-#define BEV_GLOAD()                          \
-    do {                                     \
-        la.load(a);                          \
-        load_rows<BROWS>(rb, wrow, a.Kp, kb); \
-        la.advance(a);                       \
-        kb += BK;                            \
+#define BEV_GLOAD(VA, RB)                     \
+    do {                                      \
+        la.load(a, VA);                       \
+        load_rows<BROWS>(RB, wrow, a.Kp, kb); \
+        la.advance(a);                        \
+        kb += BK;                             \
     } while (0)
-#define BEV_SWRITE(buf)                                                                   \
-    do {                                                                                  \
-        la.store(lds + (buf) * STAGE, tid);                                               \
-        store_rows<BROWS>(lds + (buf) * STAGE + (BM + (tid >> 3)) * LROW + bq * 4, rb);   \
+#define BEV_SWRITE(buf, VA, RB)                                                               \
+    do {                                                                                      \
+        la.store(lds + (buf) * STAGE, tid, VA);                                               \
+        store_rows<BROWS>(lds + (buf) * STAGE + (BM + (tid >> 3)) * LROW + bq * 4, RB);       \
     } while (0)
 
     const int nk = a.Kp / BK;
-    BEV_GLOAD();
-    BEV_SWRITE(0);
+    BEV_GLOAD(va0, rb0);
+    if (nk > 1) BEV_GLOAD(va1, rb1);
+    BEV_SWRITE(0, va0, rb0);
     __syncthreads();
     const int r32 = lane & 31, h = lane >> 5;
     for (int ks = 0; ks < nk; ++ks) {
         const int cur = ks & 1;
-        if (ks + 1 < nk) BEV_GLOAD();
+        const bool pre2 = ks + 2 < nk;
+        if (pre2) BEV_GLOAD(va0, rb0);
         const float *As = lds + cur * STAGE;
         const float *Bs = As + BM * LROW;
         // MFMA k-slot h of step p reads k = 16 h + p (p = 0..15): per half of the
@@ -331,8 +336,14 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
             }
         }
         if (ks + 1 < nk) {
-            BEV_SWRITE(cur ^ 1);
+            BEV_SWRITE(cur ^ 1, va1, rb1);
             __syncthreads();
+        }
+        if (pre2) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) va1[q] = va0[q];
+#pragma unroll
+            for (int q = 0; q < BROWS; ++q) rb1[q] = rb0[q];
         }
     }
 #undef BEV_GLOAD
@@ -409,6 +420,183 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// ResNet stem: 7x7 / stride 2 / pad 3 over Ci = 3 NCHW images, Co <= 64
+// ---------------------------------------------------------------------------
+// timm conv1 (cnn_encoder.py:26 backbone; first layer of CNNEncoder._encode_single).
+// Persistent workgroups; one output tile = 2 rows x 64 columns x Co channels,
+// wave w owns 32 pixels (row w >> 1, columns 32 (w & 1) ..) x all channels
+// (2 MFMA tiles of 32 x 32).  The tile's input patch (3 ch x 9 rows x 134
+// cols) is read ONCE with coalesced row loads and kept in LDS as even / odd
+// column planes: with stride 2, tap kx of output column ox reads column
+// 2 ox + kx, i.e. plane (kx & 1) at index ox + kx / 2, so the two k-slots of
+// one v_mfma_f32_32x32x2_f32 are the taps (kx = 2a, kx = 2a + 1) of one
+// (ci, ky) and every A operand is a conflict-free ds_read_b32 at a
+// compile-time offset (84 MFMA k-pairs: 3 ci x 7 ky x 4 a; kx = 7 has zero
+// weight).  The next tile's patch is fetched into registers during the MFMAs
+// (double-buffered LDS).  Weights are re-laid out into LDS once per workgroup
+// from the standard packed panel.
+namespace stem {
+constexpr int TW = 64, TH = 2;
+constexpr int PR = 2 * TH + 5;                     // 9 input rows
+constexpr int PC = 2 * TW + 6;                     // 134 input columns (incl. the kx = 7 pad column)
+constexpr int PP = 80;                             // plane pitch: 67 used; = 16 mod 32 -> conflict-free stores
+constexpr int RP = 2 * PP, CP = PR * RP, PATCH = 3 * CP;
+constexpr int NQ = 3 * 7 * 4;                      // k pairs
+constexpr int WP = 2 * NQ + 4;                     // weight row pitch (172 floats = 43 odd 16-B slots)
+constexpr int NE = 3 * PR * PC;                    // patch elements
+constexpr int PER_T = (NE + 255) / 256;            // per thread (15)
+}  // namespace stem
+
+struct StemArgs {
+    const float *__restrict__ x;
+    const float *__restrict__ wp;
+    const float *__restrict__ bias;
+    float *__restrict__ y;
+    int N, H, W, Kp, Co, Ho, Wo, relu, nTx, nTy;
+    int64_t ntiles;
+};
+
+__device__ __forceinline__ void stem_fetch(const StemArgs &a, int64_t t, int tid, float (&pv)[stem::PER_T]) {
+    using namespace stem;
+    const int tx = (int)(t % a.nTx);
+    const int64_t r_ = t / a.nTx;
+    const int ty = (int)(r_ % a.nTy);
+    const int64_t img = r_ / a.nTy;
+    const int row0 = 2 * ty * TH - 3, col0 = 2 * tx * TW - 3;
+    const float *xi = a.x + img * 3 * (int64_t)a.H * a.W;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+        const int e = tid + 256 * i;
+        const int cr = e / PC, c = e - cr * PC;
+        const int ci = cr / PR, r = cr - ci * PR;
+        const int gy = row0 + r, gx = col0 + c;
+        const bool in = e < NE && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+        pv[i] = in ? xi[((int64_t)ci * a.H + gy) * a.W + gx] : 0.0f;
+    }
+}
+
+__device__ __forceinline__ void stem_put(float *pl, int tid, const float (&pv)[stem::PER_T]) {
+    using namespace stem;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+        const int e = tid + 256 * i;
+        if (e < NE) {
+            const int cr = e / PC, c = e - cr * PC;
+            const int ci = cr / PR, r = cr - ci * PR;
+            pl[ci * CP + r * RP + (c & 1) * PP + (c >> 1)] = pv[i];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void k_stem(StemArgs a) {
+    using namespace stem;
+    __shared__ __attribute__((aligned(16))) float wl[64 * WP];
+    __shared__ __attribute__((aligned(16))) float pl[2 * PATCH];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+
+    // weights: wl[n][h * NQ + q] = W[n][ci][ky][kx = 2 a + h], q = (ci * 7 + ky) * 4 + a
+    for (int e = tid; e < 64 * 2 * NQ; e += 256) {
+        const int n = e / (2 * NQ), hq = e - n * (2 * NQ), hh = hq / NQ, q = hq - hh * NQ;
+        const int ci = q / 28, ky = (q % 28) / 4, kx = 2 * (q % 4) + hh;
+        float v = 0.0f;
+        if (n < a.Co && kx < 7) v = a.wp[(int64_t)n * a.Kp + (ky * 7 + kx) * 3 + ci];
+        wl[n * WP + hq] = v;
+    }
+    float pv[PER_T];
+    int64_t t = blockIdx.x;
+    if (t < a.ntiles) {
+        stem_fetch(a, t, tid, pv);
+        stem_put(pl, tid, pv);
+    }
+    __syncthreads();
+
+    const int ol = wave >> 1, oxl = 32 * (wave & 1) + r32;
+    const int abase = ol * 2 * RP + oxl + h * PP;  // + ci*CP + ky*RP + a per k pair
+    const float *wb0 = wl + r32 * WP + h * NQ, *wb1 = wl + (32 + r32) * WP + h * NQ;
+    const float b0 = (r32 < a.Co) ? a.bias[r32] : 0.0f;
+    const float b1 = (32 + r32 < a.Co) ? a.bias[32 + r32] : 0.0f;
+    int buf = 0;
+    for (; t < a.ntiles; t += gridDim.x) {
+        const int64_t tn = t + gridDim.x;
+        if (tn < a.ntiles) stem_fetch(a, tn, tid, pv);  // in flight during the MFMAs
+        const float *P = pl + buf * PATCH + abase;
+        f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
+#pragma unroll
+        for (int q4 = 0; q4 < NQ; q4 += 4) {
+            const f32x4 w0 = *(const f32x4 *)(wb0 + q4), w1 = *(const f32x4 *)(wb1 + q4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = q4 + u, ci = q / 28, ky = (q % 28) / 4, aa = q % 4;
+                const float av = P[ci * CP + ky * RP + aa];
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w0[u], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w1[u], acc1, 0, 0, 0);
+            }
+        }
+        // epilogue: D[row][col], col = channel r32 (+32), row = pixel (r & 3) + 8 (r >> 2) + 4 h
+        {
+            const int tx = (int)(t % a.nTx);
+            const int64_t r_ = t / a.nTx;
+            const int ty = (int)(r_ % a.nTy);
+            const int64_t img = r_ / a.nTy;
+            const int oy = ty * TH + ol;
+            const int oxb = tx * TW + 32 * (wave & 1);
+            if (oy < a.Ho) {
+                float *yr = a.y + ((img * a.Ho + oy) * (int64_t)a.Wo) * a.Co;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int ox = oxb + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (ox < a.Wo) {
+                        float v0 = acc0[r] + b0, v1 = acc1[r] + b1;
+                        if (a.relu) {
+                            v0 = v0 > 0.0f ? v0 : 0.0f;
+                            v1 = v1 > 0.0f ? v1 : 0.0f;
+                        }
+                        float *yp = yr + (int64_t)ox * a.Co;
+                        if (r32 < a.Co) yp[r32] = v0;
+                        if (32 + r32 < a.Co) yp[32 + r32] = v1;
+                    }
+                }
+            }
+        }
+        if (tn < a.ntiles) stem_put(pl + (buf ^ 1) * PATCH, tid, pv);
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
+int g_num_cu = 0;
+
+int launch_stem(const float *x, int N, int H, int W, const float *packed, int Kp, const float *bias, int Co,
+                float *y, int Ho, int Wo, int relu, hipStream_t st) {
+    if (g_num_cu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                    hipSuccess || n <= 0)
+            n = 256;
+        g_num_cu = n;
+    }
+    StemArgs a;
+    a.x = x;
+    a.wp = packed;
+    a.bias = bias;
+    a.y = y;
+    a.N = N;
+    a.H = H;
+    a.W = W;
+    a.Kp = Kp;
+    a.Co = Co;
+    a.Ho = Ho;
+    a.Wo = Wo;
+    a.relu = relu;
+    a.nTx = (Wo + stem::TW - 1) / stem::TW;
+    a.nTy = (Ho + stem::TH - 1) / stem::TH;
+    a.ntiles = (int64_t)N * a.nTx * a.nTy;
+    const int64_t grid = a.ntiles < 2 * (int64_t)g_num_cu ? a.ntiles : 2 * (int64_t)g_num_cu;
+    hipLaunchKernelGGL(k_stem, dim3((unsigned)grid), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
 }
 
 // NHWC max-pool (padding counts as -inf, as torch.nn.MaxPool2d); one float4
@@ -574,6 +762,9 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : 0;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    if (in_nchw && Ci == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && Co <= 64 && !residual && bias &&
+        g_conv_tile == 0)
+        return launch_stem(x, N, H, W, packed, a.Kp, bias, Co, y, Ho, Wo, relu, (hipStream_t)stream);
     return launch_tiled(a, loader, (hipStream_t)stream);
 }
 

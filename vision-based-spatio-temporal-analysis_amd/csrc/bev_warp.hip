@@ -34,6 +34,8 @@ using namespace bev;
 
 namespace {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 constexpr int TILE_W = 64;  // cells per wavefront row (one wave = one row piece)
 constexpr int TILE_H = 4;   // wavefronts per workgroup
 constexpr int NT = TILE_W * TILE_H;
@@ -424,6 +426,44 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
     }
 }
 
+// Output stores of a 64-channel chunk of an FT_H x FT_W tile, widened: the
+// accumulators go through LDS in 16-channel rounds ([ch][cell] image, two
+// buffers) and come back as float4 = 4 consecutive cells of one channel, so one
+// buffer_store_dwordx4 writes a channel's whole 8 x 32 tile (8 x 128 B) instead
+// of 64 x 4 B per wave-instruction.  Needs Wb % 4 == 0 and a pool >= 2 * 16.25 KiB.
+// Called after a workgroup barrier (the pool is free); ends with one.
+constexpr int TP = FT_W * FT_H + 4;  // [ch][cell] row pitch in floats
+__device__ __forceinline__ void store_chunk_wide(float *chunk, size_t plane, int Hb, int Wb, int i0, int j0,
+                                                 float *lds, int tid, const float (&acc)[64], int mode, double rV) {
+    const int cell = tid;  // tile-local: row = tid >> 5 (wave * 2 + half), col = tid & 31
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * 64 * sizeof(float)), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float *T = lds + (r & 1) * 16 * TP;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            float a = acc[16 * r + q];
+            asm volatile("" : "+v"(a)::"memory");
+            T[q * TP + cell] = (mode == BEV_FUSE_MEAN) ? div_rcp(a, rV) : a;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int idx = tid + 256 * k, ch = idx >> 6, quad = idx & 63;
+            const int row = quad >> 3, col = (quad & 7) * 4;
+            const int i = i0 + row, j = j0 + col;
+            if (i < Hb && j < Wb) {
+                const f32x4 v = *(const f32x4 *)(T + ch * TP + row * FT_W + col);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                       rs, (int)((i * Wb + j) * sizeof(float)),
+                                                       (int)(uint32_t)((16 * r + ch) * plane * sizeof(float)), 2);
+            }
+        }
+    }
+    __syncthreads();
+}
+
 // Footprint bbox of the workgroup for one view (wave partials -> red[] -> block).
 struct Box {
     int x0, y0, x1, y1;
@@ -667,6 +707,318 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_dma(const float *__res
         }
         if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
         __syncthreads();  // next chunk reuses red[] and the pool
+    }
+}
+
+// -------------------------------------------------------------------------
+// fused warp + reduce v2: corner-bounded footprints (default DMA path)
+// -------------------------------------------------------------------------
+// Same tile, lane mapping, LDS image layout, ring and block decomposition as
+// k_warp_fuse_dma; what changes is how a (tile, view) footprint is found and
+// therefore the per-view critical path.  The image of the tile's cell-centre
+// rectangle under x -> (H x)_{0,1} / (H x)_2 is a convex quadrilateral whenever
+// w = (H x)_2 keeps one sign on it, so the bilinear taps of every cell lie in
+// the bbox of the four corner projections widened by a bound on the fp32
+// rounding of the tap recipe.  Every wave computes that box for all views at
+// once (lane v -> view v, in double) and reads it back with readlane: no
+// cross-lane bbox reduction, no LDS exchange, and a view whose box misses the
+// feature map costs no tap arithmetic at all.  Tiles where the bound does not
+// apply (w may change sign or come near the 1e-6 clamp of geometry.py:147)
+// take the exact per-cell reduction of k_warp_fuse_dma for that view.
+// Per view:  [stage synchronously if it did not fit] -> issue LDS-DMA of
+// view v+1 -> taps of view v -> software-pipelined LDS sampling (the next 4
+// channels' four ds_read_b128 are in flight during this group's FMAs) ->
+// vmcnt(0) + one barrier.
+constexpr double EPS32 = 5.9604644775390625e-08;  // 2^-24
+constexpr int V2_MAXV = 64;                         // one view per lane
+
+// Conservative tap bbox of the BEV rectangle [xa, xb] x [ya, yb] (cell
+// centres) for homography h; ok = false when the corner bound does not apply.
+__device__ Box corner_box(const float *hf, float xa, float xb, float ya, float yb, float sx, float sy, int Wf, int Hf,
+                          bool &ok) {
+    double h[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) h[q] = (double)hf[q];
+    double ixmin = __builtin_inf(), ixmax = -__builtin_inf(), iymin = __builtin_inf(), iymax = -__builtin_inf();
+    double wmin = __builtin_inf(), swmax = 0.0, sumax = 0.0, svmax = 0.0, umax = 0.0, vmax = 0.0, aix = 0.0, aiy = 0.0;
+    int npos = 0, nneg = 0;
+    bool fin = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double x = (double)((c & 1) ? xb : xa), y = (double)((c & 2) ? yb : ya);
+        const double a0 = h[0] * x, a1 = h[1] * y, b0 = h[3] * x, b1 = h[4] * y, c0 = h[6] * x, c1 = h[7] * y;
+        const double u = a0 + a1 + h[2], v = b0 + b1 + h[5], w = c0 + c1 + h[8];
+        sumax = fmax(sumax, fabs(a0) + fabs(a1) + fabs(h[2]));
+        svmax = fmax(svmax, fabs(b0) + fabs(b1) + fabs(h[5]));
+        swmax = fmax(swmax, fabs(c0) + fabs(c1) + fabs(h[8]));
+        npos += w > 0.0;
+        nneg += w < 0.0;
+        wmin = fmin(wmin, fabs(w));
+        double rw = __builtin_amdgcn_rcp(w);  // + one Newton step: ~1e-15 relative, far inside the margin
+        rw = rw * (2.0 - w * rw);
+        const double U = u * rw, Vv = v * rw;
+        const double ix = U * (double)sx, iy = Vv * (double)sy;
+        fin = fin && __builtin_isfinite(ix) && __builtin_isfinite(iy) && __builtin_isfinite(w);
+        umax = fmax(umax, fabs(U));
+        vmax = fmax(vmax, fabs(Vv));
+        aix = fmax(aix, fabs(ix));
+        aiy = fmax(aiy, fabs(iy));
+        ixmin = fmin(ixmin, ix);
+        ixmax = fmax(ixmax, ix);
+        iymin = fmin(iymin, iy);
+        iymax = fmax(iymax, iy);
+    }
+    ok = fin && (npos == 4 || nneg == 4) && wmin > 1e-6 + 4.0 * EPS32 * swmax;
+    Box b{0x7fffffff, 0x7fffffff, -1, -1};
+    if (!ok) return b;
+    // |fp32 tap coordinate - exact| <= (dot3 error + division) / |w| + normalisation steps; x4 safety
+    const double mx = 4.0 * ((double)sx * 3.0 * EPS32 * (sumax + umax * swmax) / wmin +
+                             16.0 * EPS32 * (aix + (double)Wf + 1.0)) + 1e-3;
+    const double my = 4.0 * ((double)sy * 3.0 * EPS32 * (svmax + vmax * swmax) / wmin +
+                             16.0 * EPS32 * (aiy + (double)Hf + 1.0)) + 1e-3;
+    const double lox = fmin(fmax(ixmin - mx, -4.0), (double)Wf + 4.0);
+    const double hix = fmin(fmax(ixmax + mx, -4.0), (double)Wf + 4.0);
+    const double loy = fmin(fmax(iymin - my, -4.0), (double)Hf + 4.0);
+    const double hiy = fmin(fmax(iymax + my, -4.0), (double)Hf + 4.0);
+    const int x0 = max((int)floor(lox), 0), x1 = min((int)floor(hix) + 1, Wf - 1);
+    const int y0 = max((int)floor(loy), 0), y1 = min((int)floor(hiy) + 1, Hf - 1);
+    if (x0 <= x1 && y0 <= y1) b = Box{x0, y0, x1, y1};
+    return b;
+}
+
+// LDS sampling of one view, software-pipelined by one 4-channel group.
+template <int MODE>
+__device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t, const unsigned char *smem, int ib,
+                                                 int sx0, int sy0, int sbw, int zp) {
+    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * DPS;
+    const unsigned char *a0 = smem + ((t.valid & 1) ? pb : zp);
+    const unsigned char *a1 = smem + ((t.valid & 2) ? pb + DPS : zp);
+    const unsigned char *a2 = smem + ((t.valid & 4) ? pb + sbw * DPS : zp);
+    const unsigned char *a3 = smem + ((t.valid & 8) ? pb + (sbw + 1) * DPS : zp);
+    f32x4 c0 = *(const f32x4 *)a0, c1 = *(const f32x4 *)a1, c2 = *(const f32x4 *)a2, c3 = *(const f32x4 *)a3;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+        f32x4 n0, n1, n2, n3;
+        if (g < 15) {
+            n0 = *(const f32x4 *)(a0 + (g + 1) * 16);
+            n1 = *(const f32x4 *)(a1 + (g + 1) * 16);
+            n2 = *(const f32x4 *)(a2 + (g + 1) * 16);
+            n3 = *(const f32x4 *)(a3 + (g + 1) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float sm = bilerp(c0[u], c1[u], c2[u], c3[u], t.w);
+            float &a = acc[4 * g + u];
+            a = (MODE == BEV_FUSE_MAX) ? nan_max(a, sm) : a + sm;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // at most two groups of reads in flight
+        if (g < 15) {
+            c0 = n0;
+            c1 = n1;
+            c2 = n2;
+            c3 = n3;
+        }
+    }
+}
+
+template <int MODE, int OCC, bool WIDE>
+__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                           int64_t sW, const float *__restrict__ Hmat,
+                                                           const float *__restrict__ xs,
+                                                           const float *__restrict__ ys, int V, int C, int Hf,
+                                                           int Wf, float sx, float sy, int Hb, int Wb,
+                                                           float *__restrict__ out, int pool, int dbg) {
+    // dbg: profiling-only ablations (BEV_WARP_DEBUG; results are WRONG when set):
+    //   1 skip views that need synchronous staging, 2 skip LDS sampling, 4 skip stores, 8 skip DMA
+    // WIDE: widened float4 stores through LDS (store_chunk_wide); the launcher checks its conditions
+    constexpr bool wide = WIDE;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int zp = pool;                                    // zero pixel (256 B)
+    int *red = reinterpret_cast<int *>(smem + pool + 256);  // [16] exact-bbox exchange
+    float *htab = reinterpret_cast<float *>(smem + pool + 256 + 16 * sizeof(int));  // [V][9] homographies
+    const int maxpix = pool / DPS - 4;                      // ~1 KiB DMA rounding slack
+
+    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, nt = ntx * nty;
+    int tile = blockIdx.x;
+    {
+        const int q = nt / 8, r = nt % 8, x = tile % 8;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    const int tyb = tile / ntx, txb = tile - tyb * ntx;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i = tyb * FT_H + wave * 2 + (lane >> 5);
+    const int j = txb * FT_W + (lane & 31);
+    const int b = blockIdx.y;
+    const bool inside = (i < Hb) && (j < Wb);
+    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
+    const size_t plane = (size_t)Hb * Wb;
+    const Grid grid = make_grid(Hf, Wf);
+    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
+    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    // corner boxes of this tile, lane v <-> view v, packed in two VGPRs:
+    // lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16  (x1 + 1 == 0: empty)
+    unsigned lba, lbb;
+    {
+        const int ia = tyb * FT_H, ib = min(ia + FT_H - 1, Hb - 1);
+        const int ja = txb * FT_W, jb = min(ja + FT_W - 1, Wb - 1);
+        Box cb{0x7fffffff, 0x7fffffff, -1, -1};
+        bool ok = true;
+        if (lane < V) {
+            float hv[9];
+            load_h(Hmat, b * V + lane, hv);
+            if (wave == 0) {
+#pragma unroll
+                for (int q = 0; q < 9; ++q) htab[lane * 9 + q] = hv[q];  // visible after the prologue barrier
+            }
+            cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok);
+            // large footprints: the exact per-cell box (usually much smaller near the
+            // horizon, where adjacent cell rows map far apart) decides the staging
+            if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
+        }
+        const bool emp = cb.x1 < 0;
+        lba = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
+        lbb = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
+    }
+    auto box_of = [&](int v) {
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
+        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
+        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
+    };
+    auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
+
+    float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
+    auto taps_of = [&](int v) {
+        float h[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) h[q] = htab[v * 9 + q];  // uniform LDS address: broadcast
+        Taps t = cell_taps(h, ccx, ccy, grid, sx, sy);
+        if (!inside) t.valid = 0;
+        return t;
+    };
+
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        ccx = cx;
+        ccy = cy;
+        asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep taps per chunk (no hoisting + spills)
+        float acc[64];
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        const float *fb = feats + (int64_t)(b * V) * sN + c0;
+
+        // prologue: DMA of view 0 (if its corner box applies and fits)
+        Box bn = box_of(0);
+        int offn = -1;
+        {
+            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+            if (ok_of(0) && bn.x1 >= 0 && npix <= maxpix) {
+                offn = 0;
+                dma_block(fb, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, 0, wave, lane);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // zero pixel + image of view 0
+
+        for (int v = 0; v < V; ++v) {
+            Box bx = bn;
+            const int off = offn;
+            const float *f = fb + (int64_t)v * sN;
+            Taps t;
+            bool have_t = false;
+            if (!ok_of(v)) {
+                // exact footprint by per-cell reduction (horizon tiles); staged synchronously
+                t = taps_of(v);
+                have_t = true;
+                put_box(red, wave_box(t), wave, lane);
+                __syncthreads();
+                bx = get_box(red);
+            }
+            const bool empty = bx.x1 < 0;
+            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+            bool done = empty || ((dbg & 1) && off < 0);
+            if (!done && off < 0) {
+                // ---- synchronous staging, overlapping blocks if larger than the pool ----
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                    hb = min(bh, maxpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                if (single)  // the common case: start the copy (the pool is free since the last
+                             // end-of-view barrier), compute the taps while it lands
+                    dma_block(f, (int)sH, (int)sW, bx.x0, bx.y0, bw, bw * bh, smem, 0, wave, lane);
+                if (!have_t) {
+                    t = taps_of(v);
+                    have_t = true;
+                }
+                int mkx = 0, mky = 0;
+                if (!single && t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
+                }
+                const bool wave_any = __ballot(t.valid != 0) != 0ull;
+                if (!single && !t.valid) zero_view<MODE>(acc, v);
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        if (!single) {
+                            __syncthreads();  // earlier LDS images are no longer read
+                            dma_block(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane);
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __syncthreads();
+                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
+                        if (go) sample_view<MODE, 1>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        else if (single) zero_view<MODE>(acc, v);
+                    }
+                done = true;
+                __syncthreads();  // every wave is done with the staged blocks before DMA(v+1) reuses the pool
+            }
+            // ---- look ahead: DMA of view v+1 beside the live image of view v ----------
+            if (v + 1 < V) {
+                bn = box_of(v + 1);
+                offn = -1;
+                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+                if (ok_of(v + 1) && bn.x1 >= 0 && npix <= maxpix) {
+                    const int need = ((npix * 17 + 63) >> 6) * 1024;
+                    const int lo = (!done && off >= 0) ? off : 0;
+                    const int hi = (!done && off >= 0) ? off + (((bw * bh * 17 + 63) >> 6) * 1024) : 0;
+                    if (hi + need <= pool) offn = hi;
+                    else if (need <= lo) offn = 0;
+                    if (offn >= 0 && !(dbg & 8))
+                        dma_block(f + sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, offn, wave,
+                                  lane);
+                }
+            }
+            // ---- sample view v from its prefetched image ------------------------------
+            if (!done) {
+                if (!have_t) t = taps_of(v);
+                if (__ballot(t.valid != 0) != 0ull && !(dbg & 2))
+                    sample_view_pipe<MODE>(acc, t, smem, off, bx.x0, bx.y0, bw, zp);
+                else if (dbg & 2)
+                    acc[0] += t.w[0] + (float)t.x0;  // keep the taps live
+                else zero_view<MODE>(acc, v);
+            } else if (empty) {
+                zero_view<MODE>(acc, v);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
+            __syncthreads();  // all of it landed; image of view v and red[] are free
+        }
+        if (wide) {
+            if (!(dbg & 4))
+                store_chunk_wide(out + ((size_t)b * C + c0) * plane, plane, Hb, Wb, tyb * FT_H, txb * FT_W,
+                                 reinterpret_cast<float *>(smem), tid, acc, MODE, rV);
+        } else if (inside && !(dbg & 4)) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+        if (dbg & 4) {
+            float z = 0.f;
+            for (int q = 0; q < 64; ++q) z += acc[q];
+            if (z == 12345.f) out[0] = z;  // keep acc live
+        }
     }
 }
 
@@ -1011,6 +1363,60 @@ inline int launch_fuse_wave(const float *feats, int64_t sN, int64_t sH, int64_t 
     return last();
 }
 
+// Profiling-only ablation flags for k_warp_fuse_v2 (BEV_WARP_DEBUG, results are wrong when set).
+inline int warp_debug() {
+    static int v = [] {
+        const char *e = getenv("BEV_WARP_DEBUG");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+template <int OCC, bool WIDE>
+int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                       const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
+                       int mode, float *out, hipStream_t st, int pool) {
+    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
+    dim3 grid(ntiles, B), block(FT_NT);
+    const size_t lds = pool + 256 + 16 * sizeof(int) + V2_MAXV * 9 * sizeof(float);
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, WIDE>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, WIDE>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
+    else
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, WIDE>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
+    return last();
+}
+
+template <int OCC>
+int launch_fuse_v2_pick(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
+                        int mode, float *out, hipStream_t st, int pool) {
+    static const bool want_wide = getenv("BEV_WARP_WIDE") != nullptr;
+    if (want_wide && Wb % 4 == 0 && pool >= 2 * 16 * TP * (int)sizeof(float))
+        return launch_fuse_v2_occ<OCC, true>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode,
+                                             out, st, pool);
+    return launch_fuse_v2_occ<OCC, false>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                          st, pool);
+}
+
+inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
+                          const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                          int Hb, int Wb, int mode, float *out, hipStream_t st) {
+    const char *e = getenv("BEV_WARP_POOL_KB");
+    if (warp_occ() == 2 || mode == BEV_FUSE_MAX) {  // MAX's extra live state spills at 128 VGPRs
+        const int pool = e ? warp_pool_bytes() : 72 * 1024;
+        return launch_fuse_v2_pick<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                     st, pool);
+    }
+    const int pool = e ? warp_pool_bytes() : 36 * 1024;
+    return launch_fuse_v2_pick<4>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                 pool);
+}
+
 inline int launch_fuse_dma(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
                            const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                            int Hb, int Wb, int mode, float *out, hipStream_t st) {
@@ -1100,6 +1506,8 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
                         getenv("BEV_WARP_NO_DMA") == nullptr;
     if (dma_ok && getenv("BEV_WARP_WAVE") != nullptr)
         return launch_fuse_wave(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    if (dma_ok && V <= V2_MAXV && getenv("BEV_WARP_V1") == nullptr)
+        return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (dma_ok) return launch_fuse_dma(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
