@@ -23,6 +23,7 @@
 // to 80-B rows (conflict-free 16-lane groups).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -243,13 +244,17 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
 // LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1
-template <int WM, int WN, int TM, int TN, int LOADER>
-__global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
+// NBUF: LDS staging buffers.  2 = one barrier per K step; 1 = half the LDS (a
+// third workgroup per CU for the <= 170-VGPR tiles) at two barriers per K step.
+template <int WM, int WN, int TM, int TN, int LOADER, int NBUF>
+__global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int AROWS = BM / 32;  // A rows per thread (rows tid/8 + 32 r)
     constexpr int BROWS = BN / 32;
     constexpr int STAGE = (BM + BN) * LROW;
-    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+    constexpr int EPI = 4 * (TM * 32) * (TN * 32 + 4);  // epilogue tile (see below)
+    constexpr int LDSF = NBUF * STAGE > EPI ? NBUF * STAGE : EPI;
+    __shared__ __attribute__((aligned(16))) float lds[LDSF];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
         const int cur = ks & 1;
         const bool pre2 = ks + 2 < nk;
         if (pre2) BEV_GLOAD(va0, rb0);
-        const float *As = lds + cur * STAGE;
+        const float *As = lds + (NBUF == 2 ? cur : 0) * STAGE;
         const float *Bs = As + BM * LROW;
         // MFMA k-slot h of step p reads k = 16 h + p (p = 0..15): per half of the
         // step each lane reads two contiguous float4 of its row per operand tile.
@@ -336,7 +341,8 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
             }
         }
         if (ks + 1 < nk) {
-            BEV_SWRITE(cur ^ 1, va1, rb1);
+            if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
+            BEV_SWRITE(NBUF == 2 ? (cur ^ 1) : 0, va1, rb1);
             __syncthreads();
         }
         if (pre2) {
@@ -358,7 +364,7 @@ __global__ __launch_bounds__(256, 2) void k_conv(ConvArgs a) {
     constexpr int C4 = WC / 4;                              // float4 per row
     constexpr int RPI = 64 / C4;                            // rows per wave-instruction
     constexpr int NQ = WR / RPI;                            // float4 per lane
-    static_assert(4 * WR * ER <= 2 * STAGE, "epilogue tile must fit the staging LDS");
+    static_assert(4 * WR * ER <= LDSF, "epilogue tile must fit the staging LDS");
     __syncthreads();  // every wave is done reading the staging buffers
     float *E = lds + wave * (WR * ER);
 #pragma unroll
@@ -659,7 +665,7 @@ __global__ void k_transpose(const float *__restrict__ x, int R, int S, float *__
 
 inline int last() { return (int)hipGetLastError(); }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int NBUF = 2>
 int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t m_tiles = (a.M + BM - 1) / BM;
@@ -667,10 +673,10 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     const int64_t blocks = m_tiles * n_tiles;
     if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
     const dim3 g((unsigned)blocks), b(256);
-    if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1>), g, b, 0, st, a);
-    else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2>), g, b, 0, st, a);
-    else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3>), g, b, 0, st, a);
-    else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0>), g, b, 0, st, a);
+    if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1, NBUF>), g, b, 0, st, a);
+    else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2, NBUF>), g, b, 0, st, a);
+    else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3, NBUF>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0, NBUF>), g, b, 0, st, a);
     return last();
 }
 
@@ -695,8 +701,9 @@ int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
         if (c3 < 0.95 * best) { tile = 3; best = c3; }
         if (c2 < 0.95 * best) { tile = 2; best = c2; }
     }
-    if (tile == 2) return launch_conv<4, 1, 1, 2>(a, loader, st);  // 128 x 64 tiles
-    if (tile == 3) return launch_conv<2, 2, 1, 2>(a, loader, st);  // 64 x 128 tiles
+    static const bool nbuf1 = getenv("BEV_CONV_NBUF1") != nullptr;
+    if (tile == 2) return nbuf1 ? launch_conv<4, 1, 1, 2, 1>(a, loader, st) : launch_conv<4, 1, 1, 2>(a, loader, st);
+    if (tile == 3) return nbuf1 ? launch_conv<2, 2, 1, 2, 1>(a, loader, st) : launch_conv<2, 2, 1, 2>(a, loader, st);
     return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
 }
 

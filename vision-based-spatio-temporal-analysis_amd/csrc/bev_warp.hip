@@ -786,6 +786,39 @@ __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float y
     return b;
 }
 
+// bilerp (bev_geometry.h) of 4 channels as two independent packed chains,
+// written in interleaved order so that no packed op waits on its predecessor
+// (a dependent v_pk_* pair needs a wait state): per element exactly
+// fma(se, wse, fma(sw, wsw, fma(ne, wne, nw * wnw))), then acc + s / max.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int MODE>
+__device__ __forceinline__ void bilerp4(float (&acc)[64], int q0, const f32x4 &nw, const f32x4 &ne, const f32x4 &sw,
+                                        const f32x4 &se, const float w[4]) {
+    const f32x2 w0 = (f32x2){w[0], w[0]}, w1 = (f32x2){w[1], w[1]}, w2 = (f32x2){w[2], w[2]},
+                w3 = (f32x2){w[3], w[3]};
+    f32x2 a = nw.xy * w0, b = nw.zw * w0;
+    a = __builtin_elementwise_fma(ne.xy, w1, a);
+    b = __builtin_elementwise_fma(ne.zw, w1, b);
+    a = __builtin_elementwise_fma(sw.xy, w2, a);
+    b = __builtin_elementwise_fma(sw.zw, w2, b);
+    a = __builtin_elementwise_fma(se.xy, w3, a);
+    b = __builtin_elementwise_fma(se.zw, w3, b);
+    if (MODE == BEV_FUSE_MAX) {
+        acc[q0] = nan_max(acc[q0], a.x);
+        acc[q0 + 1] = nan_max(acc[q0 + 1], a.y);
+        acc[q0 + 2] = nan_max(acc[q0 + 2], b.x);
+        acc[q0 + 3] = nan_max(acc[q0 + 3], b.y);
+    } else {
+        f32x2 s0 = (f32x2){acc[q0], acc[q0 + 1]}, s1 = (f32x2){acc[q0 + 2], acc[q0 + 3]};
+        s0 = s0 + a;
+        s1 = s1 + b;
+        acc[q0] = s0.x;
+        acc[q0 + 1] = s0.y;
+        acc[q0 + 2] = s1.x;
+        acc[q0 + 3] = s1.y;
+    }
+}
+
 // LDS sampling of one view, software-pipelined by one 4-channel group.
 template <int MODE>
 __device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t, const unsigned char *smem, int ib,
@@ -805,12 +838,7 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t
             n2 = *(const f32x4 *)(a2 + (g + 1) * 16);
             n3 = *(const f32x4 *)(a3 + (g + 1) * 16);
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float sm = bilerp(c0[u], c1[u], c2[u], c3[u], t.w);
-            float &a = acc[4 * g + u];
-            a = (MODE == BEV_FUSE_MAX) ? nan_max(a, sm) : a + sm;
-        }
+        bilerp4<MODE>(acc, 4 * g, c0, c1, c2, c3, t.w);
         __builtin_amdgcn_sched_barrier(0);  // at most two groups of reads in flight
         if (g < 15) {
             c0 = n0;
@@ -985,11 +1013,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 offn = -1;
                 const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
                 if (ok_of(v + 1) && bn.x1 >= 0 && npix <= maxpix) {
+                    // consecutive images anchor at opposite ends of the pool: they coexist
+                    // whenever their sizes add up to at most the pool
                     const int need = ((npix * 17 + 63) >> 6) * 1024;
-                    const int lo = (!done && off >= 0) ? off : 0;
-                    const int hi = (!done && off >= 0) ? off + (((bw * bh * 17 + 63) >> 6) * 1024) : 0;
-                    if (hi + need <= pool) offn = hi;
-                    else if (need <= lo) offn = 0;
+                    if (done || off < 0) offn = 0;
+                    else if (off == 0) {
+                        if (((bw * bh * 17 + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
+                    } else if (need <= off) offn = 0;
                     if (offn >= 0 && !(dbg & 8))
                         dma_block(f + sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, offn, wave,
                                   lane);
