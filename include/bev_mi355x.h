@@ -40,6 +40,12 @@ int bev_abi_version(void);
  * 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128 output tiles for
  * bev_conv2d_f32.  Returns the previous value, or BEV_ERR_ARGS. */
 #define BEV_TUNE_CONV_TILE 1
+/* knob BEV_TUNE_WARP_POOL_KB: LDS image pool of the fused warp in KiB
+ * (0 = automatic; small pools force channel-chunked / direct units). */
+#define BEV_TUNE_WARP_POOL_KB 2
+/* knob BEV_TUNE_WARP_UNITS: 1 = route the fused warp through the unit-pipeline kernel
+ * (bev_warp_fuse.hip), 0 = the default v2 kernel.  Same results either way. */
+#define BEV_TUNE_WARP_UNITS 3
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

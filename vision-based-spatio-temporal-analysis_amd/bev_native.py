@@ -112,6 +112,8 @@ def lib():
 
 
 TUNE_CONV_TILE = 1
+TUNE_WARP_POOL_KB = 2
+TUNE_WARP_UNITS = 3
 
 
 def tune(knob: int, value: int) -> int:

@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_warp_fuse.h"
 
 namespace {
 
@@ -717,6 +718,14 @@ int bev_tune(int knob, int value) {
         const int old = g_conv_tile;
         g_conv_tile = value;
         return old;
+    }
+    if (knob == BEV_TUNE_WARP_POOL_KB) {
+        if (value < 0 || value > 150) return BEV_ERR_ARGS;
+        return bev::warp_fuse_set_pool_kb(value);
+    }
+    if (knob == BEV_TUNE_WARP_UNITS) {
+        if (value < 0 || value > 1) return BEV_ERR_ARGS;
+        return bev::warp_fuse_set_units(value);
     }
     return BEV_ERR_ARGS;
 }

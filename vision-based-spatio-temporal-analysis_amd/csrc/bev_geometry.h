@@ -56,8 +56,10 @@ struct Taps {
     unsigned valid;   // bit0 nw, bit1 ne, bit2 sw, bit3 se
 };
 
+// Unnormalised sampling coordinates (ix, iy) of one BEV cell in one feature map.
 // h[9] = world->image homography, (x, y) = BEV cell centre on the ground plane.
-__device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, const Grid &g, float sx, float sy) {
+__device__ __forceinline__ void cell_ixy(const float h[9], float x, float y, const Grid &g, float sx, float sy,
+                                         float &ix, float &iy) {
     // geometry.py:144-149
     const float u0 = dot3(h[0], h[1], h[2], x, y, 1.0f);
     const float u1 = dot3(h[3], h[4], h[5], x, y, 1.0f);
@@ -68,12 +70,27 @@ __device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, co
     // geometry.py:151-158
     const float fx = u * sx;
     const float fy = v * sy;
-    const float fWf = g.fWf, fHf = g.fHf;
     const float gx = div_rcp(fx + 0.5f, g.rWf) * 2.0f - 1.0f;  // ((fx + 0.5) / Wf) * 2 - 1
     const float gy = div_rcp(fy + 0.5f, g.rHf) * 2.0f - 1.0f;
     // grid_sampler_2d (align_corners=False): ix = (gx + 1) * Wf/2 - 0.5 as one FMA
-    const float ix = __builtin_fmaf(gx + 1.0f, fWf / 2.0f, -0.5f);
-    const float iy = __builtin_fmaf(gy + 1.0f, fHf / 2.0f, -0.5f);
+    ix = __builtin_fmaf(gx + 1.0f, g.fWf / 2.0f, -0.5f);
+    iy = __builtin_fmaf(gy + 1.0f, g.fHf / 2.0f, -0.5f);
+}
+
+// Validity bits of the four taps at (ix, iy): bit0 nw, bit1 ne, bit2 sw, bit3 se.
+// Decided in float (immune to int overflow for |ix| >> 2^31; NaN -> invalid).
+__device__ __forceinline__ unsigned ixy_valid(float ix, float iy, const Grid &g) {
+    const float xw = __builtin_floorf(ix), yn = __builtin_floorf(iy);
+    const bool vx0 = (xw >= 0.0f) & (xw < g.fWf);
+    const bool vx1 = (xw + 1.0f >= 0.0f) & (xw + 1.0f < g.fWf);
+    const bool vy0 = (yn >= 0.0f) & (yn < g.fHf);
+    const bool vy1 = (yn + 1.0f >= 0.0f) & (yn + 1.0f < g.fHf);
+    return (unsigned)(vx0 & vy0) | ((unsigned)(vx1 & vy0) << 1) | ((unsigned)(vx0 & vy1) << 2) |
+           ((unsigned)(vx1 & vy1) << 3);
+}
+
+// grid_sampler_2d bilinear taps at (ix, iy) (geometry.py:161).
+__device__ __forceinline__ Taps taps_from_ixy(float ix, float iy, const Grid &g) {
     const float xw = __builtin_floorf(ix);
     const float yn = __builtin_floorf(iy);
     const float we = ix - xw, e = 1.0f - we;
@@ -83,16 +100,21 @@ __device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, co
     t.w[1] = s * we;
     t.w[2] = n * e;
     t.w[3] = n * we;
-    // validity decided in float (immune to int overflow for |ix| >> 2^31)
-    const bool vx0 = (xw >= 0.0f) & (xw < fWf);
-    const bool vx1 = (xw + 1.0f >= 0.0f) & (xw + 1.0f < fWf);
-    const bool vy0 = (yn >= 0.0f) & (yn < fHf);
-    const bool vy1 = (yn + 1.0f >= 0.0f) & (yn + 1.0f < fHf);
+    const bool vx0 = (xw >= 0.0f) & (xw < g.fWf);
+    const bool vx1 = (xw + 1.0f >= 0.0f) & (xw + 1.0f < g.fWf);
+    const bool vy0 = (yn >= 0.0f) & (yn < g.fHf);
+    const bool vy1 = (yn + 1.0f >= 0.0f) & (yn + 1.0f < g.fHf);
     t.valid = (unsigned)(vx0 & vy0) | ((unsigned)(vx1 & vy0) << 1) | ((unsigned)(vx0 & vy1) << 2) |
               ((unsigned)(vx1 & vy1) << 3);
     t.x0 = (vx0 | vx1) ? (int)xw : 0;
     t.y0 = (vy0 | vy1) ? (int)yn : 0;
     return t;
+}
+
+__device__ __forceinline__ Taps cell_taps(const float h[9], float x, float y, const Grid &g, float sx, float sy) {
+    float ix, iy;
+    cell_ixy(h, x, y, g, sx, sy, ix, iy);
+    return taps_from_ixy(ix, iy, g);
 }
 
 // grid_sampler_2d bilinear combine: ((nw*wnw + ne*wne) + sw*wsw) + se*wse,

@@ -28,6 +28,7 @@
 #include <stdlib.h>
 
 #include "bev_geometry.h"
+#include "bev_warp_fuse.h"
 #include "../../include/bev_mi355x.h"
 
 using namespace bev;
@@ -1534,6 +1535,11 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
                         (sH % 4 == 0) && (sN % 4 == 0) &&
                         (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32) &&  // store_chunk descriptor
                         getenv("BEV_WARP_NO_DMA") == nullptr;
+    static const bool legacy = getenv("BEV_WARP_V2") != nullptr || getenv("BEV_WARP_V1") != nullptr ||
+                               getenv("BEV_WARP_WAVE") != nullptr;
+    if (!legacy && warp_fuse_units_enabled() && getenv("BEV_WARP_NO_DMA") == nullptr &&
+        warp_fuse_units_ok(sN, sC, sH, sW, feats, C, Hf, Wf, Hb, Wb))
+        return warp_fuse_units(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (dma_ok && getenv("BEV_WARP_WAVE") != nullptr)
         return launch_fuse_wave(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (dma_ok && V <= V2_MAXV && getenv("BEV_WARP_V1") == nullptr)
