@@ -21,6 +21,7 @@ a bounded sample).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -134,6 +135,22 @@ def cpu_baseline(enc, args, K, Rt):
                       "torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
 
 
+def pmc_traffic(args) -> dict:
+    """HBM bytes from the committed rocprofv3 PMC passes of this same command (tools/pmc_traffic.py):
+    conv = bytes per step over all backbone conv launches, warp = bytes per fused-warp launch.
+    Only reported for the default workload those passes ran; {} otherwise."""
+    default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone) == \
+        (7, 64, (1080, 1920), (480, 1440), 1, "resnet50")
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "r*_pmc_traffic.json")))
+    if not default or not files:
+        return {}
+    d = json.load(open(files[-1]))
+    res = {k: d[k]["traffic_bytes"] for k in ("conv", "warp") if k in d}
+    res["source"] = f"profiles/{os.path.basename(files[-1])}: {d.get('note', '')}"
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,6 +244,7 @@ def main():
     value = frames / elapsed
 
     if rank == 0:
+        pmc = pmc_traffic(args)
         flops = backbone_flops(enc, H, W) * V * B
         Hm = geom.homographies(Kd, Rtd, B, V, dev)
         alg, out_b, touched = warp_alg_bytes(geom, Hm, feats.shape, (H, W), B, V)
@@ -234,11 +252,11 @@ def main():
             "kernel": "k_conv (fp32 MFMA implicit GEMM, every backbone conv launch of one step)",
             "bound": "mfma", "achieved": round(flops / (conv_ms * 1e-3) / 1e12, 3), "peak": PEAK_F32_MFMA_TF,
             "unit": "TFLOP/s", "frac": round(flops / (conv_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TF, 4),
-            "traffic": None, "flops_per_step": flops, "conv_ms_per_step": round(conv_ms, 4),
+            "traffic": pmc.get("conv"), "flops_per_step": flops, "conv_ms_per_step": round(conv_ms, 4),
             "encoder_stage_ms": round(bb_ms, 4)}
         ach = alg / (wp_ms * 1e-3) / 1e9
         roof_wp = {"kernel": "k_warp_fuse (IPM warp + mean, fused)", "bound": "hbm", "achieved": round(ach, 1),
-                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc.get("warp"),
                    "alg_bytes_per_launch": alg, "out_bytes": out_b, "touched_src_pixels": touched,
                    "avg_us": round(wp_ms * 1e3, 2), "geometry_stage_us": round(stage_wp_ms * 1e3, 2)}
         line = {
@@ -253,6 +271,8 @@ def main():
             "roofline": roof_bb if roof_bb else roof_wp,
             "roofline_warp": roof_wp,
         }
+        if pmc:
+            line["traffic_source"] = pmc["source"]
         if h2d:
             line["h2d_inclusive"] = h2d
         if args.warp_only:

@@ -1,0 +1,57 @@
+"""Per-launch HBM traffic of the bench's dominant kernels from rocprofv3 --pmc passes.
+
+Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [--steps-key k_stem]
+
+Inputs are the run_counter_collection.csv files of two separate passes
+(`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE`) over the same `bench.py` command.
+Corrections (MI355X_MICROARCH.md, HBM section): counters are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so it
+is doubled.  WRITE_SIZE is exact for 16-B/lane stores; the warp's 4-B/lane
+stores are uncalibrated (noted in the output).
+The conv figure is per bench step (all backbone conv launches of one frame,
+steps counted by the stem launches); the warp figure is per launch.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+
+def family(name: str) -> str:
+    if "k_conv" in name or "k_stem" in name:
+        return "conv"
+    if "warp_fuse" in name:
+        return "warp"
+    return "other"
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    tot = defaultdict(float)
+    n = defaultdict(int)
+    steps = 0
+    for cnt, d in (("FETCH_SIZE", fdir), ("WRITE_SIZE", wdir)):
+        for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+            if r["Counter_Name"] != cnt:
+                continue
+            fam = family(r["Kernel_Name"])
+            tot[(fam, cnt)] += float(r["Counter_Value"]) * 1024.0
+            if cnt == "FETCH_SIZE":
+                n[fam] += 1
+                steps += "k_stem" in r["Kernel_Name"]
+    res = {}
+    for fam, per in (("conv", steps), ("warp", n["warp"])):
+        if per == 0:
+            continue
+        fetch = 2.0 * tot[(fam, "FETCH_SIZE")] / per
+        write = tot[(fam, "WRITE_SIZE")] / per
+        res[fam] = {"fetch_bytes": round(fetch), "write_bytes": round(write), "traffic_bytes": round(fetch + write),
+                    "per": "bench step" if fam == "conv" else "launch", "samples": per}
+    res["note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950 wide-read "
+                   "correction), KiB -> bytes; warp stores are 4 B/lane (WRITE_SIZE uncalibrated for that width)")
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
