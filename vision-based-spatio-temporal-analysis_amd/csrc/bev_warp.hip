@@ -383,11 +383,12 @@ __device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
 // Issue the DMA of footprint block (sx0, sy0, sbw x sbh) into LDS byte offset `off`.
 // Element offsets are 32-bit (the launcher checks that a feature map fits).
 __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
-                                          int npix, unsigned char *smem, int off, int wave, int lane) {
+                                          int npix, unsigned char *smem, int off, int wave, int lane,
+                                          int nwaves = FT_NT / 64) {
     const int ninstr = (npix * 17 + 63) >> 6;
     const float inv_bw = 1.0f / (float)sbw;
     const int base = sy0 * sH + sx0 * sW;
-    for (int k = wave; k < ninstr; k += FT_NT / 64) {
+    for (int k = wave; k < ninstr; k += nwaves) {
         const int slot = k * 64 + lane;
         const int p = slot / 17, sl = slot - p * 17;
         const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
@@ -505,23 +506,25 @@ __device__ __forceinline__ Box wave_box(const Taps &t) {
     return b;
 }
 
+template <int NW = 4>
 __device__ __forceinline__ void put_box(int *rp, const Box &b, int wave, int lane) {
     if (lane == 0) {
         rp[wave] = b.x0;
-        rp[4 + wave] = b.y0;
-        rp[8 + wave] = b.x1;
-        rp[12 + wave] = b.y1;
+        rp[NW + wave] = b.y0;
+        rp[2 * NW + wave] = b.x1;
+        rp[3 * NW + wave] = b.y1;
     }
 }
 
+template <int NW = 4>
 __device__ __forceinline__ Box get_box(const int *rp) {
-    Box b{rp[0], rp[4], rp[8], rp[12]};
+    Box b{rp[0], rp[NW], rp[2 * NW], rp[3 * NW]};
 #pragma unroll
-    for (int w = 1; w < 4; ++w) {
+    for (int w = 1; w < NW; ++w) {
         b.x0 = min(b.x0, rp[w]);
-        b.y0 = min(b.y0, rp[4 + w]);
-        b.x1 = max(b.x1, rp[8 + w]);
-        b.y1 = max(b.y1, rp[12 + w]);
+        b.y0 = min(b.y0, rp[NW + w]);
+        b.x1 = max(b.x1, rp[2 * NW + w]);
+        b.y1 = max(b.y1, rp[3 * NW + w]);
     }
     b.x0 = __builtin_amdgcn_readfirstlane(b.x0);
     b.y0 = __builtin_amdgcn_readfirstlane(b.y0);
@@ -850,8 +853,8 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t
     }
 }
 
-template <int MODE, int OCC, bool WIDE>
-__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
+template <int MODE, int OCC, bool WIDE, int TH>
+__global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                            int64_t sW, const float *__restrict__ Hmat,
                                                            const float *__restrict__ xs,
                                                            const float *__restrict__ ys, int V, int C, int Hf,
@@ -860,14 +863,19 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     // dbg: profiling-only ablations (BEV_WARP_DEBUG; results are WRONG when set):
     //   1 skip views that need synchronous staging, 2 skip LDS sampling, 4 skip stores, 8 skip DMA
     // WIDE: widened float4 stores through LDS (store_chunk_wide); the launcher checks its conditions
-    constexpr bool wide = WIDE;
+    constexpr bool wide = WIDE && TH == TH;
+    constexpr int NT = TH * FT_W, NW = NT / 64;  // TH / 2 waves, each two rows of 32 cells
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int zp = pool;                                    // zero pixel (256 B)
-    int *red = reinterpret_cast<int *>(smem + pool + 256);  // [16] exact-bbox exchange
-    float *htab = reinterpret_cast<float *>(smem + pool + 256 + 16 * sizeof(int));  // [V][9] homographies
+    int *red = reinterpret_cast<int *>(smem + pool + 256);  // [4 * NW] exact-bbox exchange
+    float *htab = reinterpret_cast<float *>(smem + pool + 256 + 4 * NW * sizeof(int));  // [V][9] homographies
     const int maxpix = pool / DPS - 4;                      // ~1 KiB DMA rounding slack
+    // dbg & 64: per-wave phase stamps (s_memtime) into out (tools/warp_phases_v2.py)
+    const bool stamp = (dbg & 64) != 0;
+    long long T0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0, T1 = 0, T2 = 0, T3 = 0;
+    long long ph_sync = 0, ph_dma = 0, ph_samp = 0, ph_wait = 0;
 
-    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, nt = ntx * nty;
+    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
     int tile = blockIdx.x;
     {
         const int q = nt / 8, r = nt % 8, x = tile % 8;
@@ -875,7 +883,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     }
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int i = tyb * FT_H + wave * 2 + (lane >> 5);
+    const int i = tyb * TH + wave * 2 + (lane >> 5);
     const int j = txb * FT_W + (lane & 31);
     const int b = blockIdx.y;
     const bool inside = (i < Hb) && (j < Wb);
@@ -889,7 +897,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     // lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16  (x1 + 1 == 0: empty)
     unsigned lba, lbb;
     {
-        const int ia = tyb * FT_H, ib = min(ia + FT_H - 1, Hb - 1);
+        const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
         const int ja = txb * FT_W, jb = min(ja + FT_W - 1, Wb - 1);
         Box cb{0x7fffffff, 0x7fffffff, -1, -1};
         bool ok = true;
@@ -916,6 +924,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     };
     auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
 
+    if (stamp) T1 = (long long)__builtin_amdgcn_s_memtime();
     float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
     auto taps_of = [&](int v) {
         float h[9];
@@ -942,13 +951,15 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
             if (ok_of(0) && bn.x1 >= 0 && npix <= maxpix) {
                 offn = 0;
-                dma_block(fb, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, 0, wave, lane);
+                dma_block(fb, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, 0, wave, lane, NW);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // zero pixel + image of view 0
+        if (stamp) T2 = (long long)__builtin_amdgcn_s_memtime();
 
         for (int v = 0; v < V; ++v) {
+            long long ta = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             Box bx = bn;
             const int off = offn;
             const float *f = fb + (int64_t)v * sN;
@@ -958,9 +969,9 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 // exact footprint by per-cell reduction (horizon tiles); staged synchronously
                 t = taps_of(v);
                 have_t = true;
-                put_box(red, wave_box(t), wave, lane);
+                put_box<NW>(red, wave_box(t), wave, lane);
                 __syncthreads();
-                bx = get_box(red);
+                bx = get_box<NW>(red);
             }
             const bool empty = bx.x1 < 0;
             const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
@@ -977,7 +988,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 const bool single = (nbx == 1) && (nby == 1);
                 if (single)  // the common case: start the copy (the pool is free since the last
                              // end-of-view barrier), compute the taps while it lands
-                    dma_block(f, (int)sH, (int)sW, bx.x0, bx.y0, bw, bw * bh, smem, 0, wave, lane);
+                    dma_block(f, (int)sH, (int)sW, bx.x0, bx.y0, bw, bw * bh, smem, 0, wave, lane, NW);
                 if (!have_t) {
                     t = taps_of(v);
                     have_t = true;
@@ -996,7 +1007,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
                         if (!single) {
                             __syncthreads();  // earlier LDS images are no longer read
-                            dma_block(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane);
+                            dma_block(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane, NW);
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
@@ -1008,6 +1019,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 done = true;
                 __syncthreads();  // every wave is done with the staged blocks before DMA(v+1) reuses the pool
             }
+            long long tb = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             // ---- look ahead: DMA of view v+1 beside the live image of view v ----------
             if (v + 1 < V) {
                 bn = box_of(v + 1);
@@ -1023,9 +1035,10 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                     } else if (need <= off) offn = 0;
                     if (offn >= 0 && !(dbg & 8))
                         dma_block(f + sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, offn, wave,
-                                  lane);
+                                  lane, NW);
                 }
             }
+            long long tc = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             // ---- sample view v from its prefetched image ------------------------------
             if (!done) {
                 if (!have_t) t = taps_of(v);
@@ -1037,12 +1050,21 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             } else if (empty) {
                 zero_view<MODE>(acc, v);
             }
+            long long td = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
             __syncthreads();  // all of it landed; image of view v and red[] are free
+            if (stamp) {
+                const long long te = (long long)__builtin_amdgcn_s_memtime();
+                ph_sync += tb - ta;
+                ph_dma += tc - tb;
+                ph_samp += td - tc;
+                ph_wait += te - td;
+            }
         }
+        if (stamp) T3 = (long long)__builtin_amdgcn_s_memtime();
         if (wide) {
             if (!(dbg & 4))
-                store_chunk_wide(out + ((size_t)b * C + c0) * plane, plane, Hb, Wb, tyb * FT_H, txb * FT_W,
+                store_chunk_wide(out + ((size_t)b * C + c0) * plane, plane, Hb, Wb, tyb * TH, txb * FT_W,
                                  reinterpret_cast<float *>(smem), tid, acc, MODE, rV);
         } else if (inside && !(dbg & 4)) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
         if (dbg & 4) {
@@ -1050,6 +1072,22 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             for (int q = 0; q < 64; ++q) z += acc[q];
             if (z == 12345.f) out[0] = z;  // keep acc live
         }
+    }
+    if (stamp && lane == 0) {
+        const long long T4 = (long long)__builtin_amdgcn_s_memtime();
+        int *rec = reinterpret_cast<int *>(out) + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) * 12;
+        rec[0] = (int)(T1 - T0);
+        rec[1] = (int)(T2 - T1);
+        rec[2] = (int)ph_sync;
+        rec[3] = (int)ph_dma;
+        rec[4] = (int)ph_samp;
+        rec[5] = (int)ph_wait;
+        rec[6] = (int)(T4 - T3);
+        rec[7] = (int)(T4 - T0);
+        rec[8] = (int)(T0 & 0x7fffffff);
+        rec[9] = (int)(T4 & 0x7fffffff);
+        rec[10] = tile;
+        rec[11] = 0;
     }
 }
 
@@ -1403,21 +1441,21 @@ inline int warp_debug() {
     return v;
 }
 
-template <int OCC, bool WIDE>
+template <int OCC, bool WIDE, int TH = FT_H>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
                        int mode, float *out, hipStream_t st, int pool) {
-    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
-    dim3 grid(ntiles, B), block(FT_NT);
-    const size_t lds = pool + 256 + 16 * sizeof(int) + V2_MAXV * 9 * sizeof(float);
+    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + TH - 1) / TH);
+    dim3 grid(ntiles, B), block(TH * FT_W);
+    const size_t lds = pool + 256 + 4 * (TH / 2) * sizeof(int) + V2_MAXV * 9 * sizeof(float);
     if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, WIDE>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, WIDE, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
                            xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
     else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, WIDE>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, WIDE, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
                            xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
     else
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, WIDE>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, WIDE, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
                            xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
     return last();
 }
@@ -1438,6 +1476,18 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                           int Hb, int Wb, int mode, float *out, hipStream_t st) {
     const char *e = getenv("BEV_WARP_POOL_KB");
+    static const int th = [] {
+        const char *t = getenv("BEV_WARP_TH");
+        return t ? atoi(t) : 8;
+    }();
+    if (th == 16 || th == 32) {  // one workgroup per CU: 8 (16) waves on a 16 (32) x 32 tile
+        const int pool = e ? warp_pool_bytes() : 140 * 1024;
+        if (th == 16)
+            return launch_fuse_v2_occ<1, false, 16>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
+                                                    mode, out, st, pool);
+        return launch_fuse_v2_occ<1, false, 32>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
+                                                mode, out, st, pool);
+    }
     if (warp_occ() == 2 || mode == BEV_FUSE_MAX) {  // MAX's extra live state spills at 128 VGPRs
         const int pool = e ? warp_pool_bytes() : 72 * 1024;
         return launch_fuse_v2_pick<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
