@@ -67,8 +67,23 @@ def backbone_flops(enc, H, W):
     def conv(c: nn.Conv2d, h, w):
         ho = (h + 2 * c.padding[0] - c.kernel_size[0]) // c.stride[0] + 1
         wo = (w + 2 * c.padding[1] - c.kernel_size[1]) // c.stride[1] + 1
-        return 2 * ho * wo * c.out_channels * c.in_channels * c.kernel_size[0] * c.kernel_size[1], ho, wo
+        return (2 * ho * wo * c.out_channels * (c.in_channels // c.groups) * c.kernel_size[0] * c.kernel_size[1],
+                ho, wo)
 
+    if enc._use_timm and hasattr(net, "conv_stem"):  # EfficientNet: stem, (pw,) dw, SE FCs, pw(l)
+        from models.encoders.efficientnet import FEATURE_STAGE, DepthwiseSeparableConv
+        f, h, w = conv(net.conv_stem, H, W)
+        total += f
+        for si in range(FEATURE_STAGE[enc.out_index] + 1):
+            for blk in net.blocks[si]:
+                if not isinstance(blk, DepthwiseSeparableConv):
+                    total += conv(blk.conv_pw, h, w)[0]
+                f, h, w = conv(blk.conv_dw, h, w)
+                total += f
+                total += 2 * (blk.se.conv_reduce.in_channels * blk.se.conv_reduce.out_channels) * 2
+                last = blk.conv_pw if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pwl
+                total += conv(last, h, w)[0]
+        return total + 2 * h * w * enc.proj.in_channels * enc.proj.out_channels
     if not enc._use_timm:
         f0, h, w = conv(net[0], H, W)
         f1, h, w = conv(net[2], h, w)
@@ -238,7 +253,8 @@ def main():
 
     bb_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))  # encoder stage (convs + pool + layout)
     stage_wp_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))  # geometry stage (homography + warp)
-    conv_ms = float(np.sum(spans.get("conv", [0.0]))) / args.steps  # conv kernels only, per step
+    # conv kernels only, per step (EfficientNet: + its depthwise convs, which the FLOP count includes)
+    conv_ms = float(np.sum(spans.get("conv", [0.0])) + np.sum(spans.get("dwconv", [0.0]))) / args.steps
     wp_ms = float(np.mean(spans["warp_fuse"]))  # the fused warp kernel only
     frames = world * B * args.steps
     value = frames / elapsed
@@ -264,7 +280,7 @@ def main():
             "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{V}-cam {H}x{W} -> {args.backbone}(layer2)+proj C={C} -> IPM warp -> mean "
+            "config": {"workload": f"{V}-cam {H}x{W} -> {args.backbone}(stride-8 features)+proj C={C} -> IPM warp -> mean "
                                    f"-> {args.bev[0]}x{args.bev[1]} BEV (BASELINE configs[1])",
                        "frames_per_gpu_per_step": B, "cameras": V, "bev": list(args.bev), "channels": C,
                        "parallelism": f"frame-sharded x{world} (no collective)"},

@@ -122,7 +122,8 @@ int bev_view_fuse_f32(const float *x, int B, int V, int64_t M, int mode, float *
  * Activations are channels-last (NHWC) fp32.  Weights are packed by
  * bev_conv_pack_weights_f32 into a [Co padded to 128][K padded to 32] panel,
  * K index k = (ky*KW + kx)*Ci + ci (the implicit-GEMM reduction order).
- * y = act( conv(x, w) + bias (+ residual) ),  act = ReLU if relu != 0.
+ * y = act( conv(x, w) + bias (+ residual) ),  act by `relu`: 0 none, 1 ReLU,
+ * 2 SiLU (x / (1 + exp(-x)); the EfficientNet trunk's pointwise convs).
  * Batch-norm (eval) is folded into (w, bias) by the host.
  * x may instead be NCHW (in_nchw = 1): the stem reads the caller's images
  * [B*V,3,H,W] directly (cnn_encoder.py:66-67 view).
@@ -160,6 +161,35 @@ int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, in
 /* device: layout conversions between NCHW and NHWC. */
 int bev_nchw_to_nhwc_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
 int bev_nhwc_to_nchw_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * EfficientNet trunk (timm efficientnet_b3 features_only, cnn_encoder.py:26,
+ * feature index out_index = 2): the layers that are not GEMMs.  All NHWC fp32,
+ * C % 4 == 0, 16-B aligned pointers.
+ * ------------------------------------------------------------------------- */
+
+/* Number of per-workgroup SE partial sums per image that bev_dwconv2d_f32
+ * writes for an Ho x Wo output (psum is [N][nb][C]). */
+int bev_dwconv_psum_blocks(int Ho, int Wo);
+
+/* device: depthwise KxK conv (K = 3 or 5; torch groups = C), BN folded:
+ *   y[n,oy,ox,c] = act( sum_{ky,kx} x[n, oy*s-pad+ky, ox*s-pad+kx, c] * wt[ky*K+kx][c] + bias[c] )
+ * (timm conv_dw -> bn -> SiLU, _efficientnet_blocks.py InvertedResidual /
+ * DepthwiseSeparableConv).  wt is tap-major [K*K][C].  act as bev_conv2d_f32.
+ * If psum != NULL, also writes the channel sums of y per workgroup
+ * (deterministic partials, [N][bev_dwconv_psum_blocks(Ho,Wo)][C]) -- the
+ * squeeze of the block's SqueezeExcite. */
+int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
+                     int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);
+
+/* device: SqueezeExcite gate from the dwconv partials (timm SqueezeExcite.forward):
+ *   mean = sum(psum[n]) / hw;  r = SiLU(w1 @ mean + b1);  gate[n] = sigmoid(w2 @ r + b2)
+ * w1 = conv_reduce.weight [rd][C], w2 = conv_expand.weight [C][rd]. */
+int bev_se_gate_f32(const float *psum, int N, int nb, int C, int hw, const float *w1, const float *b1, int rd,
+                    const float *w2, const float *b2, float *gate, void *stream);
+
+/* device: in place y[n, p, c] *= gate[n, c] for y [N][P][C] (SE excitation, x * gate). */
+int bev_channel_scale_f32(float *y, int N, int64_t P, int C, const float *gate, void *stream);
 
 #ifdef __cplusplus
 }

@@ -47,13 +47,51 @@ def resnet_features(net, x, out_index: int):
         return y
 
 
+def _bn(y, bn):
+    return F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+
+
+def _se(y, se):
+    s = y.mean((2, 3), keepdim=True)
+    s = F.silu(F.conv2d(s, se.conv_reduce.weight, se.conv_reduce.bias))
+    s = F.conv2d(s, se.conv_expand.weight, se.conv_expand.bias)
+    return y * torch.sigmoid(s)
+
+
+def _dw(y, conv):
+    return F.conv2d(y, conv.weight, None, conv.stride, conv.padding, groups=conv.groups)
+
+
+def efficientnet_features(net, x, out_index: int):
+    """features_only[out_index] of a timm-named EfficientNet `net` (timm DepthwiseSeparableConv /
+    InvertedResidual / SqueezeExcite forward, _efficientnet_blocks.py) on NCHW x."""
+    from models.encoders.efficientnet import FEATURE_STAGE, DepthwiseSeparableConv
+    with torch.no_grad():
+        y = F.silu(_bn(F.conv2d(x, net.conv_stem.weight, None, 2, 1), net.bn1))
+        for si in range(FEATURE_STAGE[out_index] + 1):
+            for blk in net.blocks[si]:
+                sc = y
+                if isinstance(blk, DepthwiseSeparableConv):
+                    z = _se(F.silu(_bn(_dw(y, blk.conv_dw), blk.bn1)), blk.se)
+                    z = _bn(F.conv2d(z, blk.conv_pw.weight), blk.bn2)
+                else:
+                    z = F.silu(_bn(F.conv2d(y, blk.conv_pw.weight), blk.bn1))
+                    z = _se(F.silu(_bn(_dw(z, blk.conv_dw), blk.bn2)), blk.se)
+                    z = _bn(F.conv2d(z, blk.conv_pwl.weight), blk.bn3)
+                y = z + sc if blk.has_skip else z
+        return y
+
+
 def encoder_forward(enc, images):
     """CNNEncoder.forward restated on torch CPU ops: [B,V,3,H,W] -> [B,V,C,Hf,Wf] (contiguous)."""
     B, V = images.shape[:2]
     x = images.reshape(B * V, *images.shape[2:])
     with torch.no_grad():
         if enc._use_timm:
-            f = resnet_features(enc.backbone, x, enc.out_index)
+            if hasattr(enc.backbone, "conv_stem"):
+                f = efficientnet_features(enc.backbone, x, enc.out_index)
+            else:
+                f = resnet_features(enc.backbone, x, enc.out_index)
             y = F.conv2d(f, enc.proj.weight, enc.proj.bias)
         else:
             s = enc.backbone

@@ -1,0 +1,126 @@
+"""EfficientNet-B3 trunk (BASELINE config 4 backbone): module layout on the CPU, kernels on the GPU.
+
+The module restates timm's efficientnet_b3 `features_only` trunk
+(cnn_encoder.py:26); timm is absent offline, so parity with timm itself is
+UNPINNED -- the layout test checks the published structure (block counts,
+channel widths, SE widths, feature channels) and the GPU tests compare the
+HIP kernels with torch fp32 CPU ops on the same weights (floating point:
+tolerance stated per test, accumulation order differs).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+DEV = "cuda:0"
+
+
+def _rand(shape, seed, scale=1.0):
+    return torch.from_numpy(np.random.default_rng(seed).standard_normal(size=shape, dtype=np.float32) * scale)
+
+
+def _perturb_bn(module):
+    g = torch.Generator().manual_seed(3)
+    for m in module.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            n = m.num_features
+            m.running_mean.copy_(torch.rand(n, generator=g) * 0.4 - 0.2)
+            m.running_var.copy_(torch.rand(n, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(n, generator=g) + 0.5)
+            m.bias.data.copy_(torch.rand(n, generator=g) * 0.4 - 0.2)
+
+
+def test_effnet_b3_layout():
+    """Published efficientnet_b3 structure: stem 40, stages [2,3,3,5,5,6,2] blocks, widths
+    [24,32,48,96,136,232,384], SE rd = block input / 4, features_only channels [24,32,48,136,384]."""
+    from models.encoders.efficientnet import efficientnet_b3
+    m = efficientnet_b3()
+    sd = m.state_dict()
+    assert sd["conv_stem.weight"].shape == (40, 3, 3, 3)
+    assert [len(s) for s in m.blocks] == [2, 3, 3, 5, 5, 6, 2]
+    widths = [s[-1].bn2.num_features if i == 0 else s[-1].bn3.num_features for i, s in enumerate(m.blocks)]
+    assert widths == [24, 32, 48, 96, 136, 232, 384]
+    assert m.feature_channels == [24, 32, 48, 136, 384]
+    assert sd["blocks.0.0.se.conv_reduce.weight"].shape == (10, 40, 1, 1)
+    assert sd["blocks.1.0.conv_pw.weight"].shape == (144, 24, 1, 1)
+    assert sd["blocks.1.0.se.conv_reduce.weight"].shape == (6, 144, 1, 1)
+    assert sd["blocks.2.0.conv_dw.weight"].shape == (192, 1, 5, 5)
+    assert sd["blocks.2.1.se.conv_expand.weight"].shape == (288, 12, 1, 1)
+    assert sd["blocks.6.1.conv_pwl.weight"].shape == (384, 2304, 1, 1)
+    n = sum(p.numel() for p in m.parameters())
+    assert 10.0e6 < n < 10.2e6, n  # timm efficientnet_b3 (12.23 M) minus conv_head / bn2 / classifier
+
+
+def test_effnet_encoder_selected():
+    from models.encoders.cnn_encoder import CNNEncoder
+    enc = CNNEncoder(out_channels=16, backbone="efficientnet_b3", pretrained=False)
+    assert enc._use_timm and hasattr(enc.backbone, "conv_stem")
+
+
+DW_CASES = [  # N, C, H, W, K, stride, act
+    (2, 40, 19, 33, 3, 1, 2),
+    (1, 144, 21, 30, 3, 2, 2),
+    (1, 192, 17, 26, 5, 2, 2),
+    (2, 288, 9, 14, 5, 1, 0),
+    (1, 1392, 6, 7, 3, 1, 2),  # > 1024 channels: channel chunks (blockIdx.z)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", DW_CASES, ids=[f"c{c[1]}_k{c[4]}s{c[5]}" for c in DW_CASES])
+def test_dwconv_and_se_vs_torch_fp32(case):
+    import bev_native as nat
+    N, C, H, W, K, s, act = case
+    x = _rand((N, C, H, W), 1)
+    w = _rand((C, 1, K, K), 2, 0.3)
+    b = _rand((C,), 3, 0.1)
+    ref = F.conv2d(x, w, b, s, K // 2, groups=C)
+    ref = F.silu(ref) if act == 2 else ref
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    wt = w.reshape(C, K * K).t().contiguous().to(DEV)
+    y, ps = nat.dwconv2d_nhwc(xd, wt, b.to(DEV), K, s, K // 2, act, want_psum=True)
+    got = y.permute(0, 3, 1, 2).cpu()
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-5, atol=1e-5)
+    # SE: squeeze from the fused partials, excite in place
+    rd = max(1, C // 24)
+    w1, b1 = _rand((rd, C), 4, 0.2), _rand((rd,), 5, 0.1)
+    w2, b2 = _rand((C, rd), 6, 0.2), _rand((C,), 7, 0.1)
+    m = ref.mean((2, 3))
+    g_ref = torch.sigmoid(F.silu(m @ w1.t() + b1) @ w2.t() + b2)
+    gate = nat.se_gate(ps, y.shape[1] * y.shape[2], w1.to(DEV), b1.to(DEV), w2.to(DEV), b2.to(DEV))
+    np.testing.assert_allclose(gate.cpu().numpy(), g_ref.numpy(), rtol=1e-5, atol=1e-6)
+    nat.channel_scale_(y, gate)
+    exc = (ref * g_ref[:, :, None, None]).numpy()
+    np.testing.assert_allclose(y.permute(0, 3, 1, 2).cpu().numpy(), exc, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_conv_silu_epilogue():
+    import bev_native as nat
+    from models.encoders.resnet import FoldedConv
+    conv = torch.nn.Conv2d(24, 144, 1, bias=False)
+    x = _rand((2, 24, 11, 13), 8)
+    fc = FoldedConv(conv.to(DEV))
+    y = fc(x.permute(0, 2, 3, 1).contiguous().to(DEV), relu=nat.ACT_SILU)
+    ref = F.silu(F.conv2d(x, conv.weight.detach().cpu()))
+    np.testing.assert_allclose(y.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("out_index", [0, 2, 3])
+def test_effnet_encoder_vs_torch_fp32(out_index):
+    """Native EfficientNet-B3 trunk to features_only[out_index] + proj vs torch fp32 CPU ops, same weights."""
+    from models.encoders.cnn_encoder import CNNEncoder
+    import backbone_ref
+    torch.manual_seed(0)
+    enc = CNNEncoder(out_channels=32, backbone="efficientnet_b3", pretrained=False, out_index=out_index)
+    _perturb_bn(enc)
+    enc.eval()
+    imgs = _rand((1, 3, 3, 96, 160), 9)
+    with torch.no_grad():
+        y = enc.to(DEV)(imgs.to(DEV)).cpu()
+        ref = backbone_ref.encoder_forward(enc.to("cpu"), imgs)
+    stride = {0: 2, 2: 8, 3: 16}[out_index]
+    assert tuple(y.shape) == tuple(ref.shape) == (1, 3, 32, 96 // stride, 160 // stride)
+    err = (y - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-4, err

@@ -49,6 +49,10 @@ SIGNATURES = {
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+    "bev_dwconv_psum_blocks": (_i, [_i, _i]),
+    "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
+    "bev_se_gate_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
+    "bev_channel_scale_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp]),
 }
 
 
@@ -291,6 +295,53 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
                                   KH, KW, stride, pad, int(relu), _ptr(out), Ho, Wo, _stream(x))
     _check(rc, "bev_conv2d_f32")
     return out
+
+
+ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2  # `relu` argument of conv2d_nhwc / dwconv2d_nhwc
+
+
+def dwconv2d_nhwc(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, K: int, stride: int, pad: int, act: int,
+                  want_psum: bool = False):
+    """Depthwise KxK conv, NHWC: x [N,H,W,C], wt [K*K, C] (tap-major, BN folded), bias [C].
+    Returns y [N,Ho,Wo,C] and, with want_psum, the SE partial channel sums [N, nb, C]."""
+    x = x.contiguous()
+    _require_gpu(x, wt, bias)
+    N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * pad - K) // stride + 1, (W + 2 * pad - K) // stride + 1
+    y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.float32)
+    psum = None
+    if want_psum:
+        nb = lib().bev_dwconv_psum_blocks(Ho, Wo)
+        _check(0 if nb > 0 else nb, "bev_dwconv_psum_blocks")
+        psum = torch.empty(N, nb, C, device=x.device, dtype=torch.float32)
+    with _span("dwconv", x):
+        rc = lib().bev_dwconv2d_f32(_ptr(x), N, H, W, C, _ptr(wt), _ptr(bias), K, stride, pad, int(act), _ptr(y), Ho,
+                                    Wo, _ptr(psum), _stream(x))
+    _check(rc, "bev_dwconv2d_f32")
+    return y, psum
+
+
+def se_gate(psum: torch.Tensor, hw: int, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor):
+    """SqueezeExcite gate [N, C] from dwconv partial sums [N, nb, C]; w1 [rd, C], w2 [C, rd]."""
+    _require_gpu(psum, w1, b1, w2, b2)
+    N, nb, C = psum.shape
+    rd = w1.shape[0]
+    gate = torch.empty(N, C, device=psum.device, dtype=torch.float32)
+    rc = lib().bev_se_gate_f32(_ptr(psum), N, nb, C, int(hw), _ptr(w1.contiguous()), _ptr(b1.contiguous()), rd,
+                               _ptr(w2.contiguous()), _ptr(b2.contiguous()), _ptr(gate), _stream(psum))
+    _check(rc, "bev_se_gate_f32")
+    return gate
+
+
+def channel_scale_(y: torch.Tensor, gate: torch.Tensor) -> torch.Tensor:
+    """In place y[n, ..., c] *= gate[n, c] for NHWC y."""
+    _require_gpu(y, gate)
+    assert y.is_contiguous() and gate.is_contiguous()
+    N, C = y.shape[0], y.shape[-1]
+    P = y.numel() // (N * C)
+    rc = lib().bev_channel_scale_f32(_ptr(y), N, P, C, _ptr(gate), _stream(y))
+    _check(rc, "bev_channel_scale_f32")
+    return y
 
 
 def conv2d_dual_nhwc(x: torch.Tensor, x2: torch.Tensor, stride2: int, packed: torch.Tensor, bias, Co: int,

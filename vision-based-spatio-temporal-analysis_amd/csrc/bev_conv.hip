@@ -59,6 +59,12 @@ __global__ void k_pack(const float *__restrict__ w, int Co, int Ci, int KH, int 
     out[t] = v;
 }
 
+// Epilogue activation: 1 = ReLU, 2 = SiLU (torch: x / (1 + exp(-x)); EfficientNet trunk).
+__device__ __forceinline__ float act_fn(float t, int act) {
+    if (act == 2) return t / (1.0f + expf(-t));
+    return t > 0.0f ? t : 0.0f;
+}
+
 struct ConvArgs {
     const float *__restrict__ x;
     const float *__restrict__ wp;
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
             }
             if (a.relu) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) o[u] = o[u] > 0.0f ? o[u] : 0.0f;
+                for (int u = 0; u < 4; ++u) o[u] = act_fn(o[u], a.relu);
             }
             *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
         } else {
@@ -422,7 +428,7 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
                 if (n + u >= a.Co) break;
                 float t = o[u];
                 if (a.res) t += a.res[m * a.Co + n + u];
-                if (a.relu) t = t > 0.0f ? t : 0.0f;
+                if (a.relu) t = act_fn(t, a.relu);
                 yp[u] = t;
             }
         }
@@ -748,7 +754,7 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
                    const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
                    int Wo, void *stream) {
     if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
-        stride <= 0 || pad < 0)
+        stride <= 0 || pad < 0 || relu < 0 || relu > 2)
         return BEV_ERR_ARGS;
     if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
         return BEV_ERR_ARGS;
@@ -779,7 +785,7 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
     if (in_nchw && Ci == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && Co <= 64 && !residual && bias &&
-        g_conv_tile == 0)
+        g_conv_tile == 0 && relu <= 1)
         return launch_stem(x, N, H, W, packed, a.Kp, bias, Co, y, Ho, Wo, relu, (hipStream_t)stream);
     return launch_tiled(a, loader, (hipStream_t)stream);
 }

@@ -1,0 +1,209 @@
+// bev_effnet.hip -- the non-GEMM layers of the EfficientNet trunk for gfx950.
+//
+// The reference builds its per-camera backbone with timm (cnn_encoder.py:26,
+// `features_only=True`, feature index out_index=2 -> stride 8); for
+// efficientnet_b3 that trunk is conv_stem -> blocks.0 (depthwise-separable)
+// -> blocks.1, blocks.2 (inverted residuals, SiLU, squeeze-excitation).  The
+// 1x1 / stem convolutions run on the MFMA implicit GEMM (bev_conv.hip, act =
+// SiLU); this file holds what is not a GEMM:
+//
+//   k_dwconv      depthwise KxK conv (BN folded) + SiLU, NHWC, float4 per
+//                 thread over channels; the thread's K*K weight quads stay in
+//                 VGPRs; the per-workgroup channel sums of the OUTPUT (the
+//                 squeeze of the SE block) are reduced in LDS and written as
+//                 deterministic partials [N][nb][C] (no atomics).
+//   k_se_gate     per image: mean = sum(partials) / (Ho*Wo), conv_reduce +
+//                 SiLU, conv_expand + sigmoid -> gate [N][C].
+//   k_chan_scale  x[n, p, c] *= gate[n, c] in place (the SE excitation).
+//
+// All three are HBM-bound streaming kernels (bytes per output element: the
+// input taps come from L1/L2 after the first touch, so ~4 B in + 4 B out).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+constexpr int DW_NT = 256;      // threads per workgroup
+constexpr int DW_PPB = 2048;    // output pixels per workgroup (one SE partial)
+
+__device__ __forceinline__ float act_f(float t, int act) {
+    if (act == 1) return t > 0.0f ? t : 0.0f;
+    if (act == 2) return t / (1.0f + expf(-t));  // torch SiLU: x / (1 + exp(-x))
+    return t;
+}
+
+template <int K>
+__global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, int H, int W, int C,
+                                                  const float *__restrict__ wt, const float *__restrict__ bias,
+                                                  int stride, int pad, int act, float *__restrict__ y, int Ho, int Wo,
+                                                  float *__restrict__ psum, int nb) {
+    __shared__ float4 red[DW_NT];
+    const int C4 = C >> 2;
+    const int CH4 = C4 <= DW_NT ? C4 : DW_NT / 2;  // channel quads per workgroup (blockIdx.z chunks)
+    const int PB = DW_NT / CH4;                     // pixels per step
+    const int tid = threadIdx.x;
+    const int pl = tid / CH4, c4 = blockIdx.z * CH4 + (tid - pl * CH4);
+    const bool active = pl < PB && c4 < C4;
+    const int n = blockIdx.y, blk = blockIdx.x;
+    const int64_t HWo = (int64_t)Ho * Wo;
+    const int64_t p0 = (int64_t)blk * DW_PPB, p1 = min(p0 + DW_PPB, HWo);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (active) {
+        float4 w[K * K];
+#pragma unroll
+        for (int t = 0; t < K * K; ++t) w[t] = *(const float4 *)(wt + (int64_t)t * C + c4 * 4);
+        const float4 b = *(const float4 *)(bias + c4 * 4);
+        const float *xn = x + (int64_t)n * H * W * C + c4 * 4;
+        float *yn = y + (int64_t)n * HWo * C + c4 * 4;
+        for (int64_t p = p0 + pl; p < p1; p += PB) {
+            const int oy = (int)(p / Wo), ox = (int)(p - (int64_t)oy * Wo);
+            const int iy0 = oy * stride - pad, ix0 = ox * stride - pad;
+            float4 acc = b;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) {
+                const int iy = iy0 + ky;
+                if (iy < 0 || iy >= H) continue;
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const int ix = ix0 + kx;
+                    if (ix < 0 || ix >= W) continue;
+                    const float4 v = *(const float4 *)(xn + ((int64_t)iy * W + ix) * C);
+                    const float4 ww = w[ky * K + kx];
+                    acc.x = __builtin_fmaf(v.x, ww.x, acc.x);
+                    acc.y = __builtin_fmaf(v.y, ww.y, acc.y);
+                    acc.z = __builtin_fmaf(v.z, ww.z, acc.z);
+                    acc.w = __builtin_fmaf(v.w, ww.w, acc.w);
+                }
+            }
+            acc.x = act_f(acc.x, act);
+            acc.y = act_f(acc.y, act);
+            acc.z = act_f(acc.z, act);
+            acc.w = act_f(acc.w, act);
+            *(float4 *)(yn + p * C) = acc;
+            s.x += acc.x;
+            s.y += acc.y;
+            s.z += acc.z;
+            s.w += acc.w;
+        }
+    }
+    if (psum == nullptr) return;
+    red[tid] = s;
+    __syncthreads();
+    if (pl == 0 && c4 < C4) {  // fixed order over the step lanes: deterministic partial
+        for (int q = 1; q < PB; ++q) {
+            const float4 t = red[q * CH4 + (tid - pl * CH4)];
+            s.x += t.x;
+            s.y += t.y;
+            s.z += t.z;
+            s.w += t.w;
+        }
+        *(float4 *)(psum + ((int64_t)n * nb + blk) * C + c4 * 4) = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_se_gate(const float *__restrict__ psum, int nb, int C, float hw,
+                                                 const float *__restrict__ w1, const float *__restrict__ b1, int rd,
+                                                 const float *__restrict__ w2, const float *__restrict__ b2,
+                                                 float *__restrict__ gate) {
+    extern __shared__ float sh[];  // mean[C], r[rd]
+    float *mean = sh, *r = sh + C;
+    const int n = blockIdx.x;
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (int q = 0; q < nb; ++q) s += psum[((int64_t)n * nb + q) * C + c];
+        mean[c] = s / hw;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < rd; j += blockDim.x) {
+        float t = b1[j];
+        for (int c = 0; c < C; ++c) t = __builtin_fmaf(w1[(int64_t)j * C + c], mean[c], t);
+        r[j] = t / (1.0f + expf(-t));  // SiLU (conv_reduce -> act1)
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float t = b2[c];
+        for (int j = 0; j < rd; ++j) t = __builtin_fmaf(w2[(int64_t)c * rd + j], r[j], t);
+        gate[(int64_t)n * C + c] = 1.0f / (1.0f + expf(-t));  // conv_expand -> sigmoid gate
+    }
+}
+
+__global__ __launch_bounds__(256) void k_chan_scale(float *__restrict__ y, int64_t P, int C,
+                                                    const float *__restrict__ gate, int64_t total4) {
+    const int C4 = C >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % C4);
+        const int64_t n = i / C4 / P;
+        float4 v = *(float4 *)(y + i * 4);
+        const float4 g = *(const float4 *)(gate + n * C + c4 * 4);
+        v.x *= g.x;
+        v.y *= g.y;
+        v.z *= g.z;
+        v.w *= g.w;
+        *(float4 *)(y + i * 4) = v;
+    }
+}
+
+inline int last() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int bev_dwconv_psum_blocks(int Ho, int Wo) {
+    if (Ho <= 0 || Wo <= 0) return BEV_ERR_ARGS;
+    return (int)(((int64_t)Ho * Wo + DW_PPB - 1) / DW_PPB);
+}
+
+int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
+                     int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream) {
+    if (!x || !wt || !bias || !y || N < 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 ||
+        stride <= 0 || pad < 0 || act < 0 || act > 2)
+        return BEV_ERR_ARGS;
+    if (K != 3 && K != 5) return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - K) / stride + 1 || Wo != (W + 2 * pad - K) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)wt | (uintptr_t)bias | (uintptr_t)y | (uintptr_t)psum) & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    const int nb = bev_dwconv_psum_blocks(Ho, Wo);
+    const int C4 = C / 4, CH4 = C4 <= DW_NT ? C4 : DW_NT / 2;
+    dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
+    hipStream_t st = (hipStream_t)stream;
+    if (K == 3)
+        hipLaunchKernelGGL(k_dwconv<3>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho, Wo,
+                           psum, nb);
+    else
+        hipLaunchKernelGGL(k_dwconv<5>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho, Wo,
+                           psum, nb);
+    return last();
+}
+
+int bev_se_gate_f32(const float *psum, int N, int nb, int C, int hw, const float *w1, const float *b1, int rd,
+                    const float *w2, const float *b2, float *gate, void *stream) {
+    if (!psum || !w1 || !b1 || !w2 || !b2 || !gate || N < 0 || nb <= 0 || C <= 0 || rd <= 0 || hw <= 0 ||
+        (C + rd) > 12288)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    hipLaunchKernelGGL(k_se_gate, dim3(N), dim3(256), (C + rd) * sizeof(float), (hipStream_t)stream, psum, nb, C,
+                       (float)hw, w1, b1, rd, w2, b2, gate);
+    return last();
+}
+
+int bev_channel_scale_f32(float *y, int N, int64_t P, int C, const float *gate, void *stream) {
+    if (!y || !gate || N < 0 || P < 0 || C <= 0 || C % 4 != 0 || (((uintptr_t)y | (uintptr_t)gate) & 15) != 0)
+        return BEV_ERR_ARGS;
+    const int64_t total4 = (int64_t)N * P * (C / 4);
+    if (total4 == 0) return 0;
+    const int64_t blocks = (total4 + 255) / 256 < 256 * 64 ? (total4 + 255) / 256 : 256 * 64;
+    hipLaunchKernelGGL(k_chan_scale, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, P, C, gate,
+                       total4);
+    return last();
+}
+
+}  // extern "C"

@@ -5,8 +5,9 @@ pretrained=True, out_index=2)` (cnn_encoder.py:15), same input conventions
 ([B,V,3,H,W], or [N,3,H,W] treated as B=1, anything else ValueError;
 cnn_encoder.py:50-72) and same state_dict layout:
 
-* backbones restated in models/encoders/resnet.py (resnet18/34/50, timm
-  names) play the role of the timm `features_only` model: `backbone.*`
+* backbones restated in models/encoders/resnet.py (resnet18/34/50) and
+  models/encoders/efficientnet.py (efficientnet_b3), with timm names, play
+  the role of the timm `features_only` model: `backbone.*`
   weights, `feats_list[out_index]`, then a lazily created 1x1 `proj`
   (cnn_encoder.py:43-46);
 * any other backbone name takes the reference's fallback stack
@@ -29,7 +30,12 @@ import torch.nn as nn
 
 import bev_native as _nat
 from .base import ViewEncoder
-from .resnet import NATIVE_BACKBONES, FoldedConv
+from .efficientnet import efficientnet_b3
+from .resnet import NATIVE_BACKBONES as _RESNETS
+from .resnet import FoldedConv
+
+# backbones with a native (HIP) trunk: timm names of BASELINE configs 1-4
+NATIVE_BACKBONES = dict(_RESNETS, efficientnet_b3=efficientnet_b3)
 
 __all__ = ["CNNEncoder", "Backbone"]
 

@@ -1,0 +1,184 @@
+"""EfficientNet-B3 trunk (timm-compatible module names) executed by the HIP kernels.
+
+The reference's per-camera backbone is `timm.create_model(name, pretrained,
+features_only=True)` (cnn_encoder.py:26) and CNNEncoder keeps
+`feats_list[out_index]` (cnn_encoder.py:41-42, out_index=2).  BASELINE
+config 4 names `efficientnet_b3`.  timm is an unpinned dependency absent from
+this image, so the graph is restated from timm's published definition of
+efficientnet_b3 (channel multiplier 1.2, depth multiplier 1.4, SiLU, SE with
+rd = block-input channels / 4, symmetric padding, BN eps 1e-5) with timm's
+parameter names (conv_stem / bn1 / blocks.S.B.{conv_dw,bn1,se,conv_pw,bn2} for
+the depthwise-separable stage, {conv_pw,bn1,conv_dw,bn2,se,conv_pwl,bn3} for
+inverted residuals), so a timm state_dict loads unchanged.  Parity with timm
+itself is therefore UNPINNED; the kernels are pinned against a torch fp32
+reference of the same weights (oracle/backbone_ref.py, tests/).
+
+features_only feature indices (timm feature_info, 'bottleneck' location):
+0 -> blocks.0 (24 ch, stride 2), 1 -> blocks.1 (32, 4), 2 -> blocks.2 (48, 8),
+3 -> blocks.4 (136, 16), 4 -> blocks.6 (384, 32).
+
+Execution (eval): NHWC on the device; stem / pointwise convs are MFMA
+implicit GEMMs with BN folded and SiLU in the epilogue (bev_conv2d_f32,
+act=2), the depthwise convs are `bev_dwconv2d_f32` (BN folded, SiLU, SE
+squeeze partials fused), the SE gate is `bev_se_gate_f32` and the excitation
+`bev_channel_scale_f32`; the projection conv adds the skip in its epilogue.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+import bev_native as _nat
+from .resnet import FoldedConv
+
+__all__ = ["EfficientNet", "efficientnet_b3", "make_divisible"]
+
+FEATURE_STAGE = {0: 0, 1: 1, 2: 2, 3: 4, 4: 6}  # features_only index -> last stage executed
+
+
+def make_divisible(v, divisor=8, min_value=None, round_limit=0.9):
+    """timm.layers.make_divisible."""
+    min_value = min_value or divisor
+    new_v = max(min_value, int(v + divisor / 2) // divisor * divisor)
+    if new_v < round_limit * v:
+        new_v += divisor
+    return new_v
+
+
+class SqueezeExcite(nn.Module):
+    def __init__(self, chs, rd):
+        super().__init__()
+        self.conv_reduce = nn.Conv2d(chs, rd, 1, bias=True)
+        self.act1 = nn.SiLU(inplace=True)
+        self.conv_expand = nn.Conv2d(rd, chs, 1, bias=True)
+        self.gate = nn.Sigmoid()
+
+
+class DepthwiseSeparableConv(nn.Module):
+    def __init__(self, in_chs, out_chs, k, stride, se_ratio):
+        super().__init__()
+        self.has_skip = stride == 1 and in_chs == out_chs
+        self.conv_dw = nn.Conv2d(in_chs, in_chs, k, stride, k // 2, groups=in_chs, bias=False)
+        self.bn1 = nn.BatchNorm2d(in_chs)
+        self.se = SqueezeExcite(in_chs, round(in_chs * se_ratio))
+        self.conv_pw = nn.Conv2d(in_chs, out_chs, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(out_chs)
+
+
+class InvertedResidual(nn.Module):
+    def __init__(self, in_chs, out_chs, k, stride, exp_ratio, se_ratio):
+        super().__init__()
+        mid = make_divisible(in_chs * exp_ratio)
+        self.has_skip = stride == 1 and in_chs == out_chs
+        self.conv_pw = nn.Conv2d(in_chs, mid, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(mid)
+        self.conv_dw = nn.Conv2d(mid, mid, k, stride, k // 2, groups=mid, bias=False)
+        self.bn2 = nn.BatchNorm2d(mid)
+        self.se = SqueezeExcite(mid, round(mid * se_ratio / exp_ratio))  # se_from_exp=False
+        self.conv_pwl = nn.Conv2d(mid, out_chs, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(out_chs)
+
+
+# (block type, repeats, kernel, stride, expansion, channels) of EfficientNet-B0; se 0.25 everywhere
+_ARCH_B0 = [("ds", 1, 3, 1, 1, 16), ("ir", 2, 3, 2, 6, 24), ("ir", 2, 5, 2, 6, 40), ("ir", 3, 3, 2, 6, 80),
+            ("ir", 3, 5, 1, 6, 112), ("ir", 4, 5, 2, 6, 192), ("ir", 1, 3, 1, 6, 320)]
+
+
+class FoldedDW:
+    """Depthwise conv + eval BN folded into tap-major weights [K*K, C] and a bias, cached on device."""
+
+    def __init__(self, conv: nn.Conv2d, bn: nn.BatchNorm2d):
+        self.fc = FoldedConv(conv, bn)
+        self._key = None
+        self.wt = self.bias = None
+
+    def prepare(self, device):
+        key = tuple((t.data_ptr(), t._version) for t in self.fc._tensors()) + (str(device),)
+        if key == self._key:
+            return
+        w, b = self.fc.folded(device)  # [C, 1, K, K]
+        C, _, K, _ = w.shape
+        self.wt = w.reshape(C, K * K).t().contiguous()
+        self.bias = b.contiguous().float()
+        self._key = key
+
+    def __call__(self, x, want_psum):
+        self.prepare(x.device)
+        c = self.fc.conv
+        return _nat.dwconv2d_nhwc(x, self.wt, self.bias, c.kernel_size[0], c.stride[0], c.padding[0], _nat.ACT_SILU,
+                                  want_psum=want_psum)
+
+
+class EfficientNet(nn.Module):
+    def __init__(self, channel_multiplier: float, depth_multiplier: float):
+        super().__init__()
+        stem = make_divisible(32 * channel_multiplier)
+        self.conv_stem = nn.Conv2d(3, stem, 3, 2, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(stem)
+        stages, cin = [], stem
+        for kind, r, k, s, e, c in _ARCH_B0:
+            cout = make_divisible(c * channel_multiplier)
+            reps = int(math.ceil(r * depth_multiplier))
+            blocks = []
+            for i in range(reps):
+                stride = s if i == 0 else 1
+                if kind == "ds":
+                    blocks.append(DepthwiseSeparableConv(cin, cout, k, stride, 0.25))
+                else:
+                    blocks.append(InvertedResidual(cin, cout, k, stride, e, 0.25))
+                cin = cout
+            stages.append(nn.Sequential(*blocks))
+        self.blocks = nn.Sequential(*stages)
+        self.feature_channels = [self.blocks[FEATURE_STAGE[i]][-1].bn2.num_features
+                                 if isinstance(self.blocks[FEATURE_STAGE[i]][-1], DepthwiseSeparableConv)
+                                 else self.blocks[FEATURE_STAGE[i]][-1].bn3.num_features for i in range(5)]
+        self._folded = {}
+
+    def _fc(self, conv, bn):
+        k = id(conv)
+        if k not in self._folded:
+            self._folded[k] = FoldedConv(conv, bn)
+        return self._folded[k]
+
+    def _fdw(self, conv, bn):
+        k = ("dw", id(conv))
+        if k not in self._folded:
+            self._folded[k] = FoldedDW(conv, bn)
+        return self._folded[k]
+
+    def _se(self, se: SqueezeExcite, y, psum):
+        """SqueezeExcite.forward: y * sigmoid(conv_expand(SiLU(conv_reduce(mean(y))))), in place on y."""
+        w1 = se.conv_reduce.weight.detach().reshape(se.conv_reduce.out_channels, -1).float()
+        w2 = se.conv_expand.weight.detach().reshape(se.conv_expand.out_channels, -1).float()
+        gate = _nat.se_gate(psum, y.shape[1] * y.shape[2], w1, se.conv_reduce.bias.detach().float(), w2,
+                            se.conv_expand.bias.detach().float())
+        return _nat.channel_scale_(y, gate)
+
+    def _block(self, blk, x):
+        if isinstance(blk, DepthwiseSeparableConv):
+            y, ps = self._fdw(blk.conv_dw, blk.bn1)(x, want_psum=True)
+            y = self._se(blk.se, y, ps)
+            return self._fc(blk.conv_pw, blk.bn2)(y, relu=_nat.ACT_NONE, residual=x if blk.has_skip else None)
+        h = self._fc(blk.conv_pw, blk.bn1)(x, relu=_nat.ACT_SILU)
+        y, ps = self._fdw(blk.conv_dw, blk.bn2)(h, want_psum=True)
+        y = self._se(blk.se, y, ps)
+        return self._fc(blk.conv_pwl, blk.bn3)(y, relu=_nat.ACT_NONE, residual=x if blk.has_skip else None)
+
+    def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
+        """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC features_only[out_index]."""
+        if self.training and torch.is_grad_enabled():
+            raise NotImplementedError("native EfficientNet executes eval-mode (folded BN) inference only")
+        if out_index not in FEATURE_STAGE:
+            raise IndexError(f"efficientnet feature index {out_index} out of range 0..4")
+        y = self._fc(self.conv_stem, self.bn1)(x, relu=_nat.ACT_SILU, in_nchw=True)
+        with torch.no_grad():
+            for si in range(FEATURE_STAGE[out_index] + 1):
+                for blk in self.blocks[si]:
+                    y = self._block(blk, y)
+        return y
+
+
+def efficientnet_b3():
+    return EfficientNet(channel_multiplier=1.2, depth_multiplier=1.4)
