@@ -169,15 +169,15 @@ int bev_nhwc_to_nchw_f32(const float *x, int N, int C, int H, int W, float *y, v
  * ------------------------------------------------------------------------- */
 
 /* Number of per-workgroup SE partial sums per image that bev_dwconv2d_f32
- * writes for an Ho x Wo output (psum is [N][nb][C]). */
-int bev_dwconv_psum_blocks(int Ho, int Wo);
+ * writes for an Ho x Wo x C output (psum is [N][nb][C]). */
+int bev_dwconv_psum_blocks(int Ho, int Wo, int C);
 
 /* device: depthwise KxK conv (K = 3 or 5; torch groups = C), BN folded:
  *   y[n,oy,ox,c] = act( sum_{ky,kx} x[n, oy*s-pad+ky, ox*s-pad+kx, c] * wt[ky*K+kx][c] + bias[c] )
  * (timm conv_dw -> bn -> SiLU, _efficientnet_blocks.py InvertedResidual /
  * DepthwiseSeparableConv).  wt is tap-major [K*K][C].  act as bev_conv2d_f32.
  * If psum != NULL, also writes the channel sums of y per workgroup
- * (deterministic partials, [N][bev_dwconv_psum_blocks(Ho,Wo)][C]) -- the
+ * (deterministic partials, [N][bev_dwconv_psum_blocks(Ho,Wo,C)][C]) -- the
  * squeeze of the block's SqueezeExcite. */
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
                      int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);

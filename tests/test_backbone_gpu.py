@@ -35,6 +35,9 @@ CASES = [
     (1, 512, 9, 11, 64, 1, 1, 0, False, False, False),    # encoder proj
     (1, 48, 9, 10, 200, 3, 1, 1, False, False, True),     # ragged Co, Ci % 16 == 0
     (1, 20, 9, 10, 33, 3, 1, 1, False, False, True),      # Ci % 16 != 0 NHWC generic
+    (2, 24, 13, 17, 144, 1, 1, 0, False, False, True),    # contiguous 1x1 loader (Ci % 4), EfficientNet expand
+    (1, 144, 9, 11, 32, 1, 1, 0, False, True, False),     # contiguous 1x1, K tail (144 = 4.5 K steps) + residual
+    (1, 40, 7, 9, 24, 1, 1, 0, False, False, False),      # contiguous 1x1, Ci < BK
 ]
 
 

@@ -49,7 +49,7 @@ SIGNATURES = {
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
-    "bev_dwconv_psum_blocks": (_i, [_i, _i]),
+    "bev_dwconv_psum_blocks": (_i, [_i, _i, _i]),
     "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_se_gate_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "bev_channel_scale_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp]),
@@ -311,7 +311,7 @@ def dwconv2d_nhwc(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, K: int,
     y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.float32)
     psum = None
     if want_psum:
-        nb = lib().bev_dwconv_psum_blocks(Ho, Wo)
+        nb = lib().bev_dwconv_psum_blocks(Ho, Wo, C)
         _check(0 if nb > 0 else nb, "bev_dwconv_psum_blocks")
         psum = torch.empty(N, nb, C, device=x.device, dtype=torch.float32)
     with _span("dwconv", x):

@@ -186,6 +186,39 @@ struct LoaderDual {
     __device__ void advance(const ConvArgs &) { k0 += BK; }
 };
 
+// A loader, pointwise 1x1 / stride 1 / pad 0 over NHWC with Ci % 4 == 0 (but not
+// % 32: EfficientNet widths 24, 40, 48, 144): row m's A data is x[m][0 .. Ci),
+// one contiguous run; a K step reads quads k0 + 4 quad, zero past Ci (K padding).
+template <int ROWS>
+struct LoaderContig {
+    static constexpr int NV = ROWS;
+    int64_t p[ROWS];
+    bool ok[ROWS];
+    int quad, k0;
+    __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int64_t m = m0 + (tid >> 3) + 32 * r;
+            ok[r] = m < a.M;
+            p[r] = (ok[r] ? m : 0) * a.Ci;
+        }
+        quad = tid & 7;
+        k0 = 0;
+    }
+    __device__ void store(float *As, int tid, const f32x4 (&v)[NV]) const {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) *(f32x4 *)(As + ((tid >> 3) + 32 * r) * LROW + quad * 4) = v[r];
+    }
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[NV]) {
+        const int k = k0 + quad * 4;
+        const bool kin = k < a.Ci;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r)
+            v[r] = (ok[r] && kin) ? *(const f32x4 *)(a.x + p[r] + k) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    __device__ void advance(const ConvArgs &) { k0 += BK; }
+};
+
 // A loader, generic path (any Ci, NHWC or NCHW input), element-wise.  Each
 // thread owns ONE output pixel (row) of the tile and a contiguous run of KPT
 // k's, so for a given k the 64 lanes of a wave read 64 neighbouring output
@@ -250,7 +283,8 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
 }
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
-// LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1
+// LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1,
+// 4 contiguous 1x1 (NHWC, Ci % 4 == 0)
 // NBUF: LDS staging buffers.  2 = one barrier per K step; 1 = half the LDS (a
 // third workgroup per CU for the <= 170-VGPR tiles) at two barriers per K step.
 template <int WM, int WN, int TM, int TN, int LOADER, int NBUF>
@@ -273,8 +307,10 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     typename std::conditional<
         LOADER == 1, LoaderFast<AROWS>,
         typename std::conditional<LOADER == 2, LoaderRow<BM, 3, 7>,
-                                  typename std::conditional<LOADER == 3, LoaderDual<AROWS>,
-                                                            LoaderRow<BM>>::type>::type>::type la;
+                                  typename std::conditional<
+                                      LOADER == 3, LoaderDual<AROWS>,
+                                      typename std::conditional<LOADER == 4, LoaderContig<AROWS>,
+                                                                LoaderRow<BM>>::type>::type>::type>::type la;
     la.init(a, m0, tid);
     const int bq = tid & 7;
     const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
@@ -683,6 +719,7 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1, NBUF>), g, b, 0, st, a);
     else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2, NBUF>), g, b, 0, st, a);
     else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3, NBUF>), g, b, 0, st, a);
+    else if (loader == 4) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 4, NBUF>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0, NBUF>), g, b, 0, st, a);
     return last();
 }
@@ -781,7 +818,9 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     a.K = Ci * KH * KW;
     a.Kp = (int)kpad(a.K);
     a.in_nchw = in_nchw;
-    const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : 0;
+    const bool pw = !in_nchw && KH == 1 && KW == 1 && stride == 1 && pad == 0 && Ci % 4 == 0 &&
+                    ((uintptr_t)x & 15) == 0;
+    const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : pw ? 4 : 0;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
     if (in_nchw && Ci == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && Co <= 64 && !residual && bias &&

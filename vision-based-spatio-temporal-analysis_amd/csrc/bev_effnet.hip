@@ -26,7 +26,11 @@
 namespace {
 
 constexpr int DW_NT = 256;      // threads per workgroup
-constexpr int DW_PPB = 2048;    // output pixels per workgroup (one SE partial)
+constexpr int DW_STEPS = 8;     // pixel steps per thread: output pixels per workgroup = DW_STEPS * (pixels per step)
+
+// Channel quads per workgroup (larger C is split over blockIdx.z) and pixels per workgroup.
+inline int dw_ch4(int C) { return C / 4 <= DW_NT ? C / 4 : DW_NT / 2; }
+inline int dw_ppb(int C) { return DW_STEPS * (DW_NT / dw_ch4(C)); }
 
 __device__ __forceinline__ float act_f(float t, int act) {
     if (act == 1) return t > 0.0f ? t : 0.0f;
@@ -38,7 +42,7 @@ template <int K>
 __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, int H, int W, int C,
                                                   const float *__restrict__ wt, const float *__restrict__ bias,
                                                   int stride, int pad, int act, float *__restrict__ y, int Ho, int Wo,
-                                                  float *__restrict__ psum, int nb) {
+                                                  float *__restrict__ psum, int nb, int ppb) {
     __shared__ float4 red[DW_NT];
     const int C4 = C >> 2;
     const int CH4 = C4 <= DW_NT ? C4 : DW_NT / 2;  // channel quads per workgroup (blockIdx.z chunks)
@@ -48,7 +52,7 @@ __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, i
     const bool active = pl < PB && c4 < C4;
     const int n = blockIdx.y, blk = blockIdx.x;
     const int64_t HWo = (int64_t)Ho * Wo;
-    const int64_t p0 = (int64_t)blk * DW_PPB, p1 = min(p0 + DW_PPB, HWo);
+    const int64_t p0 = (int64_t)blk * ppb, p1 = min(p0 + ppb, HWo);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (active) {
         float4 w[K * K];
@@ -103,19 +107,31 @@ __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, i
     }
 }
 
-__global__ __launch_bounds__(256) void k_se_gate(const float *__restrict__ psum, int nb, int C, float hw,
+constexpr int SE_NT = 1024;  // threads of the SE gate workgroup (one per image)
+
+__global__ __launch_bounds__(SE_NT) void k_se_gate(const float *__restrict__ psum, int nb, int C, float hw,
                                                  const float *__restrict__ w1, const float *__restrict__ b1, int rd,
                                                  const float *__restrict__ w2, const float *__restrict__ b2,
                                                  float *__restrict__ gate) {
     extern __shared__ float sh[];  // mean[C], r[rd]
+    __shared__ float part[SE_NT];  // [16 partial lanes][64 channels]
     float *mean = sh, *r = sh + C;
-    const int n = blockIdx.x;
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const int n = blockIdx.x, tid = threadIdx.x;
+    // squeeze: 64 channels x 16 interleaved partial sums per pass, combined in a fixed order
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        const int c = c0 + (tid & 63), q0 = tid >> 6;
         float s = 0.0f;
-        for (int q = 0; q < nb; ++q) s += psum[((int64_t)n * nb + q) * C + c];
-        mean[c] = s / hw;
+        if (c < C)
+            for (int q = q0; q < nb; q += SE_NT / 64) s += psum[((int64_t)n * nb + q) * C + c];
+        part[tid] = s;
+        __syncthreads();
+        if (tid < 64 && c < C) {
+            float t = part[tid];
+            for (int k = 1; k < SE_NT / 64; ++k) t += part[k * 64 + tid];
+            mean[c] = t / hw;
+        }
+        __syncthreads();
     }
-    __syncthreads();
     for (int j = threadIdx.x; j < rd; j += blockDim.x) {
         float t = b1[j];
         for (int c = 0; c < C; ++c) t = __builtin_fmaf(w1[(int64_t)j * C + c], mean[c], t);
@@ -155,9 +171,10 @@ inline int last() {
 
 extern "C" {
 
-int bev_dwconv_psum_blocks(int Ho, int Wo) {
-    if (Ho <= 0 || Wo <= 0) return BEV_ERR_ARGS;
-    return (int)(((int64_t)Ho * Wo + DW_PPB - 1) / DW_PPB);
+int bev_dwconv_psum_blocks(int Ho, int Wo, int C) {
+    if (Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
+    const int ppb = dw_ppb(C);
+    return (int)(((int64_t)Ho * Wo + ppb - 1) / ppb);
 }
 
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
@@ -171,16 +188,16 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
     if ((((uintptr_t)x | (uintptr_t)wt | (uintptr_t)bias | (uintptr_t)y | (uintptr_t)psum) & 15) != 0)
         return BEV_ERR_ARGS;
     if (N == 0) return 0;
-    const int nb = bev_dwconv_psum_blocks(Ho, Wo);
-    const int C4 = C / 4, CH4 = C4 <= DW_NT ? C4 : DW_NT / 2;
+    const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
+    const int C4 = C / 4, CH4 = dw_ch4(C);
     dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
     hipStream_t st = (hipStream_t)stream;
     if (K == 3)
         hipLaunchKernelGGL(k_dwconv<3>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho, Wo,
-                           psum, nb);
+                           psum, nb, ppb);
     else
         hipLaunchKernelGGL(k_dwconv<5>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho, Wo,
-                           psum, nb);
+                           psum, nb, ppb);
     return last();
 }
 
@@ -190,7 +207,7 @@ int bev_se_gate_f32(const float *psum, int N, int nb, int C, int hw, const float
         (C + rd) > 12288)
         return BEV_ERR_ARGS;
     if (N == 0) return 0;
-    hipLaunchKernelGGL(k_se_gate, dim3(N), dim3(256), (C + rd) * sizeof(float), (hipStream_t)stream, psum, nb, C,
+    hipLaunchKernelGGL(k_se_gate, dim3(N), dim3(SE_NT), (C + rd) * sizeof(float), (hipStream_t)stream, psum, nb, C,
                        (float)hw, w1, b1, rd, w2, b2, gate);
     return last();
 }
