@@ -51,6 +51,19 @@ def test_effnet_b3_layout():
     assert 10.0e6 < n < 10.2e6, n  # timm efficientnet_b3 (12.23 M) minus conv_head / bn2 / classifier
 
 
+def test_effnet_b0_b1_b2_layout():
+    """Published widths / depths of the other timm EfficientNets (b0 is configs/wildtrack.yaml:8's backbone)."""
+    from models.encoders.efficientnet import EFFICIENTNETS
+    exp = {"efficientnet_b0": ([1, 2, 2, 3, 3, 4, 1], [16, 24, 40, 112, 320], 3.595e6),
+           "efficientnet_b1": ([2, 3, 3, 4, 4, 5, 2], [16, 24, 40, 112, 320], 6.101e6),
+           "efficientnet_b2": ([2, 3, 3, 4, 4, 5, 2], [16, 24, 48, 120, 352], 7.203e6)}
+    for name, (depths, feats, n) in exp.items():
+        m = EFFICIENTNETS[name]()
+        assert [len(s) for s in m.blocks] == depths, name
+        assert m.feature_channels == feats, name
+        assert abs(sum(p.numel() for p in m.parameters()) - n) < 2e3, name  # timm total minus head / classifier
+
+
 def test_effnet_encoder_selected():
     from models.encoders.cnn_encoder import CNNEncoder
     enc = CNNEncoder(out_channels=16, backbone="efficientnet_b3", pretrained=False)
@@ -107,13 +120,15 @@ def test_conv_silu_epilogue():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("out_index", [0, 2, 3])
-def test_effnet_encoder_vs_torch_fp32(out_index):
-    """Native EfficientNet-B3 trunk to features_only[out_index] + proj vs torch fp32 CPU ops, same weights."""
+@pytest.mark.parametrize("name,out_index", [("efficientnet_b3", 0), ("efficientnet_b3", 2), ("efficientnet_b3", 3),
+                                            ("efficientnet_b0", 2)])
+def test_effnet_encoder_vs_torch_fp32(name, out_index):
+    """Native EfficientNet trunk to features_only[out_index] + proj vs torch fp32 CPU ops, same weights
+    (b3: BASELINE config 4; b0: configs/wildtrack.yaml:8)."""
     from models.encoders.cnn_encoder import CNNEncoder
     import backbone_ref
     torch.manual_seed(0)
-    enc = CNNEncoder(out_channels=32, backbone="efficientnet_b3", pretrained=False, out_index=out_index)
+    enc = CNNEncoder(out_channels=32, backbone=name, pretrained=False, out_index=out_index)
     _perturb_bn(enc)
     enc.eval()
     imgs = _rand((1, 3, 3, 96, 160), 9)

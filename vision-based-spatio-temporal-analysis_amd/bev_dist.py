@@ -7,6 +7,13 @@ spread the path over the GPUs of a node, one process per GPU:
   independent, each rank runs Backbone -> warp -> fusion on its own frames.
   No data-path collective at all; `frame_shard` just splits the frame range.
 
+* data-parallel training (BASELINE config 3): one replica of BEVNet per GPU,
+  DistributedDataParallel with gradient all-reduce over RCCL/xGMI
+  (`materialize_lazy` -> `ddp_wrap` -> `train_step`).  Per step the gradients
+  of the trainable parameters (encoder proj, BEV proj, detector: ~2.9 M
+  params, 11.6 MB fp32) fit one 25 MB bucket -> one all-reduce, overlapped
+  with the tail of the backward by DDP's bucket hooks.
+
 * camera sharding (BASELINE config 5, 16 cams at 4K, 2 cameras per GPU): each
   rank warps ITS cameras with the fused kernel in SUM mode (a partial BEV sum
   [B, C, Hb, Wb]), then ONE reduce-scatter over BEV rows gives every rank the
@@ -23,7 +30,8 @@ from typing import Optional, Tuple
 import torch
 import torch.distributed as dist
 
-__all__ = ["frame_shard", "camera_shard", "reduce_partial_bev", "camera_sharded_forward"]
+__all__ = ["frame_shard", "camera_shard", "reduce_partial_bev", "camera_sharded_forward", "materialize_lazy",
+           "ddp_wrap", "train_step"]
 
 
 def frame_shard(num_frames: int, rank: int, world: int) -> range:
@@ -76,3 +84,39 @@ def camera_sharded_forward(geom, feats_local: torch.Tensor, K_local, Rt_local, i
     part_mode = "max" if mode == "max" else "sum"
     partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
     return reduce_partial_bev(partial, num_views, mode, group, gather)
+
+
+# ---------------------------------------------------------------------------
+# data-parallel training (BASELINE config 3)
+# ---------------------------------------------------------------------------
+def materialize_lazy(model: torch.nn.Module, batch) -> None:
+    """One no-grad forward so the lazily created submodules exist (encoder proj, BEVNet proj /
+    detector: cnn_encoder.py:43-46, model_wrapper.py:70-84) before DDP and the optimizer see the
+    parameters.  (The reference builds its optimizer before they exist, quirk Q2.)"""
+    was = model.training
+    model.eval()
+    with torch.no_grad():
+        model(batch)
+    model.train(was)
+
+
+def ddp_wrap(model: torch.nn.Module, device: Optional[torch.device] = None, bucket_cap_mb: float = 25.0):
+    """DistributedDataParallel over the default group (RCCL on ROCm, gloo on CPU).  Frozen
+    parameters (requires_grad False) are not synchronised; buffers (BN statistics of a frozen
+    trunk, non-persistent grids) are not broadcast each step."""
+    from torch.nn.parallel import DistributedDataParallel
+    ids = [device.index] if device is not None and device.type == "cuda" else None
+    return DistributedDataParallel(model, device_ids=ids, broadcast_buffers=False, bucket_cap_mb=bucket_cap_mb,
+                                   gradient_as_bucket_view=True)
+
+
+def train_step(model, batch, targets, optimizer, loss_cfg=None) -> dict:
+    """One optimisation step as train.py:249-255 (fp32 path): forward, BEVNet.loss, backward
+    (DDP all-reduces the gradients when `model` is wrapped), optimizer step.  Returns the losses."""
+    optimizer.zero_grad(set_to_none=True)
+    preds = model(batch)
+    core = getattr(model, "module", model)
+    losses = core.loss(preds, targets, loss_cfg or {})
+    losses["total_loss"].backward()
+    optimizer.step()
+    return {k: float(v.detach()) for k, v in losses.items()}

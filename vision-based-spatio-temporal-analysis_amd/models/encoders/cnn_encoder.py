@@ -30,12 +30,13 @@ import torch.nn as nn
 
 import bev_native as _nat
 from .base import ViewEncoder
-from .efficientnet import efficientnet_b3
+from .efficientnet import EFFICIENTNETS
+from .proj import Proj1x1
 from .resnet import NATIVE_BACKBONES as _RESNETS
 from .resnet import FoldedConv
 
 # backbones with a native (HIP) trunk: timm names of BASELINE configs 1-4
-NATIVE_BACKBONES = dict(_RESNETS, efficientnet_b3=efficientnet_b3)
+NATIVE_BACKBONES = dict(_RESNETS, **EFFICIENTNETS)
 
 __all__ = ["CNNEncoder", "Backbone"]
 
@@ -73,14 +74,23 @@ class CNNEncoder(ViewEncoder):
         self._fb = None
         self._fproj = None
 
+    def _trunk_frozen(self) -> bool:
+        return not any(p.requires_grad for p in self.backbone.parameters())
+
     def _encode_single_nhwc(self, x: torch.Tensor) -> torch.Tensor:
         """x [N,3,H,W] NCHW -> NHWC features [N,Hf,Wf,C] (cnn_encoder.py:39-48)."""
         if self._use_timm:
-            feat = self.backbone.forward_features_nhwc(x, self.out_index)
+            if self._trunk_frozen():  # ViewEncoder.freeze(): no trunk gradients, BN on running statistics
+                with torch.no_grad():
+                    feat = self.backbone.forward_features_nhwc(x, self.out_index)
+            else:
+                feat = self.backbone.forward_features_nhwc(x, self.out_index)
             if self._feature_channels is None:
                 self._feature_channels = feat.shape[-1]
                 self.proj = nn.Conv2d(self._feature_channels, self.out_channels, kernel_size=1).to(feat.device)
                 self._fproj = FoldedConv(self.proj)
+            if torch.is_grad_enabled() and (self.proj.weight.requires_grad or self.proj.bias.requires_grad):
+                return Proj1x1.apply(feat, self.proj.weight, self.proj.bias)  # trainable proj (BASELINE config 3)
             return self._fproj(feat, relu=False)
         if self._fb is None:
             self._fb = (FoldedConv(self.backbone[0]), FoldedConv(self.backbone[2]))

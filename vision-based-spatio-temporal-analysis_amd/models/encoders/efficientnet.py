@@ -33,7 +33,8 @@ import torch.nn as nn
 import bev_native as _nat
 from .resnet import FoldedConv
 
-__all__ = ["EfficientNet", "efficientnet_b3", "make_divisible"]
+__all__ = ["EfficientNet", "efficientnet_b0", "efficientnet_b1", "efficientnet_b2", "efficientnet_b3",
+           "EFFICIENTNETS", "make_divisible"]
 
 FEATURE_STAGE = {0: 0, 1: 1, 2: 2, 3: 4, 4: 6}  # features_only index -> last stage executed
 
@@ -180,5 +181,23 @@ class EfficientNet(nn.Module):
         return y
 
 
+def efficientnet_b0():
+    """configs/wildtrack.yaml:8 (the reference's main training config)."""
+    return EfficientNet(channel_multiplier=1.0, depth_multiplier=1.0)
+
+
+def efficientnet_b1():
+    return EfficientNet(channel_multiplier=1.0, depth_multiplier=1.1)
+
+
+def efficientnet_b2():
+    return EfficientNet(channel_multiplier=1.1, depth_multiplier=1.2)
+
+
 def efficientnet_b3():
+    """BASELINE config 4."""
     return EfficientNet(channel_multiplier=1.2, depth_multiplier=1.4)
+
+
+EFFICIENTNETS = {"efficientnet_b0": efficientnet_b0, "efficientnet_b1": efficientnet_b1,
+                 "efficientnet_b2": efficientnet_b2, "efficientnet_b3": efficientnet_b3}
