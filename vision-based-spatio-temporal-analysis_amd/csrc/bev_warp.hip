@@ -382,17 +382,18 @@ __device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
 
 // Issue the DMA of footprint block (sx0, sy0, sbw x sbh) into LDS byte offset `off`.
 // Element offsets are 32-bit (the launcher checks that a feature map fits).
+template <int S = 17>
 __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
                                           int npix, unsigned char *smem, int off, int wave, int lane,
                                           int nwaves = FT_NT / 64) {
-    const int ninstr = (npix * 17 + 63) >> 6;
+    const int ninstr = (npix * S + 63) >> 6;
     const float inv_bw = 1.0f / (float)sbw;
     const int base = sy0 * sH + sx0 * sW;
     for (int k = wave; k < ninstr; k += nwaves) {
         const int slot = k * 64 + lane;
-        const int p = slot / 17, sl = slot - p * 17;
+        const int p = slot / S, sl = slot - p * S;
         const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
-        const int eo = base + py * sH + px * sW + ((sl < 16) ? sl * 4 : 0);
+        const int eo = base + py * sH + px * sW + ((sl < S - 1) ? sl * 4 : 0);
         const float *src = f + ((p < npix) ? eo : 0);  // tail lanes: any valid address
         // Inline asm on purpose: hipcc treats the builtin's LDS write as aliasing every
         // later ds_read and drains vmcnt before them, which would serialise the
@@ -413,13 +414,14 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
 // the chunk, per-lane byte offset of the cell, SGPR byte offset of the channel
 // plane -> no per-store address arithmetic.  The dispatcher guarantees the
 // chunk (64 planes) spans < 4 GiB.  aux 2 = nt (streaming, written once).
-__device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell, const float (&acc)[64], int mode,
+template <int N>
+__device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell, const float (&acc)[N], int mode,
                                             double rV) {
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * 64 * sizeof(float)), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * N * sizeof(float)), 0x00020000);
     const int voff = cell * (int)sizeof(float);
 #pragma unroll
-    for (int q = 0; q < 64; ++q) {
+    for (int q = 0; q < N; ++q) {
         float a = acc[q];
         asm volatile("" : "+v"(a)::"memory");  // convert after the previous store (no hoisted doubles)
         const float r = (mode == BEV_FUSE_MEAN) ? div_rcp(a, rV) : a;
@@ -535,16 +537,17 @@ __device__ __forceinline__ Box get_box(const int *rp) {
 
 // Sample one view for the lanes with `mine` from an image at LDS byte offset
 // `ib` (origin sx0, sy0, width sbw); invalid taps read the zero pixel `zp`.
-template <int MODE, int WIN>
-__device__ __forceinline__ void sample_view(float (&acc)[64], const Taps &t, bool mine, int v,
+template <int MODE, int WIN, int N = 64>
+__device__ __forceinline__ void sample_view(float (&acc)[N], const Taps &t, bool mine, int v,
                                             const unsigned char *smem, int ib, int sx0, int sy0, int sbw, int zp) {
-    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * DPS;
+    constexpr int PS = (N / 4 + 1) * 16;  // staged pixel stride (N channels + one pad slot)
+    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * PS;
     const unsigned char *a0 = smem + ((mine && (t.valid & 1)) ? pb : zp);
-    const unsigned char *a1 = smem + ((mine && (t.valid & 2)) ? pb + DPS : zp);
-    const unsigned char *a2 = smem + ((mine && (t.valid & 4)) ? pb + sbw * DPS : zp);
-    const unsigned char *a3 = smem + ((mine && (t.valid & 8)) ? pb + (sbw + 1) * DPS : zp);
+    const unsigned char *a1 = smem + ((mine && (t.valid & 2)) ? pb + PS : zp);
+    const unsigned char *a2 = smem + ((mine && (t.valid & 4)) ? pb + sbw * PS : zp);
+    const unsigned char *a3 = smem + ((mine && (t.valid & 8)) ? pb + (sbw + 1) * PS : zp);
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = 0; g < N / 4; ++g) {
         const float4 vnw = *(const float4 *)(a0 + g * 16);
         const float4 vne = *(const float4 *)(a1 + g * 16);
         const float4 vsw = *(const float4 *)(a2 + g * 16);
@@ -561,11 +564,11 @@ __device__ __forceinline__ void sample_view(float (&acc)[64], const Taps &t, boo
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ void zero_view(float (&acc)[64], int v) {
+template <int MODE, int N>
+__device__ __forceinline__ void zero_view(float (&acc)[N], int v) {
     if (MODE == BEV_FUSE_MAX) {
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = nan_max(acc[q], 0.0f);
+        for (int q = 0; q < N; ++q) acc[q] = nan_max(acc[q], 0.0f);
     }
 }
 
@@ -795,8 +798,8 @@ __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float y
 // (a dependent v_pk_* pair needs a wait state): per element exactly
 // fma(se, wse, fma(sw, wsw, fma(ne, wne, nw * wnw))), then acc + s / max.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int MODE>
-__device__ __forceinline__ void bilerp4(float (&acc)[64], int q0, const f32x4 &nw, const f32x4 &ne, const f32x4 &sw,
+template <int MODE, int N>
+__device__ __forceinline__ void bilerp4(float (&acc)[N], int q0, const f32x4 &nw, const f32x4 &ne, const f32x4 &sw,
                                         const f32x4 &se, const float w[4]) {
     const f32x2 w0 = (f32x2){w[0], w[0]}, w1 = (f32x2){w[1], w[1]}, w2 = (f32x2){w[2], w[2]},
                 w3 = (f32x2){w[3], w[3]};
@@ -824,19 +827,20 @@ __device__ __forceinline__ void bilerp4(float (&acc)[64], int q0, const f32x4 &n
 }
 
 // LDS sampling of one view, software-pipelined by one 4-channel group.
-template <int MODE>
-__device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t, const unsigned char *smem, int ib,
+template <int MODE, int N>
+__device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t, const unsigned char *smem, int ib,
                                                  int sx0, int sy0, int sbw, int zp) {
-    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * DPS;
+    constexpr int PS = (N / 4 + 1) * 16, NG = N / 4;
+    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * PS;
     const unsigned char *a0 = smem + ((t.valid & 1) ? pb : zp);
-    const unsigned char *a1 = smem + ((t.valid & 2) ? pb + DPS : zp);
-    const unsigned char *a2 = smem + ((t.valid & 4) ? pb + sbw * DPS : zp);
-    const unsigned char *a3 = smem + ((t.valid & 8) ? pb + (sbw + 1) * DPS : zp);
+    const unsigned char *a1 = smem + ((t.valid & 2) ? pb + PS : zp);
+    const unsigned char *a2 = smem + ((t.valid & 4) ? pb + sbw * PS : zp);
+    const unsigned char *a3 = smem + ((t.valid & 8) ? pb + (sbw + 1) * PS : zp);
     f32x4 c0 = *(const f32x4 *)a0, c1 = *(const f32x4 *)a1, c2 = *(const f32x4 *)a2, c3 = *(const f32x4 *)a3;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = 0; g < NG; ++g) {
         f32x4 n0, n1, n2, n3;
-        if (g < 15) {
+        if (g < NG - 1) {
             n0 = *(const f32x4 *)(a0 + (g + 1) * 16);
             n1 = *(const f32x4 *)(a1 + (g + 1) * 16);
             n2 = *(const f32x4 *)(a2 + (g + 1) * 16);
@@ -844,7 +848,7 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t
         }
         bilerp4<MODE>(acc, 4 * g, c0, c1, c2, c3, t.w);
         __builtin_amdgcn_sched_barrier(0);  // at most two groups of reads in flight
-        if (g < 15) {
+        if (g < NG - 1) {
             c0 = n0;
             c1 = n1;
             c2 = n2;
@@ -853,7 +857,7 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[64], const Taps &t
     }
 }
 
-template <int MODE, int OCC, bool WIDE, int TH>
+template <int MODE, int OCC, bool WIDE, int TH, int CW = 64>
 __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                            int64_t sW, const float *__restrict__ Hmat,
                                                            const float *__restrict__ xs,
@@ -863,13 +867,14 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
     // dbg: profiling-only ablations (BEV_WARP_DEBUG; results are WRONG when set):
     //   1 skip views that need synchronous staging, 2 skip LDS sampling, 4 skip stores, 8 skip DMA
     // WIDE: widened float4 stores through LDS (store_chunk_wide); the launcher checks its conditions
-    constexpr bool wide = WIDE && TH == TH;
+    constexpr bool wide = WIDE && TH == FT_H && CW == 64;
     constexpr int NT = TH * FT_W, NW = NT / 64;  // TH / 2 waves, each two rows of 32 cells
+    constexpr int SL = CW / 4 + 1, PS = SL * 16;  // DMA slots / bytes per staged pixel (CW channels + pad)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int zp = pool;                                    // zero pixel (256 B)
     int *red = reinterpret_cast<int *>(smem + pool + 256);  // [4 * NW] exact-bbox exchange
     float *htab = reinterpret_cast<float *>(smem + pool + 256 + 4 * NW * sizeof(int));  // [V][9] homographies
-    const int maxpix = pool / DPS - 4;                      // ~1 KiB DMA rounding slack
+    const int maxpix = pool / PS - 4;                      // ~1 KiB DMA rounding slack
     // dbg & 64: per-wave phase stamps (s_memtime) into out (tools/warp_phases_v2.py)
     const bool stamp = (dbg & 64) != 0;
     long long T0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0, T1 = 0, T2 = 0, T3 = 0;
@@ -935,13 +940,13 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
         return t;
     };
 
-    for (int c0 = 0; c0 < C; c0 += 64) {
+    for (int c0 = 0; c0 < C; c0 += CW) {
         ccx = cx;
         ccy = cy;
         asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep taps per chunk (no hoisting + spills)
-        float acc[64];
+        float acc[CW];
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        for (int q = 0; q < CW; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
         const float *fb = feats + (int64_t)(b * V) * sN + c0;
 
         // prologue: DMA of view 0 (if its corner box applies and fits)
@@ -951,7 +956,7 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
             if (ok_of(0) && bn.x1 >= 0 && npix <= maxpix) {
                 offn = 0;
-                dma_block(fb, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, 0, wave, lane, NW);
+                dma_block<SL>(fb, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, 0, wave, lane, NW);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -988,7 +993,7 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                 const bool single = (nbx == 1) && (nby == 1);
                 if (single)  // the common case: start the copy (the pool is free since the last
                              // end-of-view barrier), compute the taps while it lands
-                    dma_block(f, (int)sH, (int)sW, bx.x0, bx.y0, bw, bw * bh, smem, 0, wave, lane, NW);
+                    dma_block<SL>(f, (int)sH, (int)sW, bx.x0, bx.y0, bw, bw * bh, smem, 0, wave, lane, NW);
                 if (!have_t) {
                     t = taps_of(v);
                     have_t = true;
@@ -1007,13 +1012,13 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                         const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
                         if (!single) {
                             __syncthreads();  // earlier LDS images are no longer read
-                            dma_block(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane, NW);
+                            dma_block<SL>(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane, NW);
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
                         const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
                         const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE, 1>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        if (go) sample_view<MODE, 1, CW>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
                         else if (single) zero_view<MODE>(acc, v);
                     }
                 done = true;
@@ -1028,13 +1033,13 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                 if (ok_of(v + 1) && bn.x1 >= 0 && npix <= maxpix) {
                     // consecutive images anchor at opposite ends of the pool: they coexist
                     // whenever their sizes add up to at most the pool
-                    const int need = ((npix * 17 + 63) >> 6) * 1024;
+                    const int need = ((npix * SL + 63) >> 6) * 1024;
                     if (done || off < 0) offn = 0;
                     else if (off == 0) {
-                        if (((bw * bh * 17 + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
+                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
                     } else if (need <= off) offn = 0;
                     if (offn >= 0 && !(dbg & 8))
-                        dma_block(f + sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, offn, wave,
+                        dma_block<SL>(f + sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, offn, wave,
                                   lane, NW);
                 }
             }
@@ -1043,7 +1048,7 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
             if (!done) {
                 if (!have_t) t = taps_of(v);
                 if (__ballot(t.valid != 0) != 0ull && !(dbg & 2))
-                    sample_view_pipe<MODE>(acc, t, smem, off, bx.x0, bx.y0, bw, zp);
+                    sample_view_pipe<MODE, CW>(acc, t, smem, off, bx.x0, bx.y0, bw, zp);
                 else if (dbg & 2)
                     acc[0] += t.w[0] + (float)t.x0;  // keep the taps live
                 else zero_view<MODE>(acc, v);
@@ -1062,14 +1067,14 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
             }
         }
         if (stamp) T3 = (long long)__builtin_amdgcn_s_memtime();
-        if (wide) {
+        if constexpr (wide) {
             if (!(dbg & 4))
                 store_chunk_wide(out + ((size_t)b * C + c0) * plane, plane, Hb, Wb, tyb * TH, txb * FT_W,
                                  reinterpret_cast<float *>(smem), tid, acc, MODE, rV);
         } else if (inside && !(dbg & 4)) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
         if (dbg & 4) {
             float z = 0.f;
-            for (int q = 0; q < 64; ++q) z += acc[q];
+            for (int q = 0; q < CW; ++q) z += acc[q];
             if (z == 12345.f) out[0] = z;  // keep acc live
         }
     }
@@ -1441,7 +1446,7 @@ inline int warp_debug() {
     return v;
 }
 
-template <int OCC, bool WIDE, int TH = FT_H>
+template <int OCC, bool WIDE, int TH = FT_H, int CW = 64>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
                        int mode, float *out, hipStream_t st, int pool) {
@@ -1449,13 +1454,13 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
     dim3 grid(ntiles, B), block(TH * FT_W);
     const size_t lds = pool + 256 + 4 * (TH / 2) * sizeof(int) + V2_MAXV * 9 * sizeof(float);
     if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, WIDE, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, WIDE, TH, CW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
                            xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
     else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, WIDE, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, WIDE, TH, CW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
                            xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
     else
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, WIDE, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, WIDE, TH, CW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
                            xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
     return last();
 }
@@ -1480,6 +1485,18 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
         const char *t = getenv("BEV_WARP_TH");
         return t ? atoi(t) : 8;
     }();
+    static const int cw = [] {
+        const char *t = getenv("BEV_WARP_CW");
+        return t ? atoi(t) : 64;
+    }();
+    if (cw == 32 && C % 32 == 0) {  // 32-channel passes: 32-wide accumulator, 4 workgroups (16 waves) per CU
+        const int pool = e ? warp_pool_bytes() : 36 * 1024;
+        if (mode == BEV_FUSE_MAX)
+            return launch_fuse_v2_occ<2, false, FT_H, 32>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy,
+                                                          Hb, Wb, mode, out, st, pool);
+        return launch_fuse_v2_occ<4, false, FT_H, 32>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb,
+                                                      Wb, mode, out, st, pool);
+    }
     if (th == 16 || th == 32) {  // one workgroup per CU: 8 (16) waves on a 16 (32) x 32 tile
         const int pool = e ? warp_pool_bytes() : 140 * 1024;
         if (th == 16)
