@@ -141,6 +141,16 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
                    const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
                    int Wo, void *stream);
 
+/* device: as bev_conv2d_f32 (NHWC input) with every input channel scaled per image first:
+ *   y = act( conv(x * gate[n, ci], w) + bias (+ residual) )
+ * gate [N][Ci] -- the SqueezeExcite excitation of an EfficientNet block folded into the
+ * projection conv's operand load (timm InvertedResidual: se -> conv_pwl; the product x * gate
+ * is rounded to fp32 exactly as the separate `x * gate` of SqueezeExcite.forward).
+ * Needs Ci % 32 == 0, or a 1x1 / stride-1 / pad-0 conv with Ci % 4 == 0; 16-B aligned x, gate. */
+int bev_conv2d_chscale_f32(const float *x, int N, int H, int W, int Ci, const float *gate, const float *packed,
+                           const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
+                           int relu, float *y, int Ho, int Wo, void *stream);
+
 /* device: bottleneck tail as ONE GEMM (NHWC, both 1x1):
  *   y = act( x (*) W1  +  x2[:, ::s2, ::s2, :] (*) W2  + bias )
  * x [N][Ho][Wo][Ci] is conv3's input, x2 [N][H2][W2][Ci2] the block input the

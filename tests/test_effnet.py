@@ -139,3 +139,24 @@ def test_effnet_encoder_vs_torch_fp32(name, out_index):
     assert tuple(y.shape) == tuple(ref.shape) == (1, 3, 32, 96 // stride, 160 // stride)
     err = (y - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-4, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Ci", [144, 192, 40])
+def test_conv_chscale_equals_separate_excitation(Ci):
+    """SE excitation folded into the projection conv's operand load == x * gate, then the conv (bit-exact:
+    the same fp32 product feeds the same MFMA chain), and == torch fp32 within tolerance."""
+    import bev_native as nat
+    from models.encoders.resnet import FoldedConv
+    N, H, W, Co = 2, 9, 13, 48
+    x = _rand((N, H, W, Ci), 11).to(DEV)
+    gate = torch.sigmoid(_rand((N, Ci), 12)).to(DEV)
+    res = _rand((N, H, W, Co), 13).to(DEV)
+    conv = torch.nn.Conv2d(Ci, Co, 1, bias=False).to(DEV)
+    fc = FoldedConv(conv)
+    fused = fc(x, relu=nat.ACT_NONE, residual=res, ascale=gate)
+    sep = fc(nat.channel_scale_(x.clone(), gate), relu=nat.ACT_NONE, residual=res)
+    assert torch.equal(fused, sep)
+    ref = F.conv2d((x * gate[:, None, None, :]).permute(0, 3, 1, 2).cpu(), conv.weight.detach().cpu())
+    ref = ref.permute(0, 2, 3, 1) + res.cpu()
+    np.testing.assert_allclose(fused.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)

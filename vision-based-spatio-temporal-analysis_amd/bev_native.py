@@ -45,6 +45,8 @@ SIGNATURES = {
     "bev_conv_packed_size": (_i64, [_i, _i, _i, _i]),
     "bev_conv_pack_weights_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "bev_conv2d_chscale_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i,
+                                    _vp]),
     "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
@@ -276,8 +278,10 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
-                relu: bool, residual: torch.Tensor = None, in_nchw: bool = False, out: torch.Tensor = None):
-    """x: [N,H,W,Ci] NHWC (or [N,Ci,H,W] with in_nchw) -> y [N,Ho,Wo,Co] NHWC."""
+                relu: bool, residual: torch.Tensor = None, in_nchw: bool = False, out: torch.Tensor = None,
+                ascale: torch.Tensor = None):
+    """x: [N,H,W,Ci] NHWC (or [N,Ci,H,W] with in_nchw) -> y [N,Ho,Wo,Co] NHWC.
+    ascale [N, Ci]: per-image input-channel multiplier applied in the operand load (SE excitation)."""
     x = x.contiguous()
     _require_gpu(x, packed, bias, residual)
     if in_nchw:
@@ -291,8 +295,14 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
         residual = residual.contiguous()
         assert residual.shape == out.shape
     with _span("conv", x):
-        rc = lib().bev_conv2d_f32(_ptr(x), int(in_nchw), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co,
-                                  KH, KW, stride, pad, int(relu), _ptr(out), Ho, Wo, _stream(x))
+        if ascale is not None:
+            assert not in_nchw and ascale.shape == (N, Ci) and ascale.is_contiguous()
+            rc = lib().bev_conv2d_chscale_f32(_ptr(x), N, H, W, Ci, _ptr(ascale), _ptr(packed), _ptr(bias),
+                                              _ptr(residual), Co, KH, KW, stride, pad, int(relu), _ptr(out), Ho, Wo,
+                                              _stream(x))
+        else:
+            rc = lib().bev_conv2d_f32(_ptr(x), int(in_nchw), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual),
+                                      Co, KH, KW, stride, pad, int(relu), _ptr(out), Ho, Wo, _stream(x))
     _check(rc, "bev_conv2d_f32")
     return out
 

@@ -80,15 +80,23 @@ struct ConvArgs {
     // dual-source 1x1 (LOADER 3): k in [Ci, Ci + Ci2) reads x2 [N][H2][W2][Ci2] at (oy*s2, ox*s2)
     const float *__restrict__ x2;
     int Ci2, H2, W2, stride2;
+    // per-(image, input channel) multiplier of the A operand (SqueezeExcite excitation folded into
+    // the projection conv's loader: conv(x * gate)); NULL = none.  Fast and contiguous loaders only.
+    const float *__restrict__ ascale;
 };
 
 // Per-thread view of the A tile rows it loads: rows (tid >> 3) + 32 r, one 16-B quad.
 template <int ROWS>
 struct RowsA {
     int64_t pix[ROWS];  // element offset of the row's image
-    int iy0[ROWS], ix0[ROWS];
+    int iy0[ROWS], ix0[ROWS], img[ROWS];
     bool ok[ROWS];
+    bool uni;  // every row of the tile lies in one image (img[0]): one gate quad per K step
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+        {
+            const int64_t hw = (int64_t)a.Ho * a.Wo, last = (m0 + 32 * ROWS - 1 < a.M) ? m0 + 32 * ROWS - 1 : a.M - 1;
+            uni = (m0 / hw) == (last / hw);
+        }
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const int64_t m = m0 + (tid >> 3) + 32 * r;
@@ -99,6 +107,7 @@ struct RowsA {
             const int oy = (int)(t % a.Ho);
             const int n = (int)(t / a.Ho);
             pix[r] = (int64_t)n * a.H * a.W * a.Ci;
+            img[r] = n;
             iy0[r] = oy * a.stride - a.pad;
             ix0[r] = ox * a.stride - a.pad;
         }
@@ -130,6 +139,13 @@ struct LoaderFast {
             const bool in = rows.ok[r] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
             v[r] = in ? *(const f32x4 *)(a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4)
                       : (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (a.ascale && !rows.uni && in)
+                v[r] *= *(const f32x4 *)(a.ascale + (int64_t)rows.img[r] * a.Ci + ci0 + quad * 4);
+        }
+        if (a.ascale && rows.uni) {
+            const f32x4 g = *(const f32x4 *)(a.ascale + (int64_t)rows.img[0] * a.Ci + ci0 + quad * 4);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) v[r] *= g;  // out-of-range rows are 0 and stay 0
         }
     }
     __device__ void advance(const ConvArgs &a) {
@@ -192,15 +208,19 @@ struct LoaderDual {
 template <int ROWS>
 struct LoaderContig {
     static constexpr int NV = ROWS;
-    int64_t p[ROWS];
-    bool ok[ROWS];
+    int64_t p[ROWS], g[ROWS];
+    bool ok[ROWS], uni;
     int quad, k0;
     __device__ void init(const ConvArgs &a, int64_t m0, int tid) {
+        const int64_t hw = (int64_t)a.Ho * a.Wo;
+        const int64_t last = (m0 + 32 * ROWS - 1 < a.M) ? m0 + 32 * ROWS - 1 : a.M - 1;
+        uni = (m0 / hw) == (last / hw);
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const int64_t m = m0 + (tid >> 3) + 32 * r;
             ok[r] = m < a.M;
             p[r] = (ok[r] ? m : 0) * a.Ci;
+            g[r] = a.ascale ? ((ok[r] ? m : 0) / hw) * a.Ci : 0;
         }
         quad = tid & 7;
         k0 = 0;
@@ -213,8 +233,15 @@ struct LoaderContig {
         const int k = k0 + quad * 4;
         const bool kin = k < a.Ci;
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r)
+        for (int r = 0; r < ROWS; ++r) {
             v[r] = (ok[r] && kin) ? *(const f32x4 *)(a.x + p[r] + k) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (a.ascale && !uni && ok[r] && kin) v[r] *= *(const f32x4 *)(a.ascale + g[r] + k);
+        }
+        if (a.ascale && uni && kin) {
+            const f32x4 gq = *(const f32x4 *)(a.ascale + g[0] + k);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) v[r] *= gq;  // out-of-range rows are 0 and stay 0
+        }
     }
     __device__ void advance(const ConvArgs &) { k0 += BK; }
 };
@@ -787,9 +814,31 @@ int bev_conv_pack_weights_f32(const float *w, int Co, int Ci, int KH, int KW, fl
     return last();
 }
 
+static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed,
+                       const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad, int relu,
+                       float *y, int Ho, int Wo, const float *ascale, void *stream);
+
 int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed, const float *bias,
                    const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
                    int Wo, void *stream) {
+    return conv2d_impl(x, in_nchw, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, relu, y, Ho, Wo,
+                       nullptr, stream);
+}
+
+int bev_conv2d_chscale_f32(const float *x, int N, int H, int W, int Ci, const float *gate, const float *packed,
+                           const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
+                           int relu, float *y, int Ho, int Wo, void *stream) {
+    if (!gate || ((((uintptr_t)gate) | ((uintptr_t)x)) & 15) != 0 || Ci % 4 != 0) return BEV_ERR_ARGS;
+    const bool fast = Ci % BK == 0;
+    const bool contig = KH == 1 && KW == 1 && stride == 1 && pad == 0;
+    if (!fast && !contig) return BEV_ERR_ARGS;  // only the fast / contiguous loaders apply the scale
+    return conv2d_impl(x, 0, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, relu, y, Ho, Wo, gate,
+                       stream);
+}
+
+static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed,
+                       const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad, int relu,
+                       float *y, int Ho, int Wo, const float *ascale, void *stream) {
     if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
         stride <= 0 || pad < 0 || relu < 0 || relu > 2)
         return BEV_ERR_ARGS;
@@ -823,8 +872,9 @@ int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, con
     const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : pw ? 4 : 0;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    a.ascale = ascale;
     if (in_nchw && Ci == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && Co <= 64 && !residual && bias &&
-        g_conv_tile == 0 && relu <= 1)
+        g_conv_tile == 0 && relu <= 1 && !ascale)
         return launch_stem(x, N, H, W, packed, a.Kp, bias, Co, y, Ho, Wo, relu, (hipStream_t)stream);
     return launch_tiled(a, loader, (hipStream_t)stream);
 }
@@ -860,6 +910,7 @@ int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const flo
     a.Kp = (int)kpad(a.K);
     a.in_nchw = 0;
     a.x2 = x2;
+    a.ascale = nullptr;
     a.Ci2 = Ci2;
     a.H2 = H2;
     a.W2 = W2;

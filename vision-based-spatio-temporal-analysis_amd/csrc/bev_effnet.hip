@@ -120,9 +120,19 @@ __global__ __launch_bounds__(SE_NT) void k_se_gate(const float *__restrict__ psu
     // squeeze: 64 channels x 16 interleaved partial sums per pass, combined in a fixed order
     for (int c0 = 0; c0 < C; c0 += 64) {
         const int c = c0 + (tid & 63), q0 = tid >> 6;
-        float s = 0.0f;
-        if (c < C)
-            for (int q = q0; q < nb; q += SE_NT / 64) s += psum[((int64_t)n * nb + q) * C + c];
+        // 8 independent chains (loads in flight instead of one latency-bound chain), fixed combine order
+        float t8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (c < C) {
+            const float *ps = psum + (int64_t)n * nb * C + c;
+            constexpr int ST = SE_NT / 64;
+            int q = q0;
+            for (; q + 7 * ST < nb; q += 8 * ST) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) t8[u] += ps[(int64_t)(q + u * ST) * C];
+            }
+            for (int u = 0; q < nb; q += ST, ++u) t8[u & 7] += ps[(int64_t)q * C];
+        }
+        const float s = ((t8[0] + t8[1]) + (t8[2] + t8[3])) + ((t8[4] + t8[5]) + (t8[6] + t8[7]));
         part[tid] = s;
         __syncthreads();
         if (tid < 64 && c < C) {

@@ -949,21 +949,36 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
         for (int q = 0; q < CW; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
         const float *fb = feats + (int64_t)(b * V) * sN + c0;
 
-        // prologue: DMA of view 0 (if its corner box applies and fits)
-        Box bn = box_of(0);
+        // Views whose corner box is empty (the tile is outside that camera's feature map)
+        // contribute +0 (sum / mean: skipping them is exact, the accumulator is never -0)
+        // or max(acc, 0): they get no iteration, no DMA and no barrier.
+        auto live = [&](int u) { return !ok_of(u) || box_of(u).x1 >= 0; };
+        auto next_live = [&](int u) {
+            ++u;
+            while (u < V && !live(u)) {
+                zero_view<MODE>(acc, u);
+                ++u;
+            }
+            return u;
+        };
+        const int v_first = next_live(-1);
+        // prologue: DMA of the first live view (if its corner box applies and fits)
+        Box bn = box_of(v_first < V ? v_first : 0);
         int offn = -1;
-        {
+        if (v_first < V) {
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-            if (ok_of(0) && bn.x1 >= 0 && npix <= maxpix) {
+            if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
                 offn = 0;
-                dma_block<SL>(fb, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, 0, wave, lane, NW);
+                dma_block<SL>(fb + (int64_t)v_first * sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix,
+                              smem, 0, wave, lane, NW);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();  // zero pixel + image of view 0
+        __syncthreads();  // zero pixel + image of the first live view
         if (stamp) T2 = (long long)__builtin_amdgcn_s_memtime();
 
-        for (int v = 0; v < V; ++v) {
+        for (int v = v_first, vn; v < V; v = vn) {
+            vn = next_live(v);
             long long ta = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             Box bx = bn;
             const int off = offn;
@@ -1025,12 +1040,12 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                 __syncthreads();  // every wave is done with the staged blocks before DMA(v+1) reuses the pool
             }
             long long tb = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
-            // ---- look ahead: DMA of view v+1 beside the live image of view v ----------
-            if (v + 1 < V) {
-                bn = box_of(v + 1);
+            // ---- look ahead: DMA of the next live view beside the live image of view v ----
+            if (vn < V) {
+                bn = box_of(vn);
                 offn = -1;
                 const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-                if (ok_of(v + 1) && bn.x1 >= 0 && npix <= maxpix) {
+                if (ok_of(vn) && bn.x1 >= 0 && npix <= maxpix) {
                     // consecutive images anchor at opposite ends of the pool: they coexist
                     // whenever their sizes add up to at most the pool
                     const int need = ((npix * SL + 63) >> 6) * 1024;
@@ -1039,8 +1054,8 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                         if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
                     } else if (need <= off) offn = 0;
                     if (offn >= 0 && !(dbg & 8))
-                        dma_block<SL>(f + sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, offn, wave,
-                                  lane, NW);
+                        dma_block<SL>(fb + (int64_t)vn * sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix,
+                                      smem, offn, wave, lane, NW);
                 }
             }
             long long tc = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -1382,7 +1397,8 @@ inline int warp_pool_bytes() {
 inline int warp_occ() {
     static int v = [] {
         const char *e = getenv("BEV_WARP_OCC");
-        return (e && atoi(e) == 2) ? 2 : 4;
+        const int o = e ? atoi(e) : 3;  // 3: measured best (94.7 us vs 97.8 at 4, 104 at 2; r01 A/B)
+        return (o == 2 || o == 4) ? o : 3;
     }();
     return v;
 }
@@ -1509,6 +1525,11 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
         const int pool = e ? warp_pool_bytes() : 72 * 1024;
         return launch_fuse_v2_pick<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
                                      st, pool);
+    }
+    if (warp_occ() == 3) {  // 3 workgroups / 12 waves per CU: 170 VGPRs (no spills), ~49 KiB pool
+        const int pool = e ? warp_pool_bytes() : 49 * 1024;
+        return launch_fuse_v2_occ<3, false>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode,
+                                            out, st, pool);
     }
     const int pool = e ? warp_pool_bytes() : 36 * 1024;
     return launch_fuse_v2_pick<4>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,

@@ -20,8 +20,9 @@ features_only feature indices (timm feature_info, 'bottleneck' location):
 Execution (eval): NHWC on the device; stem / pointwise convs are MFMA
 implicit GEMMs with BN folded and SiLU in the epilogue (bev_conv2d_f32,
 act=2), the depthwise convs are `bev_dwconv2d_f32` (BN folded, SiLU, SE
-squeeze partials fused), the SE gate is `bev_se_gate_f32` and the excitation
-`bev_channel_scale_f32`; the projection conv adds the skip in its epilogue.
+squeeze partials fused), the SE gate is `bev_se_gate_f32`, and the excitation
+`x * gate` is applied inside the projection conv's operand load (`bev_conv2d_chscale_f32`), which also adds
+the skip in its epilogue.
 """
 from __future__ import annotations
 
@@ -149,23 +150,27 @@ class EfficientNet(nn.Module):
             self._folded[k] = FoldedDW(conv, bn)
         return self._folded[k]
 
-    def _se(self, se: SqueezeExcite, y, psum):
-        """SqueezeExcite.forward: y * sigmoid(conv_expand(SiLU(conv_reduce(mean(y))))), in place on y."""
+    def _gate(self, se: SqueezeExcite, y, psum):
+        """SqueezeExcite gate sigmoid(conv_expand(SiLU(conv_reduce(mean(y))))) [N, C]; the excitation
+        y * gate is applied by the following projection conv's operand loader (bev_conv2d_chscale_f32)."""
         w1 = se.conv_reduce.weight.detach().reshape(se.conv_reduce.out_channels, -1).float()
         w2 = se.conv_expand.weight.detach().reshape(se.conv_expand.out_channels, -1).float()
-        gate = _nat.se_gate(psum, y.shape[1] * y.shape[2], w1, se.conv_reduce.bias.detach().float(), w2,
+        return _nat.se_gate(psum, y.shape[1] * y.shape[2], w1, se.conv_reduce.bias.detach().float(), w2,
                             se.conv_expand.bias.detach().float())
-        return _nat.channel_scale_(y, gate)
+
+    def _project(self, conv, bn, y, gate, residual):
+        C = y.shape[-1]
+        if C % 32 == 0 or C % 4 == 0:  # fast / contiguous 1x1 loader: fold the excitation in
+            return self._fc(conv, bn)(y, relu=_nat.ACT_NONE, residual=residual, ascale=gate)
+        return self._fc(conv, bn)(_nat.channel_scale_(y, gate), relu=_nat.ACT_NONE, residual=residual)
 
     def _block(self, blk, x):
         if isinstance(blk, DepthwiseSeparableConv):
             y, ps = self._fdw(blk.conv_dw, blk.bn1)(x, want_psum=True)
-            y = self._se(blk.se, y, ps)
-            return self._fc(blk.conv_pw, blk.bn2)(y, relu=_nat.ACT_NONE, residual=x if blk.has_skip else None)
+            return self._project(blk.conv_pw, blk.bn2, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
         h = self._fc(blk.conv_pw, blk.bn1)(x, relu=_nat.ACT_SILU)
         y, ps = self._fdw(blk.conv_dw, blk.bn2)(h, want_psum=True)
-        y = self._se(blk.se, y, ps)
-        return self._fc(blk.conv_pwl, blk.bn3)(y, relu=_nat.ACT_NONE, residual=x if blk.has_skip else None)
+        return self._project(blk.conv_pwl, blk.bn3, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
 
     def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC features_only[out_index]."""

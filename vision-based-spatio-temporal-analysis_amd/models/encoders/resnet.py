@@ -112,11 +112,11 @@ class FoldedConv:
                 b = bn.bias.detach().to(device) + (b - bn.running_mean.detach().to(device)) * scale
         return w, b
 
-    def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False):
+    def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False, ascale=None):
         self.prepare(x.device)
         c = self.conv
         return _nat.conv2d_nhwc(x, self.packed, self.bias, c.out_channels, c.kernel_size[0], c.kernel_size[1],
-                                c.stride[0], c.padding[0], relu, residual=residual, in_nchw=in_nchw)
+                                c.stride[0], c.padding[0], relu, residual=residual, in_nchw=in_nchw, ascale=ascale)
 
 
 class FoldedTail:
