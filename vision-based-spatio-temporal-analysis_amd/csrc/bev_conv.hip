@@ -83,6 +83,7 @@ struct ConvArgs {
     // per-(image, input channel) multiplier of the A operand (SqueezeExcite excitation folded into
     // the projection conv's loader: conv(x * gate)); NULL = none.  Fast and contiguous loaders only.
     const float *__restrict__ ascale;
+    int xcd;  // 1: XCD-aware block order (the N tiles of one M block run on one XCD, sharing its L2)
 };
 
 // Per-thread view of the A tile rows it loads: rows (tid >> 3) + 32 r, one 16-B quad.
@@ -328,8 +329,16 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     const int lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
     const int n_tiles = (a.Co + BN - 1) / BN;
-    const int64_t m0 = (int64_t)(blockIdx.x / n_tiles) * BM;
-    const int n0 = (blockIdx.x % n_tiles) * BN;
+    // Consecutive blockIdx.x go round-robin over the 8 XCDs; with a.xcd the logical tile order is
+    // remapped so each XCD walks a contiguous run: the n_tiles blocks that read the same A rows are
+    // dispatched together on one XCD and share its L2 instead of fetching A once per XCD.
+    unsigned bid = blockIdx.x;
+    if (a.xcd) {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int64_t m0 = (int64_t)(bid / n_tiles) * BM;
+    const int n0 = (bid % n_tiles) * BN;
 
     typename std::conditional<
         LOADER == 1, LoaderFast<AROWS>,
@@ -753,6 +762,14 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
 
 int g_conv_tile = 0;
 
+inline int conv_xcd() {
+    static const int v = [] {
+        const char *e = getenv("BEV_CONV_XCD");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 // Tile choice + launch.  Cost model (measured on MI355X, tools/conv_micro.py
 // A/B): time ~ rounds of resident blocks (256 CUs x 2 blocks) x tile area; ties
 // go to the larger tile (better operand reuse).  Candidates: 1 = 128x128,
@@ -873,6 +890,7 @@ static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci,
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
     a.ascale = ascale;
+    a.xcd = conv_xcd();
     if (in_nchw && Ci == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && Co <= 64 && !residual && bias &&
         g_conv_tile == 0 && relu <= 1 && !ascale)
         return launch_stem(x, N, H, W, packed, a.Kp, bias, Co, y, Ho, Wo, relu, (hipStream_t)stream);
@@ -911,6 +929,7 @@ int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const flo
     a.in_nchw = 0;
     a.x2 = x2;
     a.ascale = nullptr;
+    a.xcd = conv_xcd();
     a.Ci2 = Ci2;
     a.H2 = H2;
     a.W2 = W2;
