@@ -201,6 +201,32 @@ int bev_se_gate_f32(const float *psum, int N, int nb, int C, int hw, const float
 /* device: in place y[n, p, c] *= gate[n, c] for y [N][P][C] (SE excitation, x * gate). */
 int bev_channel_scale_f32(float *y, int N, int64_t P, int C, const float *gate, void *stream);
 
+/* ---------------------------------------------------------------------------
+ * Trunk backward (training, BASELINE config 3: train.py:249-255 backpropagates
+ * through the timm trunk).  NHWC fp32; BN is frozen (folded) in training.
+ * ------------------------------------------------------------------------- */
+
+/* dz = dy * (y > 0): ReLU backward from the saved output.  n % 4 == 0. */
+int bev_relu_bwd_f32(const float *dy, const float *y, float *dz, int64_t n, void *stream);
+
+/* out [N][Hd][Wd][C] = 0 except out[n][top + s*oy][left + s*ox][c] = dz[n][oy][ox][c]
+ * (zero-inserted, padded gradient: turns a strided conv's dgrad into a stride-1 conv). */
+int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd, int Wd,
+                        float *out, void *stream);
+
+/* dW [Co][KH*KW*Ci] (k = (ky*KW + kx)*Ci + ci, OVERWRITTEN) = sum over output pixels of
+ * dz[m][co] * im2col(x)[m][k] (conv weight gradient; float atomics across m-splits). */
+int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,
+                       int KW, int stride, int pad, float *dW, void *stream);
+
+/* db [C] (OVERWRITTEN) = sum over m of dz[m][c] (bias / BN-shift gradient). */
+int bev_colsum_f32(const float *dz, int64_t M, int C, float *db, void *stream);
+
+/* dx [N][H][W][C] (OVERWRITTEN): max-pool backward with ATen's window argmax rule
+ * (first maximum in scan order, NaN wins). */
+int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride, int pad,
+                               int Ho, int Wo, float *dx, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

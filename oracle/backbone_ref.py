@@ -24,9 +24,11 @@ def _cbr(x, conv, bn, relu=True):
     return F.relu(y) if relu else y
 
 
-def resnet_features(net, x, out_index: int):
-    """features_only[out_index] of a timm-named ResNet `net` on NCHW x (any device; CPU in practice)."""
-    with torch.no_grad():
+def resnet_features(net, x, out_index: int, grad: bool = False):
+    """features_only[out_index] of a timm-named ResNet `net` on NCHW x (any device; CPU in practice).
+    BN always uses the running statistics (the native trunk's frozen-BN training semantics); with
+    grad=True autograd records the graph (reference for the native trunk backward)."""
+    with torch.set_grad_enabled(grad):
         y = _cbr(x, net.conv1, net.bn1)
         if out_index == 0:
             return y

@@ -172,3 +172,47 @@ def test_bevnet_ddp_training_frozen_trunk():
         assert losses[-1] < losses[0], losses
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_trunk_backward_vs_torch_autograd(name):
+    """Native trunk training path (frozen BN) vs torch CPU autograd on the same weights: the loss gradient
+    w.r.t. every trunk parameter and the encoder proj (floating point, atomics in wgrad: rel 1e-3)."""
+    import backbone_ref
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(0)
+    enc = CNNEncoder(out_channels=16, backbone=name, pretrained=False)
+    g = torch.Generator().manual_seed(3)
+    for m in enc.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m.running_mean.copy_(torch.rand(m.num_features, generator=g) * 0.4 - 0.2)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.bias.data.copy_(torch.rand(m.num_features, generator=g) * 0.4 - 0.2)
+    imgs = torch.randn(1, 2, 3, 70, 98, generator=g)
+    with torch.no_grad():
+        enc.eval().to(DEV)(imgs.to(DEV))  # builds the lazy proj
+    enc.train()
+    y = enc(imgs.to(DEV))
+    r = torch.randn(y.shape, generator=g)
+    (y * r.to(DEV)).sum().backward()
+    got = {k: p.grad.detach().cpu() for k, p in enc.named_parameters() if p.grad is not None}
+    enc_c = enc.to("cpu")
+    enc_c.zero_grad(set_to_none=True)
+    f = backbone_ref.resnet_features(enc_c.backbone, imgs.reshape(-1, 3, 70, 98), enc_c.out_index, grad=True)
+    yc = F.conv2d(f, enc_c.proj.weight, enc_c.proj.bias)
+    (yc.reshape(y.shape) * r).sum().backward()
+    worst, n = 0.0, 0
+    for k, p in enc_c.named_parameters():
+        ref = p.grad
+        if ref is None:  # stages past out_index are not executed (features_only, cnn_encoder.py:41-42)
+            assert k not in got, k
+            continue
+        assert k in got, k
+        n += 1
+        err = (got[k] - ref).abs().max().item() / max(ref.abs().max().item(), 1e-12)
+        worst = max(worst, err)
+        assert err < 1e-3, (k, err)
+    assert n > 20 and worst > 0.0

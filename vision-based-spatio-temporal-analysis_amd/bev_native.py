@@ -47,6 +47,11 @@ SIGNATURES = {
     "bev_conv2d_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_conv2d_chscale_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i,
                                     _vp]),
+    "bev_relu_bwd_f32": (_i, [_vp, _vp, _vp, _i64, _vp]),
+    "bev_dilate_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_conv_wgrad_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_colsum_f32": (_i, [_vp, _i64, _i, _vp, _vp]),
+    "bev_maxpool2d_bwd_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
@@ -398,3 +403,56 @@ def nhwc_to_nchw(x: torch.Tensor) -> torch.Tensor:
     y = torch.empty(N, C, H, W, device=x.device, dtype=torch.float32)
     _check(lib().bev_nhwc_to_nchw_f32(_ptr(x), N, C, H, W, _ptr(y), _stream(x)), "bev_nhwc_to_nchw_f32")
     return y
+
+
+# ---------------------------------------------------------------------------
+# trunk backward (training)
+# ---------------------------------------------------------------------------
+def relu_bwd(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    dy, y = dy.contiguous(), y.contiguous()
+    _require_gpu(dy, y)
+    dz = torch.empty_like(y)
+    _check(lib().bev_relu_bwd_f32(_ptr(dy), _ptr(y), _ptr(dz), y.numel(), _stream(y)), "bev_relu_bwd_f32")
+    return dz
+
+
+def dilate_nhwc(dz: torch.Tensor, s: int, top: int, left: int, Hd: int, Wd: int) -> torch.Tensor:
+    dz = dz.contiguous()
+    _require_gpu(dz)
+    N, Ho, Wo, C = dz.shape
+    out = torch.empty(N, Hd, Wd, C, device=dz.device, dtype=torch.float32)
+    _check(lib().bev_dilate_nhwc_f32(_ptr(dz), N, Ho, Wo, C, s, top, left, Hd, Wd, _ptr(out), _stream(dz)),
+           "bev_dilate_nhwc_f32")
+    return out
+
+
+def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stride: int, pad: int) -> torch.Tensor:
+    """x [N,H,W,Ci], dz [N,Ho,Wo,Co] (NHWC) -> dW [Co, Ci, KH, KW] (torch OIHW)."""
+    x, dz = x.contiguous(), dz.contiguous()
+    _require_gpu(x, dz)
+    N, H, W, Ci = x.shape
+    _, Ho, Wo, Co = dz.shape
+    dW = torch.empty(Co, KH, KW, Ci, device=x.device, dtype=torch.float32)
+    _check(lib().bev_conv_wgrad_f32(_ptr(x), N, H, W, Ci, _ptr(dz), Ho, Wo, Co, KH, KW, stride, pad, _ptr(dW),
+                                    _stream(x)), "bev_conv_wgrad_f32")
+    return dW.permute(0, 3, 1, 2)
+
+
+def colsum(dz: torch.Tensor) -> torch.Tensor:
+    dz = dz.contiguous()
+    _require_gpu(dz)
+    C = dz.shape[-1]
+    db = torch.empty(C, device=dz.device, dtype=torch.float32)
+    _check(lib().bev_colsum_f32(_ptr(dz), dz.numel() // C, C, _ptr(db), _stream(dz)), "bev_colsum_f32")
+    return db
+
+
+def maxpool_bwd_nhwc(x: torch.Tensor, dy: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tensor:
+    x, dy = x.contiguous(), dy.contiguous()
+    _require_gpu(x, dy)
+    N, H, W, C = x.shape
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    dx = torch.empty_like(x)
+    _check(lib().bev_maxpool2d_bwd_nhwc_f32(_ptr(x), _ptr(dy), N, H, W, C, k, stride, pad, Ho, Wo, _ptr(dx),
+                                            _stream(x)), "bev_maxpool2d_bwd_nhwc_f32")
+    return dx

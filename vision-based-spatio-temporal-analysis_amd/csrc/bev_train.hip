@@ -1,0 +1,249 @@
+// bev_train.hip -- backward kernels of the backbone trunk for gfx950 (training, BASELINE config 3).
+//
+// The reference trains its timm trunk through torch autograd (train.py:249-255, the optimizer holds the
+// trunk parameters: model_wrapper.py lazy modules do not exist yet when it is built, quirk Q2).  Here
+// every conv + (frozen, folded) BN + ReLU of the trunk has an autograd node whose backward runs:
+//
+//   k_relu_bwd     dz = dy * (y > 0)                                   (ReLU mask from the saved output)
+//   k_dilate       zero-inserted, padded copy of dz for strided dgrad  (so dgrad is a stride-1 conv)
+//   bev_conv2d_f32 dx = conv(dilate(dz), flip(W)^T)                    (the forward MFMA kernel)
+//   k_wgrad        dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k]       (LDS-tiled, split over m, f32 atomics)
+//   k_colsum       db[co] = sum_m dz[m][co]
+//   k_maxpool_bwd  dx = sum of dy over the windows whose first maximum is this input (gather, no atomics)
+//
+// All tensors NHWC fp32.  Float atomics in k_wgrad / k_colsum: the last bits of the weight gradients
+// may vary run to run (summation order); the activations' gradients are deterministic.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+inline int last() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+__global__ __launch_bounds__(256) void k_relu_bwd(const float *__restrict__ dy, const float *__restrict__ y,
+                                                  float *__restrict__ dz, int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const float4 g = ((const float4 *)dy)[i], v = ((const float4 *)y)[i];
+        ((float4 *)dz)[i] = make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f,
+                                        v.w > 0.f ? g.w : 0.f);
+    }
+}
+
+// out [N][Hd][Wd][C] (zero everywhere else): out[n][top + oy*s][left + ox*s][c] = dz[n][oy][ox][c]
+__global__ __launch_bounds__(256) void k_dilate(const float *__restrict__ dz, int N, int Ho, int Wo, int C, int s,
+                                                int top, int left, int Hd, int Wd, float *__restrict__ out) {
+    const int64_t total = (int64_t)N * Hd * Wd * (C / 4);
+    const int C4 = C / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % C4);
+        int64_t t = i / C4;
+        const int x = (int)(t % Wd);
+        t /= Wd;
+        const int y = (int)(t % Hd);
+        const int n = (int)(t / Hd);
+        const int yy = y - top, xx = x - left;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (yy >= 0 && xx >= 0 && yy % s == 0 && xx % s == 0 && yy / s < Ho && xx / s < Wo)
+            v = ((const float4 *)dz)[(((int64_t)n * Ho + yy / s) * Wo + xx / s) * C4 + c4];
+        ((float4 *)out)[i] = v;
+    }
+}
+
+// dW[co][k], k = (ky*KW + kx)*Ci + ci.  Workgroup = 64 (co) x 64 (k) outputs, 256 threads x (4 x 4);
+// loops over its slice of m in steps of 16 with both operands staged in LDS.
+constexpr int WG_T = 64, WG_M = 16;
+__global__ __launch_bounds__(256) void k_wgrad(const float *__restrict__ x, const float *__restrict__ dz, int N, int H,
+                                               int W, int Ci, int Ho, int Wo, int Co, int KH, int KW, int stride,
+                                               int pad, int64_t mchunk, float *__restrict__ dW) {
+    __shared__ float sa[WG_M][WG_T + 4];  // im2col(x)[m][k]
+    __shared__ float sd[WG_M][WG_T + 4];  // dz[m][co]
+    const int K = KH * KW * Ci;
+    const int k0 = blockIdx.x * WG_T, co0 = blockIdx.y * WG_T;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int64_t mb = (int64_t)blockIdx.z * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;  // 16 x 16 threads, 4 x 4 each
+    float acc[4][4] = {};
+    for (int64_t m = mb; m < me; m += WG_M) {
+        // stage: 16 rows x 64 columns of each operand, 4 elements per thread each
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int idx = tid + 256 * e, r = idx >> 6, c = idx & 63;
+            const int64_t mm = m + r;
+            float av = 0.f, dv = 0.f;
+            if (mm < me) {
+                const int ox = (int)(mm % Wo);
+                const int64_t t = mm / Wo;
+                const int oy = (int)(t % Ho), n = (int)(t / Ho);
+                const int k = k0 + c;
+                if (k < K) {
+                    const int ci = k % Ci, rr = k / Ci, kx = rr % KW, ky = rr / KW;
+                    const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+                    if (iy >= 0 && iy < H && ix >= 0 && ix < W) av = x[(((int64_t)n * H + iy) * W + ix) * Ci + ci];
+                }
+                if (co0 + c < Co) dv = dz[mm * Co + co0 + c];
+            }
+            sa[r][c] = av;
+            sd[r][c] = dv;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < WG_M; ++r) {
+            float a4[4], d4[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                d4[i] = sd[r][tr * 4 + i];
+                a4[i] = sa[r][tc * 4 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fmaf(d4[i], a4[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int co = co0 + tr * 4 + i;
+        if (co >= Co) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = k0 + tc * 4 + j;
+            if (k < K) atomicAdd(dW + (int64_t)co * K + k, acc[i][j]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ dz, int64_t M, int C, int64_t mchunk,
+                                                float *__restrict__ db) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const int64_t mb = (int64_t)blockIdx.y * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    float s = 0.f;
+    for (int64_t m = mb; m < me; ++m) s += dz[m * C + c];
+    atomicAdd(db + c, s);
+}
+
+// torch max_pool2d CPU/GPU semantics: the FIRST maximum in window scan order (ky, kx) wins; NaN wins.
+__global__ __launch_bounds__(256) void k_maxpool_bwd(const float *__restrict__ x, const float *__restrict__ dy, int N,
+                                                     int H, int W, int C, int k, int s, int p, int Ho, int Wo,
+                                                     float *__restrict__ dx) {
+    const int64_t total = (int64_t)N * H * W * C;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(i % C);
+        int64_t t = i / C;
+        const int ix = (int)(t % W);
+        t /= W;
+        const int iy = (int)(t % H);
+        const int n = (int)(t / H);
+        float g = 0.f;
+        // output windows covering (iy, ix): oy*s - p <= iy <= oy*s - p + k - 1
+        const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(Ho - 1, (iy + p) / s);
+        const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(Wo - 1, (ix + p) / s);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                // ATen max_pool2d: maxval = -inf, index = first in-bounds tap; update if (v > maxval || isnan(v))
+                int by = -1, bx = -1;
+                float best = -__builtin_inff();
+                for (int ky = 0; ky < k; ++ky) {
+                    const int yy = oy * s - p + ky;
+                    if (yy < 0 || yy >= H) continue;
+                    for (int kx = 0; kx < k; ++kx) {
+                        const int xx = ox * s - p + kx;
+                        if (xx < 0 || xx >= W) continue;
+                        const float v = x[(((int64_t)n * H + yy) * W + xx) * C + c];
+                        if (by < 0) {
+                            by = yy;
+                            bx = xx;
+                        }
+                        if (v > best || v != v) {
+                            best = v;
+                            by = yy;
+                            bx = xx;
+                        }
+                    }
+                }
+                if (by == iy && bx == ix) g += dy[(((int64_t)n * Ho + oy) * Wo + ox) * C + c];
+            }
+        dx[i] = g;
+    }
+}
+
+inline unsigned grid_for(int64_t n) {
+    const int64_t b = (n + 255) / 256;
+    return (unsigned)(b < 256 * 64 ? (b > 0 ? b : 1) : 256 * 64);
+}
+
+}  // namespace
+
+extern "C" {
+
+int bev_relu_bwd_f32(const float *dy, const float *y, float *dz, int64_t n, void *stream) {
+    if (!dy || !y || !dz || n < 0 || n % 4 != 0) return BEV_ERR_ARGS;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_relu_bwd, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, dy, y, dz, n / 4);
+    return last();
+}
+
+int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd, int Wd,
+                        float *out, void *stream) {
+    if (!dz || !out || N < 0 || Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0 || s <= 0 || top < 0 || left < 0 ||
+        top + s * (Ho - 1) >= Hd || left + s * (Wo - 1) >= Wd)
+        return BEV_ERR_ARGS;
+    const int64_t total = (int64_t)N * Hd * Wd * (C / 4);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_dilate, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dz, N, Ho, Wo, C, s, top,
+                       left, Hd, Wd, out);
+    return last();
+}
+
+int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,
+                       int KW, int stride, int pad, float *dW, void *stream) {
+    if (!x || !dz || !dW || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+        pad < 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1) return BEV_ERR_ARGS;
+    const int K = KH * KW * Ci;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(dW, 0, (size_t)Co * K * sizeof(float), st) != hipSuccess) return last();
+    if (M == 0) return 0;
+    const int gx = (K + WG_T - 1) / WG_T, gy = (Co + WG_T - 1) / WG_T;
+    int64_t splits = 2048 / ((int64_t)gx * gy) + 1;  // >= ~2048 workgroups
+    int64_t mchunk = (M + splits - 1) / splits;
+    mchunk = ((mchunk + WG_M - 1) / WG_M) * WG_M;
+    splits = (M + mchunk - 1) / mchunk;
+    if (splits > 65535) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL(k_wgrad, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KH,
+                       KW, stride, pad, mchunk, dW);
+    return last();
+}
+
+int bev_colsum_f32(const float *dz, int64_t M, int C, float *db, void *stream) {
+    if (!dz || !db || M < 0 || C <= 0) return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(db, 0, (size_t)C * sizeof(float), st) != hipSuccess) return last();
+    if (M == 0) return 0;
+    const int64_t splits = M < 1024 ? 1 : 1024;
+    const int64_t mchunk = (M + splits - 1) / splits;
+    hipLaunchKernelGGL(k_colsum, dim3((C + 255) / 256, (unsigned)((M + mchunk - 1) / mchunk)), dim3(256), 0, st, dz,
+                       M, C, mchunk, db);
+    return last();
+}
+
+int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride, int pad,
+                               int Ho, int Wo, float *dx, void *stream) {
+    if (!x || !dy || !dx || N < 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || stride <= 0 || pad < 0) return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1) return BEV_ERR_ARGS;
+    const int64_t total = (int64_t)N * H * W * C;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, dy, N, H, W, C, k,
+                       stride, pad, Ho, Wo, dx);
+    return last();
+}
+
+}  // extern "C"

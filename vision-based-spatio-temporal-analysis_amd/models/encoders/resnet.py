@@ -10,6 +10,9 @@ state_dict loads unchanged.  Parity with timm itself is therefore UNPINNED;
 the conv kernels are pinned against a torch fp32 reference of the same
 weights (oracle/backbone_ref.py, tests/test_backbone_gpu.py).
 
+Training (train mode with gradients): one autograd node per conv + frozen BN on
+the native forward / backward kernels (trunk_grad.py).
+
 Execution (inference / eval mode): activations stay channels-last (NHWC) on
 the device; every conv+BN(+residual)(+ReLU) is ONE `bev_conv2d_f32` launch
 with batch-norm folded into the packed weights and bias; the stem reads the
@@ -209,7 +212,7 @@ class ResNet(nn.Module):
     def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC feature map of features_only[out_index]."""
         if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("native ResNet executes eval-mode (folded BN) inference only")
+            return self._forward_train(x, out_index)
         y = self._fc(self.conv1, self.bn1)(x, relu=True, in_nchw=True)  # act1: index 0
         if out_index == 0:
             return y
@@ -217,6 +220,30 @@ class ResNet(nn.Module):
         for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
             for blk in layer:
                 y = self._block(blk, y)
+            if li == out_index:
+                return y
+        return y
+
+    def _forward_train(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
+        """Training: the same graph with one autograd node per conv + frozen BN (+ residual) (+ ReLU)
+        and native backward kernels (trunk_grad.py).  No bottleneck-tail fusion (the shortcut's
+        gradient is a separate conv backward)."""
+        from .trunk_grad import MaxPool, conv_bn_act
+        y = conv_bn_act(self.conv1, self.bn1, x, relu=True, in_nchw=True)
+        if out_index == 0:
+            return y
+        y = MaxPool.apply(y, 3, 2, 1)
+        for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
+            for blk in layer:
+                sc = y
+                if blk.downsample is not None:
+                    sc = conv_bn_act(blk.downsample[0], blk.downsample[1], y, relu=False)
+                chain = blk.convs()
+                h = y
+                for idx, (conv, bn, relu) in enumerate(chain):
+                    last = idx == len(chain) - 1
+                    h = conv_bn_act(conv, bn, h, relu=relu, residual=sc if last else None)
+                y = h
             if li == out_index:
                 return y
         return y

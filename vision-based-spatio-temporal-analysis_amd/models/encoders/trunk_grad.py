@@ -1,0 +1,100 @@
+"""Autograd for the backbone trunk on the HIP kernels (training; BASELINE config 3).
+
+The reference trains the timm trunk through torch autograd (train.py:249-255; its optimizer holds
+exactly the trunk parameters, quirk Q2).  Here every conv + BN (+ residual) (+ ReLU) of the trunk is
+ONE autograd node, `ConvBNAct`, whose forward is the same folded MFMA conv as inference and whose
+backward runs native kernels:
+
+  dz  = dy * (y > 0)                         bev_relu_bwd_f32 (from the saved output)
+  dx  = conv(dilate(dz), flip(W_f)^T)        bev_dilate_nhwc_f32 + bev_conv2d_f32 (stride 1, MFMA)
+  dWf = sum_m dz (x) im2col(x)               bev_conv_wgrad_f32
+  dbf = sum_m dz                             bev_colsum_f32
+  residual gradient = dz
+
+BatchNorm is FROZEN in training (running statistics folded into the conv, the usual setting for
+fine-tuning a detection backbone): W_f = W * s, b_f = beta - mean * s with s = gamma / sqrt(var + eps),
+so dW = dWf * s, dgamma = (sum dWf * W - mean * dbf) / sqrt(var + eps), dbeta = dbf (tiny
+parameter-sized ops).  Running statistics are not updated.  Deviation from timm's train-mode BN
+(batch statistics): documented in DESIGN.md.  `MaxPool` backward: bev_maxpool2d_bwd_nhwc_f32.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+import bev_native as _nat
+
+__all__ = ["ConvBNAct", "MaxPool", "conv_bn_act"]
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    with torch.no_grad():
+        w = conv.weight.detach().float()
+        r = torch.rsqrt(bn.running_var.detach().float() + bn.eps)
+        s = bn.weight.detach().float() * r
+        wf = (w * s.view(-1, 1, 1, 1)).contiguous()
+        bf = (bn.bias.detach().float() - bn.running_mean.detach().float() * s).contiguous()
+    return wf, bf, s, r
+
+
+def _dgrad(dz: torch.Tensor, wf: torch.Tensor, H: int, W: int, stride: int, pad: int) -> torch.Tensor:
+    """Input gradient of conv(x, wf, stride, pad) for x [N,H,W,Ci] NHWC, as a stride-1 MFMA conv."""
+    Co, Ci, K, _ = wf.shape
+    wt = wf.flip(2, 3).transpose(0, 1).contiguous()  # [Ci][Co][K][K]
+    packed = _nat.pack_conv_weight(wt)
+    zero = torch.zeros(Ci, device=dz.device, dtype=torch.float32)
+    q = K - 1 - pad
+    if stride == 1:
+        return _nat.conv2d_nhwc(dz, packed, zero, Ci, K, K, 1, q, False)
+    N, Ho, Wo, _ = dz.shape
+    ry, rx = (H + 2 * pad - K) % stride, (W + 2 * pad - K) % stride
+    Hd, Wd = stride * (Ho - 1) + 1 + 2 * q + ry, stride * (Wo - 1) + 1 + 2 * q + rx
+    d = _nat.dilate_nhwc(dz, stride, q, q, Hd, Wd)
+    return _nat.conv2d_nhwc(d, packed, zero, Ci, K, K, 1, 0, False)
+
+
+class ConvBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, conv, bn, relu: bool, in_nchw: bool, residual):
+        wf, bf, s, r = _fold(conv, bn)
+        k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        y = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(wf), bf, conv.out_channels, k, k, st, p, relu,
+                             residual=residual, in_nchw=in_nchw)
+        ctx.save_for_backward(x, y if relu else None, wf, s, r, weight)
+        ctx.meta = (conv, bn, relu, in_nchw, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, wf, s, r, weight = ctx.saved_tensors
+        conv, bn, relu, in_nchw, has_res = ctx.meta
+        k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        dy = dy.contiguous().float()
+        dz = _nat.relu_bwd(dy, y) if relu else dy
+        xn = _nat.nchw_to_nhwc(x) if in_nchw else x
+        H, W = xn.shape[1], xn.shape[2]
+        dx = _dgrad(dz, wf, H, W, st, p) if (ctx.needs_input_grad[0] and not in_nchw) else None
+        dwf = _nat.conv_wgrad(xn, dz, k, k, st, p)
+        dbf = _nat.colsum(dz)
+        dw = dwf * s.view(-1, 1, 1, 1)
+        ds = (dwf * weight.detach().float()).sum((1, 2, 3)) - bn.running_mean.detach().float() * dbf
+        dgamma = ds * r
+        return dx, dw, dgamma, dbf, None, None, None, None, (dz if has_res else None)
+
+
+def conv_bn_act(conv: nn.Conv2d, bn: nn.BatchNorm2d, x, relu: bool, residual=None, in_nchw: bool = False):
+    return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, relu, in_nchw, residual)
+
+
+class MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k: int, stride: int, pad: int):
+        ctx.save_for_backward(x)
+        ctx.meta = (k, stride, pad)
+        return _nat.maxpool_nhwc(x, k, stride, pad)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        k, stride, pad = ctx.meta
+        return _nat.maxpool_bwd_nhwc(x, dy.contiguous().float(), k, stride, pad), None, None, None
