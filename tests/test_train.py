@@ -216,3 +216,34 @@ def test_trunk_backward_vs_torch_autograd(name):
         worst = max(worst, err)
         assert err < 1e-3, (k, err)
     assert n > 20 and worst > 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_bevnet_training_trunk_end_to_end():
+    """The reference's training step (train.py:249-255, fp32) on BEVNet with the TRUNK trainable: every
+    trunk conv / BN parameter up to out_index receives a gradient through the native backward."""
+    import bev_dist
+    import bev_rig
+    from models.model_wrapper import BEVNet
+    torch.manual_seed(0)
+    B, V, H, W = 1, 3, 128, 224
+    model = BEVNet(_bevnet_cfg()).to(DEV)
+    K, Rt = bev_rig.rig(V, H, W, B)
+    g = torch.Generator().manual_seed(1)
+    batch = {"images": torch.randn(B, V, 3, H, W, generator=g).to(DEV),
+             "calib": {"intrinsic": torch.from_numpy(K).to(DEV), "extrinsic": torch.from_numpy(Rt).to(DEV)}}
+    targets = [{"boxes_world": torch.tensor([[1.0, 0.5, 0.6, 0.6], [-3.0, 2.0, 0.6, 0.6]], device=DEV)}]
+    bev_dist.materialize_lazy(model, batch)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    w0 = model.encoder.backbone.conv1.weight.detach().clone()
+    losses = [bev_dist.train_step(model, batch, targets, opt)["total_loss"] for _ in range(4)]
+    assert all(np.isfinite(losses)), losses
+    bb = model.encoder.backbone
+    for name in ("conv1.weight", "bn1.weight", "layer1.0.conv1.weight", "layer2.0.downsample.0.weight"):
+        p = dict(bb.named_parameters())[name]
+        assert p.grad is not None and p.grad.abs().sum().item() > 0, name
+    assert dict(bb.named_parameters())["layer4.0.conv1.weight"].grad is None  # past out_index: not executed
+    assert not torch.equal(bb.conv1.weight.detach(), w0)
+    assert losses[-1] < losses[0], losses

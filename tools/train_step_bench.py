@@ -1,0 +1,88 @@
+"""Training-step timing (BASELINE config 3 shape, one GPU): ResNet-50 trunk + proj -> IPM warp -> head.
+
+    python tools/train_step_bench.py [--steps 5] [--bevnet]
+
+Default: the hot path alone -- CNNEncoder (trunk trainable, native forward + backward) -> fused warp
++ mean (native forward + backward) -> sum(out * r) -> Adam step.  --bevnet: the full BEVNet (encoder,
+per-view warp, concat, BEV proj, CenterNet head, focal/L1 loss) with the reference's training step
+(train.py:249-255, fp32).  7 cameras x 3 x 1080 x 1920 synthetic images, Appendix-B rig, B = 1.
+Prints one JSON line: ms per training step and frames/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "vision-based-spatio-temporal-analysis_amd"))
+
+import torch  # noqa: E402
+
+import bev_rig  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--bevnet", action="store_true")
+    ap.add_argument("--backbone", default="resnet50")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    V, H, W = 7, 1080, 1920
+    K, Rt = bev_rig.rig(V, H, W, 1)
+    Kd, Rtd = torch.from_numpy(K).to(dev), torch.from_numpy(Rt).to(dev)
+    images = torch.randn(1, V, 3, H, W, device=dev)
+    if a.bevnet:
+        from models.model_wrapper import BEVNet
+        cfg = {"MODEL": {"BACKBONE": a.backbone, "PRETRAINED": False, "FEAT_DIM": 64, "OUT_INDEX": 2,
+                         "BEV_SIZE": [32, 480, 1440], "BEV_BOUNDS": [-24.0, 24.0, -7.2, 7.2], "BEV_PROJ_CH": 64},
+               "LOSS": {}, "EVAL": {"CONF_THRESH": 0.99}}
+        model = BEVNet(cfg).to(dev)
+        batch = {"images": images, "calib": {"intrinsic": Kd, "extrinsic": Rtd}}
+        targets = [{"boxes_world": torch.tensor([[1.0, 0.5, 0.6, 0.6], [-3.0, 2.0, 0.6, 0.6]], device=dev)}]
+        with torch.no_grad():
+            model.eval()(batch)
+        model.train()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            loss = model.loss(model(batch), targets, {})["total_loss"]
+            loss.backward()
+            opt.step()
+            return loss
+    else:
+        from models.encoders.cnn_encoder import CNNEncoder
+        from models.fusion.geometry import GeometryTransformer
+        enc = CNNEncoder(out_channels=64, backbone=a.backbone, pretrained=False).to(dev)
+        geom = GeometryTransformer(480, 1440, (-24.0, 24.0, -7.2, 7.2))
+        with torch.no_grad():
+            enc.eval()(images)
+        enc.train()
+        opt = torch.optim.Adam(enc.parameters(), lr=1e-4)
+        r = torch.randn(1, 64, 480, 1440, device=dev)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            out = geom.forward_fused(enc(images), Kd, Rtd, (H, W), "mean")
+            loss = (out * r).sum()
+            loss.backward()
+            opt.step()
+            return loss
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({"what": "bevnet train step" if a.bevnet else "hot-path train step", "backbone": a.backbone,
+                      "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
+                      "loss": float(loss)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
