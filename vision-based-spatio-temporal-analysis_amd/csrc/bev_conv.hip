@@ -771,27 +771,42 @@ inline int conv_xcd() {
 }
 
 // Tile choice + launch.  Cost model (measured on MI355X, tools/conv_micro.py
-// A/B): time ~ rounds of resident blocks (256 CUs x 2 blocks) x tile area; ties
-// go to the larger tile (better operand reuse).  Candidates: 1 = 128x128,
-// 3 = 64x128, 2 = 128x64.
+// A/B): time ~ rounds of resident blocks x tile area; ties go to the larger
+// tile (better operand reuse).  Candidates: 1 = 128x128 (2 blocks per CU),
+// 3 = 64x128 and 2 = 128x64, both with ONE LDS staging buffer so 3 blocks
+// fit per CU (r01e A/B over the ResNet-50 layers: the extra resident block
+// hides more of the load / epilogue latency than the second barrier per K
+// step costs -- 1x1 layers -4..-13 %, 3x3 layers -4..-7 %, bottleneck tails
+// -8..-13 %).  Small-M 128x64 launches (< 2 full rounds) keep the double
+// buffer.  BEV_CONV_NBUF=1|2 forces the staging depth of tiles 2 / 3.
 int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
+    const int64_t M = a.M;
+    const int Co = a.Co;
+    static const int nbuf_env = [] {
+        const char *e = getenv("BEV_CONV_NBUF");
+        return e ? atoi(e) : 0;
+    }();
+    auto nbuf1_for = [&](int tile) {
+        if (nbuf_env == 1 || nbuf_env == 2) return nbuf_env == 1;
+        return tile == 3 || M >= 400000;
+    };
     int tile = g_conv_tile;
     if (tile == 0) {
-        const int64_t M = a.M;
-        const int Co = a.Co;
-        auto cost = [&](int bm, int bn) {
+        auto cost = [&](int bm, int bn, int resident) {
             const int64_t blocks = ((M + bm - 1) / bm) * ((Co + bn - 1) / bn);
-            return (double)((blocks + 511) / 512) * bm * bn;
+            return (double)((blocks + resident - 1) / resident) * bm * bn;
         };
-        const double c1 = cost(128, 128), c3 = cost(64, 128), c2 = cost(128, 64);
+        const double c1 = cost(128, 128, 512), c3 = cost(64, 128, nbuf1_for(3) ? 768 : 512),
+                     c2 = cost(128, 64, nbuf1_for(2) ? 768 : 512);
         tile = 1;
         double best = c1;
         if (c3 < 0.95 * best) { tile = 3; best = c3; }
         if (c2 < 0.95 * best) { tile = 2; best = c2; }
     }
-    static const bool nbuf1 = getenv("BEV_CONV_NBUF1") != nullptr;
-    if (tile == 2) return nbuf1 ? launch_conv<4, 1, 1, 2, 1>(a, loader, st) : launch_conv<4, 1, 1, 2>(a, loader, st);
-    if (tile == 3) return nbuf1 ? launch_conv<2, 2, 1, 2, 1>(a, loader, st) : launch_conv<2, 2, 1, 2>(a, loader, st);
+    if (tile == 2)
+        return nbuf1_for(2) ? launch_conv<4, 1, 1, 2, 1>(a, loader, st) : launch_conv<4, 1, 1, 2>(a, loader, st);
+    if (tile == 3)
+        return nbuf1_for(3) ? launch_conv<2, 2, 1, 2, 1>(a, loader, st) : launch_conv<2, 2, 1, 2>(a, loader, st);
     return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
 }
 
