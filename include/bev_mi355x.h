@@ -37,7 +37,7 @@ extern "C" {
 int bev_abi_version(void);
 
 /* host: performance knobs (no effect on results).  knob BEV_TUNE_CONV_TILE:
- * 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128 output tiles for
+ * 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 output tiles for
  * bev_conv2d_f32.  Returns the previous value, or BEV_ERR_ARGS. */
 #define BEV_TUNE_CONV_TILE 1
 /* knob BEV_TUNE_WARP_POOL_KB: LDS image pool of the fused warp in KiB

@@ -62,6 +62,20 @@ def test_conv_vs_torch_fp32(case):
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+@pytest.mark.parametrize("case", [CASES[3], CASES[4], CASES[6], CASES[8], CASES[9], CASES[11]],
+                         ids=["l1c2_res", "l1c3_res", "s2_3x3", "proj", "ragged_co", "contig"])
+def test_conv_every_tile_vs_torch_fp32(case, tile):
+    """Every output tile shape (128x128, 128x64, 64x128, 64x64; bev_tune BEV_TUNE_CONV_TILE) forced on
+    layers the automatic choice routes elsewhere: same results within the conv tolerance."""
+    import bev_native as nat
+    old = nat.tune(1, tile)
+    try:
+        test_conv_vs_torch_fp32(case)
+    finally:
+        nat.tune(1, old)
+
+
 DUAL_CASES = [
     # N, Ci (conv3 input), Ci2 (block input), H2, W2, s2, Co
     (2, 64, 64, 17, 23, 1, 256),     # layer1 block 0: conv3 64->256 + downsample 64->256

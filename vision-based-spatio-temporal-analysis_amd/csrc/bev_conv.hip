@@ -802,11 +802,17 @@ int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
         double best = c1;
         if (c3 < 0.95 * best) { tile = 3; best = c3; }
         if (c2 < 0.95 * best) { tile = 2; best = c2; }
+        // Single-source 1x1 layers over NHWC (Ci % 32 == 0) are HBM-bound: the 64 x 64 tile (one
+        // 32 x 32 MFMA tile per wave, ~4 resident blocks per CU) trades operand reuse for memory
+        // parallelism.  r01f A/B over ResNet-50: every such layer -1..-19 % (proj 209 -> 170 us,
+        // layer1 conv1 400 -> 352 us); 3x3 layers and the dual-source tails are slower with it.
+        if (a.KH == 1 && a.KW == 1 && loader == 1 && M >= 200000) tile = 4;
     }
     if (tile == 2)
         return nbuf1_for(2) ? launch_conv<4, 1, 1, 2, 1>(a, loader, st) : launch_conv<4, 1, 1, 2>(a, loader, st);
     if (tile == 3)
         return nbuf1_for(3) ? launch_conv<2, 2, 1, 2, 1>(a, loader, st) : launch_conv<2, 2, 1, 2>(a, loader, st);
+    if (tile == 4) return launch_conv<2, 2, 1, 1, 1>(a, loader, st);  // 64 x 64
     return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
 }
 
@@ -816,7 +822,7 @@ extern "C" {
 
 int bev_tune(int knob, int value) {
     if (knob == BEV_TUNE_CONV_TILE) {
-        if (value < 0 || value > 3) return BEV_ERR_ARGS;
+        if (value < 0 || value > 4) return BEV_ERR_ARGS;
         const int old = g_conv_tile;
         g_conv_tile = value;
         return old;
