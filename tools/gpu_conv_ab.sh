@@ -2,4 +2,5 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/ab
-timeout -k 10 300 python3 tools/conv_micro.py --iters 10 --tiles 0 4 > gpurun_out/ab/t4.log 2>&1 || exit $?
+timeout -k 10 300 python3 tools/conv_micro.py --iters 10 --tiles 0 > gpurun_out/ab/x0.log 2>&1 || exit $?
+BEV_CONV_XCD=1 timeout -k 10 300 python3 tools/conv_micro.py --iters 10 --tiles 0 > gpurun_out/ab/x1.log 2>&1 || exit $?

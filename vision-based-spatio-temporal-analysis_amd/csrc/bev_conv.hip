@@ -762,10 +762,13 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
 
 int g_conv_tile = 0;
 
+// XCD-aware block order (k_conv): on by default since the smaller r01f/r01g tiles put 2-4 N tiles
+// on every A row block; A/B over ResNet-50 (r01g, same box): 3x3 layers -3..-6 %, tails -2..-4 %,
+// 1x1 conv3 / proj -5 %, sum over the layers -1.6 %.  BEV_CONV_XCD=0 restores plain order.
 inline int conv_xcd() {
     static const int v = [] {
         const char *e = getenv("BEV_CONV_XCD");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     return v;
 }
