@@ -2,5 +2,4 @@
 set -u
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/ab
-timeout -k 10 300 python3 tools/conv_micro.py --iters 10 --tiles 0 > gpurun_out/ab/x0.log 2>&1 || exit $?
-BEV_CONV_XCD=1 timeout -k 10 300 python3 tools/conv_micro.py --iters 10 --tiles 0 > gpurun_out/ab/x1.log 2>&1 || exit $?
+timeout -k 10 300 python3 tools/conv_micro.py --iters 10 --tiles 0 1 2 3 4 > gpurun_out/ab/xt.log 2>&1 || exit $?

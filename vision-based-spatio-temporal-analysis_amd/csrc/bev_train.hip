@@ -7,7 +7,8 @@
 //   k_relu_bwd     dz = dy * (y > 0)                                   (ReLU mask from the saved output)
 //   k_dilate       zero-inserted, padded copy of dz for strided dgrad  (so dgrad is a stride-1 conv)
 //   bev_conv2d_f32 dx = conv(dilate(dz), flip(W)^T)                    (the forward MFMA kernel)
-//   k_wgrad        dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k]       (LDS-tiled, split over m, f32 atomics)
+//   k_wgrad        dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k]       (LDS-tiled, split over m, f32 atomics;
+//                  k_wgrad_v4 = float4 staging without index divisions when Ci % 64 == 0)
 //   k_colsum       db[co] = sum_m dz[m][co]
 //   k_maxpool_bwd  dx = sum of dy over the windows whose first maximum is this input (gather, no atomics)
 //
@@ -118,6 +119,75 @@ __global__ __launch_bounds__(256) void k_wgrad(const float *__restrict__ x, cons
     }
 }
 
+// Same contraction for Ci % 64 == 0 and Co % 4 == 0 (every ResNet trunk conv but the stem): a 64-wide
+// k block lies inside ONE (ky, kx) tap, so it is 64 consecutive channels of one input pixel.  Each
+// thread stages one float4 of each operand per m step (row tid >> 4, columns 4 (tid & 15)); the
+// output pixel (n, oy, ox) of its row advances incrementally -- no integer division in the loop
+// (the generic kernel spends most of its time in the per-element 64-bit index decode).
+__global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, const float *__restrict__ dz, int N,
+                                                  int H, int W, int Ci, int Ho, int Wo, int Co, int KW, int stride,
+                                                  int pad, int64_t mchunk, float *__restrict__ dW) {
+    __shared__ __attribute__((aligned(16))) float sa[WG_M][WG_T + 4];
+    __shared__ __attribute__((aligned(16))) float sd[WG_M][WG_T + 4];
+    const int k0 = blockIdx.x * WG_T, co0 = blockIdx.y * WG_T;
+    const int rr = k0 / Ci, ci0 = k0 - rr * Ci, kx = rr % KW, ky = rr / KW;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int64_t mb = (int64_t)blockIdx.z * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
+    const int r = tid >> 4, c4 = tid & 15;
+    const bool dz_ok = co0 + 4 * c4 < Co;
+    // output pixel of row mb + r
+    int64_t mm = mb + r;
+    int ox, oy, n;
+    {
+        const int64_t m0 = mm < M ? mm : 0;
+        ox = (int)(m0 % Wo);
+        const int64_t t = m0 / Wo;
+        oy = (int)(t % Ho);
+        n = (int)(t / Ho);
+    }
+    float acc[4][4] = {};
+    for (int64_t m = mb; m < me; m += WG_M, mm += WG_M) {
+        float4 av = make_float4(0.f, 0.f, 0.f, 0.f), dv = av;
+        if (mm < me) {
+            const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+            if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+                av = *(const float4 *)(x + (((int64_t)n * H + iy) * W + ix) * Ci + ci0 + 4 * c4);
+            if (dz_ok) dv = *(const float4 *)(dz + mm * Co + co0 + 4 * c4);
+        }
+        *(float4 *)&sa[r][4 * c4] = av;
+        *(float4 *)&sd[r][4 * c4] = dv;
+        ox += WG_M;
+        while (ox >= Wo) {
+            ox -= Wo;
+            if (++oy == Ho) {
+                oy = 0;
+                ++n;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < WG_M; ++q) {
+            const float4 d = *(const float4 *)&sd[q][tr * 4];
+            const float4 a = *(const float4 *)&sa[q][tc * 4];
+            const float d4[4] = {d.x, d.y, d.z, d.w}, a4[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_fmaf(d4[i], a4[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+    const int64_t ldk = (int64_t)gridDim.x * WG_T;  // = K = KH * KW * Ci (a multiple of 64): every k is valid
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int co = co0 + tr * 4 + i;
+        if (co >= Co) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) atomicAdd(dW + co * ldk + k0 + tc * 4 + j, acc[i][j]);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ dz, int64_t M, int C, int64_t mchunk,
                                                 float *__restrict__ db) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -218,8 +288,12 @@ int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float 
     mchunk = ((mchunk + WG_M - 1) / WG_M) * WG_M;
     splits = (M + mchunk - 1) / mchunk;
     if (splits > 65535) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL(k_wgrad, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KH,
-                       KW, stride, pad, mchunk, dW);
+    if (Ci % WG_T == 0 && Co % 4 == 0)
+        hipLaunchKernelGGL(k_wgrad_v4, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo,
+                           Co, KW, stride, pad, mchunk, dW);
+    else
+        hipLaunchKernelGGL(k_wgrad, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co,
+                           KH, KW, stride, pad, mchunk, dW);
     return last();
 }
 
