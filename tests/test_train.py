@@ -247,3 +247,50 @@ def test_bevnet_training_trunk_end_to_end():
     assert dict(bb.named_parameters())["layer4.0.conv1.weight"].grad is None  # past out_index: not executed
     assert not torch.equal(bb.conv1.weight.detach(), w0)
     assert losses[-1] < losses[0], losses
+
+
+WGRAD_CASES = [
+    # N, Ci, H, W, Co, k, stride, pad -- Ci % 64 == 0 routes to k_wgrad_v4, the rest to k_wgrad
+    (2, 64, 13, 17, 64, 3, 1, 1),     # layer1 3x3 (v4)
+    (1, 128, 15, 21, 128, 3, 2, 1),   # strided 3x3 (v4), Wo < 16 rows wrap several output rows per step
+    (2, 64, 9, 11, 256, 1, 1, 0),     # 1x1 expand (v4)
+    (1, 256, 15, 21, 512, 1, 2, 0),   # strided 1x1 downsample (v4)
+    (1, 64, 5, 7, 200, 1, 1, 0),      # ragged Co (v4, partial co block)
+    (1, 3, 37, 53, 64, 7, 2, 3),      # stem (generic)
+    (1, 48, 9, 10, 24, 3, 1, 1),      # Ci % 64 != 0 (generic)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", WGRAD_CASES, ids=[f"ci{c[1]}_co{c[4]}_k{c[5]}s{c[6]}" for c in WGRAD_CASES])
+def test_wgrad_and_colsum_vs_torch(case):
+    """bev_conv_wgrad_f32 / bev_colsum_f32 vs torch's conv2d weight / bias gradients (fp32; float atomics
+    change the summation order: rtol 1e-4 of the gradient scale)."""
+    import bev_native as nat
+    N, Ci, H, W, Co, k, s, p = case
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, Ci, H, W, generator=g)
+    w = torch.randn(Co, Ci, k, k, generator=g, requires_grad=True)
+    b = torch.zeros(Co, requires_grad=True)
+    y = F.conv2d(x, w, b, s, p)
+    dz = torch.randn(y.shape, generator=g)
+    y.backward(dz)
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to("cuda:0")
+    dW = nat.conv_wgrad(x.permute(0, 2, 3, 1).contiguous().to("cuda:0"), dzn, k, k, s, p).cpu()
+    db = nat.colsum(dzn).cpu()
+    scale = float(w.grad.abs().max())
+    np.testing.assert_allclose(dW.numpy(), w.grad.numpy(), rtol=0, atol=1e-4 * scale)
+    np.testing.assert_allclose(db.numpy(), b.grad.numpy(), rtol=0, atol=1e-4 * float(b.grad.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,C", [(907200, 64), (5000, 512), (3000, 256), (4097, 128), (100000, 24)])
+def test_colsum_sizes(M, C):
+    """Column sums over layer-sized and ragged row counts (k_colsum_v4 and the generic kernel)."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(M)
+    dz = torch.randn(M, C, generator=g)
+    ref = dz.double().sum(0)
+    got = nat.colsum(dz.to("cuda:0")).cpu().double()
+    tol = 1e-5 * float(dz.abs().sum(0).max())
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=0, atol=tol)

@@ -3,7 +3,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 O=$GRAFT_REPO_ROOT/gpurun_out/bwd; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_warp_gpu.py tests/test_train.py -x -v -p no:cacheprovider --timeout 240 --timeout-method thread -k "backward or train or ddp" > $O/tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_train.py -x -v -p no:cacheprovider --timeout 240 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python tools/train_step_bench.py --steps 5 > $O/hot.log 2>&1 || exit $?
 timeout -k 10 300 python tools/train_step_bench.py --steps 3 --bevnet > $O/bevnet.log 2>&1 || exit $?
