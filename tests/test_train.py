@@ -294,3 +294,21 @@ def test_colsum_sizes(M, C):
     got = nat.colsum(dz.to("cuda:0")).cpu().double()
     tol = 1e-5 * float(dz.abs().sum(0).max())
     np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=0, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,H,W", [(2, 64, 37, 53), (1, 8, 16, 16), (1, 6, 11, 13), (1, 4, 9, 7)])
+def test_maxpool_bwd_vs_torch_ties(N, C, H, W):
+    """bev_maxpool2d_bwd_nhwc_f32 (3x3 / stride 2 / pad 1, the ResNet stem pool) vs torch CPU autograd on
+    integer-valued inputs, so windows hold tied maxima: the FIRST maximum in scan order takes the
+    gradient (ATen semantics).  C % 4 == 0 runs the float4 kernel, C = 6 the scalar one.  Exact."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(C * 100 + H)
+    x = torch.randint(-3, 4, (N, C, H, W), generator=g).float().requires_grad_(True)
+    y = F.max_pool2d(x, 3, 2, 1)
+    dy = torch.randn(y.shape, generator=g)
+    y.backward(dy)
+    got = nat.maxpool_bwd_nhwc(x.detach().permute(0, 2, 3, 1).contiguous().to("cuda:0"),
+                               dy.permute(0, 2, 3, 1).contiguous().to("cuda:0"), 3, 2, 1)
+    ref = x.grad.permute(0, 2, 3, 1).contiguous()
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)

@@ -10,7 +10,8 @@
 //   k_wgrad        dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k]       (LDS-tiled, split over m, f32 atomics;
 //                  k_wgrad_v4 = float4 staging without index divisions when Ci % 64 == 0)
 //   k_colsum       db[co] = sum_m dz[m][co]
-//   k_maxpool_bwd  dx = sum of dy over the windows whose first maximum is this input (gather, no atomics)
+//   k_maxpool_bwd  dx = sum of dy over the windows whose first maximum is this input (gather, no atomics;
+//                  k_maxpool_bwd_v4: four channels per thread when C % 4 == 0)
 //
 // All tensors NHWC fp32.  Float atomics in k_wgrad / k_colsum: the last bits of the weight gradients
 // may vary run to run (summation order); the activations' gradients are deterministic.
@@ -279,6 +280,63 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd(const float *__restrict__ x
     }
 }
 
+// Same gather for C % 4 == 0, four channels per thread (float4 loads; the window / index arithmetic
+// is shared by the four channels, which the scalar kernel repeats per element).
+__global__ __launch_bounds__(256) void k_maxpool_bwd_v4(const float *__restrict__ x, const float *__restrict__ dy,
+                                                        int N, int H, int W, int C, int k, int s, int p, int Ho,
+                                                        int Wo, float *__restrict__ dx) {
+    const int C4 = C >> 2;
+    const int64_t total = (int64_t)N * H * W * C4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % C4);
+        int64_t t = i / C4;
+        const int ix = (int)(t % W);
+        t /= W;
+        const int iy = (int)(t % H);
+        const int n = (int)(t / H);
+        float g[4] = {0.f, 0.f, 0.f, 0.f};
+        const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(Ho - 1, (iy + p) / s);
+        const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(Wo - 1, (ix + p) / s);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                int by[4] = {-1, -1, -1, -1}, bx[4] = {-1, -1, -1, -1};
+                float best[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+                for (int ky = 0; ky < k; ++ky) {
+                    const int yy = oy * s - p + ky;
+                    if (yy < 0 || yy >= H) continue;
+                    for (int kx = 0; kx < k; ++kx) {
+                        const int xx = ox * s - p + kx;
+                        if (xx < 0 || xx >= W) continue;
+                        const float4 q = ((const float4 *)x)[(((int64_t)n * H + yy) * W + xx) * C4 + c4];
+                        const float v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (by[u] < 0) {
+                                by[u] = yy;
+                                bx[u] = xx;
+                            }
+                            if (v[u] > best[u] || v[u] != v[u]) {
+                                best[u] = v[u];
+                                by[u] = yy;
+                                bx[u] = xx;
+                            }
+                        }
+                    }
+                }
+                const bool hit = (by[0] == iy && bx[0] == ix) || (by[1] == iy && bx[1] == ix) ||
+                                 (by[2] == iy && bx[2] == ix) || (by[3] == iy && bx[3] == ix);
+                if (hit) {
+                    const float4 d = ((const float4 *)dy)[(((int64_t)n * Ho + oy) * Wo + ox) * C4 + c4];
+                    const float dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (by[u] == iy && bx[u] == ix) g[u] += dv[u];
+                }
+            }
+        ((float4 *)dx)[i] = make_float4(g[0], g[1], g[2], g[3]);
+    }
+}
+
 inline unsigned grid_for(int64_t n) {
     const int64_t b = (n + 255) / 256;
     return (unsigned)(b < 256 * 64 ? (b > 0 ? b : 1) : 256 * 64);
@@ -359,8 +417,12 @@ int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, in
     if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1) return BEV_ERR_ARGS;
     const int64_t total = (int64_t)N * H * W * C;
     if (total == 0) return 0;
-    hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, dy, N, H, W, C, k,
-                       stride, pad, Ho, Wo, dx);
+    if (C % 4 == 0)
+        hipLaunchKernelGGL(k_maxpool_bwd_v4, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream, x, dy, N, H,
+                           W, C, k, stride, pad, Ho, Wo, dx);
+    else
+        hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, dy, N, H, W, C,
+                           k, stride, pad, Ho, Wo, dx);
     return last();
 }
 
