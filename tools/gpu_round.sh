@@ -1,12 +1,17 @@
-# Full GPU pass: parity tests, smoke, layer micro-bench, bench, rocprof kernel trace of the bench.
+# Round GPU pass: GPU tests, the default bench line, and a rocprofv3 kernel-trace summary of the same command.
+# usage (on the box): bash tools/gpu_round.sh <tag> [pytest -k expr]
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-mkdir -p gpurun_out/round
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/round/gpu_tests.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/round/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/round/smoke.log 2>&1 || exit $?
-timeout -k 10 600 python3 tools/conv_micro.py --iters 10 > gpurun_out/round/conv_micro.log 2>&1 || exit $?
-timeout -k 10 600 python bench.py > gpurun_out/round/bench.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/round/prof -o run -- python3 $R/bench.py --steps 10 --warmup 3 --cpu-iters 0 > gpurun_out/round/prof_bench.log 2>&1 || exit $?
+TAG=${1:-run}
+K=${2:-}
+O=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $O
+if [ -n "$K" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "$K" > $O/gpu_tests.log 2>&1
+else
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+fi
+rc=$?; echo "pytest rc=$rc" >> $O/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || exit $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1 || exit $?
+exit 0
