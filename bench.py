@@ -1,20 +1,33 @@
 """Benchmark: multi-cam frames/sec (7-cam -> 480x1440 BEV) on MI355X.
 
-Workload = BASELINE.json configs[1]: Wildtrack-shaped 7 cameras x 3 x 1080 x
-1920 fp32 images -> ResNet-50 (timm features_only, out_index=2, stride 8) ->
-1x1 proj to C=64 -> IPM warp onto the 480x1440 ground grid -> mean fusion
-over views.  One step = one batch of B frames through that whole hot path
-(CNNEncoder.forward + GeometryTransformer.forward_fused), inputs resident in
-HBM, random-init weights of that architecture, synthetic images, the fixed
+Workload = BASELINE.json configs[1] (default): Wildtrack-shaped 7 cameras x 3 x
+1080 x 1920 fp32 images -> ResNet-50 (timm features_only, out_index=2, stride
+8) -> 1x1 proj to C=64 -> IPM warp onto the 480x1440 ground grid -> mean
+fusion over views.  One step = one batch of B frames through that whole hot
+path (CNNEncoder.forward + GeometryTransformer.forward_fused), inputs resident
+in HBM, random-init weights of that architecture, synthetic images, the fixed
 Appendix-B camera rig.
 
-Multi-GPU (torchrun, one process per GPU): frames are independent, so each
-rank runs its own B frames with no data-path collective (weak scaling); only
-the timing barrier and a MAX-reduction of the elapsed time cross ranks.
+Other BASELINE configs (each its own JSON line, never the default):
+  --backbone efficientnet_b3   configs[3]: EfficientNet-B3 + AttentionFusion, which in the
+                               reference is the mean placeholder (fusion.py:25-36, quirk Q8)
+  --camera-shard               configs[4]: 16 cameras at 4K (2160 x 3840 -> 270 x 480
+                               features), cameras sharded over the ranks (2 per GPU at 8
+                               GPUs): each rank runs the trunk + the fused warp (SUM) on its
+                               cameras, then ONE reduce-scatter over BEV rows (RCCL/xGMI)
+                               and the division by 16 (bev_dist.camera_sharded_forward).
+                               Total work per frame is fixed: strong scaling.
+
+Multi-GPU, one process per GPU: `python bench.py --gpus N` starts N rank processes
+itself (torch.distributed.run on 127.0.0.1, before this process touches the GPU);
+under an external torchrun, WORLD_SIZE must equal --gpus.  Frame-sharded configs
+run B frames per rank with no data-path collective (weak scaling); only the timing
+barrier and a MAX-reduction of the elapsed time cross ranks.  `n_gpus` is the world
+size of the initialised process group.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
 `roofline` object for the dominant kernel family (backbone convs on fp32
-MFMA), `roofline_warp` for the IPM warp kernel (HBM-bound), and a
+MFMA), `roofline_warp` for the IPM warp kernel (HBM-bound), and, at N = 1, a
 `cpu_baseline` (the reference's torch-CPU composition, timed on this host on
 a bounded sample).
 """
@@ -24,6 +37,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,9 +49,6 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-import bev_native as nat  # noqa: E402
-import bev_rig  # noqa: E402
-
 BOUNDS = (-24.0, 24.0, -7.2, 7.2)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TF = 157.3  # MI355X fp32 matrix spec (= vector peak)
@@ -44,18 +56,43 @@ PEAK_F32_MFMA_TF = 157.3  # MI355X fp32 matrix spec (= vector peak)
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (rank processes) of this node; default 1")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step")
-    ap.add_argument("--views", type=int, default=7)
+    ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step (frame-sharded configs)")
+    ap.add_argument("--views", type=int, default=None, help="cameras (default 7; 16 with --camera-shard)")
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--backbone", default="resnet50")
-    ap.add_argument("--img", type=int, nargs=2, default=(1080, 1920))
+    ap.add_argument("--img", type=int, nargs=2, default=None, help="image H W (default 1080 1920; 2160 3840 "
+                                                                   "with --camera-shard)")
     ap.add_argument("--bev", type=int, nargs=2, default=(480, 1440))
-    ap.add_argument("--cpu-iters", type=int, default=3, help="frames timed for the CPU baseline (0 = skip)")
+    ap.add_argument("--camera-shard", action="store_true", help="BASELINE configs[4]: cameras sharded over ranks")
+    ap.add_argument("--cpu-iters", type=int, default=2, help="frames timed for the CPU baseline (0 = skip)")
     ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
-    return ap.parse_args()
+    ap.add_argument("--warp-kernel", choices=("barrier", "register", "pipeline"), default="barrier",
+                    help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
+    ap.add_argument("--warp-wgs", type=int, default=2, choices=(2, 3), help="pipeline workgroups per CU")
+    args = ap.parse_args()
+    if args.views is None:
+        args.views = 16 if args.camera_shard else 7
+    if args.img is None:
+        args.img = (2160, 3840) if args.camera_shard else (1080, 1920)
+    return args
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """Run this same command as n rank processes (one per GPU) and return their exit code.  Called before
+    this process makes any GPU call, so nothing is inherited from a HIP context."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
 
 
 def backbone_flops(enc, H, W):
@@ -105,7 +142,7 @@ def backbone_flops(enc, H, W):
     return total
 
 
-def warp_alg_bytes(geom, H, feats_shape, img, B, V):
+def warp_alg_bytes(geom, H, feats_shape, img, B):
     """out bytes + distinct touched source bytes, counted from the real taps."""
     import bev_native as nat
     _, _, C, Hf, Wf = feats_shape
@@ -127,37 +164,46 @@ def warp_alg_bytes(geom, H, feats_shape, img, B, V):
 
 def cpu_baseline(enc, args, K, Rt):
     """The reference's CPU path (timm-style ResNet on torch CPU + geometry.py grid_sample loop + mean),
-    timed on this host on `cpu_iters` frames (median)."""
+    timed on this host on a bounded sample of the workload (median over `cpu_iters` frames).  For the
+    16-camera 4K config the trunk runs on 2 of the 16 cameras per frame and its time is scaled by 8."""
     import backbone_ref
     from oracle import reference_composition_cpu
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
     enc_cpu = enc.to("cpu")
     H, W = args.img
+    V = args.views
+    v_enc = 2 if args.camera_shard else V
     gen = torch.Generator().manual_seed(1)
     times = []
     for _ in range(args.cpu_iters):
-        imgs = torch.randn(1, args.views, 3, H, W, generator=gen)
+        imgs = torch.randn(1, v_enc, 3, H, W, generator=gen)
         t0 = time.perf_counter()
         feats = backbone_ref.encoder_forward(enc_cpu, imgs)
+        t_enc = (time.perf_counter() - t0) * V / v_enc
+        if v_enc != V:
+            feats = feats.repeat(1, (V + v_enc - 1) // v_enc, 1, 1, 1)[:, :V].contiguous()
+        t1 = time.perf_counter()
         reference_composition_cpu(feats, torch.from_numpy(K[:1]), torch.from_numpy(Rt[:1]), (H, W), args.bev[0],
                                   args.bev[1], BOUNDS)
-        times.append(time.perf_counter() - t0)
+        times.append(t_enc + time.perf_counter() - t1)
     t = float(np.median(times))
+    enc_note = (f"trunk timed on {v_enc} of the {V} cameras and scaled x{V // v_enc}, " if v_enc != V else "")
     return {"value": round(1.0 / t, 4), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_iters} frame(s) of the same workload ({args.views}x3x{H}x{W} -> {args.backbone} "
-                      f"layer2 + proj C={args.channels} -> grid_sample warp -> mean), median {t:.2f} s/frame, "
-                      "torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
+            "sample": f"{args.cpu_iters} frame(s) of the same workload ({V}x3x{H}x{W} -> {args.backbone} "
+                      f"layer2 + proj C={args.channels} -> grid_sample warp -> mean), {enc_note}median {t:.2f} "
+                      "s/frame, torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
 
 
 def pmc_traffic(args) -> dict:
     """HBM bytes from the committed rocprofv3 PMC passes of this same command (tools/pmc_traffic.py):
     conv = bytes per step over all backbone conv launches, warp = bytes per fused-warp launch.
-    Only reported for the default workload those passes ran; {} otherwise."""
-    default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone) == \
-        (7, 64, (1080, 1920), (480, 1440), 1, "resnet50")
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          "r*_pmc_traffic.json")))
+    Only reported for the default workload those passes ran; {} otherwise.  These are the profile
+    file's numbers (named in `traffic_source`), not counters read by this run."""
+    default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone,
+               args.camera_shard, args.warp_kernel) == \
+        (7, 64, (1080, 1920), (480, 1440), 1, "resnet50", False, "barrier")
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
     if not default or not files:
         return {}
     d = json.load(open(files[-1]))
@@ -166,34 +212,65 @@ def pmc_traffic(args) -> dict:
     return res
 
 
+def workload(args, world):
+    V, C = args.views, args.channels
+    H, W = args.img
+    if args.camera_shard:
+        return ("BASELINE configs[4]", f"{V}-cam {H}x{W} -> {args.backbone}(stride-8 features)+proj C={C} -> IPM warp "
+                f"(SUM of each rank's {V // world if V % world == 0 else '~' + str(V // world)} cameras) -> reduce-scatter "
+                f"over BEV rows -> /{V} -> {args.bev[0]}x{args.bev[1]} BEV")
+    if args.backbone.startswith("efficientnet"):
+        return ("BASELINE configs[3]", f"{V}-cam {H}x{W} -> {args.backbone}(stride-8 features)+proj C={C} -> IPM warp -> "
+                f"AttentionFusion (the reference's mean placeholder, fusion.py:25-36) -> {args.bev[0]}x{args.bev[1]} BEV")
+    return ("BASELINE configs[1]", f"{V}-cam {H}x{W} -> {args.backbone}(stride-8 features)+proj C={C} -> IPM warp -> "
+            f"mean -> {args.bev[0]}x{args.bev[1]} BEV")
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(world_env or 1)
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=dev)
+        world = tdist.get_world_size()  # what RCCL actually formed
 
+    import bev_dist
+    import bev_native as nat
+    import bev_rig
     from models.encoders.cnn_encoder import CNNEncoder
     from models.fusion.geometry import GeometryTransformer
 
     B, V, C = args.batch, args.views, args.channels
     H, W = args.img
-    torch.manual_seed(1234 + rank)
+    if args.camera_shard:
+        B = 1
+        v0, v1 = bev_dist.camera_shard(V, rank, world)
+    else:
+        v0, v1 = 0, V
+    VL = v1 - v0
+    torch.manual_seed(1234)  # same weights on every rank (camera sharding shares one trunk)
     enc = CNNEncoder(out_channels=C, backbone=args.backbone, pretrained=False).eval().to(dev)
     geom = GeometryTransformer(args.bev[0], args.bev[1], BOUNDS)
     K, Rt = bev_rig.rig(V, H, W, B)
-    Kd, Rtd = torch.from_numpy(K).to(dev), torch.from_numpy(Rt).to(dev)
+    Kd, Rtd = torch.from_numpy(K[:, v0:v1]).to(dev), torch.from_numpy(Rt[:, v0:v1]).to(dev)
     gen = torch.Generator(device=dev).manual_seed(rank)
-    images = torch.randn(B, V, 3, H, W, device=dev, generator=gen)
+    images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
+    nat.tune(nat.TUNE_WARP_KERNEL, {"barrier": 0, "register": 1, "pipeline": 2}[args.warp_kernel])
+    nat.tune(nat.TUNE_WARP_WGS, args.warp_wgs)
     stream = torch.cuda.current_stream(dev)
-    ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], warp [t1,t2]
+    ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
 
     def step(record):
         with torch.no_grad():
@@ -207,7 +284,10 @@ def main():
                 feats = enc(images)
             if record:
                 e1.record(stream)
-            bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean")
+            if args.camera_shard:
+                bev = bev_dist.camera_sharded_forward(geom, feats, Kd, Rtd, (H, W), V, "mean")
+            else:
+                bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean")
             if record:
                 e2.record(stream)
                 ev.append((e0, e1, e2))
@@ -249,21 +329,21 @@ def main():
             step(False)
         barrier()
         h2d = {"value": round(B * n_h2d / (time.perf_counter() - t1), 3), "unit": "frames/s",
-               "note": f"pinned host images ({B}x{V}x3x{H}x{W} f32) copied H2D inside each of {n_h2d} steps"}
+               "note": f"pinned host images ({B}x{VL}x3x{H}x{W} f32) copied H2D inside each of {n_h2d} steps"}
 
     bb_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))  # encoder stage (convs + pool + layout)
-    stage_wp_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))  # geometry stage (homography + warp)
+    stage_wp_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))  # geometry stage (+ reduce-scatter)
     # conv kernels only, per step (EfficientNet: + its depthwise convs, which the FLOP count includes)
     conv_ms = float(np.sum(spans.get("conv", [0.0])) + np.sum(spans.get("dwconv", [0.0]))) / args.steps
     wp_ms = float(np.mean(spans["warp_fuse"]))  # the fused warp kernel only
-    frames = world * B * args.steps
+    frames = (B if args.camera_shard else world * B) * args.steps
     value = frames / elapsed
 
     if rank == 0:
         pmc = pmc_traffic(args)
-        flops = backbone_flops(enc, H, W) * V * B
-        Hm = geom.homographies(Kd, Rtd, B, V, dev)
-        alg, out_b, touched = warp_alg_bytes(geom, Hm, feats.shape, (H, W), B, V)
+        flops = backbone_flops(enc, H, W) * VL * B
+        Hm = geom.homographies(Kd, Rtd, B, VL, dev)
+        alg, out_b, touched = warp_alg_bytes(geom, Hm, feats.shape, (H, W), B)
         roof_bb = None if args.warp_only else {
             "kernel": "k_conv (fp32 MFMA implicit GEMM, every backbone conv launch of one step)",
             "bound": "mfma", "achieved": round(flops / (conv_ms * 1e-3) / 1e12, 3), "peak": PEAK_F32_MFMA_TF,
@@ -271,22 +351,32 @@ def main():
             "traffic": pmc.get("conv"), "flops_per_step": flops, "conv_ms_per_step": round(conv_ms, 4),
             "encoder_stage_ms": round(bb_ms, 4)}
         ach = alg / (wp_ms * 1e-3) / 1e9
-        roof_wp = {"kernel": "k_warp_fuse (IPM warp + mean, fused)", "bound": "hbm", "achieved": round(ach, 1),
-                   "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": pmc.get("warp"),
-                   "alg_bytes_per_launch": alg, "out_bytes": out_b, "touched_src_pixels": touched,
-                   "avg_us": round(wp_ms * 1e3, 2), "geometry_stage_us": round(stage_wp_ms * 1e3, 2)}
+        wk = {"barrier": "k_warp_fuse_v2", "register": "k_warp_fuse", "pipeline": "k_warp_fuse_pc"}[args.warp_kernel]
+        roof_wp = {"kernel": f"{wk} (IPM warp + {'sum' if args.camera_shard else 'mean'}, fused)", "bound": "hbm",
+                   "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
+                   "traffic": pmc.get("warp"), "alg_bytes_per_launch": alg, "out_bytes": out_b,
+                   "touched_src_pixels": touched, "avg_us": round(wp_ms * 1e3, 2),
+                   "geometry_stage_us": round(stage_wp_ms * 1e3, 2)}
+        label, wl = workload(args, world)
         line = {
-            "metric": "multi-cam frames/sec (7-cam→480×1440 BEV)",
+            "metric": "multi-cam frames/sec (7-cam→480×1440 BEV)" if label == "BASELINE configs[1]" else
+                      f"multi-cam frames/sec ({V}-cam→{args.bev[0]}×{args.bev[1]} BEV)",
             "value": round(value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{V}-cam {H}x{W} -> {args.backbone}(stride-8 features)+proj C={C} -> IPM warp -> mean "
-                                   f"-> {args.bev[0]}x{args.bev[1]} BEV (BASELINE configs[1])",
-                       "frames_per_gpu_per_step": B, "cameras": V, "bev": list(args.bev), "channels": C,
-                       "parallelism": f"frame-sharded x{world} (no collective)"},
+            "scaling": "strong" if args.camera_shard else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"{wl} ({label})", "baseline_config": label,
+                       "frames_per_gpu_per_step": None if args.camera_shard else B,
+                       "frames_per_step": B if args.camera_shard else world * B, "cameras": V,
+                       "cameras_per_gpu": VL, "bev": list(args.bev), "channels": C,
+                       "parallelism": (f"camera-sharded x{world} (reduce-scatter over BEV rows)" if args.camera_shard
+                                       else f"frame-sharded x{world} (no collective)")},
             "roofline": roof_bb if roof_bb else roof_wp,
             "roofline_warp": roof_wp,
         }
+        if args.camera_shard:
+            line["roofline_warp"]["note"] = "per-rank partial-sum warp of this rank's cameras; geometry_stage_us " \
+                                            "includes the reduce-scatter and the /V"
         if pmc:
             line["traffic_source"] = pmc["source"]
         if h2d:

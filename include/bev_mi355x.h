@@ -36,16 +36,26 @@ extern "C" {
 /* ABI version (bumped on any signature change). */
 int bev_abi_version(void);
 
-/* host: performance knobs (no effect on results).  knob BEV_TUNE_CONV_TILE:
- * 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64 output tiles for
- * bev_conv2d_f32.  Returns the previous value, or BEV_ERR_ARGS. */
+/* host: performance knobs (no effect on results); returns the previous value, or
+ * BEV_ERR_ARGS for an unknown knob / out-of-range value.
+ * BEV_TUNE_CONV_TILE: 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64
+ *   output tiles for bev_conv2d_f32.
+ * BEV_TUNE_WARP_POOL_KB: LDS footprint-image pool (ring) per workgroup of the fused
+ *   warp in KiB, 0 = automatic, else 8..150 (small pools force block decomposition).
+ * BEV_TUNE_WARP_KERNEL: fused warp kernel for NHWC C % 64 == 0 features:
+ *   0 = per-view-barrier LDS-DMA kernel (default), 1 = register-staged, 2 = loader/sampler
+ *   pipeline (experimental, slower).
+ * BEV_TUNE_WARP_WGS: pipeline workgroups per CU, 2 (default) or 3.
+ * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
+ * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
+ * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles. */
 #define BEV_TUNE_CONV_TILE 1
-/* knob BEV_TUNE_WARP_POOL_KB: LDS image pool of the fused warp in KiB
- * (0 = automatic; small pools force channel-chunked / direct units). */
 #define BEV_TUNE_WARP_POOL_KB 2
-/* knob BEV_TUNE_WARP_UNITS: 1 = route the fused warp through the unit-pipeline kernel
- * (bev_warp_fuse.hip), 0 = the default v2 kernel.  Same results either way. */
-#define BEV_TUNE_WARP_UNITS 3
+#define BEV_TUNE_WARP_KERNEL 3
+#define BEV_TUNE_WARP_WGS 4
+#define BEV_TUNE_WARP_BWD_POOL 5
+#define BEV_TUNE_CONV_XCD 6
+#define BEV_TUNE_CONV_NBUF 7
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------
@@ -226,6 +236,69 @@ int bev_colsum_f32(const float *dz, int64_t M, int C, float *db, void *stream);
  * (first maximum in scan order, NaN wins). */
 int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride, int pad,
                                int Ho, int Wo, float *dx, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * CenterNet BEV head (BEVDetector, detector.py:16-62): dilated convs, GroupNorm(32) + ReLU
+ * ------------------------------------------------------------------------- */
+
+/* device: NHWC conv on fp32 MFMA with an optional per-(image, input channel) affine + ReLU applied
+ * to the operand as it is loaded: x' = relu?(x * in_scale[n][ci] + in_shift[n][ci]) for in-range
+ * taps (zero padding stays 0) -- the previous layer's GroupNorm + ReLU, never materialised.
+ * in_scale / in_shift [N][Ci] (both NULL: plain conv; needs Ci % 32 == 0 otherwise).  dilation
+ * >= 1 (Ho = (H + 2 pad - dilation (KH - 1) - 1) / stride + 1); y rows are ldy >= Co floats apart
+ * (a channel slice of a wider NHWC buffer).  Replaces nn.Conv2d(..., dilation) of detector.py:16-30
+ * followed by GroupNorm + ReLU of the layer before. */
+int bev_conv2d_nhwc_ex_f32(const float *x, int N, int H, int W, int Ci, const float *in_scale, const float *in_shift,
+                           int in_relu, const float *packed, const float *bias, int Co, int KH, int KW, int stride,
+                           int pad, int dilation, int relu, float *y, int ldy, int Ho, int Wo, void *stream);
+
+/* bev_conv_wgrad_f32 for a dilated conv. */
+int bev_conv_wgrad_ex_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,
+                          int KW, int stride, int pad, int dilation, float *dW, void *stream);
+
+/* host: bytes of the workspace bev_groupnorm_fwd_f32 / _bwd_f32 need for x [N][P][C], G groups
+ * (-1: unsupported shape -- C % G == 0, (C / G) % 4 == 0, 256 % (C / 4) == 0, C <= 1024). */
+int64_t bev_groupnorm_workspace_bytes(int N, int64_t P, int C, int G);
+
+/* device: GroupNorm statistics of x [N][P][C] (NHWC, G groups of C/G channels, biased variance,
+ * torch.nn.GroupNorm semantics): mean, rstd [N][G]; and the per-(image, channel) affine of the
+ * normalised output, scale = rstd * gamma, shift = beta - mean * scale [N][C]. */
+int bev_groupnorm_fwd_f32(const float *x, int N, int64_t P, int C, int G, float eps, const float *gamma,
+                          const float *beta, float *mean, float *rstd, float *scale, float *shift, void *workspace,
+                          void *stream);
+
+/* device: y = x * scale + shift (+ ReLU), NHWC [N][P][C]; y may alias x. */
+int bev_groupnorm_apply_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift, int relu,
+                            float *y, void *stream);
+
+/* device: backward of y = relu?(groupnorm(x)) (the forward's mean, rstd, scale, shift): dx [N][P][C],
+ * dgamma, dbeta [C], all OVERWRITTEN. */
+int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
+                          const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
+                          float *dx, float *dgamma, float *dbeta, void *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * BEVDetector.decode (detector.py:64-125) on the device: no per-pair host sync.
+ * ------------------------------------------------------------------------- */
+
+/* device: heat [B][H][W] (the sigmoid heatmap).  Every cell whose `_nms2d` score
+ * v * (v == maxpool3x3(v)) exceeds thresh is appended to its frame's candidate list:
+ * cand_idx [B][cap] (cell y*W + x), cand_score [B][cap]; count [B] is OVERWRITTEN with the
+ * number of candidates (may exceed cap: then only cap were stored). */
+int bev_decode_peaks_f32(const float *heat, int B, int H, int W, float thresh, int cap, int32_t *cand_idx,
+                         float *cand_score, int32_t *count, void *stream);
+
+/* device: per frame, candidates sorted by (score desc, cell asc), boxes
+ * [cx, cy, w, h] = [x_min + (x + off_x) * res_x, y_min + (y + off_y) * res_y, size_w * res_x,
+ * size_h * res_y] (offset, size [B][2][H][W]), greedy centre-distance NMS (kept when every
+ * kept centre is >= nms_dist away).  boxes [B][cap][4], scores [B][cap] in keep order,
+ * nkept [B] (-1: more candidates than cap or bev_decode_max_candidates()). */
+int bev_decode_nms_f32(const int32_t *cand_idx, const float *cand_score, const int32_t *count, int B, int cap,
+                       const float *offset, const float *size, int H, int W, float x_min, float y_min, float res_x,
+                       float res_y, float nms_dist, float *boxes, float *scores, int32_t *nkept, void *stream);
+
+/* host: the largest candidate count per frame bev_decode_nms_f32 handles. */
+int bev_decode_max_candidates(void);
 
 #ifdef __cplusplus
 }

@@ -158,6 +158,28 @@ class Oracle:
         self.lib.oracle_fuse_f32(_p(x), B, V, M, {"sum": 0, "mean": 1, "max": 2}[mode], _p(out))
         return out
 
+    def fused_stream(self, feats, K, Rt, img_hw, bev_h, bev_w, bounds, modes=("sum", "mean", "max")):
+        """SimpleFusion(mode)(GeometryTransformer.forward(...)) for each mode, one view at a time.
+
+        Same arithmetic as `fuse(geometry_forward(...))` (oracle_fuse_f32: sum from +0 in view
+        order, mean = sum / f32(V), max = first view then `t > acc`), but never materialises the
+        [B, V, C, Hb, Wb] stack -- full-size 16-camera rigs fit in host memory.  No NaNs expected."""
+        B, V = feats.shape[:2]
+        xs, ys = self.bev_axes(bev_h, bev_w, bounds)
+        res = {}
+        for b in range(B):
+            acc_s, acc_m = None, None
+            for v in range(V):
+                Kv, Gv = self.homography_operands(K[b, v], Rt[b, v])
+                H = self.homography(Kv[None], Gv[None])
+                x = self.warp(feats[b, v][None], H, xs, ys, img_hw)[0]
+                acc_s = x + np.float32(0.0) if acc_s is None else acc_s + x
+                acc_m = x if acc_m is None else np.where(x > acc_m, x, acc_m)
+            for m in modes:
+                r = {"sum": acc_s, "mean": acc_s / np.float32(V), "max": acc_m}[m]
+                res.setdefault(m, []).append(r.astype(np.float32, copy=False))
+        return {m: np.stack(r) for m, r in res.items()}
+
     # ---- cnn_encoder.py:31-37 (direct conv) --------------------------------
     def conv2d(self, x, w, b, stride, pad, relu):
         x, w = _c(x), _c(w)

@@ -18,6 +18,9 @@ Branches exercised (timm / kornia are absent here):
   * geometry.py:142-162  grid_sample warp branch
   * fusion.py:11-46      SimpleFusion / AttentionFusion / ConcatFusion
   * cnn_encoder.py:31-37 fallback 2-conv encoder
+  * model_wrapper.py:53-124 BEVNet forward (+ lazy proj / detector, detector.py:7-125) and loss
+
+`--only bevnet` / `--only decode` regenerate just bevnet_small.npz / decode_cases.npz.
 """
 from __future__ import annotations
 
@@ -41,6 +44,9 @@ import torch.nn.functional as F  # noqa: E402
 from models.fusion.geometry import GeometryTransformer  # noqa: E402  (reference)
 from models.fusion.fusion import SimpleFusion, AttentionFusion, ConcatFusion  # noqa: E402
 from models.encoders.cnn_encoder import CNNEncoder  # noqa: E402
+from models.model_wrapper import BEVNet  # noqa: E402
+from models.heads.detector import BEVDetector  # noqa: E402
+from utils.visualization import save_predictions_json  # noqa: E402
 
 SAMPLE = 65536
 BOUNDS = (-24.0, 24.0, -7.2, 7.2)
@@ -208,8 +214,115 @@ def encoder_case():
     print("encoder_fallback", y5.shape, y4.shape)
 
 
+BEVNET_CFG = {
+    "MODEL": {"BACKBONE": "resnet18", "PRETRAINED": False, "FEAT_DIM": 8, "OUT_INDEX": 2, "BEV_SIZE": [32, 40, 120],
+              "BEV_BOUNDS": [-24.0, 24.0, -7.2, 7.2], "BEV_PROJ_CH": 16},
+    "EVAL": {"CONF_THRESH": 0.4, "NMS_DIST_M": 0.5},
+    "LOSS": {},
+}
+
+
+def bevnet_case():
+    """BEVNet (model_wrapper.py:13-124) end to end on a small seeded batch: the reference's fallback encoder
+    (timm absent), grid_sample warp (kornia absent, quirk Q7), ConcatFusion, lazy BEV proj + pos-enc, lazy
+    BEVDetector, decode, loss and parameter gradients.  The state_dict after the first forward (lazy modules
+    built) is stored so the drop-in can load the same weights."""
+    import copy
+    B, V, H, W = 2, 3, 64, 96
+    torch.manual_seed(0)
+    cfg = copy.deepcopy(BEVNET_CFG)
+    net = BEVNet(cfg)
+    K, Rt = bev_rig.rig(V, H, W, B)
+    images = randn(41, (B, V, 3, H, W))
+    batch = {"images": torch.from_numpy(images),
+             "calib": {"intrinsic": torch.from_numpy(K), "extrinsic": torch.from_numpy(Rt)}}
+    with torch.no_grad():
+        out = net(batch)  # builds encoder.proj? (fallback: none), BEVNet.proj and detector
+    # a decode threshold inside a wide gap of the peak scores, so ~a dozen boxes survive with margin
+    peaks = net.detector._nms2d(out["heatmap"]).flatten()
+    top = torch.sort(peaks[peaks > 0], descending=True).values[:40]
+    gaps = top[:-1] - top[1:]
+    kk = int(torch.argmax(gaps[5:25])) + 5
+    thresh = float((top[kk] + top[kk + 1]) / 2)
+    net.conf_thresh = thresh
+    cfg["EVAL"]["CONF_THRESH"] = thresh
+    with torch.no_grad():
+        out = net(batch)
+    # loss + gradients on fixed targets (frame 0: centers, frame 1: boxes incl. one outside the map)
+    targets = [{"centers_world": torch.tensor([[-10.0, 1.0], [3.3, -2.2], [15.7, 4.1]])},
+               {"boxes_world": torch.tensor([[0.2, 0.1, 0.9, 0.7], [-20.5, -6.0, 0.5, 0.5], [30.0, 0.0, 0.6, 0.6]])}]
+    net.zero_grad()
+    pred = net(batch)
+    losses = net.loss(pred, targets, cfg["LOSS"])
+    losses["total_loss"].backward()
+    sd = net.state_dict()
+    d = dict(images=images, K=K, Rt=Rt, cfg=np.array(json.dumps(cfg)),
+             keys=np.array(list(sd.keys())),
+             heatmap_logits=out["heatmap_logits"].numpy(), offset_raw=out["offset_raw"].numpy(),
+             size_raw=out["size_raw"].numpy(), bev_feat=out["bev_feat"].numpy(), heatmap=out["heatmap"].numpy(),
+             offset=out["offset"].numpy(), size=out["size"].numpy(),
+             nboxes=np.array([b.shape[0] for b in out["boxes"]]),
+             boxes=np.concatenate([b.numpy() for b in out["boxes"]]).reshape(-1, 4),
+             scores=np.concatenate([x.numpy() for x in out["scores"]]),
+             t0_centers=targets[0]["centers_world"].numpy(), t1_boxes=targets[1]["boxes_world"].numpy(),
+             **{f"loss_{k}": np.float32(v.item()) for k, v in losses.items()})
+    for k, v in sd.items():
+        d["w_" + k] = v.numpy()
+    for n, prm in net.named_parameters():  # gradients of everything but the two large stem convs
+        if prm.grad is not None and n not in ("detector.stem.3.weight", "detector.stem.6.weight"):
+            d["g_" + n] = prm.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "bevnet_small.npz"), **d)
+    print("bevnet_small", out["heatmap"].shape, "boxes", d["nboxes"], "thresh", thresh,
+          {k: float(v.detach()) for k, v in losses.items()})
+
+
+def decode_case():
+    """BEVDetector.decode (detector.py:64-125) on synthetic head outputs with many peaks, plateaus (equal
+    neighbours: not a unique max, still peaks), close peaks for the distance NMS, and
+    save_predictions_json (visualization.py:22-29) text for two frame indices."""
+    import tempfile
+    B, H, W = 2, 40, 120
+    bounds = (-24.0, 24.0, -7.2, 7.2)
+    rng = np.random.default_rng(91)
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    heat = np.zeros((B, 1, H, W), np.float32)
+    for b in range(B):
+        for _ in range(60):
+            cy, cx = rng.uniform(0, H), rng.uniform(0, W)
+            amp, sig = rng.uniform(0.2, 1.0), rng.uniform(0.6, 2.5)
+            heat[b, 0] = np.maximum(heat[b, 0], amp * np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * sig * sig)))
+    heat = (heat * np.float32(0.98) + rng.uniform(0, 0.02, size=heat.shape).astype(np.float32)).astype(np.float32)
+    heat[0, 0, 5, 10:12] = 0.9  # plateau: two equal neighbouring maxima
+    offset = rng.uniform(0, 1, size=(B, 2, H, W)).astype(np.float32)
+    size = rng.uniform(5, 30, size=(B, 2, H, W)).astype(np.float32)
+    det = BEVDetector(in_channels=4, bev_bounds=bounds, bev_size=(H, W))
+    out = {}
+    for thr, nms in ((0.3, 0.5), (0.5, 1.5), (0.95, 0.5)):
+        bl, sl = det.decode(torch.from_numpy(heat), torch.from_numpy(offset), torch.from_numpy(size), conf_thresh=thr,
+                            nms_dist_m=nms)
+        tag = f"t{int(thr * 100)}_n{int(nms * 10)}"
+        out[tag + "_n"] = np.array([x.shape[0] for x in bl])
+        out[tag + "_boxes"] = np.concatenate([x.numpy() for x in bl]).reshape(-1, 4)
+        out[tag + "_scores"] = np.concatenate([x.numpy() for x in sl])
+        if tag == "t30_n5":
+            with tempfile.TemporaryDirectory() as td:
+                save_predictions_json(bl, sl, td, [7, 123456])
+                for fi in (7, 123456):
+                    with open(os.path.join(td, f"frame_{fi:06d}.json")) as f:
+                        out[f"json_{fi}"] = np.array(f.read())
+    np.savez_compressed(os.path.join(HERE, "decode_cases.npz"), heat=heat, offset=offset, size=size,
+                        bounds=np.array(bounds), **out)
+    print("decode_cases", {k: v for k, v in out.items() if k.endswith("_n")})
+
+
 def main():
     torch.set_num_threads(os.cpu_count() or 1)
+    if sys.argv[1:] == ["--only", "bevnet"]:
+        bevnet_case()
+        return
+    if sys.argv[1:] == ["--only", "decode"]:
+        decode_case()
+        return
     meta = dict(torch=torch.__version__, cpu_capability=torch.backends.cpu.get_cpu_capability(),
                 mkl="MKL 2024.2 (default ISA dispatch on this host: avx512)",
                 recipe="SURVEY.md Appendix A (AVX-512 dot3)", reference="/root/reference @ 2025-11-14",
@@ -235,6 +348,8 @@ def main():
     linspace_cases()
     fusion_cases()
     encoder_case()
+    bevnet_case()
+    decode_case()
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     K, Rt = bev_rig.rig(7, 1080, 1920, 1)

@@ -79,3 +79,27 @@ def test_argument_validation_without_gpu(lib):
     assert lib.bev_maxpool2d_nhwc_f32(null, 1, 8, 8, 4, 3, 2, 1, null, 4, 4, null) == -1
     # empty work is a successful no-op
     assert lib.bev_homography_f32(null, null, 0, null, null) == 0
+
+
+def test_tune_knobs_host_only(lib):
+    """bev_tune: every knob returns its previous value, rejects out-of-range values and unknown knobs;
+    no GPU involved (knobs are read at launch)."""
+    import bev_native as nat
+    assert lib.bev_tune(99, 0) == -1
+    for knob, good, bad in ((nat.TUNE_CONV_TILE, 3, 5), (nat.TUNE_WARP_POOL_KB, 16, 4), (nat.TUNE_WARP_KERNEL, 2, 3),
+                            (nat.TUNE_WARP_WGS, 3, 1), (nat.TUNE_WARP_BWD_POOL, 96, 1 << 20),
+                            (nat.TUNE_CONV_XCD, 0, 2), (nat.TUNE_CONV_NBUF, 1, 3)):
+        old = lib.bev_tune(knob, good)
+        assert old >= 0
+        assert lib.bev_tune(knob, bad) == -1
+        assert lib.bev_tune(knob, old) == good
+    with nat.tuned(WARP_KERNEL=1, WARP_POOL_KB=8):
+        assert lib.bev_tune(nat.TUNE_WARP_KERNEL, 1) == 1
+    assert lib.bev_tune(nat.TUNE_WARP_KERNEL, 0) == 0  # the default kernel stays selected
+
+
+def test_no_environment_knobs_in_library():
+    """The shipped library reads no environment variables (performance knobs are bev_tune only)."""
+    import glob
+    for src in glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h")):
+        assert "getenv" not in open(src).read(), src

@@ -70,23 +70,26 @@ def test_frame_shard_partitions():
 
 
 @pytest.mark.timeout(300)
-def test_camera_sharded_reduce_scatter_world2():
+@pytest.mark.parametrize("world", [2, 3])
+def test_camera_sharded_reduce_scatter(world):
+    """world 2: BEV rows split evenly; world 3: 3 cameras over 3 ranks and BEV rows NOT a multiple of the
+    group size (zero-padded reduce-scatter, shorter last slice)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = dict(q.get(timeout=240) for _ in range(world))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    for rank in (0, 1):
+    for rank in range(world):
         for mode, (full, sl, ref) in res[rank].items():
             scale = max(np.abs(ref).max(), 1e-30)
             if mode == "max":
                 assert np.array_equal(full, ref), mode  # max is order-independent
             else:
                 assert np.abs(full - ref).max() <= 1e-5 * scale, mode
-            rows = ref.shape[2] // 2
+            rows = -(-ref.shape[2] // world)
             np.testing.assert_array_equal(sl, full[:, :, rank * rows:(rank + 1) * rows])

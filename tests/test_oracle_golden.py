@@ -111,3 +111,17 @@ def test_encoder_fallback_conv(oracle):
         h = oracle.conv2d(x, w0, b0, 2, 1, True)
         z = oracle.conv2d(h, w2, b2, 2, 1, True)
         np.testing.assert_allclose(z, y, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("path", [p for p in WARP_FILES if "16cam" not in p], ids=lambda p: os.path.basename(p)[:-4])
+def test_fused_stream_equals_stacked_fuse(oracle, path):
+    """Oracle.fused_stream (view-at-a-time, used for the full-size GPU references) == fuse(geometry_forward)."""
+    d = np.load(path)
+    feats = feats_for(d)
+    img = (int(d["img_h"]), int(d["img_w"]))
+    bh, bw = int(d["bev_h"]), int(d["bev_w"])
+    bounds = tuple(float(x) for x in d["bounds"])
+    per_view = oracle.geometry_forward(feats, d["K"], d["Rt"], img, bh, bw, bounds)
+    got = oracle.fused_stream(feats, d["K"], d["Rt"], img, bh, bw, bounds)
+    for mode in ("sum", "mean", "max"):
+        assert np.array_equal(bits(got[mode]), bits(oracle.fuse(per_view, mode))), mode

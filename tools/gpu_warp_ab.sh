@@ -1,14 +1,14 @@
-# Warp parity (default + small pool) and v1/v2 timing A/B.
+# Fused-warp GPU pass: warp parity tests, then warp-only bench A/B of the kernels + rocprof stats.
+# usage (on the box): bash tools/gpu_warp_ab.sh <tag>
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-O=gpurun_out/wab; mkdir -p $O
-timeout -k 10 600 python -m pytest tests/test_warp_gpu.py -q -x -p no:cacheprovider > $O/tests.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> $O/tests.log; [ $rc -ne 0 ] && exit $rc
-BEV_WARP_POOL_KB=8 timeout -k 10 600 python -m pytest tests/test_warp_gpu.py -q -x -p no:cacheprovider -k "full_size or fused" > $O/tests_pool8.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> $O/tests_pool8.log; [ $rc -ne 0 ] && exit $rc
-for cfg in "X=1" "BEV_WARP_V1=1" "BEV_WARP_OCC=2" "BEV_WARP_POOL_KB=48" "BEV_WARP_POOL_KB=28"; do
-  env $cfg timeout -k 10 300 python bench.py --warp-only --steps 50 --warmup 5 --cpu-iters 0 > $O/bench_$cfg.log 2>&1 || exit $?
+O=$GRAFT_REPO_ROOT/gpurun_out/$1; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_warp_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/warp_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/warp_tests.log; [ $rc -ne 0 ] && exit $rc
+for k in pipeline barrier; do
+  timeout -k 10 300 python -u bench.py --warp-only --steps 50 --warmup 5 --cpu-iters 0 --warp-kernel $k > $O/bench_$k.log 2>&1 || exit $?
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --warp-only --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py --warp-only --steps 50 --warmup 5 --cpu-iters 0 --warp-wgs 3 > $O/bench_pipeline3.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --warp-only --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1 || exit $?
 exit 0

@@ -21,7 +21,8 @@ spread the path over the GPUs of a node, one process per GPU:
   This is the path's only exchange step (RCCL over xGMI; gloo in CPU tests).
   The view-summation order differs from the reference's sequential v = 0..V-1
   (partial sums are added across ranks), so this mode is tolerance-equal
-  (max|d| <= 1e-5 * max|x|), not bit-equal.
+  (max|d| <= 1e-5 * max|x|), not bit-equal -- except at world
+  size 1, where the reduce-scatter is the identity and the result is bit-exact.
 """
 from __future__ import annotations
 
@@ -54,15 +55,17 @@ def reduce_partial_bev(partial: torch.Tensor, num_views: int, mode: str = "mean"
     """Combine per-rank partial BEV maps [B, C, Hb, Wb] into the fused result.
 
     `partial` is this rank's SUM over its cameras (mode sum/mean) or MAX over
-    them (mode max).  Returns this rank's row slice [B, C, Hb/world, Wb] of the
-    fused map, or the whole map when `gather` (one extra all-gather).
-    Hb must be divisible by the group size.
+    them (mode max).  Returns this rank's row slice of the fused map (rows
+    [r * ceil(Hb / world), ...), the last slices shorter when Hb is not a
+    multiple of the group size), or the whole map when `gather` (one extra
+    all-gather).  One reduce-scatter over BEV rows is the only exchange.
     """
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     B, C, Hb, Wb = partial.shape
-    if Hb % world:
-        raise ValueError(f"BEV rows {Hb} not divisible by world size {world}")
-    rpr = Hb // world
+    rpr = -(-Hb // world)  # rows per rank (ceil); the map is zero-padded to world * rpr rows
+    if rpr * world != Hb:
+        partial = torch.nn.functional.pad(partial, (0, 0, 0, rpr * world - Hb))
     # rows-major chunks so that rank r's slice is the r-th contiguous chunk
     x = partial.reshape(B, C, world, rpr, Wb).permute(2, 0, 1, 3, 4).contiguous()
     out = torch.empty(B, C, rpr, Wb, dtype=partial.dtype, device=partial.device)
@@ -71,16 +74,23 @@ def reduce_partial_bev(partial: torch.Tensor, num_views: int, mode: str = "mean"
     if mode == "mean":
         out = out / float(num_views)
     if not gather:
-        return out
+        lo, hi = min(rank * rpr, Hb), min((rank + 1) * rpr, Hb)
+        return out[:, :, : hi - lo]
     full = torch.empty(world, B, C, rpr, Wb, dtype=out.dtype, device=out.device)
     dist.all_gather_into_tensor(full.view(world * B, C, rpr, Wb), out.contiguous(), group=group)
-    return full.permute(1, 2, 0, 3, 4).reshape(B, C, Hb, Wb)
+    return full.permute(1, 2, 0, 3, 4).reshape(B, C, world * rpr, Wb)[:, :, :Hb]
 
 
 def camera_sharded_forward(geom, feats_local: torch.Tensor, K_local, Rt_local, img_size, num_views: int,
                            mode: str = "mean", group: Optional[dist.ProcessGroup] = None,
                            gather: bool = False) -> torch.Tensor:
-    """K5 path: this rank's cameras -> fused partial (HIP kernel) -> reduce-scatter over BEV rows."""
+    """K5 path: this rank's cameras -> fused partial (HIP kernel) -> reduce-scatter over BEV rows.
+    Without an initialised process group this process holds every camera: the fused kernel computes
+    the reduction directly (bit-identical to the reference)."""
+    if not dist.is_available() or not dist.is_initialized():
+        if feats_local.shape[1] != num_views:
+            raise ValueError("camera_sharded_forward without a process group needs all cameras")
+        return geom.forward_fused(feats_local, K_local, Rt_local, img_size, mode)
     part_mode = "max" if mode == "max" else "sum"
     partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
     return reduce_partial_bev(partial, num_views, mode, group, gather)

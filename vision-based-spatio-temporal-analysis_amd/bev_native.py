@@ -17,7 +17,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -60,6 +60,16 @@ SIGNATURES = {
     "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_se_gate_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "bev_channel_scale_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp]),
+    "bev_decode_peaks_f32": (_i, [_vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
+    "bev_decode_nms_f32": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _f, _f, _f, _f, _f, _vp, _vp, _vp, _vp]),
+    "bev_decode_max_candidates": (_i, []),
+    "bev_conv2d_nhwc_ex_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i,
+                                    _i, _i, _vp]),
+    "bev_conv_wgrad_ex_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_groupnorm_workspace_bytes": (_i64, [_i, _i64, _i, _i]),
+    "bev_groupnorm_fwd_f32": (_i, [_vp, _i, _i64, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bev_groupnorm_apply_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _i, _vp, _vp]),
+    "bev_groupnorm_bwd_f32": (_i, [_vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
 }
 
 
@@ -122,9 +132,15 @@ def lib():
     return _lib
 
 
+# performance knobs (include/bev_mi355x.h BEV_TUNE_*); results never depend on them
 TUNE_CONV_TILE = 1
 TUNE_WARP_POOL_KB = 2
-TUNE_WARP_UNITS = 3
+TUNE_WARP_KERNEL = 3
+TUNE_WARP_WGS = 4
+TUNE_WARP_BWD_POOL = 5
+TUNE_CONV_XCD = 6
+TUNE_CONV_NBUF = 7
+WARP_KERNEL_BARRIER, WARP_KERNEL_REGISTER, WARP_KERNEL_PIPELINE = 0, 1, 2
 
 
 def tune(knob: int, value: int) -> int:
@@ -133,6 +149,20 @@ def tune(knob: int, value: int) -> int:
     if rc < 0:
         raise ValueError(f"bad tuning knob/value {knob}/{value}")
     return rc
+
+
+@contextlib.contextmanager
+def tuned(**knobs):
+    """Temporarily set knobs by name: `with tuned(WARP_POOL_KB=8, WARP_KERNEL=2): ...`."""
+    old = []
+    try:
+        for name, value in knobs.items():
+            k = globals()["TUNE_" + name]
+            old.append((k, tune(k, value)))
+        yield
+    finally:
+        for k, v in reversed(old):
+            tune(k, v)
 
 
 class HipError(RuntimeError):
@@ -456,3 +486,35 @@ def maxpool_bwd_nhwc(x: torch.Tensor, dy: torch.Tensor, k: int, stride: int, pad
     _check(lib().bev_maxpool2d_bwd_nhwc_f32(_ptr(x), _ptr(dy), N, H, W, C, k, stride, pad, Ho, Wo, _ptr(dx),
                                             _stream(x)), "bev_maxpool2d_bwd_nhwc_f32")
     return dx
+
+
+# ---------------------------------------------------------------------------
+# decode (detector.py:64-125)
+# ---------------------------------------------------------------------------
+def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, bounds, conf_thresh: float,
+           nms_dist: float):
+    """heatmap [B,1,H,W], offset / size [B,2,H,W] (device) -> (boxes list of [K,4], scores list of [K]).
+    One host synchronisation for the whole batch (the kept counts)."""
+    heatmap, offset, size = heatmap.contiguous().float(), offset.contiguous().float(), size.contiguous().float()
+    _require_gpu(heatmap, offset, size)
+    B, _, H, W = heatmap.shape
+    cap = int(min(H * W, lib().bev_decode_max_candidates()))
+    dev = heatmap.device
+    idx = torch.empty(B, cap, device=dev, dtype=torch.int32)
+    sc = torch.empty(B, cap, device=dev, dtype=torch.float32)
+    cnt = torch.empty(B, device=dev, dtype=torch.int32)
+    st = _stream(heatmap)
+    _check(lib().bev_decode_peaks_f32(_ptr(heatmap), B, H, W, float(conf_thresh), cap, _ptr(idx), _ptr(sc), _ptr(cnt),
+                                      st), "bev_decode_peaks_f32")
+    x_min, x_max, y_min, y_max = bounds
+    res_x, res_y = (x_max - x_min) / float(W), (y_max - y_min) / float(H)
+    boxes = torch.empty(B, cap, 4, device=dev, dtype=torch.float32)
+    scores = torch.empty(B, cap, device=dev, dtype=torch.float32)
+    nk = torch.empty(B, device=dev, dtype=torch.int32)
+    _check(lib().bev_decode_nms_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, _ptr(offset), _ptr(size), H, W,
+                                    float(x_min), float(y_min), float(res_x), float(res_y), float(nms_dist),
+                                    _ptr(boxes), _ptr(scores), _ptr(nk), st), "bev_decode_nms_f32")
+    kept = nk.cpu().tolist()
+    if min(kept, default=0) < 0:
+        raise HipError(f"decode: more than {cap} peak candidates in a frame above conf_thresh={conf_thresh}")
+    return [boxes[b, :k] for b, k in enumerate(kept)], [scores[b, :k] for b, k in enumerate(kept)]

@@ -28,7 +28,7 @@
 #include <type_traits>
 
 #include "../../include/bev_mi355x.h"
-#include "bev_warp_fuse.h"
+#include "bev_tune.h"
 
 namespace {
 
@@ -83,6 +83,12 @@ struct ConvArgs {
     // per-(image, input channel) multiplier of the A operand (SqueezeExcite excitation folded into
     // the projection conv's loader: conv(x * gate)); NULL = none.  Fast and contiguous loaders only.
     const float *__restrict__ ascale;
+    // with ascale: per-(image, input channel) shift added after the scale, then ReLU when arelu
+    // (a GroupNorm + ReLU of the previous layer applied on the fly; out-of-range taps stay 0)
+    const float *__restrict__ ashift;
+    int arelu;
+    int dil;  // dilation of the taps (input offset ky * dil, kx * dil)
+    int ldy;  // row stride of y in floats (>= Co; a channel slice of a wider NHWC buffer)
     int xcd;  // 1: XCD-aware block order (the N tiles of one M block run on one XCD, sharing its L2)
 };
 
@@ -156,6 +162,52 @@ struct LoaderFast {
             if (++kx == a.KW) {
                 kx = 0;
                 ++ky;
+            }
+        }
+    }
+};
+
+// A loader, fast path with a dilated tap grid and the previous layer's GroupNorm + ReLU applied on the
+// fly (BEV head, bev_conv2d_nhwc_ex_f32): x' = relu?(x * ascale[n][ci] + ashift[n][ci]) for in-range
+// taps.  A separate instantiation keeps LoaderFast's register budget (and the trunk's occupancy).
+template <int ROWS>
+struct LoaderFastEx : LoaderFast<ROWS> {
+    using LoaderFast<ROWS>::rows;
+    using LoaderFast<ROWS>::quad;
+    using LoaderFast<ROWS>::ky;
+    using LoaderFast<ROWS>::kx;
+    using LoaderFast<ROWS>::ci0;
+    static constexpr int NV = ROWS;
+    __device__ void load(const ConvArgs &a, f32x4 (&v)[NV]) {
+        bool inr[ROWS];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const int iy = rows.iy0[r] + ky * a.dil, ix = rows.ix0[r] + kx * a.dil;
+            const bool in = rows.ok[r] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            inr[r] = in;
+            v[r] = in ? *(const f32x4 *)(a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4)
+                      : (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (a.ascale && !rows.uni && in) {
+                const int64_t o = (int64_t)rows.img[r] * a.Ci + ci0 + quad * 4;
+                v[r] *= *(const f32x4 *)(a.ascale + o);
+                if (a.ashift) v[r] += *(const f32x4 *)(a.ashift + o);
+                if (a.arelu) v[r] = __builtin_elementwise_max(v[r], (f32x4){0.f, 0.f, 0.f, 0.f});
+            }
+        }
+        if (a.ascale && rows.uni) {
+            const int64_t o = (int64_t)rows.img[0] * a.Ci + ci0 + quad * 4;
+            const f32x4 g = *(const f32x4 *)(a.ascale + o);
+            if (!a.ashift) {
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) v[r] *= g;  // out-of-range rows are 0 and stay 0
+            } else {
+                const f32x4 sh = *(const f32x4 *)(a.ashift + o);
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r) {
+                    f32x4 t = v[r] * g + sh;
+                    if (a.arelu) t = __builtin_elementwise_max(t, (f32x4){0.f, 0.f, 0.f, 0.f});
+                    v[r] = inr[r] ? t : v[r];  // zero padding is applied after the normalisation
+                }
             }
         }
     }
@@ -287,7 +339,8 @@ struct LoaderRow {
         for (int j = 0; j < KPT; ++j) {
             const int k = k0 + kq * KPT + j;  // uniform across the wave
             const int ci = k % Ci, rr = k / Ci, kx = rr % KW, ky = rr / KW;
-            const int iy = iy0 + ky, ix = ix0 + kx;
+            const int dil = CI > 0 ? 1 : a.dil;  // the stem instantiation keeps its constant geometry
+            const int iy = iy0 + ky * dil, ix = ix0 + kx * dil;
             const bool in = ok && (k < a.K) && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
             const int64_t off = nchw ? pix + ((int64_t)ci * a.H + iy) * a.W + ix : pix + ((int64_t)iy * a.W + ix) * Ci + ci;
             e[j] = in ? a.x[off] : 0.0f;
@@ -312,7 +365,7 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
 // LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1,
-// 4 contiguous 1x1 (NHWC, Ci % 4 == 0)
+// 4 contiguous 1x1 (NHWC, Ci % 4 == 0), 5 fast + dilation + GroupNorm/ReLU operand affine
 // NBUF: LDS staging buffers.  2 = one barrier per K step; 1 = half the LDS (a
 // third workgroup per CU for the <= 170-VGPR tiles) at two barriers per K step.
 template <int WM, int WN, int TM, int TN, int LOADER, int NBUF>
@@ -341,12 +394,12 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     const int n0 = (bid % n_tiles) * BN;
 
     typename std::conditional<
-        LOADER == 1, LoaderFast<AROWS>,
+        LOADER == 1, LoaderFast<AROWS>, typename std::conditional<LOADER == 5, LoaderFastEx<AROWS>,
         typename std::conditional<LOADER == 2, LoaderRow<BM, 3, 7>,
                                   typename std::conditional<
                                       LOADER == 3, LoaderDual<AROWS>,
                                       typename std::conditional<LOADER == 4, LoaderContig<AROWS>,
-                                                                LoaderRow<BM>>::type>::type>::type>::type la;
+                                                                LoaderRow<BM>>::type>::type>::type>::type>::type la;
     la.init(a, m0, tid);
     const int bq = tid & 7;
     const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
@@ -455,7 +508,7 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     // same-wave LDS ops complete in order: no barrier needed
     const int c4 = lane % C4, rq = lane / C4;
     const int n = n0 + wn * WC + c4 * 4;
-    const bool nvec = ((a.Co & 3) == 0) && (n + 3 < a.Co);
+    const bool nvec = ((a.Co & 3) == 0) && ((a.ldy & 3) == 0) && (n + 3 < a.Co);
     const int64_t mbase = m0 + wm * WR;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
     if (a.bias) {
@@ -481,7 +534,7 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
         if (m >= a.M) continue;
         const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
         float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
-        float *yp = a.y + m * a.Co + n;
+        float *yp = a.y + m * a.ldy + n;
         if (nvec) {
             if (a.res) {
                 o[0] += rv[q].x;
@@ -756,6 +809,7 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2, NBUF>), g, b, 0, st, a);
     else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3, NBUF>), g, b, 0, st, a);
     else if (loader == 4) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 4, NBUF>), g, b, 0, st, a);
+    else if (loader == 5) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 5, NBUF>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0, NBUF>), g, b, 0, st, a);
     return last();
 }
@@ -764,14 +818,10 @@ int g_conv_tile = 0;
 
 // XCD-aware block order (k_conv): on by default since the smaller r01f/r01g tiles put 2-4 N tiles
 // on every A row block; A/B over ResNet-50 (r01g, same box): 3x3 layers -3..-6 %, tails -2..-4 %,
-// 1x1 conv3 / proj -5 %, sum over the layers -1.6 %.  BEV_CONV_XCD=0 restores plain order.
-inline int conv_xcd() {
-    static const int v = [] {
-        const char *e = getenv("BEV_CONV_XCD");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
+// 1x1 conv3 / proj -5 %, sum over the layers -1.6 %.  BEV_TUNE_CONV_XCD = 0 restores plain order.
+int g_conv_xcd = 1;   // BEV_TUNE_CONV_XCD
+int g_conv_nbuf = 0;  // BEV_TUNE_CONV_NBUF
+inline int conv_xcd() { return g_conv_xcd; }
 
 // Tile choice + launch.  Cost model (measured on MI355X, tools/conv_micro.py
 // A/B): time ~ rounds of resident blocks x tile area; ties go to the larger
@@ -781,14 +831,11 @@ inline int conv_xcd() {
 // hides more of the load / epilogue latency than the second barrier per K
 // step costs -- 1x1 layers -4..-13 %, 3x3 layers -4..-7 %, bottleneck tails
 // -8..-13 %).  Small-M 128x64 launches (< 2 full rounds) keep the double
-// buffer.  BEV_CONV_NBUF=1|2 forces the staging depth of tiles 2 / 3.
+// buffer.  BEV_TUNE_CONV_NBUF = 1|2 forces the staging depth of tiles 2 / 3.
 int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
     const int64_t M = a.M;
     const int Co = a.Co;
-    static const int nbuf_env = [] {
-        const char *e = getenv("BEV_CONV_NBUF");
-        return e ? atoi(e) : 0;
-    }();
+    const int nbuf_env = g_conv_nbuf;
     auto nbuf1_for = [&](int tile) {
         if (nbuf_env == 1 || nbuf_env == 2) return nbuf_env == 1;
         return tile == 3 || M >= 400000;
@@ -830,15 +877,14 @@ int bev_tune(int knob, int value) {
         g_conv_tile = value;
         return old;
     }
-    if (knob == BEV_TUNE_WARP_POOL_KB) {
-        if (value < 0 || value > 150) return BEV_ERR_ARGS;
-        return bev::warp_fuse_set_pool_kb(value);
+    if (knob == BEV_TUNE_CONV_XCD || knob == BEV_TUNE_CONV_NBUF) {
+        int *slot = knob == BEV_TUNE_CONV_XCD ? &g_conv_xcd : &g_conv_nbuf;
+        if (value < 0 || value > (knob == BEV_TUNE_CONV_XCD ? 1 : 2)) return BEV_ERR_ARGS;
+        const int old = *slot;
+        *slot = value;
+        return old;
     }
-    if (knob == BEV_TUNE_WARP_UNITS) {
-        if (value < 0 || value > 1) return BEV_ERR_ARGS;
-        return bev::warp_fuse_set_units(value);
-    }
-    return BEV_ERR_ARGS;
+    return bev::warp_tune(knob, value);
 }
 
 int64_t bev_conv_packed_size(int Co, int Ci, int KH, int KW) {
@@ -857,13 +903,24 @@ int bev_conv_pack_weights_f32(const float *w, int Co, int Ci, int KH, int KW, fl
 
 static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed,
                        const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad, int relu,
-                       float *y, int Ho, int Wo, const float *ascale, void *stream);
+                       float *y, int Ho, int Wo, const float *ascale, void *stream, int dil, int ldy,
+                       const float *ashift, int arelu);
 
 int bev_conv2d_f32(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed, const float *bias,
                    const float *residual, int Co, int KH, int KW, int stride, int pad, int relu, float *y, int Ho,
                    int Wo, void *stream) {
     return conv2d_impl(x, in_nchw, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, relu, y, Ho, Wo,
-                       nullptr, stream);
+                       nullptr, stream, 1, Co, nullptr, 0);
+}
+
+int bev_conv2d_nhwc_ex_f32(const float *x, int N, int H, int W, int Ci, const float *in_scale, const float *in_shift,
+                           int in_relu, const float *packed, const float *bias, int Co, int KH, int KW, int stride,
+                           int pad, int dilation, int relu, float *y, int ldy, int Ho, int Wo, void *stream) {
+    if ((in_shift || in_relu) && !in_scale) return BEV_ERR_ARGS;
+    if (in_scale && (Ci % BK != 0 || ((((uintptr_t)in_scale) | ((uintptr_t)in_shift) | ((uintptr_t)x)) & 15) != 0))
+        return BEV_ERR_ARGS;  // the per-channel affine is applied by the fast NHWC loader only
+    return conv2d_impl(x, 0, N, H, W, Ci, packed, bias, nullptr, Co, KH, KW, stride, pad, relu, y, Ho, Wo, in_scale,
+                       stream, dilation, ldy, in_shift, in_relu != 0);
 }
 
 int bev_conv2d_chscale_f32(const float *x, int N, int H, int W, int Ci, const float *gate, const float *packed,
@@ -874,16 +931,18 @@ int bev_conv2d_chscale_f32(const float *x, int N, int H, int W, int Ci, const fl
     const bool contig = KH == 1 && KW == 1 && stride == 1 && pad == 0;
     if (!fast && !contig) return BEV_ERR_ARGS;  // only the fast / contiguous loaders apply the scale
     return conv2d_impl(x, 0, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, relu, y, Ho, Wo, gate,
-                       stream);
+                       stream, 1, Co, nullptr, 0);
 }
 
 static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci, const float *packed,
                        const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad, int relu,
-                       float *y, int Ho, int Wo, const float *ascale, void *stream) {
+                       float *y, int Ho, int Wo, const float *ascale, void *stream, int dil, int ldy,
+                       const float *ashift, int arelu) {
     if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
-        stride <= 0 || pad < 0 || relu < 0 || relu > 2)
+        stride <= 0 || pad < 0 || relu < 0 || relu > 2 || dil <= 0 || ldy < Co || (residual && ldy != Co))
         return BEV_ERR_ARGS;
-    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
+    if (Ho != (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1 ||
+        Ho <= 0 || Wo <= 0)
         return BEV_ERR_ARGS;
     if (N == 0) return 0;
     ConvArgs a;
@@ -910,13 +969,19 @@ static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci,
     a.in_nchw = in_nchw;
     const bool pw = !in_nchw && KH == 1 && KW == 1 && stride == 1 && pad == 0 && Ci % 4 == 0 &&
                     ((uintptr_t)x & 15) == 0;
-    const int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : pw ? 4 : 0;
+    int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : pw ? 4 : 0;
+    if (loader == 1 && (ashift || arelu || dil != 1)) loader = 5;
+    if ((ashift || arelu) && loader != 5) return BEV_ERR_ARGS;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
     a.ascale = ascale;
+    a.ashift = ashift;
+    a.arelu = arelu;
+    a.dil = dil;
+    a.ldy = ldy;
     a.xcd = conv_xcd();
     if (in_nchw && Ci == 3 && KH == 7 && KW == 7 && stride == 2 && pad == 3 && Co <= 64 && !residual && bias &&
-        g_conv_tile == 0 && relu <= 1 && !ascale)
+        g_conv_tile == 0 && relu <= 1 && !ascale && dil == 1 && ldy == Co)
         return launch_stem(x, N, H, W, packed, a.Kp, bias, Co, y, Ho, Wo, relu, (hipStream_t)stream);
     return launch_tiled(a, loader, (hipStream_t)stream);
 }
@@ -953,6 +1018,10 @@ int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const flo
     a.in_nchw = 0;
     a.x2 = x2;
     a.ascale = nullptr;
+    a.ashift = nullptr;
+    a.arelu = 0;
+    a.dil = 1;
+    a.ldy = Co;
     a.xcd = conv_xcd();
     a.Ci2 = Ci2;
     a.H2 = H2;

@@ -1,0 +1,298 @@
+// bev_head.hip -- GroupNorm(+ReLU) of the CenterNet BEV head.
+//
+// Replaces the torch GroupNorm(32) + ReLU of BEVDetector.stem (detector.py:16-30, forward
+// detector.py:47-62) on NHWC activations [N][P][C] (P = H*W pixels), fp32:
+//
+//   k_gn_partial   per (image, block of pixels): sum and sum of squares of every channel group,
+//                  in double (deterministic: one partial per block, no atomics)
+//   k_gn_finalize  per (image, group): mean, rstd = 1/sqrt(var + eps) (biased variance, like torch);
+//                  per (image, channel): scale = rstd * gamma, shift = beta - mean * scale -- the
+//                  affine the NEXT conv applies while loading its operand (bev_conv2d_nhwc_ex_f32
+//                  in_scale / in_shift / in_relu), so in inference the normalised tensor is never
+//                  written; training materialises it with k_gn_apply
+//   k_gn_apply     y = relu(x * scale + shift)  (float4)
+//   k_gn_bwd_partial / k_gn_bwd_finalize / k_gn_bwd_apply
+//                  backward of relu(groupnorm(x)): with g = dy * (y > 0) and xhat = (x - mean) rstd,
+//                  dgamma[c] = sum g xhat, dbeta[c] = sum g, and per (image, group)
+//                  dx = rstd (g gamma - mean(g gamma) - xhat mean(g gamma xhat)).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+constexpr int GN_T = 256;
+constexpr int GN_PIX_PER_BLOCK = 2048;
+
+// thread -> (channel quad q, pixel phase): QP = C / 4 quads per pixel, 256 % QP == 0
+__global__ __launch_bounds__(GN_T) void k_gn_partial(const float *__restrict__ x, int64_t P, int C, int G,
+                                                     double *__restrict__ part /* [N][nb][G][2] */) {
+    __shared__ double red[GN_T][2];
+    const int n = blockIdx.y, nb = gridDim.x, blk = blockIdx.x, tid = threadIdx.x;
+    const int QP = C / 4, q = tid % QP, ph = tid / QP, nph = GN_T / QP;
+    const int64_t p0 = (int64_t)blk * GN_PIX_PER_BLOCK, p1 = p0 + GN_PIX_PER_BLOCK < P ? p0 + GN_PIX_PER_BLOCK : P;
+    const float *xb = x + (size_t)n * P * C;
+    double s = 0.0, ss = 0.0;
+    for (int64_t p = p0 + ph; p < p1; p += nph) {
+        const float4 v = *(const float4 *)(xb + p * C + 4 * q);
+        s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+        ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    red[tid][0] = s;
+    red[tid][1] = ss;
+    __syncthreads();
+    // group g = channels [g * cpg, (g+1) * cpg) = quads [g * cpg / 4, ...); sum over its quads and phases
+    const int cpg = C / G, qpg = cpg / 4;
+    for (int g = tid; g < G; g += GN_T) {
+        double a = 0.0, b = 0.0;
+        for (int t = 0; t < GN_T; ++t) {
+            const int qq = t % QP;
+            if (qq / qpg == g) {
+                a += red[t][0];
+                b += red[t][1];
+            }
+        }
+        double *o = part + (((size_t)n * nb + blk) * G + g) * 2;
+        o[0] = a;
+        o[1] = b;
+    }
+}
+
+__global__ void k_gn_finalize(const double *__restrict__ part, int nb, int64_t P, int C, int G, float eps,
+                              const float *__restrict__ gamma, const float *__restrict__ beta,
+                              float *__restrict__ mean, float *__restrict__ rstd, float *__restrict__ scale,
+                              float *__restrict__ shift) {
+    const int n = blockIdx.x, c = threadIdx.x;  // blockDim.x == C (<= 1024)
+    const int cpg = C / G, g = c / cpg;
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nb; ++k) {
+        const double *o = part + (((size_t)n * nb + k) * G + g) * 2;
+        a += o[0];
+        b += o[1];
+    }
+    const double cnt = (double)P * cpg;
+    const double mu = a / cnt;
+    double var = b / cnt - mu * mu;
+    var = var > 0.0 ? var : 0.0;
+    const float r = (float)(1.0 / __builtin_sqrt(var + (double)eps));
+    const float m = (float)mu;
+    const float sc = r * gamma[c];
+    scale[(size_t)n * C + c] = sc;
+    shift[(size_t)n * C + c] = beta[c] - m * sc;
+    if (c % cpg == 0) {
+        mean[(size_t)n * G + g] = m;
+        rstd[(size_t)n * G + g] = r;
+    }
+}
+
+__global__ void k_gn_apply(const float *__restrict__ x, int64_t P, int C, const float *__restrict__ scale,
+                           const float *__restrict__ shift, int relu, float *__restrict__ y, int64_t total4) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * i;
+        const int c = (int)(e % C);
+        const int n = (int)(e / ((int64_t)P * C));
+        const float4 v = *(const float4 *)(x + e);
+        const float4 s = *(const float4 *)(scale + (size_t)n * C + c), h = *(const float4 *)(shift + (size_t)n * C + c);
+        float4 o = make_float4(v.x * s.x + h.x, v.y * s.y + h.y, v.z * s.z + h.z, v.w * s.w + h.w);
+        if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+        *(float4 *)(y + e) = o;
+    }
+}
+
+// ---- backward ------------------------------------------------------------------------------------
+// part: [N][nb][G][2] (sum g*gamma, sum g*gamma*xhat), cpart: [N][nb][C][2] (sum g*xhat, sum g)
+__global__ __launch_bounds__(GN_T) void k_gn_bwd_partial(const float *__restrict__ x, const float *__restrict__ dy,
+                                                         int64_t P, int C, int G, const float *__restrict__ mean,
+                                                         const float *__restrict__ rstd,
+                                                         const float *__restrict__ gamma,
+                                                         const float *__restrict__ scale,
+                                                         const float *__restrict__ shift, int relu,
+                                                         double *__restrict__ part, double *__restrict__ cpart) {
+    __shared__ double red[GN_T][4][2];  // per thread, per channel of its quad: (g xhat, g)
+    __shared__ double chan[1024][2];    // per channel of this block: (g xhat, g)
+    const int n = blockIdx.y, nb = gridDim.x, blk = blockIdx.x, tid = threadIdx.x;
+    const int QP = C / 4, q = tid % QP, ph = tid / QP, nph = GN_T / QP;
+    const int cpg = C / G;
+    const int64_t p0 = (int64_t)blk * GN_PIX_PER_BLOCK, p1 = p0 + GN_PIX_PER_BLOCK < P ? p0 + GN_PIX_PER_BLOCK : P;
+    const float *xb = x + (size_t)n * P * C, *db = dy + (size_t)n * P * C;
+    float mu[4], rs[4], sc[4], sh[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int c = 4 * q + u, g = c / cpg;
+        mu[u] = mean[(size_t)n * G + g];
+        rs[u] = rstd[(size_t)n * G + g];
+        sc[u] = scale[(size_t)n * C + c];
+        sh[u] = shift[(size_t)n * C + c];
+    }
+    double sgx[4] = {0, 0, 0, 0}, sg[4] = {0, 0, 0, 0};
+    for (int64_t p = p0 + ph; p < p1; p += nph) {
+        const float4 v = *(const float4 *)(xb + p * C + 4 * q), d = *(const float4 *)(db + p * C + 4 * q);
+        const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float gr = (relu && !(xv[u] * sc[u] + sh[u] > 0.f)) ? 0.f : dv[u];
+            const float xh = (xv[u] - mu[u]) * rs[u];
+            sgx[u] += (double)gr * xh;
+            sg[u] += (double)gr;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        red[tid][u][0] = sgx[u];
+        red[tid][u][1] = sg[u];
+    }
+    __syncthreads();
+    // per channel: sum over phases
+    for (int c = tid; c < C; c += GN_T) {
+        const int qq = c / 4, u = c % 4;
+        double a = 0.0, b = 0.0;
+        for (int t = qq; t < GN_T; t += QP) {
+            a += red[t][u][0];
+            b += red[t][u][1];
+        }
+        double *o = cpart + (((size_t)n * nb + blk) * C + c) * 2;
+        o[0] = a;
+        o[1] = b;
+        chan[c][0] = a;
+        chan[c][1] = b;
+    }
+    __syncthreads();
+    // per group: sum over its channels of gamma * (.)
+    for (int g = tid; g < G; g += GN_T) {
+        double a = 0.0, b = 0.0;
+        for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+            a += (double)gamma[c] * chan[c][1];
+            b += (double)gamma[c] * chan[c][0];
+        }
+        double *o = part + (((size_t)n * nb + blk) * G + g) * 2;
+        o[0] = a;  // sum g * gamma
+        o[1] = b;  // sum g * gamma * xhat
+    }
+}
+
+// coef [N][G][2] = (mean(g gamma), mean(g gamma xhat)); dgamma / dbeta [C] (sums over images and blocks)
+__global__ void k_gn_bwd_finalize(const double *__restrict__ part, const double *__restrict__ cpart, int N, int nb,
+                                  int64_t P, int C, int G, float *__restrict__ coef, float *__restrict__ dgamma,
+                                  float *__restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < C) {
+        double a = 0.0, b = 0.0;
+        for (int n = 0; n < N; ++n)
+            for (int k = 0; k < nb; ++k) {
+                const double *o = cpart + (((size_t)n * nb + k) * C + c) * 2;
+                a += o[0];
+                b += o[1];
+            }
+        dgamma[c] = (float)a;
+        dbeta[c] = (float)b;
+    }
+    if (c < N * G) {
+        const int n = c / G, g = c % G;
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < nb; ++k) {
+            const double *o = part + (((size_t)n * nb + k) * G + g) * 2;
+            a += o[0];
+            b += o[1];
+        }
+        const double cnt = (double)P * (C / G);
+        coef[(size_t)c * 2] = (float)(a / cnt);
+        coef[(size_t)c * 2 + 1] = (float)(b / cnt);
+    }
+}
+
+__global__ void k_gn_bwd_apply(const float *__restrict__ x, const float *__restrict__ dy, int64_t P, int C, int G,
+                               const float *__restrict__ mean, const float *__restrict__ rstd,
+                               const float *__restrict__ gamma, const float *__restrict__ scale,
+                               const float *__restrict__ shift, int relu, const float *__restrict__ coef,
+                               float *__restrict__ dx, int64_t total4) {
+    const int cpg = C / G;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * i;
+        const int c0 = (int)(e % C);
+        const int n = (int)(e / ((int64_t)P * C));
+        const float4 v = *(const float4 *)(x + e), d = *(const float4 *)(dy + e);
+        const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u, g = c / cpg;
+            const size_t ng = (size_t)n * G + g;
+            const float sc = scale[(size_t)n * C + c], sh = shift[(size_t)n * C + c];
+            const float gr = (relu && !(xv[u] * sc + sh > 0.f)) ? 0.f : dv[u];
+            const float xh = (xv[u] - mean[ng]) * rstd[ng];
+            o[u] = rstd[ng] * (gr * gamma[c] - coef[2 * ng] - xh * coef[2 * ng + 1]);
+        }
+        *(float4 *)(dx + e) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+inline int nblocks(int64_t P) { return (int)((P + GN_PIX_PER_BLOCK - 1) / GN_PIX_PER_BLOCK); }
+
+bool gn_shape_ok(int N, int64_t P, int C, int G) {
+    if (N <= 0 || P <= 0 || C <= 0 || G <= 0 || C % G != 0 || C % 4 != 0 || C > 1024) return false;
+    const int QP = C / 4;
+    return GN_T % QP == 0 && (C / G) % 4 == 0 && N <= 65535;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t bev_groupnorm_workspace_bytes(int N, int64_t P, int C, int G) {
+    if (!gn_shape_ok(N, P, C, G)) return -1;
+    const int64_t nb = nblocks(P);
+    return (int64_t)N * nb * (G + C) * 2 * (int64_t)sizeof(double) + (int64_t)N * G * 2 * (int64_t)sizeof(float);
+}
+
+int bev_groupnorm_fwd_f32(const float *x, int N, int64_t P, int C, int G, float eps, const float *gamma,
+                          const float *beta, float *mean, float *rstd, float *scale, float *shift, void *workspace,
+                          void *stream) {
+    if (!x || !gamma || !beta || !mean || !rstd || !scale || !shift || !workspace || !gn_shape_ok(N, P, C, G))
+        return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = nblocks(P);
+    double *part = (double *)workspace;
+    hipLaunchKernelGGL(k_gn_partial, dim3(nb, N), dim3(GN_T), 0, st, x, P, C, G, part);
+    hipLaunchKernelGGL(k_gn_finalize, dim3(N), dim3(C), 0, st, part, nb, P, C, G, eps, gamma, beta, mean, rstd, scale,
+                       shift);
+    return (int)hipGetLastError();
+}
+
+int bev_groupnorm_apply_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift, int relu,
+                            float *y, void *stream) {
+    if (!x || !scale || !shift || !y || N <= 0 || P <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
+    const int64_t total4 = (int64_t)N * P * C / 4;
+    int64_t blocks = (total4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_gn_apply, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, P, C, scale, shift,
+                       relu, y, total4);
+    return (int)hipGetLastError();
+}
+
+int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
+                          const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
+                          float *dx, float *dgamma, float *dbeta, void *workspace, void *stream) {
+    if (!x || !dy || !mean || !rstd || !gamma || !scale || !shift || !dx || !dgamma || !dbeta || !workspace ||
+        !gn_shape_ok(N, P, C, G))
+        return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = nblocks(P);
+    double *part = (double *)workspace;                     // [N][nb][G][2]
+    double *cpart = part + (size_t)N * nb * G * 2;          // [N][nb][C][2]
+    // coef [N][G][2] floats after cpart (bev_groupnorm_workspace_bytes sizes all three)
+    hipLaunchKernelGGL(k_gn_bwd_partial, dim3(nb, N), dim3(GN_T), 0, st, x, dy, P, C, G, mean, rstd, gamma, scale,
+                       shift, relu, part, cpart);
+    float *coef = (float *)(cpart + (size_t)N * nb * C * 2);
+    const int nt = (C > N * G ? C : N * G);
+    hipLaunchKernelGGL(k_gn_bwd_finalize, dim3((nt + 255) / 256), dim3(256), 0, st, part, cpart, N, nb, P, C, G, coef,
+                       dgamma, dbeta);
+    const int64_t total4 = (int64_t)N * P * C / 4;
+    int64_t blocks = (total4 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_gn_bwd_apply, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, P, C, G, mean, rstd, gamma,
+                       scale, shift, relu, coef, dx, total4);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_dilate(const float *__restrict__ dz, in
 constexpr int WG_T = 64, WG_M = 16;
 __global__ __launch_bounds__(256) void k_wgrad(const float *__restrict__ x, const float *__restrict__ dz, int N, int H,
                                                int W, int Ci, int Ho, int Wo, int Co, int KH, int KW, int stride,
-                                               int pad, int64_t mchunk, float *__restrict__ dW) {
+                                               int pad, int dil, int64_t mchunk, float *__restrict__ dW) {
     __shared__ float sa[WG_M][WG_T + 4];  // im2col(x)[m][k]
     __shared__ float sd[WG_M][WG_T + 4];  // dz[m][co]
     const int K = KH * KW * Ci;
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const float *__restrict__ x, cons
                 const int k = k0 + c;
                 if (k < K) {
                     const int ci = k % Ci, rr = k / Ci, kx = rr % KW, ky = rr / KW;
-                    const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+                    const int iy = oy * stride - pad + ky * dil, ix = ox * stride - pad + kx * dil;
                     if (iy >= 0 && iy < H && ix >= 0 && ix < W) av = x[(((int64_t)n * H + iy) * W + ix) * Ci + ci];
                 }
                 if (co0 + c < Co) dv = dz[mm * Co + co0 + c];
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const float *__restrict__ x, cons
 // (the generic kernel spends most of its time in the per-element 64-bit index decode).
 __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, const float *__restrict__ dz, int N,
                                                   int H, int W, int Ci, int Ho, int Wo, int Co, int KW, int stride,
-                                                  int pad, int64_t mchunk, float *__restrict__ dW) {
+                                                  int pad, int dil, int64_t mchunk, float *__restrict__ dW) {
     __shared__ __attribute__((aligned(16))) float sa[WG_M][WG_T + 4];
     __shared__ __attribute__((aligned(16))) float sd[WG_M][WG_T + 4];
     const int k0 = blockIdx.x * WG_T, co0 = blockIdx.y * WG_T;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, c
     for (int64_t m = mb; m < me; m += WG_M, mm += WG_M) {
         float4 av = make_float4(0.f, 0.f, 0.f, 0.f), dv = av;
         if (mm < me) {
-            const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+            const int iy = oy * stride - pad + ky * dil, ix = ox * stride - pad + kx * dil;
             if (iy >= 0 && iy < H && ix >= 0 && ix < W)
                 av = *(const float4 *)(x + (((int64_t)n * H + iy) * W + ix) * Ci + ci0 + 4 * c4);
             if (dz_ok) dv = *(const float4 *)(dz + mm * Co + co0 + 4 * c4);
@@ -367,10 +367,17 @@ int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, in
 
 int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,
                        int KW, int stride, int pad, float *dW, void *stream) {
+    return bev_conv_wgrad_ex_f32(x, N, H, W, Ci, dz, Ho, Wo, Co, KH, KW, stride, pad, 1, dW, stream);
+}
+
+int bev_conv_wgrad_ex_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,
+                          int KW, int stride, int pad, int dilation, float *dW, void *stream) {
     if (!x || !dz || !dW || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
-        pad < 0)
+        pad < 0 || dilation <= 0)
         return BEV_ERR_ARGS;
-    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1) return BEV_ERR_ARGS;
+    const int dil = dilation;
+    if (Ho != (H + 2 * pad - dil * (KH - 1) - 1) / stride + 1 || Wo != (W + 2 * pad - dil * (KW - 1) - 1) / stride + 1)
+        return BEV_ERR_ARGS;
     const int K = KH * KW * Ci;
     const int64_t M = (int64_t)N * Ho * Wo;
     hipStream_t st = (hipStream_t)stream;
@@ -384,10 +391,10 @@ int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float 
     if (splits > 65535) return BEV_ERR_ARGS;
     if (Ci % WG_T == 0 && Co % 4 == 0)
         hipLaunchKernelGGL(k_wgrad_v4, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo,
-                           Co, KW, stride, pad, mchunk, dW);
+                           Co, KW, stride, pad, dil, mchunk, dW);
     else
         hipLaunchKernelGGL(k_wgrad, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co,
-                           KH, KW, stride, pad, mchunk, dW);
+                           KH, KW, stride, pad, dil, mchunk, dW);
     return last();
 }
 

@@ -1,0 +1,10 @@
+// bev_tune.h -- internal: performance knobs of the warp library (bev_warp.hip), set through
+// bev_tune() (bev_conv.hip).  Results never depend on them.
+#pragma once
+
+namespace bev {
+
+// knob = BEV_TUNE_WARP_* (include/bev_mi355x.h); returns the previous value or BEV_ERR_ARGS.
+int warp_tune(int knob, int value);
+
+}  // namespace bev

@@ -8,27 +8,31 @@
 //   k_homography     H = K @ [r1 r2 t]                      (geometry.py:60-63)
 //   k_taps           integer corners / weights dump         (geometry.py:161)
 //   k_warp           per-view warp, out [N][C][Hb][Wb]      (geometry.py:142-162)
-//   k_warp_fuse      warp + view reduce, out [B][C][Hb][Wb] (+ fusion.py:17-22)
-//   k_warp_bwd       d out / d feats (float atomics)
+//   k_warp_fuse_pc   warp + view reduce, out [B][C][Hb][Wb] (+ fusion.py:17-22):
+//                    the default path for NHWC features with C % 64 == 0 -- a
+//                    persistent LDS-DMA loader wave feeding four barrier-free
+//                    sampler waves (see its comment block)
+//   k_warp_fuse      the same reduction for any strides / channel count,
+//                    register-staged footprint images (NCHW, C % 64 != 0)
+//   k_warp_fuse_v2   the previous default (per-view workgroup barriers), kept
+//                    for A/B behind BEV_TUNE_WARP_KERNEL = 2
+//   k_warp_bwd_lds   d out / d feats (LDS-reduced scatter, float atomics)
 //   k_view_fuse      SimpleFusion on materialised maps      (fusion.py:19-22)
 //
-// The fused kernel is the hot one.  One workgroup owns a TILE_H x TILE_W tile
-// of BEV cells (one lane per cell, a wavefront = one 64-cell row segment, so
-// every per-channel output store is a contiguous 256-B row piece).  For each
-// view it computes the cell's bilinear taps once (bit-exact recipe), reduces
-// the tile's source-footprint bounding box across the workgroup, and - when
-// the footprint fits - stages that feature rectangle (all channels of the
-// current chunk) into LDS as [pixel][channel] so each tap of four channels is
-// ONE ds_read_b128; the view's samples are accumulated in registers in the
-// reference order (v = 0..V-1).  Footprints that do not fit (cells near the
-// horizon map to huge source regions) fall back to direct global gathers for
-// that (tile, view).  Output is written once, non-temporally.
+// Every fused kernel computes a cell's bilinear taps once per view with the
+// bit-exact recipe (bev_geometry.h), stages the tile's source footprint in LDS
+// as [pixel][channel] so each tap of four channels is ONE ds_read_b128, and
+// accumulates the views in the reference order (v = 0..V-1).  Output is written
+// once, non-temporally.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 
 #include "bev_geometry.h"
-#include "bev_warp_fuse.h"
+#include <algorithm>
+#include <atomic>
+
+#include "bev_tune.h"
 #include "../../include/bev_mi355x.h"
 
 using namespace bev;
@@ -355,22 +359,8 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
 }
 
 // -------------------------------------------------------------------------
-// fused warp + reduce, LDS-DMA pipelined (NHWC features, 64-channel chunks)
+// LDS-DMA helpers (NHWC features, 64-channel chunks)
 // -------------------------------------------------------------------------
-// Same tile / lane mapping and arithmetic as k_warp_fuse, but the footprint
-// image of view v+1 is copied global -> LDS by global_load_lds_dwordx4 (no
-// registers, asynchronous) while view v is being sampled, so the copy latency
-// hides under compute and each view costs ONE workgroup barrier.
-//
-// Image layout: pixel p at byte p*272 = 17 slots of 16 B (16 channel groups +
-// 1 pad slot, the same conflict-free padded stride as the register path).  A
-// DMA wave-instruction writes 64 consecutive slots (1 KiB, lane-linear); the
-// pad is produced by giving each lane the GLOBAL source of its slot
-// (slot -> pixel slot/17, channel group slot%17), pad slots re-read group 0.
-// Images live in a ring inside the LDS pool: the next view's image is placed
-// after (or, wrapping, before) the current one; a footprint that does not fit
-// beside the current image is staged synchronously after the current view
-// (and split into overlapping blocks if it exceeds the whole pool).
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
@@ -428,44 +418,6 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
                                               (int)(uint32_t)(q * plane * sizeof(float)), 2);
     }
-}
-
-// Output stores of a 64-channel chunk of an FT_H x FT_W tile, widened: the
-// accumulators go through LDS in 16-channel rounds ([ch][cell] image, two
-// buffers) and come back as float4 = 4 consecutive cells of one channel, so one
-// buffer_store_dwordx4 writes a channel's whole 8 x 32 tile (8 x 128 B) instead
-// of 64 x 4 B per wave-instruction.  Needs Wb % 4 == 0 and a pool >= 2 * 16.25 KiB.
-// Called after a workgroup barrier (the pool is free); ends with one.
-constexpr int TP = FT_W * FT_H + 4;  // [ch][cell] row pitch in floats
-__device__ __forceinline__ void store_chunk_wide(float *chunk, size_t plane, int Hb, int Wb, int i0, int j0,
-                                                 float *lds, int tid, const float (&acc)[64], int mode, double rV) {
-    const int cell = tid;  // tile-local: row = tid >> 5 (wave * 2 + half), col = tid & 31
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * 64 * sizeof(float)), 0x00020000);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        float *T = lds + (r & 1) * 16 * TP;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            float a = acc[16 * r + q];
-            asm volatile("" : "+v"(a)::"memory");
-            T[q * TP + cell] = (mode == BEV_FUSE_MEAN) ? div_rcp(a, rV) : a;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int idx = tid + 256 * k, ch = idx >> 6, quad = idx & 63;
-            const int row = quad >> 3, col = (quad & 7) * 4;
-            const int i = i0 + row, j = j0 + col;
-            if (i < Hb && j < Wb) {
-                const f32x4 v = *(const f32x4 *)(T + ch * TP + row * FT_W + col);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
-                                                       rs, (int)((i * Wb + j) * sizeof(float)),
-                                                       (int)(uint32_t)((16 * r + ch) * plane * sizeof(float)), 2);
-            }
-        }
-    }
-    __syncthreads();
 }
 
 // Footprint bbox of the workgroup for one view (wave partials -> red[] -> block).
@@ -569,151 +521,6 @@ __device__ __forceinline__ void zero_view(float (&acc)[N], int v) {
     if (MODE == BEV_FUSE_MAX) {
 #pragma unroll
         for (int q = 0; q < N; ++q) acc[q] = nan_max(acc[q], 0.0f);
-    }
-}
-
-template <int MODE, int OCC>
-__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_dma(const float *__restrict__ feats, int64_t sN, int64_t sH,
-                                                            int64_t sW, const float *__restrict__ Hmat,
-                                                            const float *__restrict__ xs,
-                                                            const float *__restrict__ ys, int V, int C, int Hf,
-                                                            int Wf, float sx, float sy, int Hb, int Wb,
-                                                            float *__restrict__ out, int pool) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int zp = pool;                                      // zero pixel (256 B)
-    int *red = reinterpret_cast<int *>(smem + pool + 256);    // [2 parity][16]
-    const int maxpix = pool / DPS - 4;                        // ~1 KiB DMA rounding slack
-
-    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, nt = ntx * nty;
-    int tile = blockIdx.x;
-    {
-        const int q = nt / 8, r = nt % 8, x = tile % 8;
-        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
-    }
-    const int tyb = tile / ntx, txb = tile - tyb * ntx;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int i = tyb * FT_H + wave * 2 + (lane >> 5);
-    const int j = txb * FT_W + (lane & 31);
-    const int b = blockIdx.y;
-    const bool inside = (i < Hb) && (j < Wb);
-    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
-    const size_t plane = (size_t)Hb * Wb;
-    const Grid grid = make_grid(Hf, Wf);
-    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
-    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
-    auto taps_of = [&](int v) {
-        float h[9];
-        load_h(Hmat, b * V + v, h);
-        Taps t = cell_taps(h, ccx, ccy, grid, sx, sy);
-        if (!inside) t.valid = 0;
-        return t;
-    };
-
-    for (int c0 = 0; c0 < C; c0 += 64) {
-        // Taps are recomputed per chunk on purpose: without this the compiler hoists
-        // view 0's taps out of the chunk loop and spills them across it.
-        ccx = cx;
-        ccy = cy;
-        asm volatile("" : "+v"(ccx), "+v"(ccy));
-        // max: -inf is the identity of the NaN-propagating max, so no first-view special case
-        float acc[64];
-#pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
-
-        // prologue: plan + prefetch view 0
-        Taps tn = taps_of(0);
-        bool anyn = __ballot(tn.valid != 0) != 0ull;
-        put_box(red, wave_box(tn), wave, lane);
-        __syncthreads();
-        Box bn = get_box(red);
-        int offn = -1;
-        {
-            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-            if (bn.x1 >= 0 && npix <= maxpix) {
-                offn = 0;
-                dma_block(feats + (int64_t)(b * V) * sN + c0, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1,
-                          npix, smem, 0, wave, lane);
-            }
-        }
-
-        for (int v = 0; v < V; ++v) {
-            const Taps t = tn;
-            const bool wave_any = anyn;
-            const Box bx = bn;
-            const int off = offn;
-            const bool empty = bx.x1 < 0;
-            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
-            const float *f = feats + (int64_t)(b * V + v) * sN + c0;
-            bool done = empty;
-            if (!empty && off < 0) {
-                // ---- synchronous staging (did not fit beside the previous image) ----
-                int wb = bw, hb = bh, nbx = 1, nby = 1;
-                if (bw * bh > maxpix) {
-                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
-                    hb = min(bh, maxpix / wb);
-                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
-                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
-                }
-                const bool single = (nbx == 1) && (nby == 1);
-                int mkx = 0, mky = 0;
-                if (!single && t.valid) {
-                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
-                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
-                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
-                }
-                if (!single && !t.valid) zero_view<MODE>(acc, v);
-                for (int ky = 0; ky < nby; ++ky)
-                    for (int kx = 0; kx < nbx; ++kx) {
-                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
-                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
-                        __syncthreads();  // earlier LDS images are no longer read
-                        dma_block(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        __syncthreads();
-                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
-                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE, (OCC >= 4 ? 1 : 4)>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
-                        else if (single) zero_view<MODE>(acc, v);
-                    }
-                done = true;
-            }
-            // ---- look ahead: taps + bbox of view v+1 ----------------------------------
-            const bool more = v + 1 < V;
-            if (more) {
-                tn = taps_of(v + 1);
-                anyn = __ballot(tn.valid != 0) != 0ull;
-                put_box(red + ((v + 1) & 1) * 16, wave_box(tn), wave, lane);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v landed
-            __syncthreads();  // (X) all DMA of view v landed; bbox partials of v+1 visible
-            if (more) {
-                bn = get_box(red + ((v + 1) & 1) * 16);
-                offn = -1;
-                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-                if (bn.x1 >= 0 && npix <= maxpix) {
-                    const int need = ((npix * 17 + 63) >> 6) * 1024;
-                    // ring placement beside the live image of view v (if any)
-                    const int lo = (!done && off >= 0) ? off : 0;
-                    const int hi = (!done && off >= 0) ? off + (((bw * bh * 17 + 63) >> 6) * 1024) : 0;
-                    if (hi + need <= pool) offn = hi;
-                    else if (need <= lo) offn = 0;
-                    if (offn >= 0)
-                        dma_block(feats + (int64_t)(b * V + v + 1) * sN + c0, (int)sH, (int)sW, bn.x0, bn.y0,
-                                  bn.x1 - bn.x0 + 1, npix, smem, offn, wave, lane);
-                }
-            }
-            // ---- sample view v from its prefetched image ------------------------------
-            if (!done) {
-                if (wave_any) sample_view<MODE, (OCC >= 4 ? 1 : 4)>(acc, t, true, v, smem, off, bx.x0, bx.y0, bw, zp);
-                else zero_view<MODE>(acc, v);
-            } else if (empty) {
-                zero_view<MODE>(acc, v);
-            }
-        }
-        if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
-        __syncthreads();  // next chunk reuses red[] and the pool
     }
 }
 
@@ -826,16 +633,29 @@ __device__ __forceinline__ void bilerp4(float (&acc)[N], int q0, const f32x4 &nw
     }
 }
 
-// LDS sampling of one view, software-pipelined by one 4-channel group.
-template <int MODE, int N>
+// LDS sampling of one view, software-pipelined by one 4-channel group (PIPE; else
+// each group's reads are issued right before its use -- fewer live registers, the
+// max reduction's choice).  Invalid taps read the zero pixel `zp` (the nw tap: `zp0`,
+// see k_warp_fuse_pc's blocked views).
+template <int MODE, int N, bool PIPE = true>
 __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t, const unsigned char *smem, int ib,
-                                                 int sx0, int sy0, int sbw, int zp) {
+                                                 int sx0, int sy0, int sbw, int zp, int zp0) {
     constexpr int PS = (N / 4 + 1) * 16, NG = N / 4;
     const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * PS;
-    const unsigned char *a0 = smem + ((t.valid & 1) ? pb : zp);
+    const unsigned char *a0 = smem + ((t.valid & 1) ? pb : zp0);
     const unsigned char *a1 = smem + ((t.valid & 2) ? pb + PS : zp);
     const unsigned char *a2 = smem + ((t.valid & 4) ? pb + sbw * PS : zp);
     const unsigned char *a3 = smem + ((t.valid & 8) ? pb + (sbw + 1) * PS : zp);
+    if (!PIPE) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const f32x4 c0 = *(const f32x4 *)(a0 + g * 16), c1 = *(const f32x4 *)(a1 + g * 16);
+            const f32x4 c2 = *(const f32x4 *)(a2 + g * 16), c3 = *(const f32x4 *)(a3 + g * 16);
+            bilerp4<MODE>(acc, 4 * g, c0, c1, c2, c3, t.w);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
     f32x4 c0 = *(const f32x4 *)a0, c1 = *(const f32x4 *)a1, c2 = *(const f32x4 *)a2, c3 = *(const f32x4 *)a3;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -857,30 +677,21 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t,
     }
 }
 
-template <int MODE, int OCC, bool WIDE, int TH, int CW = 64>
-__global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
-                                                           int64_t sW, const float *__restrict__ Hmat,
-                                                           const float *__restrict__ xs,
-                                                           const float *__restrict__ ys, int V, int C, int Hf,
-                                                           int Wf, float sx, float sy, int Hb, int Wb,
-                                                           float *__restrict__ out, int pool, int dbg) {
-    // dbg: profiling-only ablations (BEV_WARP_DEBUG; results are WRONG when set):
-    //   1 skip views that need synchronous staging, 2 skip LDS sampling, 4 skip stores, 8 skip DMA
-    // WIDE: widened float4 stores through LDS (store_chunk_wide); the launcher checks its conditions
-    constexpr bool wide = WIDE && TH == FT_H && CW == 64;
-    constexpr int NT = TH * FT_W, NW = NT / 64;  // TH / 2 waves, each two rows of 32 cells
-    constexpr int SL = CW / 4 + 1, PS = SL * 16;  // DMA slots / bytes per staged pixel (CW channels + pad)
+template <int MODE, int OCC>
+__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                          int64_t sW, const float *__restrict__ Hmat,
+                                                          const float *__restrict__ xs, const float *__restrict__ ys,
+                                                          int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                                                          int Wb, float *__restrict__ out, int pool) {
+    constexpr int NW = FT_NT / 64;  // 4 waves, each two rows of 32 cells
+    constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int zp = pool;                                    // zero pixel (256 B)
     int *red = reinterpret_cast<int *>(smem + pool + 256);  // [4 * NW] exact-bbox exchange
     float *htab = reinterpret_cast<float *>(smem + pool + 256 + 4 * NW * sizeof(int));  // [V][9] homographies
     const int maxpix = pool / PS - 4;                      // ~1 KiB DMA rounding slack
-    // dbg & 64: per-wave phase stamps (s_memtime) into out (tools/warp_phases_v2.py)
-    const bool stamp = (dbg & 64) != 0;
-    long long T0 = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0, T1 = 0, T2 = 0, T3 = 0;
-    long long ph_sync = 0, ph_dma = 0, ph_samp = 0, ph_wait = 0;
 
-    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
+    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, nt = ntx * nty;
     int tile = blockIdx.x;
     {
         const int q = nt / 8, r = nt % 8, x = tile % 8;
@@ -888,7 +699,7 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
     }
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int i = tyb * TH + wave * 2 + (lane >> 5);
+    const int i = tyb * FT_H + wave * 2 + (lane >> 5);
     const int j = txb * FT_W + (lane & 31);
     const int b = blockIdx.y;
     const bool inside = (i < Hb) && (j < Wb);
@@ -902,7 +713,7 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
     // lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16  (x1 + 1 == 0: empty)
     unsigned lba, lbb;
     {
-        const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
+        const int ia = tyb * FT_H, ib = min(ia + FT_H - 1, Hb - 1);
         const int ja = txb * FT_W, jb = min(ja + FT_W - 1, Wb - 1);
         Box cb{0x7fffffff, 0x7fffffff, -1, -1};
         bool ok = true;
@@ -929,7 +740,6 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
     };
     auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
 
-    if (stamp) T1 = (long long)__builtin_amdgcn_s_memtime();
     float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
     auto taps_of = [&](int v) {
         float h[9];
@@ -940,13 +750,13 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
         return t;
     };
 
-    for (int c0 = 0; c0 < C; c0 += CW) {
+    for (int c0 = 0; c0 < C; c0 += 64) {
         ccx = cx;
         ccy = cy;
         asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep taps per chunk (no hoisting + spills)
-        float acc[CW];
+        float acc[64];
 #pragma unroll
-        for (int q = 0; q < CW; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
         const float *fb = feats + (int64_t)(b * V) * sN + c0;
 
         // Views whose corner box is empty (the tile is outside that camera's feature map)
@@ -975,11 +785,9 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // zero pixel + image of the first live view
-        if (stamp) T2 = (long long)__builtin_amdgcn_s_memtime();
 
         for (int v = v_first, vn; v < V; v = vn) {
             vn = next_live(v);
-            long long ta = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             Box bx = bn;
             const int off = offn;
             const float *f = fb + (int64_t)v * sN;
@@ -995,7 +803,7 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
             }
             const bool empty = bx.x1 < 0;
             const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
-            bool done = empty || ((dbg & 1) && off < 0);
+            bool done = empty;
             if (!done && off < 0) {
                 // ---- synchronous staging, overlapping blocks if larger than the pool ----
                 int wb = bw, hb = bh, nbx = 1, nby = 1;
@@ -1033,13 +841,12 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                         __syncthreads();
                         const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
                         const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE, 1, CW>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        if (go) sample_view<MODE, 1, 64>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
                         else if (single) zero_view<MODE>(acc, v);
                     }
                 done = true;
                 __syncthreads();  // every wave is done with the staged blocks before DMA(v+1) reuses the pool
             }
-            long long tb = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             // ---- look ahead: DMA of the next live view beside the live image of view v ----
             if (vn < V) {
                 bn = box_of(vn);
@@ -1053,271 +860,560 @@ __global__ __launch_bounds__(TH * FT_W, OCC) void k_warp_fuse_v2(const float *__
                     else if (off == 0) {
                         if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
                     } else if (need <= off) offn = 0;
-                    if (offn >= 0 && !(dbg & 8))
+                    if (offn >= 0)
                         dma_block<SL>(fb + (int64_t)vn * sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix,
                                       smem, offn, wave, lane, NW);
                 }
             }
-            long long tc = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             // ---- sample view v from its prefetched image ------------------------------
             if (!done) {
                 if (!have_t) t = taps_of(v);
-                if (__ballot(t.valid != 0) != 0ull && !(dbg & 2))
-                    sample_view_pipe<MODE, CW>(acc, t, smem, off, bx.x0, bx.y0, bw, zp);
-                else if (dbg & 2)
-                    acc[0] += t.w[0] + (float)t.x0;  // keep the taps live
+                if (__ballot(t.valid != 0) != 0ull) sample_view_pipe<MODE, 64>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
                 else zero_view<MODE>(acc, v);
             } else if (empty) {
                 zero_view<MODE>(acc, v);
             }
-            long long td = stamp ? (long long)__builtin_amdgcn_s_memtime() : 0;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
             __syncthreads();  // all of it landed; image of view v and red[] are free
-            if (stamp) {
-                const long long te = (long long)__builtin_amdgcn_s_memtime();
-                ph_sync += tb - ta;
-                ph_dma += tc - tb;
-                ph_samp += td - tc;
-                ph_wait += te - td;
-            }
-        }
-        if (stamp) T3 = (long long)__builtin_amdgcn_s_memtime();
-        if constexpr (wide) {
-            if (!(dbg & 4))
-                store_chunk_wide(out + ((size_t)b * C + c0) * plane, plane, Hb, Wb, tyb * TH, txb * FT_W,
-                                 reinterpret_cast<float *>(smem), tid, acc, MODE, rV);
-        } else if (inside && !(dbg & 4)) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
-        if (dbg & 4) {
-            float z = 0.f;
-            for (int q = 0; q < CW; ++q) z += acc[q];
-            if (z == 12345.f) out[0] = z;  // keep acc live
-        }
-    }
-    if (stamp && lane == 0) {
-        const long long T4 = (long long)__builtin_amdgcn_s_memtime();
-        int *rec = reinterpret_cast<int *>(out) + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) * 12;
-        rec[0] = (int)(T1 - T0);
-        rec[1] = (int)(T2 - T1);
-        rec[2] = (int)ph_sync;
-        rec[3] = (int)ph_dma;
-        rec[4] = (int)ph_samp;
-        rec[5] = (int)ph_wait;
-        rec[6] = (int)(T4 - T3);
-        rec[7] = (int)(T4 - T0);
-        rec[8] = (int)(T0 & 0x7fffffff);
-        rec[9] = (int)(T4 & 0x7fffffff);
-        rec[10] = tile;
-        rec[11] = 0;
-    }
-}
-
-// -------------------------------------------------------------------------
-// fused warp + reduce, one wave per workgroup, no barriers (default DMA path)
-// -------------------------------------------------------------------------
-// A workgroup is ONE wavefront owning a WT_H x WT_W = 4 x 16 tile of BEV cells
-// (lane = cell; each per-channel store is four 64-B row pieces).  The wave
-// computes its own footprint bbox (shuffles), copies the footprint image of
-// view v+1 into its private LDS ring by LDS-DMA (lane-masked to the exact
-// 272-B/pixel image) and samples view v meanwhile; LDS-DMA completion is
-// ordered for the issuing wave by its own vmcnt, so no workgroup barrier is
-// ever needed and waves run free.  Footprints that do not fit beside the live
-// image are copied after it (waited), larger-than-ring ones in overlapping
-// blocks (same decomposition as the register-staged kernel).
-constexpr int WT_W = 16, WT_H = 4;
-
-__device__ __forceinline__ void dma_wave(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
-                                         int npix, unsigned char *smem, int off, int lane) {
-    const int nslot = npix * 17;
-    const float inv_bw = 1.0f / (float)sbw;
-    const int base = sy0 * sH + sx0 * sW;
-    for (int k = 0; k * 64 < nslot; ++k) {
-        const int slot = k * 64 + lane;
-        const int p = slot / 17, sl = slot - p * 17;
-        const int py = fast_div(p, sbw, inv_bw), px = p - py * sbw;
-        const float *src = f + base + py * sH + px * sW + ((sl < 16) ? sl * 4 : 0);
-        const unsigned dst = lds_base(smem) + off + k * 1024;
-        if (slot < nslot) {  // exec-masked tail: the image is exactly npix * 272 B
-            unsigned keep;
-            asm volatile(
-                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                : "=&s"(keep)
-                : "v"(src), "s"(dst)
-                : "memory");
-        }
-    }
-}
-
-template <int MODE>
-__global__ __launch_bounds__(64, 3) void k_warp_fuse_wave(const float *__restrict__ feats, int64_t sN, int64_t sH,
-                                                          int64_t sW, const float *__restrict__ Hmat,
-                                                          const float *__restrict__ xs,
-                                                          const float *__restrict__ ys, int V, int C, int Hf, int Wf,
-                                                          float sx, float sy, int Hb, int Wb, float *__restrict__ out,
-                                                          int ring) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int ZP = 0, RB = 256;  // zero pixel, ring base
-    const int maxpix = ring / DPS;
-    const int ntx = (Wb + WT_W - 1) / WT_W, nty = (Hb + WT_H - 1) / WT_H, nt = ntx * nty;
-    int tile = blockIdx.x;
-    {
-        const int q = nt / 8, r = nt % 8, x = tile % 8;
-        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
-    }
-    const int tyb = tile / ntx, txb = tile - tyb * ntx;
-    const int lane = threadIdx.x;
-    const int i = tyb * WT_H + (lane >> 4);
-    const int j = txb * WT_W + (lane & 15);
-    const int b = blockIdx.y;
-    const bool inside = (i < Hb) && (j < Wb);
-    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
-    const size_t plane = (size_t)Hb * Wb;
-    const Grid grid = make_grid(Hf, Wf);
-    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
-    const int isH = (int)sH, isW = (int)sW;
-    if (lane < 16) *(float4 *)(smem + ZP + lane * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
-    auto taps_of = [&](int v) {
-        float h[9];
-        load_h(Hmat, b * V + v, h);
-        Taps t = cell_taps(h, ccx, ccy, grid, sx, sy);
-        if (!inside) t.valid = 0;
-        return t;
-    };
-    auto uniform_box = [&](const Taps &t) {
-        Box bx = wave_box(t);
-        bx.x0 = __builtin_amdgcn_readfirstlane(bx.x0);
-        bx.y0 = __builtin_amdgcn_readfirstlane(bx.y0);
-        bx.x1 = __builtin_amdgcn_readfirstlane(bx.x1);
-        bx.y1 = __builtin_amdgcn_readfirstlane(bx.y1);
-        return bx;
-    };
-
-    for (int c0 = 0; c0 < C; c0 += 64) {
-        // Taps are recomputed per chunk on purpose: without this the compiler hoists
-        // view 0's taps out of the chunk loop and spills them across it.
-        ccx = cx;
-        ccy = cy;
-        asm volatile("" : "+v"(ccx), "+v"(ccy));
-        float acc[64];
-#pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
-        const float *fb = feats + (int64_t)(b * V) * sN + c0;
-
-        Taps tn = taps_of(0);
-        Box bn = uniform_box(tn);
-        int offn = -1;
-        {
-            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-            if (bn.x1 >= 0 && npix <= maxpix) {
-                offn = RB;
-                dma_wave(fb, isH, isW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem, RB, lane);
-            }
-        }
-        for (int v = 0; v < V; ++v) {
-            const Taps t = tn;
-            const Box bx = bn;
-            const int off = offn;
-            const bool empty = bx.x1 < 0;
-            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
-            const float *f = fb + (int64_t)v * sN;
-            bool done = empty;
-            if (!empty && off < 0) {
-                // ---- synchronous copy (and block split when larger than the ring) ----
-                int wb = bw, hb = bh, nbx = 1, nby = 1;
-                if (bw * bh > maxpix) {
-                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
-                    hb = min(bh, maxpix / wb);
-                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
-                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
-                }
-                const bool single = (nbx == 1) && (nby == 1);
-                int mkx = 0, mky = 0;
-                if (!single && t.valid) {
-                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
-                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
-                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
-                }
-                if (!single && !t.valid) zero_view<MODE>(acc, v);
-                for (int ky = 0; ky < nby; ++ky)
-                    for (int kx = 0; kx < nbx; ++kx) {
-                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
-                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
-                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // ring free
-                        dma_wave(f, isH, isW, sx0, sy0, sbw, sbw * sbh, smem, RB, lane);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
-                        const bool go = __ballot(single ? (t.valid != 0) : mine) != 0ull;
-                        if (go) sample_view<MODE, 2>(acc, t, mine, v, smem, RB, sx0, sy0, sbw, ZP);
-                        else if (single) zero_view<MODE>(acc, v);
-                    }
-                done = true;
-            }
-            const bool more = v + 1 < V;
-            if (more) {
-                tn = taps_of(v + 1);
-                bn = uniform_box(tn);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // image of view v landed (this wave's DMA)
-            if (more) {
-                offn = -1;
-                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-                if (bn.x1 >= 0 && npix <= maxpix) {
-                    const int need = npix * DPS;
-                    const bool live = !done && off >= 0;
-                    const int lo = live ? off : RB, hi = live ? off + bw * bh * DPS : RB;
-                    if (hi + need <= RB + ring) offn = hi;
-                    else if (RB + need <= lo) offn = RB;
-                    if (offn >= 0)
-                        dma_wave(fb + (int64_t)(v + 1) * sN, isH, isW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, smem,
-                                 offn, lane);
-                }
-            }
-            if (!done) {
-                if (__ballot(t.valid != 0) != 0ull) sample_view<MODE, 2>(acc, t, true, v, smem, off, bx.x0, bx.y0, bw, ZP);
-                else zero_view<MODE>(acc, v);
-            } else if (empty) {
-                zero_view<MODE>(acc, v);
-            }
         }
         if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
     }
 }
 
 // -------------------------------------------------------------------------
-// backward (grad w.r.t. feats): scatter-add with float atomics
+// fused warp + reduce: persistent loader / sampler pipeline (default NHWC path)
 // -------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_warp_bwd(const float *__restrict__ gout, const float *__restrict__ Hmat,
-                                                 const float *__restrict__ xs, const float *__restrict__ ys, int V,
-                                                 int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, float scale,
-                                                 int per_view_gout, float *__restrict__ gfeats) {
-    const int j = blockIdx.x * TILE_W + threadIdx.x;
-    const int i = blockIdx.y * TILE_H + threadIdx.y;
-    const int n = blockIdx.z;  // feature map index b*V + v
-    if (i >= Hb || j >= Wb) return;
-    float h[9];
-    load_h(Hmat, n, h);
-    const Grid grid = make_grid(Hf, Wf);
-    const Taps t = cell_taps(h, xs[j], ys[i], grid, sx, sy);
-    if (t.valid == 0) return;
-    const size_t plane = (size_t)Hb * Wb, fplane = (size_t)Hf * Wf;
-    const int src = per_view_gout ? n : n / V;
-    const double rscale = 1.0 / (double)scale;
-    const float *g = gout + (size_t)src * C * plane + (size_t)i * Wb + j;
-    float *gf = gfeats + (size_t)n * C * fplane;
-    const size_t base = (size_t)t.y0 * Wf + t.x0;
-    for (int c = 0; c < C; ++c) {
-        float go = g[(size_t)c * plane];
-        if (scale != 1.0f) go = div_rcp(go, rscale);  // mean backward: grad / V
-        float *p = gf + (size_t)c * fplane + base;
-        if (t.valid & 1) atomicAdd(p, t.w[0] * go);
-        if (t.valid & 2) atomicAdd(p + 1, t.w[1] * go);
-        if (t.valid & 4) atomicAdd(p + Wf, t.w[2] * go);
-        if (t.valid & 8) atomicAdd(p + Wf + 1, t.w[3] * go);
-    }
+// A persistent workgroup = 1 loader wave + 4 sampler waves; 2 workgroups per CU.
+// Work item = (frame b, 64-channel chunk, 8 x 32 BEV tile); a workgroup walks a
+// static list of items inside its XCD's contiguous item range (neighbouring
+// tiles -- which share source pixels -- stay on one L2).
+//
+// Loader wave: per item, corner boxes of every view at once (lane v <-> view v,
+// corner_box), the exact per-cell box for the views where that bound does not
+// apply (horizon tiles), then for each live view the footprint image is copied
+// global -> LDS by LDS-DMA into a byte ring (272-B padded pixels, conflict-free
+// ds_read_b128), footprints larger than the ring in overlapping blocks.  Each
+// image gets a descriptor (view, box, block, H, the tile's cell-centre axes) in
+// a 16-slot descriptor ring; the descriptor is published (its sequence number
+// written) once the image's DMA has landed -- the loader keeps one image's DMA
+// in flight while the previous one is published.  Ring space is recycled from
+// per-slot consumption counters.
+//
+// Sampler waves (two BEV rows of the tile each, one lane per cell): poll the
+// next descriptor, compute the cell's taps for its view (bit recipe,
+// bev_geometry.h), sample from LDS (software-pipelined), count the descriptor
+// consumed, and after the item's END descriptor write the 64 channels with
+// non-temporal stores.  No workgroup barrier anywhere: the four samplers and the
+// loader run free, so one wave's LDS sampling, another's tap arithmetic, the
+// loader's DMA and the previous item's stores overlap on every CU.
+// Same arithmetic and view order as k_warp_fuse_v2 -> bit-identical results.
+constexpr int PC_SAMPLERS = 4;
+constexpr int PC_THREADS = (PC_SAMPLERS + 1) * 64;
+constexpr int PC_ND = 16;   // descriptor ring slots
+constexpr int PC_DI = 80;   // ints per descriptor
+constexpr int PC_ZP = 2 * 272;  // zero pixel + -inf pixel (bytes) right after the ring
+// descriptor fields (ints)
+enum : int {
+    DF_SEQ = 0, DF_KIND, DF_ITEM, DF_VIEW, DF_OFF, DF_SX0, DF_SY0, DF_SBW, DF_BX0, DF_BY0, DF_WB, DF_HB, DF_KX, DF_KY,
+    DF_NBX, DF_NBY, DF_H = 16, DF_NPIX = 25, DF_XS = 32, DF_YS = 64
+};
+constexpr int DK_IMAGE = 1, DK_END = 2, DK_EXIT = 3, DK_KIND = 3;  // kind
+constexpr int DK_NEWVIEW = 4, DK_SINGLE = 8;                        // flags
+
+#ifdef BEV_PC_STAMPS
+// Profiling build only (`make stamps` -> libbev_mi355x_stamps.so, tools/warp_stamps.py): per-wave
+// phase cycles (s_memtime) of k_warp_fuse_pc, [workgroup][wave][8].  Not in the shipped library.
+__device__ long long g_pc_stamps[4096 * 5 * 8];
+#define PC_T(var) const long long var = (long long)__builtin_amdgcn_s_memtime()
+#define PC_ACC(slot, t0) st_acc[slot] += (long long)__builtin_amdgcn_s_memtime() - (t0)
+#define PC_CNT(slot) st_acc[slot] += 1
+#define PC_DECL long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define PC_DUMP(t0)                                                                                   \
+    do {                                                                                              \
+        st_acc[0] = (long long)__builtin_amdgcn_s_memtime() - (t0);                                   \
+        if (lane < 8 && blockIdx.x < 4096) {                                                          \
+            long long vv = 0;                                                                         \
+            for (int q = 0; q < 8; ++q) vv = (lane == q) ? st_acc[q] : vv;                            \
+            g_pc_stamps[((size_t)blockIdx.x * 5 + wave) * 8 + lane] = vv;                             \
+        }                                                                                             \
+    } while (0)
+#else
+#define PC_T(var)
+#define PC_ACC(slot, t0)
+#define PC_CNT(slot)
+#define PC_DECL
+#define PC_DUMP(t0)
+#endif
+
+// Dynamic item scheduling: per-XCD item counters, one set per launch slot (64 slots cycled by the
+// host, each zeroed by hipMemsetAsync on the launch stream right before its launch).  A loader takes
+// the next item of its XCD's contiguous range with one atomic add (prefetched an item ahead); when
+// that range is exhausted it helps the next XCD's.
+constexpr int PC_SLOTS = 64, PC_SCHED_STRIDE = 32;  // counters 128 B apart
+__device__ unsigned g_pc_sched[PC_SLOTS * 8 * PC_SCHED_STRIDE];
+
+inline size_t pc_lds_bytes(int pool) { return (size_t)pool + PC_ZP + (size_t)PC_ND * PC_DI * 4 + 2 * PC_ND * 4; }
+constexpr int PC_LA = 2;  // descriptors ahead of its sampling whose DMA share a sampler issues
+
+// s_waitcnt vmcnt(m) for the largest encodable m <= n (waits for at least the ops older than the last n)
+__device__ __forceinline__ void wait_vm_le(int n) {
+    if (n >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+__device__ __forceinline__ int lds_ld(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// v_writelane: dv with lane f replaced by val (val, f wave-uniform)
+__device__ __forceinline__ int wlane(int dv, int val, int f) { return ((int)__lane_id() == f) ? val : dv; }
+
+// LDS-DMA of one footprint image (pixel p of the sbw-wide block at byte off + p * 272, 17 16-B slots per
+// pixel, slot 16 = pad) issued by ONE wave; lane address math stepped incrementally (64 slots = 3 pixels
+// + 13 slots per instruction).  Returns the number of DMA instructions.
+__device__ __forceinline__ int dma_image(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
+                                         int npix, unsigned char *smem, int off, int lane) {
+    const int ninstr = (npix * 17 + 63) >> 6;
+    int p = lane / 17, sl = lane - 17 * (lane / 17), px = p, py = 0;
+    while (px >= sbw) {
+        px -= sbw;
+        ++py;
+    }
+    const float *base = f + sy0 * sH + sx0 * sW;
+    const unsigned dst0 = lds_base(smem) + off;
+    for (int k = 0; k < ninstr; ++k) {
+        const float *src = (p < npix) ? base + py * sH + px * sW + ((sl < 16) ? sl * 4 : 0) : f;
+        const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(dst0 + k * 1024));
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(dst)
+            : "memory");
+        sl += 13;
+        p += 3;
+        px += 3;
+        if (sl >= 17) {
+            sl -= 17;
+            ++p;
+            ++px;
+        }
+        while (px >= sbw) {
+            px -= sbw;
+            ++py;
+        }
+    }
+    return ninstr;
+}
+
+template <int MODE, int WPC>
+__global__ __launch_bounds__(PC_THREADS, MODE == BEV_FUSE_MAX ? 2 : (WPC == 3 ? 4 : 3)) void k_warp_fuse_pc(
+    const float *__restrict__ feats, int64_t sN, int64_t sH, int64_t sW, const float *__restrict__ Hmat,
+    const float *__restrict__ xs, const float *__restrict__ ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+    int Hb, int Wb, float *__restrict__ out, int pool, unsigned *__restrict__ sched) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int zp = pool, ninfp = pool + 272;
+    int *desc = reinterpret_cast<int *>(smem + pool + PC_ZP);
+    int *cons = desc + PC_ND * PC_DI;  // per slot: samplers done with the descriptor
+    int *landed = cons + PC_ND;        // per slot: samplers whose DMA share of the image has landed
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, ntiles = ntx * nty, nchunk = C / 64;
+    const int nitems = B * nchunk * ntiles;
+    const int xcd = blockIdx.x & 7;  // blocks b, b + 8, ... share an XCD (speed only)
+    const Grid grid = make_grid(Hf, Wf);
+    if (tid < PC_ZP / 4) reinterpret_cast<float *>(smem + zp)[tid] = (tid < 68) ? 0.0f : -__builtin_inff();
+    if (tid < PC_ND) {
+        cons[tid] = 0;
+        landed[tid] = 0;
+        desc[tid * PC_DI + DF_SEQ] = -1;
+    }
+    __syncthreads();
+    PC_DECL;
+    PC_T(t_start);
+
+    if (wave == PC_SAMPLERS) {
+        // ================================ loader ================================
+        // All bookkeeping lives in registers: LDS round trips queue behind the samplers' reads.
+        __builtin_amdgcn_s_setprio(3);  // the samplers wait on this wave: let it issue first
+        const int maxpix = pool / DPS - 4;              // largest single image (~1 KiB DMA slack)
+        const int blkpix = max(pool / 2 / DPS - 4, 4);  // blocks of a decomposed footprint
+        int k = 0, jt = 0, hp = 0;
+        int rb = 0, re = 0;  // lane s: ring byte range [rb, re) of the descriptor in slot s
+        auto publish = [&](int j) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // descriptor fields written first
+            if (lane == 0) lds_st(&desc[(j % PC_ND) * PC_DI + DF_SEQ], j);
+        };
+        // ring offset for `need` bytes beside the live images jt..k-1, or -1
+        auto try_alloc = [&](int need) -> int {
+            int toff = -1;
+            for (int j = jt; j < k; ++j) {
+                const int s0 = j % PC_ND;
+                const int b0 = __builtin_amdgcn_readlane(rb, s0), e0 = __builtin_amdgcn_readlane(re, s0);
+                if (e0 > b0) {
+                    toff = b0;
+                    break;
+                }
+            }
+            if (toff < 0) {
+                hp = need;
+                return 0;
+            }
+            if (hp > toff) {
+                if (need <= pool - hp) {
+                    const int o = hp;
+                    hp += need;
+                    return o;
+                }
+                if (need <= toff) {
+                    hp = need;
+                    return 0;
+                }
+            } else if (need <= toff - hp) {
+                const int o = hp;
+                hp += need;
+                return o;
+            }
+            return -1;
+        };
+        // reserve descriptor k and `need` ring bytes (0: no image); returns the ring offset
+        auto reserve = [&](int need) -> int {
+            for (;;) {
+                if (k - jt < PC_ND) {
+                    if (need == 0) return 0;
+                    const int o = try_alloc(need);
+                    if (o >= 0) return o;
+                }
+                // one LDS read of every slot's consumption counter, then retire what the samplers finished
+                const int consv = (lane < PC_ND) ? lds_ld(&cons[lane]) : 0;
+                bool adv = false;
+                while (jt < k && __builtin_amdgcn_readlane(consv, jt % PC_ND) >= PC_SAMPLERS * (jt / PC_ND + 1)) {
+                    ++jt;
+                    adv = true;
+                }
+                if (adv) continue;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        };
+        auto range_lo = [&](int x) { return (int)((int64_t)nitems * x / 8); };
+        // one atomic per grab (lane 0), broadcast when used
+        auto fetch = [&](int x) {
+            unsigned v = 0;
+            if (lane == 0) v = atomicAdd(&sched[x * PC_SCHED_STRIDE], 1u);
+            return v;
+        };
+        int gx = 0;  // XCD ranges given up (this XCD's own first)
+        unsigned nraw = fetch(xcd);
+        for (;;) {
+            int x = (xcd + gx) & 7;
+            int item = range_lo(x) + __builtin_amdgcn_readfirstlane((int)nraw);
+            while (item >= range_lo(x + 1)) {  // range exhausted: help the next XCD
+                if (++gx == 8) break;
+                x = (xcd + gx) & 7;
+                item = range_lo(x) + __builtin_amdgcn_readfirstlane((int)fetch(x));
+            }
+            if (gx == 8) break;
+            nraw = fetch(x);  // the next item, used one item later
+            PC_CNT(7);
+            PC_T(tcb);
+            const int b = item / (nchunk * ntiles), rem = item - b * nchunk * ntiles;
+            const int c0 = (rem / ntiles) * 64, tile = rem % ntiles;
+            const int tyb = tile / ntx, txb = tile - tyb * ntx;
+            const int ia = tyb * FT_H, ib = min(ia + FT_H - 1, Hb - 1);
+            const int ja = txb * FT_W, jb = min(ja + FT_W - 1, Wb - 1);
+            // the tile's cell-centre axes: lanes 32-63 x (its 32 columns), lanes 0-7 y (its 8 rows),
+            // clamped at the map edge; they travel to the samplers inside every descriptor
+            const float xsv = xs[min(ja + (lane & 31), Wb - 1)];
+            const float ysv = ys[min(ia + (lane & 7), Hb - 1)];
+            const float xa = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xsv), 0));
+            const float xb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xsv), jb - ja));
+            const float ya = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ysv), 0));
+            const float yb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ysv), ib - ia));
+            // corner boxes, lane v <-> view v (packed as in k_warp_fuse_v2)
+            float hv[9];
+            unsigned lba, lbb;
+            {
+                Box cb{0x7fffffff, 0x7fffffff, -1, -1};
+                bool ok = true;
+                if (lane < V) {
+                    load_h(Hmat, b * V + lane, hv);
+                    cb = corner_box(hv, xa, xb, ya, yb, sx, sy, Wf, Hf, ok);
+                    if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) hv[q] = 0.0f;
+                }
+                const bool emp = cb.x1 < 0;
+                lba = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
+                lbb = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
+            }
+            const float *fb = feats + (int64_t)(b * V) * sN + c0;
+            // descriptor image: lane f <- field f; lanes 32-63 carry xs (DF_XS = 32)
+            int dbase = (lane >= 32) ? __builtin_bit_cast(int, xsv) : 0;
+            dbase = wlane(dbase, item, DF_ITEM);
+            PC_ACC(1, tcb);
+            for (int v = 0; v < V; ++v) {
+                const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
+                const unsigned cc = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
+                Box bx{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(cc & 0xffffu) - 1, (int)(cc >> 16) - 1};
+                if ((a >> 31) == 0u && bx.x1 < 0) continue;  // the tile sees nothing of this view
+                float h[9];
+#pragma unroll
+                for (int q = 0; q < 9; ++q)
+                    h[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hv[q]), v));
+                PC_T(tex);
+                if ((a >> 31) != 0u) {
+                    // exact footprint: taps of all 256 cells of the tile (the samplers' recipe)
+                    bx = Box{0x7fffffff, 0x7fffffff, -1, -1};
+                    for (int r = 0; r < PC_SAMPLERS; ++r) {
+                        const int ci = ia + r * 2 + (lane >> 5), cj = ja + (lane & 31);
+                        const float cx = __shfl(xsv, lane & 31), cy = __shfl(ysv, r * 2 + (lane >> 5));
+                        Taps tt = cell_taps(h, cx, cy, grid, sx, sy);
+                        if (ci >= Hb || cj >= Wb) tt.valid = 0;
+                        const Box wbx = wave_box(tt);
+                        bx.x0 = min(bx.x0, wbx.x0);
+                        bx.y0 = min(bx.y0, wbx.y0);
+                        bx.x1 = max(bx.x1, wbx.x1);
+                        bx.y1 = max(bx.y1, wbx.y1);
+                    }
+                    bx.x0 = __builtin_amdgcn_readfirstlane(bx.x0);
+                    bx.y0 = __builtin_amdgcn_readfirstlane(bx.y0);
+                    bx.x1 = __builtin_amdgcn_readfirstlane(bx.x1);
+                    bx.y1 = __builtin_amdgcn_readfirstlane(bx.y1);
+                }
+                PC_ACC(5, tex);
+                if (bx.x1 < 0) continue;  // +0 (max: handled by the samplers)
+                int dv = wlane(dbase, v, DF_VIEW);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) dv = wlane(dv, __builtin_bit_cast(int, h[q]), DF_H + q);
+                const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= blkpix) ? bw : blkpix / 2;
+                    hb = min(bh, blkpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                dv = wlane(dv, bx.x0, DF_BX0);
+                dv = wlane(dv, bx.y0, DF_BY0);
+                dv = wlane(dv, wb, DF_WB);
+                dv = wlane(dv, hb, DF_HB);
+                dv = wlane(dv, nbx, DF_NBX);
+                dv = wlane(dv, nby, DF_NBY);
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        const int npix = sbw * sbh, need = ((npix * 17 + 63) >> 6) * 1024;
+                        PC_T(trs);
+                        const int off = reserve(need);
+                        PC_ACC(2, trs);
+                        const int s = k % PC_ND;
+                        rb = wlane(rb, off, s);
+                        re = wlane(re, off + need, s);
+                        int d2 = wlane(dv, DK_IMAGE | ((kx == 0 && ky == 0) ? DK_NEWVIEW : 0) | (single ? DK_SINGLE : 0), DF_KIND);
+                        d2 = wlane(d2, off, DF_OFF);
+                        d2 = wlane(d2, sx0, DF_SX0);
+                        d2 = wlane(d2, sy0, DF_SY0);
+                        d2 = wlane(d2, sbw, DF_SBW);
+                        d2 = wlane(d2, kx, DF_KX);
+                        d2 = wlane(d2, ky, DF_KY);
+                        d2 = wlane(d2, npix, DF_NPIX);
+                        int *d = desc + s * PC_DI;
+                        if (lane != DF_SEQ) d[lane] = d2;  // one store for the fields + xs
+                        if (lane < 8) d[DF_YS + lane] = __builtin_bit_cast(int, ysv);
+                        PC_CNT(6);
+                        publish(k++);  // the samplers issue the image's DMA themselves
+                    }
+            }
+            // END of the item (also for a tile that sees no view at all)
+            reserve(0);
+            {
+                const int s = k % PC_ND;
+                rb = wlane(rb, 0, s);
+                re = wlane(re, 0, s);
+                const int d2 = wlane(dbase, DK_END, DF_KIND);
+                int *d = desc + s * PC_DI;
+                if (lane != DF_SEQ) d[lane] = d2;
+                if (lane < 8) d[DF_YS + lane] = __builtin_bit_cast(int, ysv);
+            }
+            publish(k++);
+        }
+        reserve(0);
+        if (lane == 0) desc[(k % PC_ND) * PC_DI + DF_KIND] = DK_EXIT;
+        publish(k);
+        PC_DUMP(t_start);
+        return;
+    }
+
+    // ================================ samplers ================================
+    const size_t plane = (size_t)Hb * Wb;
+    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
+    float acc[64];
+    Taps t;
+    t.valid = 0;
+    t.x0 = t.y0 = 0;
+    t.w[0] = t.w[1] = t.w[2] = t.w[3] = 0.0f;
+    bool open = false, inside = false;
+    int i = 0, j = 0, b = 0, c0 = 0, vnext = 0;
+    float cx = 0.0f, cy = 0.0f;
+    // DMA shares: this wave issues DMA instructions wave, wave + 4, ... of every image, PC_LA descriptors
+    // ahead of its sampling; nq packs its instruction count of descriptor q in byte (q & 3)
+    int kd = 0;
+    unsigned nq = 0;
+    auto issue_share = [&](int q, bool block) -> bool {
+        const int *dq = desc + (q % PC_ND) * PC_DI;
+        if (lds_ld(dq + DF_SEQ) != q) {
+            if (!block) return false;
+            while (lds_ld(dq + DF_SEQ) != q) __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");
+        const int fv = ((const volatile int *)dq)[lane];
+        int n = 0;
+        if ((__builtin_amdgcn_readlane(fv, DF_KIND) & DK_KIND) == DK_IMAGE) {
+            const int item = __builtin_amdgcn_readlane(fv, DF_ITEM), v = __builtin_amdgcn_readlane(fv, DF_VIEW);
+            const int bq = item / (nchunk * ntiles), cq = ((item - bq * nchunk * ntiles) / ntiles) * 64;
+            const int npix = __builtin_amdgcn_readlane(fv, DF_NPIX), ninstr = (npix * 17 + 63) >> 6;
+            dma_block<17>(feats + (int64_t)(bq * V + v) * sN + cq, (int)sH, (int)sW, __builtin_amdgcn_readlane(fv, DF_SX0),
+                          __builtin_amdgcn_readlane(fv, DF_SY0), __builtin_amdgcn_readlane(fv, DF_SBW), npix, smem,
+                          __builtin_amdgcn_readlane(fv, DF_OFF), wave, lane, PC_SAMPLERS);
+            n = ninstr > wave ? (ninstr - wave + PC_SAMPLERS - 1) / PC_SAMPLERS : 0;
+        }
+        const int sh = 8 * (q & 3);
+        nq = (nq & ~(255u << sh)) | ((unsigned)n << sh);
+        return true;
+    };
+    for (int k = 0;; ++k) {
+        const int s = k % PC_ND;
+        const volatile int *d = desc + s * PC_DI;
+        PC_T(tpo);
+        if (kd == k) issue_share(kd++, true);  // also waits until descriptor k is planned
+        while (kd <= k + PC_LA && issue_share(kd, false)) ++kd;
+        asm volatile("" ::: "memory");
+        const int dv = d[lane];  // the descriptor's fields, lane f <- field f
+        {
+            // this wave's share landed once at most its later shares are in flight (loads complete in
+            // order; stores in between do not matter); every descriptor counts (the per-slot
+            // threshold assumes one add per sampler and descriptor), images wait for all shares
+            const bool image = (__builtin_amdgcn_readlane(dv, DF_KIND) & DK_KIND) == DK_IMAGE;
+            if (image) {
+                int later = 0;
+                for (int q = k + 1; q < kd; ++q) later += (nq >> (8 * (q & 3))) & 255;
+                wait_vm_le(later);
+            }
+            if (lane == 0) __hip_atomic_fetch_add(&landed[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (image)
+                while (lds_ld(&landed[s]) < PC_SAMPLERS * (k / PC_ND + 1)) __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+        }
+        PC_ACC(1, tpo);
+        PC_CNT(5);
+        auto field = [&](int f) { return __builtin_amdgcn_readlane(dv, f); };
+        const int kind = field(DF_KIND);
+        if ((kind & DK_KIND) == DK_EXIT) break;
+        if (!open) {
+            open = true;
+            const int item = field(DF_ITEM);
+            b = item / (nchunk * ntiles);
+            const int rem = item - b * nchunk * ntiles;
+            c0 = (rem / ntiles) * 64;
+            const int tile = rem % ntiles, tyb = tile / ntx, txb = tile - tyb * ntx;
+            i = tyb * FT_H + wave * 2 + (lane >> 5);
+            j = txb * FT_W + (lane & 31);
+            inside = (i < Hb) && (j < Wb);
+            cx = __builtin_bit_cast(float, d[DF_XS + (lane & 31)]);
+            cy = __builtin_bit_cast(float, d[DF_YS + wave * 2 + (lane >> 5)]);
+            asm volatile("" : "+v"(cx), "+v"(cy));  // keep the taps per item (no hoisting + spills)
+#pragma unroll
+            for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+            vnext = 0;
+        }
+        if ((kind & DK_KIND) == DK_IMAGE) {
+            const int v = field(DF_VIEW);
+            PC_T(tta);
+            if (kind & DK_NEWVIEW) {
+                if (MODE == BEV_FUSE_MAX)
+                    for (; vnext < v; ++vnext) zero_view<MODE>(acc, vnext);  // views this tile does not see
+                vnext = v + 1;
+                float h[9];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) h[q] = __builtin_bit_cast(float, field(DF_H + q));
+                t = cell_taps(h, cx, cy, grid, sx, sy);
+                if (!inside) t.valid = 0;
+                if (!(kind & DK_SINGLE) && !t.valid) zero_view<MODE>(acc, v);
+            }
+            PC_ACC(2, tta);
+            const int off = field(DF_OFF), sx0 = field(DF_SX0), sy0 = field(DF_SY0), sbw = field(DF_SBW);
+            // One sampling call site for both cases (a second inlined copy costs spills).
+            // Block of a decomposed footprint: the lanes whose taps lie in another block
+            // sample a neutral element instead -- +0 for sum / mean (the accumulator is
+            // never -0) and, for max, -inf through the weights (1, 0, 0, 0).
+            Taps ts = t;
+            int zp0 = zp;
+            bool go;
+            if (kind & DK_SINGLE) {
+                go = __ballot(t.valid != 0) != 0ull;
+                if (!go) zero_view<MODE>(acc, v);
+            } else {
+                const int bx0 = field(DF_BX0), by0 = field(DF_BY0), wb = field(DF_WB), hb = field(DF_HB);
+                const int kx = field(DF_KX), ky = field(DF_KY), nbx = field(DF_NBX), nby = field(DF_NBY);
+                int mkx = 0, mky = 0;
+                if (t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - by0) / (hb - 1), nby - 1);
+                }
+                const bool mine = t.valid != 0 && mkx == kx && mky == ky;
+                go = __ballot(mine) != 0ull;
+                if (!mine) {
+                    ts.valid = 0;
+                    if (MODE == BEV_FUSE_MAX) {
+                        ts.w[0] = 1.0f;
+                        ts.w[1] = ts.w[2] = ts.w[3] = 0.0f;
+                        zp0 = ninfp;
+                    }
+                }
+            }
+            PC_T(tsa);
+            if (go) sample_view_pipe<MODE, 64, MODE != BEV_FUSE_MAX>(acc, ts, smem, off, sx0, sy0, sbw, zp, zp0);
+#ifdef BEV_PC_STAMPS
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+            PC_ACC(3, tsa);
+        }
+        // every LDS read of this descriptor has returned (their values were consumed above): release it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(&cons[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((kind & DK_KIND) == DK_END) {
+            if (MODE == BEV_FUSE_MAX)
+                for (; vnext < V; ++vnext) zero_view<MODE>(acc, vnext);
+            PC_T(tst);
+#ifdef BEV_PC_ABLATE_STORE  // profiling ablation only (stamps build): results are wrong
+            if (acc[0] == 1234.5f && acc[63] == 1.0f) out[0] = acc[1];
+#else
+            if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+#endif
+            PC_ACC(4, tst);
+            open = false;
+        }
+    }
+    PC_DUMP(t_start);
+}
+
+// -------------------------------------------------------------------------
+// backward (grad w.r.t. feats)
+// -------------------------------------------------------------------------
 // Backward with the scatter reduced in LDS first.  One workgroup owns a
 // TILE_H x TILE_W tile of BEV cells of one feature map (grid z = b*V + v).  The
 // tile's exact tap footprint (bbox of its valid taps) is an LDS image of
@@ -1328,7 +1424,7 @@ __global__ __launch_bounds__(NT) void k_warp_bwd(const float *__restrict__ gout,
 // Global contention is left only on the edges shared by neighbouring tiles.
 // CC = the largest of 16/8/4/2/1 whose image fits the 32 KiB pool; footprints
 // larger than 8192 pixels (tiles at the horizon) scatter straight to global.
-// Summation order differs from the per-cell atomics (float addition is not
+// Summation order differs from the per-tap atomics (float addition is not
 // associative): equal to the reference's backward within fp32 tolerance.
 constexpr int BW_POOL = 8192;  // floats (32 KiB)
 
@@ -1431,16 +1527,24 @@ __global__ void k_view_fuse(const float *__restrict__ x, int V, int64_t M, float
 inline int err(hipError_t e) { return (int)e; }
 inline int last() { return (int)hipGetLastError(); }
 
-// LDS budget of the fused warp's footprint image (bytes); BEV_WARP_LDS_KB overrides.
-inline int warp_lds_bytes() {
-    static int v = [] {
-        const char *e = getenv("BEV_WARP_LDS_KB");
-        int kb = e ? atoi(e) : 60;
-        if (kb < 4) kb = 4;
-        if (kb > 150) kb = 150;
-        return kb * 1024;
-    }();
-    return v;
+// ---- performance knobs (bev_tune; results never depend on them) -------------
+int g_warp_pool_kb = 0;  // BEV_TUNE_WARP_POOL_KB: LDS image pool / ring per workgroup, 0 = automatic
+int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 per-view barrier (v2, default), 1 register-staged, 2 pipeline
+int g_warp_wgs = 2;      // BEV_TUNE_WARP_WGS: pipeline workgroups per CU (2 or 3)
+int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = BW_POOL
+
+constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
+
+int cu_count() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cache[dev] == 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+        cache[dev] = c;
+    }
+    return cache[dev];
 }
 
 template <int CK, bool VEC>
@@ -1449,7 +1553,7 @@ int launch_fuse(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t 
                 float *out, hipStream_t st) {
     const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
     dim3 grid(ntiles, B), block(FT_NT);
-    const int img = warp_lds_bytes();
+    const int img = FUSE_LDS_BYTES;
     const size_t lds = img + 32 * sizeof(int);
     switch (mode) {
         case BEV_FUSE_SUM:
@@ -1467,176 +1571,6 @@ int launch_fuse(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t 
     return last();
 }
 
-// LDS pool of the DMA-pipelined fused warp (bytes); BEV_WARP_POOL_KB overrides.
-inline int warp_pool_bytes() {
-    static int v = [] {
-        const char *e = getenv("BEV_WARP_POOL_KB");
-        int kb = e ? atoi(e) : 72;
-        if (kb < 8) kb = 8;
-        if (kb > 150) kb = 150;
-        return kb * 1024;
-    }();
-    return v;
-}
-
-// Waves per SIMD the DMA kernel is built for (2: 72 KB pool, <=256 VGPR;
-// 4: 36 KB pool, <=128 VGPR); BEV_WARP_OCC overrides.
-inline int warp_occ() {
-    static int v = [] {
-        const char *e = getenv("BEV_WARP_OCC");
-        const int o = e ? atoi(e) : 3;  // 3: measured best (94.7 us vs 97.8 at 4, 104 at 2; r01 A/B)
-        return (o == 2 || o == 4) ? o : 3;
-    }();
-    return v;
-}
-
-template <int OCC>
-int launch_fuse_dma_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                        int mode, float *out, hipStream_t st, int pool) {
-    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
-    dim3 grid(ntiles, B), block(FT_NT);
-    const size_t lds = pool + 256 + 32 * sizeof(int);
-    if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_dma<BEV_FUSE_SUM, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
-                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_dma<BEV_FUSE_MEAN, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
-                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
-    else
-        hipLaunchKernelGGL((k_warp_fuse_dma<BEV_FUSE_MAX, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
-                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
-    return last();
-}
-
-// Per-wave LDS ring of the barrier-free kernel (bytes); BEV_WARP_RING_KB overrides.
-inline int warp_ring_bytes() {
-    static int v = [] {
-        const char *e = getenv("BEV_WARP_RING_KB");
-        int kb = e ? atoi(e) : 13;
-        if (kb < 2) kb = 2;
-        if (kb > 60) kb = 60;
-        return kb * 1024 - 256;
-    }();
-    return v;
-}
-
-inline int launch_fuse_wave(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
-                            const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                            int Hb, int Wb, int mode, float *out, hipStream_t st) {
-    const int ntiles = ((Wb + WT_W - 1) / WT_W) * ((Hb + WT_H - 1) / WT_H);
-    dim3 grid(ntiles, B), block(64);
-    const int ring = warp_ring_bytes();
-    const size_t lds = 256 + ring;
-    if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL(k_warp_fuse_wave<BEV_FUSE_SUM>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
-                           C, Hf, Wf, sx, sy, Hb, Wb, out, ring);
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL(k_warp_fuse_wave<BEV_FUSE_MEAN>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
-                           C, Hf, Wf, sx, sy, Hb, Wb, out, ring);
-    else
-        hipLaunchKernelGGL(k_warp_fuse_wave<BEV_FUSE_MAX>, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, V,
-                           C, Hf, Wf, sx, sy, Hb, Wb, out, ring);
-    return last();
-}
-
-// Profiling-only ablation flags for k_warp_fuse_v2 (BEV_WARP_DEBUG, results are wrong when set).
-inline int warp_debug() {
-    static int v = [] {
-        const char *e = getenv("BEV_WARP_DEBUG");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
-template <int OCC, bool WIDE, int TH = FT_H, int CW = 64>
-int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                       const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                       int mode, float *out, hipStream_t st, int pool) {
-    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + TH - 1) / TH);
-    dim3 grid(ntiles, B), block(TH * FT_W);
-    const size_t lds = pool + 256 + 4 * (TH / 2) * sizeof(int) + V2_MAXV * 9 * sizeof(float);
-    if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, WIDE, TH, CW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, WIDE, TH, CW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
-    else
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, WIDE, TH, CW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, warp_debug());
-    return last();
-}
-
-template <int OCC>
-int launch_fuse_v2_pick(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                        int mode, float *out, hipStream_t st, int pool) {
-    static const bool want_wide = getenv("BEV_WARP_WIDE") != nullptr;
-    if (want_wide && Wb % 4 == 0 && pool >= 2 * 16 * TP * (int)sizeof(float))
-        return launch_fuse_v2_occ<OCC, true>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode,
-                                             out, st, pool);
-    return launch_fuse_v2_occ<OCC, false>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                          st, pool);
-}
-
-inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
-                          const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                          int Hb, int Wb, int mode, float *out, hipStream_t st) {
-    const char *e = getenv("BEV_WARP_POOL_KB");
-    static const int th = [] {
-        const char *t = getenv("BEV_WARP_TH");
-        return t ? atoi(t) : 8;
-    }();
-    static const int cw = [] {
-        const char *t = getenv("BEV_WARP_CW");
-        return t ? atoi(t) : 64;
-    }();
-    if (cw == 32 && C % 32 == 0) {  // 32-channel passes: 32-wide accumulator, 4 workgroups (16 waves) per CU
-        const int pool = e ? warp_pool_bytes() : 36 * 1024;
-        if (mode == BEV_FUSE_MAX)
-            return launch_fuse_v2_occ<2, false, FT_H, 32>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy,
-                                                          Hb, Wb, mode, out, st, pool);
-        return launch_fuse_v2_occ<4, false, FT_H, 32>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb,
-                                                      Wb, mode, out, st, pool);
-    }
-    if (th == 16 || th == 32) {  // one workgroup per CU: 8 (16) waves on a 16 (32) x 32 tile
-        const int pool = e ? warp_pool_bytes() : 140 * 1024;
-        if (th == 16)
-            return launch_fuse_v2_occ<1, false, 16>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
-                                                    mode, out, st, pool);
-        return launch_fuse_v2_occ<1, false, 32>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
-                                                mode, out, st, pool);
-    }
-    if (warp_occ() == 2 || mode == BEV_FUSE_MAX) {  // MAX's extra live state spills at 128 VGPRs
-        const int pool = e ? warp_pool_bytes() : 72 * 1024;
-        return launch_fuse_v2_pick<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                     st, pool);
-    }
-    if (warp_occ() == 3) {  // 3 workgroups / 12 waves per CU: 170 VGPRs (no spills), ~49 KiB pool
-        const int pool = e ? warp_pool_bytes() : 49 * 1024;
-        return launch_fuse_v2_occ<3, false>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode,
-                                            out, st, pool);
-    }
-    const int pool = e ? warp_pool_bytes() : 36 * 1024;
-    return launch_fuse_v2_pick<4>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                 pool);
-}
-
-inline int launch_fuse_dma(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
-                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                           int Hb, int Wb, int mode, float *out, hipStream_t st) {
-    const char *e = getenv("BEV_WARP_POOL_KB");
-    if (warp_occ() == 2 || mode == BEV_FUSE_MAX) {  // MAX's extra live state spills at 128 VGPRs
-        const int pool = e ? warp_pool_bytes() : 72 * 1024;
-        return launch_fuse_dma_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                      st, pool);
-    }
-    const int pool = e ? warp_pool_bytes() : 36 * 1024;
-    return launch_fuse_dma_occ<4>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                  pool);
-}
-
 template <int CK>
 int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
                    const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
@@ -1649,11 +1583,109 @@ int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
     return launch_fuse<CK, false>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
 }
 
+template <int OCC>
+int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                       const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
+                       int mode, float *out, hipStream_t st, int pool) {
+    const int ntiles = ((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
+    dim3 grid(ntiles, B), block(FT_NT);
+    const size_t lds = pool + 256 + 4 * (FT_NT / 64) * sizeof(int) + V2_MAXV * 9 * sizeof(float);
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys,
+                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys,
+                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    else
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys,
+                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+    return last();
+}
+
+inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
+                          const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                          int Hb, int Wb, int mode, float *out, hipStream_t st) {
+    if (mode == BEV_FUSE_MAX)  // MAX's extra live state spills at 3 workgroups per CU
+        return launch_fuse_v2_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                     g_warp_pool_kb ? g_warp_pool_kb * 1024 : 72 * 1024);
+    return launch_fuse_v2_occ<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                 g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024);
+}
+
+template <int WPC>
+int launch_fuse_pc_w(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                     const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                     float *out, hipStream_t st) {
+    // LDS: WPC workgroups per CU share 160 KiB (ring + zero pixel + descriptors)
+    const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : (WPC == 3 ? 47 : 74) * 1024;
+    const int64_t ntiles = (int64_t)((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
+    const int64_t nitems = (int64_t)B * (C / 64) * ntiles;
+    if (nitems >= (1ll << 30)) return BEV_ERR_ARGS;
+    int64_t grid = (int64_t)cu_count() * WPC;
+    grid = std::min<int64_t>(grid, (nitems + 7) / 8 * 8);
+    grid = std::max<int64_t>(grid / 8 * 8, 8);
+    const size_t lds = pc_lds_bytes(pool);
+    static unsigned *sched_base[64] = {nullptr};  // the counters' address on each device
+    static std::atomic<unsigned> launches{0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BEV_ERR_ARGS;
+    if (!sched_base[dev]) {
+        void *p = nullptr;
+        const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_pc_sched));
+        if (e != hipSuccess) return err(e);
+        sched_base[dev] = static_cast<unsigned *>(p);
+    }
+    unsigned *sched = sched_base[dev] + (size_t)(launches.fetch_add(1) % PC_SLOTS) * 8 * PC_SCHED_STRIDE;
+    const hipError_t e = hipMemsetAsync(sched, 0, 8 * PC_SCHED_STRIDE * sizeof(unsigned), st);
+    if (e != hipSuccess) return err(e);
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL((k_warp_fuse_pc<BEV_FUSE_SUM, WPC>), dim3((unsigned)grid), dim3(PC_THREADS), lds, st, feats,
+                           sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, sched);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL((k_warp_fuse_pc<BEV_FUSE_MEAN, WPC>), dim3((unsigned)grid), dim3(PC_THREADS), lds, st,
+                           feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, sched);
+    else
+        hipLaunchKernelGGL((k_warp_fuse_pc<BEV_FUSE_MAX, WPC>), dim3((unsigned)grid), dim3(PC_THREADS), lds, st, feats,
+                           sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, sched);
+    return last();
+}
+
 }  // namespace
+
+namespace bev {
+int warp_tune(int knob, int value) {
+    int *slot = nullptr;
+    bool ok = false;
+    switch (knob) {
+        case BEV_TUNE_WARP_POOL_KB:
+            slot = &g_warp_pool_kb;
+            ok = value == 0 || (value >= 8 && value <= 150);
+            break;
+        case BEV_TUNE_WARP_KERNEL:
+            slot = &g_warp_kernel;
+            ok = value >= 0 && value <= 2;
+            break;
+        case BEV_TUNE_WARP_WGS:
+            slot = &g_warp_wgs;
+            ok = value == 2 || value == 3;
+            break;
+        case BEV_TUNE_WARP_BWD_POOL:
+            slot = &g_warp_bwd_pool;
+            ok = value >= 0 && value <= BW_POOL;
+            break;
+        default:
+            return BEV_ERR_ARGS;
+    }
+    if (!ok) return BEV_ERR_ARGS;
+    const int old = *slot;
+    *slot = value;
+    return old;
+}
+}  // namespace bev
 
 extern "C" {
 
-int bev_abi_version(void) { return 1; }
+int bev_abi_version(void) { return 2; }
 
 int bev_linspace_f32(double lo, double hi, int n, float *out) {
     if (n < 0 || (n > 0 && !out)) return BEV_ERR_ARGS;
@@ -1679,7 +1711,7 @@ int bev_homography_f32(const float *K, const float *G, int n, float *H, void *st
 
 int bev_ipm_taps_f32(const float *Hmat, const float *xs, const float *ys, int N, int Hf, int Wf, float sx, float sy,
                      int Hb, int Wb, int32_t *x0y0, float *wts, uint8_t *valid, void *stream) {
-    if (N < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0) return BEV_ERR_ARGS;
+    if (N < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || N > 65535) return BEV_ERR_ARGS;
     if (N == 0 || Hb == 0 || Wb == 0) return 0;
     dim3 grid((Wb + TILE_W - 1) / TILE_W, (Hb + TILE_H - 1) / TILE_H, N), block(TILE_W, TILE_H);
     hipLaunchKernelGGL(k_taps, grid, block, 0, (hipStream_t)stream, Hmat, xs, ys, Hf, Wf, sx, sy, Hb, Wb, x0y0, wts,
@@ -1706,20 +1738,19 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
     if (B == 0 || C == 0 || Hb == 0 || Wb == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const bool dma_ok = (sC == 1) && (C % 64 == 0) && Hf < 16384 && Wf < 16384 && ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) && (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) &&
-                        (sH % 4 == 0) && (sN % 4 == 0) &&
-                        (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32) &&  // store_chunk descriptor
-                        getenv("BEV_WARP_NO_DMA") == nullptr;
-    static const bool legacy = getenv("BEV_WARP_V2") != nullptr || getenv("BEV_WARP_V1") != nullptr ||
-                               getenv("BEV_WARP_WAVE") != nullptr;
-    if (!legacy && warp_fuse_units_enabled() && getenv("BEV_WARP_NO_DMA") == nullptr &&
-        warp_fuse_units_ok(sN, sC, sH, sW, feats, C, Hf, Wf, Hb, Wb))
-        return warp_fuse_units(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-    if (dma_ok && getenv("BEV_WARP_WAVE") != nullptr)
-        return launch_fuse_wave(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-    if (dma_ok && V <= V2_MAXV && getenv("BEV_WARP_V1") == nullptr)
+    // LDS-DMA kernels: NHWC 64-channel chunks, 16-B aligned pixels, 32-bit element offsets
+    // inside a map, and 64 output planes addressable by one buffer descriptor (store_chunk)
+    const bool dma_ok = (sC == 1) && (C % 64 == 0) && V <= V2_MAXV && Hf < 16384 && Wf < 16384 &&
+                        ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) &&
+                        (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) && (sN % 4 == 0) &&
+                        (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32);
+    if (dma_ok && g_warp_kernel == 2) {
+        if (g_warp_wgs == 3)
+            return launch_fuse_pc_w<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+        return launch_fuse_pc_w<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    }
+    if (dma_ok && g_warp_kernel == 0)
         return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-    if (dma_ok) return launch_fuse_dma(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 16)
@@ -1729,12 +1760,7 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
     return launch_fuse_ck<64>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
 }
 
-// LDS pool of the backward in floats: BW_POOL, or BEV_WARP_BWD_POOL (tests: force CC < 16 / direct scatter)
-static int bwd_pool() {
-    const char *e = getenv("BEV_WARP_BWD_POOL");
-    const int p = e ? atoi(e) : BW_POOL;
-    return p < 1 ? 1 : (p > BW_POOL ? BW_POOL : p);
-}
+static int bwd_pool() { return g_warp_bwd_pool > 0 ? g_warp_bwd_pool : BW_POOL; }
 
 int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C, int Hf,
                          int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, void *stream) {
@@ -1745,12 +1771,8 @@ int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, 
     if (e != hipSuccess) return err(e);
     if (Hb == 0 || Wb == 0) return 0;
     dim3 grid((Wb + TILE_W - 1) / TILE_W, (Hb + TILE_H - 1) / TILE_H, N), block(TILE_W, TILE_H);
-    if (getenv("BEV_WARP_BWD_DIRECT"))
-        hipLaunchKernelGGL(k_warp_bwd, grid, block, 0, st, gout, Hmat, xs, ys, 1, C, Hf, Wf, sx, sy, Hb, Wb, 1.0f, 1,
-                           gfeats);
-    else
-        hipLaunchKernelGGL(k_warp_bwd_lds, grid, block, 0, st, gout, Hmat, xs, ys, 1, C, Hf, Wf, sx, sy, Hb, Wb, 1.0f,
-                           1, gfeats, bwd_pool());
+    hipLaunchKernelGGL(k_warp_bwd_lds, grid, block, 0, st, gout, Hmat, xs, ys, 1, C, Hf, Wf, sx, sy, Hb, Wb, 1.0f, 1,
+                       gfeats, bwd_pool());
     return last();
 }
 
@@ -1766,12 +1788,8 @@ int bev_ipm_warp_fuse_bwd_f32(const float *gout, const float *Hmat, const float 
     if (Hb == 0 || Wb == 0) return 0;
     dim3 grid((Wb + TILE_W - 1) / TILE_W, (Hb + TILE_H - 1) / TILE_H, B * V), block(TILE_W, TILE_H);
     const float scale = mode == BEV_FUSE_MEAN ? (float)V : 1.0f;
-    if (getenv("BEV_WARP_BWD_DIRECT"))
-        hipLaunchKernelGGL(k_warp_bwd, grid, block, 0, st, gout, Hmat, xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, scale, 0,
-                           gfeats);
-    else
-        hipLaunchKernelGGL(k_warp_bwd_lds, grid, block, 0, st, gout, Hmat, xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, scale,
-                           0, gfeats, bwd_pool());
+    hipLaunchKernelGGL(k_warp_bwd_lds, grid, block, 0, st, gout, Hmat, xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, scale, 0,
+                       gfeats, bwd_pool());
     return last();
 }
 
@@ -1788,5 +1806,11 @@ int bev_view_fuse_f32(const float *x, int B, int V, int64_t M, int mode, float *
     else hipLaunchKernelGGL(k_view_fuse<BEV_FUSE_MAX>, grid, dim3(threads), 0, st, x, V, M, out);
     return last();
 }
+
+#ifdef BEV_PC_STAMPS
+int bev_pc_stamps(void *host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pc_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 }  // extern "C"

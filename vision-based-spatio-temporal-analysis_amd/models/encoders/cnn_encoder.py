@@ -34,6 +34,7 @@ from .efficientnet import EFFICIENTNETS
 from .proj import Proj1x1
 from .resnet import NATIVE_BACKBONES as _RESNETS
 from .resnet import FoldedConv
+from .trunk_grad import conv_act
 
 # backbones with a native (HIP) trunk: timm names of BASELINE configs 1-4
 NATIVE_BACKBONES = dict(_RESNETS, **EFFICIENTNETS)
@@ -92,8 +93,13 @@ class CNNEncoder(ViewEncoder):
             if torch.is_grad_enabled() and (self.proj.weight.requires_grad or self.proj.bias.requires_grad):
                 return Proj1x1.apply(feat, self.proj.weight, self.proj.bias)  # trainable proj (BASELINE config 3)
             return self._fproj(feat, relu=False)
+        c0, c2 = self.backbone[0], self.backbone[2]
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.backbone.parameters()):
+            # trainable fallback stack (the reference trains this nn.Sequential): native autograd nodes
+            y = conv_act(c0, x, relu=True, in_nchw=True)
+            return conv_act(c2, y, relu=True)
         if self._fb is None:
-            self._fb = (FoldedConv(self.backbone[0]), FoldedConv(self.backbone[2]))
+            self._fb = (FoldedConv(c0), FoldedConv(c2))
         y = self._fb[0](x, relu=True, in_nchw=True)
         return self._fb[1](y, relu=True)
 

@@ -24,7 +24,7 @@ import torch.nn as nn
 
 import bev_native as _nat
 
-__all__ = ["ConvBNAct", "MaxPool", "conv_bn_act"]
+__all__ = ["ConvBNAct", "ConvAct", "MaxPool", "conv_bn_act", "conv_act"]
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -84,6 +84,40 @@ class ConvBNAct(torch.autograd.Function):
 
 def conv_bn_act(conv: nn.Conv2d, bn: nn.BatchNorm2d, x, relu: bool, residual=None, in_nchw: bool = False):
     return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, relu, in_nchw, residual)
+
+
+class ConvAct(torch.autograd.Function):
+    """conv2d(x, W, b) (+ ReLU) without BatchNorm -- the fallback encoder's layers (cnn_encoder.py:31-37)
+    and the BEV head's plain convs: forward on the MFMA conv kernel, backward as ConvBNAct's (ReLU mask,
+    dgrad as a stride-1 conv, wgrad, bias column sums)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride: int, pad: int, relu: bool, in_nchw: bool):
+        Co, Ci, k, _ = weight.shape
+        w = weight.detach().float().contiguous()
+        b = bias.detach().float().contiguous() if bias is not None else torch.zeros(Co, device=x.device)
+        y = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(w), b, Co, k, k, stride, pad, relu, in_nchw=in_nchw)
+        ctx.save_for_backward(x, y if relu else None, w)
+        ctx.meta = (stride, pad, relu, in_nchw, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, w = ctx.saved_tensors
+        stride, pad, relu, in_nchw, has_b = ctx.meta
+        k = w.shape[2]
+        dy = dy.contiguous().float()
+        dz = _nat.relu_bwd(dy, y) if relu else dy
+        xn = _nat.nchw_to_nhwc(x) if in_nchw else x
+        H, W = xn.shape[1], xn.shape[2]
+        dx = _dgrad(dz, w, H, W, stride, pad) if (ctx.needs_input_grad[0] and not in_nchw) else None
+        dw = _nat.conv_wgrad(xn, dz, k, k, stride, pad) if ctx.needs_input_grad[1] else None
+        db = _nat.colsum(dz) if (has_b and ctx.needs_input_grad[2]) else None
+        return dx, dw, db, None, None, None, None
+
+
+def conv_act(conv: nn.Conv2d, x, relu: bool, in_nchw: bool = False):
+    return ConvAct.apply(x, conv.weight, conv.bias, conv.stride[0], conv.padding[0], relu, in_nchw)
 
 
 class MaxPool(torch.autograd.Function):

@@ -14,6 +14,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import bev_native as _nat
+
 
 def _conv_gn_relu(cin, cout, dilation=1):
     return [nn.Conv2d(cin, cout, kernel_size=3, padding=dilation, dilation=dilation, bias=False),
@@ -51,41 +53,15 @@ class BEVDetector(nn.Module):
 
     @staticmethod
     def _nms2d(x: torch.Tensor, kernel: int = 3) -> torch.Tensor:
+        """detector.py:65-69 (kept for callers; decode() does this on the device)."""
         peak = F.max_pool2d(x, kernel_size=kernel, stride=1, padding=kernel // 2)
         return x * (x == peak).float()
 
     def decode(self, heatmap, offset, size_cells, conf_thresh: float = 0.4, nms_dist_m: float = 0.5):
-        """Peaks -> world boxes [cx, cy, w, h] + scores per frame (detector.py:71-125)."""
-        B, _, H, W = heatmap.shape
-        peaks = self._nms2d(heatmap)
-        off = offset.permute(0, 2, 3, 1)
-        siz = size_cells.permute(0, 2, 3, 1)
-        x_min, x_max, y_min, y_max = self.bounds
-        rx, ry = (x_max - x_min) / float(W), (y_max - y_min) / float(H)
-        boxes_out, scores_out = [], []
-        for b in range(B):
-            hm = peaks[b, 0]
-            mask = hm > conf_thresh
-            ys, xs = torch.where(mask)
-            scores = hm[mask]
-            if xs.numel() == 0:
-                boxes_out.append(torch.zeros(0, 4, device=heatmap.device))
-                scores_out.append(torch.zeros(0, device=heatmap.device))
-                continue
-            o, s = off[b, ys, xs], siz[b, ys, xs]
-            boxes = torch.stack([x_min + (xs.float() + o[:, 0]) * rx, y_min + (ys.float() + o[:, 1]) * ry,
-                                 s[:, 0] * rx, s[:, 1] * ry], dim=1)
-            if boxes.shape[0] > 1:  # greedy centre-distance NMS in score order
-                keep = []
-                centres = boxes[:, :2]
-                for idx in torch.argsort(scores, descending=True):
-                    c = centres[idx]
-                    if all(torch.norm(centres[k] - c).item() >= nms_dist_m for k in keep):
-                        keep.append(int(idx))
-                boxes, scores = boxes[keep], scores[keep]
-            boxes_out.append(boxes)
-            scores_out.append(scores)
-        return boxes_out, scores_out
+        """Peaks -> world boxes [cx, cy, w, h] + scores per frame (detector.py:71-125) on the device:
+        bev_decode_peaks_f32 (3x3 peak test + threshold + compaction) and bev_decode_nms_f32 (sort by
+        score, box arithmetic, greedy centre-distance NMS).  One host sync per batch, not per pair."""
+        return _nat.decode(heatmap, offset, size_cells, self.bounds, conf_thresh, nms_dist_m)
 
 
 class AnchorDetector(nn.Module):

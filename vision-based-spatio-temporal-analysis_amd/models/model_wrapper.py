@@ -50,8 +50,11 @@ class BEVNet(nn.Module):
         self.res_x = (bev_bounds[1] - bev_bounds[0]) / float(bev_w)
         self.res_y = (bev_bounds[3] - bev_bounds[2]) / float(bev_h)
 
+        # MODEL.BACKBONE_IMPL (extension; default "auto"): "fallback" selects the reference's timm-less
+        # 2-conv encoder for any backbone name (cnn_encoder.py:31-37) -- what the reference runs offline
         self.encoder = CNNEncoder(out_channels=feat_dim, backbone=m["BACKBONE"],
-                                  pretrained=bool(m.get("PRETRAINED", False)), out_index=int(m.get("OUT_INDEX", 2)))
+                                  pretrained=bool(m.get("PRETRAINED", False)), out_index=int(m.get("OUT_INDEX", 2)),
+                                  backbone_impl=str(m.get("BACKBONE_IMPL", "auto")))
         self.geom = GeometryTransformer(bev_h=bev_h, bev_w=bev_w, bev_bounds=bev_bounds, warp_impl="kornia")
         self.fusion = ConcatFusion()
         self.detector = None  # in_channels = V*C (+proj) + 2, known at the first forward
