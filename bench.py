@@ -69,9 +69,8 @@ def parse():
     ap.add_argument("--camera-shard", action="store_true", help="BASELINE configs[4]: cameras sharded over ranks")
     ap.add_argument("--cpu-iters", type=int, default=2, help="frames timed for the CPU baseline (0 = skip)")
     ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
-    ap.add_argument("--warp-kernel", choices=("barrier", "register", "pipeline"), default="barrier",
+    ap.add_argument("--warp-kernel", choices=("dma", "register"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
-    ap.add_argument("--warp-wgs", type=int, default=2, choices=(2, 3), help="pipeline workgroups per CU")
     args = ap.parse_args()
     if args.views is None:
         args.views = 16 if args.camera_shard else 7
@@ -202,7 +201,7 @@ def pmc_traffic(args) -> dict:
     file's numbers (named in `traffic_source`), not counters read by this run."""
     default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone,
                args.camera_shard, args.warp_kernel) == \
-        (7, 64, (1080, 1920), (480, 1440), 1, "resnet50", False, "barrier")
+        (7, 64, (1080, 1920), (480, 1440), 1, "resnet50", False, "dma")
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
     if not default or not files:
         return {}
@@ -267,8 +266,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(rank)
     images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
-    nat.tune(nat.TUNE_WARP_KERNEL, {"barrier": 0, "register": 1, "pipeline": 2}[args.warp_kernel])
-    nat.tune(nat.TUNE_WARP_WGS, args.warp_wgs)
+    nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1}[args.warp_kernel])
     stream = torch.cuda.current_stream(dev)
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
 
@@ -351,7 +349,7 @@ def main():
             "traffic": pmc.get("conv"), "flops_per_step": flops, "conv_ms_per_step": round(conv_ms, 4),
             "encoder_stage_ms": round(bb_ms, 4)}
         ach = alg / (wp_ms * 1e-3) / 1e9
-        wk = {"barrier": "k_warp_fuse_v2", "register": "k_warp_fuse", "pipeline": "k_warp_fuse_pc"}[args.warp_kernel]
+        wk = {"dma": "k_warp_fuse_v2", "register": "k_warp_fuse"}[args.warp_kernel]
         roof_wp = {"kernel": f"{wk} (IPM warp + {'sum' if args.camera_shard else 'mean'}, fused)", "bound": "hbm",
                    "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
                    "traffic": pmc.get("warp"), "alg_bytes_per_launch": alg, "out_bytes": out_b,

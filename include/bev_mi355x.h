@@ -43,16 +43,13 @@ int bev_abi_version(void);
  * BEV_TUNE_WARP_POOL_KB: LDS footprint-image pool (ring) per workgroup of the fused
  *   warp in KiB, 0 = automatic, else 8..150 (small pools force block decomposition).
  * BEV_TUNE_WARP_KERNEL: fused warp kernel for NHWC C % 64 == 0 features:
- *   0 = per-view-barrier LDS-DMA kernel (default), 1 = register-staged, 2 = loader/sampler
- *   pipeline (experimental, slower).
- * BEV_TUNE_WARP_WGS: pipeline workgroups per CU, 2 (default) or 3.
+ *   0 = LDS-DMA kernel (default), 1 = register-staged.
  * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
-#define BEV_TUNE_WARP_WGS 4
 #define BEV_TUNE_WARP_BWD_POOL 5
 #define BEV_TUNE_CONV_XCD 6
 #define BEV_TUNE_CONV_NBUF 7

@@ -86,8 +86,8 @@ def test_tune_knobs_host_only(lib):
     no GPU involved (knobs are read at launch)."""
     import bev_native as nat
     assert lib.bev_tune(99, 0) == -1
-    for knob, good, bad in ((nat.TUNE_CONV_TILE, 3, 5), (nat.TUNE_WARP_POOL_KB, 16, 4), (nat.TUNE_WARP_KERNEL, 2, 3),
-                            (nat.TUNE_WARP_WGS, 3, 1), (nat.TUNE_WARP_BWD_POOL, 96, 1 << 20),
+    for knob, good, bad in ((nat.TUNE_CONV_TILE, 3, 5), (nat.TUNE_WARP_POOL_KB, 16, 4), (nat.TUNE_WARP_KERNEL, 1, 2),
+                            (nat.TUNE_WARP_BWD_POOL, 96, 1 << 20),
                             (nat.TUNE_CONV_XCD, 0, 2), (nat.TUNE_CONV_NBUF, 1, 3)):
         old = lib.bev_tune(knob, good)
         assert old >= 0

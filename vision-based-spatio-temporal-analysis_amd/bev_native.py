@@ -136,11 +136,10 @@ def lib():
 TUNE_CONV_TILE = 1
 TUNE_WARP_POOL_KB = 2
 TUNE_WARP_KERNEL = 3
-TUNE_WARP_WGS = 4
 TUNE_WARP_BWD_POOL = 5
 TUNE_CONV_XCD = 6
 TUNE_CONV_NBUF = 7
-WARP_KERNEL_BARRIER, WARP_KERNEL_REGISTER, WARP_KERNEL_PIPELINE = 0, 1, 2
+WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 
 def tune(knob: int, value: int) -> int:

@@ -8,14 +8,11 @@
 //   k_homography     H = K @ [r1 r2 t]                      (geometry.py:60-63)
 //   k_taps           integer corners / weights dump         (geometry.py:161)
 //   k_warp           per-view warp, out [N][C][Hb][Wb]      (geometry.py:142-162)
-//   k_warp_fuse_pc   warp + view reduce, out [B][C][Hb][Wb] (+ fusion.py:17-22):
-//                    the default path for NHWC features with C % 64 == 0 -- a
-//                    persistent LDS-DMA loader wave feeding four barrier-free
-//                    sampler waves (see its comment block)
+//   k_warp_fuse_v2   warp + view reduce, out [B][C][Hb][Wb] (+ fusion.py:17-22):
+//                    the default for NHWC features with C % 64 == 0 -- corner-bounded
+//                    footprints staged by LDS-DMA, one workgroup barrier per view
 //   k_warp_fuse      the same reduction for any strides / channel count,
 //                    register-staged footprint images (NCHW, C % 64 != 0)
-//   k_warp_fuse_v2   the previous default (per-view workgroup barriers), kept
-//                    for A/B behind BEV_TUNE_WARP_KERNEL = 2
 //   k_warp_bwd_lds   d out / d feats (LDS-reduced scatter, float atomics)
 //   k_view_fuse      SimpleFusion on materialised maps      (fusion.py:19-22)
 //
@@ -30,7 +27,6 @@
 
 #include "bev_geometry.h"
 #include <algorithm>
-#include <atomic>
 
 #include "bev_tune.h"
 #include "../../include/bev_mi355x.h"
@@ -881,537 +877,6 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
 }
 
 // -------------------------------------------------------------------------
-// fused warp + reduce: persistent loader / sampler pipeline (default NHWC path)
-// -------------------------------------------------------------------------
-// A persistent workgroup = 1 loader wave + 4 sampler waves; 2 workgroups per CU.
-// Work item = (frame b, 64-channel chunk, 8 x 32 BEV tile); a workgroup walks a
-// static list of items inside its XCD's contiguous item range (neighbouring
-// tiles -- which share source pixels -- stay on one L2).
-//
-// Loader wave: per item, corner boxes of every view at once (lane v <-> view v,
-// corner_box), the exact per-cell box for the views where that bound does not
-// apply (horizon tiles), then for each live view the footprint image is copied
-// global -> LDS by LDS-DMA into a byte ring (272-B padded pixels, conflict-free
-// ds_read_b128), footprints larger than the ring in overlapping blocks.  Each
-// image gets a descriptor (view, box, block, H, the tile's cell-centre axes) in
-// a 16-slot descriptor ring; the descriptor is published (its sequence number
-// written) once the image's DMA has landed -- the loader keeps one image's DMA
-// in flight while the previous one is published.  Ring space is recycled from
-// per-slot consumption counters.
-//
-// Sampler waves (two BEV rows of the tile each, one lane per cell): poll the
-// next descriptor, compute the cell's taps for its view (bit recipe,
-// bev_geometry.h), sample from LDS (software-pipelined), count the descriptor
-// consumed, and after the item's END descriptor write the 64 channels with
-// non-temporal stores.  No workgroup barrier anywhere: the four samplers and the
-// loader run free, so one wave's LDS sampling, another's tap arithmetic, the
-// loader's DMA and the previous item's stores overlap on every CU.
-// Same arithmetic and view order as k_warp_fuse_v2 -> bit-identical results.
-constexpr int PC_SAMPLERS = 4;
-constexpr int PC_THREADS = (PC_SAMPLERS + 1) * 64;
-constexpr int PC_ND = 16;   // descriptor ring slots
-constexpr int PC_DI = 80;   // ints per descriptor
-constexpr int PC_ZP = 2 * 272;  // zero pixel + -inf pixel (bytes) right after the ring
-// descriptor fields (ints)
-enum : int {
-    DF_SEQ = 0, DF_KIND, DF_ITEM, DF_VIEW, DF_OFF, DF_SX0, DF_SY0, DF_SBW, DF_BX0, DF_BY0, DF_WB, DF_HB, DF_KX, DF_KY,
-    DF_NBX, DF_NBY, DF_H = 16, DF_NPIX = 25, DF_XS = 32, DF_YS = 64
-};
-constexpr int DK_IMAGE = 1, DK_END = 2, DK_EXIT = 3, DK_KIND = 3;  // kind
-constexpr int DK_NEWVIEW = 4, DK_SINGLE = 8;                        // flags
-
-#ifdef BEV_PC_STAMPS
-// Profiling build only (`make stamps` -> libbev_mi355x_stamps.so, tools/warp_stamps.py): per-wave
-// phase cycles (s_memtime) of k_warp_fuse_pc, [workgroup][wave][8].  Not in the shipped library.
-__device__ long long g_pc_stamps[4096 * 5 * 8];
-#define PC_T(var) const long long var = (long long)__builtin_amdgcn_s_memtime()
-#define PC_ACC(slot, t0) st_acc[slot] += (long long)__builtin_amdgcn_s_memtime() - (t0)
-#define PC_CNT(slot) st_acc[slot] += 1
-#define PC_DECL long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}
-#define PC_DUMP(t0)                                                                                   \
-    do {                                                                                              \
-        st_acc[0] = (long long)__builtin_amdgcn_s_memtime() - (t0);                                   \
-        if (lane < 8 && blockIdx.x < 4096) {                                                          \
-            long long vv = 0;                                                                         \
-            for (int q = 0; q < 8; ++q) vv = (lane == q) ? st_acc[q] : vv;                            \
-            g_pc_stamps[((size_t)blockIdx.x * 5 + wave) * 8 + lane] = vv;                             \
-        }                                                                                             \
-    } while (0)
-#else
-#define PC_T(var)
-#define PC_ACC(slot, t0)
-#define PC_CNT(slot)
-#define PC_DECL
-#define PC_DUMP(t0)
-#endif
-
-// Dynamic item scheduling: per-XCD item counters, one set per launch slot (64 slots cycled by the
-// host, each zeroed by hipMemsetAsync on the launch stream right before its launch).  A loader takes
-// the next item of its XCD's contiguous range with one atomic add (prefetched an item ahead); when
-// that range is exhausted it helps the next XCD's.
-constexpr int PC_SLOTS = 64, PC_SCHED_STRIDE = 32;  // counters 128 B apart
-__device__ unsigned g_pc_sched[PC_SLOTS * 8 * PC_SCHED_STRIDE];
-
-inline size_t pc_lds_bytes(int pool) { return (size_t)pool + PC_ZP + (size_t)PC_ND * PC_DI * 4 + 2 * PC_ND * 4; }
-constexpr int PC_LA = 2;  // descriptors ahead of its sampling whose DMA share a sampler issues
-
-// s_waitcnt vmcnt(m) for the largest encodable m <= n (waits for at least the ops older than the last n)
-__device__ __forceinline__ void wait_vm_le(int n) {
-    if (n >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-    else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-__device__ __forceinline__ int lds_ld(const int *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// v_writelane: dv with lane f replaced by val (val, f wave-uniform)
-__device__ __forceinline__ int wlane(int dv, int val, int f) { return ((int)__lane_id() == f) ? val : dv; }
-
-// LDS-DMA of one footprint image (pixel p of the sbw-wide block at byte off + p * 272, 17 16-B slots per
-// pixel, slot 16 = pad) issued by ONE wave; lane address math stepped incrementally (64 slots = 3 pixels
-// + 13 slots per instruction).  Returns the number of DMA instructions.
-__device__ __forceinline__ int dma_image(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
-                                         int npix, unsigned char *smem, int off, int lane) {
-    const int ninstr = (npix * 17 + 63) >> 6;
-    int p = lane / 17, sl = lane - 17 * (lane / 17), px = p, py = 0;
-    while (px >= sbw) {
-        px -= sbw;
-        ++py;
-    }
-    const float *base = f + sy0 * sH + sx0 * sW;
-    const unsigned dst0 = lds_base(smem) + off;
-    for (int k = 0; k < ninstr; ++k) {
-        const float *src = (p < npix) ? base + py * sH + px * sW + ((sl < 16) ? sl * 4 : 0) : f;
-        const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(dst0 + k * 1024));
-        unsigned keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(src), "s"(dst)
-            : "memory");
-        sl += 13;
-        p += 3;
-        px += 3;
-        if (sl >= 17) {
-            sl -= 17;
-            ++p;
-            ++px;
-        }
-        while (px >= sbw) {
-            px -= sbw;
-            ++py;
-        }
-    }
-    return ninstr;
-}
-
-template <int MODE, int WPC>
-__global__ __launch_bounds__(PC_THREADS, MODE == BEV_FUSE_MAX ? 2 : (WPC == 3 ? 4 : 3)) void k_warp_fuse_pc(
-    const float *__restrict__ feats, int64_t sN, int64_t sH, int64_t sW, const float *__restrict__ Hmat,
-    const float *__restrict__ xs, const float *__restrict__ ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-    int Hb, int Wb, float *__restrict__ out, int pool, unsigned *__restrict__ sched) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int zp = pool, ninfp = pool + 272;
-    int *desc = reinterpret_cast<int *>(smem + pool + PC_ZP);
-    int *cons = desc + PC_ND * PC_DI;  // per slot: samplers done with the descriptor
-    int *landed = cons + PC_ND;        // per slot: samplers whose DMA share of the image has landed
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ntx = (Wb + FT_W - 1) / FT_W, nty = (Hb + FT_H - 1) / FT_H, ntiles = ntx * nty, nchunk = C / 64;
-    const int nitems = B * nchunk * ntiles;
-    const int xcd = blockIdx.x & 7;  // blocks b, b + 8, ... share an XCD (speed only)
-    const Grid grid = make_grid(Hf, Wf);
-    if (tid < PC_ZP / 4) reinterpret_cast<float *>(smem + zp)[tid] = (tid < 68) ? 0.0f : -__builtin_inff();
-    if (tid < PC_ND) {
-        cons[tid] = 0;
-        landed[tid] = 0;
-        desc[tid * PC_DI + DF_SEQ] = -1;
-    }
-    __syncthreads();
-    PC_DECL;
-    PC_T(t_start);
-
-    if (wave == PC_SAMPLERS) {
-        // ================================ loader ================================
-        // All bookkeeping lives in registers: LDS round trips queue behind the samplers' reads.
-        __builtin_amdgcn_s_setprio(3);  // the samplers wait on this wave: let it issue first
-        const int maxpix = pool / DPS - 4;              // largest single image (~1 KiB DMA slack)
-        const int blkpix = max(pool / 2 / DPS - 4, 4);  // blocks of a decomposed footprint
-        int k = 0, jt = 0, hp = 0;
-        int rb = 0, re = 0;  // lane s: ring byte range [rb, re) of the descriptor in slot s
-        auto publish = [&](int j) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // descriptor fields written first
-            if (lane == 0) lds_st(&desc[(j % PC_ND) * PC_DI + DF_SEQ], j);
-        };
-        // ring offset for `need` bytes beside the live images jt..k-1, or -1
-        auto try_alloc = [&](int need) -> int {
-            int toff = -1;
-            for (int j = jt; j < k; ++j) {
-                const int s0 = j % PC_ND;
-                const int b0 = __builtin_amdgcn_readlane(rb, s0), e0 = __builtin_amdgcn_readlane(re, s0);
-                if (e0 > b0) {
-                    toff = b0;
-                    break;
-                }
-            }
-            if (toff < 0) {
-                hp = need;
-                return 0;
-            }
-            if (hp > toff) {
-                if (need <= pool - hp) {
-                    const int o = hp;
-                    hp += need;
-                    return o;
-                }
-                if (need <= toff) {
-                    hp = need;
-                    return 0;
-                }
-            } else if (need <= toff - hp) {
-                const int o = hp;
-                hp += need;
-                return o;
-            }
-            return -1;
-        };
-        // reserve descriptor k and `need` ring bytes (0: no image); returns the ring offset
-        auto reserve = [&](int need) -> int {
-            for (;;) {
-                if (k - jt < PC_ND) {
-                    if (need == 0) return 0;
-                    const int o = try_alloc(need);
-                    if (o >= 0) return o;
-                }
-                // one LDS read of every slot's consumption counter, then retire what the samplers finished
-                const int consv = (lane < PC_ND) ? lds_ld(&cons[lane]) : 0;
-                bool adv = false;
-                while (jt < k && __builtin_amdgcn_readlane(consv, jt % PC_ND) >= PC_SAMPLERS * (jt / PC_ND + 1)) {
-                    ++jt;
-                    adv = true;
-                }
-                if (adv) continue;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        };
-        auto range_lo = [&](int x) { return (int)((int64_t)nitems * x / 8); };
-        // one atomic per grab (lane 0), broadcast when used
-        auto fetch = [&](int x) {
-            unsigned v = 0;
-            if (lane == 0) v = atomicAdd(&sched[x * PC_SCHED_STRIDE], 1u);
-            return v;
-        };
-        int gx = 0;  // XCD ranges given up (this XCD's own first)
-        unsigned nraw = fetch(xcd);
-        for (;;) {
-            int x = (xcd + gx) & 7;
-            int item = range_lo(x) + __builtin_amdgcn_readfirstlane((int)nraw);
-            while (item >= range_lo(x + 1)) {  // range exhausted: help the next XCD
-                if (++gx == 8) break;
-                x = (xcd + gx) & 7;
-                item = range_lo(x) + __builtin_amdgcn_readfirstlane((int)fetch(x));
-            }
-            if (gx == 8) break;
-            nraw = fetch(x);  // the next item, used one item later
-            PC_CNT(7);
-            PC_T(tcb);
-            const int b = item / (nchunk * ntiles), rem = item - b * nchunk * ntiles;
-            const int c0 = (rem / ntiles) * 64, tile = rem % ntiles;
-            const int tyb = tile / ntx, txb = tile - tyb * ntx;
-            const int ia = tyb * FT_H, ib = min(ia + FT_H - 1, Hb - 1);
-            const int ja = txb * FT_W, jb = min(ja + FT_W - 1, Wb - 1);
-            // the tile's cell-centre axes: lanes 32-63 x (its 32 columns), lanes 0-7 y (its 8 rows),
-            // clamped at the map edge; they travel to the samplers inside every descriptor
-            const float xsv = xs[min(ja + (lane & 31), Wb - 1)];
-            const float ysv = ys[min(ia + (lane & 7), Hb - 1)];
-            const float xa = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xsv), 0));
-            const float xb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, xsv), jb - ja));
-            const float ya = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ysv), 0));
-            const float yb = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ysv), ib - ia));
-            // corner boxes, lane v <-> view v (packed as in k_warp_fuse_v2)
-            float hv[9];
-            unsigned lba, lbb;
-            {
-                Box cb{0x7fffffff, 0x7fffffff, -1, -1};
-                bool ok = true;
-                if (lane < V) {
-                    load_h(Hmat, b * V + lane, hv);
-                    cb = corner_box(hv, xa, xb, ya, yb, sx, sy, Wf, Hf, ok);
-                    if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 9; ++q) hv[q] = 0.0f;
-                }
-                const bool emp = cb.x1 < 0;
-                lba = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
-                lbb = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
-            }
-            const float *fb = feats + (int64_t)(b * V) * sN + c0;
-            // descriptor image: lane f <- field f; lanes 32-63 carry xs (DF_XS = 32)
-            int dbase = (lane >= 32) ? __builtin_bit_cast(int, xsv) : 0;
-            dbase = wlane(dbase, item, DF_ITEM);
-            PC_ACC(1, tcb);
-            for (int v = 0; v < V; ++v) {
-                const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
-                const unsigned cc = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
-                Box bx{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(cc & 0xffffu) - 1, (int)(cc >> 16) - 1};
-                if ((a >> 31) == 0u && bx.x1 < 0) continue;  // the tile sees nothing of this view
-                float h[9];
-#pragma unroll
-                for (int q = 0; q < 9; ++q)
-                    h[q] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, hv[q]), v));
-                PC_T(tex);
-                if ((a >> 31) != 0u) {
-                    // exact footprint: taps of all 256 cells of the tile (the samplers' recipe)
-                    bx = Box{0x7fffffff, 0x7fffffff, -1, -1};
-                    for (int r = 0; r < PC_SAMPLERS; ++r) {
-                        const int ci = ia + r * 2 + (lane >> 5), cj = ja + (lane & 31);
-                        const float cx = __shfl(xsv, lane & 31), cy = __shfl(ysv, r * 2 + (lane >> 5));
-                        Taps tt = cell_taps(h, cx, cy, grid, sx, sy);
-                        if (ci >= Hb || cj >= Wb) tt.valid = 0;
-                        const Box wbx = wave_box(tt);
-                        bx.x0 = min(bx.x0, wbx.x0);
-                        bx.y0 = min(bx.y0, wbx.y0);
-                        bx.x1 = max(bx.x1, wbx.x1);
-                        bx.y1 = max(bx.y1, wbx.y1);
-                    }
-                    bx.x0 = __builtin_amdgcn_readfirstlane(bx.x0);
-                    bx.y0 = __builtin_amdgcn_readfirstlane(bx.y0);
-                    bx.x1 = __builtin_amdgcn_readfirstlane(bx.x1);
-                    bx.y1 = __builtin_amdgcn_readfirstlane(bx.y1);
-                }
-                PC_ACC(5, tex);
-                if (bx.x1 < 0) continue;  // +0 (max: handled by the samplers)
-                int dv = wlane(dbase, v, DF_VIEW);
-#pragma unroll
-                for (int q = 0; q < 9; ++q) dv = wlane(dv, __builtin_bit_cast(int, h[q]), DF_H + q);
-                const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
-                int wb = bw, hb = bh, nbx = 1, nby = 1;
-                if (bw * bh > maxpix) {
-                    wb = (2 * bw <= blkpix) ? bw : blkpix / 2;
-                    hb = min(bh, blkpix / wb);
-                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
-                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
-                }
-                const bool single = (nbx == 1) && (nby == 1);
-                dv = wlane(dv, bx.x0, DF_BX0);
-                dv = wlane(dv, bx.y0, DF_BY0);
-                dv = wlane(dv, wb, DF_WB);
-                dv = wlane(dv, hb, DF_HB);
-                dv = wlane(dv, nbx, DF_NBX);
-                dv = wlane(dv, nby, DF_NBY);
-                for (int ky = 0; ky < nby; ++ky)
-                    for (int kx = 0; kx < nbx; ++kx) {
-                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
-                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
-                        const int npix = sbw * sbh, need = ((npix * 17 + 63) >> 6) * 1024;
-                        PC_T(trs);
-                        const int off = reserve(need);
-                        PC_ACC(2, trs);
-                        const int s = k % PC_ND;
-                        rb = wlane(rb, off, s);
-                        re = wlane(re, off + need, s);
-                        int d2 = wlane(dv, DK_IMAGE | ((kx == 0 && ky == 0) ? DK_NEWVIEW : 0) | (single ? DK_SINGLE : 0), DF_KIND);
-                        d2 = wlane(d2, off, DF_OFF);
-                        d2 = wlane(d2, sx0, DF_SX0);
-                        d2 = wlane(d2, sy0, DF_SY0);
-                        d2 = wlane(d2, sbw, DF_SBW);
-                        d2 = wlane(d2, kx, DF_KX);
-                        d2 = wlane(d2, ky, DF_KY);
-                        d2 = wlane(d2, npix, DF_NPIX);
-                        int *d = desc + s * PC_DI;
-                        if (lane != DF_SEQ) d[lane] = d2;  // one store for the fields + xs
-                        if (lane < 8) d[DF_YS + lane] = __builtin_bit_cast(int, ysv);
-                        PC_CNT(6);
-                        publish(k++);  // the samplers issue the image's DMA themselves
-                    }
-            }
-            // END of the item (also for a tile that sees no view at all)
-            reserve(0);
-            {
-                const int s = k % PC_ND;
-                rb = wlane(rb, 0, s);
-                re = wlane(re, 0, s);
-                const int d2 = wlane(dbase, DK_END, DF_KIND);
-                int *d = desc + s * PC_DI;
-                if (lane != DF_SEQ) d[lane] = d2;
-                if (lane < 8) d[DF_YS + lane] = __builtin_bit_cast(int, ysv);
-            }
-            publish(k++);
-        }
-        reserve(0);
-        if (lane == 0) desc[(k % PC_ND) * PC_DI + DF_KIND] = DK_EXIT;
-        publish(k);
-        PC_DUMP(t_start);
-        return;
-    }
-
-    // ================================ samplers ================================
-    const size_t plane = (size_t)Hb * Wb;
-    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
-    float acc[64];
-    Taps t;
-    t.valid = 0;
-    t.x0 = t.y0 = 0;
-    t.w[0] = t.w[1] = t.w[2] = t.w[3] = 0.0f;
-    bool open = false, inside = false;
-    int i = 0, j = 0, b = 0, c0 = 0, vnext = 0;
-    float cx = 0.0f, cy = 0.0f;
-    // DMA shares: this wave issues DMA instructions wave, wave + 4, ... of every image, PC_LA descriptors
-    // ahead of its sampling; nq packs its instruction count of descriptor q in byte (q & 3)
-    int kd = 0;
-    unsigned nq = 0;
-    auto issue_share = [&](int q, bool block) -> bool {
-        const int *dq = desc + (q % PC_ND) * PC_DI;
-        if (lds_ld(dq + DF_SEQ) != q) {
-            if (!block) return false;
-            while (lds_ld(dq + DF_SEQ) != q) __builtin_amdgcn_s_sleep(1);
-        }
-        asm volatile("" ::: "memory");
-        const int fv = ((const volatile int *)dq)[lane];
-        int n = 0;
-        if ((__builtin_amdgcn_readlane(fv, DF_KIND) & DK_KIND) == DK_IMAGE) {
-            const int item = __builtin_amdgcn_readlane(fv, DF_ITEM), v = __builtin_amdgcn_readlane(fv, DF_VIEW);
-            const int bq = item / (nchunk * ntiles), cq = ((item - bq * nchunk * ntiles) / ntiles) * 64;
-            const int npix = __builtin_amdgcn_readlane(fv, DF_NPIX), ninstr = (npix * 17 + 63) >> 6;
-            dma_block<17>(feats + (int64_t)(bq * V + v) * sN + cq, (int)sH, (int)sW, __builtin_amdgcn_readlane(fv, DF_SX0),
-                          __builtin_amdgcn_readlane(fv, DF_SY0), __builtin_amdgcn_readlane(fv, DF_SBW), npix, smem,
-                          __builtin_amdgcn_readlane(fv, DF_OFF), wave, lane, PC_SAMPLERS);
-            n = ninstr > wave ? (ninstr - wave + PC_SAMPLERS - 1) / PC_SAMPLERS : 0;
-        }
-        const int sh = 8 * (q & 3);
-        nq = (nq & ~(255u << sh)) | ((unsigned)n << sh);
-        return true;
-    };
-    for (int k = 0;; ++k) {
-        const int s = k % PC_ND;
-        const volatile int *d = desc + s * PC_DI;
-        PC_T(tpo);
-        if (kd == k) issue_share(kd++, true);  // also waits until descriptor k is planned
-        while (kd <= k + PC_LA && issue_share(kd, false)) ++kd;
-        asm volatile("" ::: "memory");
-        const int dv = d[lane];  // the descriptor's fields, lane f <- field f
-        {
-            // this wave's share landed once at most its later shares are in flight (loads complete in
-            // order; stores in between do not matter); every descriptor counts (the per-slot
-            // threshold assumes one add per sampler and descriptor), images wait for all shares
-            const bool image = (__builtin_amdgcn_readlane(dv, DF_KIND) & DK_KIND) == DK_IMAGE;
-            if (image) {
-                int later = 0;
-                for (int q = k + 1; q < kd; ++q) later += (nq >> (8 * (q & 3))) & 255;
-                wait_vm_le(later);
-            }
-            if (lane == 0) __hip_atomic_fetch_add(&landed[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (image)
-                while (lds_ld(&landed[s]) < PC_SAMPLERS * (k / PC_ND + 1)) __builtin_amdgcn_s_sleep(1);
-            asm volatile("" ::: "memory");
-        }
-        PC_ACC(1, tpo);
-        PC_CNT(5);
-        auto field = [&](int f) { return __builtin_amdgcn_readlane(dv, f); };
-        const int kind = field(DF_KIND);
-        if ((kind & DK_KIND) == DK_EXIT) break;
-        if (!open) {
-            open = true;
-            const int item = field(DF_ITEM);
-            b = item / (nchunk * ntiles);
-            const int rem = item - b * nchunk * ntiles;
-            c0 = (rem / ntiles) * 64;
-            const int tile = rem % ntiles, tyb = tile / ntx, txb = tile - tyb * ntx;
-            i = tyb * FT_H + wave * 2 + (lane >> 5);
-            j = txb * FT_W + (lane & 31);
-            inside = (i < Hb) && (j < Wb);
-            cx = __builtin_bit_cast(float, d[DF_XS + (lane & 31)]);
-            cy = __builtin_bit_cast(float, d[DF_YS + wave * 2 + (lane >> 5)]);
-            asm volatile("" : "+v"(cx), "+v"(cy));  // keep the taps per item (no hoisting + spills)
-#pragma unroll
-            for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
-            vnext = 0;
-        }
-        if ((kind & DK_KIND) == DK_IMAGE) {
-            const int v = field(DF_VIEW);
-            PC_T(tta);
-            if (kind & DK_NEWVIEW) {
-                if (MODE == BEV_FUSE_MAX)
-                    for (; vnext < v; ++vnext) zero_view<MODE>(acc, vnext);  // views this tile does not see
-                vnext = v + 1;
-                float h[9];
-#pragma unroll
-                for (int q = 0; q < 9; ++q) h[q] = __builtin_bit_cast(float, field(DF_H + q));
-                t = cell_taps(h, cx, cy, grid, sx, sy);
-                if (!inside) t.valid = 0;
-                if (!(kind & DK_SINGLE) && !t.valid) zero_view<MODE>(acc, v);
-            }
-            PC_ACC(2, tta);
-            const int off = field(DF_OFF), sx0 = field(DF_SX0), sy0 = field(DF_SY0), sbw = field(DF_SBW);
-            // One sampling call site for both cases (a second inlined copy costs spills).
-            // Block of a decomposed footprint: the lanes whose taps lie in another block
-            // sample a neutral element instead -- +0 for sum / mean (the accumulator is
-            // never -0) and, for max, -inf through the weights (1, 0, 0, 0).
-            Taps ts = t;
-            int zp0 = zp;
-            bool go;
-            if (kind & DK_SINGLE) {
-                go = __ballot(t.valid != 0) != 0ull;
-                if (!go) zero_view<MODE>(acc, v);
-            } else {
-                const int bx0 = field(DF_BX0), by0 = field(DF_BY0), wb = field(DF_WB), hb = field(DF_HB);
-                const int kx = field(DF_KX), ky = field(DF_KY), nbx = field(DF_NBX), nby = field(DF_NBY);
-                int mkx = 0, mky = 0;
-                if (t.valid) {
-                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
-                    mkx = (nbx == 1) ? 0 : min((xlo - bx0) / (wb - 1), nbx - 1);
-                    mky = (nby == 1) ? 0 : min((ylo - by0) / (hb - 1), nby - 1);
-                }
-                const bool mine = t.valid != 0 && mkx == kx && mky == ky;
-                go = __ballot(mine) != 0ull;
-                if (!mine) {
-                    ts.valid = 0;
-                    if (MODE == BEV_FUSE_MAX) {
-                        ts.w[0] = 1.0f;
-                        ts.w[1] = ts.w[2] = ts.w[3] = 0.0f;
-                        zp0 = ninfp;
-                    }
-                }
-            }
-            PC_T(tsa);
-            if (go) sample_view_pipe<MODE, 64, MODE != BEV_FUSE_MAX>(acc, ts, smem, off, sx0, sy0, sbw, zp, zp0);
-#ifdef BEV_PC_STAMPS
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-            PC_ACC(3, tsa);
-        }
-        // every LDS read of this descriptor has returned (their values were consumed above): release it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(&cons[s], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if ((kind & DK_KIND) == DK_END) {
-            if (MODE == BEV_FUSE_MAX)
-                for (; vnext < V; ++vnext) zero_view<MODE>(acc, vnext);
-            PC_T(tst);
-#ifdef BEV_PC_ABLATE_STORE  // profiling ablation only (stamps build): results are wrong
-            if (acc[0] == 1234.5f && acc[63] == 1.0f) out[0] = acc[1];
-#else
-            if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
-#endif
-            PC_ACC(4, tst);
-            open = false;
-        }
-    }
-    PC_DUMP(t_start);
-}
-
-// -------------------------------------------------------------------------
 // backward (grad w.r.t. feats)
 // -------------------------------------------------------------------------
 // Backward with the scatter reduced in LDS first.  One workgroup owns a
@@ -1529,8 +994,7 @@ inline int last() { return (int)hipGetLastError(); }
 
 // ---- performance knobs (bev_tune; results never depend on them) -------------
 int g_warp_pool_kb = 0;  // BEV_TUNE_WARP_POOL_KB: LDS image pool / ring per workgroup, 0 = automatic
-int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 per-view barrier (v2, default), 1 register-staged, 2 pipeline
-int g_warp_wgs = 2;      // BEV_TUNE_WARP_WGS: pipeline workgroups per CU (2 or 3)
+int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 LDS-DMA kernel (k_warp_fuse_v2, default), 1 register-staged
 int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = BW_POOL
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
@@ -1612,44 +1076,6 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
                                  g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024);
 }
 
-template <int WPC>
-int launch_fuse_pc_w(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                     const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
-                     float *out, hipStream_t st) {
-    // LDS: WPC workgroups per CU share 160 KiB (ring + zero pixel + descriptors)
-    const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : (WPC == 3 ? 47 : 74) * 1024;
-    const int64_t ntiles = (int64_t)((Wb + FT_W - 1) / FT_W) * ((Hb + FT_H - 1) / FT_H);
-    const int64_t nitems = (int64_t)B * (C / 64) * ntiles;
-    if (nitems >= (1ll << 30)) return BEV_ERR_ARGS;
-    int64_t grid = (int64_t)cu_count() * WPC;
-    grid = std::min<int64_t>(grid, (nitems + 7) / 8 * 8);
-    grid = std::max<int64_t>(grid / 8 * 8, 8);
-    const size_t lds = pc_lds_bytes(pool);
-    static unsigned *sched_base[64] = {nullptr};  // the counters' address on each device
-    static std::atomic<unsigned> launches{0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return BEV_ERR_ARGS;
-    if (!sched_base[dev]) {
-        void *p = nullptr;
-        const hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(g_pc_sched));
-        if (e != hipSuccess) return err(e);
-        sched_base[dev] = static_cast<unsigned *>(p);
-    }
-    unsigned *sched = sched_base[dev] + (size_t)(launches.fetch_add(1) % PC_SLOTS) * 8 * PC_SCHED_STRIDE;
-    const hipError_t e = hipMemsetAsync(sched, 0, 8 * PC_SCHED_STRIDE * sizeof(unsigned), st);
-    if (e != hipSuccess) return err(e);
-    if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_pc<BEV_FUSE_SUM, WPC>), dim3((unsigned)grid), dim3(PC_THREADS), lds, st, feats,
-                           sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, sched);
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_pc<BEV_FUSE_MEAN, WPC>), dim3((unsigned)grid), dim3(PC_THREADS), lds, st,
-                           feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, sched);
-    else
-        hipLaunchKernelGGL((k_warp_fuse_pc<BEV_FUSE_MAX, WPC>), dim3((unsigned)grid), dim3(PC_THREADS), lds, st, feats,
-                           sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, sched);
-    return last();
-}
-
 }  // namespace
 
 namespace bev {
@@ -1663,11 +1089,7 @@ int warp_tune(int knob, int value) {
             break;
         case BEV_TUNE_WARP_KERNEL:
             slot = &g_warp_kernel;
-            ok = value >= 0 && value <= 2;
-            break;
-        case BEV_TUNE_WARP_WGS:
-            slot = &g_warp_wgs;
-            ok = value == 2 || value == 3;
+            ok = value >= 0 && value <= 1;
             break;
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
@@ -1744,11 +1166,6 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
                         ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) &&
                         (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) && (sN % 4 == 0) &&
                         (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32);
-    if (dma_ok && g_warp_kernel == 2) {
-        if (g_warp_wgs == 3)
-            return launch_fuse_pc_w<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-        return launch_fuse_pc_w<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
-    }
     if (dma_ok && g_warp_kernel == 0)
         return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 4)
@@ -1806,11 +1223,5 @@ int bev_view_fuse_f32(const float *x, int B, int V, int64_t M, int mode, float *
     else hipLaunchKernelGGL(k_view_fuse<BEV_FUSE_MAX>, grid, dim3(threads), 0, st, x, V, M, out);
     return last();
 }
-
-#ifdef BEV_PC_STAMPS
-int bev_pc_stamps(void *host, size_t bytes) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pc_stamps), bytes, 0, hipMemcpyDeviceToHost);
-}
-#endif
 
 }  // extern "C"
