@@ -517,3 +517,92 @@ def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, boun
     if min(kept, default=0) < 0:
         raise HipError(f"decode: more than {cap} peak candidates in a frame above conf_thresh={conf_thresh}")
     return [boxes[b, :k] for b, k in enumerate(kept)], [scores[b, :k] for b, k in enumerate(kept)]
+
+
+# ---------------------------------------------------------------------------
+# BEV head (detector.py:16-62): dilated / operand-affine convs, GroupNorm
+# ---------------------------------------------------------------------------
+def conv2d_nhwc_ex(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, K: int, pad: int, dilation: int = 1,
+                   in_scale: torch.Tensor = None, in_shift: torch.Tensor = None, in_relu: bool = False,
+                   out: torch.Tensor = None, relu: bool = False) -> torch.Tensor:
+    """Stride-1 KxK conv over NHWC x [N,H,W,Ci] with dilation and the previous layer's GroupNorm + ReLU
+    applied to the operand (in_scale / in_shift [N, Ci]).  `out` may be a wider NHWC buffer [N,Ho,Wo,>=Co]
+    whose first Co channels receive y."""
+    x = x.contiguous()
+    _require_gpu(x, packed, bias, in_scale, in_shift)
+    N, H, W, Ci = x.shape
+    Ho, Wo = H + 2 * pad - dilation * (K - 1), W + 2 * pad - dilation * (K - 1)
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    assert out.shape[:3] == (N, Ho, Wo) and out.shape[3] >= Co and out.stride(3) == 1 and out.is_contiguous()
+    with _span("conv", x):
+        rc = lib().bev_conv2d_nhwc_ex_f32(_ptr(x), N, H, W, Ci, _ptr(in_scale), _ptr(in_shift), int(in_relu),
+                                          _ptr(packed), _ptr(bias), Co, K, K, 1, pad, dilation, int(relu), _ptr(out),
+                                          out.shape[3], Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_nhwc_ex_f32")
+    return out
+
+
+def conv_wgrad_ex(x: torch.Tensor, dz: torch.Tensor, K: int, pad: int, dilation: int) -> torch.Tensor:
+    """Stride-1 dilated conv weight gradient: x [N,H,W,Ci], dz [N,Ho,Wo,Co] -> dW [Co, Ci, K, K] (OIHW view)."""
+    x, dz = x.contiguous(), dz.contiguous()
+    _require_gpu(x, dz)
+    N, H, W, Ci = x.shape
+    _, Ho, Wo, Co = dz.shape
+    dW = torch.empty(Co, K, K, Ci, device=x.device, dtype=torch.float32)
+    _check(lib().bev_conv_wgrad_ex_f32(_ptr(x), N, H, W, Ci, _ptr(dz), Ho, Wo, Co, K, K, 1, pad, dilation, _ptr(dW),
+                                       _stream(x)), "bev_conv_wgrad_ex_f32")
+    return dW.permute(0, 3, 1, 2)
+
+
+def _gn_workspace(N, P, C, G, device):
+    nbytes = lib().bev_groupnorm_workspace_bytes(N, P, C, G)
+    if nbytes < 0:
+        raise HipError(f"GroupNorm shape not supported: C={C}, G={G}")
+    return torch.empty((nbytes + 7) // 8, device=device, dtype=torch.float64)
+
+
+def groupnorm_fwd(x: torch.Tensor, G: int, gamma: torch.Tensor, beta: torch.Tensor, eps: float):
+    """x [N,H,W,C] NHWC -> (mean [N,G], rstd [N,G], scale [N,C], shift [N,C])."""
+    _require_gpu(x, gamma, beta)
+    assert x.is_contiguous()
+    N, C = x.shape[0], x.shape[-1]
+    P = x.numel() // (N * C)
+    dev = x.device
+    mean = torch.empty(N, G, device=dev)
+    rstd = torch.empty(N, G, device=dev)
+    scale = torch.empty(N, C, device=dev)
+    shift = torch.empty(N, C, device=dev)
+    ws = _gn_workspace(N, P, C, G, dev)
+    with _span("groupnorm", x):
+        rc = lib().bev_groupnorm_fwd_f32(_ptr(x), N, P, C, G, float(eps), _ptr(gamma.detach().contiguous()),
+                                         _ptr(beta.detach().contiguous()), _ptr(mean), _ptr(rstd), _ptr(scale),
+                                         _ptr(shift), _ptr(ws), _stream(x))
+    _check(rc, "bev_groupnorm_fwd_f32")
+    return mean, rstd, scale, shift
+
+
+def groupnorm_apply(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, relu: bool) -> torch.Tensor:
+    _require_gpu(x, scale, shift)
+    assert x.is_contiguous()
+    N, C = x.shape[0], x.shape[-1]
+    y = torch.empty_like(x)
+    _check(lib().bev_groupnorm_apply_f32(_ptr(x), N, x.numel() // (N * C), C, _ptr(scale), _ptr(shift), int(relu),
+                                         _ptr(y), _stream(x)), "bev_groupnorm_apply_f32")
+    return y
+
+
+def groupnorm_bwd(x, dy, G, mean, rstd, gamma, scale, shift, relu: bool):
+    """-> (dx [N,H,W,C], dgamma [C], dbeta [C]) of y = relu?(groupnorm(x))."""
+    x, dy = x.contiguous(), dy.contiguous()
+    _require_gpu(x, dy, mean, rstd, gamma, scale, shift)
+    N, C = x.shape[0], x.shape[-1]
+    P = x.numel() // (N * C)
+    dx = torch.empty_like(x)
+    dg = torch.empty(C, device=x.device)
+    db = torch.empty(C, device=x.device)
+    ws = _gn_workspace(N, P, C, G, x.device)
+    _check(lib().bev_groupnorm_bwd_f32(_ptr(x), _ptr(dy), N, P, C, G, _ptr(mean), _ptr(rstd),
+                                       _ptr(gamma.detach().contiguous()), _ptr(scale), _ptr(shift), int(relu), _ptr(dx),
+                                       _ptr(dg), _ptr(db), _ptr(ws), _stream(x)), "bev_groupnorm_bwd_f32")
+    return dx, dg, db

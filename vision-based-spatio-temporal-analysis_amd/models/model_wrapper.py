@@ -1,17 +1,24 @@
 """BEVNet -- drop-in for project/models/model_wrapper.py (what train.py / inference.py import).
 
-Wiring (model_wrapper.py:41-43, 53-69): CNNEncoder -> GeometryTransformer
-(warp_impl='kornia', which -- as in the reference without kornia -- runs the
-grid_sample semantics, quirk Q7) -> ConcatFusion -> lazy 1x1 BEV proj ->
-2-channel positional encoding -> lazy BEVDetector -> decode.  The encoder and
-the warp run on the HIP kernels; proj / head / decode / loss run on torch ops
-(they are downstream of the fused BEV hot path).
+Same cfg keys, attribute names (encoder, geom, fusion, proj, detector, pos_enc), lazily created modules
+(proj, detector) and output dict as the reference (model_wrapper.py:13-124), so state_dicts and the train /
+inference loops carry over.  Deliberate difference: lazily created modules are placed on the feature device
+(the reference creates the encoder proj on the CPU, quirk Q2).
 
-Same cfg keys, attribute names (encoder, geom, fusion, proj, detector,
-pos_enc) and output dict as the reference, so state_dicts and the train /
-inference loops carry over.  Deliberate difference: lazily created modules
-are placed on the feature device (the reference creates the encoder proj on
-the CPU, quirk Q2).
+The computation is reorganised for the GPU:
+
+* BEV projection.  The reference warps every camera's C-channel map to the BEV grid, concatenates the
+  V*C-channel result and applies the 1x1 `proj` (model_wrapper.py:74-81).  The bilinear IPM warp is linear
+  and acts per channel, and the zero fill of out-of-image cells commutes with a channel mix, so
+      proj(concat_v warp_v(f_v)) = sum_v warp_v(W_v f_v) + b,   W_v = proj.weight[:, v*C:(v+1)*C].
+  Here each camera's features are first mixed down to P = BEV_PROJ_CH channels in image space (MFMA 1x1
+  conv over Hf*Wf pixels instead of Hb*Wb cells) and the V projected maps are warped and summed by ONE fused
+  kernel (bev_ipm_warp_fuse_f32, mode "sum") -- the [B, V*C, Hb, Wb] tensor is never formed.  Same value up
+  to fp32 reassociation (the BEVNet parity test pins it against the reference's own outputs).
+* The head input is assembled channels-last ([B, Hb, Wb, ceil32(P+2)]: projection, pos-enc, zero pad) and
+  fed to BEVDetector.forward_nhwc; `bev_feat` is returned as an NCHW view of it.
+* Training targets are built for the whole batch at once (no per-object Python loop / host syncs): gaussian
+  splats are one scatter_reduce('amax') over every object's footprint.
 """
 import math
 from typing import Any, Dict, List, Tuple
@@ -20,10 +27,57 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import bev_native as _nat
+
 from .encoders.cnn_encoder import CNNEncoder
 from .fusion.fusion import ConcatFusion
-from .fusion.geometry import GeometryTransformer
-from .heads.detector import BEVDetector
+from .fusion.geometry import GeometryTransformer, _WarpFuseFn
+from .heads.detector import BEVDetector, _ceil_to
+
+
+class _ViewProjection(torch.autograd.Function):
+    """g[b, v] = W_v (1x1) f[b, v] for channels-last per-camera maps f [B,V,C,Hf,Wf]; returns the projected
+    maps as a [B,V,P,Hf,Wf] view of a [B,V,Hf,Wf,P] buffer (the layout the fused warp reads)."""
+
+    @staticmethod
+    def forward(ctx, feats, weight, panels):
+        B, V, C, Hf, Wf = feats.shape
+        P = weight.shape[0]
+        fl = feats.permute(0, 1, 3, 4, 2)
+        if not fl.is_contiguous():
+            fl = fl.contiguous()
+        g = torch.empty(B, V, Hf, Wf, P, device=feats.device, dtype=torch.float32)
+        zero = torch.zeros(P, device=feats.device)
+        for v in range(V):
+            for b in range(B):
+                _nat.conv2d_nhwc_ex(fl[b, v][None], panels[v], zero, P, 1, 0, out=g[b, v][None])
+        ctx.save_for_backward(fl, weight)
+        return g.permute(0, 1, 4, 2, 3)
+
+    @staticmethod
+    def backward(ctx, dg):
+        fl, weight = ctx.saved_tensors
+        B, V, Hf, Wf, C = fl.shape
+        P = weight.shape[0]
+        dgn = _nat.nchw_to_nhwc(dg.reshape(B * V, P, Hf, Wf)).view(B, V, Hf, Wf, P)
+        dfeat = dw = None
+        w = weight.detach().float().view(P, V, C)
+        if ctx.needs_input_grad[0]:
+            dfeat = torch.empty(B, V, Hf, Wf, C, device=dg.device, dtype=torch.float32)
+            zero = torch.zeros(C, device=dg.device)
+            for v in range(V):
+                wt = _nat.pack_conv_weight(w[:, v].t().contiguous().view(C, P, 1, 1))
+                for b in range(B):
+                    _nat.conv2d_nhwc_ex(dgn[b, v][None], wt, zero, C, 1, 0, out=dfeat[b, v][None])
+            dfeat = dfeat.permute(0, 1, 4, 2, 3)
+        if ctx.needs_input_grad[1]:
+            parts = []
+            for v in range(V):
+                acc = _nat.conv_wgrad_ex(fl[:, v], dgn[:, v], 1, 0, 1) if B == 1 else \
+                    sum(_nat.conv_wgrad_ex(fl[b, v][None], dgn[b, v][None], 1, 0, 1) for b in range(B))
+                parts.append(acc)
+            dw = torch.cat(parts, dim=1)
+        return dfeat, dw, None
 
 
 class BEVNet(nn.Module):
@@ -57,90 +111,152 @@ class BEVNet(nn.Module):
                                   backbone_impl=str(m.get("BACKBONE_IMPL", "auto")))
         self.geom = GeometryTransformer(bev_h=bev_h, bev_w=bev_w, bev_bounds=bev_bounds, warp_impl="kornia")
         self.fusion = ConcatFusion()
-        self.detector = None  # in_channels = V*C (+proj) + 2, known at the first forward
+        self.detector = None  # in_channels = (BEV_PROJ_CH or V*C) + 2, known at the first forward
         self.proj = None
         self.bev_h, self.bev_w = bev_h, bev_w
         self.bounds = bev_bounds
         self.register_buffer("pos_enc", self._create_pos_enc(bev_h, bev_w, bev_bounds), persistent=False)
+        self._proj_panels = (None, None)
 
     @staticmethod
     def _stack_calib(c):
         return torch.stack([torch.stack(v, dim=0) for v in c], dim=0) if isinstance(c, list) else c
 
+    def _view_panels(self, V: int, C: int):
+        """Packed per-camera slices W_v of proj.weight (cached until the parameter changes)."""
+        w = self.proj.weight
+        key = (w.data_ptr(), w._version, V, C)
+        if self._proj_panels[0] != key:
+            with torch.no_grad():
+                wv = w.detach().float().view(w.shape[0], V, C)
+                panels = [_nat.pack_conv_weight(wv[:, v].contiguous().view(-1, C, 1, 1)) for v in range(V)]
+            self._proj_panels = (key, panels)
+        return self._proj_panels[1]
+
+    def _bev_main(self, feats, H, img_hw):
+        """[B,V,C,Hf,Wf] features -> BEV map before pos-enc: proj(concat of per-view warps), NCHW (any strides)."""
+        B, V, C = feats.shape[:3]
+        xs, ys = self.geom._device_axes(feats.device)
+        if self.proj is None and self.bev_proj_ch > 0:
+            self.proj = nn.Conv2d(V * C, self.bev_proj_ch, kernel_size=1).to(feats.device)
+        if self.proj is None:  # no projection: the concatenated per-view warps (model_wrapper.py:80)
+            per_view = _WarpFn_views(feats, H, xs, ys, img_hw)
+            return self.fusion(per_view.view(B, V, C, self.bev_h, self.bev_w))
+        g = _ViewProjection.apply(feats, self.proj.weight, self._view_panels(V, C))
+        s = _WarpFuseFn.apply(g, H, xs, ys, img_hw, "sum")
+        return s + self.proj.bias.view(1, -1, 1, 1)
+
     def forward(self, batch: Dict) -> Dict:
         images = batch["images"]  # [B, V, 3, H, W]
-        B, V, _, H, W = images.shape
+        B, V, _, Hi, Wi = images.shape
         feats = self.encoder(images)
         K = self._stack_calib(batch["calib"]["intrinsic"])
         Rt = self._stack_calib(batch["calib"]["extrinsic"])
-        bev_per_view = self.geom(feats, K, Rt, img_size=(H, W))  # quirk Q1: network-input size
-        bev_concat = self.fusion(bev_per_view)
-        if self.proj is None and self.bev_proj_ch > 0:
-            self.proj = nn.Conv2d(bev_concat.shape[1], self.bev_proj_ch, kernel_size=1).to(bev_concat.device)
-        bev_main = self.proj(bev_concat) if self.proj is not None else bev_concat
-        bev_feat = torch.cat([bev_main, self.pos_enc.unsqueeze(0).expand(B, -1, -1, -1)], dim=1)
+        H = self.geom.homographies(K, Rt, B, V, feats.device)
+        main = self._bev_main(feats, H, (Hi, Wi))  # quirk Q1: network-input size
+        P = main.shape[1]
         if self.detector is None:
-            self.detector = BEVDetector(in_channels=bev_feat.shape[1], bev_bounds=self.bounds,
-                                        bev_size=(self.bev_h, self.bev_w),
-                                        default_box_wh=self.default_box_wh).to(bev_feat.device)
-        det = self.detector(bev_feat)
+            self.detector = BEVDetector(in_channels=P + 2, bev_bounds=self.bounds, bev_size=(self.bev_h, self.bev_w),
+                                        default_box_wh=self.default_box_wh).to(main.device)
+        cp = self.detector.input_channels_padded
+        pos = self.pos_enc.permute(1, 2, 0).unsqueeze(0).expand(B, -1, -1, -1)
+        parts = [main.permute(0, 2, 3, 1), pos]
+        if cp > P + 2:
+            parts.append(main.new_zeros(B, self.bev_h, self.bev_w, cp - P - 2))
+        x = torch.cat(parts, dim=-1)  # [B, Hb, Wb, cp] channels-last head operand
+        det = self.detector.forward_nhwc(x)
         boxes, scores = self.detector.decode(det["heatmap"], det["offset"], det["size"],
                                              conf_thresh=self.conf_thresh, nms_dist_m=self.nms_dist_m)
         return {"heatmap": det["heatmap"], "heatmap_logits": det["heatmap_logits"], "boxes": boxes, "scores": scores,
                 "offset": det["offset"], "offset_raw": det["offset_raw"], "size": det["size"],
-                "size_raw": det["size_raw"], "bev_feat": bev_feat}
+                "size_raw": det["size_raw"], "bev_feat": x[..., :P + 2].permute(0, 3, 1, 2)}
 
     # ---- training objective (model_wrapper.py:105-247) --------------------------
     def loss(self, preds: Dict, targets: List[Dict], loss_cfg: Dict[str, Any]) -> Dict[str, torch.Tensor]:
         t = self._build_training_targets(targets)
         hm_loss = self._heatmap_focal_loss(preds["heatmap_logits"], t["heatmap"])
-        mask = t["mask"].unsqueeze(-1)
-        denom = mask.sum() + 1e-4
-        off = self._gather_feat(preds["offset"], t["indices"])
-        off_loss = F.l1_loss(off * mask, t["offset"] * mask, reduction="sum") / denom
-        siz = self._gather_feat(preds["size_raw"], t["indices"])
-        size_loss = F.l1_loss(siz * mask, t["size_log"] * mask, reduction="sum") / denom
+        m = t["mask"].unsqueeze(-1)
+        n = m.sum() + 1e-4
+        off_loss = (self._gather_feat(preds["offset"], t["indices"]) - t["offset"]).mul(m).abs().sum() / n
+        size_loss = (self._gather_feat(preds["size_raw"], t["indices"]) - t["size_log"]).mul(m).abs().sum() / n
         total = self.hm_weight * hm_loss + self.offset_weight * off_loss + self.size_weight * size_loss
         return {"heatmap_loss": hm_loss, "offset_loss": off_loss, "size_loss": size_loss, "total_loss": total}
 
-    def _build_training_targets(self, targets: List[Dict]) -> Dict[str, torch.Tensor]:
-        dev = next(self.parameters()).device
-        B = len(targets)
-        hm = torch.zeros(B, 1, self.bev_h, self.bev_w, device=dev)
-        indices = torch.zeros(B, self.max_objects, dtype=torch.long, device=dev)
-        mask = torch.zeros(B, self.max_objects, dtype=torch.float32, device=dev)
-        offset = torch.zeros(B, self.max_objects, 2, device=dev)
-        size_log = torch.zeros(B, self.max_objects, 2, device=dev)
-        x_min, _, y_min, _ = self.bounds
-        wh = torch.tensor(self.default_box_wh, device=dev, dtype=torch.float32)
+    def _target_boxes(self, targets: List[Dict], dev) -> Tuple[torch.Tensor, torch.Tensor]:
+        """All frames' boxes [N, 4] (cx, cy, w, h; centre-only targets get DEFAULT_BOX_WH) + frame index [N]."""
+        boxes, frame = [], []
         for b, tgt in enumerate(targets):
-            boxes = tgt.get("boxes_world", None)
-            if boxes is None or boxes.numel() == 0:
+            bx = tgt.get("boxes_world", None)
+            if bx is None or bx.numel() == 0:
                 c = tgt.get("centers_world", None)
+                bx = None
                 if c is not None and c.numel() > 0:
-                    boxes = torch.cat([c, wh.to(c.device).repeat(c.shape[0], 1)], dim=1)
-            if boxes is None or boxes.numel() == 0:
+                    c = c.to(dev, torch.float32).reshape(-1, 2)
+                    bx = torch.cat([c, c.new_tensor(self.default_box_wh).expand(c.shape[0], 2)], dim=1)
+            if bx is None:
                 continue
-            boxes = boxes.to(dev)
-            rel = torch.stack([(boxes[:, 0] - x_min) / self.res_x, (boxes[:, 1] - y_min) / self.res_y], dim=1)
-            ok = (rel[:, 0] >= 0) & (rel[:, 0] < self.bev_w) & (rel[:, 1] >= 0) & (rel[:, 1] < self.bev_h)
-            if not torch.any(ok):
-                continue
-            keep = torch.nonzero(ok, as_tuple=False).squeeze(1)[: self.max_objects]
-            rel, sizes = rel[keep], boxes[keep, 2:]
-            gfl = torch.floor(rel)
-            w_cells = (sizes[:, 0] / self.res_x).clamp(min=1e-3)
-            h_cells = (sizes[:, 1] / self.res_y).clamp(min=1e-3)
-            radii = self._gaussian_radius_tensor(w_cells, h_cells)
-            gi = gfl.to(torch.long)
-            n = rel.shape[0]
-            indices[b, :n] = gi[:, 1] * self.bev_w + gi[:, 0]
-            mask[b, :n] = 1.0
-            offset[b, :n] = rel - gfl
-            size_log[b, :n] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
-            for k in range(n):
-                hm[b, 0] = self._draw_gaussian(hm[b, 0], (int(gi[k, 0]), int(gi[k, 1])), int(radii[k]))
+            bx = bx.to(dev, torch.float32).reshape(-1, bx.shape[-1])
+            boxes.append(bx[:, :4])
+            frame.append(torch.full((bx.shape[0],), b, device=dev, dtype=torch.long))
+        if not boxes:
+            return torch.zeros(0, 4, device=dev), torch.zeros(0, dtype=torch.long, device=dev)
+        return torch.cat(boxes), torch.cat(frame)
+
+    def _build_training_targets(self, targets: List[Dict]) -> Dict[str, torch.Tensor]:
+        """CenterNet targets (model_wrapper.py:127-203) for the whole batch at once: the first MAX_OBJECTS
+        in-grid objects of each frame fill its slots in order; heatmap = per-cell max of their gaussians."""
+        dev = next(self.parameters()).device
+        B, M, Hb, Wb = len(targets), self.max_objects, self.bev_h, self.bev_w
+        hm = torch.zeros(B, 1, Hb, Wb, device=dev)
+        indices = torch.zeros(B, M, dtype=torch.long, device=dev)
+        mask = torch.zeros(B, M, device=dev)
+        offset = torch.zeros(B, M, 2, device=dev)
+        size_log = torch.zeros(B, M, 2, device=dev)
+        boxes, frame = self._target_boxes(targets, dev)
+        if boxes.shape[0] == 0:
+            return {"heatmap": hm, "indices": indices, "mask": mask, "offset": offset, "size_log": size_log}
+        x_min, _, y_min, _ = self.bounds
+        gx = (boxes[:, 0] - x_min) / self.res_x
+        gy = (boxes[:, 1] - y_min) / self.res_y
+        inside = (gx >= 0) & (gx < Wb) & (gy >= 0) & (gy < Hb)
+        # slot = rank among the frame's in-grid objects (boxes are grouped by frame, in order)
+        run = torch.cumsum(inside.long(), 0)
+        first = torch.searchsorted(frame, torch.arange(B, device=dev))
+        before = torch.where(first > 0, run[(first - 1).clamp(min=0)], torch.zeros_like(first))
+        slot = run - 1 - before[frame]
+        sel = inside & (slot < M)
+        b, s = frame[sel], slot[sel]
+        gx, gy, wh = gx[sel], gy[sel], boxes[sel, 2:4]
+        cx, cy = torch.floor(gx), torch.floor(gy)
+        w_cells = (wh[:, 0] / self.res_x).clamp(min=1e-3)
+        h_cells = (wh[:, 1] / self.res_y).clamp(min=1e-3)
+        indices[b, s] = cy.long() * Wb + cx.long()
+        mask[b, s] = 1.0
+        offset[b, s] = torch.stack([gx - cx, gy - cy], dim=1)
+        size_log[b, s] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
+        self._splat_gaussians(hm, b, cx.long(), cy.long(), self._gaussian_radius_tensor(w_cells, h_cells))
         return {"heatmap": hm, "indices": indices, "mask": mask, "offset": offset, "size_log": size_log}
+
+    @staticmethod
+    def _splat_gaussians(hm: torch.Tensor, b, cx, cy, radius):
+        """hm[b, 0] = max(hm, exp(-(dx^2+dy^2) / (2 sigma^2))) over each object's clipped (2r+1)^2 window,
+        sigma = (2r+1)/6 (the splat of model_wrapper.py:250-276); radius <= 0 draws nothing."""
+        keep = radius > 0
+        if not bool(keep.any()):
+            return
+        b, cx, cy, radius = b[keep], cx[keep], cy[keep], radius[keep]
+        _, _, Hb, Wb = hm.shape
+        R = int(radius.max())
+        d = torch.arange(-R, R + 1, device=hm.device)
+        dy, dx = d.view(-1, 1).expand(-1, d.numel()).reshape(-1), d.repeat(d.numel())
+        x = cx[:, None] + dx[None]
+        y = cy[:, None] + dy[None]
+        r = radius[:, None]
+        ok = (dx.abs()[None] <= r) & (dy.abs()[None] <= r) & (x >= 0) & (x < Wb) & (y >= 0) & (y < Hb)
+        two_s2 = ((2.0 * radius.double() + 1.0) / 6.0) ** 2 * 2.0  # the reference's python-float denominator
+        val = torch.exp(-(dx * dx + dy * dy).float()[None] / two_s2.float()[:, None])
+        flat = (b[:, None] * Hb + y) * Wb + x
+        hm.view(-1).scatter_reduce_(0, flat[ok], val[ok], reduce="amax", include_self=True)
 
     def _gaussian_radius_tensor(self, width_cells: torch.Tensor, height_cells: torch.Tensor) -> torch.Tensor:
         """CenterNet radius, same tensor arithmetic (and rounding) as model_wrapper.py:205-233."""
@@ -163,12 +279,13 @@ class BEVNet(nn.Module):
         return torch.floor(r).to(torch.long)
 
     def _heatmap_focal_loss(self, pred_logits: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
-        p = torch.clamp(torch.sigmoid(pred_logits), min=1e-4, max=1 - 1e-4)
-        pos = gt.eq(1.0)
-        neg = gt.lt(1.0)
-        pos_loss = torch.log(p) * torch.pow(1 - p, self.hm_alpha) * pos
-        neg_loss = torch.log(1 - p) * torch.pow(p, self.hm_alpha) * torch.pow(1 - gt, self.hm_beta) * neg
-        return -(pos_loss.sum() + neg_loss.sum()) / pos.float().sum().clamp(min=1.0)
+        """Penalty-reduced focal loss (model_wrapper.py:235-247), normalised by the number of gt peaks."""
+        p = torch.sigmoid(pred_logits).clamp(1e-4, 1 - 1e-4)
+        peak = gt == 1.0
+        pos = torch.where(peak, p.log() * (1 - p).pow(self.hm_alpha), torch.zeros_like(p))
+        neg = torch.where(gt < 1.0, (1 - p).log() * p.pow(self.hm_alpha) * (1 - gt).pow(self.hm_beta),
+                          torch.zeros_like(p))
+        return -(pos.sum() + neg.sum()) / peak.sum().float().clamp(min=1.0)
 
     def _gaussian_radius(self, width_cells: float, height_cells: float) -> int:
         """Scalar variant (unused by loss()); keeps the reference's '/2' for r2 (quirk Q10)."""
@@ -184,29 +301,45 @@ class BEVNet(nn.Module):
         return max(self.gaussian_min_radius, int(min(r1, r2, r3)))
 
     def _draw_gaussian(self, heatmap: torch.Tensor, center: Tuple[int, int], radius: int) -> torch.Tensor:
-        radius = int(radius)
-        if radius <= 0:
-            return heatmap
-        sigma = (2 * radius + 1) / 6.0
-        x, y = center
+        """Single-object splat into a [H, W] map, in place (model_wrapper.py:250-276 API)."""
+        x, y = int(center[0]), int(center[1])
         H, W = heatmap.shape
-        if x < 0 or y < 0 or x >= W or y >= H:
-            return heatmap
-        left, right = min(x, radius), min(W - x - 1, radius)
-        top, bottom = min(y, radius), min(H - y - 1, radius)
-        yr = torch.arange(-top, bottom + 1, device=heatmap.device, dtype=heatmap.dtype)
-        xr = torch.arange(-left, right + 1, device=heatmap.device, dtype=heatmap.dtype)
-        yy, xx = torch.meshgrid(yr, xr, indexing="ij")
-        g = torch.exp(-(xx ** 2 + yy ** 2) / (2 * sigma * sigma))
-        patch = heatmap[y - top:y + bottom + 1, x - left:x + right + 1]
-        torch.maximum(patch, g, out=patch)
+        if int(radius) > 0 and 0 <= x < W and 0 <= y < H:
+            dev = heatmap.device
+            self._splat_gaussians(heatmap.view(1, 1, H, W), torch.zeros(1, dtype=torch.long, device=dev),
+                                  torch.tensor([x], device=dev), torch.tensor([y], device=dev),
+                                  torch.tensor([int(radius)], device=dev))
         return heatmap
 
     @staticmethod
     def _gather_feat(feat: torch.Tensor, indices: torch.Tensor) -> torch.Tensor:
-        B, C, H, W = feat.shape
-        flat = feat.view(B, C, -1).permute(0, 2, 1)
-        return torch.gather(flat, 1, indices.unsqueeze(-1).expand(-1, -1, C))
+        """feat [B, C, H, W], indices [B, K] flat cell ids -> [B, K, C]."""
+        B, C = feat.shape[:2]
+        return feat.reshape(B, C, -1).gather(2, indices[:, None, :].expand(B, C, -1)).transpose(1, 2)
+
+    def _geom_consistency_loss(self, targets: List[Dict], num_samples: int = 128) -> torch.Tensor:
+        """image -> world round trip of random BEV cell centres for the first target's cameras
+        (model_wrapper.py:317-340, unused by loss(), kept for callers)."""
+        dev = next(self.parameters()).device
+        zero = torch.zeros((), device=dev)
+        calib = targets[0].get("calib", None) if targets else None
+        if calib is None:
+            return zero
+        Ks, Rts = calib.get("intrinsic", []), calib.get("extrinsic", [])
+        x_min, x_max, y_min, y_max = self.bounds
+        yy, xx = torch.meshgrid(torch.linspace(y_min, y_max, self.bev_h, device=dev),
+                                torch.linspace(x_min, x_max, self.bev_w, device=dev), indexing="ij")
+        pts = torch.stack([xx.reshape(-1), yy.reshape(-1), torch.ones_like(xx).reshape(-1)], dim=1)
+        pts = pts[torch.randperm(pts.shape[0], device=dev)[:num_samples]]
+        loss = zero
+        for K, Rt in zip(Ks, Rts):
+            fwd = GeometryTransformer._compute_homography(K.to(dev), Rt.to(dev))
+            uvw = fwd @ pts.T
+            w = torch.where(uvw[2:3].abs() < 1e-6, torch.ones_like(uvw[2:3]), uvw[2:3])
+            img = torch.cat([uvw[:2] / w, torch.ones_like(w)], dim=0)
+            back = GeometryTransformer._compute_img_to_world_homography(K.to(dev), Rt.to(dev)) @ img
+            loss = loss + F.l1_loss(back[:2].T, pts[:, :2])
+        return loss / max(1, len(Ks))
 
     @staticmethod
     def _create_pos_enc(H: int, W: int, bounds: Tuple[float, float, float, float]) -> torch.Tensor:
@@ -215,3 +348,11 @@ class BEVNet(nn.Module):
         yy, xx = torch.meshgrid(torch.linspace(y_min, y_max, H), torch.linspace(x_min, x_max, W), indexing="ij")
         return torch.stack([torch.sin(2.0 * torch.pi * ((xx - x_min) / (x_max - x_min))),
                             torch.cos(2.0 * torch.pi * ((yy - y_min) / (y_max - y_min)))], dim=0)
+
+
+def _WarpFn_views(feats, H, xs, ys, img_hw):
+    """Per-view warps [B*V, C, Hb, Wb] with autograd (GeometryTransformer.forward without the calib step)."""
+    from .fusion.geometry import _WarpFn
+    B, V, C, Hf, Wf = feats.shape
+    f4 = feats.reshape(B * V, C, Hf, Wf) if feats.is_contiguous() else feats.flatten(0, 1)
+    return _WarpFn.apply(f4, H, xs, ys, tuple(img_hw))
