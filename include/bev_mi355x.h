@@ -275,6 +275,32 @@ int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int
                           float *dx, float *dgamma, float *dbeta, void *workspace, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * BatchNorm with batch statistics (training the trunk in model.train(), reference train.py:222;
+ * torch.nn.BatchNorm2d train-mode semantics) on NHWC activations viewed as rows z [M][C], M = N*H*W.
+ * Replaces the train-mode BN of timm's trunk (cnn_encoder.py:26 -> timm ResNet bn1/bn2/bn3).
+ * ------------------------------------------------------------------------- */
+
+/* host: workspace bytes for bev_batchnorm_train_fwd_f32 / _bwd_f32 (-1: C % 4 != 0 or M <= 0). */
+int64_t bev_batchnorm_workspace_bytes(int64_t M, int C);
+
+/* device: per-channel batch mean, rstd = 1/sqrt(biased var + eps), scale = gamma * rstd, shift = beta - mean *
+ * scale [C]; running_mean / running_var (both or neither) <- (1 - momentum) * running + momentum * batch value
+ * (unbiased variance M/(M-1)). */
+int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, float momentum, const float *gamma,
+                                const float *beta, float *running_mean, float *running_var, float *mean, float *rstd,
+                                float *scale, float *shift, void *workspace, void *stream);
+
+/* device: y = z * scale + shift (+ residual [M][C]) (+ ReLU), per channel. */
+int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                            const float *residual, int relu, float *y, void *stream);
+
+/* device: backward of y = act(batchnorm(z) (+ residual)) given dy and the forward output y (NULL: no ReLU):
+ * dz [M][C], dres [M][C] (the gradient reaching the residual; may be NULL), dgamma, dbeta [C], all OVERWRITTEN. */
+int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
+                          const float *rstd, const float *gamma, float *dz, float *dres, float *dgamma, float *dbeta,
+                          void *workspace, void *stream);
+
+/* ---------------------------------------------------------------------------
  * BEVDetector.decode (detector.py:64-125) on the device: no per-pair host sync.
  * ------------------------------------------------------------------------- */
 

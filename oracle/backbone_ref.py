@@ -4,8 +4,9 @@ Restates, with plain torch CPU ops, what timm's `features_only` ResNet
 computes up to feature index `out_index` (cnn_encoder.py:26,41-42) followed
 by the encoder's 1x1 projection (cnn_encoder.py:43-46), reading the weights
 of our timm-named module (models/encoders/resnet.py) so both sides use the
-same parameters.  BatchNorm runs unfused (F.batch_norm, eval statistics) --
-the HIP path folds it, so the comparison is tolerance-based (fp32 order of
+same parameters.  BatchNorm runs unfused (F.batch_norm; eval statistics, or batch statistics
+with the running-stat update when the BN module is in training mode) -- the HIP path folds eval
+BN into the conv, so the comparison is tolerance-based (fp32 order of
 accumulation differs; rtol 1e-4 per SURVEY.md §8d).  Parity with timm itself
 is unpinned (timm is absent offline).
 
@@ -17,19 +18,21 @@ import torch
 import torch.nn.functional as F
 
 
-def _cbr(x, conv, bn, relu=True):
+def _cbr(x, conv, bn, relu=True, act=F.relu):
     y = F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding)
     if bn is not None:
-        y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
-    return F.relu(y) if relu else y
+        y = F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.training,
+                         bn.momentum if bn.momentum is not None else 0.0, bn.eps)
+    return act(y) if relu else y
 
 
-def resnet_features(net, x, out_index: int, grad: bool = False):
+def resnet_features(net, x, out_index: int, grad: bool = False, act=F.relu):
     """features_only[out_index] of a timm-named ResNet `net` on NCHW x (any device; CPU in practice).
-    BN always uses the running statistics (the native trunk's frozen-BN training semantics); with
-    grad=True autograd records the graph (reference for the native trunk backward)."""
+    BN follows each module's mode (eval: running statistics; training: batch statistics + running-stat
+    update); with grad=True autograd records the graph (reference for the native trunk backward).
+    `act` replaces every ReLU (in execution order), e.g. by the native run's masks for gradient checks."""
     with torch.set_grad_enabled(grad):
-        y = _cbr(x, net.conv1, net.bn1)
+        y = _cbr(x, net.conv1, net.bn1, act=act)
         if out_index == 0:
             return y
         y = F.max_pool2d(y, 3, 2, 1)
@@ -42,8 +45,8 @@ def resnet_features(net, x, out_index: int, grad: bool = False):
                 z = x_in
                 for idx, (conv, bn, _) in enumerate(chain):
                     last = idx == len(chain) - 1
-                    z = _cbr(z, conv, bn, relu=not last)
-                y = F.relu(z + sc)
+                    z = _cbr(z, conv, bn, relu=not last, act=act)
+                y = act(z + sc)
             if li == out_index:
                 return y
         return y

@@ -176,10 +176,14 @@ def test_bevnet_ddp_training_frozen_trunk():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(240)
+@pytest.mark.parametrize("bn_mode", ["batch", "frozen"])
 @pytest.mark.parametrize("name", ["resnet18", "resnet50"])
-def test_trunk_backward_vs_torch_autograd(name):
-    """Native trunk training path (frozen BN) vs torch CPU autograd on the same weights: the loss gradient
-    w.r.t. every trunk parameter and the encoder proj (floating point, atomics in wgrad: rel 1e-3)."""
+def test_trunk_backward_vs_torch_autograd(name, bn_mode):
+    """Native trunk training path vs torch CPU autograd on the same weights: the loss gradient w.r.t. every
+    trunk parameter and the encoder proj (floating point, atomics in wgrad: rel 1e-3).
+    bn_mode "batch": model.train() as the reference's train.py:222 -- BatchNorm with batch statistics, and the
+    running statistics updated by the momentum rule (checked too); "frozen": BN modules in eval() inside the
+    training model -- running statistics folded into the conv."""
     import backbone_ref
     from models.encoders.cnn_encoder import CNNEncoder
     torch.manual_seed(0)
@@ -195,16 +199,49 @@ def test_trunk_backward_vs_torch_autograd(name):
     with torch.no_grad():
         enc.eval().to(DEV)(imgs.to(DEV))  # builds the lazy proj
     enc.train()
-    y = enc(imgs.to(DEV))
+    if bn_mode == "frozen":
+        for m in enc.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+    stats0 = {k: b.detach().cpu().clone() for k, b in enc.named_buffers() if "running" in k}
+    # record the native ReLU decisions (batch mode: every ReLU is in bev_batchnorm_apply_f32) so the float64
+    # reference takes the same ones -- an element within fp32 rounding of 0 may switch sides and then carries
+    # its full upstream gradient, and through the batch statistics that reaches a whole channel
+    import bev_native as nat
+    masks, apply0 = [], nat.batchnorm_apply
+
+    def recording_apply(z, scale, shift, residual=None, relu=False):
+        out = apply0(z, scale, shift, residual, relu)
+        if relu:
+            masks.append((out > 0).permute(0, 3, 1, 2).double().cpu())
+        return out
+
+    nat.batchnorm_apply = recording_apply
+    try:
+        y = enc(imgs.to(DEV))
+    finally:
+        nat.batchnorm_apply = apply0
     r = torch.randn(y.shape, generator=g)
     (y * r.to(DEV)).sum().backward()
     got = {k: p.grad.detach().cpu() for k, p in enc.named_parameters() if p.grad is not None}
-    enc_c = enc.to("cpu")
+    stats1 = {k: b.detach().cpu().clone() for k, b in enc.named_buffers() if "running" in k}
+    enc_c = enc.to("cpu").double()  # float64 reference: the error measured is the native path's
     enc_c.zero_grad(set_to_none=True)
-    f = backbone_ref.resnet_features(enc_c.backbone, imgs.reshape(-1, 3, 70, 98), enc_c.out_index, grad=True)
+    with torch.no_grad():
+        for k, b in enc_c.named_buffers():
+            if k in stats0:
+                b.copy_(stats0[k])
+    r = r.double()
+    act = F.relu
+    if bn_mode == "batch":
+        act = lambda t: t * masks.pop(0)  # noqa: E731
+    f = backbone_ref.resnet_features(enc_c.backbone, imgs.double().reshape(-1, 3, 70, 98), enc_c.out_index, grad=True,
+                                     act=act)
     yc = F.conv2d(f, enc_c.proj.weight, enc_c.proj.bias)
+    close_y = (y.detach().cpu() - yc.detach().reshape(y.shape)).abs().max() / yc.abs().max()
+    assert float(close_y) < 1e-4, float(close_y)
     (yc.reshape(y.shape) * r).sum().backward()
-    worst, n = 0.0, 0
+    worst, n, errs = 0.0, 0, {}
     for k, p in enc_c.named_parameters():
         ref = p.grad
         if ref is None:  # stages past out_index are not executed (features_only, cnn_encoder.py:41-42)
@@ -212,10 +249,18 @@ def test_trunk_backward_vs_torch_autograd(name):
             continue
         assert k in got, k
         n += 1
-        err = (got[k] - ref).abs().max().item() / max(ref.abs().max().item(), 1e-12)
+        err = (got[k].double() - ref).abs().max().item() / max(ref.abs().max().item(), 1e-12)
         worst = max(worst, err)
-        assert err < 1e-3, (k, err)
-    assert n > 20 and worst > 0.0
+        errs[k] = err
+    assert n > 20 and worst > 0.0 and not masks
+    assert worst < 1e-3, sorted(errs.items(), key=lambda t: -t[1])[:6]
+    moved = 0
+    for k, b in enc_c.named_buffers():  # the reference's own running-stat update, from the same start
+        if k in stats1:
+            err = (stats1[k].double() - b).abs().max().item() / max(b.abs().max().item(), 1e-12)
+            assert err < 1e-4, (k, err)
+            moved += int(not torch.equal(stats1[k], stats0[k]))
+    assert (moved > 0) == (bn_mode == "batch")
 
 
 @pytest.mark.gpu
@@ -312,3 +357,61 @@ def test_maxpool_bwd_vs_torch_ties(N, C, H, W):
                                dy.permute(0, 2, 3, 1).contiguous().to("cuda:0"), 3, 2, 1)
     ref = x.grad.permute(0, 2, 3, 1).contiguous()
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+
+
+BN_CASES = [(2, 64, 13, 17, True, True), (1, 384, 9, 11, True, False), (3, 24, 7, 5, False, False),
+            (2, 512, 40, 60, True, True), (1, 4, 1, 3, False, True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", BN_CASES, ids=[f"n{c[0]}c{c[1]}_{c[2]}x{c[3]}_r{int(c[4])}s{int(c[5])}" for c in BN_CASES])
+def test_batchnorm_train_kernels_vs_torch(case):
+    """bev_batchnorm_train_fwd / apply / bwd vs torch's train-mode F.batch_norm (+ residual) (+ ReLU) autograd
+    in float64: output, dz, d residual, dgamma, dbeta and the running-stat update."""
+    import bev_native as nat
+    N, C, H, W, relu, res = case
+    g = torch.Generator().manual_seed(C + H)
+    z = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    gamma = torch.rand(C, generator=g) + 0.5
+    beta = torch.randn(C, generator=g) * 0.3
+    r = torch.randn(N, C, H, W, generator=g) if res else None
+    dy = torch.randn(N, C, H, W, generator=g)
+    rm0, rv0 = torch.rand(C, generator=g), torch.rand(C, generator=g) + 0.5
+    zd = z.double().requires_grad_(True)
+    gd, bd = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    rd = r.double().requires_grad_(True) if res else None
+    rm, rv = rm0.double().clone(), rv0.double().clone()
+    ref = F.batch_norm(zd, rm, rv, gd, bd, True, 0.1, 1e-5)
+    if res:
+        ref = ref + rd
+    if relu:
+        ref = torch.relu(ref)
+    ref.backward(dy.double())
+
+    def nhwc(t):
+        return t.permute(0, 2, 3, 1).contiguous().to(DEV)
+
+    zg = nhwc(z)
+    grm, grv = rm0.to(DEV), rv0.to(DEV)
+    mean, rstd, scale, shift = nat.batchnorm_train_fwd(zg, gamma.to(DEV), beta.to(DEV), grm, grv, 1e-5, 0.1)
+    y = nat.batchnorm_apply(zg, scale, shift, nhwc(r) if res else None, relu)
+    dz, dres, dgm, dbt = nat.batchnorm_bwd(nhwc(dy), y if relu else None, zg, mean, rstd, gamma.to(DEV), res)
+
+    def chk(got, want, tol, what):
+        got = got.detach().double().cpu()
+        if got.dim() == 4:
+            got = got.permute(0, 3, 1, 2)
+        want = want.detach()
+        err = (got - want).abs().max().item() / max(want.abs().max().item(), 1e-12)
+        assert err < tol, (what, err)
+
+    chk(y, ref, 1e-5, "y")
+    if relu:  # gradient checks need the same ReLU decisions: drop elements within rounding of 0
+        assert int(((y.permute(0, 3, 1, 2).cpu() > 0) != (ref.detach() > 0)).sum()) == 0
+    chk(dz, zd.grad, 1e-4, "dz")
+    chk(dgm, gd.grad, 1e-4, "dgamma")
+    chk(dbt, bd.grad, 1e-5, "dbeta")
+    if res:
+        chk(dres, rd.grad, 1e-6, "dres")
+    chk(grm, rm, 1e-5, "running_mean")
+    chk(grv, rv, 1e-5, "running_var")

@@ -67,6 +67,10 @@ SIGNATURES = {
                                     _i, _i, _vp]),
     "bev_conv_wgrad_ex_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_groupnorm_workspace_bytes": (_i64, [_i, _i64, _i, _i]),
+    "bev_batchnorm_workspace_bytes": (_i64, [_i64, _i]),
+    "bev_batchnorm_train_fwd_f32": (_i, [_vp, _i64, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bev_batchnorm_apply_f32": (_i, [_vp, _i64, _i, _vp, _vp, _vp, _i, _vp, _vp]),
+    "bev_batchnorm_bwd_f32": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_groupnorm_fwd_f32": (_i, [_vp, _i, _i64, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_groupnorm_apply_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _i, _vp, _vp]),
     "bev_groupnorm_bwd_f32": (_i, [_vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
@@ -606,3 +610,61 @@ def groupnorm_bwd(x, dy, G, mean, rstd, gamma, scale, shift, relu: bool):
                                        _ptr(gamma.detach().contiguous()), _ptr(scale), _ptr(shift), int(relu), _ptr(dx),
                                        _ptr(dg), _ptr(db), _ptr(ws), _stream(x)), "bev_groupnorm_bwd_f32")
     return dx, dg, db
+
+
+# ---------------------------------------------------------------------------
+# BatchNorm with batch statistics (trunk training, train.py:222)
+# ---------------------------------------------------------------------------
+def _bn_workspace(M, C, device):
+    nbytes = lib().bev_batchnorm_workspace_bytes(M, C)
+    if nbytes < 0:
+        raise HipError(f"BatchNorm shape not supported: M={M}, C={C}")
+    return torch.empty((nbytes + 7) // 8, device=device, dtype=torch.float64)
+
+
+def batchnorm_train_fwd(z: torch.Tensor, gamma, beta, running_mean, running_var, eps: float, momentum: float):
+    """z [..., C] NHWC contiguous -> (mean, rstd, scale, shift) [C]; running stats updated in place (if given)."""
+    _require_gpu(z, gamma, beta, running_mean, running_var)
+    assert z.is_contiguous()
+    C = z.shape[-1]
+    M = z.numel() // C
+    dev = z.device
+    mean, rstd, scale, shift = (torch.empty(C, device=dev) for _ in range(4))
+    ws = _bn_workspace(M, C, dev)
+    with _span("batchnorm", z):
+        rc = lib().bev_batchnorm_train_fwd_f32(_ptr(z), M, C, float(eps), float(momentum),
+                                               _ptr(gamma.detach().contiguous()), _ptr(beta.detach().contiguous()),
+                                               _ptr(running_mean), _ptr(running_var), _ptr(mean), _ptr(rstd), _ptr(scale),
+                                               _ptr(shift), _ptr(ws), _stream(z))
+    _check(rc, "bev_batchnorm_train_fwd_f32")
+    return mean, rstd, scale, shift
+
+
+def batchnorm_apply(z: torch.Tensor, scale, shift, residual=None, relu: bool = False) -> torch.Tensor:
+    _require_gpu(z, scale, shift, residual)
+    assert z.is_contiguous()
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == z.shape
+    C = z.shape[-1]
+    y = torch.empty_like(z)
+    _check(lib().bev_batchnorm_apply_f32(_ptr(z), z.numel() // C, C, _ptr(scale), _ptr(shift), _ptr(residual),
+                                         int(relu), _ptr(y), _stream(z)), "bev_batchnorm_apply_f32")
+    return y
+
+
+def batchnorm_bwd(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_dres: bool):
+    """-> (dz, dres or None, dgamma, dbeta) of y = relu?(batchnorm(z) (+ res)); y None means no ReLU."""
+    dy = dy.contiguous()
+    _require_gpu(dy, y, z, mean, rstd, gamma)
+    C = z.shape[-1]
+    M = z.numel() // C
+    dz = torch.empty_like(z)
+    dres = torch.empty_like(z) if want_dres else None
+    dg = torch.empty(C, device=z.device)
+    db = torch.empty(C, device=z.device)
+    ws = _bn_workspace(M, C, z.device)
+    _check(lib().bev_batchnorm_bwd_f32(_ptr(dy), _ptr(y), _ptr(z), M, C, _ptr(mean), _ptr(rstd),
+                                       _ptr(gamma.detach().contiguous()), _ptr(dz), _ptr(dres), _ptr(dg), _ptr(db),
+                                       _ptr(ws), _stream(z)), "bev_batchnorm_bwd_f32")
+    return dz, dres, dg, db

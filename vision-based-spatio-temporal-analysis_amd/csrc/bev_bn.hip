@@ -1,0 +1,247 @@
+// bev_bn.hip -- BatchNorm with batch statistics for training the backbone trunk (timm's BN in
+// model.train(), reference train.py:222), on NHWC activations viewed as rows [M][C] (M = N*H*W), fp32:
+//
+//   forward   k_bn_partial<Stats>  per block of rows: per-channel (sum z, sum z^2) in double
+//             k_bn_finalize        mean, biased var, rstd = 1/sqrt(var + eps), scale = gamma*rstd,
+//                                  shift = beta - mean*scale; running_mean / running_var updated with
+//                                  the momentum rule and the unbiased variance (torch's train-mode BN)
+//             k_bn_apply           y = act(z*scale + shift (+ residual))   (float4)
+//   backward  k_bn_partial<Grads>  per channel (sum g, sum g*xhat), g = dy * (y > 0 if relu), xhat =
+//                                  (z - mean) * rstd
+//             k_bn_bwd_finalize    k1 = sum g / M, k2 = sum g xhat / M, dbeta, dgamma
+//             k_bn_bwd_apply       dz = gamma * rstd * (g - k1 - xhat * k2); d(residual) = g
+//
+// The partials are one per (row block, channel): deterministic, no float atomics.  Every pass is a
+// streaming read of the activation (HBM-bound; a few us per trunk layer at BEV-rig sizes).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+constexpr int BN_T = 256;
+constexpr int BN_ROWS = 1024;  // rows per block
+constexpr int BN_QB = 64;      // channel quads per block (256 channels)
+
+struct Stats {  // (z, z^2)
+    const float *z;
+    __device__ void at(int64_t i, float4 &a, float4 &b) const {
+        const float4 v = *(const float4 *)(z + i);
+        a = v;
+        b = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
+    }
+};
+
+struct Grads {  // (g, g * xhat)
+    const float *dy, *y, *z, *mean, *rstd;
+    int C;
+    __device__ void at(int64_t i, float4 &a, float4 &b) const {
+        const int c = (int)(i % C);
+        const float4 d = *(const float4 *)(dy + i), v = *(const float4 *)(z + i);
+        float g[4] = {d.x, d.y, d.z, d.w};
+        if (y) {
+            const float4 o = *(const float4 *)(y + i);
+            const float ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
+        }
+        const float zv[4] = {v.x, v.y, v.z, v.w};
+        float h[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h[u] = g[u] * ((zv[u] - mean[c + u]) * rstd[c + u]);
+        a = make_float4(g[0], g[1], g[2], g[3]);
+        b = make_float4(h[0], h[1], h[2], h[3]);
+    }
+};
+
+// grid (row blocks, channel slices of BN_QB quads); part [nb][C][2]
+template <class F>
+__global__ __launch_bounds__(BN_T) void k_bn_partial(F f, int64_t M, int C, double *__restrict__ part) {
+    __shared__ double red[BN_T][4][2];
+    const int C4 = C / 4, tid = threadIdx.x, blk = blockIdx.x;
+    const int qb = C4 < BN_QB ? C4 : BN_QB;  // quads handled per block
+    const int q = tid % qb, ph = tid / qb, nph = BN_T / qb;
+    const int qg = blockIdx.y * BN_QB + q;
+    const int64_t r0 = (int64_t)blk * BN_ROWS, r1 = r0 + BN_ROWS < M ? r0 + BN_ROWS : M;
+    double s[4] = {0, 0, 0, 0}, t[4] = {0, 0, 0, 0};
+    if (ph < nph && qg < C4) {
+        for (int64_t r = r0 + ph; r < r1; r += nph) {
+            float4 a, b;
+            f.at(r * C + 4 * qg, a, b);
+            s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
+            t[0] += b.x; t[1] += b.y; t[2] += b.z; t[3] += b.w;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        red[tid][u][0] = s[u];
+        red[tid][u][1] = t[u];
+    }
+    __syncthreads();
+    if (tid < 4 * qb) {
+        const int qq = tid / 4, u = tid % 4, c = 4 * (blockIdx.y * BN_QB + qq) + u;
+        if (c < C) {
+            double a = 0.0, b = 0.0;
+            for (int p = 0; p < nph; ++p) {
+                a += red[p * qb + qq][u][0];
+                b += red[p * qb + qq][u][1];
+            }
+            double *o = part + ((size_t)blk * C + c) * 2;
+            o[0] = a;
+            o[1] = b;
+        }
+    }
+}
+
+__global__ void k_bn_finalize(const double *__restrict__ part, int nb, int64_t M, int C, float eps, float momentum,
+                              const float *__restrict__ gamma, const float *__restrict__ beta,
+                              float *__restrict__ running_mean, float *__restrict__ running_var,
+                              float *__restrict__ mean, float *__restrict__ rstd, float *__restrict__ scale,
+                              float *__restrict__ shift) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nb; ++k) {
+        a += part[((size_t)k * C + c) * 2];
+        b += part[((size_t)k * C + c) * 2 + 1];
+    }
+    const double mu = a / (double)M;
+    double var = b / (double)M - mu * mu;
+    var = var > 0.0 ? var : 0.0;
+    const float r = (float)(1.0 / __builtin_sqrt(var + (double)eps));
+    const float sc = gamma[c] * r;
+    mean[c] = (float)mu;
+    rstd[c] = r;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mu * sc;
+    if (running_mean) {
+        const float unb = (float)(M > 1 ? var * (double)M / (double)(M - 1) : var);
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mu;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+}
+
+__global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__restrict__ scale,
+                           const float *__restrict__ shift, const float *__restrict__ res, int relu,
+                           float *__restrict__ y, int64_t total4) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * i;
+        const int c = (int)(e % C);
+        const float4 v = *(const float4 *)(z + e);
+        const float4 s = *(const float4 *)(scale + c), h = *(const float4 *)(shift + c);
+        float4 o = make_float4(v.x * s.x + h.x, v.y * s.y + h.y, v.z * s.z + h.z, v.w * s.w + h.w);
+        if (res) {
+            const float4 r = *(const float4 *)(res + e);
+            o = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
+        }
+        if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+        *(float4 *)(y + e) = o;
+    }
+}
+
+// coef [C][2] = (sum g / M, sum g xhat / M)
+__global__ void k_bn_bwd_finalize(const double *__restrict__ part, int nb, int64_t M, int C, float *__restrict__ coef,
+                                  float *__restrict__ dgamma, float *__restrict__ dbeta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nb; ++k) {
+        a += part[((size_t)k * C + c) * 2];
+        b += part[((size_t)k * C + c) * 2 + 1];
+    }
+    dbeta[c] = (float)a;
+    dgamma[c] = (float)b;
+    coef[2 * c] = (float)(a / (double)M);
+    coef[2 * c + 1] = (float)(b / (double)M);
+}
+
+__global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__restrict__ y, const float *__restrict__ z,
+                               int C, const float *__restrict__ mean, const float *__restrict__ rstd,
+                               const float *__restrict__ gamma, const float *__restrict__ coef, float *__restrict__ dz,
+                               float *__restrict__ dres, int64_t total4) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * i;
+        const int c0 = (int)(e % C);
+        const float4 d = *(const float4 *)(dy + e), v = *(const float4 *)(z + e);
+        float g[4] = {d.x, d.y, d.z, d.w};
+        if (y) {
+            const float4 o = *(const float4 *)(y + e);
+            const float ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
+        }
+        const float zv[4] = {v.x, v.y, v.z, v.w};
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int c = c0 + u;
+            const float xh = (zv[u] - mean[c]) * rstd[c];
+            o[u] = gamma[c] * rstd[c] * (g[u] - coef[2 * c] - xh * coef[2 * c + 1]);
+        }
+        *(float4 *)(dz + e) = make_float4(o[0], o[1], o[2], o[3]);
+        if (dres) *(float4 *)(dres + e) = make_float4(g[0], g[1], g[2], g[3]);
+    }
+}
+
+inline int row_blocks(int64_t M) { return (int)((M + BN_ROWS - 1) / BN_ROWS); }
+inline bool bn_shape_ok(int64_t M, int C) { return M > 0 && C > 0 && C % 4 == 0 && row_blocks(M) < (1 << 30); }
+
+inline unsigned stream_blocks(int64_t total4) {
+    int64_t b = (total4 + 255) / 256;
+    return (unsigned)(b > 8192 ? 8192 : b);
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t bev_batchnorm_workspace_bytes(int64_t M, int C) {
+    if (!bn_shape_ok(M, C)) return -1;
+    return (int64_t)row_blocks(M) * C * 2 * (int64_t)sizeof(double) + (int64_t)C * 2 * (int64_t)sizeof(float);
+}
+
+int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, float momentum, const float *gamma,
+                                const float *beta, float *running_mean, float *running_var, float *mean, float *rstd,
+                                float *scale, float *shift, void *workspace, void *stream) {
+    if (!z || !gamma || !beta || !mean || !rstd || !scale || !shift || !workspace || !bn_shape_ok(M, C) ||
+        (!running_mean) != (!running_var))
+        return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = row_blocks(M);
+    double *part = (double *)workspace;
+    const dim3 grid(nb, (C / 4 + BN_QB - 1) / BN_QB);
+    hipLaunchKernelGGL(k_bn_partial<Stats>, grid, dim3(BN_T), 0, st, Stats{z}, M, C, part);
+    hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, M, C, eps, momentum, gamma,
+                       beta, running_mean, running_var, mean, rstd, scale, shift);
+    return (int)hipGetLastError();
+}
+
+int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                            const float *residual, int relu, float *y, void *stream) {
+    if (!z || !scale || !shift || !y || !bn_shape_ok(M, C)) return BEV_ERR_ARGS;
+    const int64_t total4 = M * C / 4;
+    hipLaunchKernelGGL(k_bn_apply, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C, scale, shift,
+                       residual, relu, y, total4);
+    return (int)hipGetLastError();
+}
+
+int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
+                          const float *rstd, const float *gamma, float *dz, float *dres, float *dgamma, float *dbeta,
+                          void *workspace, void *stream) {
+    if (!dy || !z || !mean || !rstd || !gamma || !dz || !dgamma || !dbeta || !workspace || !bn_shape_ok(M, C))
+        return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = row_blocks(M);
+    double *part = (double *)workspace;
+    float *coef = (float *)(part + (size_t)nb * C * 2);
+    const dim3 grid(nb, (C / 4 + BN_QB - 1) / BN_QB);
+    hipLaunchKernelGGL(k_bn_partial<Grads>, grid, dim3(BN_T), 0, st, Grads{dy, y, z, mean, rstd, C}, M, C, part);
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, M, C, coef, dgamma, dbeta);
+    const int64_t total4 = M * C / 4;
+    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,
+                       coef, dz, dres, total4);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

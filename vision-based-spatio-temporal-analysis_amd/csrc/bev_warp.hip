@@ -360,7 +360,6 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
-constexpr int DPS = 272;  // bytes per staged pixel
 
 __device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
     return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)p;

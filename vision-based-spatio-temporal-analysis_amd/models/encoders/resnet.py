@@ -10,8 +10,9 @@ state_dict loads unchanged.  Parity with timm itself is therefore UNPINNED;
 the conv kernels are pinned against a torch fp32 reference of the same
 weights (oracle/backbone_ref.py, tests/test_backbone_gpu.py).
 
-Training (train mode with gradients): one autograd node per conv + frozen BN on
-the native forward / backward kernels (trunk_grad.py).
+Training (train mode with gradients): one autograd node per conv + BN on the native
+forward / backward kernels (trunk_grad.py); BN uses batch statistics when its module is in
+training mode (timm under model.train()), the folded running statistics when it is in eval().
 
 Execution (inference / eval mode): activations stay channels-last (NHWC) on
 the device; every conv+BN(+residual)(+ReLU) is ONE `bev_conv2d_f32` launch
@@ -225,8 +226,8 @@ class ResNet(nn.Module):
         return y
 
     def _forward_train(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
-        """Training: the same graph with one autograd node per conv + frozen BN (+ residual) (+ ReLU)
-        and native backward kernels (trunk_grad.py).  No bottleneck-tail fusion (the shortcut's
+        """Training: the same graph with one autograd node per conv + BN (+ residual) (+ ReLU)
+        and native backward kernels (trunk_grad.py; batch-statistics or frozen BN per module mode).  No bottleneck-tail fusion (the shortcut's
         gradient is a separate conv backward)."""
         from .trunk_grad import MaxPool, conv_bn_act
         y = conv_bn_act(self.conv1, self.bn1, x, relu=True, in_nchw=True)

@@ -11,11 +11,20 @@ backward runs native kernels:
   dbf = sum_m dz                             bev_colsum_f32
   residual gradient = dz
 
-BatchNorm is FROZEN in training (running statistics folded into the conv, the usual setting for
-fine-tuning a detection backbone): W_f = W * s, b_f = beta - mean * s with s = gamma / sqrt(var + eps),
-so dW = dWf * s, dgamma = (sum dWf * W - mean * dbf) / sqrt(var + eps), dbeta = dbf (tiny
-parameter-sized ops).  Running statistics are not updated.  Deviation from timm's train-mode BN
-(batch statistics): documented in DESIGN.md.  `MaxPool` backward: bev_maxpool2d_bwd_nhwc_f32.
+BatchNorm follows the module's own mode, as torch does:
+
+* `bn.training` (model.train(), what the reference's train.py:222 runs): BATCH statistics --
+  `ConvBNTrain`: z = conv(x, W) (MFMA), per-channel batch mean / variance of z
+  (bev_batchnorm_train_fwd_f32, which also updates running_mean / running_var with the momentum
+  rule and counts num_batches_tracked), y = act(z * scale + shift (+ residual))
+  (bev_batchnorm_apply_f32); backward bev_batchnorm_bwd_f32 (dz, d residual, dgamma, dbeta) then
+  the conv dgrad / wgrad above.
+* `bn.eval()` inside a training model (the usual way to freeze BN when fine-tuning): running
+  statistics folded into the conv -- `ConvBNAct`: W_f = W * s, b_f = beta - mean * s with
+  s = gamma / sqrt(var + eps), so dW = dWf * s, dgamma = (sum dWf * W - mean * dbf) / sqrt(var + eps),
+  dbeta = dbf (tiny parameter-sized ops).
+
+`MaxPool` backward: bev_maxpool2d_bwd_nhwc_f32.
 """
 from __future__ import annotations
 
@@ -24,7 +33,7 @@ import torch.nn as nn
 
 import bev_native as _nat
 
-__all__ = ["ConvBNAct", "ConvAct", "MaxPool", "conv_bn_act", "conv_act"]
+__all__ = ["ConvBNAct", "ConvBNTrain", "ConvAct", "MaxPool", "conv_bn_act", "conv_act"]
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -82,8 +91,43 @@ class ConvBNAct(torch.autograd.Function):
         return dx, dw, dgamma, dbf, None, None, None, None, (dz if has_res else None)
 
 
+class ConvBNTrain(torch.autograd.Function):
+    """act(BN_batch(conv(x, W)) (+ residual)) with batch statistics (train-mode BatchNorm2d)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, conv, bn, relu: bool, in_nchw: bool, residual):
+        k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        w = weight.detach().float().contiguous()
+        Co = conv.out_channels
+        z = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(w), torch.zeros(Co, device=x.device), Co, k, k, st, p, False,
+                             in_nchw=in_nchw)
+        track = bn.track_running_stats and bn.running_mean is not None
+        if track:
+            bn.num_batches_tracked.add_(1)
+        momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+        mean, rstd, scale, shift = _nat.batchnorm_train_fwd(z, gamma, beta, bn.running_mean if track else None,
+                                                            bn.running_var if track else None, bn.eps, momentum)
+        y = _nat.batchnorm_apply(z, scale, shift, residual, relu)
+        ctx.save_for_backward(x, z, y if relu else None, w, mean, rstd, gamma)
+        ctx.meta = (k, st, p, in_nchw, residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, y, w, mean, rstd, gamma = ctx.saved_tensors
+        k, st, p, in_nchw, has_res = ctx.meta
+        dz, dres, dgamma, dbeta = _nat.batchnorm_bwd(dy.float(), y, z, mean, rstd, gamma, has_res)
+        xn = _nat.nchw_to_nhwc(x) if in_nchw else x
+        H, W = xn.shape[1], xn.shape[2]
+        dx = _dgrad(dz, w, H, W, st, p) if (ctx.needs_input_grad[0] and not in_nchw) else None
+        dw = _nat.conv_wgrad(xn, dz, k, k, st, p)
+        return dx, dw, dgamma, dbeta, None, None, None, None, dres
+
+
 def conv_bn_act(conv: nn.Conv2d, bn: nn.BatchNorm2d, x, relu: bool, residual=None, in_nchw: bool = False):
-    return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, relu, in_nchw, residual)
+    """One trunk layer in training: batch-statistics BN when `bn.training`, else the folded frozen BN."""
+    fn = ConvBNTrain if bn.training else ConvBNAct
+    return fn.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, relu, in_nchw, residual)
 
 
 class ConvAct(torch.autograd.Function):
