@@ -46,13 +46,15 @@ int bev_abi_version(void);
  *   0 = LDS-DMA kernel (default), 1 = register-staged.
  * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
- * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles. */
+ * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.
+ * BEV_TUNE_WGRAD_MFMA: 1 (default) = conv weight gradient on the MFMA, 0 = the VALU float4 kernel. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
 #define BEV_TUNE_WARP_BWD_POOL 5
 #define BEV_TUNE_CONV_XCD 6
 #define BEV_TUNE_CONV_NBUF 7
+#define BEV_TUNE_WGRAD_MFMA 8
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

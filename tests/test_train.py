@@ -295,22 +295,27 @@ def test_bevnet_training_trunk_end_to_end():
 
 
 WGRAD_CASES = [
-    # N, Ci, H, W, Co, k, stride, pad -- Ci % 64 == 0 routes to k_wgrad_v4, the rest to k_wgrad
+    # N, Ci, H, W, Co, k, stride, pad -- the host pads Ci / Co to multiples of 4, every case runs k_wgrad_v4
     (2, 64, 13, 17, 64, 3, 1, 1),     # layer1 3x3 (v4)
     (1, 128, 15, 21, 128, 3, 2, 1),   # strided 3x3 (v4), Wo < 16 rows wrap several output rows per step
     (2, 64, 9, 11, 256, 1, 1, 0),     # 1x1 expand (v4)
     (1, 256, 15, 21, 512, 1, 2, 0),   # strided 1x1 downsample (v4)
     (1, 64, 5, 7, 200, 1, 1, 0),      # ragged Co (v4, partial co block)
-    (1, 3, 37, 53, 64, 7, 2, 3),      # stem (generic)
-    (1, 48, 9, 10, 24, 3, 1, 1),      # Ci % 64 != 0 (generic)
+    (1, 3, 37, 53, 64, 7, 2, 3),      # stem (Ci padded 3 -> 4)
+    (1, 48, 9, 10, 24, 3, 1, 1),      # Ci % 64 != 0: 64-wide k blocks straddle taps
+    (1, 96, 11, 13, 512, 3, 1, 1),    # BEV head conv1 operand (66 channels padded to 96)
+    (1, 128, 9, 10, 5, 3, 1, 1),      # the head's 5 outputs (Co padded to 8)
+    (2, 24, 12, 14, 16, 3, 1, 2),     # pad 2 (dilated head geometry without dilation)
+    (2, 64, 70, 90, 192, 3, 1, 1),    # many m splits and co / k tiles (ragged last tile of 128)
 ]
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mfma", [1, 0], ids=["mfma", "valu"])
 @pytest.mark.parametrize("case", WGRAD_CASES, ids=[f"ci{c[1]}_co{c[4]}_k{c[5]}s{c[6]}" for c in WGRAD_CASES])
-def test_wgrad_and_colsum_vs_torch(case):
-    """bev_conv_wgrad_f32 / bev_colsum_f32 vs torch's conv2d weight / bias gradients (fp32; float atomics
-    change the summation order: rtol 1e-4 of the gradient scale)."""
+def test_wgrad_and_colsum_vs_torch(case, mfma):
+    """bev_conv_wgrad_f32 (MFMA kernel and the VALU float4 kernel) / bev_colsum_f32 vs torch's conv2d weight /
+    bias gradients (fp32; float atomics change the summation order: rtol 1e-4 of the gradient scale)."""
     import bev_native as nat
     N, Ci, H, W, Co, k, s, p = case
     g = torch.Generator().manual_seed(5)
@@ -321,7 +326,8 @@ def test_wgrad_and_colsum_vs_torch(case):
     dz = torch.randn(y.shape, generator=g)
     y.backward(dz)
     dzn = dz.permute(0, 2, 3, 1).contiguous().to("cuda:0")
-    dW = nat.conv_wgrad(x.permute(0, 2, 3, 1).contiguous().to("cuda:0"), dzn, k, k, s, p).cpu()
+    with nat.tuned(WGRAD_MFMA=mfma):
+        dW = nat.conv_wgrad(x.permute(0, 2, 3, 1).contiguous().to("cuda:0"), dzn, k, k, s, p).cpu()
     db = nat.colsum(dzn).cpu()
     scale = float(w.grad.abs().max())
     np.testing.assert_allclose(dW.numpy(), w.grad.numpy(), rtol=0, atol=1e-4 * scale)

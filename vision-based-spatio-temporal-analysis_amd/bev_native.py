@@ -143,6 +143,7 @@ TUNE_WARP_KERNEL = 3
 TUNE_WARP_BWD_POOL = 5
 TUNE_CONV_XCD = 6
 TUNE_CONV_NBUF = 7
+TUNE_WGRAD_MFMA = 8
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 
@@ -459,16 +460,14 @@ def dilate_nhwc(dz: torch.Tensor, s: int, top: int, left: int, Hd: int, Wd: int)
     return out
 
 
+def _pad_last(t: torch.Tensor, m: int) -> torch.Tensor:
+    c = t.shape[-1]
+    return t if c % m == 0 else torch.nn.functional.pad(t, (0, m - c % m))
+
+
 def conv_wgrad(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stride: int, pad: int) -> torch.Tensor:
     """x [N,H,W,Ci], dz [N,Ho,Wo,Co] (NHWC) -> dW [Co, Ci, KH, KW] (torch OIHW)."""
-    x, dz = x.contiguous(), dz.contiguous()
-    _require_gpu(x, dz)
-    N, H, W, Ci = x.shape
-    _, Ho, Wo, Co = dz.shape
-    dW = torch.empty(Co, KH, KW, Ci, device=x.device, dtype=torch.float32)
-    _check(lib().bev_conv_wgrad_f32(_ptr(x), N, H, W, Ci, _ptr(dz), Ho, Wo, Co, KH, KW, stride, pad, _ptr(dW),
-                                    _stream(x)), "bev_conv_wgrad_f32")
-    return dW.permute(0, 3, 1, 2)
+    return conv_wgrad_ex(x, dz, KH, pad, 1, stride=stride, KW=KW)
 
 
 def colsum(dz: torch.Tensor) -> torch.Tensor:
@@ -547,16 +546,21 @@ def conv2d_nhwc_ex(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, K: int,
     return out
 
 
-def conv_wgrad_ex(x: torch.Tensor, dz: torch.Tensor, K: int, pad: int, dilation: int) -> torch.Tensor:
-    """Stride-1 dilated conv weight gradient: x [N,H,W,Ci], dz [N,Ho,Wo,Co] -> dW [Co, Ci, K, K] (OIHW view)."""
-    x, dz = x.contiguous(), dz.contiguous()
-    _require_gpu(x, dz)
+def conv_wgrad_ex(x: torch.Tensor, dz: torch.Tensor, K: int, pad: int, dilation: int, stride: int = 1,
+                  KW: int = None) -> torch.Tensor:
+    """Conv weight gradient (dilation, stride): x [N,H,W,Ci], dz [N,Ho,Wo,Co] -> dW [Co, Ci, K, KW] (OIHW view).
+    Ci and Co are zero-padded to multiples of 4 here (the stem's 3 input channels, the head's 5 outputs) so
+    every call takes the float4 kernel; the padding's gradient rows / columns are sliced off."""
+    KH, KW = K, (K if KW is None else KW)
     N, H, W, Ci = x.shape
     _, Ho, Wo, Co = dz.shape
-    dW = torch.empty(Co, K, K, Ci, device=x.device, dtype=torch.float32)
-    _check(lib().bev_conv_wgrad_ex_f32(_ptr(x), N, H, W, Ci, _ptr(dz), Ho, Wo, Co, K, K, 1, pad, dilation, _ptr(dW),
-                                       _stream(x)), "bev_conv_wgrad_ex_f32")
-    return dW.permute(0, 3, 1, 2)
+    xp, dzp = _pad_last(x.contiguous(), 4).contiguous(), _pad_last(dz.contiguous(), 4).contiguous()
+    _require_gpu(xp, dzp)
+    Cip, Cop = xp.shape[-1], dzp.shape[-1]
+    dW = torch.empty(Cop, KH, KW, Cip, device=x.device, dtype=torch.float32)
+    _check(lib().bev_conv_wgrad_ex_f32(_ptr(xp), N, H, W, Cip, _ptr(dzp), Ho, Wo, Cop, KH, KW, stride, pad, dilation,
+                                       _ptr(dW), _stream(x)), "bev_conv_wgrad_ex_f32")
+    return dW[:Co, :, :, :Ci].permute(0, 3, 1, 2)
 
 
 def _gn_workspace(N, P, C, G, device):

@@ -26,7 +26,7 @@ constexpr int BN_QB = 64;      // channel quads per block (256 channels)
 
 struct Stats {  // (z, z^2)
     const float *z;
-    __device__ void at(int64_t i, float4 &a, float4 &b) const {
+    __device__ void at(int64_t i, int, float4 &a, float4 &b) const {
         const float4 v = *(const float4 *)(z + i);
         a = v;
         b = make_float4(v.x * v.x, v.y * v.y, v.z * v.z, v.w * v.w);
@@ -35,9 +35,7 @@ struct Stats {  // (z, z^2)
 
 struct Grads {  // (g, g * xhat)
     const float *dy, *y, *z, *mean, *rstd;
-    int C;
-    __device__ void at(int64_t i, float4 &a, float4 &b) const {
-        const int c = (int)(i % C);
+    __device__ void at(int64_t i, int c, float4 &a, float4 &b) const {
         const float4 d = *(const float4 *)(dy + i), v = *(const float4 *)(z + i);
         float g[4] = {d.x, d.y, d.z, d.w};
         if (y) {
@@ -68,7 +66,7 @@ __global__ __launch_bounds__(BN_T) void k_bn_partial(F f, int64_t M, int C, doub
     if (ph < nph && qg < C4) {
         for (int64_t r = r0 + ph; r < r1; r += nph) {
             float4 a, b;
-            f.at(r * C + 4 * qg, a, b);
+            f.at(r * C + 4 * qg, 4 * qg, a, b);
             s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
             t[0] += b.x; t[1] += b.y; t[2] += b.z; t[3] += b.w;
         }
@@ -94,18 +92,40 @@ __global__ __launch_bounds__(BN_T) void k_bn_partial(F f, int64_t M, int C, doub
     }
 }
 
-__global__ void k_bn_finalize(const double *__restrict__ part, int nb, int64_t M, int C, float eps, float momentum,
+// Column sums of part [nb][C][2] for 16 channels per block: 16 row-block phases per channel, LDS reduce.
+constexpr int FIN_C = 16, FIN_P = 16;
+__device__ inline bool fin_sums(const double *__restrict__ part, int nb, int C, double &a, double &b) {
+    __shared__ double red[FIN_P][FIN_C][2];
+    const int cl = threadIdx.x % FIN_C, ph = threadIdx.x / FIN_C, c = blockIdx.x * FIN_C + cl;
+    double s = 0.0, t = 0.0;
+    if (c < C) {
+#pragma unroll 4
+        for (int k = ph; k < nb; k += FIN_P) {
+            s += part[((size_t)k * C + c) * 2];
+            t += part[((size_t)k * C + c) * 2 + 1];
+        }
+    }
+    red[ph][cl][0] = s;
+    red[ph][cl][1] = t;
+    __syncthreads();
+    if (ph != 0 || c >= C) return false;
+    a = 0.0;
+    b = 0.0;
+    for (int p = 0; p < FIN_P; ++p) {
+        a += red[p][cl][0];
+        b += red[p][cl][1];
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize(const double *__restrict__ part, int nb, int64_t M, int C, float eps, float momentum,
                               const float *__restrict__ gamma, const float *__restrict__ beta,
                               float *__restrict__ running_mean, float *__restrict__ running_var,
                               float *__restrict__ mean, float *__restrict__ rstd, float *__restrict__ scale,
                               float *__restrict__ shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double a = 0.0, b = 0.0;
-    for (int k = 0; k < nb; ++k) {
-        a += part[((size_t)k * C + c) * 2];
-        b += part[((size_t)k * C + c) * 2 + 1];
-    }
+    double a, b;
+    if (!fin_sums(part, nb, C, a, b)) return;
+    const int c = blockIdx.x * FIN_C + threadIdx.x;
     const double mu = a / (double)M;
     double var = b / (double)M - mu * mu;
     var = var > 0.0 ? var : 0.0;
@@ -122,12 +142,15 @@ __global__ void k_bn_finalize(const double *__restrict__ part, int nb, int64_t M
     }
 }
 
+// IT: uint32_t when the element count fits (no 64-bit divisions in the channel decode), else int64_t
+template <typename IT>
 __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__restrict__ scale,
                            const float *__restrict__ shift, const float *__restrict__ res, int relu,
-                           float *__restrict__ y, int64_t total4) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = 4 * i;
-        const int c = (int)(e % C);
+                           float *__restrict__ y, IT total4) {
+    const IT C4 = (IT)(C / 4);
+    for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * (int64_t)i;
+        const int c = 4 * (int)(i % C4);
         const float4 v = *(const float4 *)(z + e);
         const float4 s = *(const float4 *)(scale + c), h = *(const float4 *)(shift + c);
         float4 o = make_float4(v.x * s.x + h.x, v.y * s.y + h.y, v.z * s.z + h.z, v.w * s.w + h.w);
@@ -141,28 +164,28 @@ __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__re
 }
 
 // coef [C][2] = (sum g / M, sum g xhat / M)
-__global__ void k_bn_bwd_finalize(const double *__restrict__ part, int nb, int64_t M, int C, float *__restrict__ coef,
-                                  float *__restrict__ dgamma, float *__restrict__ dbeta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double a = 0.0, b = 0.0;
-    for (int k = 0; k < nb; ++k) {
-        a += part[((size_t)k * C + c) * 2];
-        b += part[((size_t)k * C + c) * 2 + 1];
-    }
+__global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_bwd_finalize(const double *__restrict__ part, int nb, int64_t M,
+                                                                    int C, float *__restrict__ coef,
+                                                                    float *__restrict__ dgamma,
+                                                                    float *__restrict__ dbeta) {
+    double a, b;
+    if (!fin_sums(part, nb, C, a, b)) return;
+    const int c = blockIdx.x * FIN_C + threadIdx.x;
     dbeta[c] = (float)a;
     dgamma[c] = (float)b;
     coef[2 * c] = (float)(a / (double)M);
     coef[2 * c + 1] = (float)(b / (double)M);
 }
 
+template <typename IT>
 __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__restrict__ y, const float *__restrict__ z,
                                int C, const float *__restrict__ mean, const float *__restrict__ rstd,
                                const float *__restrict__ gamma, const float *__restrict__ coef, float *__restrict__ dz,
-                               float *__restrict__ dres, int64_t total4) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = 4 * i;
-        const int c0 = (int)(e % C);
+                               float *__restrict__ dres, IT total4) {
+    const IT C4 = (IT)(C / 4);
+    for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * (int64_t)i;
+        const int c0 = 4 * (int)(i % C4);
         const float4 d = *(const float4 *)(dy + e), v = *(const float4 *)(z + e);
         float g[4] = {d.x, d.y, d.z, d.w};
         if (y) {
@@ -212,7 +235,7 @@ int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, flo
     double *part = (double *)workspace;
     const dim3 grid(nb, (C / 4 + BN_QB - 1) / BN_QB);
     hipLaunchKernelGGL(k_bn_partial<Stats>, grid, dim3(BN_T), 0, st, Stats{z}, M, C, part);
-    hipLaunchKernelGGL(k_bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, M, C, eps, momentum, gamma,
+    hipLaunchKernelGGL(k_bn_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st, part, nb, M, C, eps, momentum, gamma,
                        beta, running_mean, running_var, mean, rstd, scale, shift);
     return (int)hipGetLastError();
 }
@@ -221,8 +244,12 @@ int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale
                             const float *residual, int relu, float *y, void *stream) {
     if (!z || !scale || !shift || !y || !bn_shape_ok(M, C)) return BEV_ERR_ARGS;
     const int64_t total4 = M * C / 4;
-    hipLaunchKernelGGL(k_bn_apply, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C, scale, shift,
-                       residual, relu, y, total4);
+    if (total4 < ((int64_t)1 << 32) - 65536 * 256)
+        hipLaunchKernelGGL(k_bn_apply<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C,
+                           scale, shift, residual, relu, y, (uint32_t)total4);
+    else
+        hipLaunchKernelGGL(k_bn_apply<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C,
+                           scale, shift, residual, relu, y, total4);
     return (int)hipGetLastError();
 }
 
@@ -236,11 +263,16 @@ int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64
     double *part = (double *)workspace;
     float *coef = (float *)(part + (size_t)nb * C * 2);
     const dim3 grid(nb, (C / 4 + BN_QB - 1) / BN_QB);
-    hipLaunchKernelGGL(k_bn_partial<Grads>, grid, dim3(BN_T), 0, st, Grads{dy, y, z, mean, rstd, C}, M, C, part);
-    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, M, C, coef, dgamma, dbeta);
+    hipLaunchKernelGGL(k_bn_partial<Grads>, grid, dim3(BN_T), 0, st, Grads{dy, y, z, mean, rstd}, M, C, part);
+    hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st, part, nb, M, C,
+                       coef, dgamma, dbeta);
     const int64_t total4 = M * C / 4;
-    hipLaunchKernelGGL(k_bn_bwd_apply, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,
-                       coef, dz, dres, total4);
+    if (total4 < ((int64_t)1 << 32) - 65536 * 256)
+        hipLaunchKernelGGL(k_bn_bwd_apply<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean,
+                           rstd, gamma, coef, dz, dres, (uint32_t)total4);
+    else
+        hipLaunchKernelGGL(k_bn_bwd_apply<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean,
+                           rstd, gamma, coef, dz, dres, total4);
     return (int)hipGetLastError();
 }
 

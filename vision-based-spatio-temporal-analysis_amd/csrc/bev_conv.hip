@@ -884,6 +884,7 @@ int bev_tune(int knob, int value) {
         *slot = value;
         return old;
     }
+    if (knob == BEV_TUNE_WGRAD_MFMA) return bev::train_tune(knob, value);
     return bev::warp_tune(knob, value);
 }
 

@@ -8,7 +8,7 @@
 //   k_dilate       zero-inserted, padded copy of dz for strided dgrad  (so dgrad is a stride-1 conv)
 //   bev_conv2d_f32 dx = conv(dilate(dz), flip(W)^T)                    (the forward MFMA kernel)
 //   k_wgrad        dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k]       (LDS-tiled, split over m, f32 atomics;
-//                  k_wgrad_v4 = float4 staging without index divisions when Ci % 64 == 0)
+//                  k_wgrad_v4 = float4 staging without index divisions when Ci % 4 == 0 and Co % 4 == 0)
 //   k_colsum       db[co] = sum_m dz[m][co]
 //   k_maxpool_bwd  dx = sum of dy over the windows whose first maximum is this input (gather, no atomics;
 //                  k_maxpool_bwd_v4: four channels per thread when C % 4 == 0)
@@ -19,8 +19,11 @@
 #include <stdint.h>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_tune.h"
 
 namespace {
+
+int g_wgrad_mfma = 1;  // bev_tune(BEV_TUNE_WGRAD_MFMA): 0 = the VALU k_wgrad_v4 (A/B)
 
 inline int last() {
     const hipError_t e = hipGetLastError();
@@ -120,22 +123,25 @@ __global__ __launch_bounds__(256) void k_wgrad(const float *__restrict__ x, cons
     }
 }
 
-// Same contraction for Ci % 64 == 0 and Co % 4 == 0 (every ResNet trunk conv but the stem): a 64-wide
-// k block lies inside ONE (ky, kx) tap, so it is 64 consecutive channels of one input pixel.  Each
-// thread stages one float4 of each operand per m step (row tid >> 4, columns 4 (tid & 15)); the
-// output pixel (n, oy, ox) of its row advances incrementally -- no integer division in the loop
-// (the generic kernel spends most of its time in the per-element 64-bit index decode).
+// Same contraction for Ci % 4 == 0 and Co % 4 == 0 (every trunk / head conv once the stem's 3 input channels
+// and the head's 5 outputs are zero-padded to 4 / 8 by the host).  Each thread stages one float4 of each
+// operand per m step (row tid >> 4, columns 4 (tid & 15)); its k column (tap ky, kx and channel ci) is fixed
+// for the whole loop and decoded once, and the output pixel (n, oy, ox) of its row advances incrementally --
+// no integer division in the loop (the generic kernel spends most of its time in the per-element 64-bit index
+// decode).
 __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, const float *__restrict__ dz, int N,
-                                                  int H, int W, int Ci, int Ho, int Wo, int Co, int KW, int stride,
-                                                  int pad, int dil, int64_t mchunk, float *__restrict__ dW) {
+                                                  int H, int W, int Ci, int Ho, int Wo, int Co, int KW, int K,
+                                                  int stride, int pad, int dil, int64_t mchunk, float *__restrict__ dW) {
     __shared__ __attribute__((aligned(16))) float sa[WG_M][WG_T + 4];
     __shared__ __attribute__((aligned(16))) float sd[WG_M][WG_T + 4];
     const int k0 = blockIdx.x * WG_T, co0 = blockIdx.y * WG_T;
-    const int rr = k0 / Ci, ci0 = k0 - rr * Ci, kx = rr % KW, ky = rr / KW;
     const int64_t M = (int64_t)N * Ho * Wo;
     const int64_t mb = (int64_t)blockIdx.z * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
     const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
     const int r = tid >> 4, c4 = tid & 15;
+    const int kk = k0 + 4 * c4;  // this thread's staged k column (4 channels of one tap)
+    const bool k_ok = kk < K;
+    const int rr = k_ok ? kk / Ci : 0, ci = kk - rr * Ci, kx = rr % KW, ky = rr / KW;
     const bool dz_ok = co0 + 4 * c4 < Co;
     // output pixel of row mb + r
     int64_t mm = mb + r;
@@ -152,8 +158,8 @@ __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, c
         float4 av = make_float4(0.f, 0.f, 0.f, 0.f), dv = av;
         if (mm < me) {
             const int iy = oy * stride - pad + ky * dil, ix = ox * stride - pad + kx * dil;
-            if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-                av = *(const float4 *)(x + (((int64_t)n * H + iy) * W + ix) * Ci + ci0 + 4 * c4);
+            if (k_ok && iy >= 0 && iy < H && ix >= 0 && ix < W)
+                av = *(const float4 *)(x + (((int64_t)n * H + iy) * W + ix) * Ci + ci);
             if (dz_ok) dv = *(const float4 *)(dz + mm * Co + co0 + 4 * c4);
         }
         *(float4 *)&sa[r][4 * c4] = av;
@@ -179,14 +185,196 @@ __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, c
         }
         __syncthreads();
     }
-    const int64_t ldk = (int64_t)gridDim.x * WG_T;  // = K = KH * KW * Ci (a multiple of 64): every k is valid
+    const int kc = k0 + tc * 4;
+    if (kc >= K) return;  // K % 4 == 0: the thread's 4 columns are all valid or all not
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int co = co0 + tr * 4 + i;
         if (co >= Co) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) atomicAdd(dW + co * ldk + k0 + tc * 4 + j, acc[i][j]);
+        for (int j = 0; j < 4; ++j) atomicAdd(dW + (int64_t)co * K + kc + j, acc[i][j]);
     }
+}
+
+
+// ---- weight gradient on the MFMA --------------------------------------------------------------------
+// dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k] as a GEMM whose reduction runs over the output pixels m.
+// Workgroup tile CT (co) x KT (k) = (WCO x TM x 32) x (WK x TN x 32), WCO x WK = 4 waves of TM x TN
+// v_mfma_f32_32x32x2_f32 tiles -- 128 x 128 in general, 64 x 256 for 64-channel layers, 256 x 64 for K = 64,
+// 32 x 512 for the BEV head's 5 (-> 8) outputs, so the MFMA tiles are not half empty on the narrow layers.
+// Each step stages 32 pixels of both operands TRANSPOSED into LDS ([co][m] and [k][m], 144-B rows) so the
+// MFMA fragments are contiguous float4 reads along m, exactly like k_conv's A/B panels; the next step's global
+// loads are issued into registers before the current step's MFMAs.  A thread's staged k column (one tap, 4
+// channels) is decoded once, and the output pixels of its rows advance incrementally.  The m range is split
+// over a 1-D XCD-aware grid (the tiles of one m split run on one XCD and share its L2); partial tiles are
+// added with float atomics (summation order varies in the last bits, as in k_wgrad).
+typedef float wf32x16 __attribute__((ext_vector_type(16)));
+typedef float wf32x4 __attribute__((ext_vector_type(4)));
+constexpr int WM_BM = 32, WM_LROW = 36;
+
+// LDS element (row c, pixel m) of a staged operand: 36-float rows; the 16-B group of m is XOR-swizzled by
+// c >> 4 so the transposed staging writes (lanes = consecutive float4 columns c = 4 ac + u) hit distinct
+// banks, while the float4 fragment reads (16 consecutive rows share one key) stay contiguous and
+// conflict-free.
+__device__ __forceinline__ int wsw(int c, int m) { return c * WM_LROW + ((((m >> 2) ^ ((c >> 4) & 7)) << 2) | (m & 3)); }
+
+template <int WCO, int TM, int TN, int NBUF>
+__global__ __launch_bounds__(256, TN == 4 ? 1 : 2) void k_wgrad_mfma(const float *__restrict__ x, const float *__restrict__ dz,
+                                                       int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
+                                                       int K, int stride, int pad, int dil, int64_t mchunk,
+                                                       int ctiles, int ntiles, float *__restrict__ dW) {
+    constexpr int WK = 4 / WCO, CT = WCO * TM * 32, KT = WK * TN * 32;
+    constexpr int ACOLS = CT / 4, ARPP = 256 / ACOLS, AQ = WM_BM / ARPP;  // float4 columns, rows per pass, passes
+    constexpr int BCOLS = KT / 4, BRPP = 256 / BCOLS, BQ = WM_BM / BRPP;
+    constexpr int STAGE = (CT + KT) * WM_LROW;
+    __shared__ __attribute__((aligned(16))) float lds[NBUF * STAGE];
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int tile = (int)(bid % (unsigned)ntiles);
+    const int64_t split = bid / (unsigned)ntiles;
+    const int co0 = (tile % ctiles) * CT, k0 = (tile / ctiles) * KT;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int64_t mb = split * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    if (mb >= me) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wco = wave / WK, wk = wave % WK;
+    const int ac = tid % ACOLS, ar = tid / ACOLS;  // A staging: float4 column ac, rows ar + ARPP q
+    const int bc = tid % BCOLS, br = tid / BCOLS;  // B staging: float4 column bc, rows br + BRPP q
+    const bool c_ok = co0 + 4 * ac < Co;
+    const int kk = k0 + 4 * bc;
+    const bool k_ok = kk < K;
+    const int tap = k_ok ? kk / Ci : 0, ci = kk - tap * Ci, kx = tap % KW, ky = tap / KW;
+    int px[BQ], py[BQ], pn[BQ];
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+        int64_t m = mb + br + BRPP * q;
+        m = m < M ? m : 0;
+        px[q] = (int)(m % Wo);
+        const int64_t t = m / Wo;
+        py[q] = (int)(t % Ho);
+        pn[q] = (int)(t / Ho);
+    }
+    wf32x4 ra[AQ], rx[BQ];
+    int64_t ms = mb;  // first pixel of the step being loaded
+    auto gload = [&]() {
+#pragma unroll
+        for (int q = 0; q < AQ; ++q) {
+            const int64_t m = ms + ar + ARPP * q;
+            ra[q] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+            if (m < me && c_ok) ra[q] = *(const wf32x4 *)(dz + m * Co + co0 + 4 * ac);
+        }
+#pragma unroll
+        for (int q = 0; q < BQ; ++q) {
+            const int64_t m = ms + br + BRPP * q;
+            rx[q] = (wf32x4){0.f, 0.f, 0.f, 0.f};
+            if (m < me) {
+                const int iy = py[q] * stride - pad + ky * dil, ix = px[q] * stride - pad + kx * dil;
+                if (k_ok && iy >= 0 && iy < H && ix >= 0 && ix < W)
+                    rx[q] = *(const wf32x4 *)(x + (((int64_t)pn[q] * H + iy) * W + ix) * Ci + ci);
+            }
+            px[q] += WM_BM;
+            while (px[q] >= Wo) {
+                px[q] -= Wo;
+                if (++py[q] == Ho) {
+                    py[q] = 0;
+                    ++pn[q];
+                }
+            }
+        }
+        ms += WM_BM;
+    };
+    auto swrite = [&](int buf) {
+        float *As = lds + buf * STAGE, *Bs = As + CT * WM_LROW;
+#pragma unroll
+        for (int q = 0; q < AQ; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) As[wsw(4 * ac + u, ar + ARPP * q)] = ra[q][u];
+#pragma unroll
+        for (int q = 0; q < BQ; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) Bs[wsw(4 * bc + u, br + BRPP * q)] = rx[q][u];
+    };
+    wf32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (wf32x16){0};
+    const int nsteps = (int)((me - mb + WM_BM - 1) / WM_BM);
+    gload();
+    swrite(0);
+    __syncthreads();
+    const int r32 = lane & 31, h = lane >> 5;
+    for (int st = 0; st < nsteps; ++st) {
+        const bool more = st + 1 < nsteps;
+        if (more) gload();
+        const float *As = lds + (NBUF == 2 ? (st & 1) : 0) * STAGE, *Bs = As + CT * WM_LROW;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            wf32x4 fa[TM][2], fb[TN][2];
+            const int m0 = h * 16 + half * 8;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int c = wco * TM * 32 + i * 32 + r32;
+                fa[i][0] = *(const wf32x4 *)(As + wsw(c, m0));
+                fa[i][1] = *(const wf32x4 *)(As + wsw(c, m0 + 4));
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int c = wk * TN * 32 + j * 32 + r32;
+                fb[j][0] = *(const wf32x4 *)(Bs + wsw(c, m0));
+                fb[j][1] = *(const wf32x4 *)(Bs + wsw(c, m0 + 4));
+            }
+#pragma unroll
+            for (int p = 0; p < 8; ++p)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][p >> 2][p & 3], fb[j][p >> 2][p & 3],
+                                                                         acc[i][j], 0, 0, 0);
+        }
+        if (NBUF == 2) {  // write the other buffer while slower waves still read this one
+            if (more) swrite((st + 1) & 1);
+            __syncthreads();
+        } else {
+            __syncthreads();
+            if (more) {
+                swrite(0);
+                __syncthreads();
+            }
+        }
+    }
+    // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int k = k0 + wk * TN * 32 + j * 32 + r32;
+            if (k >= K) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wco * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (co < Co) atomicAdd(dW + (int64_t)co * K + k, acc[i][j][r]);
+            }
+        }
+}
+
+template <int WCO, int TM, int TN, int NBUF = 1>
+int launch_wgrad_mfma(const float *x, const float *dz, int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
+                      int K, int stride, int pad, int dil, float *dW, hipStream_t st) {
+    constexpr int CT = WCO * TM * 32, KT = (4 / WCO) * TN * 32;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int ct = (Co + CT - 1) / CT, kt = (K + KT - 1) / KT, nt = ct * kt;
+    int64_t sp = 1024 / nt + 1;  // >= ~1024 workgroups (2 per CU resident)
+    int64_t mc = (M + sp - 1) / sp;
+    mc = ((mc + WM_BM - 1) / WM_BM) * WM_BM;
+    sp = (M + mc - 1) / mc;
+    if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL((k_wgrad_mfma<WCO, TM, TN, NBUF>), dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci,
+                       Ho, Wo, Co, KW, K, stride, pad, dil, mc, ct, nt, dW);
+    return 0;
 }
 
 __global__ __launch_bounds__(256) void k_colsum(const float *__restrict__ dz, int64_t M, int C, int64_t mchunk,
@@ -389,9 +577,22 @@ int bev_conv_wgrad_ex_f32(const float *x, int N, int H, int W, int Ci, const flo
     mchunk = ((mchunk + WG_M - 1) / WG_M) * WG_M;
     splits = (M + mchunk - 1) / mchunk;
     if (splits > 65535) return BEV_ERR_ARGS;
-    if (Ci % WG_T == 0 && Co % 4 == 0)
+    if (Ci % 4 == 0 && Co % 4 == 0 && g_wgrad_mfma) {
+        // tile shape by the narrow dimension: 32 x 512 (Co <= 32), 64 x 256 (Co <= 64), 256 x 64 (K <= 64),
+        // else 128 x 128
+        int rc;
+        if (Co <= 32)
+            rc = launch_wgrad_mfma<1, 1, 4>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+        else if (Co <= 64)
+            rc = launch_wgrad_mfma<1, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+        else if (K <= 64)
+            rc = launch_wgrad_mfma<4, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+        else
+            rc = launch_wgrad_mfma<2, 2, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+        if (rc) return rc;
+    } else if (Ci % 4 == 0 && Co % 4 == 0)
         hipLaunchKernelGGL(k_wgrad_v4, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo,
-                           Co, KW, stride, pad, dil, mchunk, dW);
+                           Co, KW, K, stride, pad, dil, mchunk, dW);
     else
         hipLaunchKernelGGL(k_wgrad, dim3(gx, gy, (unsigned)splits), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co,
                            KH, KW, stride, pad, dil, mchunk, dW);
@@ -434,3 +635,12 @@ int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, in
 }
 
 }  // extern "C"
+
+namespace bev {
+int train_tune(int knob, int value) {
+    if (knob != BEV_TUNE_WGRAD_MFMA || value < 0 || value > 1) return BEV_ERR_ARGS;
+    const int old = g_wgrad_mfma;
+    g_wgrad_mfma = value;
+    return old;
+}
+}  // namespace bev

@@ -1,4 +1,4 @@
-// bev_tune.h -- internal: performance knobs of the warp library (bev_warp.hip), set through
+// bev_tune.h -- internal: performance knobs of the warp (bev_warp.hip) and training (bev_train.hip) kernels, set through
 // bev_tune() (bev_conv.hip).  Results never depend on them.
 #pragma once
 
@@ -6,5 +6,8 @@ namespace bev {
 
 // knob = BEV_TUNE_WARP_* (include/bev_mi355x.h); returns the previous value or BEV_ERR_ARGS.
 int warp_tune(int knob, int value);
+
+// knob = BEV_TUNE_WGRAD_MFMA (bev_train.hip).
+int train_tune(int knob, int value);
 
 }  // namespace bev

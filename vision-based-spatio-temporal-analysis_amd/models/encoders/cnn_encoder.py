@@ -81,7 +81,7 @@ class CNNEncoder(ViewEncoder):
     def _encode_single_nhwc(self, x: torch.Tensor) -> torch.Tensor:
         """x [N,3,H,W] NCHW -> NHWC features [N,Hf,Wf,C] (cnn_encoder.py:39-48)."""
         if self._use_timm:
-            if self._trunk_frozen():  # ViewEncoder.freeze(): no trunk gradients, BN on running statistics
+            if self._trunk_frozen():  # ViewEncoder.freeze(): no trunk gradients (BN still follows train/eval)
                 with torch.no_grad():
                     feat = self.backbone.forward_features_nhwc(x, self.out_index)
             else:

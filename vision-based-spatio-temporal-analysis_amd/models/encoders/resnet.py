@@ -212,7 +212,7 @@ class ResNet(nn.Module):
 
     def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC feature map of features_only[out_index]."""
-        if self.training and torch.is_grad_enabled():
+        if self.training:  # torch semantics: train-mode BN uses batch statistics, with or without autograd
             return self._forward_train(x, out_index)
         y = self._fc(self.conv1, self.bn1)(x, relu=True, in_nchw=True)  # act1: index 0
         if out_index == 0:
