@@ -20,7 +20,8 @@ Branches exercised (timm / kornia are absent here):
   * cnn_encoder.py:31-37 fallback 2-conv encoder
   * model_wrapper.py:53-124 BEVNet forward (+ lazy proj / detector, detector.py:7-125) and loss
 
-`--only bevnet` / `--only decode` regenerate just bevnet_small.npz / decode_cases.npz.
+`--only bevnet` / `--only decode` / `--only img2world` regenerate just bevnet_small.npz / decode_cases.npz /
+img2world_cases.npz.
 """
 from __future__ import annotations
 
@@ -153,6 +154,27 @@ def homography_cases():
         out[n + "_H"] = h
     np.savez_compressed(os.path.join(HERE, "homography_cases.npz"), **out)
     print("homography_cases", len(cases))
+
+
+def img2world_cases():
+    """_compute_img_to_world_homography (geometry.py:66-78): inverse, or pinv when det is nan/inf/|det| < 1e-8,
+    on the Appendix-B rig, random calibrations, an exactly singular and a near-singular one."""
+    K7, Rt7 = bev_rig.rig(7, 1080, 1920, 1)
+    rng = np.random.default_rng(17)
+    Ks = [K7[0, v] for v in range(7)] + [rng.standard_normal((3, 3)).astype(np.float32) * 50 + np.eye(3, dtype=np.float32) * 500
+                                        for _ in range(3)]
+    Rts = [Rt7[0, v] for v in range(7)] + [rng.standard_normal((4, 4)).astype(np.float32) for _ in range(3)]
+    Ks.append(np.eye(3, dtype=np.float32))          # singular: R = I, t = 0 -> third column of [r1 r2 t] is 0
+    Rts.append(np.eye(4, dtype=np.float32))
+    near = np.eye(4, dtype=np.float32)
+    near[:3, 3] = [0.0, 0.0, 1e-9]                  # |det| ~ 1e-9 < 1e-8 -> pinv branch
+    Ks.append(np.eye(3, dtype=np.float32))
+    Rts.append(near)
+    out = {"K": np.stack(Ks), "Rt": np.stack(Rts)}
+    out["H_i2w"] = np.stack([GeometryTransformer._compute_img_to_world_homography(torch.from_numpy(k), torch.from_numpy(r)).numpy()
+                             for k, r in zip(Ks, Rts)])
+    np.savez_compressed(os.path.join(HERE, "img2world_cases.npz"), **out)
+    print("img2world_cases", len(Ks))
 
 
 def linspace_cases():
@@ -323,6 +345,9 @@ def main():
     if sys.argv[1:] == ["--only", "decode"]:
         decode_case()
         return
+    if sys.argv[1:] == ["--only", "img2world"]:
+        img2world_cases()
+        return
     meta = dict(torch=torch.__version__, cpu_capability=torch.backends.cpu.get_cpu_capability(),
                 mkl="MKL 2024.2 (default ISA dispatch on this host: avx512)",
                 recipe="SURVEY.md Appendix A (AVX-512 dot3)", reference="/root/reference @ 2025-11-14",
@@ -345,6 +370,7 @@ def main():
     # W7: C=1, tiny BEV and a feature map smaller than one tile (1x1) edge case
     warp_case("warp_w7_tiny", 1, 2, 1, 3, 5, (1080, 1920), (7, 9), 7, full=True)
     homography_cases()
+    img2world_cases()
     linspace_cases()
     fusion_cases()
     encoder_case()

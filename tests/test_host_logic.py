@@ -101,3 +101,15 @@ def test_encoder_surface_and_state_dict_names():
         e(torch.zeros(3, 32, 32))
     with pytest.raises(ValueError):
         CNNEncoder(backbone_impl="gpu")
+
+
+def test_img_to_world_homography_matches_reference_fixture():
+    """GeometryTransformer._compute_img_to_world_homography (geometry.py:66-78) vs the reference's own outputs
+    (tests/golden/img2world_cases.npz): Appendix-B rig, random calibrations, exactly singular and |det| < 1e-8
+    (pinv branch).  Inverse via LAPACK on both sides: rel 1e-5 of each matrix's scale."""
+    import numpy as np
+    from models.fusion.geometry import GeometryTransformer
+    d = np.load(os.path.join(GOLDEN, "img2world_cases.npz"))
+    for K, Rt, ref in zip(d["K"], d["Rt"], d["H_i2w"]):
+        got = GeometryTransformer._compute_img_to_world_homography(torch.from_numpy(K), torch.from_numpy(Rt)).numpy()
+        np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5 * max(np.abs(ref).max(), 1e-12))
