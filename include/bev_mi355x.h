@@ -201,6 +201,11 @@ int bev_dwconv_psum_blocks(int Ho, int Wo, int C);
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
                      int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);
 
+/* device: depthwise conv weight gradient (training): dW [K*K][C] (tap-major, like wt) =
+ * sum over n, output pixels of dz[n][p][c] * x[n][tap t of p][c]; OVERWRITTEN (float atomics inside). */
+int bev_dwconv_wgrad_f32(const float *x, int N, int H, int W, int C, const float *dz, int Ho, int Wo, int K, int stride,
+                         int pad, float *dW, void *stream);
+
 /* device: SqueezeExcite gate from the dwconv partials (timm SqueezeExcite.forward):
  *   mean = sum(psum[n]) / hw;  r = SiLU(w1 @ mean + b1);  gate[n] = sigmoid(w2 @ r + b2)
  * w1 = conv_reduce.weight [rd][C], w2 = conv_expand.weight [C][rd]. */
@@ -292,15 +297,31 @@ int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, flo
                                 const float *beta, float *running_mean, float *running_var, float *mean, float *rstd,
                                 float *scale, float *shift, void *workspace, void *stream);
 
-/* device: y = z * scale + shift (+ residual [M][C]) (+ ReLU), per channel. */
+/* device: y = act(z * scale + shift (+ residual [M][C])), per channel; act 0 none, 1 ReLU, 2 SiLU. */
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
-                            const float *residual, int relu, float *y, void *stream);
+                            const float *residual, int act, float *y, void *stream);
 
-/* device: backward of y = act(batchnorm(z) (+ residual)) given dy and the forward output y (NULL: no ReLU):
- * dz [M][C], dres [M][C] (the gradient reaching the residual; may be NULL), dgamma, dbeta [C], all OVERWRITTEN. */
+/* device: backward of y = act(batchnorm(z) (+ residual)): act 1 (ReLU) takes its mask from the forward output
+ * y, act 2 (SiLU) recomputes u = z * scale + shift; frozen = 1 for running statistics (the mean / variance are
+ * constants: dz = gamma * rstd * g).  dz [M][C], dres [M][C] (the gradient reaching the residual; may be NULL),
+ * dgamma, dbeta [C], all OVERWRITTEN. */
 int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
-                          const float *rstd, const float *gamma, float *dz, float *dres, float *dgamma, float *dbeta,
-                          void *workspace, void *stream);
+                          const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
+                          int frozen, float *dz, float *dres, float *dgamma, float *dbeta, void *workspace,
+                          void *stream);
+
+/* host: workspace bytes of bev_channel_sums_f32 (-1: C % 4 != 0 or an empty shape). */
+int64_t bev_channel_sums_workspace_bytes(int N, int64_t P, int C);
+
+/* device: per-image channel sums out[n][c] = sum_p x[n][p][c] (* x2[n][p][c] when x2 != NULL), NHWC, double
+ * partials (the SqueezeExcite squeeze of timm's SqueezeExcite.forward, and its gate gradient). */
+int bev_channel_sums_f32(const float *x, const float *x2, int N, int64_t P, int C, float *out, void *workspace,
+                         void *stream);
+
+/* device: y[n][p][c] = x[n][p][c] * a[n][c] (+ b[n][c] when b != NULL), out of place (the SE excitation and
+ * its input gradient). */
+int bev_channel_affine_f32(const float *x, int N, int64_t P, int C, const float *a, const float *b, float *y,
+                           void *stream);
 
 /* ---------------------------------------------------------------------------
  * BEVDetector.decode (detector.py:64-125) on the device: no per-pair host sync.

@@ -53,7 +53,8 @@ def resnet_features(net, x, out_index: int, grad: bool = False, act=F.relu):
 
 
 def _bn(y, bn):
-    return F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
+    return F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, bn.training,
+                        bn.momentum if bn.momentum is not None else 0.0, bn.eps)
 
 
 def _se(y, se):
@@ -67,11 +68,12 @@ def _dw(y, conv):
     return F.conv2d(y, conv.weight, None, conv.stride, conv.padding, groups=conv.groups)
 
 
-def efficientnet_features(net, x, out_index: int):
+def efficientnet_features(net, x, out_index: int, grad: bool = False):
     """features_only[out_index] of a timm-named EfficientNet `net` (timm DepthwiseSeparableConv /
-    InvertedResidual / SqueezeExcite forward, _efficientnet_blocks.py) on NCHW x."""
+    InvertedResidual / SqueezeExcite forward, _efficientnet_blocks.py) on NCHW x.  BN follows each module's
+    mode; with grad=True autograd records the graph (reference for the native trunk backward)."""
     from models.encoders.efficientnet import FEATURE_STAGE, DepthwiseSeparableConv
-    with torch.no_grad():
+    with torch.set_grad_enabled(grad):
         y = F.silu(_bn(F.conv2d(x, net.conv_stem.weight, None, 2, 1), net.bn1))
         for si in range(FEATURE_STAGE[out_index] + 1):
             for blk in net.blocks[si]:

@@ -210,9 +210,9 @@ def test_trunk_backward_vs_torch_autograd(name, bn_mode):
     import bev_native as nat
     masks, apply0 = [], nat.batchnorm_apply
 
-    def recording_apply(z, scale, shift, residual=None, relu=False):
-        out = apply0(z, scale, shift, residual, relu)
-        if relu:
+    def recording_apply(z, scale, shift, residual=None, act=0):
+        out = apply0(z, scale, shift, residual, act)
+        if act == 1:
             masks.append((out > 0).permute(0, 3, 1, 2).double().cpu())
         return out
 
@@ -365,17 +365,20 @@ def test_maxpool_bwd_vs_torch_ties(N, C, H, W):
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
 
 
-BN_CASES = [(2, 64, 13, 17, True, True), (1, 384, 9, 11, True, False), (3, 24, 7, 5, False, False),
-            (2, 512, 40, 60, True, True), (1, 4, 1, 3, False, True)]
+BN_CASES = [(2, 64, 13, 17, 1, True, False), (1, 384, 9, 11, 1, False, False), (3, 24, 7, 5, 0, False, False),
+            (2, 512, 40, 60, 1, True, False), (1, 4, 1, 3, 0, True, False), (2, 144, 11, 13, 2, False, False),
+            (1, 96, 9, 7, 2, False, True), (2, 64, 6, 9, 1, True, True)]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", BN_CASES, ids=[f"n{c[0]}c{c[1]}_{c[2]}x{c[3]}_r{int(c[4])}s{int(c[5])}" for c in BN_CASES])
+@pytest.mark.parametrize("case", BN_CASES, ids=[f"n{c[0]}c{c[1]}_{c[2]}x{c[3]}_a{c[4]}r{int(c[5])}f{int(c[6])}"
+                                                for c in BN_CASES])
 def test_batchnorm_train_kernels_vs_torch(case):
-    """bev_batchnorm_train_fwd / apply / bwd vs torch's train-mode F.batch_norm (+ residual) (+ ReLU) autograd
-    in float64: output, dz, d residual, dgamma, dbeta and the running-stat update."""
+    """bev_batchnorm_train_fwd / apply / bwd vs torch's F.batch_norm (+ residual) (+ ReLU / SiLU) autograd in
+    float64: output, dz, d residual, dgamma, dbeta and the running-stat update; "frozen" = running statistics
+    (a BN module in eval() inside a training model)."""
     import bev_native as nat
-    N, C, H, W, relu, res = case
+    N, C, H, W, act, res, frozen = case
     g = torch.Generator().manual_seed(C + H)
     z = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
     gamma = torch.rand(C, generator=g) + 0.5
@@ -387,11 +390,10 @@ def test_batchnorm_train_kernels_vs_torch(case):
     gd, bd = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
     rd = r.double().requires_grad_(True) if res else None
     rm, rv = rm0.double().clone(), rv0.double().clone()
-    ref = F.batch_norm(zd, rm, rv, gd, bd, True, 0.1, 1e-5)
+    ref = F.batch_norm(zd, rm, rv, gd, bd, not frozen, 0.1, 1e-5)
     if res:
         ref = ref + rd
-    if relu:
-        ref = torch.relu(ref)
+    ref = torch.relu(ref) if act == 1 else F.silu(ref) if act == 2 else ref
     ref.backward(dy.double())
 
     def nhwc(t):
@@ -399,9 +401,15 @@ def test_batchnorm_train_kernels_vs_torch(case):
 
     zg = nhwc(z)
     grm, grv = rm0.to(DEV), rv0.to(DEV)
-    mean, rstd, scale, shift = nat.batchnorm_train_fwd(zg, gamma.to(DEV), beta.to(DEV), grm, grv, 1e-5, 0.1)
-    y = nat.batchnorm_apply(zg, scale, shift, nhwc(r) if res else None, relu)
-    dz, dres, dgm, dbt = nat.batchnorm_bwd(nhwc(dy), y if relu else None, zg, mean, rstd, gamma.to(DEV), res)
+    if frozen:
+        mean, rstd = grm.clone(), torch.rsqrt(grv + 1e-5)
+        scale = gamma.to(DEV) * rstd
+        shift = beta.to(DEV) - mean * scale
+    else:
+        mean, rstd, scale, shift = nat.batchnorm_train_fwd(zg, gamma.to(DEV), beta.to(DEV), grm, grv, 1e-5, 0.1)
+    y = nat.batchnorm_apply(zg, scale, shift, nhwc(r) if res else None, act)
+    dz, dres, dgm, dbt = nat.batchnorm_bwd(nhwc(dy), y if act == 1 else None, zg, mean, rstd, gamma.to(DEV), res,
+                                           act, scale, shift, frozen)
 
     def chk(got, want, tol, what):
         got = got.detach().double().cpu()
@@ -412,12 +420,112 @@ def test_batchnorm_train_kernels_vs_torch(case):
         assert err < tol, (what, err)
 
     chk(y, ref, 1e-5, "y")
-    if relu:  # gradient checks need the same ReLU decisions: drop elements within rounding of 0
+    if act == 1:  # gradient checks need the same ReLU decisions: drop elements within rounding of 0
         assert int(((y.permute(0, 3, 1, 2).cpu() > 0) != (ref.detach() > 0)).sum()) == 0
     chk(dz, zd.grad, 1e-4, "dz")
     chk(dgm, gd.grad, 1e-4, "dgamma")
     chk(dbt, bd.grad, 1e-5, "dbeta")
     if res:
-        chk(dres, rd.grad, 1e-6, "dres")
+        chk(dres, rd.grad, 1e-5, "dres")
     chk(grm, rm, 1e-5, "running_mean")
     chk(grv, rv, 1e-5, "running_var")
+
+
+DW_CASES = [(2, 96, 17, 23, 3, 1), (1, 144, 20, 31, 3, 2), (2, 40, 13, 11, 5, 1), (1, 240, 18, 22, 5, 2),
+            (1, 1152, 5, 7, 3, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", DW_CASES, ids=[f"c{c[1]}_k{c[4]}s{c[5]}" for c in DW_CASES])
+def test_dwconv_wgrad_and_channel_ops_vs_torch(case):
+    """bev_dwconv_wgrad_f32 vs torch's grouped-conv weight gradient; bev_channel_sums_f32 (of x and of x * x2)
+    and bev_channel_affine_f32 vs torch (float64 references)."""
+    import bev_native as nat
+    N, C, H, W, K, s = case
+    g = torch.Generator().manual_seed(C + K)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.zeros(C, 1, K, K, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x.double(), w, stride=s, padding=K // 2, groups=C)
+    dz = torch.randn(y.shape, generator=g)
+    y.backward(dz.double())
+    dW = nat.dwconv_wgrad(x.permute(0, 2, 3, 1).contiguous().to(DEV), dz.permute(0, 2, 3, 1).contiguous().to(DEV),
+                          K, s, K // 2)
+    got = dW.t().reshape(C, 1, K, K).double().cpu()
+    assert (got - w.grad).abs().max().item() <= 1e-4 * w.grad.abs().max().item()
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x2 = torch.randn(N, H, W, C, generator=g)
+    sums = nat.channel_sums(xn).double().cpu()
+    assert (sums - x.double().sum((2, 3))).abs().max().item() <= 1e-5 * x.abs().sum((2, 3)).max().item()
+    prod = nat.channel_sums(xn, x2.to(DEV)).double().cpu()
+    want = (x.permute(0, 2, 3, 1).double() * x2.double()).sum((1, 2))
+    assert (prod - want).abs().max().item() <= 1e-5 * (x.permute(0, 2, 3, 1) * x2).abs().sum((1, 2)).max().item()
+    a, b = torch.randn(N, C, generator=g), torch.randn(N, C, generator=g)
+    aff = nat.channel_affine(xn, a.to(DEV), b.to(DEV)).cpu()
+    assert torch.equal(aff, x.permute(0, 2, 3, 1) * a[:, None, None, :] + b[:, None, None, :])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("bn_mode", ["batch", "frozen"])
+@pytest.mark.parametrize("name", ["efficientnet_b0", "efficientnet_b3"])
+def test_effnet_trunk_backward_vs_torch_autograd(name, bn_mode):
+    """Native EfficientNet training path (stem / pointwise conv + BN + SiLU, depthwise conv, SqueezeExcite,
+    skip) vs float64 torch autograd of the timm graph on the same weights: every trunk parameter's gradient
+    and the running-stat updates.  SiLU is smooth, so no activation decision can flip: rel 1e-3."""
+    import backbone_ref
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(1)
+    enc = CNNEncoder(out_channels=16, backbone=name, pretrained=False)
+    g = torch.Generator().manual_seed(5)
+    for m in enc.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m.running_mean.copy_(torch.rand(m.num_features, generator=g) * 0.4 - 0.2)
+            m.running_var.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.weight.data.copy_(torch.rand(m.num_features, generator=g) + 0.5)
+            m.bias.data.copy_(torch.rand(m.num_features, generator=g) * 0.4 - 0.2)
+    imgs = torch.randn(1, 2, 3, 64, 96, generator=g)
+    with torch.no_grad():
+        enc.eval().to(DEV)(imgs.to(DEV))  # builds the lazy proj
+    enc.train()
+    if bn_mode == "frozen":
+        for m in enc.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+    stats0 = {k: b.detach().cpu().clone() for k, b in enc.named_buffers() if "running" in k}
+    y = enc(imgs.to(DEV))
+    r = torch.randn(y.shape, generator=g)
+    (y * r.to(DEV)).sum().backward()
+    got = {k: p.grad.detach().cpu() for k, p in enc.named_parameters() if p.grad is not None}
+    stats1 = {k: b.detach().cpu().clone() for k, b in enc.named_buffers() if "running" in k}
+    enc_c = enc.to("cpu").double()
+    enc_c.zero_grad(set_to_none=True)
+    with torch.no_grad():
+        for k, b in enc_c.named_buffers():
+            if k in stats0:
+                b.copy_(stats0[k])
+    f = backbone_ref.efficientnet_features(enc_c.backbone, imgs.double().reshape(-1, 3, 64, 96), enc_c.out_index,
+                                           grad=True)
+    yc = F.conv2d(f, enc_c.proj.weight, enc_c.proj.bias)
+    fwd = (y.detach().cpu().double() - yc.detach().reshape(y.shape)).abs().max() / yc.abs().max()
+    assert float(fwd) < 1e-4, float(fwd)
+    (yc.reshape(y.shape) * r.double()).sum().backward()
+    # The bias of a projection BN (no activation) whose output feeds a conv + batch-statistics BN has an
+    # (exactly) vanishing gradient apart from the skip path -- the next BN removes any per-channel shift -- so
+    # each error is taken relative to max(its own scale, 1e-4 of the largest parameter gradient: fp32 leaves a
+    # ~1e-7 residue of the cancelled part).
+    floor = 1e-4 * max(p.grad.abs().max().item() for p in enc_c.parameters() if p.grad is not None)
+    errs = {}
+    for k, p in enc_c.named_parameters():
+        if p.grad is None:
+            assert k not in got, k
+            continue
+        assert k in got, k
+        errs[k] = (got[k].double() - p.grad).abs().max().item() / max(p.grad.abs().max().item(), floor)
+    assert len(errs) > 30
+    assert max(errs.values()) < 1e-3, sorted(errs.items(), key=lambda t: -t[1])[:6]
+    moved = 0
+    for k, b in enc_c.named_buffers():
+        if k in stats1:
+            assert (stats1[k].double() - b).abs().max().item() <= 1e-4 * max(b.abs().max().item(), 1e-12), k
+            moved += int(not torch.equal(stats1[k], stats0[k]))
+    assert (moved > 0) == (bn_mode == "batch")

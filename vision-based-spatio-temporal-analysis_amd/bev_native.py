@@ -17,7 +17,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -70,7 +70,12 @@ SIGNATURES = {
     "bev_batchnorm_workspace_bytes": (_i64, [_i64, _i]),
     "bev_batchnorm_train_fwd_f32": (_i, [_vp, _i64, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_batchnorm_apply_f32": (_i, [_vp, _i64, _i, _vp, _vp, _vp, _i, _vp, _vp]),
-    "bev_batchnorm_bwd_f32": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "bev_batchnorm_bwd_f32": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp,
+                                   _vp, _vp]),
+    "bev_channel_sums_workspace_bytes": (_i64, [_i, _i64, _i]),
+    "bev_channel_sums_f32": (_i, [_vp, _vp, _i, _i64, _i, _vp, _vp, _vp]),
+    "bev_channel_affine_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _vp, _vp]),
+    "bev_dwconv_wgrad_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_groupnorm_fwd_f32": (_i, [_vp, _i, _i64, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_groupnorm_apply_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _i, _vp, _vp]),
     "bev_groupnorm_bwd_f32": (_i, [_vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
@@ -644,7 +649,8 @@ def batchnorm_train_fwd(z: torch.Tensor, gamma, beta, running_mean, running_var,
     return mean, rstd, scale, shift
 
 
-def batchnorm_apply(z: torch.Tensor, scale, shift, residual=None, relu: bool = False) -> torch.Tensor:
+def batchnorm_apply(z: torch.Tensor, scale, shift, residual=None, act: int = 0) -> torch.Tensor:
+    """y = act(z * scale + shift (+ residual)), act 0 none / 1 ReLU / 2 SiLU (ACT_*)."""
     _require_gpu(z, scale, shift, residual)
     assert z.is_contiguous()
     if residual is not None:
@@ -653,14 +659,16 @@ def batchnorm_apply(z: torch.Tensor, scale, shift, residual=None, relu: bool = F
     C = z.shape[-1]
     y = torch.empty_like(z)
     _check(lib().bev_batchnorm_apply_f32(_ptr(z), z.numel() // C, C, _ptr(scale), _ptr(shift), _ptr(residual),
-                                         int(relu), _ptr(y), _stream(z)), "bev_batchnorm_apply_f32")
+                                         int(act), _ptr(y), _stream(z)), "bev_batchnorm_apply_f32")
     return y
 
 
-def batchnorm_bwd(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_dres: bool):
-    """-> (dz, dres or None, dgamma, dbeta) of y = relu?(batchnorm(z) (+ res)); y None means no ReLU."""
+def batchnorm_bwd(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_dres: bool, act: int = 1,
+                  scale=None, shift=None, frozen: bool = False):
+    """-> (dz, dres or None, dgamma, dbeta) of y = act(batchnorm(z) (+ res)).  act 1 needs the forward output y,
+    act 2 (SiLU) the forward's scale / shift; frozen: running statistics (no batch-statistic terms)."""
     dy = dy.contiguous()
-    _require_gpu(dy, y, z, mean, rstd, gamma)
+    _require_gpu(dy, y, z, mean, rstd, gamma, scale, shift)
     C = z.shape[-1]
     M = z.numel() // C
     dz = torch.empty_like(z)
@@ -669,6 +677,52 @@ def batchnorm_bwd(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_
     db = torch.empty(C, device=z.device)
     ws = _bn_workspace(M, C, z.device)
     _check(lib().bev_batchnorm_bwd_f32(_ptr(dy), _ptr(y), _ptr(z), M, C, _ptr(mean), _ptr(rstd),
-                                       _ptr(gamma.detach().contiguous()), _ptr(dz), _ptr(dres), _ptr(dg), _ptr(db),
-                                       _ptr(ws), _stream(z)), "bev_batchnorm_bwd_f32")
+                                       _ptr(gamma.detach().contiguous()), _ptr(scale), _ptr(shift), int(act),
+                                       int(frozen), _ptr(dz), _ptr(dres), _ptr(dg), _ptr(db), _ptr(ws), _stream(z)),
+           "bev_batchnorm_bwd_f32")
     return dz, dres, dg, db
+
+
+# ---------------------------------------------------------------------------
+# SqueezeExcite / depthwise training helpers (EfficientNet trunk)
+# ---------------------------------------------------------------------------
+def channel_sums(x: torch.Tensor, x2: torch.Tensor = None) -> torch.Tensor:
+    """x (and x2) [N, H, W, C] NHWC -> [N, C] per-image channel sums of x (* x2)."""
+    x = x.contiguous()
+    x2 = x2.contiguous() if x2 is not None else None
+    _require_gpu(x, x2)
+    N, C = x.shape[0], x.shape[-1]
+    P = x.numel() // (N * C)
+    nbytes = lib().bev_channel_sums_workspace_bytes(N, P, C)
+    if nbytes < 0:
+        raise HipError(f"channel_sums shape not supported: {tuple(x.shape)}")
+    ws = torch.empty((nbytes + 7) // 8, device=x.device, dtype=torch.float64)
+    out = torch.empty(N, C, device=x.device)
+    _check(lib().bev_channel_sums_f32(_ptr(x), _ptr(x2), N, P, C, _ptr(out), _ptr(ws), _stream(x)),
+           "bev_channel_sums_f32")
+    return out
+
+
+def channel_affine(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor:
+    """y[n, ..., c] = x[n, ..., c] * a[n, c] (+ b[n, c]) for NHWC x, out of place."""
+    x = x.contiguous()
+    a = a.contiguous()
+    b = b.contiguous() if b is not None else None
+    _require_gpu(x, a, b)
+    N, C = x.shape[0], x.shape[-1]
+    y = torch.empty_like(x)
+    _check(lib().bev_channel_affine_f32(_ptr(x), N, x.numel() // (N * C), C, _ptr(a), _ptr(b), _ptr(y), _stream(x)),
+           "bev_channel_affine_f32")
+    return y
+
+
+def dwconv_wgrad(x: torch.Tensor, dz: torch.Tensor, K: int, stride: int, pad: int) -> torch.Tensor:
+    """Depthwise weight gradient: x [N,H,W,C], dz [N,Ho,Wo,C] -> dW [K*K, C] (tap-major)."""
+    x, dz = x.contiguous(), dz.contiguous()
+    _require_gpu(x, dz)
+    N, H, W, C = x.shape
+    _, Ho, Wo, _ = dz.shape
+    dW = torch.empty(K * K, C, device=x.device)
+    _check(lib().bev_dwconv_wgrad_f32(_ptr(x), N, H, W, C, _ptr(dz), Ho, Wo, K, stride, pad, _ptr(dW), _stream(x)),
+           "bev_dwconv_wgrad_f32")
+    return dW

@@ -5,11 +5,17 @@
 //             k_bn_finalize        mean, biased var, rstd = 1/sqrt(var + eps), scale = gamma*rstd,
 //                                  shift = beta - mean*scale; running_mean / running_var updated with
 //                                  the momentum rule and the unbiased variance (torch's train-mode BN)
-//             k_bn_apply           y = act(z*scale + shift (+ residual))   (float4)
-//   backward  k_bn_partial<Grads>  per channel (sum g, sum g*xhat), g = dy * (y > 0 if relu), xhat =
-//                                  (z - mean) * rstd
+//             k_bn_apply           y = act(z*scale + shift (+ residual)), act = none / ReLU / SiLU (float4)
+//   backward  k_bn_partial<Grads>  per channel (sum g, sum g*xhat), g = dy * act'(u) (ReLU: y > 0 from the
+//                                  saved output; SiLU: u = z*scale + shift recomputed), xhat = (z - mean) * rstd
 //             k_bn_bwd_finalize    k1 = sum g / M, k2 = sum g xhat / M, dbeta, dgamma
 //             k_bn_bwd_apply       dz = gamma * rstd * (g - k1 - xhat * k2); d(residual) = g
+//   A BN module in eval() inside a training model ("frozen": running statistics) uses the same apply and
+//   backward with k1 = k2 = 0 (its statistics are constants).
+//
+// Per-image channel sums (the SqueezeExcite squeeze and its backward, EfficientNet training):
+//             k_img_partial / k_img_finalize   out[n][c] = sum_p x[n][p][c] (* x2[n][p][c])
+//             k_chan_affine                     y[n][p][c] = x[n][p][c] * a[n][c] (+ b[n][c])
 //
 // The partials are one per (row block, channel): deterministic, no float atomics.  Every pass is a
 // streaming read of the activation (HBM-bound; a few us per trunk layer at BEV-rig sizes).
@@ -33,17 +39,38 @@ struct Stats {  // (z, z^2)
     }
 };
 
+// SiLU' (u) = s (1 + u (1 - s)), s = sigmoid(u) = 1 / (1 + exp(-u)) (torch's SiLU backward)
+__device__ __forceinline__ float silu_grad(float u) {
+    const float sg = 1.0f / (1.0f + expf(-u));
+    return sg * (1.0f + u * (1.0f - sg));
+}
+
+// g = dy * act'(u) for the 4 channels c .. c+3 of element i (act 1: y > 0; act 2: u = z * scale + shift)
+__device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const float *y, const float4 v,
+                                         const float *scale, const float *shift, int act, int64_t i, int c) {
+    g[0] = d.x;
+    g[1] = d.y;
+    g[2] = d.z;
+    g[3] = d.w;
+    if (act == 1) {
+        const float4 o = *(const float4 *)(y + i);
+        const float ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
+    } else if (act == 2) {
+        const float zv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] *= silu_grad(zv[u] * scale[c + u] + shift[c + u]);
+    }
+}
+
 struct Grads {  // (g, g * xhat)
-    const float *dy, *y, *z, *mean, *rstd;
+    const float *dy, *y, *z, *mean, *rstd, *scale, *shift;
+    int act;
     __device__ void at(int64_t i, int c, float4 &a, float4 &b) const {
         const float4 d = *(const float4 *)(dy + i), v = *(const float4 *)(z + i);
-        float g[4] = {d.x, d.y, d.z, d.w};
-        if (y) {
-            const float4 o = *(const float4 *)(y + i);
-            const float ov[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
-        }
+        float g[4];
+        act_grad(g, d, y, v, scale, shift, act, i, c);
         const float zv[4] = {v.x, v.y, v.z, v.w};
         float h[4];
 #pragma unroll
@@ -55,7 +82,7 @@ struct Grads {  // (g, g * xhat)
 
 // grid (row blocks, channel slices of BN_QB quads); part [nb][C][2]
 template <class F>
-__global__ __launch_bounds__(BN_T) void k_bn_partial(F f, int64_t M, int C, double *__restrict__ part) {
+__device__ __forceinline__ void k_bn_partial_body(const F &f, int64_t M, int C, double *__restrict__ part) {
     __shared__ double red[BN_T][4][2];
     const int C4 = C / 4, tid = threadIdx.x, blk = blockIdx.x;
     const int qb = C4 < BN_QB ? C4 : BN_QB;  // quads handled per block
@@ -90,6 +117,11 @@ __global__ __launch_bounds__(BN_T) void k_bn_partial(F f, int64_t M, int C, doub
             o[1] = b;
         }
     }
+}
+
+template <class F>
+__global__ __launch_bounds__(BN_T) void k_bn_partial(F f, int64_t M, int C, double *__restrict__ part) {
+    k_bn_partial_body(f, M, C, part);
 }
 
 // Column sums of part [nb][C][2] for 16 channels per block: 16 row-block phases per channel, LDS reduce.
@@ -145,7 +177,7 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize(const double *__r
 // IT: uint32_t when the element count fits (no 64-bit divisions in the channel decode), else int64_t
 template <typename IT>
 __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__restrict__ scale,
-                           const float *__restrict__ shift, const float *__restrict__ res, int relu,
+                           const float *__restrict__ shift, const float *__restrict__ res, int act,
                            float *__restrict__ y, IT total4) {
     const IT C4 = (IT)(C / 4);
     for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
@@ -158,14 +190,17 @@ __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__re
             const float4 r = *(const float4 *)(res + e);
             o = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
         }
-        if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+        if (act == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+        if (act == 2)  // torch SiLU: x / (1 + exp(-x))
+            o = make_float4(o.x / (1.0f + expf(-o.x)), o.y / (1.0f + expf(-o.y)), o.z / (1.0f + expf(-o.z)),
+                            o.w / (1.0f + expf(-o.w)));
         *(float4 *)(y + e) = o;
     }
 }
 
 // coef [C][2] = (sum g / M, sum g xhat / M)
 __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_bwd_finalize(const double *__restrict__ part, int nb, int64_t M,
-                                                                    int C, float *__restrict__ coef,
+                                                                    int C, int frozen, float *__restrict__ coef,
                                                                     float *__restrict__ dgamma,
                                                                     float *__restrict__ dbeta) {
     double a, b;
@@ -173,27 +208,23 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_bwd_finalize(const double 
     const int c = blockIdx.x * FIN_C + threadIdx.x;
     dbeta[c] = (float)a;
     dgamma[c] = (float)b;
-    coef[2 * c] = (float)(a / (double)M);
-    coef[2 * c + 1] = (float)(b / (double)M);
+    coef[2 * c] = frozen ? 0.f : (float)(a / (double)M);
+    coef[2 * c + 1] = frozen ? 0.f : (float)(b / (double)M);
 }
 
 template <typename IT>
 __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__restrict__ y, const float *__restrict__ z,
                                int C, const float *__restrict__ mean, const float *__restrict__ rstd,
-                               const float *__restrict__ gamma, const float *__restrict__ coef, float *__restrict__ dz,
-                               float *__restrict__ dres, IT total4) {
+                               const float *__restrict__ gamma, const float *__restrict__ scale,
+                               const float *__restrict__ shift, int act, const float *__restrict__ coef,
+                               float *__restrict__ dz, float *__restrict__ dres, IT total4) {
     const IT C4 = (IT)(C / 4);
     for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
         const int64_t e = 4 * (int64_t)i;
         const int c0 = 4 * (int)(i % C4);
         const float4 d = *(const float4 *)(dy + e), v = *(const float4 *)(z + e);
-        float g[4] = {d.x, d.y, d.z, d.w};
-        if (y) {
-            const float4 o = *(const float4 *)(y + e);
-            const float ov[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
-        }
+        float g[4];
+        act_grad(g, d, y, v, scale, shift, act, e, c0);
         const float zv[4] = {v.x, v.y, v.z, v.w};
         float o[4];
 #pragma unroll
@@ -204,6 +235,55 @@ __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__rest
         }
         *(float4 *)(dz + e) = make_float4(o[0], o[1], o[2], o[3]);
         if (dres) *(float4 *)(dres + e) = make_float4(g[0], g[1], g[2], g[3]);
+    }
+}
+
+
+// ---- per-image channel sums and channel affine (SqueezeExcite training) -------------------------------
+struct Prod {  // (x * x2, unused)
+    const float *x, *x2;
+    __device__ void at(int64_t i, int, float4 &a, float4 &b) const {
+        const float4 v = *(const float4 *)(x + i);
+        if (x2) {
+            const float4 w = *(const float4 *)(x2 + i);
+            a = make_float4(v.x * w.x, v.y * w.y, v.z * w.z, v.w * w.w);
+        } else {
+            a = v;
+        }
+        b = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+};
+
+// grid (row blocks, channel slices, images): image n's rows are [n P, (n+1) P); part [N][nb][C][2]
+__global__ __launch_bounds__(BN_T) void k_img_partial(Prod f, int64_t P, int C, double *__restrict__ part) {
+    const int n = blockIdx.z;
+    const int64_t off = (int64_t)n * P * C;
+    Prod g{f.x + off, f.x2 ? f.x2 + off : nullptr};
+    k_bn_partial_body(g, P, C, part + (size_t)n * gridDim.x * C * 2);
+}
+
+__global__ __launch_bounds__(FIN_C * FIN_P) void k_img_finalize(const double *__restrict__ part, int nb, int C,
+                                                               float *__restrict__ out) {
+    const int n = blockIdx.y;
+    double a, b;
+    if (!fin_sums(part + (size_t)n * nb * C * 2, nb, C, a, b)) return;
+    out[(size_t)n * C + blockIdx.x * FIN_C + threadIdx.x] = (float)a;
+}
+
+template <typename IT>
+__global__ void k_chan_affine(const float *__restrict__ x, int C, IT P4, const float *__restrict__ a,
+                              const float *__restrict__ b, float *__restrict__ y, IT total4) {
+    const IT C4 = (IT)(C / 4);
+    for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
+        const int64_t e = 4 * (int64_t)i;
+        const int64_t nc = (int64_t)(i / P4) * C + 4 * (int64_t)(i % C4);  // image n = i / (P * C4)
+        const float4 v = *(const float4 *)(x + e), s = *(const float4 *)(a + nc);
+        float4 o = make_float4(v.x * s.x, v.y * s.y, v.z * s.z, v.w * s.w);
+        if (b) {
+            const float4 t = *(const float4 *)(b + nc);
+            o = make_float4(o.x + t.x, o.y + t.y, o.z + t.z, o.w + t.w);
+        }
+        *(float4 *)(y + e) = o;
     }
 }
 
@@ -241,38 +321,72 @@ int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, flo
 }
 
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
-                            const float *residual, int relu, float *y, void *stream) {
-    if (!z || !scale || !shift || !y || !bn_shape_ok(M, C)) return BEV_ERR_ARGS;
+                            const float *residual, int act, float *y, void *stream) {
+    if (!z || !scale || !shift || !y || !bn_shape_ok(M, C) || act < 0 || act > 2) return BEV_ERR_ARGS;
     const int64_t total4 = M * C / 4;
     if (total4 < ((int64_t)1 << 32) - 65536 * 256)
         hipLaunchKernelGGL(k_bn_apply<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C,
-                           scale, shift, residual, relu, y, (uint32_t)total4);
+                           scale, shift, residual, act, y, (uint32_t)total4);
     else
         hipLaunchKernelGGL(k_bn_apply<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C,
-                           scale, shift, residual, relu, y, total4);
+                           scale, shift, residual, act, y, total4);
     return (int)hipGetLastError();
 }
 
 int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
-                          const float *rstd, const float *gamma, float *dz, float *dres, float *dgamma, float *dbeta,
-                          void *workspace, void *stream) {
-    if (!dy || !z || !mean || !rstd || !gamma || !dz || !dgamma || !dbeta || !workspace || !bn_shape_ok(M, C))
+                          const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
+                          int frozen, float *dz, float *dres, float *dgamma, float *dbeta, void *workspace,
+                          void *stream) {
+    if (!dy || !z || !mean || !rstd || !gamma || !dz || !dgamma || !dbeta || !workspace || !bn_shape_ok(M, C) ||
+        act < 0 || act > 2 || (act == 1 && !y) || (act == 2 && (!scale || !shift)))
         return BEV_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;
     const int nb = row_blocks(M);
     double *part = (double *)workspace;
     float *coef = (float *)(part + (size_t)nb * C * 2);
     const dim3 grid(nb, (C / 4 + BN_QB - 1) / BN_QB);
-    hipLaunchKernelGGL(k_bn_partial<Grads>, grid, dim3(BN_T), 0, st, Grads{dy, y, z, mean, rstd}, M, C, part);
+    hipLaunchKernelGGL(k_bn_partial<Grads>, grid, dim3(BN_T), 0, st, Grads{dy, y, z, mean, rstd, scale, shift, act}, M, C, part);
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st, part, nb, M, C,
-                       coef, dgamma, dbeta);
+                       frozen, coef, dgamma, dbeta);
     const int64_t total4 = M * C / 4;
     if (total4 < ((int64_t)1 << 32) - 65536 * 256)
         hipLaunchKernelGGL(k_bn_bwd_apply<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean,
-                           rstd, gamma, coef, dz, dres, (uint32_t)total4);
+                           rstd, gamma, scale, shift, act, coef, dz, dres, (uint32_t)total4);
     else
         hipLaunchKernelGGL(k_bn_bwd_apply<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean,
-                           rstd, gamma, coef, dz, dres, total4);
+                           rstd, gamma, scale, shift, act, coef, dz, dres, total4);
+    return (int)hipGetLastError();
+}
+
+int64_t bev_channel_sums_workspace_bytes(int N, int64_t P, int C) {
+    if (N <= 0 || !bn_shape_ok(P, C)) return -1;
+    return (int64_t)N * row_blocks(P) * C * 2 * (int64_t)sizeof(double);
+}
+
+int bev_channel_sums_f32(const float *x, const float *x2, int N, int64_t P, int C, float *out, void *workspace,
+                         void *stream) {
+    if (!x || !out || !workspace || N <= 0 || N > 65535 || !bn_shape_ok(P, C)) return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    const int nb = row_blocks(P);
+    double *part = (double *)workspace;
+    hipLaunchKernelGGL(k_img_partial, dim3(nb, (C / 4 + BN_QB - 1) / BN_QB, N), dim3(BN_T), 0, st, Prod{x, x2}, P, C,
+                       part);
+    hipLaunchKernelGGL(k_img_finalize, dim3((C + FIN_C - 1) / FIN_C, N), dim3(FIN_C * FIN_P), 0, st, part, nb, C, out);
+    return (int)hipGetLastError();
+}
+
+int bev_channel_affine_f32(const float *x, int N, int64_t P, int C, const float *a, const float *b, float *y,
+                           void *stream) {
+    if (!x || !a || !y || N <= 0 || P <= 0 || C <= 0 || C % 4 != 0 ||
+        (((uintptr_t)x | (uintptr_t)a | (uintptr_t)b | (uintptr_t)y) & 15) != 0)
+        return BEV_ERR_ARGS;
+    const int64_t total4 = (int64_t)N * P * C / 4, P4 = P * (C / 4);
+    if (total4 < ((int64_t)1 << 32) - 65536 * 256)
+        hipLaunchKernelGGL(k_chan_affine<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, x,
+                           C, (uint32_t)P4, a, b, y, (uint32_t)total4);
+    else
+        hipLaunchKernelGGL(k_chan_affine<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, x, C,
+                           P4, a, b, y, total4);
     return (int)hipGetLastError();
 }
 

@@ -15,6 +15,9 @@
 //   k_se_gate     per image: mean = sum(partials) / (Ho*Wo), conv_reduce +
 //                 SiLU, conv_expand + sigmoid -> gate [N][C].
 //   k_chan_scale  x[n, p, c] *= gate[n, c] in place (the SE excitation).
+//   k_dw_wgrad    training: depthwise weight gradient dW[t][c] = sum_{n,p} dz[n,p,c] x[n, tap t of p, c], the
+//                 k_dwconv thread layout with K*K float4 accumulators per thread, reduced over the workgroup's
+//                 pixel lanes in LDS and added to dW with float atomics (one per workgroup, tap and channel).
 //
 // All three are HBM-bound streaming kernels (bytes per output element: the
 // input taps come from L1/L2 after the first touch, so ~4 B in + 4 B out).
@@ -172,6 +175,72 @@ __global__ __launch_bounds__(256) void k_chan_scale(float *__restrict__ y, int64
     }
 }
 
+
+template <int K>
+__global__ __launch_bounds__(DW_NT) void k_dw_wgrad(const float *__restrict__ x, int H, int W, int C,
+                                                    const float *__restrict__ dz, int stride, int pad, int Ho, int Wo,
+                                                    int ppb, float *__restrict__ dW) {
+    __shared__ float4 red[DW_NT];
+    const int C4 = C >> 2;
+    const int CH4 = C4 <= DW_NT ? C4 : DW_NT / 2;
+    const int PB = DW_NT / CH4;
+    const int tid = threadIdx.x;
+    const int pl = tid / CH4, c4 = blockIdx.z * CH4 + (tid - pl * CH4);
+    const bool active = pl < PB && c4 < C4;
+    const int n = blockIdx.y, blk = blockIdx.x;
+    const int64_t HWo = (int64_t)Ho * Wo;
+    const int64_t p0 = (int64_t)blk * ppb, p1 = min(p0 + ppb, HWo);
+    float4 acc[K * K];
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) acc[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (active) {
+        const float *xn = x + (int64_t)n * H * W * C + c4 * 4;
+        const float *dn = dz + (int64_t)n * HWo * C + c4 * 4;
+        for (int64_t p = p0 + pl; p < p1; p += PB) {
+            const int oy = (int)(p / Wo), ox = (int)(p - (int64_t)oy * Wo);
+            const int iy0 = oy * stride - pad, ix0 = ox * stride - pad;
+            const float4 g = *(const float4 *)(dn + p * C);
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) {
+                const int iy = iy0 + ky;
+                if (iy < 0 || iy >= H) continue;
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const int ix = ix0 + kx;
+                    if (ix < 0 || ix >= W) continue;
+                    const float4 v = *(const float4 *)(xn + ((int64_t)iy * W + ix) * C);
+                    float4 &a = acc[ky * K + kx];
+                    a.x = __builtin_fmaf(g.x, v.x, a.x);
+                    a.y = __builtin_fmaf(g.y, v.y, a.y);
+                    a.z = __builtin_fmaf(g.z, v.z, a.z);
+                    a.w = __builtin_fmaf(g.w, v.w, a.w);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) {
+        red[tid] = acc[t];
+        __syncthreads();
+        if (pl == 0 && c4 < C4) {
+            float4 s = acc[t];
+            for (int q = 1; q < PB; ++q) {
+                const float4 u = red[q * CH4 + tid];
+                s.x += u.x;
+                s.y += u.y;
+                s.z += u.z;
+                s.w += u.w;
+            }
+            float *o = dW + (int64_t)t * C + c4 * 4;
+            atomicAdd(o, s.x);
+            atomicAdd(o + 1, s.y);
+            atomicAdd(o + 2, s.z);
+            atomicAdd(o + 3, s.w);
+        }
+        __syncthreads();
+    }
+}
+
 inline int last() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -230,6 +299,27 @@ int bev_channel_scale_f32(float *y, int N, int64_t P, int C, const float *gate, 
     const int64_t blocks = (total4 + 255) / 256 < 256 * 64 ? (total4 + 255) / 256 : 256 * 64;
     hipLaunchKernelGGL(k_chan_scale, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, y, P, C, gate,
                        total4);
+    return last();
+}
+
+int bev_dwconv_wgrad_f32(const float *x, int N, int H, int W, int C, const float *dz, int Ho, int Wo, int K, int stride,
+                         int pad, float *dW, void *stream) {
+    if (!x || !dz || !dW || N < 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || stride <= 0 || pad < 0)
+        return BEV_ERR_ARGS;
+    if (K != 3 && K != 5) return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - K) / stride + 1 || Wo != (W + 2 * pad - K) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)dz | (uintptr_t)dW) & 15) != 0) return BEV_ERR_ARGS;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(dW, 0, (size_t)K * K * C * sizeof(float), st) != hipSuccess) return last();
+    if (N == 0) return 0;
+    const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
+    const int C4 = C / 4, CH4 = dw_ch4(C);
+    dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
+    if (K == 3)
+        hipLaunchKernelGGL(k_dw_wgrad<3>, grid, dim3(DW_NT), 0, st, x, H, W, C, dz, stride, pad, Ho, Wo, ppb, dW);
+    else
+        hipLaunchKernelGGL(k_dw_wgrad<5>, grid, dim3(DW_NT), 0, st, x, H, W, C, dz, stride, pad, Ho, Wo, ppb, dW);
     return last();
 }
 

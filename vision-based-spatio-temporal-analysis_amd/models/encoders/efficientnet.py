@@ -23,6 +23,9 @@ act=2), the depthwise convs are `bev_dwconv2d_f32` (BN folded, SiLU, SE
 squeeze partials fused), the SE gate is `bev_se_gate_f32`, and the excitation
 `x * gate` is applied inside the projection conv's operand load (`bev_conv2d_chscale_f32`), which also adds
 the skip in its epilogue.
+
+Training (model.train()): the same graph on autograd nodes with native backward kernels (trunk_grad.py:
+ConvBNTrain with SiLU, DWConvBNTrain, SqueezeExcite); BN with batch statistics.
 """
 from __future__ import annotations
 
@@ -174,16 +177,45 @@ class EfficientNet(nn.Module):
 
     def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC features_only[out_index]."""
-        if self.training and torch.is_grad_enabled():
-            raise NotImplementedError("native EfficientNet executes eval-mode (folded BN) inference only")
         if out_index not in FEATURE_STAGE:
             raise IndexError(f"efficientnet feature index {out_index} out of range 0..4")
+        if self.training:  # torch semantics: train-mode BN uses batch statistics, with or without autograd
+            return self._forward_train(x, out_index)
         y = self._fc(self.conv_stem, self.bn1)(x, relu=_nat.ACT_SILU, in_nchw=True)
         with torch.no_grad():
             for si in range(FEATURE_STAGE[out_index] + 1):
                 for blk in self.blocks[si]:
                     y = self._block(blk, y)
         return y
+
+    def _forward_train(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
+        """Training (model.train()): every conv + BN (+ SiLU) (+ skip), depthwise conv and SqueezeExcite is one
+        autograd node on the native forward / backward kernels; BN with batch statistics (or running statistics
+        for BN modules in eval()), like timm's trunk in the reference's train.py:222."""
+        from .trunk_grad import ConvBNTrain
+        y = ConvBNTrain.apply(x, self.conv_stem.weight, self.bn1.weight, self.bn1.bias, self.conv_stem, self.bn1, 2,
+                              True, None)
+        for si in range(FEATURE_STAGE[out_index] + 1):
+            for blk in self.blocks[si]:
+                y = _train_block(blk, y)
+        return y
+
+
+def _train_block(blk, y):
+    """timm DepthwiseSeparableConv / InvertedResidual forward on the training autograd nodes (trunk_grad)."""
+    from .trunk_grad import ConvBNTrain, DWConvBNTrain, SqueezeExcite
+    se = blk.se
+    res = y if blk.has_skip else None
+    if isinstance(blk, DepthwiseSeparableConv):
+        h = DWConvBNTrain.apply(y, blk.conv_dw.weight, blk.bn1.weight, blk.bn1.bias, blk.conv_dw, blk.bn1, 2)
+        h = SqueezeExcite.apply(h, se.conv_reduce.weight, se.conv_reduce.bias, se.conv_expand.weight,
+                                se.conv_expand.bias)
+        return ConvBNTrain.apply(h, blk.conv_pw.weight, blk.bn2.weight, blk.bn2.bias, blk.conv_pw, blk.bn2, 0, False,
+                                 res)
+    h = ConvBNTrain.apply(y, blk.conv_pw.weight, blk.bn1.weight, blk.bn1.bias, blk.conv_pw, blk.bn1, 2, False, None)
+    h = DWConvBNTrain.apply(h, blk.conv_dw.weight, blk.bn2.weight, blk.bn2.bias, blk.conv_dw, blk.bn2, 2)
+    h = SqueezeExcite.apply(h, se.conv_reduce.weight, se.conv_reduce.bias, se.conv_expand.weight, se.conv_expand.bias)
+    return ConvBNTrain.apply(h, blk.conv_pwl.weight, blk.bn3.weight, blk.bn3.bias, blk.conv_pwl, blk.bn3, 0, False, res)
 
 
 def efficientnet_b0():

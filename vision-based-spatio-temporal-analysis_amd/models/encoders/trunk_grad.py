@@ -33,7 +33,8 @@ import torch.nn as nn
 
 import bev_native as _nat
 
-__all__ = ["ConvBNAct", "ConvBNTrain", "ConvAct", "MaxPool", "conv_bn_act", "conv_act"]
+__all__ = ["ConvBNAct", "ConvBNTrain", "DWConvBNTrain", "SqueezeExcite", "ConvAct", "MaxPool", "conv_bn_act",
+           "conv_act"]
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -91,32 +92,48 @@ class ConvBNAct(torch.autograd.Function):
         return dx, dw, dgamma, dbf, None, None, None, None, (dz if has_res else None)
 
 
-class ConvBNTrain(torch.autograd.Function):
-    """act(BN_batch(conv(x, W)) (+ residual)) with batch statistics (train-mode BatchNorm2d)."""
-
-    @staticmethod
-    def forward(ctx, x, weight, gamma, beta, conv, bn, relu: bool, in_nchw: bool, residual):
-        k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
-        w = weight.detach().float().contiguous()
-        Co = conv.out_channels
-        z = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(w), torch.zeros(Co, device=x.device), Co, k, k, st, p, False,
-                             in_nchw=in_nchw)
+def _bn_affine(bn: nn.BatchNorm2d, z: torch.Tensor, gamma, beta):
+    """(mean, rstd, scale, shift, frozen) of BN over NHWC z: batch statistics (+ running-stat update) when the
+    module is training, its running statistics (constants) when it is in eval()."""
+    if bn.training:
         track = bn.track_running_stats and bn.running_mean is not None
         if track:
             bn.num_batches_tracked.add_(1)
         momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
         mean, rstd, scale, shift = _nat.batchnorm_train_fwd(z, gamma, beta, bn.running_mean if track else None,
                                                             bn.running_var if track else None, bn.eps, momentum)
-        y = _nat.batchnorm_apply(z, scale, shift, residual, relu)
-        ctx.save_for_backward(x, z, y if relu else None, w, mean, rstd, gamma)
-        ctx.meta = (k, st, p, in_nchw, residual is not None)
+        return mean, rstd, scale, shift, False
+    with torch.no_grad():
+        mean = bn.running_mean.detach().float().contiguous()
+        rstd = torch.rsqrt(bn.running_var.detach().float() + bn.eps)
+        scale = (gamma.detach().float() * rstd).contiguous()
+        shift = (beta.detach().float() - mean * scale).contiguous()
+    return mean, rstd, scale, shift, True
+
+
+class ConvBNTrain(torch.autograd.Function):
+    """act(BN(conv(x, W)) (+ residual)), act 0 none / 1 ReLU / 2 SiLU; BN with batch statistics (train-mode
+    BatchNorm2d) or, for a BN module in eval(), its running statistics."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, conv, bn, act: int, in_nchw: bool, residual):
+        k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        w = weight.detach().float().contiguous()
+        Co = conv.out_channels
+        z = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(w), torch.zeros(Co, device=x.device), Co, k, k, st, p, False,
+                             in_nchw=in_nchw)
+        mean, rstd, scale, shift, frozen = _bn_affine(bn, z, gamma, beta)
+        y = _nat.batchnorm_apply(z, scale, shift, residual, act)
+        ctx.save_for_backward(x, z, y if act == 1 else None, w, mean, rstd, gamma, scale, shift)
+        ctx.meta = (k, st, p, in_nchw, residual is not None, int(act), frozen)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, z, y, w, mean, rstd, gamma = ctx.saved_tensors
-        k, st, p, in_nchw, has_res = ctx.meta
-        dz, dres, dgamma, dbeta = _nat.batchnorm_bwd(dy.float(), y, z, mean, rstd, gamma, has_res)
+        x, z, y, w, mean, rstd, gamma, scale, shift = ctx.saved_tensors
+        k, st, p, in_nchw, has_res, act, frozen = ctx.meta
+        dz, dres, dgamma, dbeta = _nat.batchnorm_bwd(dy.float(), y, z, mean, rstd, gamma, has_res, act, scale, shift,
+                                                     frozen)
         xn = _nat.nchw_to_nhwc(x) if in_nchw else x
         H, W = xn.shape[1], xn.shape[2]
         dx = _dgrad(dz, w, H, W, st, p) if (ctx.needs_input_grad[0] and not in_nchw) else None
@@ -124,10 +141,82 @@ class ConvBNTrain(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, None, None, None, None, dres
 
 
+class DWConvBNTrain(torch.autograd.Function):
+    """act(BN(depthwise_conv(x, W))) for the EfficientNet trunk (timm conv_dw -> bn -> SiLU), NHWC.
+    Forward: bev_dwconv2d_f32 (raw, no bias), BatchNorm kernels.  Backward: BN backward, dgrad = depthwise
+    conv of the (zero-inserted) gradient with the flipped taps, wgrad = bev_dwconv_wgrad_f32."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, conv, bn, act: int):
+        C, K, st, p = conv.out_channels, conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        wt = weight.detach().float().reshape(C, K * K).t().contiguous()  # [K*K, C] tap-major
+        zero = torch.zeros(C, device=x.device)
+        z, _ = _nat.dwconv2d_nhwc(x, wt, zero, K, st, p, _nat.ACT_NONE)
+        mean, rstd, scale, shift, frozen = _bn_affine(bn, z, gamma, beta)
+        y = _nat.batchnorm_apply(z, scale, shift, None, act)
+        ctx.save_for_backward(x, z, y if act == 1 else None, wt, mean, rstd, gamma, scale, shift)
+        ctx.meta = (K, st, p, int(act), frozen)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, y, wt, mean, rstd, gamma, scale, shift = ctx.saved_tensors
+        K, st, p, act, frozen = ctx.meta
+        dz, _, dgamma, dbeta = _nat.batchnorm_bwd(dy.float(), y, z, mean, rstd, gamma, False, act, scale, shift,
+                                                  frozen)
+        N, H, W, C = x.shape
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wf = wt.view(K, K, C).flip(0, 1).reshape(K * K, C).contiguous()
+            zero = torch.zeros(C, device=x.device)
+            q = K - 1 - p
+            if st == 1:
+                dx, _ = _nat.dwconv2d_nhwc(dz, wf, zero, K, 1, q, _nat.ACT_NONE)
+            else:
+                Ho, Wo = dz.shape[1], dz.shape[2]
+                ry, rx = (H + 2 * p - K) % st, (W + 2 * p - K) % st
+                Hd, Wd = st * (Ho - 1) + 1 + 2 * q + ry, st * (Wo - 1) + 1 + 2 * q + rx
+                dx, _ = _nat.dwconv2d_nhwc(_nat.dilate_nhwc(dz, st, q, q, Hd, Wd), wf, zero, K, 1, 0, _nat.ACT_NONE)
+        dW = _nat.dwconv_wgrad(x, dz, K, st, p).t().reshape(C, 1, K, K)
+        return dx, dW, dgamma, dbeta, None, None, None
+
+
+class SqueezeExcite(torch.autograd.Function):
+    """timm SqueezeExcite: y * sigmoid(expand(silu(reduce(mean_hw(y))))) over NHWC y.  The big-tensor work is
+    native (per-image channel sums, the excitation as a channel affine); the [N, C] MLP is parameter-sized."""
+
+    @staticmethod
+    def _gate(s, w1, b1, w2, b2):
+        r = torch.nn.functional.silu(s @ w1.reshape(w1.shape[0], -1).t() + b1)
+        return torch.sigmoid(r @ w2.reshape(w2.shape[0], -1).t() + b2)
+
+    @staticmethod
+    def forward(ctx, y, w1, b1, w2, b2):
+        P = y.shape[1] * y.shape[2]
+        s = _nat.channel_sums(y) / P
+        g = SqueezeExcite._gate(s, w1.detach(), b1.detach(), w2.detach(), b2.detach()).contiguous()
+        ctx.save_for_backward(y, s, g, w1, b1, w2, b2)
+        return _nat.channel_affine(y, g)
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, s, g, w1, b1, w2, b2 = ctx.saved_tensors
+        P = y.shape[1] * y.shape[2]
+        dout = dout.contiguous().float()
+        dg = _nat.channel_sums(dout, y)  # d gate = sum_p dout * y
+        leaves = [t.detach().requires_grad_(True) for t in (s, w1, b1, w2, b2)]
+        with torch.enable_grad():
+            gate = SqueezeExcite._gate(*leaves)
+            ds, dw1, db1, dw2, db2 = torch.autograd.grad(gate, leaves, dg)
+        dy = _nat.channel_affine(dout, g, ds / P)  # dout * gate + d mean / P (broadcast over pixels)
+        return dy, dw1, db1, dw2, db2
+
+
 def conv_bn_act(conv: nn.Conv2d, bn: nn.BatchNorm2d, x, relu: bool, residual=None, in_nchw: bool = False):
-    """One trunk layer in training: batch-statistics BN when `bn.training`, else the folded frozen BN."""
-    fn = ConvBNTrain if bn.training else ConvBNAct
-    return fn.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, relu, in_nchw, residual)
+    """One ResNet layer in training: batch-statistics BN when `bn.training`, else the folded frozen BN."""
+    if bn.training:
+        return ConvBNTrain.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, 1 if relu else 0, in_nchw, residual)
+    return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, relu, in_nchw, residual)
 
 
 class ConvAct(torch.autograd.Function):
