@@ -346,6 +346,13 @@ int bev_decode_nms_f32(const int32_t *cand_idx, const float *cand_score, const i
 /* host: the largest candidate count per frame bev_decode_nms_f32 handles. */
 int bev_decode_max_candidates(void);
 
+/* Camera-image ingest (data/transforms.py:12-19 T.ToTensor + T.Normalize, applied per image in
+ * data/wildtrack_loader.py:368-374): src [N][H][W][3] uint8 RGB (device) -> out [N][3][H][W]
+ * fp32, out = (float(src) / 255 - mean[c]) / std[c] with torch's rounding (bit-exact).
+ * mean, std: host float[3]. */
+int bev_image_normalize_u8_f32(const uint8_t *src, int N, int H, int W, const float *mean, const float *std,
+                               float *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

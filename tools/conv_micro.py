@@ -95,14 +95,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("layers", nargs="*", default=list(LAYERS) + list(DUAL))
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--tiles", type=int, nargs="*", default=[0], help="BEV_TUNE_CONV_TILE values to A/B")
+    ap.add_argument("--knob", default="CONV_TILE", help="bev_tune knob to A/B (TUNE_<name>)")
+    ap.add_argument("--values", type=int, nargs="*", default=[0], help="knob values, interleaved per round")
     a = ap.parse_args()
+    knob = getattr(nat, "TUNE_" + a.knob)
     for rnd in range(2):  # interleaved rounds, same process
-        for t in a.tiles:
-            nat.tune(nat.TUNE_CONV_TILE, t)
-            print(f"-- round {rnd} tile {t}")
+        for v in a.values:
+            old = nat.tune(knob, v)
+            print(f"-- round {rnd} {a.knob}={v}")
             for name in a.layers:
                 (run_dual if name in DUAL else run)(name, a.iters)
+            nat.tune(knob, old)
 
 
 if __name__ == "__main__":

@@ -78,6 +78,7 @@ SIGNATURES = {
     "bev_dwconv_wgrad_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_groupnorm_fwd_f32": (_i, [_vp, _i, _i64, _i, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_groupnorm_apply_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _i, _vp, _vp]),
+    "bev_image_normalize_u8_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_groupnorm_bwd_f32": (_i, [_vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
 }
 
@@ -726,3 +727,20 @@ def dwconv_wgrad(x: torch.Tensor, dz: torch.Tensor, K: int, stride: int, pad: in
     _check(lib().bev_dwconv_wgrad_f32(_ptr(x), N, H, W, C, _ptr(dz), Ho, Wo, K, stride, pad, _ptr(dW), _stream(x)),
            "bev_dwconv_wgrad_f32")
     return dW
+
+
+def image_normalize_u8(src: torch.Tensor, mean, std, out: torch.Tensor = None) -> torch.Tensor:
+    """[N, H, W, 3] uint8 RGB on the GPU -> [N, 3, H, W] fp32 (ToTensor + Normalize, bit-exact)."""
+    if not src.is_cuda:
+        raise HipError("image_normalize_u8 needs a ROCm device tensor (got a CPU tensor); no CPU fallback")
+    if src.dtype != torch.uint8 or src.dim() != 4 or src.shape[3] != 3:
+        raise ValueError(f"image_normalize_u8 expects [N, H, W, 3] uint8, got {tuple(src.shape)} {src.dtype}")
+    src = src.contiguous()
+    N, H, W, _ = src.shape
+    if out is None:
+        out = torch.empty(N, 3, H, W, device=src.device, dtype=torch.float32)
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    _check(lib().bev_image_normalize_u8_f32(_ptr(src), N, H, W, m, s, _ptr(out), _stream(src)),
+           "bev_image_normalize_u8_f32")
+    return out
