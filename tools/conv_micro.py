@@ -32,6 +32,7 @@ LAYERS = {
     "l2.1.c2": (128, 128, 3, 1, 135, 240, False, False),
     "l2.1.c3": (128, 512, 1, 1, 135, 240, True, False),
     "proj": (512, 64, 1, 1, 135, 240, False, False),
+    "g512": (512, 512, 1, 1, 135, 240, False, False),  # plain GEMM shape (M 226800 x N 512 x K 512): loop ceiling
 }
 # fused bottleneck tails (bev_conv2d_dual_f32): name: (Ci conv3 in, Ci2 block in, Co, s2, H2, W2)
 DUAL = {
@@ -93,13 +94,14 @@ def run(name, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("layers", nargs="*", default=list(LAYERS) + list(DUAL))
+    ap.add_argument("layers", nargs="*", default=[k for k in LAYERS if k != "g512"] + list(DUAL))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--knob", default="CONV_TILE", help="bev_tune knob to A/B (TUNE_<name>)")
     ap.add_argument("--values", type=int, nargs="*", default=[0], help="knob values, interleaved per round")
+    ap.add_argument("--rounds", type=int, default=2)
     a = ap.parse_args()
     knob = getattr(nat, "TUNE_" + a.knob)
-    for rnd in range(2):  # interleaved rounds, same process
+    for rnd in range(a.rounds):  # interleaved rounds, same process
         for v in a.values:
             old = nat.tune(knob, v)
             print(f"-- round {rnd} {a.knob}={v}")

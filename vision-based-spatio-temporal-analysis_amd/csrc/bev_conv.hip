@@ -38,6 +38,11 @@ constexpr int LROW = BK + 4;  // LDS row stride in floats (144 B: 9 slots, odd -
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector: promotes to VGPRs reliably
 
+// 16 zero bytes in device memory: out-of-range operand taps load from here (an unconditional load
+// through a selected pointer), so the K loop has no branches around loads and hipcc's vmcnt
+// bookkeeping stays exact (a select on the loaded VALUE gets sunk into a branch around the load).
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
+
 __host__ __device__ inline int64_t kpad(int K) { return (K + BK - 1) / BK * BK; }
 __host__ __device__ inline int64_t copad(int Co) { return (Co + 127) / 128 * 128; }
 
@@ -124,7 +129,8 @@ struct RowsA {
 // A loader, fast path: NHWC, Ci % 32 == 0 -> a K step is one (ky, kx) and 32
 // consecutive channels, i.e. one contiguous 128-B run per output pixel.  The
 // (ky, kx, ci0) position advances incrementally (no divisions in the loop).
-template <int ROWS>
+// SCALE: multiply by the per-(image, channel) ascale (SE excitation; LOADER 6).
+template <int ROWS, bool SCALE = false>
 struct LoaderFast {
     static constexpr int NV = ROWS;  // float4 per thread and K step
     RowsA<ROWS> rows;
@@ -144,12 +150,12 @@ struct LoaderFast {
         for (int r = 0; r < ROWS; ++r) {
             const int iy = rows.iy0[r] + ky, ix = rows.ix0[r] + kx;
             const bool in = rows.ok[r] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            v[r] = in ? *(const f32x4 *)(a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4)
-                      : (f32x4){0.f, 0.f, 0.f, 0.f};
-            if (a.ascale && !rows.uni && in)
+            const float *src = in ? a.x + rows.pix[r] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + quad * 4 : g_zero4;
+            v[r] = *(const f32x4 *)src;
+            if (SCALE && !rows.uni && in)
                 v[r] *= *(const f32x4 *)(a.ascale + (int64_t)rows.img[r] * a.Ci + ci0 + quad * 4);
         }
-        if (a.ascale && rows.uni) {
+        if (SCALE && rows.uni) {
             const f32x4 g = *(const f32x4 *)(a.ascale + (int64_t)rows.img[0] * a.Ci + ci0 + quad * 4);
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) v[r] *= g;  // out-of-range rows are 0 and stay 0
@@ -249,7 +255,7 @@ struct LoaderDual {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const int64_t off = (first ? p1[r] : p2[r]) + quad * 4;
-            v[r] = ok[r] ? *(const f32x4 *)(src + off) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            v[r] = *(const f32x4 *)(ok[r] ? src + off : g_zero4);
         }
     }
     __device__ void advance(const ConvArgs &) { k0 += BK; }
@@ -365,7 +371,8 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
 
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
 // LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1,
-// 4 contiguous 1x1 (NHWC, Ci % 4 == 0), 5 fast + dilation + GroupNorm/ReLU operand affine
+// 4 contiguous 1x1 (NHWC, Ci % 4 == 0), 5 fast + dilation + GroupNorm/ReLU operand affine,
+// 6 fast + per-(image, channel) operand scale
 // NBUF: LDS staging buffers.  2 = one barrier per K step; 1 = half the LDS (a
 // third workgroup per CU for the <= 170-VGPR tiles) at two barriers per K step.
 template <int WM, int WN, int TM, int TN, int LOADER, int NBUF>
@@ -394,12 +401,13 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     const int n0 = (bid % n_tiles) * BN;
 
     typename std::conditional<
-        LOADER == 1, LoaderFast<AROWS>, typename std::conditional<LOADER == 5, LoaderFastEx<AROWS>,
+        LOADER == 1, LoaderFast<AROWS>, typename std::conditional<LOADER == 6, LoaderFast<AROWS, true>,
+        typename std::conditional<LOADER == 5, LoaderFastEx<AROWS>,
         typename std::conditional<LOADER == 2, LoaderRow<BM, 3, 7>,
                                   typename std::conditional<
                                       LOADER == 3, LoaderDual<AROWS>,
                                       typename std::conditional<LOADER == 4, LoaderContig<AROWS>,
-                                                                LoaderRow<BM>>::type>::type>::type>::type>::type la;
+                                                                LoaderRow<BM>>::type>::type>::type>::type>::type>::type la;
     la.init(a, m0, tid);
     const int bq = tid & 7;
     const float *wrow = a.wp + (int64_t)(n0 + (tid >> 3)) * a.Kp + bq * 4;
@@ -410,10 +418,10 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
 
-    // global -> register prefetch, TWO K steps ahead (helpers, not lambdas: register
+    // global -> register prefetch, TWO K steps ahead (macros, not lambdas: register
     // arrays captured by reference were address-taken and landed in scratch).
-    // Step ks: registers set 0 receive step ks+2 while the MFMAs consume LDS
-    // buffer ks&1; set 1 (step ks+1) is then written to the other LDS buffer.
+    // Step ks: register set ks&1 receives step ks+2 while the MFMAs consume LDS
+    // buffer ks&1; the other set (step ks+1) is then written to the other LDS buffer.
     constexpr int NV = decltype(la)::NV;
     f32x4 va0[NV], va1[NV], rb0[BROWS], rb1[BROWS];
     int kb = 0;  // k offset of the B panel
@@ -424,10 +432,10 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
         la.advance(a);                        \
         kb += BK;                             \
     } while (0)
-#define BEV_SWRITE(buf, VA, RB)                                                               \
-    do {                                                                                      \
-        la.store(lds + (buf) * STAGE, tid, VA);                                               \
-        store_rows<BROWS>(lds + (buf) * STAGE + (BM + (tid >> 3)) * LROW + bq * 4, RB);       \
+#define BEV_SWRITE(buf, VA, RB)                                                                        \
+    do {                                                                                               \
+        la.store(lds + (NBUF == 2 ? (buf) : 0) * STAGE, tid, VA);                                      \
+        store_rows<BROWS>(lds + (NBUF == 2 ? (buf) : 0) * STAGE + (BM + (tid >> 3)) * LROW + bq * 4, RB); \
     } while (0)
 
     const int nk = a.Kp / BK;
@@ -436,54 +444,71 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     BEV_SWRITE(0, va0, rb0);
     __syncthreads();
     const int r32 = lane & 31, h = lane >> 5;
-    for (int ks = 0; ks < nk; ++ks) {
-        const int cur = ks & 1;
-        const bool pre2 = ks + 2 < nk;
-        if (pre2) BEV_GLOAD(va0, rb0);
-        const float *As = lds + (NBUF == 2 ? cur : 0) * STAGE;
-        const float *Bs = As + BM * LROW;
-        // MFMA k-slot h of step p reads k = 16 h + p (p = 0..15): per half of the
-        // step each lane reads two contiguous float4 of its row per operand tile.
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            f32x4 fa[TM][2], fb[TN][2];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const float *pa = As + (wm * TM * 32 + i * 32 + r32) * LROW + h * 16 + half * 8;
-                fa[i][0] = *(const f32x4 *)pa;
-                fa[i][1] = *(const f32x4 *)(pa + 4);
-            }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const float *pb = Bs + (wn * TN * 32 + j * 32 + r32) * LROW + h * 16 + half * 8;
-                fb[j][0] = *(const f32x4 *)pb;
-                fb[j][1] = *(const f32x4 *)(pb + 4);
-            }
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const float av = fa[i][p >> 2][p & 3];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const float bv = fb[j][p >> 2][p & 3];
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
-                    }
-                }
-            }
-        }
-        if (ks + 1 < nk) {
-            if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
-            BEV_SWRITE(NBUF == 2 ? (cur ^ 1) : 0, va1, rb1);
-            __syncthreads();
-        }
-        if (pre2) {
-#pragma unroll
-            for (int q = 0; q < NV; ++q) va1[q] = va0[q];
-#pragma unroll
-            for (int q = 0; q < BROWS; ++q) rb1[q] = rb0[q];
-        }
+    // MFMAs of one K step from LDS buffer BUF.  MFMA k-slot h of step p reads k = 16 h + p
+    // (p = 0..15): per half of the step each lane reads two contiguous float4 of its row per tile.
+#define BEV_MFMA_STEP(BUF)                                                                           \
+    do {                                                                                             \
+        const float *As = lds + (NBUF == 2 ? (BUF) : 0) * STAGE;                                     \
+        const float *Bs = As + BM * LROW;                                                            \
+        _Pragma("unroll") for (int half = 0; half < 2; ++half) {                                     \
+            f32x4 fa[TM][2], fb[TN][2];                                                              \
+            _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                         \
+                const float *pa = As + (wm * TM * 32 + i * 32 + r32) * LROW + h * 16 + half * 8;     \
+                fa[i][0] = *(const f32x4 *)pa;                                                       \
+                fa[i][1] = *(const f32x4 *)(pa + 4);                                                 \
+            }                                                                                        \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                         \
+                const float *pb = Bs + (wn * TN * 32 + j * 32 + r32) * LROW + h * 16 + half * 8;     \
+                fb[j][0] = *(const f32x4 *)pb;                                                       \
+                fb[j][1] = *(const f32x4 *)(pb + 4);                                                 \
+            }                                                                                        \
+            _Pragma("unroll") for (int p = 0; p < 8; ++p) {                                          \
+                _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                     \
+                    const float av = fa[i][p >> 2][p & 3];                                           \
+                    _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                 \
+                        const float bv = fb[j][p >> 2][p & 3];                                       \
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0); \
+                    }                                                                                \
+                }                                                                                    \
+            }                                                                                        \
+        }                                                                                            \
+    } while (0)
+    // Two K steps per trip with the register sets in ping-pong (no copies), so the loads of step
+    // ks + 2 stay in flight across step ks + 1 and are waited for only when written to LDS.  The
+    // loop body issues its loads unconditionally (the last steps are peeled off below): with no
+    // path that skips a load, hipcc's waitcnt pass keeps the counted vmcnt for the older set.
+#define BEV_SYNC_WRITE(BUF, VA, RB)                                      \
+    do {                                                                 \
+        if (NBUF == 1) __syncthreads(); /* single buffer: reads done */ \
+        BEV_SWRITE(BUF, VA, RB);                                         \
+        __syncthreads();                                                 \
+    } while (0)
+    int ks = 0;
+    for (; ks + 3 < nk; ks += 2) {
+        BEV_GLOAD(va0, rb0);  // step ks + 2 -> set 0
+        BEV_MFMA_STEP(0);
+        BEV_SYNC_WRITE(1, va1, rb1);  // step ks + 1
+        BEV_GLOAD(va1, rb1);  // step ks + 3 -> set 1
+        BEV_MFMA_STEP(1);
+        BEV_SYNC_WRITE(0, va0, rb0);  // step ks + 2
     }
+    // 1, 2 or 3 steps left (set 1 holds step ks + 1 when it exists)
+    if (ks + 2 < nk) {
+        BEV_GLOAD(va0, rb0);  // step ks + 2
+        BEV_MFMA_STEP(0);
+        BEV_SYNC_WRITE(1, va1, rb1);
+        BEV_MFMA_STEP(1);
+        BEV_SYNC_WRITE(0, va0, rb0);
+        BEV_MFMA_STEP(0);
+    } else if (ks + 1 < nk) {
+        BEV_MFMA_STEP(0);
+        BEV_SYNC_WRITE(1, va1, rb1);
+        BEV_MFMA_STEP(1);
+    } else {
+        BEV_MFMA_STEP(0);
+    }
+#undef BEV_SYNC_WRITE
+#undef BEV_MFMA_STEP
 #undef BEV_GLOAD
 #undef BEV_SWRITE
 
@@ -810,6 +835,7 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3, NBUF>), g, b, 0, st, a);
     else if (loader == 4) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 4, NBUF>), g, b, 0, st, a);
     else if (loader == 5) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 5, NBUF>), g, b, 0, st, a);
+    else if (loader == 6) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 6, NBUF>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 0, NBUF>), g, b, 0, st, a);
     return last();
 }
@@ -856,7 +882,7 @@ int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
         // 32 x 32 MFMA tile per wave, ~4 resident blocks per CU) trades operand reuse for memory
         // parallelism.  r01f A/B over ResNet-50: every such layer -1..-19 % (proj 209 -> 170 us,
         // layer1 conv1 400 -> 352 us); 3x3 layers and the dual-source tails are slower with it.
-        if (a.KH == 1 && a.KW == 1 && loader == 1 && M >= 200000) tile = 4;
+        if (a.KH == 1 && a.KW == 1 && (loader == 1 || loader == 6) && M >= 200000) tile = 4;
     }
     if (tile == 2)
         return nbuf1_for(2) ? launch_conv<4, 1, 1, 2, 1>(a, loader, st) : launch_conv<4, 1, 1, 2>(a, loader, st);
@@ -972,6 +998,7 @@ static int conv2d_impl(const float *x, int in_nchw, int N, int H, int W, int Ci,
                     ((uintptr_t)x & 15) == 0;
     int loader = (!in_nchw && Ci % BK == 0) ? 1 : (in_nchw && Ci == 3 && KH == 7 && KW == 7) ? 2 : pw ? 4 : 0;
     if (loader == 1 && (ashift || arelu || dil != 1)) loader = 5;
+    else if (loader == 1 && ascale) loader = 6;
     if ((ashift || arelu) && loader != 5) return BEV_ERR_ARGS;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
