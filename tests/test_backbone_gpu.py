@@ -26,6 +26,7 @@ CASES = [
     # N, Ci, H, W, Co, K, stride, pad, nchw_in, residual, relu
     (2, 3, 37, 53, 64, 7, 2, 3, True, False, True),    # stem (k_stem: LDS patch, even/odd planes)
     (1, 3, 45, 301, 24, 7, 2, 3, True, False, False),  # stem, ragged Co / partial tiles, no relu
+    (2, 3, 541, 963, 64, 7, 2, 3, True, False, True),  # stem, > 2 tiles per persistent workgroup, odd edges
     (1, 16, 20, 30, 24, 3, 2, 1, False, False, True),   # fallback encoder 2nd conv
     (2, 64, 17, 23, 64, 3, 1, 1, False, True, True),    # layer1 3x3 + residual
     (2, 64, 17, 23, 256, 1, 1, 0, False, True, True),   # 1x1 expand + residual
@@ -150,3 +151,21 @@ def test_resnet_encoder_vs_torch_fp32(name):
     assert tuple(y.shape) == tuple(ref.shape) == (1, 3, 64, 12, 20)
     err = (y - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-4, err
+
+
+@pytest.mark.parametrize("groups,offset", [(2, 0), (3, 0), (2, 1), (3, 3)])
+def test_resnet_stream_groups_bit_exact(groups, offset):
+    """Inference split over image groups on separate streams == one stream, bit for bit (same kernels,
+    same per-element accumulation order), including an uneven split and the output written in place."""
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(1)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(DEV)
+    imgs = _rand((1, 5, 3, 90, 150), 9).to(DEV)
+    with torch.no_grad():
+        ref = enc(imgs).clone()
+        enc.backbone.stream_groups, enc.backbone.stream_offset = groups, offset
+        got = enc(imgs)
+        torch.cuda.synchronize()
+        enc.backbone.stream_groups, enc.backbone.stream_offset = 1, 0
+    assert got.shape == ref.shape
+    assert torch.equal(got.contiguous().view(torch.int32), ref.contiguous().view(torch.int32))

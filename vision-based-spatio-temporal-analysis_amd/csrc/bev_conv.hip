@@ -589,28 +589,33 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
 // ResNet stem: 7x7 / stride 2 / pad 3 over Ci = 3 NCHW images, Co <= 64
 // ---------------------------------------------------------------------------
 // timm conv1 (cnn_encoder.py:26 backbone; first layer of CNNEncoder._encode_single).
-// Persistent workgroups; one output tile = 2 rows x 64 columns x Co channels,
-// wave w owns 32 pixels (row w >> 1, columns 32 (w & 1) ..) x all channels
-// (2 MFMA tiles of 32 x 32).  The tile's input patch (3 ch x 9 rows x 134
-// cols) is read ONCE with coalesced row loads and kept in LDS as even / odd
-// column planes: with stride 2, tap kx of output column ox reads column
-// 2 ox + kx, i.e. plane (kx & 1) at index ox + kx / 2, so the two k-slots of
-// one v_mfma_f32_32x32x2_f32 are the taps (kx = 2a, kx = 2a + 1) of one
-// (ci, ky) and every A operand is a conflict-free ds_read_b32 at a
-// compile-time offset (84 MFMA k-pairs: 3 ci x 7 ky x 4 a; kx = 7 has zero
-// weight).  The next tile's patch is fetched into registers during the MFMAs
-// (double-buffered LDS).  Weights are re-laid out into LDS once per workgroup
-// from the standard packed panel.
+// Persistent workgroups; one output tile = 4 rows x 64 columns x Co channels, wave w owns
+// output row w (2 x 2 MFMA tiles of 32 pixels x 32 channels, 64 accumulators).  The tile's
+// input patch (3 ch x 13 rows x 133 cols) is read once with coalesced row loads and kept in
+// LDS as even / odd column planes: with stride 2, tap kx of output column ox reads column
+// 2 ox + kx, i.e. plane (kx & 1) at index ox + kx / 2, so every A operand is a conflict-free
+// ds_read_b32 at a per-(tap, k-slot) constant offset.  The 147 taps t = (ci * 7 + ky) * 7 + kx
+// are packed densely into 74 MFMA k-pairs (k-slot h of pair q is tap 2 q + h; the one padding
+// slot has zero weight), 12 % fewer MFMAs than pairing (kx, kx + 1) within a row.  The next
+// tile's patch is fetched into registers during the MFMAs and written to the single LDS patch
+// buffer between two barriers, so weights (39 KiB) + patch (24 KiB) leave room for two
+// workgroups per CU.  Weights are re-laid out into LDS once per workgroup from the packed panel.
 namespace stem {
-constexpr int TW = 64, TH = 2;
-constexpr int PR = 2 * TH + 5;                     // 9 input rows
-constexpr int PC = 2 * TW + 6;                     // 134 input columns (incl. the kx = 7 pad column)
+constexpr int TW = 64, TH = 4;
+constexpr int PR = 2 * TH + 5;                     // 13 input rows
+constexpr int PC = 2 * TW + 5;                     // 133 input columns
 constexpr int PP = 80;                             // plane pitch: 67 used; = 16 mod 32 -> conflict-free stores
 constexpr int RP = 2 * PP, CP = PR * RP, PATCH = 3 * CP;
-constexpr int NQ = 3 * 7 * 4;                      // k pairs
-constexpr int WP = 2 * NQ + 4;                     // weight row pitch (172 floats = 43 odd 16-B slots)
+constexpr int NT = 147;                            // taps
+constexpr int NQ = (NT + 1) / 2;                   // 74 k pairs
+constexpr int NQP = 76;                            // per-k-slot weight run (multiple of 4)
+constexpr int WP = 2 * NQP + 4;                    // weight row pitch (156 floats = 39 odd 16-B slots)
 constexpr int NE = 3 * PR * PC;                    // patch elements
-constexpr int PER_T = (NE + 255) / 256;            // per thread (15)
+constexpr int PER_T = (NE + 255) / 256;            // per thread (21)
+// LDS offset of tap t relative to (output row 0, output column 0) of the patch
+__host__ __device__ constexpr int tap_off(int t) {
+    return (t / 49) * CP + ((t % 49) / 7) * RP + ((t % 7) & 1) * PP + ((t % 7) >> 1);
+}
 }  // namespace stem
 
 struct StemArgs {
@@ -637,7 +642,8 @@ __device__ __forceinline__ void stem_fetch(const StemArgs &a, int64_t t, int tid
         const int ci = cr / PR, r = cr - ci * PR;
         const int gy = row0 + r, gx = col0 + c;
         const bool in = e < NE && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
-        pv[i] = in ? xi[((int64_t)ci * a.H + gy) * a.W + gx] : 0.0f;
+        // unconditional load through a selected pointer (no branch around the load)
+        pv[i] = *(in ? xi + ((int64_t)ci * a.H + gy) * a.W + gx : (const float *)g_zero4);
     }
 }
 
@@ -656,77 +662,89 @@ __device__ __forceinline__ void stem_put(float *pl, int tid, const float (&pv)[s
 
 __global__ __launch_bounds__(256, 2) void k_stem(StemArgs a) {
     using namespace stem;
-    __shared__ __attribute__((aligned(16))) float wl[64 * WP];
-    __shared__ __attribute__((aligned(16))) float pl[2 * PATCH];
+    __shared__ __attribute__((aligned(16))) float lds[64 * WP + PATCH];
+    float *wl = lds, *pl = lds + 64 * WP;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
 
-    // weights: wl[n][h * NQ + q] = W[n][ci][ky][kx = 2 a + h], q = (ci * 7 + ky) * 4 + a
-    for (int e = tid; e < 64 * 2 * NQ; e += 256) {
-        const int n = e / (2 * NQ), hq = e - n * (2 * NQ), hh = hq / NQ, q = hq - hh * NQ;
-        const int ci = q / 28, ky = (q % 28) / 4, kx = 2 * (q % 4) + hh;
+    // weights: wl[n][h * NQP + q] = W[n][tap 2 q + h]; packed k = (ky * 7 + kx) * 3 + ci
+    for (int e = tid; e < 64 * 2 * NQP; e += 256) {
+        const int n = e / (2 * NQP), hq = e - n * (2 * NQP), hh = hq / NQP, q = hq - hh * NQP;
+        const int tp = 2 * q + hh;
         float v = 0.0f;
-        if (n < a.Co && kx < 7) v = a.wp[(int64_t)n * a.Kp + (ky * 7 + kx) * 3 + ci];
+        if (n < a.Co && tp < NT) {
+            const int ci = tp / 49, ky = (tp % 49) / 7, kx = tp % 7;
+            v = a.wp[(int64_t)n * a.Kp + (ky * 7 + kx) * 3 + ci];
+        }
         wl[n * WP + hq] = v;
     }
     float pv[PER_T];
     int64_t t = blockIdx.x;
-    if (t < a.ntiles) {
-        stem_fetch(a, t, tid, pv);
-        stem_put(pl, tid, pv);
-    }
+    stem_fetch(a, t < a.ntiles ? t : 0, tid, pv);
+    stem_put(pl, tid, pv);
     __syncthreads();
 
-    const int ol = wave >> 1, oxl = 32 * (wave & 1) + r32;
-    const int abase = ol * 2 * RP + oxl + h * PP;  // + ci*CP + ky*RP + a per k pair
-    const float *wb0 = wl + r32 * WP + h * NQ, *wb1 = wl + (32 + r32) * WP + h * NQ;
+    const float *P = pl + wave * 2 * RP + r32;  // output row `wave`, column r32 (+ 32 for the second M tile)
+    const float *wb0 = wl + r32 * WP + h * NQP, *wb1 = wl + (32 + r32) * WP + h * NQP;
     const float b0 = (r32 < a.Co) ? a.bias[r32] : 0.0f;
     const float b1 = (32 + r32 < a.Co) ? a.bias[32 + r32] : 0.0f;
-    int buf = 0;
     for (; t < a.ntiles; t += gridDim.x) {
         const int64_t tn = t + gridDim.x;
-        if (tn < a.ntiles) stem_fetch(a, tn, tid, pv);  // in flight during the MFMAs
-        const float *P = pl + buf * PATCH + abase;
-        f32x16 acc0 = (f32x16){0}, acc1 = (f32x16){0};
+        stem_fetch(a, tn < a.ntiles ? tn : t, tid, pv);  // in flight during the MFMAs
+        f32x16 acc00 = (f32x16){0}, acc01 = (f32x16){0}, acc10 = (f32x16){0}, acc11 = (f32x16){0};
+        int hv = h;
+        asm volatile("" : "+v"(hv));  // per-tile opaque: the 74 per-pair lane offsets are not hoisted into VGPRs
 #pragma unroll
         for (int q4 = 0; q4 < NQ; q4 += 4) {
             const f32x4 w0 = *(const f32x4 *)(wb0 + q4), w1 = *(const f32x4 *)(wb1 + q4);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int q = q4 + u, ci = q / 28, ky = (q % 28) / 4, aa = q % 4;
-                const float av = P[ci * CP + ky * RP + aa];
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w0[u], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w1[u], acc1, 0, 0, 0);
+                const int q = q4 + u;
+                if (q >= NQ) break;
+                // k-slot h reads tap 2 q + h (the padding slot 147 re-reads tap 146 with zero weight)
+                const int o0 = tap_off(2 * q), o1 = tap_off(2 * q + 1 < NT ? 2 * q + 1 : NT - 1);
+                const float *pa = P + (hv ? o1 - o0 : 0);  // k-slot 1 lanes: the odd tap
+                const float av0 = pa[o0], av1 = pa[o0 + 32];
+                acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(av0, w0[u], acc00, 0, 0, 0);
+                acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(av0, w1[u], acc01, 0, 0, 0);
+                acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(av1, w0[u], acc10, 0, 0, 0);
+                acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(av1, w1[u], acc11, 0, 0, 0);
             }
+            __builtin_amdgcn_sched_barrier(0);  // bound the operand reads in flight (VGPR budget of 2 waves / SIMD)
         }
-        // epilogue: D[row][col], col = channel r32 (+32), row = pixel (r & 3) + 8 (r >> 2) + 4 h
+        // epilogue: D[row][col], col = channel r32 (+32), row = pixel (r & 3) + 8 (r >> 2) + 4 h (+32)
         {
             const int tx = (int)(t % a.nTx);
             const int64_t r_ = t / a.nTx;
             const int ty = (int)(r_ % a.nTy);
             const int64_t img = r_ / a.nTy;
-            const int oy = ty * TH + ol;
-            const int oxb = tx * TW + 32 * (wave & 1);
+            const int oy = ty * TH + wave;
+            const int oxb = tx * TW;
             if (oy < a.Ho) {
                 float *yr = a.y + ((img * a.Ho + oy) * (int64_t)a.Wo) * a.Co;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int ox = oxb + (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (ox < a.Wo) {
-                        float v0 = acc0[r] + b0, v1 = acc1[r] + b1;
-                        if (a.relu) {
-                            v0 = v0 > 0.0f ? v0 : 0.0f;
-                            v1 = v1 > 0.0f ? v1 : 0.0f;
+                for (int mt = 0; mt < 2; ++mt) {
+                    const f32x16 &c0 = mt ? acc10 : acc00;
+                    const f32x16 &c1 = mt ? acc11 : acc01;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int ox = oxb + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (ox < a.Wo) {
+                            float v0 = c0[r] + b0, v1 = c1[r] + b1;
+                            if (a.relu) {
+                                v0 = v0 > 0.0f ? v0 : 0.0f;
+                                v1 = v1 > 0.0f ? v1 : 0.0f;
+                            }
+                            float *yp = yr + (int64_t)ox * a.Co;
+                            if (r32 < a.Co) yp[r32] = v0;
+                            if (32 + r32 < a.Co) yp[32 + r32] = v1;
                         }
-                        float *yp = yr + (int64_t)ox * a.Co;
-                        if (r32 < a.Co) yp[r32] = v0;
-                        if (32 + r32 < a.Co) yp[32 + r32] = v1;
                     }
                 }
             }
         }
-        if (tn < a.ntiles) stem_put(pl + (buf ^ 1) * PATCH, tid, pv);
+        __syncthreads();  // every wave is done reading the patch
+        stem_put(pl, tid, pv);
         __syncthreads();
-        buf ^= 1;
     }
 }
 
