@@ -29,7 +29,30 @@ import torch.nn as nn
 
 import bev_native as _nat
 
-__all__ = ["GeometryTransformer", "ViewProjection", "gather_calibration"]
+__all__ = ["GeometryTransformer", "ViewProjection", "gather_calibration", "KORNIA_AVAILABLE"]
+
+# The reference's `_HAS_KORNIA` (geometry.py:5-9).  kornia is absent from this image, so by default
+# warp_impl='kornia' runs the grid_sample semantics exactly like the reference does here (quirk Q7).
+# Set True to get the branch the reference takes where kornia IS installed (geometry.py:124-141):
+# kornia.geometry.transform.warp_perspective semantics, restated (kornia's published algorithm:
+# normalize_homography -> inverse -> normalized meshgrid -> transform_points -> grid_sample,
+# align_corners=False) and run on the same fused HIP warp kernel.  Parity UNPINNED (no kornia here).
+KORNIA_AVAILABLE = False
+
+
+def _normal_transform_pixel(h: int, w: int, dtype, device) -> torch.Tensor:
+    """kornia normal_transform_pixel: pixel [0, w-1] x [0, h-1] -> [-1, 1]^2 (eps 1e-14 for size 1)."""
+    T = torch.eye(3, dtype=dtype, device=device)
+    T[0, 0] = 2.0 / (1e-14 if w == 1 else w - 1.0)
+    T[1, 1] = 2.0 / (1e-14 if h == 1 else h - 1.0)
+    T[0, 2] = T[1, 2] = -1.0
+    return T
+
+
+def _kornia_axis(n: int) -> torch.Tensor:
+    """kornia create_meshgrid(normalized_coordinates=True) axis: (linspace(0, n-1, n) / (n-1) - 0.5) * 2."""
+    a = torch.linspace(0, n - 1, n, dtype=torch.float32)
+    return (a / (n - 1) - 0.5) * 2 if n > 1 else a
 
 
 def _homography_operands(K: torch.Tensor, Rt: torch.Tensor):
@@ -140,8 +163,8 @@ class GeometryTransformer(nn.Module):
         self.bounds = bev_bounds  # (x_min, x_max, y_min, y_max)
         self.res_x = (bev_bounds[1] - bev_bounds[0]) / bev_w
         self.res_y = (bev_bounds[3] - bev_bounds[2]) / bev_h
-        # 'kornia' is accepted for API compatibility; like the reference without
-        # kornia (geometry.py:124) it runs the grid_sample semantics (quirk Q7).
+        # 'kornia': grid_sample semantics like the reference without kornia (geometry.py:124, quirk Q7),
+        # or kornia's warp_perspective semantics when KORNIA_AVAILABLE is set (see kornia_homographies).
         self.warp_impl = warp_impl if warp_impl in ("grid_sample", "kornia") else "grid_sample"
         xs, ys = self._axes()
         self.register_buffer("ground_grid", self._create_ground_grid(xs, ys), persistent=False)
@@ -195,25 +218,76 @@ class GeometryTransformer(nn.Module):
         K33, G33 = gather_calibration(intrinsics, extrinsics, B, V, device)
         return _nat.homography(K33, G33)
 
+    def kornia_homographies(self, intrinsics, extrinsics, B: int, V: int, Hf: int, Wf: int, img_size, device):
+        """kornia-branch sampling maps (geometry.py:124-141) in the kernel's parametrization.
+
+        Per view: M = A_w2bev @ inv(K [r1 r2 t]) @ S_feat2img (feature pixel -> BEV pixel; the reference
+        falls back to pinv when |det| < 1e-8); kornia's warp_perspective samples src at
+        T (xn, yn, 1) with T = inv(N_bev @ M @ inv(N_feat)) over the normalized BEV meshgrid, then
+        grid_sample(align_corners=False) un-normalizes ix = ((gx + 1) Wf - 1) / 2.  Folding that
+        un-normalization into T gives one homography H' with ix = (H'_0 . p) / (H'_2 . p), p = (xn, yn, 1):
+        the warp kernel runs it with the normalized axes and a unit feature scale.  Views whose M is
+        singular (NaN / inf / |det| < 1e-8) take the reference's grid_sample fallback, expressed in the
+        same parametrization (world x = a xn + b).  Computed in float64 on the device, no host sync.
+        Returns (H' [B*V, 9] fp32, xs [Wb], ys [Hb]) and the kernel's img_hw = (Hf, Wf).
+        """
+        K33, G33 = gather_calibration(intrinsics, extrinsics, B, V, device)
+        f64 = torch.float64
+        Hw = K33.to(f64) @ G33.to(f64)  # world plane -> image pixels
+        det = torch.linalg.det(Hw)
+        bad = torch.isnan(det) | torch.isinf(det) | (det.abs() < 1e-8)
+        Hw_safe = torch.where(bad[:, None, None], torch.eye(3, dtype=f64, device=device), Hw)
+        Hi = torch.where(bad[:, None, None], torch.linalg.pinv(Hw), torch.linalg.inv(Hw_safe))
+        H_img, W_img = img_size
+        S = torch.diag(torch.tensor([W_img / float(Wf), H_img / float(Hf), 1.0], dtype=f64, device=device))
+        min_x, _, min_y, _ = self.bounds
+        A = torch.tensor([[1.0 / self.res_x, 0.0, -min_x / self.res_x], [0.0, 1.0 / self.res_y, -min_y / self.res_y],
+                          [0.0, 0.0, 1.0]], dtype=f64, device=device)
+        M = A @ Hi @ S
+        detM = torch.linalg.det(M)
+        singular = torch.isnan(detM) | torch.isinf(detM) | (detM.abs() < 1e-8)
+        Nd = _normal_transform_pixel(self.bev_h, self.bev_w, f64, device)
+        Ns = _normal_transform_pixel(Hf, Wf, f64, device)
+        D = Nd @ torch.where(singular[:, None, None], torch.eye(3, dtype=f64, device=device), M) @ torch.linalg.inv(Ns)
+        T = torch.linalg.inv(D)  # src_norm <- dst_norm
+        U = torch.tensor([[Wf / 2.0, 0.0, (Wf - 1) / 2.0], [0.0, Hf / 2.0, (Hf - 1) / 2.0], [0.0, 0.0, 1.0]],
+                         dtype=f64, device=device)
+        Hk = U @ T
+        # grid_sample fallback in the normalized parametrization: world = a * n + b per axis
+        ax = self.res_x * (self.bev_w - 1) / 2.0
+        ay = self.res_y * (self.bev_h - 1) / 2.0
+        Nw = torch.tensor([[ax, 0.0, min_x + 0.5 * self.res_x + ax], [0.0, ay, min_y + 0.5 * self.res_y + ay],
+                           [0.0, 0.0, 1.0]], dtype=f64, device=device)
+        Sg = torch.diag(torch.tensor([Wf / float(W_img), Hf / float(H_img), 1.0], dtype=f64, device=device))
+        Hg = Sg @ Hw @ Nw
+        Hp = torch.where(singular[:, None, None], Hg, Hk).to(torch.float32).reshape(-1, 9).contiguous()
+        xs = _kornia_axis(self.bev_w).to(device)
+        ys = _kornia_axis(self.bev_h).to(device)
+        return Hp, xs, ys, (Hf, Wf)
+
+    def _sampling(self, feats, intrinsics, extrinsics, img_size):
+        B, V, _, Hf, Wf = feats.shape
+        device = feats.device
+        if self.warp_impl == "kornia" and KORNIA_AVAILABLE:
+            return self.kornia_homographies(intrinsics, extrinsics, B, V, Hf, Wf, img_size, device)
+        H = self.homographies(intrinsics, extrinsics, B, V, device)
+        xs, ys = self._device_axes(device)
+        return H, xs, ys, tuple(img_size)
+
     def forward(self, feats: torch.Tensor, intrinsics, extrinsics,
                 img_size: Tuple[int, int] = (1080, 1920)) -> torch.Tensor:
         """feats [B,V,C,Hf,Wf] -> per-view BEV maps [B,V,C,H_bev,W_bev] (geometry.py:80-163)."""
         B, V, C, Hf, Wf = feats.shape
-        device = feats.device
-        H = self.homographies(intrinsics, extrinsics, B, V, device)
-        xs, ys = self._device_axes(device)
+        H, xs, ys, hw = self._sampling(feats, intrinsics, extrinsics, img_size)
         f4 = feats.reshape(B * V, C, Hf, Wf) if feats.is_contiguous() else feats.flatten(0, 1)
-        out = _WarpFn.apply(f4, H, xs, ys, tuple(img_size))
+        out = _WarpFn.apply(f4, H, xs, ys, hw)
         return out.view(B, V, C, self.bev_h, self.bev_w)
 
     def forward_fused(self, feats: torch.Tensor, intrinsics, extrinsics, img_size: Tuple[int, int] = (1080, 1920),
                       mode: str = "mean") -> torch.Tensor:
         """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev]."""
-        B, V, C, Hf, Wf = feats.shape
-        device = feats.device
-        H = self.homographies(intrinsics, extrinsics, B, V, device)
-        xs, ys = self._device_axes(device)
-        return _WarpFuseFn.apply(feats, H, xs, ys, tuple(img_size), mode)
+        H, xs, ys, hw = self._sampling(feats, intrinsics, extrinsics, img_size)
+        return _WarpFuseFn.apply(feats, H, xs, ys, hw, mode)
 
 
 # north_star vocabulary alias

@@ -133,10 +133,9 @@ class BEVNet(nn.Module):
             self._proj_panels = (key, panels)
         return self._proj_panels[1]
 
-    def _bev_main(self, feats, H, img_hw):
+    def _bev_main(self, feats, H, xs, ys, img_hw):
         """[B,V,C,Hf,Wf] features -> BEV map before pos-enc: proj(concat of per-view warps), NCHW (any strides)."""
         B, V, C = feats.shape[:3]
-        xs, ys = self.geom._device_axes(feats.device)
         if self.proj is None and self.bev_proj_ch > 0:
             self.proj = nn.Conv2d(V * C, self.bev_proj_ch, kernel_size=1).to(feats.device)
         if self.proj is None:  # no projection: the concatenated per-view warps (model_wrapper.py:80)
@@ -152,8 +151,9 @@ class BEVNet(nn.Module):
         feats = self.encoder(images)
         K = self._stack_calib(batch["calib"]["intrinsic"])
         Rt = self._stack_calib(batch["calib"]["extrinsic"])
-        H = self.geom.homographies(K, Rt, B, V, feats.device)
-        main = self._bev_main(feats, H, (Hi, Wi))  # quirk Q1: network-input size
+        # quirk Q1: network-input size; warp_impl='kornia' -> grid_sample semantics unless KORNIA_AVAILABLE
+        H, xs, ys, hw = self.geom._sampling(feats, K, Rt, (Hi, Wi))
+        main = self._bev_main(feats, H, xs, ys, hw)
         P = main.shape[1]
         if self.detector is None:
             self.detector = BEVDetector(in_channels=P + 2, bev_bounds=self.bounds, bev_size=(self.bev_h, self.bev_w),
