@@ -173,6 +173,19 @@ int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const flo
                         int stride2, const float *packed, const float *bias, int Co, int relu, float *y,
                         void *stream);
 
+/* device: two chained convolutions in ONE launch (NHWC):
+ *   h = act(conv(x, W1) + bias)               (KH x KW, stride, pad; Co = 64 or 128 channels)
+ *   y = act2(h (*) W2 + bias2 + residual)     (1x1, Co -> Co2, Co2 % 128 == 0)
+ * h never leaves the chip: each workgroup holds all Co channels of h for its pixels in LDS and
+ * runs the 1x1 GEMM on them.  packed / packed2 = bev_conv_pack_weights_f32 of W1 [Co][Ci][KH][KW]
+ * and W2 [Co2][Co][1][1] (BN folded); residual [N][Ho][Wo][Co2] or NULL; Ci % 32 == 0; 16-B aligned
+ * x / panels.  Bit-identical to bev_conv2d_f32(x -> h) followed by bev_conv2d_f32(h -> y).
+ * Replaces timm Bottleneck.forward's conv2 -> bn2 -> act2 -> conv3 -> bn3 (+ shortcut) -> act3 for
+ * the blocks without a downsample, inside the features_only trunk (cnn_encoder.py:26, 41-42). */
+int bev_conv2d_chain_f32(const float *x, int N, int H, int W, int Ci, const float *packed, const float *bias, int Co,
+                         int KH, int KW, int stride, int pad, int relu, const float *packed2, const float *bias2,
+                         int Co2, const float *residual, int relu2, float *y, int Ho, int Wo, void *stream);
+
 /* device: NHWC max-pool (timm ResNet stem: 3x3, stride 2, pad 1). */
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
                            int Wo, void *stream);

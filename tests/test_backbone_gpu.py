@@ -103,6 +103,51 @@ def test_conv_dual_vs_torch_fp32(case):
     np.testing.assert_allclose(y.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
+CHAIN_CASES = [
+    # N, Ci, H, W, Co (conv2 out), K, stride, Co2, residual
+    (2, 64, 17, 23, 64, 3, 1, 256, True),     # ResNet-50 layer1 blocks 1-2: 3x3 64->64, 1x1 64->256 + x
+    (1, 128, 15, 21, 128, 3, 1, 512, True),   # layer2 blocks 1-3: 3x3 128->128, 1x1 128->512 + x
+    (3, 64, 9, 37, 64, 3, 2, 128, False),     # strided, no residual, ragged last block (M = 3 * 5 * 19)
+    (1, 96, 7, 5, 128, 1, 1, 384, True),      # 1x1 first conv, M < one block, 3 chunks per wave
+]
+
+
+@pytest.mark.parametrize("case", CHAIN_CASES, ids=[f"ci{c[1]}_co{c[4]}_k{c[5]}s{c[6]}_co2{c[7]}" for c in CHAIN_CASES])
+def test_conv_chain_bit_exact_vs_two_launches(case):
+    """bev_conv2d_chain_f32 (conv -> LDS -> 1x1 conv in one launch) == the two separate bev_conv2d_f32
+    launches bit for bit (same K order for both GEMMs), and both == torch fp32 within the conv tolerance."""
+    import bev_native as nat
+    N, Ci, H, W, Co, k, s, Co2, resid = case
+    p = k // 2
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    x = _rand((N, Ci, H, W), 21)
+    w1 = _rand((Co, Ci, k, k), 22, scale=(2.0 / (Ci * k * k)) ** 0.5)
+    b1 = _rand((Co,), 23)
+    w2 = _rand((Co2, Co, 1, 1), 24, scale=(2.0 / Co) ** 0.5)
+    b2 = _rand((Co2,), 25)
+    r = _rand((N, Co2, Ho, Wo), 26) if resid else None
+    xin = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    rin = r.permute(0, 2, 3, 1).contiguous().to(DEV) if resid else None
+    pk1, pk2 = nat.pack_conv_weight(w1.to(DEV)), nat.pack_conv_weight(w2.to(DEV))
+    h = nat.conv2d_nhwc(xin, pk1, b1.to(DEV), Co, k, k, s, p, True)
+    two = nat.conv2d_nhwc(h, pk2, b2.to(DEV), Co2, 1, 1, 1, 0, True, residual=rin)
+    one = nat.conv2d_chain_nhwc(xin, pk1, b1.to(DEV), Co, k, k, s, p, 1, pk2, b2.to(DEV), Co2, 1, residual=rin)
+    torch.cuda.synchronize()
+    assert torch.equal(one.view(torch.int32), two.view(torch.int32))
+    ref = F.conv2d(F.relu(F.conv2d(x, w1, b1, s, p)), w2, b2)
+    ref = F.relu(ref + r if resid else ref)
+    np.testing.assert_allclose(one.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_conv_chain_rejects_unsupported_shapes():
+    import bev_native as nat
+    x = torch.zeros(1, 5, 5, 64, device=DEV)
+    pk = nat.pack_conv_weight(torch.zeros(96, 64, 3, 3, device=DEV))
+    pk2 = nat.pack_conv_weight(torch.zeros(256, 96, 1, 1, device=DEV))
+    with pytest.raises(nat.HipError):  # Co must be 64 or 128 (one workgroup holds every channel of h)
+        nat.conv2d_chain_nhwc(x, pk, None, 96, 3, 3, 1, 1, 1, pk2, None, 256, 1)
+
+
 def test_maxpool_and_layouts_exact():
     import bev_native as nat
     x = _rand((2, 64, 31, 45), 5)
@@ -151,6 +196,22 @@ def test_resnet_encoder_vs_torch_fp32(name):
     assert tuple(y.shape) == tuple(ref.shape) == (1, 3, 64, 12, 20)
     err = (y - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-4, err
+
+
+def test_resnet_chain_fusion_bit_exact():
+    """ResNet-50 trunk with the bottleneck conv2 -> conv3 chains in one launch (FoldedChain) == the
+    unchained launches, bit for bit."""
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(2)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(DEV)
+    imgs = _rand((1, 3, 3, 90, 150), 10).to(DEV)
+    with torch.no_grad():
+        enc.backbone.fuse_chain = False
+        ref = enc(imgs).clone()
+        enc.backbone.fuse_chain = True
+        got = enc(imgs)
+        torch.cuda.synchronize()
+    assert torch.equal(got.contiguous().view(torch.int32), ref.contiguous().view(torch.int32))
 
 
 @pytest.mark.parametrize("groups,offset", [(2, 0), (3, 0), (2, 1), (3, 3)])

@@ -17,7 +17,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -53,6 +53,8 @@ SIGNATURES = {
     "bev_colsum_f32": (_i, [_vp, _i64, _i, _vp, _vp]),
     "bev_maxpool2d_bwd_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
+    "bev_conv2d_chain_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
+                                  _i, _i, _vp]),
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
@@ -413,6 +415,27 @@ def conv2d_dual_nhwc(x: torch.Tensor, x2: torch.Tensor, stride2: int, packed: to
         rc = lib().bev_conv2d_dual_f32(_ptr(x), N, Ho, Wo, Ci, _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed),
                                        _ptr(bias), Co, int(relu), _ptr(out), _stream(x))
     _check(rc, "bev_conv2d_dual_f32")
+    return out
+
+
+def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
+                      relu: int, packed2: torch.Tensor, bias2, Co2: int, relu2: int, residual: torch.Tensor = None,
+                      out: torch.Tensor = None):
+    """act2(act(conv(x) + bias) (*) W2 + bias2 + residual) in one launch; x [N,H,W,Ci] NHWC -> [N,Ho,Wo,Co2]."""
+    x = x.contiguous()
+    _require_gpu(x, packed, bias, packed2, bias2, residual)
+    N, H, W, Ci = x.shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co2, device=x.device, dtype=torch.float32)
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == out.shape
+    with _span("conv", x):
+        rc = lib().bev_conv2d_chain_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad,
+                                        int(relu), _ptr(packed2), _ptr(bias2), Co2, _ptr(residual), int(relu2),
+                                        _ptr(out), Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_chain_f32")
     return out
 
 

@@ -95,6 +95,10 @@ struct ConvArgs {
     int dil;  // dilation of the taps (input offset ky * dil, kx * dil)
     int ldy;  // row stride of y in floats (>= Co; a channel slice of a wider NHWC buffer)
     int xcd;  // 1: XCD-aware block order (the N tiles of one M block run on one XCD, sharing its L2)
+    // chained pointwise conv (EPI 1, bev_conv2d_chain_f32): y = act2(h (*) W2 + bias2 + res), h = this conv's output
+    const float *__restrict__ wp2;
+    const float *__restrict__ bias2;
+    int Co2, Kp2, relu2;
 };
 
 // Per-thread view of the A tile rows it loads: rows (tid >> 3) + 32 r, one 16-B quad.
@@ -369,13 +373,125 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
     for (int r = 0; r < R; ++r) *(f32x4 *)(p + 32 * r * LROW) = v[r];
 }
 
+// ---------------------------------------------------------------------------
+// Chained pointwise epilogue (EPI 1; bev_conv2d_chain_f32)
+// ---------------------------------------------------------------------------
+// timm Bottleneck.forward without a downsample: act3(bn3(conv3(act2(bn2(conv2(h1))))) + x).
+// The block's BM x BN tile of h2 = act(conv2(h1) + b2) holds EVERY channel of h2 for its BM
+// pixels (BN == Co), so conv3 (1x1, K2 = Co) runs on it straight from LDS:
+//     y = act2( h2 (*) W3 + b3 + res )
+// and h2 never makes its HBM round trip (write + read of M x Co floats).  Each wave computes its
+// 32 rows x (Co2 / WN) columns in 64-column chunks (2 MFMA tiles); the W3 fragments stream from
+// L2 (the panel is shared by every block) one 16-deep half step ahead; the chunk's residual is
+// loaded before its MFMAs.  K2 order = the main loop's (k-slot h of MFMA p reads 16 h + 8 half + p
+// inside each 32-deep step), so y is bit-identical to the two-launch chain.
+// Buffer resources (base, byte size): the uniform parts of every address go to the SGPR soffset,
+// and loads / stores past the block's last row (num_records) return 0 / are dropped.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chain_rsrc(const float *p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)(uint32_t)bytes, 0x00020000);
+}
+
+// W2 fragments of half step t (k = 32 (t >> 1) + 16 hh + 8 (t & 1) + 0..7) for columns c0 + 32 j + r32.
+__device__ __forceinline__ void chain_load_b(__amdgpu_buffer_rsrc_t rw, int kp2, int voff, int c0, int t,
+                                             f32x4 (&w)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int so = ((c0 + 32 * j) * kp2 + 32 * (t >> 1) + 8 * (t & 1) + 4 * q) * 4;
+            w[j][q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, voff, so, 0));
+        }
+}
+
+__device__ __forceinline__ void chain_mfma(f32x16 (&acc)[2], const float *ap, int t, const f32x4 (&w)[2][2]) {
+    const float *pa = ap + 32 * (t >> 1) + 8 * (t & 1);
+    const f32x4 a0 = *(const f32x4 *)pa, a1 = *(const f32x4 *)(pa + 4);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const float av = (p < 4 ? a0 : a1)[p & 3];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w[j][p >> 2][p & 3], acc[j], 0, 0, 0);
+    }
+}
+
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void chain_epilogue(const ConvArgs &a, float *lds, const f32x16 (&acc)[TM][TN], int wm,
+                                               int wn, int lane, int64_t m0) {
+    static_assert(TM == 1 && TN == 2, "chain epilogue: each wave owns 32 rows x 64 channels of h2");
+    constexpr int BM = WM * 32, BN = WN * 64, LA = BN + 4;  // h2 image [BM][LA]: 4 LA B = odd 16-B slot count
+    constexpr int HS = BN / 16;                              // 16-deep half steps per 64-column chunk (K2 = BN)
+    const int r32 = lane & 31, hh = lane >> 5;
+    __syncthreads();  // every wave is done with the staging buffers
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int col = wn * 64 + j * 32 + r32;
+        const float bj = a.bias ? a.bias[col] : 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float o = acc[0][j][r] + bj;
+            if (a.relu) o = act_fn(o, a.relu);
+            lds[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh) * LA + col] = o;
+        }
+    }
+    __syncthreads();
+    const int ncols = a.Co2 / WN, nch = ncols / 64;
+    const int cb = wn * ncols;
+    const float *ap = lds + (wm * 32 + r32) * LA + 16 * hh;
+    // this block's rows of res / y: [m0, min(m0 + BM, M)) x Co2 (ldy == Co2)
+    const int64_t rows = (a.M - m0 < BM) ? a.M - m0 : BM;
+    const int64_t base = m0 * a.Co2;
+    const __amdgpu_buffer_rsrc_t ry = chain_rsrc(a.y + base, rows * a.Co2 * 4);
+    const __amdgpu_buffer_rsrc_t rr = chain_rsrc(a.res ? a.res + base : a.y + base, rows * a.Co2 * 4);
+    const __amdgpu_buffer_rsrc_t rw = chain_rsrc(a.wp2, (int64_t)copad(a.Co2) * a.Kp2 * 4);
+    const int vw = (r32 * a.Kp2 + 16 * hh) * 4;                // lane part of a W2 address
+    const int vo = ((wm * 32 + 4 * hh) * a.Co2 + r32) * 4;     // lane part of a res / y address
+    f32x4 wA[2][2], wB[2][2];
+    chain_load_b(rw, a.Kp2, vw, cb, 0, wA);
+    for (int nc = 0; nc < nch; ++nc) {
+        const int c0 = cb + 64 * nc;
+        float rv[2][16];
+        if (a.res) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    rv[j][r] = __builtin_bit_cast(
+                        float, __builtin_amdgcn_raw_buffer_load_b32(
+                                   rr, vo, (((r & 3) + 8 * (r >> 2)) * a.Co2 + c0 + 32 * j) * 4, 0));
+        }
+        f32x16 acc2[2] = {(f32x16){0}, (f32x16){0}};
+#pragma unroll
+        for (int t = 0; t < HS; t += 2) {
+            chain_load_b(rw, a.Kp2, vw, c0, t + 1, wB);
+            chain_mfma(acc2, ap, t, wA);
+            // after the chunk's last half step: the next chunk's first (clamped: the load is unconditional)
+            const bool lst = (t + 2 == HS);
+            chain_load_b(rw, a.Kp2, vw, lst ? (nc + 1 < nch ? c0 + 64 : c0) : c0, lst ? 0 : t + 2, wA);
+            chain_mfma(acc2, ap, t + 1, wB);
+            __builtin_amdgcn_sched_barrier(0);  // one half step of W2 in flight (VGPR budget of 3 blocks / CU)
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float bj = a.bias2 ? a.bias2[c0 + 32 * j + r32] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float o = acc2[j][r] + bj;
+                if (a.res) o += rv[j][r];
+                if (a.relu2) o = act_fn(o, a.relu2);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry, vo,
+                                                      (((r & 3) + 8 * (r >> 2)) * a.Co2 + c0 + 32 * j) * 4, 0);
+            }
+        }
+    }
+}
+
 // Block = WM x WN waves; each wave owns TM x TN MFMA tiles of 32 x 32.
 // LOADER: 0 generic, 1 fast (NHWC, Ci % 32 == 0), 2 stem (NCHW, Ci = 3, 7 x 7), 3 dual 1x1,
 // 4 contiguous 1x1 (NHWC, Ci % 4 == 0), 5 fast + dilation + GroupNorm/ReLU operand affine,
 // 6 fast + per-(image, channel) operand scale
 // NBUF: LDS staging buffers.  2 = one barrier per K step; 1 = half the LDS (a
 // third workgroup per CU for the <= 170-VGPR tiles) at two barriers per K step.
-template <int WM, int WN, int TM, int TN, int LOADER, int NBUF>
+template <int WM, int WN, int TM, int TN, int LOADER, int NBUF, int CHAIN = 0>
 __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int AROWS = BM / 32;  // A rows per thread (rows tid/8 + 32 r)
@@ -511,6 +627,11 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
 #undef BEV_MFMA_STEP
 #undef BEV_GLOAD
 #undef BEV_SWRITE
+    if constexpr (CHAIN == 1) {
+        static_assert(WM * 32 * (WN * TN * 32 + 4) <= LDSF, "chain epilogue: h tile must fit the LDS");
+        chain_epilogue<WM, WN, TM, TN>(a, lds, acc, wm, wn, lane, m0);
+        return;
+    }
 
     // ---- epilogue through LDS ---------------------------------------------------
     // The wave's (TM*32) x (TN*32) accumulator tile goes to LDS, then every lane
@@ -910,6 +1031,18 @@ int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
     return launch_conv<2, 2, 2, 2>(a, loader, st);                 // 128 x 128 tiles
 }
 
+// Chained conv (EPI 1): one M block holds all Co channels of the first conv -- 128 x 64 tiles
+// for Co = 64 (ResNet layer1), 64 x 128 for Co = 128 (layer2); one LDS staging buffer (3 blocks / CU).
+int launch_chain(const ConvArgs &a, hipStream_t st) {
+    const int bm = a.Co == 64 ? 128 : 64;
+    const int64_t blocks = (a.M + bm - 1) / bm;
+    if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
+    const dim3 g((unsigned)blocks), b(256);
+    if (a.Co == 64) hipLaunchKernelGGL((k_conv<4, 1, 1, 2, 1, 1, 1>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_conv<2, 2, 1, 2, 1, 1, 1>), g, b, 0, st, a);
+    return last();
+}
+
 }  // namespace
 
 extern "C" {
@@ -1074,6 +1207,50 @@ int bev_conv2d_dual_f32(const float *x, int N, int Ho, int Wo, int Ci, const flo
     a.W2 = W2;
     a.stride2 = stride2;
     return launch_tiled(a, 3, (hipStream_t)stream);
+}
+
+int bev_conv2d_chain_f32(const float *x, int N, int H, int W, int Ci, const float *packed, const float *bias, int Co,
+                         int KH, int KW, int stride, int pad, int relu, const float *packed2, const float *bias2,
+                         int Co2, const float *residual, int relu2, float *y, int Ho, int Wo, void *stream) {
+    if (!x || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+        pad < 0 || relu < 0 || relu > 2 || relu2 < 0 || relu2 > 2)
+        return BEV_ERR_ARGS;
+    if (Ci % BK != 0 || (Co != 64 && Co != 128) || Co2 <= 0 || Co2 % 128 != 0 || ((uintptr_t)x & 15) != 0 ||
+        (((uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvArgs a{};
+    a.x = x;
+    a.wp = packed;
+    a.bias = bias;
+    a.res = residual;
+    a.y = y;
+    a.N = N;
+    a.H = H;
+    a.W = W;
+    a.Ci = Ci;
+    a.Co = Co;
+    a.KH = KH;
+    a.KW = KW;
+    a.stride = stride;
+    a.pad = pad;
+    a.Ho = Ho;
+    a.Wo = Wo;
+    a.relu = relu;
+    a.M = (int64_t)N * Ho * Wo;
+    a.K = Ci * KH * KW;
+    a.Kp = (int)kpad(a.K);
+    a.dil = 1;
+    a.ldy = Co2;
+    a.xcd = conv_xcd();
+    a.wp2 = packed2;
+    a.bias2 = bias2;
+    a.Co2 = Co2;
+    a.Kp2 = (int)kpad(Co);
+    a.relu2 = relu2;
+    return launch_chain(a, (hipStream_t)stream);
 }
 
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,

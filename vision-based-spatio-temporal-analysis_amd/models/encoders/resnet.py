@@ -164,6 +164,35 @@ class FoldedTail:
                                      self.main.conv.out_channels, relu=True, out=out)
 
 
+class FoldedChain:
+    """Bottleneck conv2/bn2/act2 -> conv3/bn3 (+ identity shortcut) -> act3 as ONE launch.
+
+    timm Bottleneck.forward for a block without a downsample computes
+    act3(bn3(conv3(act2(bn2(conv2(h1))))) + x); with both BNs folded, bev_conv2d_chain_f32 keeps
+    the conv2 output of each workgroup's pixels (all `width` channels) in LDS and runs conv3 on it,
+    so that tensor is never written to HBM.  Bit-identical to the two separate launches.
+    """
+
+    def __init__(self, c2: FoldedConv, c3: FoldedConv):
+        self.c2, self.c3 = c2, c3
+
+    @staticmethod
+    def applies(blk) -> bool:
+        c2, c3 = blk.conv2, blk.conv3
+        return (blk.downsample is None and c2.out_channels in (64, 128) and c2.in_channels % 32 == 0
+                and c2.kernel_size[0] == c2.kernel_size[1] and c2.dilation == (1, 1) and c2.groups == 1
+                and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.padding == (0, 0)
+                and c3.out_channels % 128 == 0)
+
+    def __call__(self, h, x, out=None):
+        self.c2.prepare(h.device)
+        self.c3.prepare(h.device)
+        c2 = self.c2.conv
+        return _nat.conv2d_chain_nhwc(h, self.c2.packed, self.c2.bias, c2.out_channels, c2.kernel_size[0],
+                                      c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU, self.c3.packed,
+                                      self.c3.bias, self.c3.conv.out_channels, _nat.ACT_RELU, residual=x, out=out)
+
+
 def stage_of(out_index: int) -> int:
     """features_only index -> number of residual stages to run (0: act1, 1: layer1, ...)."""
     return max(0, out_index)
@@ -193,6 +222,7 @@ class ResNet(nn.Module):
                 nn.init.zeros_(m.bias)
         self._folded = {}
         self.fuse_shortcut = True  # bottleneck conv3 + downsample as one dual-source GEMM
+        self.fuse_chain = True  # bottleneck conv2 -> conv3 (+ identity) in one launch (h2 stays in LDS)
         # Inference: split the images into this many groups, each run on its own HIP stream, so the
         # HBM- / latency-bound 1x1 layers of one group overlap the MFMA-bound 3x3 layers of another (the
         # images are independent; every layer still runs as one kernel per group; bit-identical output).
@@ -321,7 +351,16 @@ class ResNet(nn.Module):
             self._folded[k] = FoldedTail(self._fc(blk.conv3, blk.bn3), self._fc(blk.downsample[0], blk.downsample[1]))
         return self._folded[k]
 
+    def _chain(self, blk):
+        k = ("chain", id(blk))
+        if k not in self._folded:
+            self._folded[k] = FoldedChain(self._fc(blk.conv2, blk.bn2), self._fc(blk.conv3, blk.bn3))
+        return self._folded[k]
+
     def _block(self, blk, x, out=None):
+        if isinstance(blk, Bottleneck) and self.fuse_chain and FoldedChain.applies(blk):
+            h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
+            return self._chain(blk)(h, x, out=out)
         if isinstance(blk, Bottleneck) and self.fuse_shortcut and FoldedTail.applies(blk):
             h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
             h = self._fc(blk.conv2, blk.bn2)(h, relu=True)
