@@ -186,6 +186,19 @@ int bev_conv2d_chain_f32(const float *x, int N, int H, int W, int Ci, const floa
                          int KH, int KW, int stride, int pad, int relu, const float *packed2, const float *bias2,
                          int Co2, const float *residual, int relu2, float *y, int Ho, int Wo, void *stream);
 
+/* device: as bev_conv2d_chain_f32 for a bottleneck WITH a downsample shortcut (block 0 of a stage):
+ *   h = act(conv(x, W1) + bias)
+ *   y = act2( [h | x2[:, ::s2, ::s2, :]] (*) W2 + bias2 )     (1x1 over K2 = Co + Ci2)
+ * x2 [N][H2][W2][Ci2] is the block input the 1x1/stride-s2 downsample reads (Ho = (H2-1)/s2 + 1);
+ * packed2 = bev_conv_pack_weights_f32 of [W3 | Wds] as [Co2][Co + Ci2][1][1], bias2 = b3 + bds
+ * (the bev_conv2d_dual_f32 panel).  Ci2 % 32 == 0, x2 < 4 GiB, 16-B aligned.  Bit-identical to
+ * bev_conv2d_f32(x -> h) followed by bev_conv2d_dual_f32(h, x2 -> y).  Replaces timm
+ * Bottleneck.forward's conv2 -> bn2 -> act2 -> conv3 -> bn3 (+ downsample(shortcut)) -> act3. */
+int bev_conv2d_chain_dual_f32(const float *x, int N, int H, int W, int Ci, const float *packed, const float *bias,
+                              int Co, int KH, int KW, int stride, int pad, int relu, const float *x2, int H2, int W2,
+                              int Ci2, int stride2, const float *packed2, const float *bias2, int Co2, int relu2,
+                              float *y, int Ho, int Wo, void *stream);
+
 /* device: NHWC max-pool (timm ResNet stem: 3x3, stride 2, pad 1). */
 int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y, int Ho,
                            int Wo, void *stream);

@@ -139,6 +139,41 @@ def test_conv_chain_bit_exact_vs_two_launches(case):
     np.testing.assert_allclose(one.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
+CHAIN_DUAL_CASES = [
+    # N, Ci (conv2 in), H, W, Co, stride (conv2), Ci2 (block input), H2, W2, s2, Co2
+    (2, 64, 17, 23, 64, 1, 64, 17, 23, 1, 256),      # layer1 block 0 (downsample 64 -> 256, stride 1)
+    (1, 128, 15, 21, 128, 2, 256, 15, 21, 2, 512),   # layer2 block 0 (3x3 stride 2, downsample stride 2)
+    (3, 32, 9, 10, 64, 3, 96, 9, 10, 3, 128),        # stride 3, odd sizes, ragged last block
+]
+
+
+@pytest.mark.parametrize("case", CHAIN_DUAL_CASES, ids=[f"co{c[4]}_s{c[5]}_ci2{c[6]}_co2{c[10]}" for c in CHAIN_DUAL_CASES])
+def test_conv_chain_dual_bit_exact_vs_two_launches(case):
+    """bev_conv2d_chain_dual_f32 == bev_conv2d_f32 (3x3) then bev_conv2d_dual_f32 (conv3 + downsample), bit for
+    bit, and == torch fp32 relu(conv3(h) + ds(x) + b) within the conv tolerance."""
+    import bev_native as nat
+    N, Ci, H, W, Co, s, Ci2, H2, W2, s2, Co2 = case
+    x = _rand((N, Ci, H, W), 31)
+    xb = _rand((N, Ci2, H2, W2), 32)
+    w1 = _rand((Co, Ci, 3, 3), 33, scale=(2.0 / (Ci * 9)) ** 0.5)
+    b1 = _rand((Co,), 34)
+    w3 = _rand((Co2, Co, 1, 1), 35, scale=(2.0 / Co) ** 0.5)
+    wd = _rand((Co2, Ci2, 1, 1), 36, scale=(2.0 / Ci2) ** 0.5)
+    b2 = _rand((Co2,), 37)
+    xin = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xbin = xb.permute(0, 2, 3, 1).contiguous().to(DEV)
+    pk1 = nat.pack_conv_weight(w1.to(DEV))
+    pk2 = nat.pack_conv_weight(torch.cat([w3, wd], 1).to(DEV))
+    h = nat.conv2d_nhwc(xin, pk1, b1.to(DEV), Co, 3, 3, s, 1, True)
+    two = nat.conv2d_dual_nhwc(h, xbin, s2, pk2, b2.to(DEV), Co2, True)
+    one = nat.conv2d_chain_dual_nhwc(xin, pk1, b1.to(DEV), Co, 3, 3, s, 1, 1, xbin, s2, pk2, b2.to(DEV), Co2, 1)
+    torch.cuda.synchronize()
+    assert one.shape == two.shape
+    assert torch.equal(one.view(torch.int32), two.view(torch.int32))
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(x, w1, b1, s, 1)), w3) + F.conv2d(xb, wd, stride=s2) + b2.view(1, -1, 1, 1))
+    np.testing.assert_allclose(one.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+
+
 def test_conv_chain_rejects_unsupported_shapes():
     import bev_native as nat
     x = torch.zeros(1, 5, 5, 64, device=DEV)

@@ -71,6 +71,37 @@ CHAIN = {
     "l1.1.chain": (64, 64, 256, 270, 480),
     "l2.1.chain": (128, 128, 512, 135, 240),
 }
+# chained block-0 bodies (bev_conv2d_chain_dual_f32): name: (Ci, Co, Co2, H, W, stride, Ci2) -- 3x3 Ci->Co
+# (stride), then [h2 | x[::stride]] 1x1 -> Co2; x [N][H][W][Ci2] is the block input
+CHAIN_DUAL = {
+    "l1.0.chain": (64, 64, 256, 270, 480, 1, 64),
+    "l2.0.chain": (128, 128, 512, 270, 480, 2, 256),
+}
+
+
+def run_chain_dual(name, iters):
+    Ci, Co, Co2, H, W, s, Ci2 = CHAIN_DUAL[name]
+    Ho, Wo = (H - 1) // s + 1, (W - 1) // s + 1
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    h = torch.randn(N, H, W, Ci, device=dev, generator=g)
+    x = torch.randn(N, H, W, Ci2, device=dev, generator=g)
+    p1 = nat.pack_conv_weight(torch.randn(Co, Ci, 3, 3, device=dev, generator=g) * (2.0 / (Ci * 9)) ** 0.5)
+    p2 = nat.pack_conv_weight(torch.randn(Co2, Co + Ci2, 1, 1, device=dev, generator=g) * (2.0 / (Co + Ci2)) ** 0.5)
+    b1, b2 = torch.randn(Co, device=dev, generator=g), torch.randn(Co2, device=dev, generator=g)
+    out = torch.empty(N, Ho, Wo, Co2, device=dev)
+    for _ in range(3):
+        nat.conv2d_chain_dual_nhwc(h, p1, b1, Co, 3, 3, s, 1, 1, x, s, p2, b2, Co2, 1, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        nat.conv2d_chain_dual_nhwc(h, p1, b1, Co, 3, 3, s, 1, 1, x, s, p2, b2, Co2, 1, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    flops = 2 * N * Ho * Wo * (Co * Ci * 9 + Co2 * (Co + Ci2))
+    byts = 4 * (h.numel() + N * Ho * Wo * Ci2 + out.numel())
+    print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
 
 
 def run_chain(name, iters):
@@ -125,7 +156,7 @@ def run(name, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("layers", nargs="*", default=[k for k in LAYERS if k != "g512"] + list(DUAL) + list(CHAIN))
+    ap.add_argument("layers", nargs="*", default=[k for k in LAYERS if k != "g512"] + list(DUAL) + list(CHAIN) + list(CHAIN_DUAL))
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--knob", default="CONV_TILE", help="bev_tune knob to A/B (TUNE_<name>)")
     ap.add_argument("--values", type=int, nargs="*", default=[0], help="knob values, interleaved per round")
@@ -137,7 +168,8 @@ def main():
             old = nat.tune(knob, v)
             print(f"-- round {rnd} {a.knob}={v}")
             for name in a.layers:
-                (run_dual if name in DUAL else run_chain if name in CHAIN else run)(name, a.iters)
+                (run_dual if name in DUAL else run_chain if name in CHAIN else run_chain_dual if name in CHAIN_DUAL
+                 else run)(name, a.iters)
             nat.tune(knob, old)
 
 

@@ -55,6 +55,8 @@ SIGNATURES = {
     "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_conv2d_chain_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
                                   _i, _i, _vp]),
+    "bev_conv2d_chain_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i,
+                                       _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
@@ -436,6 +438,26 @@ def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: 
                                         int(relu), _ptr(packed2), _ptr(bias2), Co2, _ptr(residual), int(relu2),
                                         _ptr(out), Ho, Wo, _stream(x))
     _check(rc, "bev_conv2d_chain_f32")
+    return out
+
+
+def conv2d_chain_dual_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int,
+                           pad: int, relu: int, x2: torch.Tensor, stride2: int, packed2: torch.Tensor, bias2, Co2: int,
+                           relu2: int, out: torch.Tensor = None):
+    """act2([act(conv(x) + bias) | x2[:, ::s2, ::s2]] (*) W2 + bias2) in one launch (bottleneck with downsample)."""
+    x = x.contiguous()
+    x2 = x2.contiguous()
+    _require_gpu(x, packed, bias, x2, packed2, bias2)
+    N, H, W, Ci = x.shape
+    _, H2, W2, Ci2 = x2.shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co2, device=x.device, dtype=torch.float32)
+    with _span("conv", x):
+        rc = lib().bev_conv2d_chain_dual_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad,
+                                             int(relu), _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed2), _ptr(bias2),
+                                             Co2, int(relu2), _ptr(out), Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_chain_dual_f32")
     return out
 
 

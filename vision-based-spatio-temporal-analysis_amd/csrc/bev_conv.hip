@@ -385,8 +385,9 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
 // L2 (the panel is shared by every block) one 16-deep half step ahead; the chunk's residual is
 // loaded before its MFMAs.  K2 order = the main loop's (k-slot h of MFMA p reads 16 h + 8 half + p
 // inside each 32-deep step), so y is bit-identical to the two-launch chain.
-// Buffer resources (base, byte size): the uniform parts of every address go to the SGPR soffset,
-// and loads / stores past the block's last row (num_records) return 0 / are dropped.
+// Buffer resources (base, byte size): the lane's row is in the VGPR offset (the part the range
+// check sees), so loads / stores of rows past the block's last one return 0 / are dropped; the
+// uniform column / k offset goes to the SGPR soffset.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t chain_rsrc(const float *p, int64_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), 0, (int)(uint32_t)bytes, 0x00020000);
 }
@@ -403,9 +404,8 @@ __device__ __forceinline__ void chain_load_b(__amdgpu_buffer_rsrc_t rw, int kp2,
         }
 }
 
-__device__ __forceinline__ void chain_mfma(f32x16 (&acc)[2], const float *ap, int t, const f32x4 (&w)[2][2]) {
-    const float *pa = ap + 32 * (t >> 1) + 8 * (t & 1);
-    const f32x4 a0 = *(const f32x4 *)pa, a1 = *(const f32x4 *)(pa + 4);
+__device__ __forceinline__ void chain_mfma_r(f32x16 (&acc)[2], const f32x4 &a0, const f32x4 &a1,
+                                             const f32x4 (&w)[2][2]) {
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
         const float av = (p < 4 ? a0 : a1)[p & 3];
@@ -414,12 +414,25 @@ __device__ __forceinline__ void chain_mfma(f32x16 (&acc)[2], const float *ap, in
     }
 }
 
+__device__ __forceinline__ void chain_mfma(f32x16 (&acc)[2], const float *ap, int t, const f32x4 (&w)[2][2]) {
+    const float *pa = ap + 32 * (t >> 1) + 8 * (t & 1);
+    chain_mfma_r(acc, *(const f32x4 *)pa, *(const f32x4 *)(pa + 4), w);
+}
+
+// x2 (shortcut) operand of half step t >= BN / 16: k2 = 32 (t >> 1) + 16 hh + 8 (t & 1) - BN of the
+// lane's strided pixel (16 hh is in voff).  With no x2 the resource has 0 records: the load returns 0.
+__device__ __forceinline__ void chain_load_x(__amdgpu_buffer_rsrc_t rx, int voff, int t, int bn, f32x4 (&x)[2]) {
+    const int so = (32 * (t >> 1) + 8 * (t & 1) - bn) * 4;
+    x[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, so, 0));
+    x[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, voff, so + 16, 0));
+}
+
 template <int WM, int WN, int TM, int TN>
 __device__ __forceinline__ void chain_epilogue(const ConvArgs &a, float *lds, const f32x16 (&acc)[TM][TN], int wm,
                                                int wn, int lane, int64_t m0) {
     static_assert(TM == 1 && TN == 2, "chain epilogue: each wave owns 32 rows x 64 channels of h2");
     constexpr int BM = WM * 32, BN = WN * 64, LA = BN + 4;  // h2 image [BM][LA]: 4 LA B = odd 16-B slot count
-    constexpr int HS = BN / 16;                              // 16-deep half steps per 64-column chunk (K2 = BN)
+    constexpr int HS = BN / 16;                              // 16-deep half steps of the h2 part (K = BN)
     const int r32 = lane & 31, hh = lane >> 5;
     __syncthreads();  // every wave is done with the staging buffers
 #pragma unroll
@@ -445,10 +458,24 @@ __device__ __forceinline__ void chain_epilogue(const ConvArgs &a, float *lds, co
     const __amdgpu_buffer_rsrc_t rw = chain_rsrc(a.wp2, (int64_t)copad(a.Co2) * a.Kp2 * 4);
     const int vw = (r32 * a.Kp2 + 16 * hh) * 4;                // lane part of a W2 address
     const int vo = ((wm * 32 + 4 * hh) * a.Co2 + r32) * 4;     // lane part of a res / y address
-    f32x4 wA[2][2], wB[2][2];
+    // dual (downsample shortcut): K2 = [h2 | x2 at the lane row's strided pixel], x2 [N][H2][W2][Ci2]
+    const int hs2 = a.x2 ? a.Ci2 / 16 : 0;
+    __amdgpu_buffer_rsrc_t rx = chain_rsrc(a.y, 0);
+    int vx = 0;
+    if (a.x2) {
+        int64_t m = m0 + wm * 32 + r32;
+        m = m < a.M ? m : a.M - 1;
+        const int ox = (int)(m % a.Wo);
+        const int64_t q = m / a.Wo;
+        const int oy = (int)(q % a.Ho);
+        const int64_t n = q / a.Ho;
+        rx = chain_rsrc(a.x2, (int64_t)a.N * a.H2 * a.W2 * a.Ci2 * 4);
+        vx = (int)((((n * a.H2 + (int64_t)oy * a.stride2) * a.W2 + (int64_t)ox * a.stride2) * a.Ci2 + 16 * hh) * 4);
+    }
+    f32x4 wA[2][2], wB[2][2], xA[2], xB[2];
     chain_load_b(rw, a.Kp2, vw, cb, 0, wA);
     for (int nc = 0; nc < nch; ++nc) {
-        const int c0 = cb + 64 * nc;
+        const int c0 = cb + 64 * nc, cn = nc + 1 < nch ? c0 + 64 : c0;  // next chunk (clamped)
         float rv[2][16];
         if (a.res) {
 #pragma unroll
@@ -456,19 +483,35 @@ __device__ __forceinline__ void chain_epilogue(const ConvArgs &a, float *lds, co
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
                     rv[j][r] = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(
-                                   rr, vo, (((r & 3) + 8 * (r >> 2)) * a.Co2 + c0 + 32 * j) * 4, 0));
+                        float, __builtin_amdgcn_raw_buffer_load_b32(rr, vo + ((r & 3) + 8 * (r >> 2)) * a.Co2 * 4,
+                                                                    (c0 + 32 * j) * 4, 0));
         }
         f32x16 acc2[2] = {(f32x16){0}, (f32x16){0}};
 #pragma unroll
         for (int t = 0; t < HS; t += 2) {
             chain_load_b(rw, a.Kp2, vw, c0, t + 1, wB);
             chain_mfma(acc2, ap, t, wA);
-            // after the chunk's last half step: the next chunk's first (clamped: the load is unconditional)
+            // after the h2 part's last half step: the x2 part's first, or the next chunk's first
+            // (unconditional loads: clamped chunk; x2 loads read 0 without an x2)
             const bool lst = (t + 2 == HS);
-            chain_load_b(rw, a.Kp2, vw, lst ? (nc + 1 < nch ? c0 + 64 : c0) : c0, lst ? 0 : t + 2, wA);
+            if (lst) {
+                chain_load_b(rw, a.Kp2, vw, hs2 ? c0 : cn, hs2 ? HS : 0, wA);
+                chain_load_x(rx, vx, HS, BN, xA);
+            } else {
+                chain_load_b(rw, a.Kp2, vw, c0, t + 2, wA);
+            }
             chain_mfma(acc2, ap, t + 1, wB);
             __builtin_amdgcn_sched_barrier(0);  // one half step of W2 in flight (VGPR budget of 3 blocks / CU)
+        }
+        for (int t = HS; t < HS + hs2; t += 2) {
+            chain_load_b(rw, a.Kp2, vw, c0, t + 1, wB);
+            chain_load_x(rx, vx, t + 1, BN, xB);
+            chain_mfma_r(acc2, xA[0], xA[1], wA);
+            const bool lst = (t + 2 == HS + hs2);
+            chain_load_b(rw, a.Kp2, vw, lst ? cn : c0, lst ? 0 : t + 2, wA);
+            chain_load_x(rx, vx, lst ? t + 1 : t + 2, BN, xA);
+            chain_mfma_r(acc2, xB[0], xB[1], wB);
+            __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -478,8 +521,8 @@ __device__ __forceinline__ void chain_epilogue(const ConvArgs &a, float *lds, co
                 float o = acc2[j][r] + bj;
                 if (a.res) o += rv[j][r];
                 if (a.relu2) o = act_fn(o, a.relu2);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry, vo,
-                                                      (((r & 3) + 8 * (r >> 2)) * a.Co2 + c0 + 32 * j) * 4, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry,
+                                                      vo + ((r & 3) + 8 * (r >> 2)) * a.Co2 * 4, (c0 + 32 * j) * 4, 0);
             }
         }
     }
@@ -1250,6 +1293,63 @@ int bev_conv2d_chain_f32(const float *x, int N, int H, int W, int Ci, const floa
     a.Co2 = Co2;
     a.Kp2 = (int)kpad(Co);
     a.relu2 = relu2;
+    a.x2 = nullptr;
+    a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    return launch_chain(a, (hipStream_t)stream);
+}
+
+int bev_conv2d_chain_dual_f32(const float *x, int N, int H, int W, int Ci, const float *packed, const float *bias,
+                              int Co, int KH, int KW, int stride, int pad, int relu, const float *x2, int H2, int W2,
+                              int Ci2, int stride2, const float *packed2, const float *bias2, int Co2, int relu2,
+                              float *y, int Ho, int Wo, void *stream) {
+    if (!x2 || Ci2 <= 0 || Ci2 % BK != 0 || H2 <= 0 || W2 <= 0 || stride2 <= 0 || ((uintptr_t)x2 & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H2 - 1) / stride2 + 1 || Wo != (W2 - 1) / stride2 + 1) return BEV_ERR_ARGS;
+    if ((int64_t)N * H2 * W2 * Ci2 * 4 > (int64_t)0xffffffff) return BEV_ERR_ARGS;  // 32-bit buffer offsets
+    // validate / fill the common part through the plain entry point's checks, then launch with x2
+    if (!x || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+        pad < 0 || relu < 0 || relu > 2 || relu2 < 0 || relu2 > 2)
+        return BEV_ERR_ARGS;
+    if (Ci % BK != 0 || (Co != 64 && Co != 128) || Co2 <= 0 || Co2 % 128 != 0 || ((uintptr_t)x & 15) != 0 ||
+        (((uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvArgs a{};
+    a.x = x;
+    a.wp = packed;
+    a.bias = bias;
+    a.res = nullptr;
+    a.y = y;
+    a.N = N;
+    a.H = H;
+    a.W = W;
+    a.Ci = Ci;
+    a.Co = Co;
+    a.KH = KH;
+    a.KW = KW;
+    a.stride = stride;
+    a.pad = pad;
+    a.Ho = Ho;
+    a.Wo = Wo;
+    a.relu = relu;
+    a.M = (int64_t)N * Ho * Wo;
+    a.K = Ci * KH * KW;
+    a.Kp = (int)kpad(a.K);
+    a.dil = 1;
+    a.ldy = Co2;
+    a.xcd = conv_xcd();
+    a.wp2 = packed2;
+    a.bias2 = bias2;
+    a.Co2 = Co2;
+    a.Kp2 = (int)kpad(Co + Ci2);
+    a.relu2 = relu2;
+    a.x2 = x2;
+    a.Ci2 = Ci2;
+    a.H2 = H2;
+    a.W2 = W2;
+    a.stride2 = stride2;
     return launch_chain(a, (hipStream_t)stream);
 }
 

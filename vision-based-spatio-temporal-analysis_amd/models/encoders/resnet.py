@@ -193,6 +193,36 @@ class FoldedChain:
                                       self.c3.bias, self.c3.conv.out_channels, _nat.ACT_RELU, residual=x, out=out)
 
 
+class FoldedChainTail:
+    """Bottleneck conv2/bn2/act2 -> [conv3/bn3 + downsample conv/bn] -> act3 as ONE launch (block 0).
+
+    bev_conv2d_chain_dual_f32: conv2's output stays in LDS and the dual-source 1x1 GEMM of
+    FoldedTail (K = [h2 | x[::s]]) runs on it.  Bit-identical to conv2 followed by FoldedTail.
+    """
+
+    def __init__(self, c2: FoldedConv, tail: FoldedTail):
+        self.c2, self.tail = c2, tail
+
+    @staticmethod
+    def applies(blk) -> bool:
+        c2 = blk.conv2
+        # the shortcut operand streams from L2 once per 64-column chunk: measured (r02k, 7 x 1080p ResNet-50)
+        # layer1 block 0 (64-channel shortcut) 1333 -> 1203 us, layer2 block 0 (256 channels) 1335 -> 1440 us
+        return (FoldedTail.applies(blk) and blk.downsample[0].in_channels <= c2.out_channels
+                and c2.out_channels in (64, 128) and c2.in_channels % 32 == 0
+                and c2.kernel_size[0] == c2.kernel_size[1] and c2.dilation == (1, 1) and c2.groups == 1
+                and blk.conv3.out_channels % 128 == 0)
+
+    def __call__(self, h, x, out=None):
+        self.c2.prepare(h.device)
+        self.tail.prepare(h.device)
+        c2 = self.c2.conv
+        return _nat.conv2d_chain_dual_nhwc(h, self.c2.packed, self.c2.bias, c2.out_channels, c2.kernel_size[0],
+                                           c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU, x,
+                                           self.tail.short.conv.stride[0], self.tail.packed, self.tail.bias,
+                                           self.tail.main.conv.out_channels, _nat.ACT_RELU, out=out)
+
+
 def stage_of(out_index: int) -> int:
     """features_only index -> number of residual stages to run (0: act1, 1: layer1, ...)."""
     return max(0, out_index)
@@ -361,6 +391,12 @@ class ResNet(nn.Module):
         if isinstance(blk, Bottleneck) and self.fuse_chain and FoldedChain.applies(blk):
             h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
             return self._chain(blk)(h, x, out=out)
+        if isinstance(blk, Bottleneck) and self.fuse_chain and self.fuse_shortcut and FoldedChainTail.applies(blk):
+            k = ("chaintail", id(blk))
+            if k not in self._folded:
+                self._folded[k] = FoldedChainTail(self._fc(blk.conv2, blk.bn2), self._tail(blk))
+            h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
+            return self._folded[k](h, x, out=out)
         if isinstance(blk, Bottleneck) and self.fuse_shortcut and FoldedTail.applies(blk):
             h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
             h = self._fc(blk.conv2, blk.bn2)(h, relu=True)
