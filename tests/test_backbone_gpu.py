@@ -77,6 +77,35 @@ def test_conv_every_tile_vs_torch_fp32(case, tile):
         nat.tune(1, old)
 
 
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("case", [CASES[4], CASES[5], CASES[6], CASES[7], CASES[8], CASES[9], CASES[10]],
+                         ids=["l1c2_res", "l1c3_res", "1x1", "s2_3x3", "s2_1x1", "proj", "ragged_co"])
+def test_conv_lds_dma_bit_exact_vs_register_staging(case, tile):
+    """BEV_TUNE_CONV_DMA: operands staged global -> LDS by LDS-DMA (k_conv_dma, swizzled 128-B rows) ==
+    staged through registers (k_conv), bit for bit, on every tile shape (same MFMA order)."""
+    import bev_native as nat
+    N, Ci, H, W, Co, k, s, p, nchw, resid, relu = case
+    x = _rand((N, H, W, Ci), 41).to(DEV)
+    w = _rand((Co, Ci, k, k), 42, scale=(2.0 / (Ci * k * k)) ** 0.5).to(DEV)
+    b = _rand((Co,), 43).to(DEV)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    r = _rand((N, Ho, Wo, Co), 44).to(DEV) if resid else None
+    packed = nat.pack_conv_weight(w)
+    outs = []
+    old_t = nat.tune(nat.TUNE_CONV_TILE, tile)
+    try:
+        for dma in (0, 2):
+            old = nat.tune(nat.TUNE_CONV_DMA, dma)
+            try:
+                outs.append(nat.conv2d_nhwc(x, packed, b, Co, k, k, s, p, relu, residual=r))
+            finally:
+                nat.tune(nat.TUNE_CONV_DMA, old)
+    finally:
+        nat.tune(nat.TUNE_CONV_TILE, old_t)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 DUAL_CASES = [
     # N, Ci (conv3 input), Ci2 (block input), H2, W2, s2, Co
     (2, 64, 64, 17, 23, 1, 256),     # layer1 block 0: conv3 64->256 + downsample 64->256
@@ -131,9 +160,14 @@ def test_conv_chain_bit_exact_vs_two_launches(case):
     pk1, pk2 = nat.pack_conv_weight(w1.to(DEV)), nat.pack_conv_weight(w2.to(DEV))
     h = nat.conv2d_nhwc(xin, pk1, b1.to(DEV), Co, k, k, s, p, True)
     two = nat.conv2d_nhwc(h, pk2, b2.to(DEV), Co2, 1, 1, 1, 0, True, residual=rin)
-    one = nat.conv2d_chain_nhwc(xin, pk1, b1.to(DEV), Co, k, k, s, p, 1, pk2, b2.to(DEV), Co2, 1, residual=rin)
-    torch.cuda.synchronize()
-    assert torch.equal(one.view(torch.int32), two.view(torch.int32))
+    for dma in (0, 2):  # chain kernel with register-staged and LDS-DMA operands
+        old = nat.tune(nat.TUNE_CONV_DMA, dma)
+        try:
+            one = nat.conv2d_chain_nhwc(xin, pk1, b1.to(DEV), Co, k, k, s, p, 1, pk2, b2.to(DEV), Co2, 1, residual=rin)
+        finally:
+            nat.tune(nat.TUNE_CONV_DMA, old)
+        torch.cuda.synchronize()
+        assert torch.equal(one.view(torch.int32), two.view(torch.int32)), dma
     ref = F.conv2d(F.relu(F.conv2d(x, w1, b1, s, p)), w2, b2)
     ref = F.relu(ref + r if resid else ref)
     np.testing.assert_allclose(one.permute(0, 3, 1, 2).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)

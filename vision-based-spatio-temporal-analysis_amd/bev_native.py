@@ -154,6 +154,7 @@ TUNE_WARP_BWD_POOL = 5
 TUNE_CONV_XCD = 6
 TUNE_CONV_NBUF = 7
 TUNE_WGRAD_MFMA = 8
+TUNE_CONV_DMA = 9
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 

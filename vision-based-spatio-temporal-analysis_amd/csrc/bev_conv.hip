@@ -373,6 +373,82 @@ __device__ __forceinline__ void store_rows(float *p, const f32x4 (&v)[R]) {
     for (int r = 0; r < R; ++r) *(f32x4 *)(p + 32 * r * LROW) = v[r];
 }
 
+// Standard epilogue: the wave's (TM*32) x (TN*32) accumulator tile goes to LDS (4 * 32 TM x (32 TN + 4)
+// floats for the block; the caller sizes its LDS for it), then every lane issues ALL its residual float4
+// loads at once (deep memory parallelism for the memory-bound 1x1 layers), combines and stores whole
+// float4 row pieces.
+template <int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs &a, float *lds, const f32x16 (&acc)[TM][TN], int wave,
+                                              int lane, int wm, int wn, int64_t m0, int n0) {
+    const int r32 = lane & 31, h = lane >> 5;
+    // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
+    constexpr int WR = TM * 32, WC = TN * 32, ER = WC + 4;  // wave tile, LDS row stride
+    constexpr int C4 = WC / 4;                              // float4 per row
+    constexpr int RPI = 64 / C4;                            // rows per wave-instruction
+    constexpr int NQ = WR / RPI;                            // float4 per lane
+    __syncthreads();  // every wave is done reading the staging buffers
+    float *E = lds + wave * (WR * ER);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) E[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
+    // same-wave LDS ops complete in order: no barrier needed
+    const int c4 = lane % C4, rq = lane / C4;
+    const int n = n0 + wn * WC + c4 * 4;
+    const bool nvec = ((a.Co & 3) == 0) && ((a.ldy & 3) == 0) && (n + 3 < a.Co);
+    const int64_t mbase = m0 + wm * WR;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.bias) {
+        if (nvec) bv = *(const float4 *)(a.bias + n);
+        else {
+            bv.x = n < a.Co ? a.bias[n] : 0.f;
+            bv.y = n + 1 < a.Co ? a.bias[n + 1] : 0.f;
+            bv.z = n + 2 < a.Co ? a.bias[n + 2] : 0.f;
+            bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
+        }
+    }
+    float4 rv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int64_t m = mbase + rq + RPI * q;
+        rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int row = rq + RPI * q;
+        const int64_t m = mbase + row;
+        if (m >= a.M) continue;
+        const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
+        float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
+        float *yp = a.y + m * a.ldy + n;
+        if (nvec) {
+            if (a.res) {
+                o[0] += rv[q].x;
+                o[1] += rv[q].y;
+                o[2] += rv[q].z;
+                o[3] += rv[q].w;
+            }
+            if (a.relu) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o[u] = act_fn(o[u], a.relu);
+            }
+            *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (n + u >= a.Co) break;
+                float t = o[u];
+                if (a.res) t += a.res[m * a.Co + n + u];
+                if (a.relu) t = act_fn(t, a.relu);
+                yp[u] = t;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Chained pointwise epilogue (EPI 1; bev_conv2d_chain_f32)
 // ---------------------------------------------------------------------------
@@ -676,77 +752,168 @@ __global__ __launch_bounds__(256, NBUF == 1 ? 3 : 2) void k_conv(ConvArgs a) {
         return;
     }
 
-    // ---- epilogue through LDS ---------------------------------------------------
-    // The wave's (TM*32) x (TN*32) accumulator tile goes to LDS, then every lane
-    // issues ALL its residual float4 loads at once (deep memory parallelism for
-    // the memory-bound 1x1 layers), combines and stores whole float4 row pieces.
-    // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5).
-    constexpr int WR = TM * 32, WC = TN * 32, ER = WC + 4;  // wave tile, LDS row stride
-    constexpr int C4 = WC / 4;                              // float4 per row
-    constexpr int RPI = 64 / C4;                            // rows per wave-instruction
-    constexpr int NQ = WR / RPI;                            // float4 per lane
-    static_assert(4 * WR * ER <= LDSF, "epilogue tile must fit the staging LDS");
-    __syncthreads();  // every wave is done reading the staging buffers
-    float *E = lds + wave * (WR * ER);
+    conv_epilogue<TM, TN>(a, lds, acc, wave, lane, wm, wn, m0, n0);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA operand path (NHWC, Ci % 32 == 0: the fast loader's layers): k_conv_dma
+// ---------------------------------------------------------------------------
+// Same tiles, MFMA order (bit-identical results) and epilogues as k_conv<.., LOADER 1, ..>; the K-step
+// operands go global -> LDS by global_load_lds_dwordx4 instead of through registers: no staging VGPRs,
+// no ds_write, double-buffered, one barrier per K step.  One DMA instruction moves 8 rows x 32 k
+// (1 KiB) and writes lane l's 16 B at slot l, so rows are 128 B with no padding; the 16-B chunk c of
+// row r is stored at chunk c ^ ((r >> 1) & 7) (each lane fetches the logical chunk its slot holds),
+// which makes the fragment reads conflict-free: every 16-lane ds_read_b128 group covers 8 even and
+// 8 odd rows whose swizzles are all distinct.  Out-of-range taps and rows read a zero quad.
+__device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)p;
+}
+
+__device__ __forceinline__ void lds_dma16(const float *src, unsigned dst_any) {
+    const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)dst_any);  // wave-uniform LDS address
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(dst)
+        : "memory");
+}
+
+template <int WM, int WN, int TM, int TN, int CHAIN>
+__global__ __launch_bounds__(256, (TM * TN > 2) ? 2 : 3) void k_conv_dma(ConvArgs a) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int STAGE = (BM + BN) * 32;  // floats per stage
+    constexpr int EPI = 4 * (TM * 32) * (TN * 32 + 4);
+    constexpr int CHT = CHAIN ? WM * 32 * (WN * TN * 32 + 4) : 0;
+    constexpr int L0 = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+    constexpr int LDSF = CHT > L0 ? CHT : L0;
+    constexpr int NA = BM / 8, NB = BN / 8;  // DMA instructions (1 KiB) per stage for A and B
+    constexpr int QA = NA / 4, QB = NB / 4;  // per wave
+    static_assert(NA % 4 == 0 && NB % 4 == 0, "whole DMA instructions per wave");
+    __shared__ __attribute__((aligned(16))) float lds[LDSF];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int n_tiles = (a.Co + BN - 1) / BN;
+    unsigned bid = blockIdx.x;
+    if (a.xcd) {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, x = bid % 8;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    }
+    const int64_t m0 = (int64_t)(bid / n_tiles) * BM;
+    const int n0 = (bid % n_tiles) * BN;
+
+    // this lane's DMA slots: instruction i = wave + 4 q, row 8 i + lane / 8 (of the A or the B tile),
+    // logical chunk (lane & 7) ^ ((row >> 1) & 7)
+    const int rsub = lane >> 3;
+    int64_t abase[QA];  // element offset of (image, iy0, ix0) + chunk, valid only with the tap in range
+    int aiy[QA], aix[QA];
+    bool aok[QA];
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+        const int row = 8 * (wave + 4 * q) + rsub;
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int64_t m = m0 + row;
+        aok[q] = m < a.M;
+        const int64_t mm = aok[q] ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int64_t n = t / a.Ho;
+        aiy[q] = oy * a.stride - a.pad;
+        aix[q] = ox * a.stride - a.pad;
+        abase[q] = ((n * a.H + aiy[q]) * a.W + aix[q]) * a.Ci + 4 * c;
+    }
+    const float *bsrc[QB];
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+        const int row = 8 * (wave + 4 * q) + rsub;
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        bsrc[q] = a.wp + (int64_t)(n0 + row) * a.Kp + 4 * c;
+    }
+    const unsigned lbase = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_base((const unsigned char *)lds));
+    int ky = 0, kx = 0, ci0 = 0, kb = 0;
+    auto issue = [&](int buf) {
+        const unsigned d0 = lbase + (unsigned)(buf * STAGE * 4);
+        const int64_t toff = ((int64_t)ky * a.W + kx) * a.Ci + ci0;
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int iy = aiy[q] + ky, ix = aix[q] + kx;
+            const bool in = aok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            lds_dma16(in ? a.x + abase[q] + toff : g_zero4, d0 + (unsigned)((wave + 4 * q) * 1024));
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q)
+            lds_dma16(bsrc[q] + kb, d0 + (unsigned)((NA + wave + 4 * q) * 1024));
+        kb += BK;
+        ci0 += BK;
+        if (ci0 == a.Ci) {
+            ci0 = 0;
+            if (++kx == a.KW) {
+                kx = 0;
+                ++ky;
+            }
+        }
+    };
+
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    const int r32 = lane & 31, h = lane >> 5, sw = (r32 >> 1) & 7;
+    // fragment chunk offsets (floats) of half 0 / 1: logical chunks 4 h + 2 half + {0, 1}
+    const int f00 = ((4 * h) ^ sw) * 4, f01 = ((4 * h + 1) ^ sw) * 4;
+    const int f10 = ((4 * h + 2) ^ sw) * 4, f11 = ((4 * h + 3) ^ sw) * 4;
+
+    const int nk = a.Kp / BK;
+    issue(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+        const int cur = ks & 1;
+        if (ks + 1 < nk) issue(cur ^ 1);
+        const float *As = lds + cur * STAGE;
+        const float *Bs = As + BM * 32;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) E[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
-    // same-wave LDS ops complete in order: no barrier needed
-    const int c4 = lane % C4, rq = lane / C4;
-    const int n = n0 + wn * WC + c4 * 4;
-    const bool nvec = ((a.Co & 3) == 0) && ((a.ldy & 3) == 0) && (n + 3 < a.Co);
-    const int64_t mbase = m0 + wm * WR;
-    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (a.bias) {
-        if (nvec) bv = *(const float4 *)(a.bias + n);
-        else {
-            bv.x = n < a.Co ? a.bias[n] : 0.f;
-            bv.y = n + 1 < a.Co ? a.bias[n + 1] : 0.f;
-            bv.z = n + 2 < a.Co ? a.bias[n + 2] : 0.f;
-            bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
-        }
-    }
-    float4 rv[NQ];
+        for (int half = 0; half < 2; ++half) {
+            const int o0 = half ? f10 : f00, o1 = half ? f11 : f01;
+            f32x4 fa[TM][2], fb[TN][2];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int64_t m = mbase + rq + RPI * q;
-        rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int row = rq + RPI * q;
-        const int64_t m = mbase + row;
-        if (m >= a.M) continue;
-        const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
-        float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
-        float *yp = a.y + m * a.ldy + n;
-        if (nvec) {
-            if (a.res) {
-                o[0] += rv[q].x;
-                o[1] += rv[q].y;
-                o[2] += rv[q].z;
-                o[3] += rv[q].w;
+            for (int i = 0; i < TM; ++i) {
+                const float *pa = As + (wm * TM * 32 + i * 32 + r32) * 32;
+                fa[i][0] = *(const f32x4 *)(pa + o0);
+                fa[i][1] = *(const f32x4 *)(pa + o1);
             }
-            if (a.relu) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) o[u] = act_fn(o[u], a.relu);
+            for (int j = 0; j < TN; ++j) {
+                const float *pb = Bs + (wn * TN * 32 + j * 32 + r32) * 32;
+                fb[j][0] = *(const f32x4 *)(pb + o0);
+                fb[j][1] = *(const f32x4 *)(pb + o1);
             }
-            *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (n + u >= a.Co) break;
-                float t = o[u];
-                if (a.res) t += a.res[m * a.Co + n + u];
-                if (a.relu) t = act_fn(t, a.relu);
-                yp[u] = t;
+            for (int p = 0; p < 8; ++p) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const float av = fa[i][p >> 2][p & 3];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const float bv = fb[j][p >> 2][p & 3];
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+                    }
+                }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step ks + 1 landed
+        __syncthreads();                                   // all of it; buffer cur is free again
     }
+    if constexpr (CHAIN == 1) {
+        chain_epilogue<WM, WN, TM, TN>(a, lds, acc, wm, wn, lane, m0);
+        return;
+    }
+    conv_epilogue<TM, TN>(a, lds, acc, wave, lane, wm, wn, m0, n0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1004,6 +1171,12 @@ __global__ void k_transpose(const float *__restrict__ x, int R, int S, float *__
 
 inline int last() { return (int)hipGetLastError(); }
 
+// BEV_TUNE_CONV_DMA: fast-loader layers stage their operands by LDS-DMA (k_conv_dma).  1 = on the 64-column
+// tiles only: r02l A/B over the ResNet-50 layers (7 x 1080p), LDS-DMA vs register staging: 128 x 64 and 64 x 64
+// tiles (layer1) -1..-4 %, 64 x 128 tiles (layer2) +1..+3 %.  2 = every tile, 0 = none.
+int g_conv_dma = 1;
+inline bool use_dma(int bn) { return g_conv_dma == 2 || (g_conv_dma == 1 && bn == 64); }
+
 template <int WM, int WN, int TM, int TN, int NBUF = 2>
 int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -1012,7 +1185,8 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     const int64_t blocks = m_tiles * n_tiles;
     if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
     const dim3 g((unsigned)blocks), b(256);
-    if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1, NBUF>), g, b, 0, st, a);
+    if (loader == 1 && use_dma(BN)) hipLaunchKernelGGL((k_conv_dma<WM, WN, TM, TN, 0>), g, b, 0, st, a);
+    else if (loader == 1) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 1, NBUF>), g, b, 0, st, a);
     else if (loader == 2) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 2, NBUF>), g, b, 0, st, a);
     else if (loader == 3) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 3, NBUF>), g, b, 0, st, a);
     else if (loader == 4) hipLaunchKernelGGL((k_conv<WM, WN, TM, TN, 4, NBUF>), g, b, 0, st, a);
@@ -1081,7 +1255,10 @@ int launch_chain(const ConvArgs &a, hipStream_t st) {
     const int64_t blocks = (a.M + bm - 1) / bm;
     if (blocks > 0x7fffffff) return BEV_ERR_ARGS;
     const dim3 g((unsigned)blocks), b(256);
-    if (a.Co == 64) hipLaunchKernelGGL((k_conv<4, 1, 1, 2, 1, 1, 1>), g, b, 0, st, a);
+    if (use_dma(a.Co)) {
+        if (a.Co == 64) hipLaunchKernelGGL((k_conv_dma<4, 1, 1, 2, 1>), g, b, 0, st, a);
+        else hipLaunchKernelGGL((k_conv_dma<2, 2, 1, 2, 1>), g, b, 0, st, a);
+    } else if (a.Co == 64) hipLaunchKernelGGL((k_conv<4, 1, 1, 2, 1, 1, 1>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_conv<2, 2, 1, 2, 1, 1, 1>), g, b, 0, st, a);
     return last();
 }
@@ -1095,6 +1272,12 @@ int bev_tune(int knob, int value) {
         if (value < 0 || value > 4) return BEV_ERR_ARGS;
         const int old = g_conv_tile;
         g_conv_tile = value;
+        return old;
+    }
+    if (knob == BEV_TUNE_CONV_DMA) {
+        if (value < 0 || value > 2) return BEV_ERR_ARGS;
+        const int old = g_conv_dma;
+        g_conv_dma = value;
         return old;
     }
     if (knob == BEV_TUNE_CONV_XCD || knob == BEV_TUNE_CONV_NBUF) {
