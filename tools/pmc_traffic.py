@@ -1,6 +1,6 @@
 """Per-launch HBM traffic of the bench's dominant kernels from rocprofv3 --pmc passes.
 
-Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [--steps-key k_stem]
+Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> <out.json> [stem_launches_per_step]
 
 Inputs are the run_counter_collection.csv files of two separate passes
 (`--pmc FETCH_SIZE` and `--pmc WRITE_SIZE`) over the same `bench.py` command.
@@ -9,7 +9,9 @@ FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced reads, so it
 is doubled.  WRITE_SIZE is exact for 16-B/lane stores; the warp's 4-B/lane
 stores are uncalibrated (noted in the output).
 The conv figure is per bench step (all backbone conv launches of one frame,
-steps counted by the stem launches); the warp figure is per launch.
+steps counted by the stem launches: one per image group, ResNet.stream_groups = 2 by
+default); the warp figure is per launch.  The chained bottleneck kernels store 4 B/lane
+(their WRITE_SIZE share is uncalibrated, like the warp's).
 """
 import csv
 import json
@@ -27,6 +29,7 @@ def family(name: str) -> str:
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    groups = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     tot = defaultdict(float)
     n = defaultdict(int)
     steps = 0
@@ -40,6 +43,7 @@ def main():
                 n[fam] += 1
                 steps += "k_stem" in r["Kernel_Name"]
     res = {}
+    steps //= groups
     for fam, per in (("conv", steps), ("warp", n["warp"])):
         if per == 0:
             continue
@@ -48,7 +52,8 @@ def main():
         res[fam] = {"fetch_bytes": round(fetch), "write_bytes": round(write), "traffic_bytes": round(fetch + write),
                     "per": "bench step" if fam == "conv" else "launch", "samples": per}
     res["note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950 wide-read "
-                   "correction), KiB -> bytes; warp stores are 4 B/lane (WRITE_SIZE uncalibrated for that width)")
+                   "correction), KiB -> bytes; warp and chained-conv stores are 4 B/lane (WRITE_SIZE uncalibrated for "
+                   "that width)")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
