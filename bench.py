@@ -4,7 +4,9 @@ Workload = BASELINE.json configs[1] (default): Wildtrack-shaped 7 cameras x 3 x
 1080 x 1920 fp32 images -> ResNet-50 (timm features_only, out_index=2, stride
 8) -> 1x1 proj to C=64 -> IPM warp onto the 480x1440 ground grid -> mean
 fusion over views.  One step = one batch of B frames through that whole hot
-path (CNNEncoder.forward + GeometryTransformer.forward_fused), inputs resident
+path (CNNEncoder.forward + GeometryTransformer.forward_fused); B = 2 by default,
+the reference's own Wildtrack inference batch (inference.py:27 builds its
+DataLoader with cfg['DATA']['BATCH_SIZE'], configs/wildtrack.yaml:2 = 2); inputs resident
 in HBM, random-init weights of that architecture, synthetic images, the fixed
 Appendix-B camera rig.
 
@@ -59,7 +61,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (rank processes) of this node; default 1")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1, help="frames per GPU per step (frame-sharded configs)")
+    ap.add_argument("--batch", type=int, default=2, help="frames per GPU per step (frame-sharded configs); default 2 = "
+                    "the reference's Wildtrack inference batch (inference.py:27 DataLoader(batch_size=cfg['DATA']"
+                    "['BATCH_SIZE']), configs/wildtrack.yaml:2 BATCH_SIZE: 2)")
     ap.add_argument("--views", type=int, default=None, help="cameras (default 7; 16 with --camera-shard)")
     ap.add_argument("--channels", type=int, default=64)
     ap.add_argument("--backbone", default="resnet50")
@@ -204,7 +208,7 @@ def pmc_traffic(args) -> dict:
     file's numbers (named in `traffic_source`), not counters read by this run."""
     default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone,
                args.camera_shard, args.warp_kernel) == \
-        (7, 64, (1080, 1920), (480, 1440), 1, "resnet50", False, "dma")
+        (7, 64, (1080, 1920), (480, 1440), 2, "resnet50", False, "dma")
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
     if not default or not files:
         return {}
@@ -383,6 +387,9 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{wl} ({label})", "baseline_config": label,
                        "frames_per_gpu_per_step": None if args.camera_shard else B,
+                       "batch_source": ("camera-sharded: one frame per step" if args.camera_shard else
+                                        "reference inference batch: inference.py:27, configs/wildtrack.yaml:2"
+                                        if B == 2 else "--batch"),
                        "frames_per_step": B if args.camera_shard else world * B, "cameras": V,
                        "cameras_per_gpu": VL, "bev": list(args.bev), "channels": C,
                        "parallelism": (f"camera-sharded x{world} (reduce-scatter over BEV rows)" if args.camera_shard
