@@ -464,6 +464,70 @@ def test_dwconv_wgrad_and_channel_ops_vs_torch(case):
     assert torch.equal(aff, x.permute(0, 2, 3, 1) * a[:, None, None, :] + b[:, None, None, :])
 
 
+def _bevnet_ddp_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # both ranks share the box's one GPU
+    try:
+        import bev_dist
+        import bev_rig
+        from models.model_wrapper import BEVNet
+        torch.manual_seed(100 + rank)  # different init per rank: DDP must broadcast rank 0's parameters
+        B, V, H, W = 2, 3, 128, 224
+        K, Rt = bev_rig.rig(V, H, W, B)
+        g = torch.Generator().manual_seed(1)
+        imgs = torch.randn(B, V, 3, H, W, generator=g)
+        boxes = [torch.tensor([[1.0, 0.5, 0.6, 0.6], [-3.0, 2.0, 0.6, 0.6]]), torch.tensor([[4.0, -1.0, 0.6, 0.6]])]
+        sl = bev_dist.frame_shard(B, rank, world)
+        batch = {"images": imgs[sl.start:sl.stop].to(DEV),
+                 "calib": {"intrinsic": torch.from_numpy(K[sl.start:sl.stop]).to(DEV),
+                           "extrinsic": torch.from_numpy(Rt[sl.start:sl.stop]).to(DEV)}}
+        targets = [{"boxes_world": b.to(DEV)} for b in boxes[sl.start:sl.stop]]
+        model = BEVNet(_bevnet_cfg()).to(DEV)
+        model.encoder.freeze()
+        bev_dist.materialize_lazy(model, batch)
+        ddp = bev_dist.ddp_wrap(model, torch.device(DEV))
+        # parameters only: BN running statistics are per-rank buffers (ddp_wrap: broadcast_buffers=False; each
+        # rank's train-mode BatchNorm sees its own frame)
+        init = {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters()}
+        opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-3)
+        model.train()
+        losses = [bev_dist.train_step(ddp, batch, targets, opt)["total_loss"] for _ in range(2)]
+        q.put((rank, init, {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters()}, losses))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bevnet_ddp_world2_replicas_identical():
+    """The real BEVNet (native encoder / warp / head) under DDP at world 2: two rank processes, one frame each,
+    gradients all-reduced (gloo; both ranks on the box's single GPU).  Rank 0's parameters are broadcast at
+    wrap time and both replicas' parameters are bit-identical after the steps; the trainable ones moved."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bevnet_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, init, after, losses = q.get(timeout=240)
+        res[r] = (init, after, losses)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    moved = 0
+    for k in res[0][0]:
+        assert np.array_equal(res[0][0][k], res[1][0][k]), k  # broadcast from rank 0
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k  # identical replicas after the steps
+        moved += not np.array_equal(res[0][0][k], res[0][1][k])
+    assert moved > 0
+    assert all(np.isfinite(res[r][2]).all() for r in (0, 1))
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(240)
 @pytest.mark.parametrize("bn_mode", ["batch", "frozen"])

@@ -8,8 +8,8 @@ freeze() runs), this autograd Function keeps the data path native:
 
   forward   y  = x (*) W + b          bev_conv2d_f32 (1x1, NHWC)
   backward  dX = dY (*) W^T           bev_conv2d_f32 with the transposed panel
-            dW = dY^T X, db = sum dY  plain library GEMM / reduction (rocBLAS /
-                                      hipBLASLt through torch.matmul)
+            dW = dY^T X               bev_conv_wgrad_f32 (1x1: MFMA GEMM over pixels)
+            db = sum dY               bev_colsum_f32
 
 so the loss gradient reaches the BEV features through the native warp
 backward (geometry.py _WarpFn -> bev_ipm_warp_bwd_f32) and then this proj.
@@ -44,9 +44,9 @@ class Proj1x1(torch.autograd.Function):
             packed_t = _nat.pack_conv_weight(weight.detach().float().transpose(0, 1).contiguous())
             zero = torch.zeros(Ci, device=gy.device, dtype=torch.float32)
             dx = _nat.conv2d_nhwc(gy, packed_t, zero, Ci, 1, 1, 1, 0, False)
-        g2 = gy.reshape(-1, Co)
         if ctx.needs_input_grad[1]:
-            dw = (g2.t() @ feat.reshape(-1, Ci)).view(Co, Ci, 1, 1).to(weight.dtype)
+            # [Co, Ci] storage with the parameter's strides (DDP's bucket views compare strides exactly)
+            dw = _nat.conv_wgrad(feat, gy, 1, 1, 1, 0).reshape(Co, Ci).clone().view(Co, Ci, 1, 1).to(weight.dtype)
         if ctx.needs_input_grad[2]:
-            db = g2.sum(0)
+            db = _nat.colsum(gy)
         return dx, dw, db

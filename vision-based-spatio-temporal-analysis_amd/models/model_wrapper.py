@@ -75,8 +75,10 @@ class _ViewProjection(torch.autograd.Function):
             for v in range(V):
                 acc = _nat.conv_wgrad_ex(fl[:, v], dgn[:, v], 1, 0, 1) if B == 1 else \
                     sum(_nat.conv_wgrad_ex(fl[b, v][None], dgn[b, v][None], 1, 0, 1) for b in range(B))
-                parts.append(acc)
-            dw = torch.cat(parts, dim=1)
+                parts.append(acc.reshape(P, C))
+            # [P, V*C] storage with the parameter's strides (the per-view OIHW views are channels-last-strided;
+            # DDP's bucket views compare strides exactly)
+            dw = torch.cat(parts, dim=1).view(P, V * C, 1, 1)
         return dfeat, dw, None
 
 
