@@ -76,6 +76,9 @@ DW_CASES = [  # N, C, H, W, K, stride, act
     (1, 192, 17, 26, 5, 2, 2),
     (2, 288, 9, 14, 5, 1, 0),
     (1, 1392, 6, 7, 3, 1, 2),  # > 1024 channels: channel chunks (blockIdx.z)
+    (1, 64, 19, 23, 3, 1, 2),    # C % 32 == 0: LDS-tiled kernel, partial 8 x 8 tiles
+    (2, 96, 13, 11, 3, 2, 0),    # tiled, stride 2
+    (1, 320, 10, 9, 5, 2, 2),    # tiled, 10 channel chunks, k5 s2
 ]
 
 

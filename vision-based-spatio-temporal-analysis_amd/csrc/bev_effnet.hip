@@ -110,6 +110,100 @@ __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, i
     }
 }
 
+
+// LDS-tiled depthwise conv: a workgroup owns an 8 x 8 output-pixel tile x 8 channel quads (32 channels = one
+// 128-B line of every pixel).  The tile's input patch ((8-1)*s + K)^2 pixels x 8 quads is staged in LDS once
+// (pixel stride 9 quads: conflict-free ds_read_b128 for stride 1 and 2), so the K*K taps of every output read
+// LDS instead of re-streaming 1-KB pixels from L2 (the per-pixel kernel's K=5 working set exceeds the 32-KB L1).
+// Thread = (quad q, output column c, output rows r and r + 4).  Per output the taps are applied in the same
+// order as k_dwconv (ky-major, kx-minor, out-of-range taps skipped), so y is bit-identical to it; the SE
+// partial sums are per tile (fixed order), so their rounding differs from k_dwconv's partition.
+constexpr int DT_T = 8;   // output tile: 8 x 8 pixels
+constexpr int DT_Q = 8;   // channel quads per workgroup
+constexpr int DT_PS = 9;  // LDS pixel stride in quads
+
+inline int dt_tiles(int Ho, int Wo) { return ((Ho + DT_T - 1) / DT_T) * ((Wo + DT_T - 1) / DT_T); }
+
+template <int K, int S>
+__global__ __launch_bounds__(256) void k_dwconv_t(const float *__restrict__ x, int H, int W, int C,
+                                                  const float *__restrict__ wt, const float *__restrict__ bias,
+                                                  int pad, int act, float *__restrict__ y, int Ho, int Wo,
+                                                  float *__restrict__ psum, int nb) {
+    constexpr int PR = (DT_T - 1) * S + K;  // patch rows = cols
+    __shared__ float4 patch[PR * PR * DT_PS];
+    __shared__ float4 red[256];
+    const int C4 = C >> 2;
+    const int tid = threadIdx.x, q = tid & 7, pl = tid >> 3, c = pl & 7, r = pl >> 3;  // r = 0..3
+    const int n = blockIdx.y, tile = blockIdx.x, q0 = blockIdx.z * DT_Q;
+    const int ntx = (Wo + DT_T - 1) / DT_T;
+    const int oy0 = (tile / ntx) * DT_T, ox0 = (tile % ntx) * DT_T;
+    const int iy0 = oy0 * S - pad, ix0 = ox0 * S - pad;
+    const int nq = C4 - q0 < DT_Q ? C4 - q0 : DT_Q;
+    const float *xn = x + (int64_t)n * H * W * C;
+    for (int e = tid; e < PR * PR * DT_Q; e += 256) {
+        const int qq = e & 7, pp = e >> 3, pr = pp / PR, pc = pp - pr * PR;
+        const int iy = iy0 + pr, ix = ix0 + pc;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (qq < nq && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+            v = *(const float4 *)(xn + ((int64_t)iy * W + ix) * C + (q0 + qq) * 4);
+        patch[(pr * PR + pc) * DT_PS + qq] = v;
+    }
+    __syncthreads();
+    float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q < nq) {
+        const int cq = q0 + q;
+        float4 w[K * K];
+#pragma unroll
+        for (int t = 0; t < K * K; ++t) w[t] = *(const float4 *)(wt + (int64_t)t * C + cq * 4);
+        const float4 b = *(const float4 *)(bias + cq * 4);
+        const int ox = ox0 + c;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int rr = r + 4 * h, oy = oy0 + rr;
+            if (oy >= Ho || ox >= Wo) continue;
+            float4 acc = b;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) {
+                const int iy = iy0 + rr * S + ky;
+                if (iy < 0 || iy >= H) continue;
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const int ix = ix0 + c * S + kx;
+                    if (ix < 0 || ix >= W) continue;
+                    const float4 v = patch[((rr * S + ky) * PR + c * S + kx) * DT_PS + q];
+                    const float4 ww = w[ky * K + kx];
+                    acc.x = __builtin_fmaf(v.x, ww.x, acc.x);
+                    acc.y = __builtin_fmaf(v.y, ww.y, acc.y);
+                    acc.z = __builtin_fmaf(v.z, ww.z, acc.z);
+                    acc.w = __builtin_fmaf(v.w, ww.w, acc.w);
+                }
+            }
+            acc.x = act_f(acc.x, act);
+            acc.y = act_f(acc.y, act);
+            acc.z = act_f(acc.z, act);
+            acc.w = act_f(acc.w, act);
+            *(float4 *)(y + (((int64_t)n * Ho + oy) * Wo + ox) * C + cq * 4) = acc;
+            s4.x += acc.x;
+            s4.y += acc.y;
+            s4.z += acc.z;
+            s4.w += acc.w;
+        }
+    }
+    if (psum == nullptr) return;
+    red[tid] = s4;
+    __syncthreads();
+    if (pl == 0 && q < nq) {  // fixed order over the 32 pixel lanes: deterministic partial
+        for (int l = 1; l < 32; ++l) {
+            const float4 t = red[l * 8 + q];
+            s4.x += t.x;
+            s4.y += t.y;
+            s4.z += t.z;
+            s4.w += t.w;
+        }
+        *(float4 *)(psum + ((int64_t)n * nb + tile) * C + (q0 + q) * 4) = s4;
+    }
+}
+
 constexpr int SE_NT = 1024;  // threads of the SE gate workgroup (one per image)
 
 __global__ __launch_bounds__(SE_NT) void k_se_gate(const float *__restrict__ psum, int nb, int C, float hw,
@@ -250,8 +344,15 @@ inline int last() {
 
 extern "C" {
 
+// k_dwconv_t when every workgroup gets whole 128-B channel lines (C % 32 == 0); r02p micro (7 x 1080p B3 shapes):
+// C 192 k3 659 -> 427 us, 192 k5 s2 735 -> 572, 288 k5 927 -> 341; with partial chunks (C 40, 144) it lost
+// (562 -> 641, 650 -> 1065), so those keep the per-pixel kernel.  The choice depends on C only, so the SE
+// partial count below always matches the kernel that runs.
+inline bool dw_tiled(int C) { return C % 32 == 0; }
+
 int bev_dwconv_psum_blocks(int Ho, int Wo, int C) {
     if (Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
+    if (dw_tiled(C)) return dt_tiles(Ho, Wo);  // one SE partial per 8 x 8 output tile
     const int ppb = dw_ppb(C);
     return (int)(((int64_t)Ho * Wo + ppb - 1) / ppb);
 }
@@ -267,16 +368,30 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
     if ((((uintptr_t)x | (uintptr_t)wt | (uintptr_t)bias | (uintptr_t)y | (uintptr_t)psum) & 15) != 0)
         return BEV_ERR_ARGS;
     if (N == 0) return 0;
-    const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
-    const int C4 = C / 4, CH4 = dw_ch4(C);
-    dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
     hipStream_t st = (hipStream_t)stream;
-    if (K == 3)
-        hipLaunchKernelGGL(k_dwconv<3>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho, Wo,
-                           psum, nb, ppb);
+    if (dw_tiled(C) && stride != 1 && stride != 2) return BEV_ERR_ARGS;  // the tiled kernel: stride 1 or 2
+    if (!dw_tiled(C)) {
+        const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
+        const int C4 = C / 4, CH4 = dw_ch4(C);
+        dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
+        if (K == 3)
+            hipLaunchKernelGGL(k_dwconv<3>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho,
+                               Wo, psum, nb, ppb);
+        else
+            hipLaunchKernelGGL(k_dwconv<5>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho,
+                               Wo, psum, nb, ppb);
+        return last();
+    }
+    const int nb = dt_tiles(Ho, Wo), C4 = C / 4;
+    dim3 grid(nb, N, (C4 + DT_Q - 1) / DT_Q);
+    if (K == 3 && stride == 1)
+        hipLaunchKernelGGL((k_dwconv_t<3, 1>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    else if (K == 3)
+        hipLaunchKernelGGL((k_dwconv_t<3, 2>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    else if (stride == 1)
+        hipLaunchKernelGGL((k_dwconv_t<5, 1>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     else
-        hipLaunchKernelGGL(k_dwconv<5>, grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, stride, pad, act, y, Ho, Wo,
-                           psum, nb, ppb);
+        hipLaunchKernelGGL((k_dwconv_t<5, 2>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     return last();
 }
 
@@ -313,7 +428,7 @@ int bev_dwconv_wgrad_f32(const float *x, int N, int H, int W, int C, const float
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(dW, 0, (size_t)K * K * C * sizeof(float), st) != hipSuccess) return last();
     if (N == 0) return 0;
-    const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
+    const int ppb = dw_ppb(C), nb = (int)(((int64_t)Ho * Wo + ppb - 1) / ppb);  // its own pixel partition
     const int C4 = C / 4, CH4 = dw_ch4(C);
     dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
     if (K == 3)
