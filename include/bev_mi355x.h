@@ -227,8 +227,9 @@ int bev_dwconv_psum_blocks(int Ho, int Wo, int C);
  * DepthwiseSeparableConv).  wt is tap-major [K*K][C].  act as bev_conv2d_f32.
  * If psum != NULL, also writes the channel sums of y per workgroup
  * (deterministic partials, [N][bev_dwconv_psum_blocks(Ho,Wo,C)][C]) -- the
- * squeeze of the block's SqueezeExcite.  C % 32 == 0 runs an LDS-tiled kernel (8 x 8 output
- * pixels x 32 channels per workgroup) that takes stride 1 or 2; other C any stride. */
+ * squeeze of the block's SqueezeExcite.  C % 32 == 0 (and C % 8 == 0 for outputs of <= 65536 pixels)
+ * runs an LDS-tiled kernel (8-row output tiles x 32 / 16 / 8 channels per workgroup) that takes stride
+ * 1 or 2; the other shapes any stride. */
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
                      int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);
 

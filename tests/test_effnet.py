@@ -76,9 +76,11 @@ DW_CASES = [  # N, C, H, W, K, stride, act
     (1, 192, 17, 26, 5, 2, 2),
     (2, 288, 9, 14, 5, 1, 0),
     (1, 1392, 6, 7, 3, 1, 2),  # > 1024 channels: channel chunks (blockIdx.z)
-    (1, 64, 19, 23, 3, 1, 2),    # C % 32 == 0: LDS-tiled kernel, partial 8 x 8 tiles
+    (1, 64, 19, 23, 3, 1, 2),    # LDS-tiled kernel (8-quad chunks), partial 8 x 8 tiles
     (2, 96, 13, 11, 3, 2, 0),    # tiled, stride 2
     (1, 320, 10, 9, 5, 2, 2),    # tiled, 10 channel chunks, k5 s2
+    (1, 20, 9, 12, 3, 1, 2),     # odd channel-quad count: per-pixel kernel
+    (1, 36, 11, 7, 5, 2, 0),     # odd quads, k5 s2: per-pixel kernel
 ]
 
 

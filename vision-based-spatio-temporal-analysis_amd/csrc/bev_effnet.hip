@@ -111,55 +111,58 @@ __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, i
 }
 
 
-// LDS-tiled depthwise conv: a workgroup owns an 8 x 8 output-pixel tile x 8 channel quads (32 channels = one
-// 128-B line of every pixel).  The tile's input patch ((8-1)*s + K)^2 pixels x 8 quads is staged in LDS once
-// (pixel stride 9 quads: conflict-free ds_read_b128 for stride 1 and 2), so the K*K taps of every output read
-// LDS instead of re-streaming 1-KB pixels from L2 (the per-pixel kernel's K=5 working set exceeds the 32-KB L1).
-// Thread = (quad q, output column c, output rows r and r + 4).  Per output the taps are applied in the same
-// order as k_dwconv (ky-major, kx-minor, out-of-range taps skipped), so y is bit-identical to it; the SE
-// partial sums are per tile (fixed order), so their rounding differs from k_dwconv's partition.
-constexpr int DT_T = 8;   // output tile: 8 x 8 pixels
-constexpr int DT_Q = 8;   // channel quads per workgroup
-constexpr int DT_PS = 9;  // LDS pixel stride in quads
+// LDS-tiled depthwise conv: a workgroup owns an 8-row output-pixel tile x DQ channel quads (DQ = 8: 32 channels =
+// one 128-B line of every pixel, 8 columns; DQ = 4: 8 columns; DQ = 2: 16 columns).  The tile's input patch is
+// staged in LDS once (pixel stride DQ + 1 quads: conflict-free ds_read_b128 for stride 1 and 2), so the K*K taps
+// of every output read LDS instead of re-streaming whole pixels from L2 (the per-pixel kernel's K=5 working set
+// over 1-KB pixels exceeds the 32-KB L1).  Per output the taps are applied in the same order as k_dwconv
+// (ky-major, kx-minor, out-of-range taps skipped), so y is bit-identical to it; the SE partial sums are per tile
+// (fixed order), so their rounding differs from k_dwconv's partition.
+constexpr int DT_R = 8;  // output tile rows
+__host__ __device__ constexpr int dt_cols(int dq) { return dq == 2 ? 16 : 8; }
 
-inline int dt_tiles(int Ho, int Wo) { return ((Ho + DT_T - 1) / DT_T) * ((Wo + DT_T - 1) / DT_T); }
+inline int dw_dq(int C) {
+    const int C4 = C / 4;
+    return C4 % 8 == 0 ? 8 : C4 % 4 == 0 ? 4 : C4 % 2 == 0 ? 2 : 0;
+}
+inline int dt_tiles(int Ho, int Wo, int dq) {
+    return ((Ho + DT_R - 1) / DT_R) * ((Wo + dt_cols(dq) - 1) / dt_cols(dq));
+}
 
-template <int K, int S>
+template <int K, int S, int DQ>
 __global__ __launch_bounds__(256) void k_dwconv_t(const float *__restrict__ x, int H, int W, int C,
                                                   const float *__restrict__ wt, const float *__restrict__ bias,
                                                   int pad, int act, float *__restrict__ y, int Ho, int Wo,
                                                   float *__restrict__ psum, int nb) {
-    constexpr int PR = (DT_T - 1) * S + K;  // patch rows = cols
-    __shared__ float4 patch[PR * PR * DT_PS];
+    constexpr int TC = dt_cols(DQ), NPL = 256 / DQ, OPT = DT_R * TC / NPL, RS = DT_R / OPT;
+    constexpr int PRR = (DT_R - 1) * S + K, PRC = (TC - 1) * S + K, PS = DQ + 1;
+    __shared__ float4 patch[PRR * PRC * PS];
     __shared__ float4 red[256];
-    const int C4 = C >> 2;
-    const int tid = threadIdx.x, q = tid & 7, pl = tid >> 3, c = pl & 7, r = pl >> 3;  // r = 0..3
-    const int n = blockIdx.y, tile = blockIdx.x, q0 = blockIdx.z * DT_Q;
-    const int ntx = (Wo + DT_T - 1) / DT_T;
-    const int oy0 = (tile / ntx) * DT_T, ox0 = (tile % ntx) * DT_T;
+    const int tid = threadIdx.x, q = tid % DQ, pl = tid / DQ, c = pl % TC, r = pl / TC;  // r < RS
+    const int n = blockIdx.y, tile = blockIdx.x, cq = blockIdx.z * DQ + q;
+    const int ntx = (Wo + TC - 1) / TC;
+    const int oy0 = (tile / ntx) * DT_R, ox0 = (tile % ntx) * TC;
     const int iy0 = oy0 * S - pad, ix0 = ox0 * S - pad;
-    const int nq = C4 - q0 < DT_Q ? C4 - q0 : DT_Q;
-    const float *xn = x + (int64_t)n * H * W * C;
-    for (int e = tid; e < PR * PR * DT_Q; e += 256) {
-        const int qq = e & 7, pp = e >> 3, pr = pp / PR, pc = pp - pr * PR;
+    const float *xn = x + (int64_t)n * H * W * C + blockIdx.z * DQ * 4;
+    for (int e = tid; e < PRR * PRC * DQ; e += 256) {
+        const int qq = e % DQ, pp = e / DQ, pr = pp / PRC, pc = pp - pr * PRC;
         const int iy = iy0 + pr, ix = ix0 + pc;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (qq < nq && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-            v = *(const float4 *)(xn + ((int64_t)iy * W + ix) * C + (q0 + qq) * 4);
-        patch[(pr * PR + pc) * DT_PS + qq] = v;
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+            v = *(const float4 *)(xn + ((int64_t)iy * W + ix) * C + qq * 4);
+        patch[(pr * PRC + pc) * PS + qq] = v;
     }
     __syncthreads();
     float4 s4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (q < nq) {
-        const int cq = q0 + q;
+    {
         float4 w[K * K];
 #pragma unroll
         for (int t = 0; t < K * K; ++t) w[t] = *(const float4 *)(wt + (int64_t)t * C + cq * 4);
         const float4 b = *(const float4 *)(bias + cq * 4);
         const int ox = ox0 + c;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int rr = r + 4 * h, oy = oy0 + rr;
+        for (int h = 0; h < OPT; ++h) {
+            const int rr = r + RS * h, oy = oy0 + rr;
             if (oy >= Ho || ox >= Wo) continue;
             float4 acc = b;
 #pragma unroll
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256) void k_dwconv_t(const float *__restrict__ x, i
                 for (int kx = 0; kx < K; ++kx) {
                     const int ix = ix0 + c * S + kx;
                     if (ix < 0 || ix >= W) continue;
-                    const float4 v = patch[((rr * S + ky) * PR + c * S + kx) * DT_PS + q];
+                    const float4 v = patch[((rr * S + ky) * PRC + c * S + kx) * PS + q];
                     const float4 ww = w[ky * K + kx];
                     acc.x = __builtin_fmaf(v.x, ww.x, acc.x);
                     acc.y = __builtin_fmaf(v.y, ww.y, acc.y);
@@ -192,16 +195,30 @@ __global__ __launch_bounds__(256) void k_dwconv_t(const float *__restrict__ x, i
     if (psum == nullptr) return;
     red[tid] = s4;
     __syncthreads();
-    if (pl == 0 && q < nq) {  // fixed order over the 32 pixel lanes: deterministic partial
-        for (int l = 1; l < 32; ++l) {
-            const float4 t = red[l * 8 + q];
+    if (pl == 0) {  // fixed order over the pixel lanes: deterministic partial
+        for (int l = 1; l < NPL; ++l) {
+            const float4 t = red[l * DQ + q];
             s4.x += t.x;
             s4.y += t.y;
             s4.z += t.z;
             s4.w += t.w;
         }
-        *(float4 *)(psum + ((int64_t)n * nb + tile) * C + (q0 + q) * 4) = s4;
+        *(float4 *)(psum + ((int64_t)n * nb + tile) * C + cq * 4) = s4;
     }
+}
+
+template <int K, int S>
+void launch_dwconv_t(int dq, dim3 grid, hipStream_t st, const float *x, int H, int W, int C, const float *wt,
+                     const float *bias, int pad, int act, float *y, int Ho, int Wo, float *psum, int nb) {
+    if (dq == 8)
+        hipLaunchKernelGGL((k_dwconv_t<K, S, 8>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                           psum, nb);
+    else if (dq == 4)
+        hipLaunchKernelGGL((k_dwconv_t<K, S, 4>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                           psum, nb);
+    else
+        hipLaunchKernelGGL((k_dwconv_t<K, S, 2>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                           psum, nb);
 }
 
 constexpr int SE_NT = 1024;  // threads of the SE gate workgroup (one per image)
@@ -344,15 +361,21 @@ inline int last() {
 
 extern "C" {
 
-// k_dwconv_t when every workgroup gets whole 128-B channel lines (C % 32 == 0); r02p micro (7 x 1080p B3 shapes):
-// C 192 k3 659 -> 427 us, 192 k5 s2 735 -> 572, 288 k5 927 -> 341; with partial chunks (C 40, 144) it lost
-// (562 -> 641, 650 -> 1065), so those keep the per-pixel kernel.  The choice depends on C only, so the SE
-// partial count below always matches the kernel that runs.
-inline bool dw_tiled(int C) { return C % 32 == 0; }
+// Which kernel: k_dwconv_t with 8-quad (32-channel) chunks whenever C % 32 == 0 -- r02r micro (7 x 1080p B3 shapes):
+// C 192 k3 659 -> 435 us, 192 k5 s2 735 -> 572, 288 k5 927 -> 340 -- and with 4- / 2-quad chunks only for outputs of
+// at most 64 Ki pixels per image: r02r, B0's k5 layers at 135 x 240 (C 144 / 240) gain (B0 training step 44.6 ->
+// 42.9 ms) while B3's 540 x 960 C 40 and 270 x 480 C 144 layers lose badly (572 -> 1360, 665 -> 1042 us: 32- / 64-B
+// pixel segments per patch load).  The choice depends on (Ho, Wo, C) only, so the SE partial count below always
+// matches the kernel that runs.
+inline int dw_tiled_dq(int Ho, int Wo, int C) {
+    const int dq = dw_dq(C);
+    return (dq == 8 || (dq > 0 && (int64_t)Ho * Wo <= 65536)) ? dq : 0;
+}
 
 int bev_dwconv_psum_blocks(int Ho, int Wo, int C) {
     if (Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
-    if (dw_tiled(C)) return dt_tiles(Ho, Wo);  // one SE partial per 8 x 8 output tile
+    const int dq = dw_tiled_dq(Ho, Wo, C);
+    if (dq) return dt_tiles(Ho, Wo, dq);  // one SE partial per output tile
     const int ppb = dw_ppb(C);
     return (int)(((int64_t)Ho * Wo + ppb - 1) / ppb);
 }
@@ -369,8 +392,9 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
         return BEV_ERR_ARGS;
     if (N == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    if (dw_tiled(C) && stride != 1 && stride != 2) return BEV_ERR_ARGS;  // the tiled kernel: stride 1 or 2
-    if (!dw_tiled(C)) {
+    const int dq = dw_tiled_dq(Ho, Wo, C);
+    if (dq && stride != 1 && stride != 2) return BEV_ERR_ARGS;  // the tiled kernel: stride 1 or 2
+    if (!dq) {
         const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
         const int C4 = C / 4, CH4 = dw_ch4(C);
         dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
@@ -382,16 +406,12 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
                                Wo, psum, nb, ppb);
         return last();
     }
-    const int nb = dt_tiles(Ho, Wo), C4 = C / 4;
-    dim3 grid(nb, N, (C4 + DT_Q - 1) / DT_Q);
-    if (K == 3 && stride == 1)
-        hipLaunchKernelGGL((k_dwconv_t<3, 1>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
-    else if (K == 3)
-        hipLaunchKernelGGL((k_dwconv_t<3, 2>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
-    else if (stride == 1)
-        hipLaunchKernelGGL((k_dwconv_t<5, 1>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
-    else
-        hipLaunchKernelGGL((k_dwconv_t<5, 2>), grid, dim3(256), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    const int nb = dt_tiles(Ho, Wo, dq);
+    dim3 grid(nb, N, C / 4 / dq);
+    if (K == 3 && stride == 1) launch_dwconv_t<3, 1>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    else if (K == 3) launch_dwconv_t<3, 2>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    else if (stride == 1) launch_dwconv_t<5, 1>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    else launch_dwconv_t<5, 2>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     return last();
 }
 
