@@ -201,6 +201,35 @@ def cpu_baseline(enc, args, K, Rt):
                       "s/frame, torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
 
 
+def cpu_k1(args, K, Rt):
+    """BASELINE configs[0] (K1): the reference's v1.0 CPU-only path with a ResNet-18 trunk (README.md:48-55):
+    7 cameras x 1080p -> ResNet-18 features_only[2] + 1x1 proj -> geometry.py grid_sample warp -> mean, on this
+    host's cores (torch CPU fp32, random init), one frame.  Reported beside the GPU line, never as `value`."""
+    import torch.nn as nn
+
+    import backbone_ref
+    from models.encoders.cnn_encoder import CNNEncoder
+    from oracle import reference_composition_cpu
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    torch.manual_seed(18)
+    enc = CNNEncoder(out_channels=args.channels, backbone="resnet18", pretrained=False).eval()
+    enc.proj = nn.Conv2d(enc.backbone.feature_info[2], args.channels, 1)  # the lazy proj, built on the CPU
+    H, W = args.img
+    imgs = torch.randn(1, args.views, 3, H, W, generator=torch.Generator().manual_seed(3))
+    t0 = time.perf_counter()
+    feats = backbone_ref.encoder_forward(enc, imgs)
+    t1 = time.perf_counter()
+    reference_composition_cpu(feats, torch.from_numpy(K[:1]), torch.from_numpy(Rt[:1]), (H, W), args.bev[0],
+                              args.bev[1], BOUNDS)
+    t2 = time.perf_counter()
+    return {"config": "BASELINE configs[0]: 7-cam ResNet-18 + IPM + mean, CPU-only forward (v1.0 path)",
+            "value": round(1.0 / (t2 - t0), 4), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"1 frame ({args.views}x3x{H}x{W} -> resnet18 layer2 + proj C={args.channels} -> grid_sample "
+                      f"warp -> mean, {args.bev[0]}x{args.bev[1]}): trunk {t1 - t0:.2f} s + warp/mean {t2 - t1:.2f} s, "
+                      "torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
+
+
 def pmc_traffic(args) -> dict:
     """HBM bytes from the committed rocprofv3 PMC passes of this same command (tools/pmc_traffic.py):
     conv = bytes per step over all backbone conv launches, warp = bytes per fused-warp launch.
@@ -408,6 +437,8 @@ def main():
             line["metric"] = "IPM warp+mean launches/sec (warp-only profiling mode)"
         if world == 1 and args.cpu_iters > 0 and not args.warp_only:
             line["cpu_baseline"] = cpu_baseline(enc, args, K, Rt)
+            if not args.camera_shard and args.views == 7 and tuple(args.img) == (1080, 1920):
+                line["cpu_k1"] = cpu_k1(args, K, Rt)
         print(json.dumps(line), flush=True)
     if dist:
         torch.distributed.destroy_process_group()

@@ -218,18 +218,18 @@ int bev_nhwc_to_nchw_f32(const float *x, int N, int C, int H, int W, float *y, v
  * ------------------------------------------------------------------------- */
 
 /* Number of per-workgroup SE partial sums per image that bev_dwconv2d_f32
- * writes for an Ho x Wo x C output (psum is [N][nb][C]). */
-int bev_dwconv_psum_blocks(int Ho, int Wo, int C);
+ * writes for an Ho x Wo x C output at `stride` (psum is [N][nb][C]). */
+int bev_dwconv_psum_blocks(int Ho, int Wo, int C, int stride);
 
 /* device: depthwise KxK conv (K = 3 or 5; torch groups = C), BN folded:
  *   y[n,oy,ox,c] = act( sum_{ky,kx} x[n, oy*s-pad+ky, ox*s-pad+kx, c] * wt[ky*K+kx][c] + bias[c] )
  * (timm conv_dw -> bn -> SiLU, _efficientnet_blocks.py InvertedResidual /
  * DepthwiseSeparableConv).  wt is tap-major [K*K][C].  act as bev_conv2d_f32.
  * If psum != NULL, also writes the channel sums of y per workgroup
- * (deterministic partials, [N][bev_dwconv_psum_blocks(Ho,Wo,C)][C]) -- the
+ * (deterministic partials, [N][bev_dwconv_psum_blocks(Ho,Wo,C,stride)][C]) -- the
  * squeeze of the block's SqueezeExcite.  C % 32 == 0 (and C % 8 == 0 for outputs of <= 65536 pixels)
- * runs an LDS-tiled kernel (8-row output tiles x 32 / 16 / 8 channels per workgroup) that takes stride
- * 1 or 2; the other shapes any stride. */
+ * at stride 1 or 2 runs an LDS-tiled kernel (8-row output tiles x 32 / 16 / 8 channels per workgroup);
+ * every other shape and stride the per-pixel kernel. */
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
                      int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);
 
@@ -249,7 +249,8 @@ int bev_channel_scale_f32(float *y, int N, int64_t P, int C, const float *gate, 
 
 /* ---------------------------------------------------------------------------
  * Trunk backward (training, BASELINE config 3: train.py:249-255 backpropagates
- * through the timm trunk).  NHWC fp32; BN is frozen (folded) in training.
+ * through the timm trunk).  NHWC fp32.  BatchNorm in training uses batch statistics
+ * (bev_batchnorm_* below) or, for a BN module in eval(), the folded running statistics.
  * ------------------------------------------------------------------------- */
 
 /* dz = dy * (y > 0): ReLU backward from the saved output.  n % 4 == 0. */
@@ -370,13 +371,26 @@ int bev_decode_peaks_f32(const float *heat, int B, int H, int W, float thresh, i
  * [cx, cy, w, h] = [x_min + (x + off_x) * res_x, y_min + (y + off_y) * res_y, size_w * res_x,
  * size_h * res_y] (offset, size [B][2][H][W]), greedy centre-distance NMS (kept when every
  * kept centre is >= nms_dist away).  boxes [B][cap][4], scores [B][cap] in keep order,
- * nkept [B] (-1: more candidates than cap or bev_decode_max_candidates()). */
+ * nkept [B] (-1: more candidates than cap or bev_decode_max_candidates(); such frames are
+ * finished by bev_decode_nms_large_f32). */
 int bev_decode_nms_f32(const int32_t *cand_idx, const float *cand_score, const int32_t *count, int B, int cap,
                        const float *offset, const float *size, int H, int W, float x_min, float y_min, float res_x,
                        float res_y, float nms_dist, float *boxes, float *scores, int32_t *nkept, void *stream);
 
-/* host: the largest candidate count per frame bev_decode_nms_f32 handles. */
+/* host: the largest candidate count per frame bev_decode_nms_f32 handles (its LDS sort). */
 int bev_decode_max_candidates(void);
+
+/* device: the same sort + greedy NMS for frames with more than bev_decode_max_candidates()
+ * candidates (count[b] <= cap; other frames are left untouched): keys sorted in global memory
+ * (keys [B][P] workspace, P a power of two >= every such count, P >= 2 * max_candidates), the
+ * greedy NMS in blocks of 64 candidates -- each block is tested against every centre kept so far
+ * in parallel, then resolved in order inside one wave.  Same outputs as bev_decode_nms_f32 would
+ * give without its LDS limit, so a reference-valid heatmap never fails (detector.py:71-125 has
+ * no candidate limit). */
+int bev_decode_nms_large_f32(const int32_t *cand_idx, const float *cand_score, const int32_t *count, int B, int cap,
+                             int P, const float *offset, const float *size, int H, int W, float x_min, float y_min,
+                             float res_x, float res_y, float nms_dist, uint64_t *keys, float *boxes, float *scores,
+                             int32_t *nkept, void *stream);
 
 /* Camera-image ingest (data/transforms.py:12-19 T.ToTensor + T.Normalize, applied per image in
  * data/wildtrack_loader.py:368-374): src [N][H][W][3] uint8 RGB (device) -> out [N][3][H][W]

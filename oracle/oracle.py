@@ -192,17 +192,13 @@ class Oracle:
         return y
 
 
-def reference_composition_cpu(feats, K, Rt, img_hw, bev_h, bev_w, bounds):
-    """The reference's torch-CPU warp + mean composition, op for op.
-
-    Restates geometry.py:90-163 (grid_sample branch, per-(b,v) Python loop,
-    zero-initialised bev_out) followed by SimpleFusion('mean') (fusion.py:21).
-    Used as the CPU baseline that bench.py times; inputs are torch CPU tensors.
-    """
+def reference_grid_cpu(K, Rt, img_hw, Hf, Wf, bev_h, bev_w, bounds):
+    """The grid_sample grid the reference builds for each (b, v): geometry.py:26-27 (linspace ground grid),
+    :143-158 (H = K [r1 r2 t], uvw = H g, w_safe, u / w, rescale, normalise), torch CPU fp32 ops as the
+    reference runs them.  K [B,V,3,3], Rt [B,V,4,4] -> grid [B,V,Hb,Wb,2] fp32."""
     import torch
-    import torch.nn.functional as F
 
-    B, V, C, Hf, Wf = feats.shape
+    B, V = K.shape[:2]
     H_img, W_img = img_hw
     x0, x1, y0, y1 = bounds
     rx, ry = (x1 - x0) / bev_w, (y1 - y0) / bev_h
@@ -210,8 +206,8 @@ def reference_composition_cpu(feats, K, Rt, img_hw, bev_h, bev_w, bounds):
     ys = torch.linspace(y0 + 0.5 * ry, y1 - 0.5 * ry, bev_h)
     yy, xx = torch.meshgrid(ys, xs, indexing="ij")
     ground = torch.stack([xx, yy, torch.ones_like(xx)], dim=-1)
-    bev = torch.zeros(B, V, C, bev_h, bev_w)
     g_flat = ground.reshape(-1, 3).T
+    grid = torch.empty(B, V, bev_h, bev_w, 2)
     for b in range(B):
         for v in range(V):
             Kb, Rtb = K[b, v][:3, :3], Rt[b, v]
@@ -229,7 +225,26 @@ def reference_composition_cpu(feats, K, Rt, img_hw, bev_h, bev_w, bounds):
             nrm = fp.clone()
             nrm[..., 0] = (nrm[..., 0] + 0.5) / Wf * 2.0 - 1.0
             nrm[..., 1] = (nrm[..., 1] + 0.5) / Hf * 2.0 - 1.0
-            s = F.grid_sample(feats[b, v][None], nrm[None], mode="bilinear", padding_mode="zeros",
+            grid[b, v] = nrm
+    return grid
+
+
+def reference_composition_cpu(feats, K, Rt, img_hw, bev_h, bev_w, bounds):
+    """The reference's torch-CPU warp + mean composition, op for op.
+
+    Restates geometry.py:90-163 (grid_sample branch, per-(b,v) Python loop,
+    zero-initialised bev_out) followed by SimpleFusion('mean') (fusion.py:21).
+    Used as the CPU baseline that bench.py times; inputs are torch CPU tensors.
+    """
+    import torch
+    import torch.nn.functional as F
+
+    B, V, C, Hf, Wf = feats.shape
+    grid = reference_grid_cpu(K, Rt, img_hw, Hf, Wf, bev_h, bev_w, bounds)
+    bev = torch.zeros(B, V, C, bev_h, bev_w)
+    for b in range(B):
+        for v in range(V):
+            s = F.grid_sample(feats[b, v][None], grid[b, v][None], mode="bilinear", padding_mode="zeros",
                               align_corners=False)
             bev[b, v] = s[0]
     return bev.mean(dim=1)

@@ -20,8 +20,8 @@ Branches exercised (timm / kornia are absent here):
   * cnn_encoder.py:31-37 fallback 2-conv encoder
   * model_wrapper.py:53-124 BEVNet forward (+ lazy proj / detector, detector.py:7-125) and loss
 
-`--only bevnet` / `--only decode` / `--only img2world` regenerate just bevnet_small.npz / decode_cases.npz /
-img2world_cases.npz.
+`--only bevnet` / `--only decode` / `--only decode_large` / `--only img2world` regenerate just bevnet_small.npz /
+decode_cases.npz / decode_large.npz / img2world_cases.npz.
 """
 from __future__ import annotations
 
@@ -337,6 +337,65 @@ def decode_case():
     print("decode_cases", {k: v for k, v in out.items() if k.endswith("_n")})
 
 
+def decode_large_inputs(case: str):
+    """Seeded inputs of decode_large.npz (regenerated bit-for-bit by the test from the same seeds)."""
+    if case == "noise":  # frame 0: uniform noise (~1/9 of the cells are 3x3 peaks), frame 1: a few blobs
+        B, H, W, seed = 2, 480, 720, 2024
+    else:  # "levels": 8 quantised levels -> plateaus and equal scores everywhere (ties in the sort)
+        B, H, W, seed = 1, 200, 300, 2025
+    rng = np.random.default_rng(seed)
+    heat = rng.random((B, 1, H, W), dtype=np.float32)
+    if case == "noise":
+        # distinct scores (a permutation of k / HW): torch.argsort(descending=True) is not stable, so with
+        # equal scores the reference's order would be whatever libstdc++'s introsort leaves
+        heat[0, 0] = (rng.permutation(H * W).astype(np.float64) / (H * W)).astype(np.float32).reshape(H, W)
+        yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+        heat[1, 0] = 0.0
+        for _ in range(40):
+            cy, cx = rng.uniform(0, H), rng.uniform(0, W)
+            heat[1, 0] = np.maximum(heat[1, 0], np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / 18.0).astype(np.float32))
+    else:
+        heat = (np.floor(heat * np.float32(8.0)) / np.float32(8.0)).astype(np.float32)
+    offset = rng.random((B, 2, H, W), dtype=np.float32)
+    size = (rng.random((B, 2, H, W), dtype=np.float32) * np.float32(25.0) + np.float32(5.0)).astype(np.float32)
+    return heat, offset, size
+
+
+DECODE_LARGE = {"noise": (0.05, 2.0), "levels": (0.1, 1.0)}  # case -> (conf_thresh, nms_dist_m)
+
+
+def decode_large_case():
+    """BEVDetector.decode (detector.py:71-125) with far more candidates per frame than one LDS sort holds
+    (tens of thousands): the reference has no limit, so neither may the drop-in.  Inputs are seeded
+    (decode_large_inputs); only their sha256 and the reference's boxes / scores are stored."""
+    import time
+    out = {}
+    for case, (thr, nms) in DECODE_LARGE.items():
+        heat, offset, size = decode_large_inputs(case)
+        B, _, H, W = heat.shape
+        det = BEVDetector(in_channels=4, bev_bounds=BOUNDS, bev_size=(H, W))
+        t0 = time.time()
+        argsort = torch.argsort
+        if case == "levels":
+            # equal scores everywhere: the reference's unstable argsort leaves ties in an unspecified order
+            # (libstdc++ introsort on the CPU, another order on CUDA); pin the documented stable order,
+            # which is the order the drop-in promises (score desc, cell asc)
+            torch.argsort = lambda t, descending=False: argsort(t, descending=descending, stable=True)
+        try:
+            bl, sl = det.decode(torch.from_numpy(heat), torch.from_numpy(offset), torch.from_numpy(size),
+                                conf_thresh=thr, nms_dist_m=nms)
+        finally:
+            torch.argsort = argsort
+        ncand = [int((det._nms2d(torch.from_numpy(heat))[b, 0] > thr).sum()) for b in range(B)]
+        print(f"decode_large {case}: candidates {ncand}, kept {[x.shape[0] for x in bl]}, {time.time() - t0:.1f} s")
+        out[case + "_sha_in"] = np.array(sha(heat) + sha(offset) + sha(size))
+        out[case + "_ncand"] = np.array(ncand)
+        out[case + "_n"] = np.array([x.shape[0] for x in bl])
+        out[case + "_boxes"] = np.concatenate([x.numpy() for x in bl]).reshape(-1, 4)
+        out[case + "_scores"] = np.concatenate([x.numpy() for x in sl])
+    np.savez_compressed(os.path.join(HERE, "decode_large.npz"), **out)
+
+
 def main():
     torch.set_num_threads(os.cpu_count() or 1)
     if sys.argv[1:] == ["--only", "bevnet"]:
@@ -344,6 +403,9 @@ def main():
         return
     if sys.argv[1:] == ["--only", "decode"]:
         decode_case()
+        return
+    if sys.argv[1:] == ["--only", "decode_large"]:
+        decode_large_case()
         return
     if sys.argv[1:] == ["--only", "img2world"]:
         img2world_cases()
@@ -376,6 +438,7 @@ def main():
     encoder_case()
     bevnet_case()
     decode_case()
+    decode_large_case()
     with open(os.path.join(HERE, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     K, Rt = bev_rig.rig(7, 1080, 1920, 1)

@@ -299,3 +299,66 @@ def test_resnet_stream_groups_bit_exact(groups, offset):
         enc.backbone.stream_groups, enc.backbone.stream_offset = 1, 0
     assert got.shape == ref.shape
     assert torch.equal(got.contiguous().view(torch.int32), ref.contiguous().view(torch.int32))
+
+
+def test_resnet_stream_groups_cold_cache_and_repack():
+    """a fresh model run straight away with 2 stream groups (every folded panel packed during this
+    call) and again after in-place weight / BN-statistic updates (re-pack) == the single-stream trunk, bit for bit.
+    The panels are packed on the caller's stream before the groups fork (ResNet._prepare_eval)."""
+    import copy
+    from models.encoders.resnet import resnet50
+    torch.manual_seed(3)
+    a = resnet50().eval()
+    b = copy.deepcopy(a)
+    a.to(DEV)
+    b.to(DEV)
+    a.stream_groups, b.stream_groups = 2, 1
+    x = _rand((6, 3, 90, 150), 12).to(DEV)
+    outs = []
+    with torch.no_grad():
+        for it in range(2):
+            if it == 1:
+                for m in (a, b):
+                    m.layer1[0].conv2.weight.mul_(1.5)
+                    m.layer2[1].bn2.running_var.mul_(2.0)
+                    m.bn1.bias.add_(0.1)
+            ya = a.forward_features_nhwc(x, 2)
+            yb = b.forward_features_nhwc(x, 2)
+            torch.cuda.synchronize()
+            assert torch.equal(ya.view(torch.int32), yb.view(torch.int32))
+            outs.append(ya.clone())
+    assert not torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+def test_resnet50_encoder_full_1080p_bench_geometry():
+    """The bench's exact encoder call (BASELINE configs[1]: 2 frames x 7 cameras x 3 x 1080 x 1920, ResNet-50 to
+    layer2 + proj to C=64, two stream groups of 7 images, so the same tiles, chains, LDS-DMA staging and XCD
+    order the bench times) vs the torch fp32 CPU restatement (oracle/backbone_ref.py) on the first and last image
+    of each stream group (images are independent), max |err| <= 1e-4 * max |ref| per image (SURVEY §8d rtol)."""
+    from models.encoders.cnn_encoder import CNNEncoder
+    import backbone_ref
+    torch.manual_seed(1234)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False)
+    g = torch.Generator().manual_seed(5)
+    for m in enc.modules():  # non-trivial BN statistics so the folding is exercised
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.2, 0.2, generator=g)
+            m.running_var.uniform_(0.5, 1.5, generator=g)
+            m.weight.data.uniform_(0.5, 1.5, generator=g)
+            m.bias.data.uniform_(-0.2, 0.2, generator=g)
+    enc.eval()
+    imgs = torch.randn(2, 7, 3, 1080, 1920, generator=torch.Generator().manual_seed(0))
+    enc_gpu = enc.to(DEV)
+    assert enc_gpu.backbone.stream_groups == 2
+    with torch.no_grad():
+        y = enc_gpu(imgs.to(DEV))
+        torch.cuda.synchronize()
+    assert tuple(y.shape) == (2, 7, 64, 135, 240)
+    pick = ((0, 0), (0, 6), (1, 0), (1, 6))  # group 0 = images 0..6, group 1 = images 7..13
+    got = torch.stack([y[b, v] for b, v in pick]).cpu()
+    enc_cpu = enc.to("cpu")
+    ref = backbone_ref.encoder_forward(enc_cpu, torch.stack([imgs[b, v] for b, v in pick]).unsqueeze(0))[0]
+    for i in range(len(pick)):
+        err = (got[i] - ref[i]).abs().max().item() / ref[i].abs().max().item()
+        assert err <= 1e-4, (pick[i], err)

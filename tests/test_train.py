@@ -489,8 +489,8 @@ def _bevnet_ddp_worker(rank, world, port, q):
         model.encoder.freeze()
         bev_dist.materialize_lazy(model, batch)
         ddp = bev_dist.ddp_wrap(model, torch.device(DEV))
-        # parameters only: BN running statistics are per-rank buffers (ddp_wrap: broadcast_buffers=False; each
-        # rank's train-mode BatchNorm sees its own frame)
+        # parameters: BN running statistics are updated from each rank's own frame and broadcast from rank 0
+        # at the next forward (ddp_wrap: broadcast_buffers=True), so after the last step they may differ
         init = {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters()}
         opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-3)
         model.train()

@@ -62,6 +62,11 @@ def reduce_partial_bev(partial: torch.Tensor, num_views: int, mode: str = "mean"
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if partial.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device collectives here: exchange through host memory (CPU-process-group tests and
+        # hosts without RCCL); RCCL groups exchange device buffers directly over xGMI
+        out = reduce_partial_bev(partial.cpu(), num_views, mode, group, gather)
+        return out.to(partial.device)
     B, C, Hb, Wb = partial.shape
     rpr = -(-Hb // world)  # rows per rank (ceil); the map is zero-padded to world * rpr rows
     if rpr * world != Hb:
@@ -110,23 +115,51 @@ def materialize_lazy(model: torch.nn.Module, batch) -> None:
     model.train(was)
 
 
-def ddp_wrap(model: torch.nn.Module, device: Optional[torch.device] = None, bucket_cap_mb: float = 25.0):
-    """DistributedDataParallel over the default group (RCCL on ROCm, gloo on CPU).  Frozen
-    parameters (requires_grad False) are not synchronised; buffers (BN statistics of a frozen
-    trunk, non-persistent grids) are not broadcast each step."""
+def non_persistent_buffers(model: torch.nn.Module):
+    """Fully qualified names of the buffers that are not state (ground grid, pos-enc): derived from the
+    config, identical on every rank, never worth a broadcast."""
+    names = []
+    for mname, m in model.named_modules():
+        for b in getattr(m, "_non_persistent_buffers_set", ()):
+            names.append(f"{mname}.{b}" if mname else b)
+    return names
+
+
+def ddp_wrap(model: torch.nn.Module, device: Optional[torch.device] = None, bucket_cap_mb: float = 25.0,
+             broadcast_buffers: bool = True):
+    """DistributedDataParallel over the default group (RCCL on ROCm, gloo on CPU).  Frozen parameters
+    (requires_grad False) are not synchronised.
+
+    Buffers: a trainable trunk's BatchNorm uses each rank's own batch statistics (per-rank batch = the
+    reference's batch under weak scaling) and updates its running statistics from them.  With
+    broadcast_buffers (DDP's default, kept) rank 0's running statistics are broadcast at every forward, so all
+    replicas hold the same buffers and the checkpoint rank 0 writes (train.py:336-343) is what every rank would
+    write; the ground grid / pos-enc (non-persistent, config-derived) are excluded from that broadcast."""
     from torch.nn.parallel import DistributedDataParallel
+    DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(model, non_persistent_buffers(model))
     ids = [device.index] if device is not None and device.type == "cuda" else None
-    return DistributedDataParallel(model, device_ids=ids, broadcast_buffers=False, bucket_cap_mb=bucket_cap_mb,
-                                   gradient_as_bucket_view=True)
+    return DistributedDataParallel(model, device_ids=ids, broadcast_buffers=broadcast_buffers,
+                                   bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)
 
 
-def train_step(model, batch, targets, optimizer, loss_cfg=None) -> dict:
-    """One optimisation step as train.py:249-255 (fp32 path): forward, BEVNet.loss, backward
-    (DDP all-reduces the gradients when `model` is wrapped), optimizer step.  Returns the losses."""
+def train_step(model, batch, targets, optimizer, loss_cfg=None, scaler=None) -> dict:
+    """One optimisation step as train.py:238-255: forward, BEVNet.loss, backward (DDP all-reduces the
+    gradients when `model` is wrapped), optimizer step.  With a `torch.amp.GradScaler` (the reference's
+    default, RUNTIME.USE_AMP: true) the forward and loss run under autocast(float16) -- the native kernels
+    compute in fp32 inside it (bev_native.amp_fwd) -- and the step goes through scaler.scale / step / update,
+    which skips it when a gradient is not finite.  Returns the losses."""
     optimizer.zero_grad(set_to_none=True)
-    preds = model(batch)
     core = getattr(model, "module", model)
-    losses = core.loss(preds, targets, loss_cfg or {})
-    losses["total_loss"].backward()
-    optimizer.step()
+    if scaler is not None:
+        with torch.autocast("cuda", dtype=torch.float16):
+            preds = model(batch)
+            losses = core.loss(preds, targets, loss_cfg or {})
+        scaler.scale(losses["total_loss"]).backward()
+        scaler.step(optimizer)
+        scaler.update()
+    else:
+        preds = model(batch)
+        losses = core.loss(preds, targets, loss_cfg or {})
+        losses["total_loss"].backward()
+        optimizer.step()
     return {k: float(v.detach()) for k, v in losses.items()}

@@ -17,7 +17,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -60,13 +60,15 @@ SIGNATURES = {
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
-    "bev_dwconv_psum_blocks": (_i, [_i, _i, _i]),
+    "bev_dwconv_psum_blocks": (_i, [_i, _i, _i, _i]),
     "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_se_gate_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "bev_channel_scale_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp]),
     "bev_decode_peaks_f32": (_i, [_vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "bev_decode_nms_f32": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _f, _f, _f, _f, _f, _vp, _vp, _vp, _vp]),
     "bev_decode_max_candidates": (_i, []),
+    "bev_decode_nms_large_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _i, _i, _f, _f, _f, _f, _f, _vp, _vp, _vp,
+                                      _vp, _vp]),
     "bev_conv2d_nhwc_ex_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i,
                                     _i, _i, _vp]),
     "bev_conv_wgrad_ex_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
@@ -182,6 +184,14 @@ def tuned(**knobs):
 
 class HipError(RuntimeError):
     pass
+
+
+# Mixed precision (the reference trains under torch.autocast(float16) + GradScaler, train.py:168-173,238-247):
+# every native autograd Function runs its forward with autocast disabled and its floating inputs cast to
+# fp32 (the kernels' arithmetic type, wider than the reference's fp16 convs), and its backward under the
+# forward's autocast state -- torch's custom-extension contract (torch.amp.custom_fwd / custom_bwd).
+amp_fwd = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+amp_bwd = torch.amp.custom_bwd(device_type="cuda")
 
 
 def _check(rc: int, name: str):
@@ -371,7 +381,7 @@ def dwconv2d_nhwc(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, K: int,
     y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.float32)
     psum = None
     if want_psum:
-        nb = lib().bev_dwconv_psum_blocks(Ho, Wo, C)
+        nb = lib().bev_dwconv_psum_blocks(Ho, Wo, C, stride)
         _check(0 if nb > 0 else nb, "bev_dwconv_psum_blocks")
         psum = torch.empty(N, nb, C, device=x.device, dtype=torch.float32)
     with _span("dwconv", x):
@@ -548,11 +558,13 @@ def maxpool_bwd_nhwc(x: torch.Tensor, dy: torch.Tensor, k: int, stride: int, pad
 def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, bounds, conf_thresh: float,
            nms_dist: float):
     """heatmap [B,1,H,W], offset / size [B,2,H,W] (device) -> (boxes list of [K,4], scores list of [K]).
-    One host synchronisation for the whole batch (the kept counts)."""
+    Like the reference there is no candidate limit: a frame with more candidates than the LDS sort holds
+    (bev_decode_max_candidates) is finished by the global-memory sort + blocked NMS (bev_decode_nms_large_f32).
+    One host synchronisation per batch (two when some frame needs the large path)."""
     heatmap, offset, size = heatmap.contiguous().float(), offset.contiguous().float(), size.contiguous().float()
     _require_gpu(heatmap, offset, size)
     B, _, H, W = heatmap.shape
-    cap = int(min(H * W, lib().bev_decode_max_candidates()))
+    cap = H * W  # every cell can be a candidate (plateaus): the candidate list never overflows
     dev = heatmap.device
     idx = torch.empty(B, cap, device=dev, dtype=torch.int32)
     sc = torch.empty(B, cap, device=dev, dtype=torch.float32)
@@ -565,13 +577,25 @@ def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, boun
     boxes = torch.empty(B, cap, 4, device=dev, dtype=torch.float32)
     scores = torch.empty(B, cap, device=dev, dtype=torch.float32)
     nk = torch.empty(B, device=dev, dtype=torch.int32)
-    _check(lib().bev_decode_nms_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, _ptr(offset), _ptr(size), H, W,
-                                    float(x_min), float(y_min), float(res_x), float(res_y), float(nms_dist),
+    args = (float(x_min), float(y_min), float(res_x), float(res_y), float(nms_dist))
+    _check(lib().bev_decode_nms_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, _ptr(offset), _ptr(size), H, W, *args,
                                     _ptr(boxes), _ptr(scores), _ptr(nk), st), "bev_decode_nms_f32")
-    kept = nk.cpu().tolist()
+    kc = torch.stack([nk, cnt]).cpu()
+    kept, counts = kc[0].tolist(), kc[1].tolist()
     if min(kept, default=0) < 0:
-        raise HipError(f"decode: more than {cap} peak candidates in a frame above conf_thresh={conf_thresh}")
+        big = max(c for k, c in zip(kept, counts) if k < 0)
+        P = max(2 * DECODE_SORT_CHUNK, 1 << (big - 1).bit_length())
+        keys = torch.empty(B, P, device=dev, dtype=torch.int64)
+        _check(lib().bev_decode_nms_large_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, P, _ptr(offset), _ptr(size), H,
+                                              W, *args, _ptr(keys), _ptr(boxes), _ptr(scores), _ptr(nk), st),
+               "bev_decode_nms_large_f32")
+        kept = nk.cpu().tolist()
+        if min(kept, default=0) < 0:
+            raise HipError("decode: large-candidate path left a frame unfinished")
     return [boxes[b, :k] for b, k in enumerate(kept)], [scores[b, :k] for b, k in enumerate(kept)]
+
+
+DECODE_SORT_CHUNK = 8192  # keys per LDS chunk of the large-path sort (bev_decode.hip SORT_CHUNK)
 
 
 # ---------------------------------------------------------------------------

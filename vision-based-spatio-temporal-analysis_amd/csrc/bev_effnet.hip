@@ -365,16 +365,17 @@ extern "C" {
 // C 192 k3 659 -> 435 us, 192 k5 s2 735 -> 572, 288 k5 927 -> 340 -- and with 4- / 2-quad chunks only for outputs of
 // at most 64 Ki pixels per image: r02r, B0's k5 layers at 135 x 240 (C 144 / 240) gain (B0 training step 44.6 ->
 // 42.9 ms) while B3's 540 x 960 C 40 and 270 x 480 C 144 layers lose badly (572 -> 1360, 665 -> 1042 us: 32- / 64-B
-// pixel segments per patch load).  The choice depends on (Ho, Wo, C) only, so the SE partial count below always
-// matches the kernel that runs.
-inline int dw_tiled_dq(int Ho, int Wo, int C) {
+// pixel segments per patch load).  The tiled kernel takes stride 1 or 2; other strides run the per-pixel kernel.
+// The choice depends on (Ho, Wo, C, stride) only, so the SE partial count below always matches the kernel that runs.
+inline int dw_tiled_dq(int Ho, int Wo, int C, int stride) {
     const int dq = dw_dq(C);
+    if (stride != 1 && stride != 2) return 0;
     return (dq == 8 || (dq > 0 && (int64_t)Ho * Wo <= 65536)) ? dq : 0;
 }
 
-int bev_dwconv_psum_blocks(int Ho, int Wo, int C) {
-    if (Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
-    const int dq = dw_tiled_dq(Ho, Wo, C);
+int bev_dwconv_psum_blocks(int Ho, int Wo, int C, int stride) {
+    if (Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0 || stride <= 0) return BEV_ERR_ARGS;
+    const int dq = dw_tiled_dq(Ho, Wo, C, stride);
     if (dq) return dt_tiles(Ho, Wo, dq);  // one SE partial per output tile
     const int ppb = dw_ppb(C);
     return (int)(((int64_t)Ho * Wo + ppb - 1) / ppb);
@@ -392,10 +393,9 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
         return BEV_ERR_ARGS;
     if (N == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const int dq = dw_tiled_dq(Ho, Wo, C);
-    if (dq && stride != 1 && stride != 2) return BEV_ERR_ARGS;  // the tiled kernel: stride 1 or 2
+    const int dq = dw_tiled_dq(Ho, Wo, C, stride);
     if (!dq) {
-        const int nb = bev_dwconv_psum_blocks(Ho, Wo, C), ppb = dw_ppb(C);
+        const int nb = bev_dwconv_psum_blocks(Ho, Wo, C, stride), ppb = dw_ppb(C);
         const int C4 = C / 4, CH4 = dw_ch4(C);
         dim3 grid(nb, N, (C4 + CH4 - 1) / CH4);
         if (K == 3)

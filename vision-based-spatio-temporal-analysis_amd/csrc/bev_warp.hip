@@ -1106,7 +1106,7 @@ int warp_tune(int knob, int value) {
 
 extern "C" {
 
-int bev_abi_version(void) { return 4; }
+int bev_abi_version(void) { return 5; }
 
 int bev_linspace_f32(double lo, double hi, int n, float *out) {
     if (n < 0 || (n > 0 && !out)) return BEV_ERR_ARGS;

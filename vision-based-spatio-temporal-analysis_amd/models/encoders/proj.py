@@ -25,6 +25,7 @@ __all__ = ["Proj1x1"]
 
 class Proj1x1(torch.autograd.Function):
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, feat: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
         """feat [N,H,W,Ci] NHWC, weight [Co,Ci,1,1], bias [Co] -> y [N,H,W,Co] NHWC."""
         Co = weight.shape[0]
@@ -35,6 +36,7 @@ class Proj1x1(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, gy: torch.Tensor):
         feat, weight = ctx.saved_tensors
         Co, Ci = weight.shape[0], weight.shape[1]

@@ -184,9 +184,12 @@ class FoldedChain:
                 and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.padding == (0, 0)
                 and c3.out_channels % 128 == 0)
 
+    def prepare(self, device):
+        self.c2.prepare(device)
+        self.c3.prepare(device)
+
     def __call__(self, h, x, out=None):
-        self.c2.prepare(h.device)
-        self.c3.prepare(h.device)
+        self.prepare(h.device)
         c2 = self.c2.conv
         return _nat.conv2d_chain_nhwc(h, self.c2.packed, self.c2.bias, c2.out_channels, c2.kernel_size[0],
                                       c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU, self.c3.packed,
@@ -213,9 +216,12 @@ class FoldedChainTail:
                 and c2.kernel_size[0] == c2.kernel_size[1] and c2.dilation == (1, 1) and c2.groups == 1
                 and blk.conv3.out_channels % 128 == 0)
 
+    def prepare(self, device):
+        self.c2.prepare(device)
+        self.tail.prepare(device)
+
     def __call__(self, h, x, out=None):
-        self.c2.prepare(h.device)
-        self.tail.prepare(h.device)
+        self.prepare(h.device)
         c2 = self.c2.conv
         return _nat.conv2d_chain_dual_nhwc(h, self.c2.packed, self.c2.bias, c2.out_channels, c2.kernel_size[0],
                                            c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU, x,
@@ -319,8 +325,24 @@ class ResNet(nn.Module):
             H, W = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         return x.shape[0], H, W, self.feature_info[oi]
 
+    def _prepare_eval(self, device, out_index: int):
+        """Fold + pack every conv the eval chain up to `out_index` runs, on the caller's stream.  Called
+        before the image groups fork onto their side streams, so no group can read a panel (or a freed old
+        one) while another group's stream is still re-packing it."""
+        self._fc(self.conv1, self.bn1).prepare(device)
+        if out_index == 0:
+            return
+        for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
+            for blk in layer:
+                for f in self._block_plan(blk)[1]:
+                    if f is not None:
+                        f.prepare(device)
+            if li == out_index:
+                return
+
     def _forward_eval_streams(self, x: torch.Tensor, out_index: int, G: int) -> torch.Tensor:
         dev = x.device
+        self._prepare_eval(dev, out_index)
         cur = torch.cuda.current_stream(dev)
         side = self._streams.setdefault(dev, [])
         while len(side) < G:
@@ -387,28 +409,35 @@ class ResNet(nn.Module):
             self._folded[k] = FoldedChain(self._fc(blk.conv2, blk.bn2), self._fc(blk.conv3, blk.bn3))
         return self._folded[k]
 
-    def _block(self, blk, x, out=None):
+    def _block_plan(self, blk):
+        """(kind, folded executors) of one residual block on the eval path."""
         if isinstance(blk, Bottleneck) and self.fuse_chain and FoldedChain.applies(blk):
-            h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
-            return self._chain(blk)(h, x, out=out)
+            return "chain", [self._fc(blk.conv1, blk.bn1), self._chain(blk)]
         if isinstance(blk, Bottleneck) and self.fuse_chain and self.fuse_shortcut and FoldedChainTail.applies(blk):
             k = ("chaintail", id(blk))
             if k not in self._folded:
                 self._folded[k] = FoldedChainTail(self._fc(blk.conv2, blk.bn2), self._tail(blk))
-            h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
-            return self._folded[k](h, x, out=out)
+            return "chaintail", [self._fc(blk.conv1, blk.bn1), self._folded[k]]
         if isinstance(blk, Bottleneck) and self.fuse_shortcut and FoldedTail.applies(blk):
-            h = self._fc(blk.conv1, blk.bn1)(x, relu=True)
-            h = self._fc(blk.conv2, blk.bn2)(h, relu=True)
-            return self._tail(blk)(h, x, out=out)
-        sc = x
-        if blk.downsample is not None:
-            sc = self._fc(blk.downsample[0], blk.downsample[1])(x, relu=False)
+            return "tail", [self._fc(blk.conv1, blk.bn1), self._fc(blk.conv2, blk.bn2), self._tail(blk)]
+        ds = self._fc(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None
+        return "plain", [ds] + [self._fc(conv, bn) for conv, bn, _ in blk.convs()]
+
+    def _block(self, blk, x, out=None):
+        kind, fs = self._block_plan(blk)
+        if kind in ("chain", "chaintail"):
+            h = fs[0](x, relu=True)
+            return fs[1](h, x, out=out)
+        if kind == "tail":
+            h = fs[0](x, relu=True)
+            h = fs[1](h, relu=True)
+            return fs[2](h, x, out=out)
+        sc = fs[0](x, relu=False) if fs[0] is not None else x
         chain = blk.convs()
         y = x
-        for idx, (conv, bn, relu) in enumerate(chain):
+        for idx, ((conv, bn, relu), f) in enumerate(zip(chain, fs[1:])):
             last = idx == len(chain) - 1
-            y = self._fc(conv, bn)(y, relu=relu, residual=sc if last else None, out=out if last else None)
+            y = f(y, relu=relu, residual=sc if last else None, out=out if last else None)
         return y
 
 

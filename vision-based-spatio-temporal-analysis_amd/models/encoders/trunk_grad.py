@@ -65,6 +65,7 @@ def _dgrad(dz: torch.Tensor, wf: torch.Tensor, H: int, W: int, stride: int, pad:
 
 class ConvBNAct(torch.autograd.Function):
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, weight, gamma, beta, conv, bn, relu: bool, in_nchw: bool, residual):
         wf, bf, s, r = _fold(conv, bn)
         k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
@@ -75,6 +76,7 @@ class ConvBNAct(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dy):
         x, y, wf, s, r, weight = ctx.saved_tensors
         conv, bn, relu, in_nchw, has_res = ctx.meta
@@ -116,6 +118,7 @@ class ConvBNTrain(torch.autograd.Function):
     BatchNorm2d) or, for a BN module in eval(), its running statistics."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, weight, gamma, beta, conv, bn, act: int, in_nchw: bool, residual):
         k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
         w = weight.detach().float().contiguous()
@@ -129,6 +132,7 @@ class ConvBNTrain(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dy):
         x, z, y, w, mean, rstd, gamma, scale, shift = ctx.saved_tensors
         k, st, p, in_nchw, has_res, act, frozen = ctx.meta
@@ -147,6 +151,7 @@ class DWConvBNTrain(torch.autograd.Function):
     conv of the (zero-inserted) gradient with the flipped taps, wgrad = bev_dwconv_wgrad_f32."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, weight, gamma, beta, conv, bn, act: int):
         C, K, st, p = conv.out_channels, conv.kernel_size[0], conv.stride[0], conv.padding[0]
         wt = weight.detach().float().reshape(C, K * K).t().contiguous()  # [K*K, C] tap-major
@@ -159,6 +164,7 @@ class DWConvBNTrain(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dy):
         x, z, y, wt, mean, rstd, gamma, scale, shift = ctx.saved_tensors
         K, st, p, act, frozen = ctx.meta
@@ -191,6 +197,7 @@ class SqueezeExcite(torch.autograd.Function):
         return torch.sigmoid(r @ w2.reshape(w2.shape[0], -1).t() + b2)
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, y, w1, b1, w2, b2):
         P = y.shape[1] * y.shape[2]
         s = _nat.channel_sums(y) / P
@@ -199,6 +206,7 @@ class SqueezeExcite(torch.autograd.Function):
         return _nat.channel_affine(y, g)
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dout):
         y, s, g, w1, b1, w2, b2 = ctx.saved_tensors
         P = y.shape[1] * y.shape[2]
@@ -225,6 +233,7 @@ class ConvAct(torch.autograd.Function):
     dgrad as a stride-1 conv, wgrad, bias column sums)."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, weight, bias, stride: int, pad: int, relu: bool, in_nchw: bool):
         Co, Ci, k, _ = weight.shape
         w = weight.detach().float().contiguous()
@@ -235,6 +244,7 @@ class ConvAct(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dy):
         x, y, w = ctx.saved_tensors
         stride, pad, relu, in_nchw, has_b = ctx.meta
@@ -255,12 +265,14 @@ def conv_act(conv: nn.Conv2d, x, relu: bool, in_nchw: bool = False):
 
 class MaxPool(torch.autograd.Function):
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, k: int, stride: int, pad: int):
         ctx.save_for_backward(x)
         ctx.meta = (k, stride, pad)
         return _nat.maxpool_nhwc(x, k, stride, pad)
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
         k, stride, pad = ctx.meta

@@ -25,6 +25,7 @@ __all__ = ["FusionModule", "SimpleFusion", "AttentionFusion", "ConcatFusion", "B
 
 class _FuseFn(torch.autograd.Function):
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, mode):
         out = _nat.view_fuse(x, mode)
         ctx.mode = mode
@@ -34,6 +35,7 @@ class _FuseFn(torch.autograd.Function):
         return out
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, g):
         V = ctx.V
         if ctx.mode == "sum":

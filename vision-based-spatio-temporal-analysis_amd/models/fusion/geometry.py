@@ -126,12 +126,14 @@ class _WarpFn(torch.autograd.Function):
     """Per-view warp with a gradient to feats (the grid is constant)."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, feats4, H, xs, ys, img_hw):
         ctx.save_for_backward(H, xs, ys)
         ctx.meta = (feats4.shape[2], feats4.shape[3], img_hw)
         return _nat.warp(feats4, H, xs, ys, img_hw)
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, gout):
         H, xs, ys = ctx.saved_tensors
         Hf, Wf, img_hw = ctx.meta
@@ -140,12 +142,14 @@ class _WarpFn(torch.autograd.Function):
 
 class _WarpFuseFn(torch.autograd.Function):
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, feats5, H, xs, ys, img_hw, mode):
         ctx.save_for_backward(H, xs, ys)
         ctx.meta = (feats5.shape[1], feats5.shape[3], feats5.shape[4], img_hw, mode)
         return _nat.warp_fuse(feats5, H, xs, ys, img_hw, mode)
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, gout):
         H, xs, ys = ctx.saved_tensors
         V, Hf, Wf, img_hw, mode = ctx.meta

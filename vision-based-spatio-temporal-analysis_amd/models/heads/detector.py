@@ -60,6 +60,7 @@ class _HeadConv(torch.autograd.Function):
     """Stride-1 'same' KxK conv of an NHWC operand (padding = dilation * (K // 2)), native both ways."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, x, weight, bias, dil: int):
         Co, Ci, K, _ = weight.shape
         cp = x.shape[-1]
@@ -75,6 +76,7 @@ class _HeadConv(torch.autograd.Function):
         return y
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dil, Ci, has_b = ctx.meta
@@ -96,12 +98,14 @@ class _GroupNormReLU(torch.autograd.Function):
     """relu(GroupNorm(32)(z)) over NHWC z, materialised (training), native backward."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, z, gamma, beta, eps: float):
         mean, rstd, scale, shift = _nat.groupnorm_fwd(z, _GROUPS, gamma, beta, eps)
         ctx.save_for_backward(z, gamma, mean, rstd, scale, shift)
         return _nat.groupnorm_apply(z, scale, shift, True)
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, da):
         z, gamma, mean, rstd, scale, shift = ctx.saved_tensors
         dz, dg, db = _nat.groupnorm_bwd(z, da, _GROUPS, mean, rstd, gamma, scale, shift, True)

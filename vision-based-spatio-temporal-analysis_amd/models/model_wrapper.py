@@ -40,6 +40,7 @@ class _ViewProjection(torch.autograd.Function):
     maps as a [B,V,P,Hf,Wf] view of a [B,V,Hf,Wf,P] buffer (the layout the fused warp reads)."""
 
     @staticmethod
+    @_nat.amp_fwd
     def forward(ctx, feats, weight, panels):
         B, V, C, Hf, Wf = feats.shape
         P = weight.shape[0]
@@ -55,6 +56,7 @@ class _ViewProjection(torch.autograd.Function):
         return g.permute(0, 1, 4, 2, 3)
 
     @staticmethod
+    @_nat.amp_bwd
     def backward(ctx, dg):
         fl, weight = ctx.saved_tensors
         B, V, Hf, Wf, C = fl.shape
