@@ -148,6 +148,36 @@ def backbone_flops(enc, H, W):
     return total
 
 
+def backbone_bytes(enc, H, W):
+    """Algorithmic HBM bytes of one image through the EfficientNet trunk + proj as the launches run it: every
+    launch reads its input once and writes its output once (+ the residual it adds), fp32 NHWC; the SE
+    excitation is applied in the projection conv's operand load (no extra pass).  Weights are negligible."""
+    from models.encoders.efficientnet import FEATURE_STAGE, DepthwiseSeparableConv
+    net = enc.backbone
+
+    def out_hw(c, h, w):
+        return (h + 2 * c.padding[0] - c.kernel_size[0]) // c.stride[0] + 1, \
+            (w + 2 * c.padding[1] - c.kernel_size[1]) // c.stride[1] + 1
+
+    h, w = out_hw(net.conv_stem, H, W)
+    total = 4 * (3 * H * W + h * w * net.conv_stem.out_channels)
+    for si in range(FEATURE_STAGE[enc.out_index] + 1):
+        for blk in net.blocks[si]:
+            cin = blk.conv_dw.in_channels if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pw.in_channels
+            x_bytes = 4 * h * w * cin
+            if not isinstance(blk, DepthwiseSeparableConv):
+                total += x_bytes + 4 * h * w * blk.conv_pw.out_channels  # expand 1x1
+            cdw = blk.conv_dw.in_channels
+            h2, w2 = out_hw(blk.conv_dw, h, w)
+            total += 4 * (h * w * cdw + h2 * w2 * cdw)  # depthwise
+            last = blk.conv_pw if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pwl
+            total += 4 * (h2 * w2 * cdw + h2 * w2 * last.out_channels)  # projection (+ excitation)
+            if blk.has_skip:
+                total += 4 * h2 * w2 * last.out_channels  # residual read
+            h, w = h2, w2
+    return total + 4 * h * w * (enc.proj.in_channels + enc.proj.out_channels)
+
+
 def warp_alg_bytes(geom, H, feats_shape, img, B):
     """out bytes + distinct touched source bytes, counted from the real taps."""
     import bev_native as nat
@@ -407,6 +437,18 @@ def main():
                    "touched_src_pixels": touched, "avg_us": round(wp_ms * 1e3, 2),
                    "geometry_stage_us": round(stage_wp_ms * 1e3, 2)}
         label, wl = workload(args, world)
+        roof_bb_hbm = None
+        if not args.warp_only and args.backbone.startswith("efficientnet"):
+            # EfficientNet trunk: depthwise / pointwise layers stream their tensors -- HBM-bound, not MFMA-bound
+            nbytes = backbone_bytes(enc, H, W) * VL * B
+            ach_bb = nbytes / (bb_ms * 1e-3) / 1e9
+            roof_bb_hbm = {"kernel": "k_conv + k_dwconv(_t) + k_se_gate (EfficientNet trunk + proj, every launch of "
+                                     "one step)", "bound": "hbm", "achieved": round(ach_bb, 1), "peak": PEAK_HBM_GBS,
+                           "unit": "GB/s", "frac": round(ach_bb / PEAK_HBM_GBS, 4), "traffic": None,
+                           "alg_bytes_per_step": nbytes, "encoder_stage_ms": round(bb_ms, 4),
+                           "timing": "HIP events on the caller stream around the whole encoder stage",
+                           "bytes": "each launch reads its input once and writes its output once (+ residual), "
+                                    "fp32 NHWC (bench.backbone_bytes)"}
         line = {
             "metric": "multi-cam frames/sec (7-cam→480×1440 BEV)" if label == "BASELINE configs[1]" else
                       f"multi-cam frames/sec ({V}-cam→{args.bev[0]}×{args.bev[1]} BEV)",
@@ -423,9 +465,11 @@ def main():
                        "cameras_per_gpu": VL, "bev": list(args.bev), "channels": C,
                        "parallelism": (f"camera-sharded x{world} (reduce-scatter over BEV rows)" if args.camera_shard
                                        else f"frame-sharded x{world} (no collective)")},
-            "roofline": roof_bb if roof_bb else roof_wp,
+            "roofline": roof_bb_hbm or roof_bb or roof_wp,
             "roofline_warp": roof_wp,
         }
+        if roof_bb_hbm:
+            line["roofline_mfma"] = roof_bb
         if args.camera_shard:
             line["roofline_warp"]["note"] = "per-rank partial-sum warp of this rank's cameras; geometry_stage_us " \
                                             "includes the reduce-scatter and the /V"

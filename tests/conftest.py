@@ -32,3 +32,21 @@ def oracle():
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+def gather_results(procs, q, n: int, timeout: float):
+    """n results from spawned rank processes; fails as soon as a rank died instead of waiting out the timeout
+    (a rank that raised never puts its result)."""
+    import queue
+    import time
+    out, t0 = [], time.time()
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=5))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead:
+                raise AssertionError(f"a rank process exited with {dead} before reporting")
+            if time.time() - t0 > timeout:
+                raise AssertionError(f"no result from the rank processes within {timeout} s")
+    return out

@@ -17,7 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN, PKG
+from conftest import GOLDEN, PKG, gather_results
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -116,7 +116,7 @@ def test_camera_sharded_forward_world2_kernel_partials(oracle, tmp_path):
     procs = [ctx.Process(target=_cam_worker, args=(r, 2, port, ref_path, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = dict(gather_results(procs, q, 2, 240))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

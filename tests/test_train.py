@@ -18,7 +18,7 @@ import torch.multiprocessing as mp
 import torch.nn as nn
 import torch.nn.functional as F
 
-from conftest import PKG
+from conftest import PKG, gather_results
 
 
 class _Stand(nn.Module):
@@ -513,8 +513,7 @@ def test_bevnet_ddp_world2_replicas_identical():
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
-        r, init, after, losses = q.get(timeout=240)
+    for r, init, after, losses in gather_results(procs, q, 2, 240):
         res[r] = (init, after, losses)
     for p in procs:
         p.join(60)

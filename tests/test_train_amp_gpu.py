@@ -9,7 +9,8 @@ optimizer are the fp32 gradients times the loss scale, which scaler.unscale_ rem
 
 Tolerances: the fixture pin (bevnet_small.npz, the reference BEVNet's own gradients) uses test_bevnet_gpu's
 fp32 tolerances unchanged (rtol 1e-3, atol 1e-3 x max|ref|); the ResNet-50 BEVNet step is compared with a
-float64 torch restatement of the reference graph (oracle/bevnet_ref.py): outputs and losses rel 1e-4, every
+float64 torch restatement of the reference graph (oracle/bevnet_ref.py; its loss evaluated in fp32 like the
+native run's): outputs and losses rel 1e-4, every
 parameter gradient max|d| <= 1e-3 x max(its own max|ref|, 1e-4 x the largest gradient), BN running statistics
 rel 1e-4.
 """
@@ -26,7 +27,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 import torch.nn as nn
 
-from conftest import GOLDEN, PKG
+from conftest import GOLDEN, PKG, gather_results
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -104,9 +105,10 @@ def _randomize_bn(model, seed):
                 m.weight.copy_(torch.rand(m.num_features, generator=g) + 0.5)
                 m.bias.copy_(torch.rand(m.num_features, generator=g) * 0.4 - 0.2)
         for m in (model.detector.stem[1], model.detector.stem[4], model.detector.stem[7]):
-            m.weight.uniform_(0.5, 1.5, generator=g)
-            m.bias.normal_(0, 0.2, generator=g)
-        model.detector.offset_head.weight.normal_(0, 0.05, generator=g)  # CenterNet init zeroes it
+            m.weight.copy_(torch.rand(m.weight.shape, generator=g) + 0.5)
+            m.bias.copy_(torch.randn(m.bias.shape, generator=g) * 0.2)
+        w = model.detector.offset_head.weight  # the CenterNet init zeroes it
+        w.copy_(torch.randn(w.shape, generator=g) * 0.05)
 
 
 def _reference_copy(model, cfg):
@@ -195,7 +197,11 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
         a, r = preds[k].detach().double().cpu(), out[k].detach()
         err = (a - r).abs().max().item() / max(r.abs().max().item(), 1e-12)
         assert err < 1e-4, (k, err)
-    ref_losses = ref.loss(out, [{"boxes_world": b.double()} for b in boxes], cfg["LOSS"])
+    # the loss is torch code in both (BEVNet.loss); evaluate it in fp32 on the reference graph's outputs, as the
+    # native run does (the focal loss's log(1 - p) near p = 1 is only as precise as fp32 p), so that the
+    # comparison measures the kernels, not fp32-vs-float64 loss arithmetic
+    out32 = {k: v.float() for k, v in out.items()}
+    ref_losses = ref.loss(out32, [{"boxes_world": b} for b in boxes], cfg["LOSS"])
     for k in ("heatmap_loss", "offset_loss", "size_loss", "total_loss"):
         a, r = float(losses[k].detach()), float(ref_losses[k].detach())
         assert abs(a - r) <= 1e-4 * abs(r) + 1e-7, (k, a, r)
@@ -256,7 +262,9 @@ def _r50_ddp_worker(rank, world, port, q):
         model.eval()
         with torch.no_grad():
             ddp(batch)
-        q.put((rank, init, {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters()}, losses,
+        skip = set(bev_dist.unexecuted_parameters(model))  # never run, never synchronised
+        q.put((rank, {k: v for k, v in init.items() if k not in skip},
+               {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters() if k not in skip}, losses,
                init_bufs, bufs(), scaler.get_scale()))
     finally:
         dist.destroy_process_group()
@@ -276,8 +284,7 @@ def test_bevnet_r50_ddp_world2_trainable_trunk_amp():
     for p in procs:
         p.start()
     res = {}
-    for _ in range(2):
-        r, init, after, losses, b0, b1, scale = q.get(timeout=360)
+    for r, init, after, losses, b0, b1, scale in gather_results(procs, q, 2, 360):
         res[r] = (init, after, losses, b0, b1, scale)
     for p in procs:
         p.join(60)

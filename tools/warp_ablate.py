@@ -1,0 +1,57 @@
+"""Time the fused warp with parts of its work removed (tools/warp_ablate.sh variants; WARP_ABLATE bits in
+bev_warp.hip: 1 no mean division, 2 no staging, 4 no LDS sampling, 8 no tap arithmetic, 16 no stores) on the
+bench workload (7 cams, C = 64 channels-last, 135 x 240 features -> 480 x 1440, mean, batch 2).  Results of
+the variants are wrong by construction; only their launch times are read.
+
+    python tools/warp_ablate.py 0 1 2 4 8 16
+"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "vision-based-spatio-temporal-analysis_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+import bev_native as nat  # noqa: E402
+import bev_rig  # noqa: E402
+from models.fusion.geometry import GeometryTransformer  # noqa: E402
+from bench import BOUNDS  # noqa: E402
+
+
+def main():
+    bits = sys.argv[1:] or ["0"]
+    dev = torch.device("cuda")
+    B, V, C, H, W, Hf, Wf = 2, 7, 64, 1080, 1920, 135, 240
+    feats = torch.randn(B, V, Hf, Wf, C, device=dev).permute(0, 1, 4, 2, 3)
+    geom = GeometryTransformer(480, 1440, BOUNDS)
+    K, Rt = bev_rig.rig(V, H, W, B)
+    Hm, xs, ys, hw = geom._sampling(feats, torch.from_numpy(K).to(dev), torch.from_numpy(Rt).to(dev), (H, W))
+    sx, sy = nat._scales(Hf, Wf, hw)
+    out = torch.empty(B, C, 480, 1440, device=dev)
+    s = feats.stride()
+    libs = {b: ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{b}.so")) for b in bits}
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    args = (nat._ptr(feats), s[1], s[2], s[3], s[4], nat._ptr(Hm), nat._ptr(xs), nat._ptr(ys), B, V, C, Hf, Wf, sx, sy,
+            480, 1440, 1, nat._ptr(out), st)
+    for L in libs.values():
+        L.bev_ipm_warp_fuse_f32.restype = ctypes.c_int
+        L.bev_ipm_warp_fuse_f32.argtypes = nat.SIGNATURES["bev_ipm_warp_fuse_f32"][1]
+    for rnd in range(3):
+        for b, L in libs.items():
+            for _ in range(3):
+                assert L.bev_ipm_warp_fuse_f32(*args) == 0
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            n = 30
+            for _ in range(n):
+                L.bev_ipm_warp_fuse_f32(*args)
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"round {rnd} variant {b:>6}: {e0.elapsed_time(e1) / n * 1e3:8.1f} us per launch", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -125,6 +125,20 @@ def non_persistent_buffers(model: torch.nn.Module):
     return names
 
 
+def unexecuted_parameters(model: torch.nn.Module):
+    """Fully qualified names of trunk parameters the forward never uses: timm features_only builds every
+    stage, CNNEncoder keeps feats_list[out_index] (cnn_encoder.py:41-42) and the stages past it are not run.
+    A single-GPU loop does not notice; DDP would wait for their gradients forever (or need
+    find_unused_parameters, a graph walk every step), so they are excluded from synchronisation."""
+    names = []
+    for mname, m in model.named_modules():
+        bb = getattr(m, "backbone", None)
+        if bb is not None and hasattr(bb, "unexecuted_parameter_names") and hasattr(m, "out_index"):
+            pre = f"{mname}.backbone." if mname else "backbone."
+            names += [pre + n for n in bb.unexecuted_parameter_names(m.out_index)]
+    return names
+
+
 def ddp_wrap(model: torch.nn.Module, device: Optional[torch.device] = None, bucket_cap_mb: float = 25.0,
              broadcast_buffers: bool = True):
     """DistributedDataParallel over the default group (RCCL on ROCm, gloo on CPU).  Frozen parameters
@@ -134,9 +148,11 @@ def ddp_wrap(model: torch.nn.Module, device: Optional[torch.device] = None, buck
     reference's batch under weak scaling) and updates its running statistics from them.  With
     broadcast_buffers (DDP's default, kept) rank 0's running statistics are broadcast at every forward, so all
     replicas hold the same buffers and the checkpoint rank 0 writes (train.py:336-343) is what every rank would
-    write; the ground grid / pos-enc (non-persistent, config-derived) are excluded from that broadcast."""
+    write; the ground grid / pos-enc (non-persistent, config-derived) are excluded from that broadcast, and so are
+    the trunk stages the encoder never runs (unexecuted_parameters)."""
     from torch.nn.parallel import DistributedDataParallel
-    DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(model, non_persistent_buffers(model))
+    DistributedDataParallel._set_params_and_buffers_to_ignore_for_model(
+        model, non_persistent_buffers(model) + unexecuted_parameters(model))
     ids = [device.index] if device is not None and device.type == "cuda" else None
     return DistributedDataParallel(model, device_ids=ids, broadcast_buffers=broadcast_buffers,
                                    bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True)

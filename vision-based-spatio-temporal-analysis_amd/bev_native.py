@@ -636,7 +636,7 @@ def conv_wgrad_ex(x: torch.Tensor, dz: torch.Tensor, K: int, pad: int, dilation:
     dW = torch.empty(Cop, KH, KW, Cip, device=x.device, dtype=torch.float32)
     _check(lib().bev_conv_wgrad_ex_f32(_ptr(xp), N, H, W, Cip, _ptr(dzp), Ho, Wo, Cop, KH, KW, stride, pad, dilation,
                                        _ptr(dW), _stream(x)), "bev_conv_wgrad_ex_f32")
-    return dW[:Co, :, :, :Ci].permute(0, 3, 1, 2)
+    return dW[:Co, :, :, :Ci].permute(0, 3, 1, 2).contiguous()  # the parameter's OIHW strides (DDP bucket views)
 
 
 def _gn_workspace(N, P, C, G, device):

@@ -65,8 +65,17 @@ __device__ __forceinline__ void cell_ixy(const float h[9], float x, float y, con
     const float u1 = dot3(h[3], h[4], h[5], x, y, 1.0f);
     const float w = dot3(h[6], h[7], h[8], x, y, 1.0f);
     const float ws = (__builtin_fabsf(w) < 1e-6f) ? 1.0f : w;
-    const float u = u0 / ws;
-    const float v = u1 / ws;
+    // u0 / ws and u1 / ws as IEEE f32 divisions, through ONE double reciprocal of ws: rcp_f64 refined by two
+    // Newton steps is within ~2^-53 of 1/ws, so (double)u0 * rws lies within 2^-51 (relative) of the exact
+    // quotient, inside div_rcp's 2^-49 midpoint margin -> the same float as u0 / ws (12 VALU instead of the
+    // two 13-instruction f32 division sequences).
+    const double wd = (double)ws;
+    double rws = __builtin_amdgcn_rcp(wd);
+    rws = __builtin_fma(rws, __builtin_fma(-wd, rws, 1.0), rws);
+    rws = __builtin_fma(rws, __builtin_fma(-wd, rws, 1.0), rws);
+    if (__builtin_isinf(ws)) rws = __builtin_copysign(0.0, wd);  // x / inf (the Newton step would give NaN)
+    const float u = div_rcp(u0, rws);
+    const float v = div_rcp(u1, rws);
     // geometry.py:151-158
     const float fx = u * sx;
     const float fy = v * sy;

@@ -175,6 +175,13 @@ class EfficientNet(nn.Module):
         y, ps = self._fdw(blk.conv_dw, blk.bn2)(h, want_psum=True)
         return self._project(blk.conv_pwl, blk.bn3, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
 
+    def unexecuted_parameter_names(self, out_index: int):
+        """Parameters of the stages past features_only[out_index]: never run, so never given a gradient
+        (DistributedDataParallel must not wait for them)."""
+        last = FEATURE_STAGE[out_index]
+        return [f"blocks.{si}.{n}" for si in range(last + 1, len(self.blocks))
+                for n, _ in self.blocks[si].named_parameters()]
+
     def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC features_only[out_index]."""
         if out_index not in FEATURE_STAGE:

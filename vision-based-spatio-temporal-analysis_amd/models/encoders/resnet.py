@@ -285,6 +285,12 @@ class ResNet(nn.Module):
             self._folded[k] = FoldedConv(conv, bn)
         return self._folded[k]
 
+    def unexecuted_parameter_names(self, out_index: int):
+        """Parameters of the residual stages past features_only[out_index] (not run: stage_of), which never
+        receive a gradient (DistributedDataParallel must not wait for them)."""
+        return [f"layer{li}.{n}" for li in range(stage_of(out_index) + 1, 5)
+                for n, _ in getattr(self, f"layer{li}").named_parameters()]
+
     def forward_features_nhwc(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """x: images [N,3,H,W] NCHW fp32 on the device -> NHWC feature map of features_only[out_index]."""
         if self.training:  # torch semantics: train-mode BN uses batch statistics, with or without autograd
