@@ -47,7 +47,8 @@ int bev_abi_version(void);
  * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.
- * BEV_TUNE_WGRAD_MFMA: 1 (default) = conv weight gradient on the MFMA, 0 = the VALU float4 kernel.
+ * BEV_TUNE_WGRAD_MFMA: conv weight gradient on the MFMA with natural-layout operands copied by LDS-DMA
+ *   (2, default), on the MFMA with transposed register staging (1), or the VALU float4 kernel (0).
  * BEV_TUNE_CONV_DMA: NHWC Ci % 32 == 0 convs stage their operands global -> LDS by LDS-DMA on
  *   1 (default) = the 64-column output tiles, 2 = every tile, 0 = none (through registers); same
  *   results bit for bit. */

@@ -311,10 +311,11 @@ WGRAD_CASES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mfma", [1, 0], ids=["mfma", "valu"])
+@pytest.mark.parametrize("mfma", [2, 1, 0], ids=["mfma_nat", "mfma_transposed", "valu"])
 @pytest.mark.parametrize("case", WGRAD_CASES, ids=[f"ci{c[1]}_co{c[4]}_k{c[5]}s{c[6]}" for c in WGRAD_CASES])
 def test_wgrad_and_colsum_vs_torch(case, mfma):
-    """bev_conv_wgrad_f32 (MFMA kernel and the VALU float4 kernel) / bev_colsum_f32 vs torch's conv2d weight /
+    """bev_conv_wgrad_f32 (the natural-layout LDS-DMA MFMA kernel, the transposed-staging MFMA kernel, the VALU
+    float4 kernel) / bev_colsum_f32 vs torch's conv2d weight /
     bias gradients (fp32; float atomics change the summation order: rtol 1e-4 of the gradient scale)."""
     import bev_native as nat
     N, Ci, H, W, Co, k, s, p = case

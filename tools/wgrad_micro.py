@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("layers", nargs="*", default=list(LAYERS))
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--kernels", type=int, nargs="*", default=[2, 1], help="BEV_TUNE_WGRAD_MFMA values to A/B")
     a = ap.parse_args()
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -38,17 +39,23 @@ def main():
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         x = torch.randn(N, H, W, Ci, device=dev, generator=g)
         dz = torch.randn(N, Ho, Wo, Co, device=dev, generator=g)
-        for _ in range(2):
-            nat.conv_wgrad(x, dz, k, k, s, p)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.iters):
-            nat.conv_wgrad(x, dz, k, k, s, p)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / a.iters
-        flops = 2.0 * N * Ho * Wo * Co * Ci * k * k
-        print(f"{name:6s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF", flush=True)
+        ref = None
+        for kern in a.kernels:
+            with nat.tuned(WGRAD_MFMA=kern):
+                for _ in range(2):
+                    dw = nat.conv_wgrad(x, dz, k, k, s, p)
+                ref = dw if ref is None else ref
+                err = float((dw - ref).abs().max() / ref.abs().max())
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    nat.conv_wgrad(x, dz, k, k, s, p)
+                e1.record()
+                torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            flops = 2.0 * N * Ho * Wo * Co * Ci * k * k
+            print(f"{name:6s} kernel {kern}: {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  (rel diff vs first {err:.1e})",
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -23,7 +23,9 @@
 
 namespace {
 
-int g_wgrad_mfma = 1;  // bev_tune(BEV_TUNE_WGRAD_MFMA): 0 = the VALU k_wgrad_v4 (A/B)
+int g_wgrad_mfma = 2;  // bev_tune(BEV_TUNE_WGRAD_MFMA): 2 = k_wgrad_nat (default), 1 = k_wgrad_mfma, 0 = k_wgrad_v4
+typedef float wf32x16 __attribute__((ext_vector_type(16)));
+typedef float wf32x4 __attribute__((ext_vector_type(4)));
 
 inline int last() {
     const hipError_t e = hipGetLastError();
@@ -197,7 +199,174 @@ __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, c
 }
 
 
-// ---- weight gradient on the MFMA --------------------------------------------------------------------
+// ---- weight gradient on the MFMA, natural-layout operands by LDS-DMA (default) ----------------------
+// v_mfma_f32_32x32x2_f32 takes ONE A and ONE B value per lane: A[i][kk] from lane i + 32 kk, B[kk][j] from
+// lane j + 32 kk.  For dW = dz^T im2col(x) the MFMA's reduction index kk is the output pixel m, so a lane needs
+// dz[m0 + kk][co0 + i] and im2col(x)[m0 + kk][k0 + j]: 32 consecutive elements of ONE pixel row per half-wave,
+// i.e. both operands in their natural [pixel][channel] layout.  Each step therefore copies 32 pixel rows of
+// both operands global -> LDS with global_load_lds_dwordx4 (no staging registers, no transposing ds_writes;
+// invalid taps / rows read a zero quad), double-buffered, and the fragments are conflict-free ds_read_b32 of
+// consecutive dwords.  Same tiles, m split and float-atomic epilogue as k_wgrad_mfma below.
+__device__ __attribute__((aligned(16))) float g_wzero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
+
+__device__ __forceinline__ unsigned wg_lds_base(const void *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char *)p;
+}
+
+__device__ __forceinline__ void wg_dma16(const float *src, unsigned dst_any) {
+    const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)dst_any);  // wave-uniform LDS address
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(dst)
+        : "memory");
+}
+
+template <int WCO, int TM, int TN>
+__global__ __launch_bounds__(256, 2) void k_wgrad_nat(const float *__restrict__ x, const float *__restrict__ dz, int N,
+                                                      int H, int W, int Ci, int Ho, int Wo, int Co, int KW, int K,
+                                                      int stride, int pad, int dil, int64_t mchunk, int ctiles,
+                                                      int ntiles, float *__restrict__ dW) {
+    constexpr int WK = 4 / WCO, CT = WCO * TM * 32, KT = WK * TN * 32;
+    constexpr int AF = CT / 4, BF = KT / 4;             // float4 per pixel row of each operand
+    constexpr int QA = 32 * AF / 256, QB = 32 * BF / 256;  // DMA instructions per wave and step
+    constexpr int STAGE = 32 * (CT + KT);               // floats per stage
+    static_assert((32 * AF) % 256 == 0 && (32 * BF) % 256 == 0, "whole DMA instructions per wave");
+    __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int tile = (int)(bid % (unsigned)ntiles);
+    const int64_t split = bid / (unsigned)ntiles;
+    const int co0 = (tile % ctiles) * CT, k0 = (tile / ctiles) * KT;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int64_t mb = split * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    if (mb >= me) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wco = wave / WK, wk = wave % WK;
+
+    // first pixel of the step being copied, as (image, row, column); each DMA instruction's pixel rows and
+    // channel columns are decoded on the fly (few registers: up to 16 instructions per wave and step)
+    int mpx, mpy, mpn;
+    {
+        const int64_t t = mb / Wo;
+        mpx = (int)(mb - t * Wo);
+        mpy = (int)(t % Ho);
+        mpn = (int)(t / Ho);
+    }
+    const unsigned lbase = wg_lds_base(lds);
+    int64_t ms = mb;
+    auto issue = [&](int buf) {
+        const unsigned d0 = lbase + (unsigned)(buf * STAGE * 4);
+#pragma unroll
+        for (int q = 0; q < QA; ++q) {
+            const int f = (wave + 4 * q) * 64 + lane, row = f / AF, col = f % AF;
+            const int64_t m = ms + row;
+            const float *src = (m < me && co0 + 4 * col < Co) ? dz + m * Co + co0 + 4 * col : g_wzero4;
+            wg_dma16(src, d0 + (unsigned)((wave + 4 * q) * 1024));
+        }
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+            const int f = (wave + 4 * q) * 64 + lane, row = f / BF;
+            const int k = k0 + 4 * (f % BF);
+            const int tap = k / Ci, ci = k - tap * Ci, ky = tap / KW, kx = tap - ky * KW;
+            int px = mpx + row, py = mpy, pn = mpn;
+            while (px >= Wo) {  // rows of one step span at most 32 pixels
+                px -= Wo;
+                if (++py == Ho) {
+                    py = 0;
+                    ++pn;
+                }
+            }
+            const int iy = py * stride - pad + ky * dil, ix = px * stride - pad + kx * dil;
+            const bool in = ms + row < me && k < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const float *src = in ? x + (((int64_t)pn * H + iy) * W + ix) * Ci + ci : g_wzero4;
+            wg_dma16(src, d0 + (unsigned)(CT * 32 * 4 + (wave + 4 * q) * 1024));
+        }
+        ms += 32;
+        mpx += 32;
+        while (mpx >= Wo) {
+            mpx -= Wo;
+            if (++mpy == Ho) {
+                mpy = 0;
+                ++mpn;
+            }
+        }
+    };
+    wf32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (wf32x16){0};
+    const int nsteps = (int)((me - mb + 31) / 32);
+    issue(0);
+    const int r32 = lane & 31, h = lane >> 5;
+    for (int st = 0; st < nsteps; ++st) {
+        if (st + 1 < nsteps) {
+            issue((st + 1) & 1);
+            // this wave's copies of step st are done; the ones of step st + 1 stay in flight
+            if (QA + QB == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else if (QA + QB == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (QA + QB == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if (QA + QB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (QA + QB == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();  // every wave's share of step st is in LDS
+        const float *As = lds + (st & 1) * STAGE, *Bs = As + CT * 32;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) {
+            const int row = 2 * p + h;
+            float fa[TM], fb[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[i] = As[row * CT + wco * TM * 32 + i * 32 + r32];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[j] = Bs[row * KT + wk * TN * 32 + j * 32 + r32];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();  // step st's buffer is free for step st + 2
+    }
+    // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int k = k0 + wk * TN * 32 + j * 32 + r32;
+            if (k >= K) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int co = co0 + wco * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (co < Co) atomicAdd(dW + (int64_t)co * K + k, acc[i][j][r]);
+            }
+        }
+}
+
+template <int WCO, int TM, int TN>
+int launch_wgrad_nat(const float *x, const float *dz, int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
+                     int K, int stride, int pad, int dil, float *dW, hipStream_t st) {
+    constexpr int CT = WCO * TM * 32, KT = (4 / WCO) * TN * 32;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int ct = (Co + CT - 1) / CT, kt = (K + KT - 1) / KT, nt = ct * kt;
+    int64_t sp = 1024 / nt + 1;  // >= ~1024 workgroups (2 per CU resident)
+    int64_t mc = (M + sp - 1) / sp;
+    mc = ((mc + 31) / 32) * 32;
+    sp = (M + mc - 1) / mc;
+    if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL((k_wgrad_nat<WCO, TM, TN>), dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho,
+                       Wo, Co, KW, K, stride, pad, dil, mc, ct, nt, dW);
+    return 0;
+}
+
+// ---- weight gradient on the MFMA, transposed staging (BEV_TUNE_WGRAD_MFMA = 1) ------------------------
 // dW[co][k] = sum_m dz[m][co] * im2col(x)[m][k] as a GEMM whose reduction runs over the output pixels m.
 // Workgroup tile CT (co) x KT (k) = (WCO x TM x 32) x (WK x TN x 32), WCO x WK = 4 waves of TM x TN
 // v_mfma_f32_32x32x2_f32 tiles -- 128 x 128 in general, 64 x 256 for 64-channel layers, 256 x 64 for K = 64,
@@ -208,8 +377,6 @@ __global__ __launch_bounds__(256) void k_wgrad_v4(const float *__restrict__ x, c
 // channels) is decoded once, and the output pixels of its rows advance incrementally.  The m range is split
 // over a 1-D XCD-aware grid (the tiles of one m split run on one XCD and share its L2); partial tiles are
 // added with float atomics (summation order varies in the last bits, as in k_wgrad).
-typedef float wf32x16 __attribute__((ext_vector_type(16)));
-typedef float wf32x4 __attribute__((ext_vector_type(4)));
 constexpr int WM_BM = 32, WM_LROW = 36;
 
 // LDS element (row c, pixel m) of a staged operand: 36-float rows; the 16-B group of m is XOR-swizzled by
@@ -581,7 +748,16 @@ int bev_conv_wgrad_ex_f32(const float *x, int N, int H, int W, int Ci, const flo
         // tile shape by the narrow dimension: 32 x 512 (Co <= 32), 64 x 256 (Co <= 64), 256 x 64 (K <= 64),
         // else 128 x 128
         int rc;
-        if (Co <= 32)
+        if (g_wgrad_mfma == 2) {
+            if (Co <= 32)
+                rc = launch_wgrad_nat<1, 1, 4>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+            else if (Co <= 64)
+                rc = launch_wgrad_nat<1, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+            else if (K <= 64)
+                rc = launch_wgrad_nat<4, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+            else
+                rc = launch_wgrad_nat<2, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
+        } else if (Co <= 32)
             rc = launch_wgrad_mfma<1, 1, 4>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
         else if (Co <= 64)
             rc = launch_wgrad_mfma<1, 2, 2>(x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K, stride, pad, dil, dW, st);
@@ -638,7 +814,7 @@ int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, in
 
 namespace bev {
 int train_tune(int knob, int value) {
-    if (knob != BEV_TUNE_WGRAD_MFMA || value < 0 || value > 1) return BEV_ERR_ARGS;
+    if (knob != BEV_TUNE_WGRAD_MFMA || value < 0 || value > 2) return BEV_ERR_ARGS;
     const int old = g_wgrad_mfma;
     g_wgrad_mfma = value;
     return old;

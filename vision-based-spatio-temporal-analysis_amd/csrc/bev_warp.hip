@@ -705,12 +705,20 @@ __device__ __forceinline__ void tile_cell(int lane, int wave, int &r, int &c) {
     }
 }
 
-template <int MODE, int OCC, int TH = 8>
+// Frames per workgroup (FPW = 2, tcache >= 0): a static rig gives every frame of a batch the same homographies
+// (Wildtrack's cameras do not move), so the workgroup of a tile runs the frames one after the other and the
+// second pass reads each cell's taps from an LDS record written by the first instead of recomputing them:
+// (x0, y0) as int16 (-32768: no valid tap along that axis) + the fractional offsets we = ix - floor(ix) and
+// n = iy - floor(iy), from which the weights and validity bits are rebuilt with the same fp32 operations
+// (bit-identical).  The geometry is compared per view in the prologue; frames that differ take a full pass.
+// The same records serve every further 64-channel chunk of a frame.
+template <int MODE, int OCC, int TH = 8, int FPW = 1>
 __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                           int64_t sW, const float *__restrict__ Hmat,
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
-                                                          int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
-                                                          int Wb, float *__restrict__ out, int pool) {
+                                                          int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                                                          int Hb, int Wb, float *__restrict__ out, int pool,
+                                                          int tcache) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
     constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
@@ -732,50 +740,58 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     tile_cell<TH>(lane, wave, tr, tc);
     const int i = tyb * TH + tr;
     const int j = txb * TW + tc;
-    const int b = blockIdx.y;
+    const int b0 = blockIdx.y * FPW;
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
     const Grid grid = make_grid(Hf, Wf);
     const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+    unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes, [2 V] same flag
+    unsigned *tc0 = reinterpret_cast<unsigned *>(smem + (tcache >= 0 ? tcache : 0));  // [V][256] packed x0, y0
+    float2 *tc1 = reinterpret_cast<float2 *>(tc0 + V * FT_NT);                         // [V][256] (we, n)
 
-    // corner boxes of this tile, lane v <-> view v, packed in two VGPRs:
-    // lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16  (x1 + 1 == 0: empty)
+    // corner boxes of this tile for frame bb, lane v <-> view v, packed in two VGPRs (wave 0 computes them in
+    // double, the others read them): lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16
+    // (x1 + 1 == 0: empty).  With FPW = 2 wave 0 also compares frame bb + 1's homographies with bb's.
     unsigned lba = 0, lbb = 0;
-    unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes (WARP_OPT & 1)
-    if (!(WARP_OPT & 1) || wave == 0) {
-        const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
-        const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
-        Box cb{0x7fffffff, 0x7fffffff, -1, -1};
-        bool ok = true;
-        if (lane < V) {
-            float hv[9];
-            load_h(Hmat, b * V + lane, hv);
-            if (wave == 0) {
+    bool same = false;
+    auto prologue = [&](int bb, bool check_next) {
+        if (wave == 0) {
+            const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
+            const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
+            Box cb{0x7fffffff, 0x7fffffff, -1, -1};
+            bool ok = true, eq = true;
+            if (lane < V) {
+                float hv[9];
+                load_h(Hmat, bb * V + lane, hv);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) htab[lane * 9 + q] = hv[q];  // visible after the prologue barrier
+                for (int q = 0; q < 9; ++q) htab[lane * 9 + q] = hv[q];  // visible after the barrier below
+                if (check_next) {
+                    float hn[9];
+                    load_h(Hmat, (bb + 1) * V + lane, hn);
+#pragma unroll
+                    for (int q = 0; q < 9; ++q) eq = eq && (__float_as_uint(hn[q]) == __float_as_uint(hv[q]));
+                }
+                cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok);
+                // large footprints: the exact per-cell box (usually much smaller near the
+                // horizon, where adjacent cell rows map far apart) decides the staging
+                if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
             }
-            cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok);
-            // large footprints: the exact per-cell box (usually much smaller near the
-            // horizon, where adjacent cell rows map far apart) decides the staging
-            if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
-        }
-        const bool emp = cb.x1 < 0;
-        lba = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
-        lbb = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
-    }
-    if (WARP_OPT & 1) {  // one wave computes the boxes (double arithmetic), the others read them
-        if (wave == 0 && lane < V) {
-            btab[2 * lane] = lba;
-            btab[2 * lane + 1] = lbb;
+            const bool emp = cb.x1 < 0;
+            if (lane < V) {
+                btab[2 * lane] = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
+                btab[2 * lane + 1] = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
+            }
+            const bool all_eq = check_next && __ballot(lane < V && !eq) == 0ull;
+            if (lane == 0) btab[2 * V2_MAXV] = all_eq ? 1u : 0u;
         }
         __syncthreads();
-        if (lane < V) {
-            lba = btab[2 * lane];
-            lbb = btab[2 * lane + 1];
-        }
-    }
+        lba = lane < V ? btab[2 * lane] : 0u;
+        lbb = lane < V ? btab[2 * lane + 1] : 0u;
+        same = btab[2 * V2_MAXV] != 0u;
+    };
+    prologue(b0, FPW > 1 && b0 + 1 < B && tcache >= 0);
     auto box_of = [&](int v) {
         const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
         const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
@@ -784,11 +800,39 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
 
     float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
+    bool cache_rd = false;     // this chunk reads the tap records (written by an earlier chunk / frame)
     auto taps_of = [&](int v) {
+        Taps t;
+        if (cache_rd) {
+            const unsigned pk = tc0[v * FT_NT + tid];
+            const float2 f = tc1[v * FT_NT + tid];
+            const int x0s = (int)(short)(pk & 0xffffu), y0s = (int)(short)(pk >> 16);
+            const float e = 1.0f - f.x, s = 1.0f - f.y;  // taps_from_ixy's arithmetic
+            t.w[0] = s * e;
+            t.w[1] = s * f.x;
+            t.w[2] = f.y * e;
+            t.w[3] = f.y * f.x;
+            const bool vx0 = x0s >= 0 && x0s < Wf, vx1 = x0s >= -1 && x0s + 1 < Wf;
+            const bool vy0 = y0s >= 0 && y0s < Hf, vy1 = y0s >= -1 && y0s + 1 < Hf;
+            t.valid = (unsigned)(vx0 & vy0) | ((unsigned)(vx1 & vy0) << 1) | ((unsigned)(vx0 & vy1) << 2) |
+                      ((unsigned)(vx1 & vy1) << 3);
+            t.x0 = (vx0 | vx1) ? x0s : 0;
+            t.y0 = (vy0 | vy1) ? y0s : 0;
+            return t;
+        }
         float h[9];
 #pragma unroll
         for (int q = 0; q < 9; ++q) h[q] = htab[v * 9 + q];  // uniform LDS address: broadcast
-        Taps t = cell_taps(h, ccx, ccy, grid, sx, sy);
+        float ix, iy;
+        cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
+        t = taps_from_ixy(ix, iy, grid);
+        if (FPW > 1 && tcache >= 0) {
+            const float xw = __builtin_floorf(ix), yn = __builtin_floorf(iy);
+            const bool xv = xw >= -1.0f && xw < grid.fWf, yv = yn >= -1.0f && yn < grid.fHf;  // vx0 | vx1, vy0 | vy1
+            const int x0s = (inside && xv) ? t.x0 : -32768, y0s = (inside && yv) ? t.y0 : -32768;
+            tc0[v * FT_NT + tid] = ((unsigned)x0s & 0xffffu) | ((unsigned)y0s << 16);
+            tc1[v * FT_NT + tid] = make_float2(ix - xw, iy - yn);
+        }
         if (WARP_ABLATE & 8) {
             const Box bb = box_of(v);
             t.x0 = bb.x0 + (lane & 1);
@@ -800,7 +844,15 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         return t;
     };
 
-    for (int c0 = 0; c0 < C; c0 += 64) {
+    for (int pass = 0; pass < FPW; ++pass) {
+      const int b = b0 + pass;
+      if (b >= B) break;
+      if (pass > 0 && !same) {  // this frame's geometry differs: its own boxes and homographies
+          __syncthreads();
+          prologue(b, false);
+      }
+      for (int c0 = 0; c0 < C; c0 += 64) {
+        cache_rd = FPW > 1 && tcache >= 0 && (c0 > 0 || (pass > 0 && same));
         ccx = cx;
         ccy = cy;
         asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep taps per chunk (no hoisting + spills)
@@ -928,6 +980,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             __syncthreads();  // all of it landed; image of view v and red[] are free
         }
         if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+      }
     }
 }
 
@@ -1105,25 +1158,31 @@ int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
 #ifndef WARP_TILE_H
 #define WARP_TILE_H 16  // fused-warp tile: 16 x 16 (default) or 8 x 32 cells (A/B builds)
 #endif
+#ifndef WARP_PAIR
+#define WARP_PAIR 1  // frames per workgroup with the LDS tap records: 0 off, 1 on (pool shrunk to keep 3 WG / CU)
+#endif
+constexpr int V2_FIXED = 256 + 4 * (FT_NT / 64) * (int)sizeof(int) + V2_MAXV * 9 * (int)sizeof(float) +
+                         (2 * V2_MAXV + 4) * (int)sizeof(unsigned);  // zero pixel, red, htab, btab + flag
+constexpr int V2_TC_MAXV = 8;  // tap records only for rigs of up to 8 cameras (12 B per cell and view)
 
-template <int OCC>
+template <int OCC, int FPW>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                       int mode, float *out, hipStream_t st, int pool) {
+                       int mode, float *out, hipStream_t st, int pool, int tc_bytes) {
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
-    dim3 grid(ntiles, B), block(FT_NT);
-    const size_t lds = pool + 256 + 4 * (FT_NT / 64) * sizeof(int) + V2_MAXV * 9 * sizeof(float) +
-                       V2_MAXV * 2 * sizeof(unsigned);
+    dim3 grid(ntiles, (B + FPW - 1) / FPW), block(FT_NT);
+    const int tcache = tc_bytes > 0 ? pool + V2_FIXED : -1;
+    const size_t lds = (size_t)pool + V2_FIXED + (tc_bytes > 0 ? tc_bytes : 0);
     if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
-                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache);
     else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
-                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache);
     else
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs,
-                           ys, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool);
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache);
     return last();
 }
 
@@ -1131,10 +1190,19 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                           int Hb, int Wb, int mode, float *out, hipStream_t st) {
     if (mode == BEV_FUSE_MAX)  // MAX's extra live state spills at 3 workgroups per CU
-        return launch_fuse_v2_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                     g_warp_pool_kb ? g_warp_pool_kb * 1024 : 72 * 1024);
-    return launch_fuse_v2_occ<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                 g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024);
+        return launch_fuse_v2_occ<2, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                        st, g_warp_pool_kb ? g_warp_pool_kb * 1024 : 72 * 1024, 0);
+    // tap records: worth it when a workgroup runs two frames or several 64-channel chunks
+    const int tc_bytes = V * FT_NT * 12;
+    const bool pair = WARP_PAIR && V <= V2_TC_MAXV && (B > 1 || C > 64);
+    // 3 workgroups per CU: pool + fixed + records <= 160 KiB / 3 (the pool shrinks by the records)
+    const int budget = 163840 / 3 - V2_FIXED - 64;
+    const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : ((pair ? budget - tc_bytes : 49 * 1024) & ~1023);
+    if (pair && pool >= 16 * 1024 && pool + V2_FIXED + tc_bytes <= 160 * 1024)
+        return launch_fuse_v2_occ<3, 2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                        pool, tc_bytes);
+    return launch_fuse_v2_occ<3, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                    g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024, 0);
 }
 
 }  // namespace
