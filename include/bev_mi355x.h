@@ -276,6 +276,26 @@ int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, in
                                int Ho, int Wo, float *dx, void *stream);
 
 /* ---------------------------------------------------------------------------
+ * Mixed precision (train.py:238-247, configs/wildtrack.yaml:45 USE_AMP): the convolutions a training step
+ * runs under torch.autocast(float16) -- fp16 operands (round to nearest even, as autocast's casts), fp32
+ * accumulation -- on the fp16 matrix cores.  Activations stay fp32 NHWC; NHWC Ci % 32 == 0.
+ * ------------------------------------------------------------------------- */
+
+/* host: number of fp16 elements of a packed weight panel ([Co pad 128][K pad 32]). */
+int64_t bev_conv_packed_size_h16(int Co, int Ci, int KH, int KW);
+
+/* device: OIHW fp32 weights -> fp16 panel (k = (ky*KW + kx)*Ci + ci), packed [size] uint16 storage. */
+int bev_conv_pack_weights_h16(const float *w, int Co, int Ci, int KH, int KW, uint16_t *packed, void *stream);
+
+/* device: y[m][n] (row pitch ldy) = act(sum_k f16(x)[m][k] * packed[n][k] + bias[n] (+ residual[m][n])),
+ * fp32 sum, NHWC x [N][H][W][Ci] fp32, stride / pad / dilation as bev_conv2d_nhwc_ex_f32; act 0 none,
+ * 1 ReLU, 2 SiLU; bias / residual may be NULL (residual needs ldy == Co).  Replaces nn.Conv2d under autocast
+ * (cnn_encoder.py:26 timm trunk, detector.py:16-30 head) forward and input-gradient convolutions. */
+int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                       const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
+                       float *y, int ldy, int Ho, int Wo, void *stream);
+
+/* ---------------------------------------------------------------------------
  * CenterNet BEV head (BEVDetector, detector.py:16-62): dilated convs, GroupNorm(32) + ReLU
  * ------------------------------------------------------------------------- */
 

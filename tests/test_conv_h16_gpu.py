@@ -1,0 +1,118 @@
+"""bev_conv2d_h16_f32: the autocast(float16) convolution (fp16 operands, fp32 accumulation) on the fp16 matrix
+cores, against a float64 convolution of the fp16-rounded operands.
+
+The products of two fp16 values are exact in fp32, so the kernel's only error is the fp32 summation order: the
+bar is the worst-case fp32 summation bound K * 2^-24 * sum_k |x_k w_k| per output (K = Ci * KH * KW), and the
+typical error must sit far below it (max err / sum|terms| < 2e-6).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _case(N, H, W, Ci, Co, K, stride, pad, dil, act, residual=False, ldy=None, seed=0):
+    import bev_native as nat
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, H, W, Ci, generator=g)
+    w = torch.randn(Co, Ci, K, K, generator=g) / (Ci * K * K) ** 0.5
+    b = torch.randn(Co, generator=g)
+    Ho = (H + 2 * pad - dil * (K - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dil * (K - 1) - 1) // stride + 1
+    r = torch.randn(N, Ho, Wo, Co, generator=g) if residual else None
+    with nat._half_mode(True):
+        packed = nat.pack_conv_weight(w.to(DEV))
+    assert packed.dtype == torch.float16
+    out = None
+    if ldy is not None:
+        out = torch.full((N, Ho, Wo, ldy), 7.0, device=DEV)
+    y = nat.conv2d_nhwc_h16(x.to(DEV), packed, b.to(DEV), Co, K, K, stride, pad, dil, act,
+                            residual=None if r is None else r.to(DEV), out=out)
+    torch.cuda.synchronize()
+    y = y.cpu().double()
+    # float64 reference of the fp16-rounded operands
+    xh, wh = x.half().double().permute(0, 3, 1, 2), w.half().double()
+    z = F.conv2d(xh, wh, None, stride, pad, dil).permute(0, 2, 3, 1)
+    mag = F.conv2d(xh.abs(), wh.abs(), None, stride, pad, dil).permute(0, 2, 3, 1)
+    ref = z + b.double()
+    if r is not None:
+        ref = ref + r.double()
+    if act == 1:
+        ref = ref.clamp_min(0)
+    elif act == 2:
+        ref = ref * torch.sigmoid(ref)
+    if ldy is not None:
+        assert bool((y[..., Co:] == 7.0).all()), "columns past Co written"
+        y = y[..., :Co]
+    Kt = Ci * K * K
+    err = (y - ref).abs()
+    bound = Kt * 2.0 ** -24 * (mag + b.double().abs() + (r.double().abs() if r is not None else 0)) + 1e-6
+    if act == 2:
+        bound = bound * 1.2 + 1e-6
+    assert bool((err <= bound).all()), float((err - bound).max())
+    assert float((err / (mag + 1e-3)).max()) < 2e-6
+    # and it is the fp16 arithmetic, not fp32: the fp32 conv of the raw operands differs
+    z32 = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), None, stride, pad, dil).permute(0, 2, 3, 1)
+    assert float((z32 - z).abs().max()) > 10 * float(err.max())
+
+
+@pytest.mark.parametrize("shape", [
+    dict(N=2, H=20, W=24, Ci=64, Co=128, K=3, stride=1, pad=1, dil=1, act=0),
+    dict(N=1, H=17, W=33, Ci=32, Co=200, K=3, stride=2, pad=1, dil=1, act=1),
+    dict(N=2, H=16, W=19, Ci=128, Co=128, K=3, stride=1, pad=2, dil=2, act=1),
+    dict(N=3, H=9, W=11, Ci=96, Co=5, K=1, stride=1, pad=0, dil=1, act=0),
+    dict(N=1, H=14, W=14, Ci=256, Co=64, K=1, stride=1, pad=0, dil=1, act=1, residual=True),
+    dict(N=1, H=12, W=13, Ci=32, Co=40, K=3, stride=1, pad=1, dil=1, act=2),
+    dict(N=1, H=10, W=10, Ci=64, Co=30, K=3, stride=1, pad=1, dil=1, act=0, ldy=64),
+    dict(N=1, H=23, W=29, Ci=64, Co=64, K=7, stride=2, pad=3, dil=1, act=1),
+], ids=lambda d: f"{d['Ci']}to{d['Co']}k{d['K']}s{d['stride']}d{d['dil']}a{d['act']}")
+def test_conv_h16_vs_float64_of_rounded_operands(shape):
+    _case(**shape)
+
+
+def test_conv_h16_rejects_bad_arguments():
+    import bev_native as nat
+    x = torch.zeros(1, 4, 4, 48, device=DEV)
+    with nat._half_mode(True):
+        assert nat.pack_conv_weight(torch.zeros(8, 48, 3, 3, device=DEV)).dtype == torch.float32  # 48 % 32 != 0
+        packed = nat.pack_conv_weight(torch.zeros(8, 64, 3, 3, device=DEV))
+    with pytest.raises(nat.HipError):  # Ci of x is not the panel's and not a multiple of 32
+        nat.conv2d_nhwc_h16(x, packed, torch.zeros(8, device=DEV), 8, 3, 3, 1, 1)
+    with pytest.raises(nat.HipError):
+        nat.conv2d_nhwc_h16(x, packed.float(), torch.zeros(8, device=DEV), 8, 3, 3, 1, 1)
+
+
+def test_amp_functions_take_half_convs_only_under_autocast():
+    """The native Functions pick the fp16 panel exactly when called under autocast(float16) with
+    AMP_HALF_CONVS on."""
+    import bev_native as nat
+    from models.encoders import trunk_grad
+    conv = torch.nn.Conv2d(64, 64, 3, padding=1, bias=True).to(DEV)
+    x = torch.randn(1, 8, 8, 64, device=DEV, requires_grad=True)
+    seen = []
+    orig = nat.conv2d_nhwc_h16
+
+    def spy(*a, **k):
+        seen.append(True)
+        return orig(*a, **k)
+
+    nat.conv2d_nhwc_h16 = spy
+    try:
+        trunk_grad.conv_act(conv, x, True).sum().backward()
+        assert not seen
+        with torch.autocast("cuda", dtype=torch.float16):
+            y = trunk_grad.conv_act(conv, x, True)
+        assert y.dtype == torch.float32 and len(seen) == 1
+        y.sum().backward()
+        assert len(seen) == 2  # the dgrad conv too
+        old, nat.AMP_HALF_CONVS = nat.AMP_HALF_CONVS, False
+        try:
+            with torch.autocast("cuda", dtype=torch.float16):
+                trunk_grad.conv_act(conv, x, True)
+        finally:
+            nat.AMP_HALF_CONVS = old
+        assert len(seen) == 2
+    finally:
+        nat.conv2d_nhwc_h16 = orig

@@ -492,11 +492,13 @@ def _bevnet_ddp_worker(rank, world, port, q):
         ddp = bev_dist.ddp_wrap(model, torch.device(DEV))
         # parameters: BN running statistics are updated from each rank's own frame and broadcast from rank 0
         # at the next forward (ddp_wrap: broadcast_buffers=True), so after the last step they may differ
-        init = {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters()}
+        skip = set(bev_dist.unexecuted_parameters(model))  # trunk stages past OUT_INDEX: never run, never synced
+        init = {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters() if k not in skip}
         opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=1e-3)
         model.train()
         losses = [bev_dist.train_step(ddp, batch, targets, opt)["total_loss"] for _ in range(2)]
-        q.put((rank, init, {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters()}, losses))
+        q.put((rank, init, {k: v.detach().cpu().numpy().copy() for k, v in model.named_parameters() if k not in skip},
+               losses))
     finally:
         dist.destroy_process_group()
 

@@ -2,17 +2,19 @@
 
 The reference trains BEVNet with RUNTIME.USE_AMP: true (configs/wildtrack.yaml:45): forward and loss under
 `autocast(dtype=torch.float16)`, then `scaler.scale(loss).backward()`, `scaler.step(optimizer)`,
-`scaler.update()` (train.py:168-173,238-247).  The drop-in's native autograd Functions run their forward with
-autocast disabled and fp32 inputs (bev_native.amp_fwd: torch's custom-extension contract), so under AMP every
-kernel still computes in fp32 -- wider than the reference's fp16 convs -- and the gradients that reach the
-optimizer are the fp32 gradients times the loss scale, which scaler.unscale_ removes exactly (a power of two).
+`scaler.update()` (train.py:168-173,238-247).  The drop-in's native autograd Functions follow torch's
+custom-extension contract (bev_native.amp_fwd / amp_bwd): fp32 inputs, autocast off inside -- and what autocast
+puts on fp16 in the reference, the convolutions, runs on fp16 operands with fp32 accumulation
+(bev_conv2d_h16_f32; bev_native.AMP_HALF_CONVS, default on) forward and dgrad, while BN / GroupNorm / warp / loss
+/ wgrad stay fp32.  With AMP_HALF_CONVS off every kernel computes in fp32 under autocast.
 
-Tolerances: the fixture pin (bevnet_small.npz, the reference BEVNet's own gradients) uses test_bevnet_gpu's
-fp32 tolerances unchanged (rtol 1e-3, atol 1e-3 x max|ref|); the ResNet-50 BEVNet step is compared with a
-float64 torch restatement of the reference graph (oracle/bevnet_ref.py; its loss evaluated in fp32 like the
-native run's): outputs and losses rel 1e-4, every
-parameter gradient max|d| <= 1e-3 x max(its own max|ref|, 1e-4 x the largest gradient), BN running statistics
-rel 1e-4.
+Tolerances: the fixture pin (bevnet_small.npz, the reference BEVNet's own fp32 gradients) uses test_bevnet_gpu's
+fp32 tolerances unchanged with fp32 kernels (rtol 1e-3, atol 1e-3 x max|ref|) and 1e-2 with fp16 convs.  The
+ResNet-50 BEVNet step is compared with a torch restatement of the reference graph (oracle/bevnet_ref.py)
+evaluated in float64 and in float32 on the CPU -- under AMP with the fp16 rounding of every conv operand the
+native path rounds emulated (_H16Conv) -- and every output, loss and parameter gradient of the native run must be
+within 4x the float32 reference's own distance from the float64 value (floor 1e-5 of the scale): as accurate as
+the reference's arithmetic; BN running statistics rel 1e-4.
 """
 import copy
 import json
@@ -42,11 +44,15 @@ def _autocast():
 
 
 @pytest.mark.timeout(240)
-def test_bevnet_amp_step_matches_reference_fp32_gradients():
+@pytest.mark.parametrize("half", [False, True], ids=["fp32-kernels", "fp16-convs"])
+def test_bevnet_amp_step_matches_reference_fp32_gradients(half, monkeypatch):
     """train.py:238-247 on the pinned reference BEVNet (bevnet_small.npz): the AMP branch's losses and its
-    unscaled gradients equal the reference's own fp32 values within the fp32 tolerances; scaler.step then
-    takes the step (no inf / NaN found) and every parameter stays finite."""
+    unscaled gradients equal the reference's own fp32 values within the fp32 tolerances (fp16-operand convs:
+    1e-2); scaler.step then takes the step (no inf / NaN found) and every parameter stays finite."""
+    import bev_native as nat
     from test_bevnet_gpu import PATH, build, close, targets_of
+    monkeypatch.setattr(nat, "AMP_HALF_CONVS", half)
+    tol = 1e-2 if half else 1e-3
     d = np.load(PATH)
     net, batch, cfg = build(d)
     net.train()
@@ -59,7 +65,7 @@ def test_bevnet_amp_step_matches_reference_fp32_gradients():
         loss = losses["total_loss"] / 1.0
     for k in ("heatmap_loss", "offset_loss", "size_loss", "total_loss"):
         assert losses[k].dtype == torch.float32
-        close(float(losses[k].detach()), float(d["loss_" + k]), 1e-4, 0.0, k)
+        close(float(losses[k].detach()), float(d["loss_" + k]), tol / 10, 0.0, k)
     scale0 = scaler.get_scale()
     scaler.scale(loss).backward()
     scaler.unscale_(opt)
@@ -69,7 +75,7 @@ def test_bevnet_amp_step_matches_reference_fp32_gradients():
         if key.startswith("g_"):
             g = params[key[2:]].grad
             assert g is not None and g.dtype == torch.float32, key
-            close(g.cpu().numpy(), d[key], 1e-3, 1e-3, "amp grad " + key[2:])
+            close(g.cpu().numpy(), d[key], tol, tol, "amp grad " + key[2:])
             checked += 1
     assert checked >= 15
     before = {k: p.detach().clone() for k, p in params.items()}
@@ -111,8 +117,50 @@ def _randomize_bn(model, seed):
         w.copy_(torch.randn(w.shape, generator=g) * 0.05)
 
 
-def _reference_copy(model, cfg):
-    """A CPU float64 BEVNet with the lazy modules built at the same shapes and `model`'s state loaded."""
+def _r16(t):
+    return t.to(torch.float16).to(t.dtype)
+
+
+class _H16Conv(torch.autograd.Function):
+    """F.conv2d with the native AMP path's fp16 roundings (bev_native.pack_conv_weight / conv2d_nhwc under
+    autocast): forward operands rounded to fp16 when Ci % 32 == 0, dgrad operands (the scaled output gradient
+    and the weight) when Co % 32 == 0, wgrad unrounded; everything else in the tensor's own dtype."""
+    scale = 1.0  # the GradScaler scale the native backward ran at (fp16 rounding of dy * scale)
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, dilation, groups):
+        h = groups == 1 and w.shape[1] % 32 == 0
+        ctx.save_for_backward(x, w)
+        ctx.meta = (stride, padding, dilation, groups, b is not None)
+        return _ORIG_CONV(_r16(x) if h else x, _r16(w) if h else w, b, stride, padding, dilation, groups)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, padding, dilation, groups, has_b = ctx.meta
+        h = groups == 1 and w.shape[0] % 32 == 0
+        s = _H16Conv.scale
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv2d_input(x.shape, _r16(w) if h else w, _r16(dy * s) / s if h else dy, stride,
+                                            padding, dilation, groups)
+        if ctx.needs_input_grad[1]:
+            dw = torch.nn.grad.conv2d_weight(x, w.shape, dy, stride, padding, dilation, groups)
+        if has_b and ctx.needs_input_grad[2]:
+            db = dy.sum((0, 2, 3))
+        return dx, dw, db, None, None, None, None
+
+
+_ORIG_CONV = torch.nn.functional.conv2d
+
+
+def _h16_conv2d(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+    return _H16Conv.apply(x, w, b, stride, padding, dilation, groups)
+
+
+def _reference_copy(model, cfg, dtype=torch.float64):
+    """A CPU BEVNet (float64, or float32 for the reference's own arithmetic) with the lazy modules built at the
+    same shapes and `model`'s state loaded."""
     from models.encoders.resnet import FoldedConv  # noqa: F401  (module import only)
     from models.heads.detector import BEVDetector
     from models.model_wrapper import BEVNet
@@ -124,7 +172,7 @@ def _reference_copy(model, cfg):
     ref.detector = BEVDetector(in_channels=model.detector.in_channels, bev_bounds=model.bounds,
                                bev_size=(model.bev_h, model.bev_w), default_box_wh=model.default_box_wh)
     ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()}, strict=True)
-    return ref.double()
+    return ref.to(dtype)
 
 
 @pytest.mark.timeout(300)
@@ -149,8 +197,10 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
     bev_dist.materialize_lazy(model, batch)
     _randomize_bn(model, 7)
     ref = _reference_copy(model, cfg)
+    ref32 = _reference_copy(model, cfg, torch.float32)
     model.train()
     ref.train()
+    ref32.train()
 
     trunk_masks, head_masks = [], []
     bn_apply, gn_apply = nat.batchnorm_apply, nat.groupnorm_apply
@@ -187,36 +237,55 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
         scaler.unscale_(opt)
     got = {k: p.grad.detach().double().cpu() for k, p in model.named_parameters() if p.grad is not None}
     stats = {k: b.detach().double().cpu() for k, b in model.named_buffers() if "running" in k}
+    assert len(trunk_masks) > 20 and len(head_masks) == 3
 
-    n_trunk = len(trunk_masks)
-    it = iter(trunk_masks)
-    out = bevnet_ref.bevnet_train_forward(ref, imgs.double(), K, Rt, trunk_act=lambda t: t * next(it),
-                                          head_masks=head_masks)
-    assert n_trunk > 20 and len(head_masks) == 3
+    # the reference graph in float64 (the exact value) and in float32 (the reference's own arithmetic: torch CPU
+    # fp32), with the native ReLU decisions
+    def run(net, dt):
+        it = iter(trunk_masks)
+        out = bevnet_ref.bevnet_train_forward(net, imgs.to(dt), K, Rt, trunk_act=lambda t: t * next(it).to(dt),
+                                              head_masks=[m.to(dt) for m in head_masks])
+        ls = net.loss(out, [{"boxes_world": b.to(dt)} for b in boxes], cfg["LOSS"])
+        ls["total_loss"].backward()
+        return out, ls
+
+    half = amp and nat.AMP_HALF_CONVS
+    if half:
+        _H16Conv.scale = float(scaler.get_scale())
+        torch.nn.functional.conv2d = _h16_conv2d
+    try:
+        out64, ls64 = run(ref, torch.float64)
+        out32, ls32 = run(ref32, torch.float32)
+    finally:
+        torch.nn.functional.conv2d = _ORIG_CONV
+    worst = []
+
+    # The bar: the native fp32 result is as close to the float64 value as the reference's own fp32 evaluation is
+    # (error <= 4 x the fp32 reference's error, floor 1e-5 of the scale) -- fp32 through a 50-layer trunk with
+    # batch-statistics BN and a focal loss summed over every BEV cell is only that accurate.
+    def bounded(native, r64, r32, what):
+        scale = max(float(r64.abs().max()), 1e-30)
+        e_nat = float((native.double() - r64.double()).abs().max()) / scale
+        e_32 = float((r32.double() - r64.double()).abs().max()) / scale
+        worst.append((e_nat / (e_32 + 1e-12), what, e_nat, e_32))
+        assert e_nat <= 4.0 * e_32 + 1e-5, (what, e_nat, e_32)
+        return e_nat, e_32
+
     for k in ("heatmap_logits", "offset_raw", "size_raw", "bev_feat"):
-        a, r = preds[k].detach().double().cpu(), out[k].detach()
-        err = (a - r).abs().max().item() / max(r.abs().max().item(), 1e-12)
-        assert err < 1e-4, (k, err)
-    # the loss is torch code in both (BEVNet.loss); evaluate it in fp32 on the reference graph's outputs, as the
-    # native run does (the focal loss's log(1 - p) near p = 1 is only as precise as fp32 p), so that the
-    # comparison measures the kernels, not fp32-vs-float64 loss arithmetic
-    out32 = {k: v.float() for k, v in out.items()}
-    ref_losses = ref.loss(out32, [{"boxes_world": b} for b in boxes], cfg["LOSS"])
+        bounded(preds[k].detach().cpu(), out64[k].detach(), out32[k].detach(), k)
     for k in ("heatmap_loss", "offset_loss", "size_loss", "total_loss"):
-        a, r = float(losses[k].detach()), float(ref_losses[k].detach())
-        assert abs(a - r) <= 1e-4 * abs(r) + 1e-7, (k, a, r)
-    ref_losses["total_loss"].backward()
-    gmax = max(p.grad.abs().max().item() for p in ref.parameters() if p.grad is not None)
-    errs = {}
+        bounded(losses[k].detach().cpu().reshape(1), ls64[k].detach().reshape(1), ls32[k].detach().reshape(1), k)
+    p32 = dict(ref32.named_parameters())
+    n = 0
     for k, p in ref.named_parameters():
         if p.grad is None:
             assert k not in got, k
             continue
         assert k in got, f"no native gradient for {k}"
-        errs[k] = (got[k] - p.grad).abs().max().item() / max(p.grad.abs().max().item(), 1e-4 * gmax)
-    trunk = [k for k in errs if k.startswith("encoder.backbone.")]
-    assert len(trunk) > 40 and any(k.startswith("detector.") for k in errs) and "proj.weight" in errs
-    assert max(errs.values()) < 1e-3, sorted(errs.items(), key=lambda t: -t[1])[:6]
+        bounded(got[k], p.grad, p32[k].grad, "grad " + k)
+        n += 1
+    assert n > 60
+    print("worst native / fp32-reference error ratios:", sorted(worst, reverse=True)[:3])
     for k, b in ref.named_buffers():
         if k in stats:
             err = (stats[k] - b).abs().max().item() / max(b.abs().max().item(), 1e-12)

@@ -1,11 +1,12 @@
 """Training-step timing (BASELINE config 3 shape, one GPU): ResNet-50 trunk + proj -> IPM warp -> head.
 
-    python tools/train_step_bench.py [--steps 5] [--bevnet]
+    python tools/train_step_bench.py [--steps 5] [--bevnet] [--amp] [--fp32-kernels]
 
 Default: the hot path alone -- CNNEncoder (trunk trainable, native forward + backward) -> fused warp
 + mean (native forward + backward) -> sum(out * r) -> Adam step.  --bevnet: the full BEVNet (encoder,
 per-view warp, concat, BEV proj, CenterNet head, focal/L1 loss) with the reference's training step
-(train.py:249-255, fp32).  7 cameras x 3 x 1080 x 1920 synthetic images, Appendix-B rig, B = 1.
+(train.py:249-255, fp32; --amp: the RUNTIME.USE_AMP branch, autocast(float16) + GradScaler, train.py:238-247,
+with fp16-operand convs unless --fp32-kernels).  7 cameras x 3 x 1080 x 1920 synthetic images, Appendix-B rig, B = 1.
 Prints one JSON line: ms per training step and frames/s.
 """
 import argparse
@@ -28,7 +29,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--bevnet", action="store_true")
     ap.add_argument("--backbone", default="resnet50")
+    ap.add_argument("--amp", action="store_true")
+    ap.add_argument("--fp32-kernels", action="store_true")
     a = ap.parse_args()
+    import bev_native
+    bev_native.AMP_HALF_CONVS = not a.fp32_kernels
+    scaler = torch.amp.GradScaler("cuda") if a.amp else None
     dev = torch.device("cuda:0")
     V, H, W = 7, 1080, 1920
     K, Rt = bev_rig.rig(V, H, W, 1)
@@ -49,9 +55,15 @@ def main():
 
         def step():
             opt.zero_grad(set_to_none=True)
-            loss = model.loss(model(batch), targets, {})["total_loss"]
-            loss.backward()
-            opt.step()
+            with torch.autocast("cuda", dtype=torch.float16, enabled=scaler is not None):
+                loss = model.loss(model(batch), targets, {})["total_loss"]
+            if scaler is None:
+                loss.backward()
+                opt.step()
+            else:
+                scaler.scale(loss).backward()
+                scaler.step(opt)
+                scaler.update()
             return loss
     else:
         from models.encoders.cnn_encoder import CNNEncoder
@@ -66,10 +78,16 @@ def main():
 
         def step():
             opt.zero_grad(set_to_none=True)
-            out = geom.forward_fused(enc(images), Kd, Rtd, (H, W), "mean")
-            loss = (out * r).sum()
-            loss.backward()
-            opt.step()
+            with torch.autocast("cuda", dtype=torch.float16, enabled=scaler is not None):
+                out = geom.forward_fused(enc(images), Kd, Rtd, (H, W), "mean")
+                loss = (out.float() * r).sum()
+            if scaler is None:
+                loss.backward()
+                opt.step()
+            else:
+                scaler.scale(loss).backward()
+                scaler.step(opt)
+                scaler.update()
             return loss
     for _ in range(a.warmup):
         step()
@@ -80,6 +98,7 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     print(json.dumps({"what": "bevnet train step" if a.bevnet else "hot-path train step", "backbone": a.backbone,
+                      "amp": a.amp, "half_convs": a.amp and not a.fp32_kernels,
                       "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
                       "loss": float(loss)}), flush=True)
 

@@ -10,8 +10,10 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import functools
 import os
 import subprocess
+import threading
 
 import torch
 
@@ -86,6 +88,9 @@ SIGNATURES = {
     "bev_groupnorm_apply_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _i, _vp, _vp]),
     "bev_image_normalize_u8_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_groupnorm_bwd_f32": (_i, [_vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "bev_conv_packed_size_h16": (_i64, [_i, _i, _i, _i]),
+    "bev_conv_pack_weights_h16": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+    "bev_conv2d_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
 }
 
 
@@ -187,11 +192,51 @@ class HipError(RuntimeError):
 
 
 # Mixed precision (the reference trains under torch.autocast(float16) + GradScaler, train.py:168-173,238-247):
-# every native autograd Function runs its forward with autocast disabled and its floating inputs cast to
-# fp32 (the kernels' arithmetic type, wider than the reference's fp16 convs), and its backward under the
-# forward's autocast state -- torch's custom-extension contract (torch.amp.custom_fwd / custom_bwd).
-amp_fwd = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
-amp_bwd = torch.amp.custom_bwd(device_type="cuda")
+# every native autograd Function runs its forward with autocast disabled and its floating inputs cast to fp32,
+# and its backward in the forward's precision mode -- torch's custom-extension contract (torch.amp.custom_fwd /
+# custom_bwd).  What autocast(float16) puts on fp16 in the reference -- its convolutions -- runs here on fp16
+# operands with fp32 accumulation too (bev_conv2d_h16_f32, the fp16 matrix cores) when AMP_HALF_CONVS is on
+# (default); BatchNorm / GroupNorm / the warp / the loss stay fp32 as under autocast.  AMP_HALF_CONVS = False
+# keeps every kernel in fp32 under autocast (wider than the reference).
+AMP_HALF_CONVS = True
+_AMP_LOCAL = threading.local()
+
+
+def half_convs() -> bool:
+    """True inside the forward / backward of a native Function called under autocast(float16)."""
+    return getattr(_AMP_LOCAL, "half", False)
+
+
+@contextlib.contextmanager
+def _half_mode(on: bool):
+    prev = half_convs()
+    _AMP_LOCAL.half = on
+    try:
+        yield
+    finally:
+        _AMP_LOCAL.half = prev
+
+
+def amp_fwd(fn):
+    @functools.wraps(fn)
+    def forward(ctx, *args, **kwargs):
+        on = (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16
+              and AMP_HALF_CONVS)
+        ctx._bev_half = on
+        with torch.autocast("cuda", enabled=False), _half_mode(on):
+            args = [a.float() if isinstance(a, torch.Tensor) and a.is_floating_point() and a.dtype != torch.float32
+                    else a for a in args]
+            return fn(ctx, *args, **kwargs)
+    return forward
+
+
+def amp_bwd(fn):
+    @functools.wraps(fn)
+    def backward(ctx, *grads):
+        with torch.autocast("cuda", enabled=False), _half_mode(getattr(ctx, "_bev_half", False)):
+            return fn(ctx, *[g.float() if isinstance(g, torch.Tensor) and g.is_floating_point() else g
+                             for g in grads])
+    return backward
 
 
 def _check(rc: int, name: str):
@@ -327,10 +372,18 @@ def view_fuse(x: torch.Tensor, mode: str) -> torch.Tensor:
 # backbone
 # ---------------------------------------------------------------------------
 def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
-    """OIHW fp32 (device) -> packed MFMA panel."""
+    """OIHW fp32 (device) -> packed MFMA panel: fp32, or fp16 (torch.float16 storage) inside a native Function
+    run under autocast(float16) when the conv takes the fp16 kernel (Ci % 32 == 0) -- the conv calls below
+    dispatch on the panel's dtype."""
     w = w.detach().contiguous()
     _require_gpu(w)
     Co, Ci, KH, KW = w.shape
+    if half_convs() and Ci % 32 == 0:
+        n = lib().bev_conv_packed_size_h16(Co, Ci, KH, KW)
+        out = torch.empty(n, device=w.device, dtype=torch.float16)
+        _check(lib().bev_conv_pack_weights_h16(_ptr(w), Co, Ci, KH, KW, _ptr(out), _stream(w)),
+               "bev_conv_pack_weights_h16")
+        return out
     n = lib().bev_conv_packed_size(Co, Ci, KH, KW)
     out = torch.empty(n, device=w.device, dtype=torch.float32)
     _check(lib().bev_conv_pack_weights_f32(_ptr(w), Co, Ci, KH, KW, _ptr(out), _stream(w)), "bev_conv_pack_weights_f32")
@@ -343,6 +396,12 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
     """x: [N,H,W,Ci] NHWC (or [N,Ci,H,W] with in_nchw) -> y [N,Ho,Wo,Co] NHWC.
     ascale [N, Ci]: per-image input-channel multiplier applied in the operand load (SE excitation)."""
     x = x.contiguous()
+    if packed.dtype == torch.float16:  # autocast(float16): the fp16 matrix-core kernel
+        if ascale is not None:
+            raise HipError("the fp16 conv takes no operand channel scale (the SE gate is applied apart in training)")
+        if in_nchw:
+            x = nchw_to_nhwc(x)
+        return conv2d_nhwc_h16(x, packed, bias, Co, KH, KW, stride, pad, 1, int(relu), residual=residual, out=out)
     _require_gpu(x, packed, bias, residual)
     if in_nchw:
         N, Ci, H, W = x.shape
@@ -368,6 +427,30 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
 
 
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2  # `relu` argument of conv2d_nhwc / dwconv2d_nhwc
+
+
+def conv2d_nhwc_h16(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
+                    dilation: int = 1, act: int = 0, residual: torch.Tensor = None, out: torch.Tensor = None):
+    """fp16-operand / fp32-accumulate conv (autocast(float16) arithmetic): x [N,H,W,Ci] fp32 NHWC, packed = the
+    fp16 panel of pack_conv_weight under half_convs() -> y [N,Ho,Wo,Co] fp32 (or the first Co channels of a wider
+    NHWC `out`)."""
+    x = x.contiguous()
+    _require_gpu(x, bias, residual)
+    if not packed.is_cuda or packed.dtype != torch.float16:
+        raise HipError("conv2d_nhwc_h16 needs the fp16 weight panel on the device")
+    N, H, W, Ci = x.shape
+    Ho, Wo = (H + 2 * pad - dilation * (KH - 1) - 1) // stride + 1, (W + 2 * pad - dilation * (KW - 1) - 1) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    assert out.shape[:3] == (N, Ho, Wo) and out.shape[3] >= Co and out.is_contiguous() and out.dtype == torch.float32
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == (N, Ho, Wo, Co) and out.shape[3] == Co
+    with _span("conv", x):
+        rc = lib().bev_conv2d_h16_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co, KH, KW,
+                                      stride, pad, dilation, int(act), _ptr(out), out.shape[3], Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_h16_f32")
+    return out
 
 
 def dwconv2d_nhwc(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, K: int, stride: int, pad: int, act: int,
@@ -608,6 +691,10 @@ def conv2d_nhwc_ex(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, K: int,
     applied to the operand (in_scale / in_shift [N, Ci]).  `out` may be a wider NHWC buffer [N,Ho,Wo,>=Co]
     whose first Co channels receive y."""
     x = x.contiguous()
+    if packed.dtype == torch.float16:  # autocast(float16): the fp16 matrix-core kernel
+        if in_scale is not None or in_shift is not None:
+            raise HipError("the fp16 conv takes no operand affine (GroupNorm is materialised in training)")
+        return conv2d_nhwc_h16(x, packed, bias, Co, K, K, 1, pad, dilation, int(relu), out=out)
     _require_gpu(x, packed, bias, in_scale, in_shift)
     N, H, W, Ci = x.shape
     Ho, Wo = H + 2 * pad - dilation * (K - 1), W + 2 * pad - dilation * (K - 1)

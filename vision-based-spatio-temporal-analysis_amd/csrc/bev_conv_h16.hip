@@ -1,0 +1,240 @@
+// bev_conv_h16.hip -- the convolutions of a training step under torch.autocast(float16) (BASELINE config 3).
+//
+// The reference trains with RUNTIME.USE_AMP: true (configs/wildtrack.yaml:45): inside
+// autocast(dtype=float16) (train.py:238-247) every nn.Conv2d of the timm trunk and of BEVDetector runs on fp16
+// operands (autocast rounds the fp32 activation and the fp32 weight to fp16, round-to-nearest-even) with fp32
+// accumulation, forward and backward.  This kernel is that arithmetic on the MI355X matrix cores:
+//     y[m][n] = act( sum_k f16(A[m][k]) * f16(W[k][n]) + bias[n] (+ res[m][n]) )     (fp32 sum)
+// on v_mfma_f32_32x32x16_f16 (16x the fp32 MFMA rate; the products of two fp16 values are exact in fp32, so the
+// result equals an fp32 convolution of the fp16-rounded operands up to the order of the fp32 additions).
+// Activations stay fp32 NHWC in HBM (the BatchNorm / GroupNorm / loss kernels around the convs run in fp32, as
+// under autocast); A is converted to fp16 as it is staged into LDS, the weights are packed to fp16 once.
+//
+// Implicit GEMM, m = (image, oy, ox), n = output channel, k = (ky, kx, ci) with Ci % 32 == 0 (one tap and 32
+// consecutive channels per K step).  256 threads = 2 x 2 waves of 64 x 64 outputs (2 x 2 MFMA tiles of 32 x 32),
+// block tile 128 x 128, K step 32 (two 16-deep MFMA k-slices), operands [row][k] in LDS with 80-B rows (5 odd
+// 16-B slots: conflict-free ds_read_b128 fragments), double-buffered: the next step's global loads are issued
+// before this step's MFMAs.  Fragment map (cdna_hip_programming.md §3): lane l holds A[row l & 31][k 8 (l >> 5)
+// + j] and B[k 8 (l >> 5) + j][col l & 31], j = 0..7.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int HBM = 128, HBN = 128, HBK = 32;
+constexpr int HROW = 40;  // halves per LDS row: 32 + 8 pad = 80 B = 5 slots (odd: 16 rows -> 16 distinct slots)
+
+__device__ __attribute__((aligned(16))) float g_hzero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
+
+__host__ __device__ inline int64_t kpad_h(int K) { return (K + HBK - 1) / HBK * HBK; }
+__host__ __device__ inline int64_t copad_h(int Co) { return (Co + HBN - 1) / HBN * HBN; }
+
+// OIHW fp32 -> [Co_pad][K_pad] fp16 (RNE, like autocast's weight cast), k = (ky*KW + kx)*Ci + ci
+__global__ void k_pack_h16(const float *__restrict__ w, int Co, int Ci, int KH, int KW, int64_t Kp, int64_t Cop,
+                           _Float16 *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= Kp * Cop) return;
+    const int n = (int)(t / Kp);
+    const int k = (int)(t % Kp);
+    const int K = Ci * KH * KW;
+    float v = 0.0f;
+    if (n < Co && k < K) {
+        const int ci = k % Ci, r = k / Ci, kx = r % KW, ky = r / KW;
+        v = w[(((int64_t)n * Ci + ci) * KH + ky) * KW + kx];
+    }
+    out[t] = (_Float16)v;
+}
+
+struct ConvH {
+    const float *__restrict__ x;
+    const _Float16 *__restrict__ wp;
+    const float *__restrict__ bias;
+    const float *__restrict__ res;
+    float *__restrict__ y;
+    int N, H, W, Ci, Co, KH, KW, stride, pad, dil, Ho, Wo, act, ldy, Kp;
+    int64_t M;
+};
+
+__device__ __forceinline__ float act_h(float t, int act) {
+    if (act == 2) return t / (1.0f + expf(-t));
+    if (act == 1) return t > 0.0f ? t : 0.0f;
+    return t;
+}
+
+__global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2][(HBM + HBN) * HROW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntn = (a.Co + HBN - 1) / HBN;
+    const int64_t ntm = (a.M + HBM - 1) / HBM;
+    unsigned bid = blockIdx.x;
+    {  // XCD-aware order: consecutive blocks (the N tiles of one M block) on one XCD
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int64_t mt = bid / (unsigned)ntn;
+    const int nt = (int)(bid % (unsigned)ntn);
+    if (mt >= ntm) return;
+    const int64_t m0 = mt * HBM;
+    const int n0 = nt * HBN;
+
+    // A staging: rows (tid >> 3) + 32 q, channel quad tid & 7 (4 channels -> 4 halves)
+    const int aq = tid & 7;
+    int64_t pix[4];
+    int iy0[4], ix0[4];
+    bool rok[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t m = m0 + (tid >> 3) + 32 * q;
+        rok[q] = m < a.M;
+        const int64_t mm = rok[q] ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int n = (int)(t / a.Ho);
+        pix[q] = (int64_t)n * a.H * a.W * a.Ci;
+        iy0[q] = oy * a.stride - a.pad;
+        ix0[q] = ox * a.stride - a.pad;
+    }
+    // B staging: weight row n0 + (tid >> 1), halves 16 (tid & 1) .. + 15 of the K step
+    const _Float16 *wrow = a.wp + (int64_t)(n0 + (tid >> 1)) * a.Kp + 16 * (tid & 1);
+
+    f32x4 ra[4];
+    uint4 rb[2];
+    int ky = 0, kx = 0, ci0 = 0;  // tap and channel offset of the K step being loaded
+    int64_t kb = 0;
+    auto gload = [&]() {
+        const int dy = ky * a.dil, dx = kx * a.dil;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int iy = iy0[q] + dy, ix = ix0[q] + dx;
+            const bool in = rok[q] && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            const float *src = in ? a.x + pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + 4 * aq : g_hzero4;
+            ra[q] = *(const f32x4 *)src;
+        }
+        rb[0] = *(const uint4 *)(wrow + kb);
+        rb[1] = *(const uint4 *)(wrow + kb + 8);
+        kb += HBK;
+        ci0 += HBK;
+        if (ci0 == a.Ci) {
+            ci0 = 0;
+            if (++kx == a.KW) {
+                kx = 0;
+                ++ky;
+            }
+        }
+    };
+    auto swrite = [&](int buf) {
+        _Float16 *As = lds[buf], *Bs = As + HBM * HROW;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const h16x4 h = {(_Float16)ra[q][0], (_Float16)ra[q][1], (_Float16)ra[q][2], (_Float16)ra[q][3]};
+            *(h16x4 *)(As + ((tid >> 3) + 32 * q) * HROW + 4 * aq) = h;
+        }
+        *(uint4 *)(Bs + (tid >> 1) * HROW + 16 * (tid & 1)) = rb[0];
+        *(uint4 *)(Bs + (tid >> 1) * HROW + 16 * (tid & 1) + 8) = rb[1];
+    };
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    const int nsteps = a.Kp / HBK;
+    gload();
+    swrite(0);
+    __syncthreads();
+    const int r32 = lane & 31, h = lane >> 5;
+    for (int st = 0; st < nsteps; ++st) {
+        const bool more = st + 1 < nsteps;
+        if (more) gload();
+        const _Float16 *As = lds[st & 1], *Bs = As + HBM * HROW;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            h16x8 fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i] = *(const h16x8 *)(As + (wm * 64 + i * 32 + r32) * HROW + kk * 16 + 8 * h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[j] = *(const h16x8 *)(Bs + (wn * 64 + j * 32 + r32) * HROW + kk * 16 + 8 * h);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) swrite((st + 1) & 1);  // the other buffer: its last readers passed the previous barrier
+        __syncthreads();
+    }
+    // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + r32;
+            if (col >= a.Co) continue;
+            const float bv = a.bias ? a.bias[col] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= a.M) continue;
+                float v = acc[i][j][r] + bv;
+                if (a.res) v += a.res[row * a.Co + col];
+                a.y[row * a.ldy + col] = act_h(v, a.act);
+            }
+        }
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t bev_conv_packed_size_h16(int Co, int Ci, int KH, int KW) {
+    if (Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;
+    return copad_h(Co) * kpad_h(Ci * KH * KW);
+}
+
+int bev_conv_pack_weights_h16(const float *w, int Co, int Ci, int KH, int KW, uint16_t *packed, void *stream) {
+    if (!w || !packed || Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;
+    const int64_t Kp = kpad_h(Ci * KH * KW), Cop = copad_h(Co), n = Kp * Cop;
+    hipLaunchKernelGGL(k_pack_h16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, Co, Ci, KH,
+                       KW, Kp, Cop, (_Float16 *)packed);
+    return (int)hipGetLastError();
+}
+
+int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                       const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
+                       float *y, int ldy, int Ho, int Wo, void *stream) {
+    if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
+        stride <= 0 || pad < 0 || dilation <= 0 || act < 0 || act > 2 || ldy < Co)
+        return BEV_ERR_ARGS;
+    if (Ci % HBK != 0) return BEV_ERR_ARGS;  // one tap and 32 channels per K step
+    if (Ho != (H + 2 * pad - dilation * (KH - 1) - 1) / stride + 1 ||
+        Wo != (W + 2 * pad - dilation * (KW - 1) - 1) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
+    if (residual && ldy != Co) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvH a;
+    a.x = x;
+    a.wp = (const _Float16 *)packed;
+    a.bias = bias;
+    a.res = residual;
+    a.y = y;
+    a.N = N, a.H = H, a.W = W, a.Ci = Ci, a.Co = Co, a.KH = KH, a.KW = KW, a.stride = stride, a.pad = pad;
+    a.dil = dilation, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = ldy;
+    a.Kp = (int)kpad_h(Ci * KH * KW);
+    a.M = (int64_t)N * Ho * Wo;
+    const int64_t blocks = ((a.M + HBM - 1) / HBM) * ((Co + HBN - 1) / HBN);
+    if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL(k_conv_h16, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -225,7 +225,7 @@ __device__ __forceinline__ void wg_dma16(const float *src, unsigned dst_any) {
 }
 
 template <int WCO, int TM, int TN>
-__global__ __launch_bounds__(256, 2) void k_wgrad_nat(const float *__restrict__ x, const float *__restrict__ dz, int N,
+__global__ __launch_bounds__(256, TN == 4 ? 1 : 2) void k_wgrad_nat(const float *__restrict__ x, const float *__restrict__ dz, int N,
                                                       int H, int W, int Ci, int Ho, int Wo, int Co, int KW, int K,
                                                       int stride, int pad, int dil, int64_t mchunk, int ctiles,
                                                       int ntiles, float *__restrict__ dW) {

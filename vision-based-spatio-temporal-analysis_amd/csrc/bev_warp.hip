@@ -37,6 +37,9 @@
 #ifndef WARP_ABLATE
 #define WARP_ABLATE 0
 #endif
+#ifndef WARP_HSCALAR
+#define WARP_HSCALAR 1  // fused warp: homographies of the tap recipe by scalar loads (1) or from the LDS table (0)
+#endif
 // Fused-warp variants under A/B (results identical): 1 corner boxes by wave 0 only, shared through LDS.
 #ifndef WARP_OPT
 #define WARP_OPT 1
@@ -801,6 +804,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
 
     float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
     bool cache_rd = false;     // this chunk reads the tap records (written by an earlier chunk / frame)
+    int hbase = b0 * V;        // homography row of view 0 of the frame being sampled
     auto taps_of = [&](int v) {
         Taps t;
         if (cache_rd) {
@@ -822,7 +826,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         }
         float h[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) h[q] = htab[v * 9 + q];  // uniform LDS address: broadcast
+        for (int q = 0; q < 9; ++q) {  // wave-uniform address: scalar loads (no LDS cycles on the sampling path)
+#if WARP_HSCALAR
+            h[q] = Hmat[__builtin_amdgcn_readfirstlane((hbase + v) * 9) + q];
+#else
+            h[q] = htab[v * 9 + q];
+#endif
+        }
         float ix, iy;
         cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
         t = taps_from_ixy(ix, iy, grid);
@@ -847,6 +857,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     for (int pass = 0; pass < FPW; ++pass) {
       const int b = b0 + pass;
       if (b >= B) break;
+      hbase = b * V;
       if (pass > 0 && !same) {  // this frame's geometry differs: its own boxes and homographies
           __syncthreads();
           prologue(b, false);
@@ -1159,7 +1170,11 @@ int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
 #define WARP_TILE_H 16  // fused-warp tile: 16 x 16 (default) or 8 x 32 cells (A/B builds)
 #endif
 #ifndef WARP_PAIR
-#define WARP_PAIR 1  // frames per workgroup with the LDS tap records: 0 off, 1 on (pool shrunk to keep 3 WG / CU)
+#define WARP_PAIR 0  // frames per workgroup with the LDS tap records: 0 off (default), 1 on (A/B builds; r03d:
+                     // 176 vs 131 us for the batch-2 bench launch -- half the workgroups, a tail and a smaller pool)
+#endif
+#ifndef WARP_OCC
+#define WARP_OCC 3   // workgroups per CU the default (mean / sum) kernel is compiled and sized for
 #endif
 constexpr int V2_FIXED = 256 + 4 * (FT_NT / 64) * (int)sizeof(int) + V2_MAXV * 9 * (int)sizeof(float) +
                          (2 * V2_MAXV + 4) * (int)sizeof(unsigned);  // zero pixel, red, htab, btab + flag
@@ -1201,8 +1216,10 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
     if (pair && pool >= 16 * 1024 && pool + V2_FIXED + tc_bytes <= 160 * 1024)
         return launch_fuse_v2_occ<3, 2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
                                         pool, tc_bytes);
-    return launch_fuse_v2_occ<3, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                    g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024, 0);
+    return launch_fuse_v2_occ<WARP_OCC, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                           st, g_warp_pool_kb ? g_warp_pool_kb * 1024 :
+                                           ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) < 49 * 1024 ?
+                                           ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) : 49 * 1024, 0);
 }
 
 }  // namespace
