@@ -295,6 +295,13 @@ int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16
                        const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
                        float *y, int ldy, int Ho, int Wo, void *stream);
 
+/* Weight gradient of a convolution under autocast(float16): dW[co][(ky*KW + kx)*Ci + ci] =
+ * sum over output pixels of f16(dz) * f16(x) with fp32 accumulation (the fp16 matrix cores), dW [Co][KH*KW*Ci]
+ * fp32 (zeroed by the call).  x [N,H,W,Ci], dz [N,Ho,Wo,Co] NHWC fp32, Ci % 4 == 0, Co % 4 == 0, 16-B aligned.
+ * Replaces the conv weight gradient autograd computes for the reference's autocast branch (train.py:238-247). */
+int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
+                           int KH, int KW, int stride, int pad, int dilation, float *dW, void *stream);
+
 /* ---------------------------------------------------------------------------
  * CenterNet BEV head (BEVDetector, detector.py:16-62): dilated convs, GroupNorm(32) + ReLU
  * ------------------------------------------------------------------------- */

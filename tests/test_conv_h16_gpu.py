@@ -116,3 +116,36 @@ def test_amp_functions_take_half_convs_only_under_autocast():
         assert len(seen) == 2
     finally:
         nat.conv2d_nhwc_h16 = orig
+
+
+@pytest.mark.parametrize("shape", [
+    dict(N=2, H=20, W=24, Ci=64, Co=128, K=3, stride=1, pad=1, dil=1),
+    dict(N=1, H=33, W=17, Ci=32, Co=200, K=3, stride=2, pad=1, dil=1),
+    dict(N=2, H=16, W=19, Ci=128, Co=36, K=3, stride=1, pad=2, dil=2),
+    dict(N=3, H=9, W=11, Ci=96, Co=8, K=1, stride=1, pad=0, dil=1),
+    dict(N=1, H=40, W=40, Ci=256, Co=64, K=1, stride=1, pad=0, dil=1),
+], ids=lambda d: f"{d['Ci']}to{d['Co']}k{d['K']}s{d['stride']}d{d['dil']}")
+def test_wgrad_h16_vs_float64_of_rounded_operands(shape):
+    """conv_wgrad_ex under half_convs(): fp16 operands, fp32 sums (split over pixels, float atomics) against the
+    float64 weight gradient of the fp16-rounded operands; relative to sum |terms| < 2e-6."""
+    import bev_native as nat
+    N, H, W, Ci, Co, K = shape["N"], shape["H"], shape["W"], shape["Ci"], shape["Co"], shape["K"]
+    st, pad, dil = shape["stride"], shape["pad"], shape["dil"]
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, H, W, Ci, generator=g)
+    Ho = (H + 2 * pad - dil * (K - 1) - 1) // st + 1
+    Wo = (W + 2 * pad - dil * (K - 1) - 1) // st + 1
+    dz = torch.randn(N, Ho, Wo, Co, generator=g) * 1e-3
+    with nat._half_mode(True):
+        dw = nat.conv_wgrad_ex(x.to(DEV), dz.to(DEV), K, pad, dil, stride=st)
+    torch.cuda.synchronize()
+    xh, dh = x.half().double().permute(0, 3, 1, 2), dz.half().double().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xh, (Co, Ci, K, K), dh, st, pad, dil)
+    mag = torch.nn.grad.conv2d_weight(xh.abs(), (Co, Ci, K, K), dh.abs(), st, pad, dil)
+    err = (dw.cpu().double() - ref).abs()
+    assert dw.shape == (Co, Ci, K, K)
+    assert float((err / (mag + 1e-12)).max()) < 2e-6
+    # and it is the fp16 arithmetic: the float64 gradient of the raw operands differs by more
+    raw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (Co, Ci, K, K), dz.double().permute(0, 3, 1, 2),
+                                      st, pad, dil)
+    assert float((raw - ref).abs().max()) > 10 * float(err.max())

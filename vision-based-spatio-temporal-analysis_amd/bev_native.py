@@ -91,6 +91,7 @@ SIGNATURES = {
     "bev_conv_packed_size_h16": (_i64, [_i, _i, _i, _i]),
     "bev_conv_pack_weights_h16": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
+    "bev_conv_wgrad_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
 }
 
 
@@ -194,9 +195,10 @@ class HipError(RuntimeError):
 # Mixed precision (the reference trains under torch.autocast(float16) + GradScaler, train.py:168-173,238-247):
 # every native autograd Function runs its forward with autocast disabled and its floating inputs cast to fp32,
 # and its backward in the forward's precision mode -- torch's custom-extension contract (torch.amp.custom_fwd /
-# custom_bwd).  What autocast(float16) puts on fp16 in the reference -- its convolutions -- runs here on fp16
-# operands with fp32 accumulation too (bev_conv2d_h16_f32, the fp16 matrix cores) when AMP_HALF_CONVS is on
-# (default); BatchNorm / GroupNorm / the warp / the loss stay fp32 as under autocast.  AMP_HALF_CONVS = False
+# custom_bwd).  What autocast(float16) puts on fp16 in the reference -- its convolutions, forward, input gradient
+# and weight gradient -- runs here on fp16 operands with fp32 accumulation too (bev_conv2d_h16_f32 /
+# bev_conv_wgrad_h16_f32, the fp16 matrix cores) when AMP_HALF_CONVS is on (default) and the conv has
+# Ci % 32 == 0; BatchNorm / GroupNorm / the warp / the loss stay fp32 as under autocast.  AMP_HALF_CONVS = False
 # keeps every kernel in fp32 under autocast (wider than the reference).
 AMP_HALF_CONVS = True
 _AMP_LOCAL = threading.local()
@@ -721,6 +723,10 @@ def conv_wgrad_ex(x: torch.Tensor, dz: torch.Tensor, K: int, pad: int, dilation:
     _require_gpu(xp, dzp)
     Cip, Cop = xp.shape[-1], dzp.shape[-1]
     dW = torch.empty(Cop, KH, KW, Cip, device=x.device, dtype=torch.float32)
+    if half_convs() and Ci % 32 == 0:  # autocast(float16): the weight gradient of an fp16 conv on the fp16 MFMA
+        _check(lib().bev_conv_wgrad_h16_f32(_ptr(xp), N, H, W, Cip, _ptr(dzp), Ho, Wo, Cop, KH, KW, stride, pad,
+                                            dilation, _ptr(dW), _stream(x)), "bev_conv_wgrad_h16_f32")
+        return dW[:Co, :, :, :Ci].permute(0, 3, 1, 2).contiguous()
     _check(lib().bev_conv_wgrad_ex_f32(_ptr(xp), N, H, W, Cip, _ptr(dzp), Ho, Wo, Cop, KH, KW, stride, pad, dilation,
                                        _ptr(dW), _stream(x)), "bev_conv_wgrad_ex_f32")
     return dW[:Co, :, :, :Ci].permute(0, 3, 1, 2).contiguous()  # the parameter's OIHW strides (DDP bucket views)

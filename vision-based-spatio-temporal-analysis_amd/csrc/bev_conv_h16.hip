@@ -191,9 +191,161 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
         }
 }
 
+// ---- weight gradient under autocast(float16): dW[co][k] = sum_m f16(dz[m][co]) * f16(im2col(x)[m][k]) ----------
+// The reduction index of v_mfma_f32_32x32x16_f16 is the output pixel m: lane l needs 8 consecutive pixels of one
+// channel (A = dz^T, B = im2col(x)), so both operands are staged TRANSPOSED into LDS as fp16 [channel][pixel]
+// rows of 40 halves (the forward kernel's conflict-free 80-B rows).  Each thread loads four pixel rows of one
+// channel quad (float4, coalesced along channels), rounds them to fp16 and writes each channel's four pixels
+// as one ds_write_b64.  Block tile 128 (co) x 128 (k), 2 x 2 waves of 64 x 64, 32 pixels per step, registers
+// prefetched one step ahead, double-buffered LDS; the pixel range is split over workgroups and the partial
+// tiles are added with float atomics (summation order varies in the last bits, as in the fp32 kernels).
+constexpr int WT = 128, WMS = 32;
+
+__global__ __launch_bounds__(256, 2) void k_wgrad_h16(const float *__restrict__ x, const float *__restrict__ dz,
+                                                       int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
+                                                       int K, int stride, int pad, int dil, int64_t mchunk, int ctiles,
+                                                       int ntiles, float *__restrict__ dW) {
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2][2 * WT * HROW];
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int tile = (int)(bid % (unsigned)ntiles);
+    const int64_t split = bid / (unsigned)ntiles;
+    const int co0 = (tile % ctiles) * WT, k0 = (tile / ctiles) * WT;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int64_t mb = split * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    if (mb >= me) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+    const int rg = tid >> 5, q = tid & 31;  // staging: pixel rows 4 rg .. 4 rg + 3, channel quad q
+    const int co = co0 + 4 * q;
+    const bool co_ok = co < Co;
+    const int k = k0 + 4 * q;  // 4 consecutive k inside one tap (Ci % 4 == 0)
+    const bool k_ok = k < K;
+    const int tap = k_ok ? k / Ci : 0, ci = k - tap * Ci, ky = tap / KW, kx = tap - ky * KW;
+    // (image, row, column) of this thread's first pixel row in the current step
+    int px, py, pn;
+    {
+        const int64_t m = mb + 4 * rg, t = m / Wo;
+        px = (int)(m - t * Wo);
+        py = (int)(t % Ho);
+        pn = (int)(t / Ho);
+    }
+    int64_t ms = mb;
+    f32x4 ra[4], rb[4];
+    auto gload = [&]() {
+        int x1 = px, y1 = py, n1 = pn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t m = ms + 4 * rg + r;
+            const bool mok = m < me;
+            ra[r] = (mok && co_ok) ? *(const f32x4 *)(dz + m * Co + co) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            const int iy = y1 * stride - pad + ky * dil, ix = x1 * stride - pad + kx * dil;
+            const bool in = mok && k_ok && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            rb[r] = in ? *(const f32x4 *)(x + (((int64_t)n1 * H + iy) * W + ix) * Ci + ci) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            if (++x1 == Wo) {
+                x1 = 0;
+                if (++y1 == Ho) {
+                    y1 = 0;
+                    ++n1;
+                }
+            }
+        }
+        ms += WMS;
+        px += WMS;
+        while (px >= Wo) {
+            px -= Wo;
+            if (++py == Ho) {
+                py = 0;
+                ++pn;
+            }
+        }
+    };
+    auto swrite = [&](int buf) {
+        _Float16 *As = lds[buf], *Bs = As + WT * HROW;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const h16x4 ha = {(_Float16)ra[0][c], (_Float16)ra[1][c], (_Float16)ra[2][c], (_Float16)ra[3][c]};
+            const h16x4 hb = {(_Float16)rb[0][c], (_Float16)rb[1][c], (_Float16)rb[2][c], (_Float16)rb[3][c]};
+            *(h16x4 *)(As + (4 * q + c) * HROW + 4 * rg) = ha;
+            *(h16x4 *)(Bs + (4 * q + c) * HROW + 4 * rg) = hb;
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    const int nsteps = (int)((me - mb + WMS - 1) / WMS);
+    gload();
+    swrite(0);
+    __syncthreads();
+    const int r32 = lane & 31, h = lane >> 5;
+    for (int st = 0; st < nsteps; ++st) {
+        const bool more = st + 1 < nsteps;
+        if (more) gload();
+        const _Float16 *As = lds[st & 1], *Bs = As + WT * HROW;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            h16x8 fa[2], fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fa[i] = *(const h16x8 *)(As + (wm * 64 + i * 32 + r32) * HROW + kk * 16 + 8 * h);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) fb[j] = *(const h16x8 *)(Bs + (wn * 64 + j * 32 + r32) * HROW + kk * 16 + 8 * h);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) swrite((st + 1) & 1);
+        __syncthreads();
+    }
+    // D[row][col]: row = co (A rows), col = k; row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5), col = lane & 31
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int kc = k0 + wn * 64 + j * 32 + r32;
+            if (kc >= K) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int cr = co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (cr < Co) atomicAdd(dW + (int64_t)cr * K + kc, acc[i][j][r]);
+            }
+        }
+}
+
 }  // namespace
 
 extern "C" {
+
+int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
+                           int KH, int KW, int stride, int pad, int dilation, float *dW, void *stream) {
+    if (!x || !dz || !dW || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+        pad < 0 || dilation <= 0)
+        return BEV_ERR_ARGS;
+    if (Ci % 4 != 0 || Co % 4 != 0 || (((uintptr_t)x | (uintptr_t)dz) & 15) != 0) return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - dilation * (KH - 1) - 1) / stride + 1 ||
+        Wo != (W + 2 * pad - dilation * (KW - 1) - 1) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    const int K = KH * KW * Ci;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(dW, 0, (size_t)Co * K * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
+    if (M == 0) return 0;
+    const int ct = (Co + WT - 1) / WT, kt = (K + WT - 1) / WT, nt = ct * kt;
+    int64_t sp = 1024 / nt + 1;  // >= ~1024 workgroups
+    int64_t mc = (M + sp - 1) / sp;
+    mc = ((mc + WMS - 1) / WMS) * WMS;
+    sp = (M + mc - 1) / mc;
+    if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL(k_wgrad_h16, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K,
+                       stride, pad, dilation, mc, ct, nt, dW);
+    return (int)hipGetLastError();
+}
+
 
 int64_t bev_conv_packed_size_h16(int Co, int Ci, int KH, int KW) {
     if (Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;

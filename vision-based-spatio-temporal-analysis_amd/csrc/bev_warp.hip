@@ -410,6 +410,62 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
     }
 }
 
+// The same DMA through a buffer descriptor based at the block origin (byte strides sH4 / sW4 < 2^24, every
+// byte offset of the feature map < 2^31 -- the launcher checks): per lane only 24-bit integer products and a
+// 32-bit offset, no 64-bit address arithmetic (slot / 17 as (slot * 61681) >> 20, exact for slot < 69632,
+// i.e. footprints < 4096 pixels).  The pad slot (sl == 16) re-reads channel group 0 (any in-range address).
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+template <int S = 17>
+__device__ __forceinline__ void dma_block_buf(const float *__restrict__ f, int sH4, int sW4, int sx0, int sy0, int sbw,
+                                              int npix, unsigned char *smem, int off, int wave, int lane,
+                                              int nwaves = FT_NT / 64) {
+    static_assert(S == 17, "slot decomposition assumes 17 slots per pixel");
+    if (WARP_ABLATE & 2) return;
+    const int ninstr = (npix * S + 63) >> 6;
+    const float inv_bw = 1.0f / (float)sbw;
+    const uint64_t a = (uint64_t)(uintptr_t)f + (uint64_t)((int64_t)sy0 * sH4 + (int64_t)sx0 * sW4);
+    const v4i_t rsrc = {__builtin_amdgcn_readfirstlane((int)(uint32_t)a),
+                        __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu)), 0x7fffffff, 0x00020000};
+    for (int k = wave; k < ninstr; k += nwaves) {
+        const unsigned slot = (unsigned)(k * 64 + lane);
+        const unsigned p = __umul24(slot, 61681u) >> 20;
+        const unsigned sl = slot - ((p << 4) + p);
+        int q = (int)((float)p * inv_bw);
+        int r = (int)p - (int)__umul24((unsigned)q, (unsigned)sbw);
+        const bool hi = r >= sbw, lo = r < 0;
+        q += (int)hi - (int)lo;
+        r += (lo ? sbw : 0) - (hi ? sbw : 0);
+        unsigned voff = __umul24((unsigned)q, (unsigned)sH4) + __umul24((unsigned)r, (unsigned)sW4) + ((sl & 15u) << 4);
+        voff = ((int)p < npix) ? voff : 0u;  // tail lanes: any in-range address
+        const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_base(smem) + off + k * 1024));
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(voff), "s"(dst), "s"(rsrc)
+            : "memory");
+    }
+}
+
+#ifndef WARP_STAMP
+#define WARP_STAMP 0  // timing builds only (tools/warp_stamps.py): per-workgroup s_memtime stamps of the v2 phases
+#endif
+#if WARP_STAMP
+__device__ unsigned long long g_warp_stamp[16384 * 6];
+#define STAMP(k)                                                                                             \
+    do {                                                                                                     \
+        const unsigned sb_ = blockIdx.x + blockIdx.y * gridDim.x;                                            \
+        if (threadIdx.x == 0 && sb_ < 16384) g_warp_stamp[sb_ * 6 + (k)] = __builtin_amdgcn_s_memtime();      \
+    } while (0)
+#else
+#define STAMP(k) ((void)0)
+#endif
+
+#ifndef WARP_DMABUF
+#define WARP_DMABUF 1  // fused warp v2: footprint DMA through a buffer descriptor (1) or 64-bit global addresses (0)
+#endif
+
 // Output stores of a 64-channel chunk through a buffer descriptor: SGPR base of
 // the chunk, per-lane byte offset of the cell, SGPR byte offset of the channel
 // plane -> no per-store address arithmetic.  The dispatcher guarantees the
@@ -739,8 +795,16 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     }
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    STAMP(0);
     int tr, tc;
     tile_cell<TH>(lane, wave, tr, tc);
+    // footprint DMA: buffer-descriptor form when the byte strides fit 24 bits and the map 2^31 bytes (uniform)
+    const bool bufdma = WARP_DMABUF && sH * 4 < (1 << 24) && sW * 4 < (1 << 24) &&
+                        ((int64_t)Hf * sH + (int64_t)Wf * sW) * 4 < (1ll << 31);
+    auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
+        if (bufdma) dma_block_buf<SL>(fp, (int)sH * 4, (int)sW * 4, x0, y0, w, n, smem, o, wave, lane, NW);
+        else dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, wave, lane, NW);
+    };
     const int i = tyb * TH + tr;
     const int j = txb * TW + tc;
     const int b0 = blockIdx.y * FPW;
@@ -795,6 +859,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         same = btab[2 * V2_MAXV] != 0u;
     };
     prologue(b0, FPW > 1 && b0 + 1 < B && tcache >= 0);
+    STAMP(1);
     auto box_of = [&](int v) {
         const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
         const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
@@ -892,12 +957,12 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
             if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
                 offn = 0;
-                dma_block<SL>(fb + (int64_t)v_first * sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix,
-                              smem, 0, wave, lane, NW);
+                dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, 0);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // zero pixel + image of the first live view
+        STAMP(2);
 
         for (int v = v_first, vn; v < V; v = vn) {
             vn = next_live(v);
@@ -929,7 +994,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 const bool single = (nbx == 1) && (nby == 1);
                 if (single)  // the common case: start the copy (the pool is free since the last
                              // end-of-view barrier), compute the taps while it lands
-                    dma_block<SL>(f, (int)sH, (int)sW, bx.x0, bx.y0, bw, bw * bh, smem, 0, wave, lane, NW);
+                    dma(f, bx.x0, bx.y0, bw, bw * bh, 0);
                 if (!have_t) {
                     t = taps_of(v);
                     have_t = true;
@@ -948,7 +1013,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
                         if (!single) {
                             __syncthreads();  // earlier LDS images are no longer read
-                            dma_block<SL>(f, (int)sH, (int)sW, sx0, sy0, sbw, sbw * sbh, smem, 0, wave, lane, NW);
+                            dma(f, sx0, sy0, sbw, sbw * sbh, 0);
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
@@ -974,8 +1039,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
                     } else if (need <= off) offn = 0;
                     if (offn >= 0)
-                        dma_block<SL>(fb + (int64_t)vn * sN, (int)sH, (int)sW, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix,
-                                      smem, offn, wave, lane, NW);
+                        dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, offn);
                 }
             }
             // ---- sample view v from its prefetched image ------------------------------
@@ -990,7 +1054,9 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
             __syncthreads();  // all of it landed; image of view v and red[] are free
         }
+        STAMP(3);
         if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+        STAMP(4);
       }
     }
 }
@@ -1254,6 +1320,14 @@ int warp_tune(int knob, int value) {
 extern "C" {
 
 int bev_abi_version(void) { return 5; }
+
+#if WARP_STAMP
+int bev_warp_stamp_read(unsigned long long *host, int n) {  // timing builds only
+    if (n > 16384 * 6) n = 16384 * 6;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_warp_stamp), (size_t)n * sizeof(unsigned long long), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 
 int bev_linspace_f32(double lo, double hi, int n, float *out) {
     if (n < 0 || (n > 0 && !out)) return BEV_ERR_ARGS;
