@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--stream-offset", type=int, default=None, help="ResNet inference: stagger of the stream groups")
     ap.add_argument("--cpu-iters", type=int, default=2, help="frames timed for the CPU baseline (0 = skip)")
     ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
-    ap.add_argument("--warp-kernel", choices=("dma", "register"), default="dma",
+    ap.add_argument("--warp-kernel", choices=("dma", "register", "wave"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
     args = ap.parse_args()
     if args.views is None:
@@ -337,7 +337,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(rank)
     images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
-    nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1}[args.warp_kernel])
+    nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1, "wave": 2}[args.warp_kernel])
     stream = torch.cuda.current_stream(dev)
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
 

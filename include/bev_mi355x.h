@@ -43,7 +43,8 @@ int bev_abi_version(void);
  * BEV_TUNE_WARP_POOL_KB: LDS footprint-image pool (ring) per workgroup of the fused
  *   warp in KiB, 0 = automatic, else 8..150 (small pools force block decomposition).
  * BEV_TUNE_WARP_KERNEL: fused warp kernel for NHWC C % 64 == 0 features:
- *   0 = LDS-DMA kernel (default), 1 = register-staged.
+ *   0 = LDS-DMA kernel (default), 1 = register-staged, 2 = wave-independent LDS-DMA kernel (per-wave
+ *   footprints, no workgroup barrier).
  * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.
@@ -101,6 +102,16 @@ int bev_ipm_warp_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int
 int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                           int Hb, int Wb, int mode, float *out, void *stream);
+
+/* bev_ipm_warp_fuse_f32 with a caller-owned device workspace of at least
+ * bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb) bytes (8-B aligned, stream-ordered like the output): the
+ * fused kernel's per-(frame, tile, view) footprint boxes are then computed by a separate small launch instead of
+ * inside every workgroup (same results, bit for bit).  A null or short workspace = bev_ipm_warp_fuse_f32. */
+int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb);
+int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                             const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                             int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
+                             void *stream);
 
 /* Bilinear corners for index-exactness checks: x0y0 [N][Hb][Wb][2] int32
  * (0 when both taps of an axis are out of range), wts [N][Hb][Wb][4] (nw, ne,

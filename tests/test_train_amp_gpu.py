@@ -16,7 +16,7 @@ ResNet-50 BEVNet step is compared with a torch restatement of the reference grap
 evaluated in float64 and in float32 on the CPU -- under AMP with the fp16 rounding of every conv operand the
 native path rounds emulated (_H16Conv) -- and every output, loss and parameter gradient of the native run must be
 within 4x the float32 reference's own distance from the float64 value (floor 1e-5 of the scale): as accurate as
-the reference's arithmetic; BN running statistics rel 1e-4.
+the reference's arithmetic; BN running statistics rel 1e-4 (5e-4 with fp16 convs).
 """
 import copy
 import json
@@ -247,7 +247,7 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
     for net in (ref, ref32):
         net._build_training_targets = lambda _t, t_ref=t_ref: t_ref
     # and the loss of the native outputs evaluated on the CPU in float64 equals the native loss
-    cpu_loss = ref.loss({k: v.detach().cpu().double() for k, v in preds.items()},
+    cpu_loss = ref.loss({k: v.detach().cpu().double() for k, v in preds.items() if isinstance(v, torch.Tensor)},
                         [{"boxes_world": b.double()} for b in boxes], cfg["LOSS"])
     for k in ("heatmap_loss", "offset_loss", "size_loss"):
         a, b = float(losses[k]), float(cpu_loss[k])
@@ -306,7 +306,7 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
     for k, b in ref.named_buffers():
         if k in stats:
             err = (stats[k] - b).abs().max().item() / max(b.abs().max().item(), 1e-12)
-            assert err < 1e-4, (k, err)
+            assert err < (5e-4 if half else 1e-4), (k, err)  # fp16 convs: rounding flips move the batch stats
 
 
 def _free_port():
@@ -343,7 +343,7 @@ def _r50_ddp_worker(rank, world, port, q):
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
         scaler = torch.amp.GradScaler("cuda")
         model.train()
-        losses = [bev_dist.train_step(ddp, batch, targets, opt, scaler=scaler)["total_loss"] for _ in range(2)]
+        losses = [bev_dist.train_step(ddp, batch, targets, opt, scaler=scaler)["total_loss"] for _ in range(3)]
         # an eval forward through DDP broadcasts rank 0's buffers (broadcast_buffers=True) and updates none
         model.eval()
         with torch.no_grad():
@@ -361,8 +361,10 @@ def test_bevnet_r50_ddp_world2_trainable_trunk_amp():
     """K3 at world 2 as train.py would run it under DDP: ResNet-50 BEVNet with the TRUNK trainable (batch-
     statistics BN), autocast(float16) + GradScaler, one frame per rank, gradients all-reduced (gloo; both ranks
     on the box's single GPU).  Rank 0's parameters are broadcast at wrap time; after the steps both replicas'
-    parameters are bit-identical and moved (trunk included), the scaler found no inf, and rank 0's BN running
-    statistics -- broadcast at each forward (bev_dist.ddp_wrap) -- are what both ranks hold."""
+    parameters are bit-identical and moved (trunk included), the scalers agree, and rank 0's BN running
+    statistics -- broadcast at each forward (bev_dist.ddp_wrap) -- are what both ranks hold.  Three steps: with fp16
+    convs the first step at the initial scale 65536 may meet an inf (GradScaler skips it and halves the scale, as in
+    the reference's own AMP), the others are taken."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -385,4 +387,5 @@ def test_bevnet_r50_ddp_world2_trainable_trunk_amp():
         assert np.array_equal(res[0][4][k], res[1][4][k]), k
     assert any(not np.array_equal(res[0][3][k], res[0][4][k]) for k in res[0][3])  # batch statistics moved
     assert all(np.isfinite(res[r][2]).all() for r in (0, 1))
-    assert res[0][5] == res[1][5] == 65536.0
+    # the scale both ranks hold: 65536 unless a step met an fp16 inf (fp16 convs), then halved -- on both ranks
+    assert res[0][5] == res[1][5] and res[0][5] in (65536.0, 32768.0, 16384.0)

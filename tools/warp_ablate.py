@@ -32,22 +32,35 @@ def main():
     sx, sy = nat._scales(Hf, Wf, hw)
     out = torch.empty(B, C, 480, 1440, device=dev)
     s = feats.stride()
-    libs = {b: ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{b}.so")) for b in bits}
+    # a trailing "n" times the same library without the workspace (the in-kernel corner-box prologue)
+    libs = {b: ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{b.rstrip('n') or b}.so"))
+            for b in bits}
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ws = torch.empty(nat.lib().bev_ipm_warp_fuse_workspace_bytes(B, V, 480, 1440), device=dev, dtype=torch.uint8)
     args = (nat._ptr(feats), s[1], s[2], s[3], s[4], nat._ptr(Hm), nat._ptr(xs), nat._ptr(ys), B, V, C, Hf, Wf, sx, sy,
-            480, 1440, 1, nat._ptr(out), st)
+            480, 1440, 1, nat._ptr(out), nat._ptr(ws), ws.numel(), st)
     for L in libs.values():
-        L.bev_ipm_warp_fuse_f32.restype = ctypes.c_int
-        L.bev_ipm_warp_fuse_f32.argtypes = nat.SIGNATURES["bev_ipm_warp_fuse_f32"][1]
+        L.bev_ipm_warp_fuse_ws_f32.restype = ctypes.c_int
+        L.bev_ipm_warp_fuse_ws_f32.argtypes = nat.SIGNATURES["bev_ipm_warp_fuse_ws_f32"][1]
+    args_n = args[:-3] + (None, 0, st)
+    # a leading "w" times the wave-independent kernel (bev_tune(BEV_TUNE_WARP_KERNEL, 2)); libwarp_ablate_w<b>.so
+    # must be a separate copy of the library (its own knob state)
+    for b, L in libs.items():
+        if b.startswith("w"):
+            tune = getattr(L, "_ZN3bev9warp_tuneEii")  # bev::warp_tune (bev_warp.hip alone has no bev_tune)
+            tune.restype = ctypes.c_int
+            tune.argtypes = [ctypes.c_int, ctypes.c_int]
+            assert tune(nat.TUNE_WARP_KERNEL, 2) >= 0
     for rnd in range(3):
         for b, L in libs.items():
+            a = args_n if b.endswith("n") else args
             for _ in range(3):
-                assert L.bev_ipm_warp_fuse_f32(*args) == 0
+                assert L.bev_ipm_warp_fuse_ws_f32(*a) == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             n = 30
             for _ in range(n):
-                L.bev_ipm_warp_fuse_f32(*args)
+                L.bev_ipm_warp_fuse_ws_f32(*a)
             e1.record()
             torch.cuda.synchronize()
             print(f"round {rnd} variant {b:>6}: {e0.elapsed_time(e1) / n * 1e3:8.1f} us per launch", flush=True)

@@ -34,15 +34,21 @@ def main():
     out = torch.empty(B, C, 480, 1440, device=dev)
     s = feats.stride()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ws = torch.empty(nat.lib().bev_ipm_warp_fuse_workspace_bytes(B, V, 480, 1440), device=dev, dtype=torch.uint8)
     args = (nat._ptr(feats), s[1], s[2], s[3], s[4], nat._ptr(Hm), nat._ptr(xs), nat._ptr(ys), B, V, C, Hf, Wf, sx, sy,
-            480, 1440, 1, nat._ptr(out), st)
+            480, 1440, 1, nat._ptr(out), nat._ptr(ws), ws.numel(), st)
     nwg = ((1440 + 15) // 16) * ((480 + 15) // 16) * B
     for name in names:
         L = ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{name}.so"))
-        L.bev_ipm_warp_fuse_f32.restype = ctypes.c_int
-        L.bev_ipm_warp_fuse_f32.argtypes = nat.SIGNATURES["bev_ipm_warp_fuse_f32"][1]
+        if name.startswith("w"):  # the wave-independent kernel (a separate copy of the library)
+            tune = getattr(L, "_ZN3bev9warp_tuneEii")  # bev::warp_tune (bev_warp.hip alone has no bev_tune)
+            tune.restype = ctypes.c_int
+            tune.argtypes = [ctypes.c_int, ctypes.c_int]
+            assert tune(nat.TUNE_WARP_KERNEL, 2) >= 0
+        L.bev_ipm_warp_fuse_ws_f32.restype = ctypes.c_int
+        L.bev_ipm_warp_fuse_ws_f32.argtypes = nat.SIGNATURES["bev_ipm_warp_fuse_ws_f32"][1]
         for _ in range(5):
-            assert L.bev_ipm_warp_fuse_f32(*args) == 0
+            assert L.bev_ipm_warp_fuse_ws_f32(*args) == 0
         torch.cuda.synchronize()
         buf = (ctypes.c_ulonglong * (16384 * 6))()
         assert L.bev_warp_stamp_read(buf, 16384 * 6) == 0

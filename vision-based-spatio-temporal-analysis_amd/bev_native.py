@@ -19,7 +19,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -40,6 +40,9 @@ SIGNATURES = {
     "bev_ipm_warp_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
     "bev_ipm_warp_fuse_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
                                    _i, _vp, _vp]),
+    "bev_ipm_warp_fuse_workspace_bytes": (_i64, [_i, _i, _i, _i]),
+    "bev_ipm_warp_fuse_ws_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
+                                      _i, _vp, _vp, _i64, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_ipm_warp_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
     "bev_ipm_warp_fuse_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _vp]),
@@ -316,10 +319,14 @@ def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, o
     if out is None:
         out = torch.empty(B, C, Hb, Wb, device=feats.device, dtype=torch.float32)
     s = feats.stride()
+    # the per-(frame, tile, view) footprint boxes go to a stream-ordered workspace (a small launch of their own)
+    nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
+    ws = torch.empty(max(nws, 8), device=feats.device, dtype=torch.uint8)
     with _span("warp_fuse", feats):
-        rc = lib().bev_ipm_warp_fuse_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C,
-                                         Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _stream(feats))
-    _check(rc, "bev_ipm_warp_fuse_f32")
+        rc = lib().bev_ipm_warp_fuse_ws_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C,
+                                            Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _ptr(ws), nws,
+                                            _stream(feats))
+    _check(rc, "bev_ipm_warp_fuse_ws_f32")
     return out
 
 

@@ -476,14 +476,23 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * N * sizeof(float)), 0x00020000);
     const int voff = cell * (int)sizeof(float);
+    static_assert(N % 8 == 0, "stores in groups of 8 channels");
 #pragma unroll
-    for (int q = 0; q < N; ++q) {
-        float a = acc[q];
-        asm volatile("" : "+v"(a)::"memory");  // convert after the previous store (no hoisted doubles)
-        const float r = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? div_rcp(a, rV) : a;
-        if ((WARP_ABLATE & 16) && r != 1.2345e-30f) continue;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
-                                              (int)(uint32_t)(q * plane * sizeof(float)), 2);
+    for (int q0 = 0; q0 < N; q0 += 8) {
+        // eight independent divisions, then their stores: the group is pinned after the previous group's
+        // stores (no hoisted doubles for all N channels), the chains inside it overlap
+        float a[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a[u] = acc[q0 + u];
+        asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),
+                     "+v"(a[7])::"memory");
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float r = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? div_rcp(a[u], rV) : a[u];
+            if ((WARP_ABLATE & 16) && r != 1.2345e-30f) continue;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
+                                                  (int)(uint32_t)((q0 + u) * plane * sizeof(float)), 2);
+        }
     }
 }
 
@@ -777,7 +786,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
                                                           int B, int V, int C, int Hf, int Wf, float sx, float sy,
                                                           int Hb, int Wb, float *__restrict__ out, int pool,
-                                                          int tcache) {
+                                                          int tcache, const uint2 *__restrict__ boxes) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
     constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
@@ -824,6 +833,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     unsigned lba = 0, lbb = 0;
     bool same = false;
     auto prologue = [&](int bb, bool check_next) {
+        if (WARP_HSCALAR && boxes != nullptr) {  // precomputed by k_warp_boxes (FPW = 1): every wave reads them
+            const uint2 bx = lane < V ? boxes[((int64_t)bb * nt + tile) * V + lane] : make_uint2(0u, 0u);
+            lba = bx.x;
+            lbb = bx.y;
+            same = false;
+            return;
+        }
         if (wave == 0) {
             const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
             const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
@@ -960,6 +976,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, 0);
             }
         }
+        // the first live view's taps while its footprint lands (exact-bbox views reduce their taps first)
+        Taps tf;
+        bool have_f = false;
+        if (v_first < V && ok_of(v_first)) {
+            tf = taps_of(v_first);
+            have_f = true;
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // zero pixel + image of the first live view
         STAMP(2);
@@ -971,6 +994,11 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             const float *f = fb + (int64_t)v * sN;
             Taps t;
             bool have_t = false;
+            if (have_f) {
+                t = tf;
+                have_t = true;
+                have_f = false;
+            }
             if (!ok_of(v)) {
                 // exact footprint by per-cell reduction (horizon tiles); staged synchronously
                 t = taps_of(v);
@@ -1058,6 +1086,264 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
         STAMP(4);
       }
+    }
+}
+
+// Corner boxes of every (frame, tile, view) for k_warp_fuse_v2 (FPW = 1), one thread each: the tile prologue's
+// arithmetic (corner_box + the pool-size test) moved out of the sampling kernel, whose workgroups then start
+// with one 8-byte load per view instead of a double-precision latency chain on one wave while three wait.
+template <int TH, int TW = FT_NT / TH>
+__global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hmat, const float *__restrict__ xs,
+                                                    const float *__restrict__ ys, int V, int Hf, int Wf, float sx,
+                                                    float sy, int Hb, int Wb, int maxpix, int nty,
+                                                    uint2 *__restrict__ boxes) {
+    const int ntx = (Wb + TW - 1) / TW, nt = ntx * nty;  // nty >= ceil(Hb / TH) box-tile rows (extra rows: empty)
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int b = blockIdx.y;
+    if (t >= (int64_t)nt * V) return;
+    const int tile = (int)(t / V), v = (int)(t - (int64_t)tile * V);
+    const int tyb = tile / ntx, txb = tile - tyb * ntx;
+    const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
+    const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
+    bool ok = true;
+    Box cb{0x7fffffff, 0x7fffffff, -1, -1};
+    if (ia < Hb) {
+        float hv[9];
+        load_h(Hmat, b * V + v, hv);
+        cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok);
+    }
+    if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
+    const bool emp = cb.x1 < 0;
+    boxes[((int64_t)b * nt + tile) * V + v] =
+        make_uint2((emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u),
+                   emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16));
+}
+
+// -------------------------------------------------------------------------
+// fused warp + reduce, wave-independent (k_warp_fuse_w): no workgroup barrier
+// -------------------------------------------------------------------------
+// The workgroup's four waves share nothing but the launch: wave w owns the 4 x 16 cells of rows 4w .. 4w + 3 of
+// the 16 x 16 tile (the same cells, lanes, taps, sampling order and stores as k_warp_fuse_v2<.., 16, 1>, hence
+// bit-identical results), and stages, for each view, the footprint of ITS cells into its own slice of LDS (pool
+// `wpool` bytes + a zero pixel).  Its own LDS-DMA completes under its own vmcnt, so the per-view workgroup barrier
+// of v2 is gone: the waves drift apart and hide each other's DMA / tap / sampling latency.  Footprints are
+// per-wave corner boxes (k_warp_boxes over 4 x 16 tiles; in-lane if no workspace); the ring anchors consecutive
+// images at opposite ends of the pool; a footprint larger than what is free is staged synchronously, in
+// overlapping blocks when larger than the pool; tiles where the corner bound does not apply reduce their exact
+// per-cell box by shuffles.  Staging volume ~2x v2's (smaller tiles overlap more), LDS-read and VALU work equal.
+template <int MODE, int OCC>
+__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_w(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                         int64_t sW, const float *__restrict__ Hmat,
+                                                         const float *__restrict__ xs, const float *__restrict__ ys,
+                                                         int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                                                         int Hb, int Wb, float *__restrict__ out, int wpool,
+                                                         const uint2 *__restrict__ boxes) {
+    constexpr int TH = 16, TW = 16, SL = 17, PS = SL * 16;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ib = wave * (wpool + 256);  // this wave's pool (byte offset in smem), zero pixel after it
+    const int zp = ib + wpool;
+    const int maxpix = wpool / PS - 4;
+    const int ntx = (Wb + TW - 1) / TW, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
+    int tile = blockIdx.x;
+    {
+        const int q = nt / 8, r = nt % 8, x = tile % 8;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    const int tyb = tile / ntx, txb = tile - tyb * ntx;
+    const int wtile = (tyb * 4 + wave) * ntx + txb;  // this wave's 4 x 16 box tile
+    STAMP(0);
+    int tr, tc;
+    tile_cell<TH>(lane, wave, tr, tc);
+    const bool bufdma = WARP_DMABUF && sH * 4 < (1 << 24) && sW * 4 < (1 << 24) &&
+                        ((int64_t)Hf * sH + (int64_t)Wf * sW) * 4 < (1ll << 31);
+    auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
+        if (bufdma) dma_block_buf<SL>(fp, (int)sH * 4, (int)sW * 4, x0, y0, w, n, smem, o, 0, lane, 1);
+        else dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, 0, lane, 1);
+    };
+    const int i = tyb * TH + tr;
+    const int j = txb * TW + tc;
+    const int b = blockIdx.y;
+    const bool inside = (i < Hb) && (j < Wb);
+    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
+    const size_t plane = (size_t)Hb * Wb;
+    const Grid grid = make_grid(Hf, Wf);
+    const double rV = recip_uniform(V);
+    if (lane < 16) *(float4 *)(smem + zp + lane * 16) = make_float4(0.f, 0.f, 0.f, 0.f);  // read after, same wave
+
+    // per-wave corner boxes, lane v <-> view v (v2's packing)
+    unsigned lba = 0, lbb = 0;
+    if (boxes != nullptr) {
+        const uint2 bx = lane < V ? boxes[((int64_t)b * (nt * 4) + wtile) * V + lane] : make_uint2(0u, 0u);
+        lba = bx.x;
+        lbb = bx.y;
+    } else if (lane < V) {
+        const int ia = tyb * TH + 4 * wave, ibr = min(ia + 3, Hb - 1);
+        const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
+        Box cb{0x7fffffff, 0x7fffffff, -1, -1};
+        bool ok = true;
+        if (ia < Hb) {
+            float hv[9];
+            load_h(Hmat, b * V + lane, hv);
+            cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ibr], sx, sy, Wf, Hf, ok);
+            if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
+        }
+        const bool emp = cb.x1 < 0;
+        lba = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
+        lbb = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
+    }
+    STAMP(1);
+    auto box_of = [&](int v) {
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
+        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
+        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
+    };
+    auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
+    const int hbase = b * V;
+    float ccx = cx, ccy = cy;
+    auto taps_of = [&](int v) {
+        float h[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane((hbase + v) * 9) + q];
+        float ix, iy;
+        cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
+        Taps t = taps_from_ixy(ix, iy, grid);
+        if (WARP_ABLATE & 8) {
+            const Box bb = box_of(v);
+            t.x0 = bb.x0 + (lane & 1);
+            t.y0 = bb.y0;
+            t.valid = (bb.x1 > bb.x0 + 1 && bb.y1 > bb.y0) ? 15u : 0u;
+            t.w[0] = t.w[1] = t.w[2] = t.w[3] = 0.25f;
+        }
+        if (!inside) t.valid = 0;
+        return t;
+    };
+
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        ccx = cx;
+        ccy = cy;
+        asm volatile("" : "+v"(ccx), "+v"(ccy));  // taps per chunk (no hoisting + spills)
+        float acc[64];
+#pragma unroll
+        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        const float *fb = feats + (int64_t)(b * V) * sN + c0;
+        auto live = [&](int u) { return !ok_of(u) || box_of(u).x1 >= 0; };
+        auto next_live = [&](int u) {
+            ++u;
+            while (u < V && !live(u)) {
+                zero_view<MODE>(acc, u);
+                ++u;
+            }
+            return u;
+        };
+        const int v_first = next_live(-1);
+        Box bn = box_of(v_first < V ? v_first : 0);
+        int offn = -1;
+        if (v_first < V) {
+            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+            if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
+                offn = ib;
+                dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, ib);
+            }
+        }
+        Taps tf;
+        bool have_f = false;
+        if (v_first < V && ok_of(v_first)) {
+            tf = taps_of(v_first);
+            have_f = true;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's own DMA: visible to its own reads
+        STAMP(2);
+
+        for (int v = v_first, vn; v < V; v = vn) {
+            vn = next_live(v);
+            Box bx = bn;
+            const int off = offn;
+            const float *f = fb + (int64_t)v * sN;
+            Taps t;
+            bool have_t = false;
+            if (have_f) {
+                t = tf;
+                have_t = true;
+                have_f = false;
+            }
+            if (!ok_of(v)) {  // exact per-cell box of this wave's cells (shuffle reduction, no exchange)
+                t = taps_of(v);
+                have_t = true;
+                bx = wave_box(t);
+            }
+            const bool empty = bx.x1 < 0;
+            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+            bool done = empty;
+            if (!done && off < 0) {
+                // synchronous staging (overlapping blocks if larger than the pool); the pool's previous
+                // images have been read: every earlier ds_read's result was consumed by its FMAs
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                    hb = min(bh, maxpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                if (single) dma(f, bx.x0, bx.y0, bw, bw * bh, ib);
+                if (!have_t) {
+                    t = taps_of(v);
+                    have_t = true;
+                }
+                int mkx = 0, mky = 0;
+                if (!single && t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
+                }
+                const bool wave_any = __ballot(t.valid != 0) != 0ull;
+                if (!single && !t.valid) zero_view<MODE>(acc, v);
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        if (!single) {
+                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous block's reads returned
+                            dma(f, sx0, sy0, sbw, sbw * sbh, ib);
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
+                        if (go) sample_view<MODE, 1, 64>(acc, t, mine, v, smem, ib, sx0, sy0, sbw, zp);
+                        else if (single) zero_view<MODE>(acc, v);
+                    }
+                done = true;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pool is free for the next DMA
+            }
+            // look ahead: DMA of the next live view beside the live image of view v
+            if (vn < V) {
+                bn = box_of(vn);
+                offn = -1;
+                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+                if (ok_of(vn) && bn.x1 >= 0 && npix <= maxpix) {
+                    const int need = ((npix * SL + 63) >> 6) * 1024;
+                    if (done || off < 0) offn = ib;
+                    else if (off == ib) {
+                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= wpool) offn = ib + wpool - need;
+                    } else if (need <= off - ib) offn = ib;
+                    if (offn >= 0) dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, offn);
+                }
+            }
+            if (!done) {
+                if (!have_t) t = taps_of(v);
+                if (WARP_ABLATE & 4) acc[0] += t.w[0] * t.w[3] + (float)(t.x0 + t.y0 + (int)t.valid);
+                else if (__ballot(t.valid != 0) != 0ull)
+                    sample_view_pipe<MODE, 64>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+                else zero_view<MODE>(acc, v);
+            } else if (empty) {
+                zero_view<MODE>(acc, v);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // view v + 1's image landed
+        }
+        STAMP(3);
+        if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+        STAMP(4);
     }
 }
 
@@ -1249,30 +1535,65 @@ constexpr int V2_TC_MAXV = 8;  // tap records only for rigs of up to 8 cameras (
 template <int OCC, int FPW>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                       int mode, float *out, hipStream_t st, int pool, int tc_bytes) {
+                       int mode, float *out, hipStream_t st, int pool, int tc_bytes, uint2 *boxes) {
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
     dim3 grid(ntiles, (B + FPW - 1) / FPW), block(FT_NT);
     const int tcache = tc_bytes > 0 ? pool + V2_FIXED : -1;
     const size_t lds = (size_t)pool + V2_FIXED + (tc_bytes > 0 ? tc_bytes : 0);
+    if (FPW != 1 || !WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (frame pairs / LDS homographies)
+    if (boxes) {
+        const int maxpix = pool / (17 * 16) - 4;  // the kernel's own pool test
+        hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
+                           st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes);
+    }
     if (mode == BEV_FUSE_SUM)
         hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache);
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache, boxes);
     else if (mode == BEV_FUSE_MEAN)
         hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache);
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache, boxes);
     else
         hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache);
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache, boxes);
+    return last();
+}
+
+// wave-independent kernel: 4 x (pool + zero pixel) per workgroup, OCC workgroups per CU
+template <int OCC>
+int launch_fuse_w_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                      const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                      float *out, hipStream_t st, uint2 *boxes) {
+    const int ntx = (Wb + 15) / 16, nty = (Hb + 15) / 16;
+    const int wpool = g_warp_pool_kb ? g_warp_pool_kb * 1024 / 4 : ((163840 / OCC - 64) / 4 - 256) & ~1023;
+    if (wpool < 4096) return BEV_ERR_ARGS;
+    if (boxes) {
+        const int maxpix = wpool / (17 * 16) - 4;
+        hipLaunchKernelGGL((k_warp_boxes<4, 16>), dim3((unsigned)(((int64_t)ntx * nty * 4 * V + 255) / 256), B),
+                           dim3(256), 0, st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, nty * 4, boxes);
+    }
+    dim3 grid(ntx * nty, B), block(FT_NT);
+    const size_t lds = (size_t)4 * (wpool + 256);
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL((k_warp_fuse_w<BEV_FUSE_SUM, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B,
+                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, wpool, boxes);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL((k_warp_fuse_w<BEV_FUSE_MEAN, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys,
+                           B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, wpool, boxes);
+    else if constexpr (OCC == 2)  // MAX's extra live state spills at 3 workgroups per CU
+        hipLaunchKernelGGL((k_warp_fuse_w<BEV_FUSE_MAX, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B,
+                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, wpool, boxes);
+    else
+        return BEV_ERR_ARGS;
     return last();
 }
 
 inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                          int Hb, int Wb, int mode, float *out, hipStream_t st) {
+                          int Hb, int Wb, int mode, float *out, hipStream_t st, uint2 *boxes) {
     if (mode == BEV_FUSE_MAX)  // MAX's extra live state spills at 3 workgroups per CU
         return launch_fuse_v2_occ<2, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                        st, g_warp_pool_kb ? g_warp_pool_kb * 1024 : 72 * 1024, 0);
+                                        st, g_warp_pool_kb ? g_warp_pool_kb * 1024 : 72 * 1024, 0, boxes);
     // tap records: worth it when a workgroup runs two frames or several 64-channel chunks
     const int tc_bytes = V * FT_NT * 12;
     const bool pair = WARP_PAIR && V <= V2_TC_MAXV && (B > 1 || C > 64);
@@ -1281,11 +1602,11 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
     const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : ((pair ? budget - tc_bytes : 49 * 1024) & ~1023);
     if (pair && pool >= 16 * 1024 && pool + V2_FIXED + tc_bytes <= 160 * 1024)
         return launch_fuse_v2_occ<3, 2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                        pool, tc_bytes);
+                                        pool, tc_bytes, boxes);
     return launch_fuse_v2_occ<WARP_OCC, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
                                            st, g_warp_pool_kb ? g_warp_pool_kb * 1024 :
                                            ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) < 49 * 1024 ?
-                                           ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) : 49 * 1024, 0);
+                                           ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) : 49 * 1024, 0, boxes);
 }
 
 }  // namespace
@@ -1301,7 +1622,7 @@ int warp_tune(int knob, int value) {
             break;
         case BEV_TUNE_WARP_KERNEL:
             slot = &g_warp_kernel;
-            ok = value >= 0 && value <= 1;
+            ok = value >= 0 && value <= 2;
             break;
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
@@ -1319,7 +1640,7 @@ int warp_tune(int knob, int value) {
 
 extern "C" {
 
-int bev_abi_version(void) { return 5; }
+int bev_abi_version(void) { return 6; }
 
 #if WARP_STAMP
 int bev_warp_stamp_read(unsigned long long *host, int n) {  // timing builds only
@@ -1372,9 +1693,26 @@ int bev_ipm_warp_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int
     return last();
 }
 
+int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb) {
+    if (B < 0 || V <= 0 || Hb < 0 || Wb < 0) return BEV_ERR_ARGS;
+    // the larger of the two box tables: v2's (TH x TW tiles) and the wave-independent kernel's (4 x 16)
+    constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
+    const int64_t v2 = (((int64_t)Wb + TW - 1) / TW) * (((int64_t)Hb + TH - 1) / TH);
+    const int64_t wv = (((int64_t)Wb + 15) / 16) * (((int64_t)Hb + 15) / 16) * 4;
+    return (int64_t)B * (v2 > wv ? v2 : wv) * V * (int64_t)sizeof(uint2);
+}
+
 int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                           int Hb, int Wb, int mode, float *out, void *stream) {
+    return bev_ipm_warp_fuse_ws_f32(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                    nullptr, 0, stream);
+}
+
+int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                             const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                             int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
+                             void *stream) {
     if (B < 0 || V <= 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B > 65535) return BEV_ERR_ARGS;
     if ((int64_t)Hf * Wf >= (1 << 22)) return BEV_ERR_ARGS;  // fast_div range of the footprint index
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
@@ -1386,8 +1724,19 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
                         ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) &&
                         (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) && (sN % 4 == 0) &&
                         (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32);
-    if (dma_ok && g_warp_kernel == 0)
-        return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
+    if (dma_ok && g_warp_kernel != 1)
+    {
+        const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
+        uint2 *boxes = (workspace && workspace_bytes >= need && ((uintptr_t)workspace & 7) == 0)
+                           ? reinterpret_cast<uint2 *>(workspace) : nullptr;
+        if (g_warp_kernel == 2)
+            return mode == BEV_FUSE_MAX
+                       ? launch_fuse_w_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                              st, boxes)
+                       : launch_fuse_w_occ<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                              st, boxes);
+        return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st, boxes);
+    }
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     if (C <= 16)
