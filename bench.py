@@ -430,7 +430,7 @@ def main():
                        "the caller stream around the whole encoder, incl. the max-pool); per-launch spans sum "
                        "higher because launches of the two groups run concurrently")}
         ach = alg / (wp_ms * 1e-3) / 1e9
-        wk = {"dma": "k_warp_fuse_v2", "register": "k_warp_fuse"}[args.warp_kernel]
+        wk = {"dma": "k_warp_fuse_v2", "register": "k_warp_fuse", "wave": "k_warp_fuse_w"}[args.warp_kernel]
         roof_wp = {"kernel": f"{wk} (IPM warp + {'sum' if args.camera_shard else 'mean'}, fused)", "bound": "hbm",
                    "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
                    "traffic": pmc.get("warp"), "alg_bytes_per_launch": alg, "out_bytes": out_b,

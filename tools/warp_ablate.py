@@ -51,7 +51,7 @@ def main():
             tune.restype = ctypes.c_int
             tune.argtypes = [ctypes.c_int, ctypes.c_int]
             assert tune(nat.TUNE_WARP_KERNEL, 2) >= 0
-    for rnd in range(3):
+    for rnd in range(int(os.environ.get("ROUNDS", "5"))):
         for b, L in libs.items():
             a = args_n if b.endswith("n") else args
             for _ in range(3):

@@ -448,6 +448,9 @@ __device__ __forceinline__ void dma_block_buf(const float *__restrict__ f, int s
     }
 }
 
+#ifndef WARP_PIPE
+#define WARP_PIPE 1  // fused warp v2: LDS sampling software-pipelined by one 4-channel group (1) or not (0)
+#endif
 #ifndef WARP_STAMP
 #define WARP_STAMP 0  // timing builds only (tools/warp_stamps.py): per-workgroup s_memtime stamps of the v2 phases
 #endif
@@ -463,7 +466,7 @@ __device__ unsigned long long g_warp_stamp[16384 * 6];
 #endif
 
 #ifndef WARP_DMABUF
-#define WARP_DMABUF 1  // fused warp v2: footprint DMA through a buffer descriptor (1) or 64-bit global addresses (0)
+#define WARP_DMABUF 0  // fused warp v2: footprint DMA through a buffer descriptor (1; r03m A/B: 1-8 % slower) or 64-bit global addresses (0)
 #endif
 
 // Output stores of a 64-channel chunk through a buffer descriptor: SGPR base of
@@ -1074,7 +1077,8 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             if (!done) {
                 if (!have_t) t = taps_of(v);
                 if (WARP_ABLATE & 4) acc[0] += t.w[0] * t.w[3] + (float)(t.x0 + t.y0 + (int)t.valid);
-                else if (__ballot(t.valid != 0) != 0ull) sample_view_pipe<MODE, 64>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+                else if (__ballot(t.valid != 0) != 0ull)
+                    sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
                 else zero_view<MODE>(acc, v);
             } else if (empty) {
                 zero_view<MODE>(acc, v);
