@@ -52,7 +52,9 @@ int bev_abi_version(void);
  *   (2, default), on the MFMA with transposed register staging (1), or the VALU float4 kernel (0).
  * BEV_TUNE_CONV_DMA: NHWC Ci % 32 == 0 convs stage their operands global -> LDS by LDS-DMA on
  *   1 (default) = the 64-column output tiles, 2 = every tile, 0 = none (through registers); same
- *   results bit for bit. */
+ *   results bit for bit.
+ * BEV_TUNE_CONV_X6_TILE: output tile of the split-bf16 fp32 convs (bev_conv2d_x6_f32 / _dual_x6_f32):
+ *   0 = automatic, 1 = 128x128, 2 = 128x64. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -61,6 +63,7 @@ int bev_abi_version(void);
 #define BEV_TUNE_CONV_NBUF 7
 #define BEV_TUNE_WGRAD_MFMA 8
 #define BEV_TUNE_CONV_DMA 9
+#define BEV_TUNE_CONV_X6_TILE 10
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------
@@ -312,6 +315,35 @@ int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16
  * Replaces the conv weight gradient autograd computes for the reference's autocast branch (train.py:238-247). */
 int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
                            int KH, int KW, int stride, int pad, int dilation, float *dW, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * fp32 convolutions on the bf16 matrix cores (exact three-way operand split; bev_conv_x6.hip)
+ * Every fp32 operand v is stored as bf16 h + m + l with v == h + m + l exactly; the six bf16 x bf16 partial
+ * products above 2^-27 |a b| are summed in the fp32 accumulator (the dropped three are below fp32 rounding),
+ * so the result is an fp32 convolution as accurate as the exact-f32 MFMA kernels of bev_conv2d_f32, at 2.67x
+ * their matrix-core rate.  Summation order differs from bev_conv2d_f32: fp32-tolerance equal, not bitwise.
+ * ------------------------------------------------------------------------- */
+
+/* host: number of bf16 elements of a split weight panel ([Co pad 128][K pad 16 / 16][3][16]). */
+int64_t bev_conv_packed_size_x6(int Co, int Ci, int KH, int KW);
+
+/* device: OIHW fp32 weights -> split bf16 panel (k = (ky*KW + kx)*Ci + ci), packed [size] uint16 storage. */
+int bev_conv_pack_weights_x6(const float *w, int Co, int Ci, int KH, int KW, uint16_t *packed, void *stream);
+
+/* device: y[m][n] (row pitch ldy) = act(sum_k x[m][k] * w[n][k] + bias[n] (+ residual[m][n])) in fp32 through the
+ * split panel; NHWC x [N][H][W][Ci] fp32 with Ci % 16 == 0, 16-B aligned; stride / pad / dilation as
+ * bev_conv2d_nhwc_ex_f32; act 0 none, 1 ReLU, 2 SiLU; bias / residual may be NULL (residual needs ldy == Co).
+ * Replaces the nn.Conv2d (+ folded eval BN) layers of the timm trunk and the lazy 1x1 projection
+ * (cnn_encoder.py:26,41-46) -- the same contract as bev_conv2d_f32 for NHWC inputs. */
+int bev_conv2d_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                      const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
+                      float *y, int ldy, int Ho, int Wo, void *stream);
+
+/* device: bev_conv2d_dual_f32 (bottleneck conv3 + downsample shortcut as one GEMM over K = [x | x2[::s2]]) through
+ * the split panel of the concatenated [Co][Ci + Ci2] weights; Ci, Ci2 % 16 == 0; act as above. */
+int bev_conv2d_dual_x6_f32(const float *x, int N, int Ho, int Wo, int Ci, const float *x2, int H2, int W2, int Ci2,
+                           int stride2, const uint16_t *packed, const float *bias, int Co, int act, float *y,
+                           void *stream);
 
 /* ---------------------------------------------------------------------------
  * CenterNet BEV head (BEVDetector, detector.py:16-62): dilated convs, GroupNorm(32) + ReLU

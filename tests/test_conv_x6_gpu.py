@@ -1,0 +1,136 @@
+"""fp32 convolutions on the bf16 matrix cores by exact three-way operand split (bev_conv2d_x6_f32,
+bev_conv2d_dual_x6_f32; csrc/bev_conv_x6.hip) -- the default arithmetic of the inference trunk.
+
+The reference runs these convs (timm trunk + lazy 1x1 proj, cnn_encoder.py:26,41-46) as fp32 nn.Conv2d.  The
+split kernels must be an fp32 convolution: every case is compared against float64 torch, and their error must not
+exceed the exact-f32 MFMA kernel's (bev_conv2d_f32) by more than a small factor -- fp32 accuracy, not bf16
+accuracy.  The tolerance (fp32 rtol 1e-4 vs torch fp32) is asserted too.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import bev_native as nat
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _case(N, H, W, Ci, Co, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, Ci, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Co, Ci, K, K, generator=g, dtype=torch.float64) / (Ci * K * K) ** 0.5
+    b = torch.randn(Co, generator=g, dtype=torch.float64) * 0.1
+    return x, w, b
+
+
+def _ref(x, w, b, stride, pad, dil, act, res=None):
+    y = F.conv2d(x, w, b, stride=stride, padding=pad, dilation=dil)
+    if res is not None:
+        y = y + res
+    if act == 1:
+        y = torch.relu(y)
+    elif act == 2:
+        y = F.silu(y)
+    return y
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+CASES = [
+    # N, H, W, Ci, Co, K, stride, pad, dil, act, residual
+    (2, 23, 37, 64, 64, 3, 1, 1, 1, 1, False),    # layer1 conv2 shape class, ragged M
+    (1, 30, 41, 128, 128, 3, 2, 1, 1, 1, False),  # layer2 block-0 conv2 (stride 2)
+    (2, 17, 19, 256, 64, 1, 1, 0, 1, 1, False),   # conv1 (1x1 reduce)
+    (2, 17, 19, 64, 256, 1, 1, 0, 1, 1, True),    # conv3 + identity residual + ReLU
+    (1, 21, 22, 48, 80, 3, 1, 2, 2, 2, False),    # dilation 2, SiLU, Co not a multiple of 64
+    (1, 9, 13, 512, 64, 1, 1, 0, 1, 0, False),    # the encoder's 1x1 proj (no activation)
+    (3, 15, 16, 16, 200, 3, 1, 1, 1, 1, True),    # Ci = 16 (one K step per tap), three N tiles
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"c{i}" for i in range(len(CASES))])
+def test_x6_conv_fp32_accuracy_vs_float64(case):
+    N, H, W, Ci, Co, K, s, p, d, act, with_res = case
+    x, w, b = _case(N, H, W, Ci, Co, K, 1234 + Ci + Co)
+    Ho, Wo = (H + 2 * p - d * (K - 1) - 1) // s + 1, (W + 2 * p - d * (K - 1) - 1) // s + 1
+    res = torch.randn(N, Co, Ho, Wo, dtype=torch.float64, generator=torch.Generator().manual_seed(7)) if with_res else None
+    # float64 reference on the fp32-rounded operands (what both kernels see)
+    x32, w32, b32 = x.float(), w.float(), b.float()
+    res32 = res.float() if res is not None else None
+    ref = _ref(x32.double(), w32.double(), b32.double(), s, p, d, act, res32.double() if res is not None else None)
+    ref = _nhwc(ref)
+    xd = _nhwc(x32).to(DEV)
+    rd = _nhwc(res32).to(DEV) if res is not None else None
+    bd = b32.to(DEV)
+    p6 = nat.pack_conv_weight_x6(w32.to(DEV))
+    assert p6.dtype == torch.bfloat16
+    y6 = nat.conv2d_nhwc_x6(xd, p6, bd, Co, K, K, s, p, d, act, residual=rd)
+    torch.cuda.synchronize()
+    e6 = (y6.cpu().double() - ref).abs()
+    scale = ref.abs().max().item()
+    assert torch.isfinite(y6).all()
+    assert e6.max().item() <= 1e-5 * scale, (e6.max().item(), scale)
+    torch.testing.assert_close(y6.cpu().double(), ref, rtol=1e-4, atol=1e-4 * scale)
+    if d == 1:  # the exact-f32 MFMA kernel on the same operands: the split kernel is no less accurate (within 4x)
+        pf = nat.pack_conv_weight(w32.to(DEV))
+        yf = nat.conv2d_nhwc(xd, pf, bd, Co, K, K, s, p, act == 1, residual=rd) if act != 2 else None
+        if yf is not None:
+            ef = (yf.cpu().double() - ref).abs()
+            assert e6.max().item() <= 4 * ef.max().item() + 1e-7 * scale, (e6.max().item(), ef.max().item())
+            assert e6.mean().item() <= 4 * ef.mean().item() + 1e-9 * scale, (e6.mean().item(), ef.mean().item())
+
+
+def test_x6_tiles_bit_identical():
+    """Both output tiles (BEV_TUNE_CONV_X6_TILE 1 = 128x128, 2 = 128x64) sum every output in the same K order."""
+    N, H, W, Ci, Co = 2, 19, 29, 64, 192
+    x, w, b = _case(N, H, W, Ci, Co, 3, 5)
+    xd, bd = _nhwc(x.float()).to(DEV), b.float().to(DEV)
+    p6 = nat.pack_conv_weight_x6(w.float().to(DEV))
+    outs = []
+    for t in (1, 2):
+        with nat.tuned(CONV_X6_TILE=t):
+            outs.append(nat.conv2d_nhwc_x6(xd, p6, bd, Co, 3, 3, 1, 1, 1, 1))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("stride2,Ci,Ci2,Co", [(1, 64, 64, 256), (2, 128, 256, 512)])
+def test_x6_dual_accuracy(stride2, Ci, Ci2, Co):
+    """Bottleneck conv3 + downsample shortcut as one split-bf16 GEMM (FoldedTail) vs float64."""
+    g = torch.Generator().manual_seed(11 + Ci2)
+    N, H2, W2 = 2, 21, 26
+    Ho, Wo = (H2 - 1) // stride2 + 1, (W2 - 1) // stride2 + 1
+    h = torch.randn(N, Ci, Ho, Wo, generator=g).float()
+    x2 = torch.randn(N, Ci2, H2, W2, generator=g).float()
+    w1 = (torch.randn(Co, Ci, 1, 1, generator=g) / Ci ** 0.5).float()
+    w2 = (torch.randn(Co, Ci2, 1, 1, generator=g) / Ci2 ** 0.5).float()
+    b = (torch.randn(Co, generator=g) * 0.1).float()
+    ref = torch.relu(F.conv2d(h.double(), w1.double(), b.double()) + F.conv2d(x2.double(), w2.double(), stride=stride2))
+    ref = _nhwc(ref)
+    wcat = torch.cat([w1.reshape(Co, -1), w2.reshape(Co, -1)], 1).reshape(Co, Ci + Ci2, 1, 1).contiguous()
+    p6 = nat.pack_conv_weight_x6(wcat.to(DEV))
+    y = nat.conv2d_dual_nhwc(_nhwc(h).to(DEV), _nhwc(x2).to(DEV), stride2, p6, b.to(DEV), Co, relu=True)
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    e = (y.cpu().double() - ref).abs().max().item()
+    assert e <= 1e-5 * scale, (e, scale)
+
+
+def test_x6_resnet50_encoder_matches_f32_path():
+    """The ResNet-50 CNNEncoder (the bench's trunk) in the split-bf16 arithmetic vs the exact-f32 MFMA chains."""
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(0)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(DEV)
+    imgs = torch.randn(1, 3, 3, 96, 160, device=DEV)
+    with torch.no_grad():
+        with nat.conv_arith_mode("f32"):
+            ref = enc(imgs).float().clone()
+        with nat.conv_arith_mode("bf16x6"):
+            got = enc(imgs).float().clone()
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4 * scale)

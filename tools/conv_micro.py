@@ -17,6 +17,7 @@ import torch  # noqa: E402
 import bev_native as nat  # noqa: E402
 
 N = 7
+ARITH = "f32"  # --arith: panel of the plain / dual layers (bf16x6 = the split-bf16 kernels)
 # name: (Ci, Co, k, stride, H_in, W_in, residual, nchw_in)
 LAYERS = {
     "stem": (3, 64, 7, 2, 1080, 1920, False, True),
@@ -50,7 +51,7 @@ def run_dual(name, iters):
     x = torch.randn(N, H2, W2, Ci2, device=dev, generator=g)
     w = torch.randn(Co, Ci + Ci2, 1, 1, device=dev, generator=g) * (2.0 / (Ci + Ci2)) ** 0.5
     b = torch.randn(Co, device=dev, generator=g)
-    packed = nat.pack_conv_weight(w)
+    packed = nat.pack_conv_weight_x6(w) if ARITH == "bf16x6" else nat.pack_conv_weight(w)
     out = torch.empty(N, Ho, Wo, Co, device=dev)
     for _ in range(3):
         nat.conv2d_dual_nhwc(h, x, s2, packed, b, Co, True, out=out)
@@ -138,7 +139,7 @@ def run(name, iters):
     w = torch.randn(Co, Ci, k, k, device=dev, generator=g) * (2.0 / (Ci * k * k)) ** 0.5
     b = torch.randn(Co, device=dev, generator=g)
     r = torch.randn(N, Ho, Wo, Co, device=dev, generator=g) if res else None
-    packed = nat.pack_conv_weight(w)
+    packed = nat.pack_conv_weight_x6(w) if (ARITH == "bf16x6" and not nchw) else nat.pack_conv_weight(w)
     out = torch.empty(N, Ho, Wo, Co, device=dev)
     for _ in range(3):
         nat.conv2d_nhwc(x, packed, b, Co, k, k, s, p, True, residual=r, in_nchw=nchw, out=out)
@@ -161,7 +162,10 @@ def main():
     ap.add_argument("--knob", default="CONV_TILE", help="bev_tune knob to A/B (TUNE_<name>)")
     ap.add_argument("--values", type=int, nargs="*", default=[0], help="knob values, interleaved per round")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--arith", choices=("f32", "bf16x6"), default="f32")
     a = ap.parse_args()
+    global ARITH
+    ARITH = a.arith
     knob = getattr(nat, "TUNE_" + a.knob)
     for rnd in range(a.rounds):  # interleaved rounds, same process
         for v in a.values:

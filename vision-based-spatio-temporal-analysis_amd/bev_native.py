@@ -95,6 +95,10 @@ SIGNATURES = {
     "bev_conv_pack_weights_h16": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
     "bev_conv_wgrad_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_conv_packed_size_x6": (_i64, [_i, _i, _i, _i]),
+    "bev_conv_pack_weights_x6": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+    "bev_conv2d_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
+    "bev_conv2d_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
 }
 
 
@@ -166,6 +170,7 @@ TUNE_CONV_XCD = 6
 TUNE_CONV_NBUF = 7
 TUNE_WGRAD_MFMA = 8
 TUNE_CONV_DMA = 9
+TUNE_CONV_X6_TILE = 10
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 
@@ -205,6 +210,36 @@ class HipError(RuntimeError):
 # keeps every kernel in fp32 under autocast (wider than the reference).
 AMP_HALF_CONVS = True
 _AMP_LOCAL = threading.local()
+
+
+# fp32 arithmetic of the inference trunk convs (ResNet FoldedConv / FoldedTail, the encoder's 1x1 proj):
+# "bf16x6" = bev_conv2d_x6_f32 / bev_conv2d_dual_x6_f32 -- every fp32 operand split exactly into three bf16 terms,
+# the six partial products above 2^-27 relative on the bf16 matrix cores, fp32 accumulation: an fp32 convolution as
+# accurate as the exact-f32 MFMA kernels at 2.67x their matrix-core rate (tests/test_conv_x6_gpu.py measures both
+# against float64); "f32" = bev_conv2d_f32 and the chained bottleneck kernels (exact-f32 MFMA, bitwise an fmaf chain).
+CONV_ARITHS = ("f32", "bf16x6")
+_ARITH = {"mode": "bf16x6"}
+
+
+def conv_arith() -> str:
+    return _ARITH["mode"]
+
+
+def set_conv_arith(mode: str) -> str:
+    """Select the trunk conv arithmetic (CONV_ARITHS); returns the previous mode."""
+    if mode not in CONV_ARITHS:
+        raise ValueError(f"conv arithmetic {mode!r} not in {CONV_ARITHS}")
+    prev, _ARITH["mode"] = _ARITH["mode"], mode
+    return prev
+
+
+@contextlib.contextmanager
+def conv_arith_mode(mode: str):
+    prev = set_conv_arith(mode)
+    try:
+        yield
+    finally:
+        set_conv_arith(prev)
 
 
 def half_convs() -> bool:
@@ -399,12 +434,52 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def pack_conv_weight_x6(w: torch.Tensor) -> torch.Tensor:
+    """OIHW fp32 (device) -> split-bf16 panel (torch.bfloat16 storage) of bev_conv2d_x6_f32 / _dual_x6_f32; the
+    conv calls below dispatch on the panel's dtype."""
+    w = w.detach().contiguous().float()
+    _require_gpu(w)
+    Co, Ci, KH, KW = w.shape
+    n = lib().bev_conv_packed_size_x6(Co, Ci, KH, KW)
+    out = torch.empty(n, device=w.device, dtype=torch.bfloat16)
+    _check(lib().bev_conv_pack_weights_x6(_ptr(w), Co, Ci, KH, KW, _ptr(out), _stream(w)), "bev_conv_pack_weights_x6")
+    return out
+
+
+def conv2d_nhwc_x6(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
+                   dilation: int = 1, act: int = 0, residual: torch.Tensor = None, out: torch.Tensor = None):
+    """fp32 conv through the split-bf16 panel (bev_conv2d_x6_f32): x [N,H,W,Ci] fp32 NHWC, Ci % 16 == 0 -> y
+    [N,Ho,Wo,Co] fp32 (or the first Co channels of a wider NHWC `out`)."""
+    x = x.contiguous()
+    _require_gpu(x, bias, residual)
+    if not packed.is_cuda or packed.dtype != torch.bfloat16:
+        raise HipError("conv2d_nhwc_x6 needs the split-bf16 weight panel on the device")
+    N, H, W, Ci = x.shape
+    Ho, Wo = (H + 2 * pad - dilation * (KH - 1) - 1) // stride + 1, (W + 2 * pad - dilation * (KW - 1) - 1) // stride + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    assert out.shape[:3] == (N, Ho, Wo) and out.shape[3] >= Co and out.is_contiguous() and out.dtype == torch.float32
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == (N, Ho, Wo, Co) and out.shape[3] == Co
+    with _span("conv", x):
+        rc = lib().bev_conv2d_x6_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co, KH, KW,
+                                     stride, pad, dilation, int(act), _ptr(out), out.shape[3], Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_x6_f32")
+    return out
+
+
 def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
                 relu: bool, residual: torch.Tensor = None, in_nchw: bool = False, out: torch.Tensor = None,
                 ascale: torch.Tensor = None):
     """x: [N,H,W,Ci] NHWC (or [N,Ci,H,W] with in_nchw) -> y [N,Ho,Wo,Co] NHWC.
-    ascale [N, Ci]: per-image input-channel multiplier applied in the operand load (SE excitation)."""
+    ascale [N, Ci]: per-image input-channel multiplier applied in the operand load (SE excitation).
+    The kernel follows the panel: fp32 (bev_conv2d_f32), split bf16 (bev_conv2d_x6_f32), fp16 (autocast)."""
     x = x.contiguous()
+    if packed.dtype == torch.bfloat16:
+        if ascale is not None or in_nchw:
+            raise HipError("the split-bf16 conv takes NHWC inputs without an operand channel scale")
+        return conv2d_nhwc_x6(x, packed, bias, Co, KH, KW, stride, pad, 1, int(relu), residual=residual, out=out)
     if packed.dtype == torch.float16:  # autocast(float16): the fp16 matrix-core kernel
         if ascale is not None:
             raise HipError("the fp16 conv takes no operand channel scale (the SE gate is applied apart in training)")
@@ -511,11 +586,19 @@ def conv2d_dual_nhwc(x: torch.Tensor, x2: torch.Tensor, stride2: int, packed: to
     """act(x (*) W1 + x2[:, ::s2, ::s2] (*) W2 + bias), both 1x1, NHWC: x [N,Ho,Wo,Ci], x2 [N,H2,W2,Ci2]."""
     x = x.contiguous()
     x2 = x2.contiguous()
-    _require_gpu(x, x2, packed, bias)
+    _require_gpu(x, x2, bias, packed if packed.dtype != torch.bfloat16 else None)
+    if not packed.is_cuda:
+        raise HipError("conv2d_dual_nhwc needs the weight panel on the device")
     N, Ho, Wo, Ci = x.shape
     _, H2, W2, Ci2 = x2.shape
     if out is None:
         out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    if packed.dtype == torch.bfloat16:
+        with _span("conv", x):
+            rc = lib().bev_conv2d_dual_x6_f32(_ptr(x), N, Ho, Wo, Ci, _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed),
+                                              _ptr(bias), Co, int(relu), _ptr(out), _stream(x))
+        _check(rc, "bev_conv2d_dual_x6_f32")
+        return out
     with _span("conv", x):
         rc = lib().bev_conv2d_dual_f32(_ptr(x), N, Ho, Wo, Ci, _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed),
                                        _ptr(bias), Co, int(relu), _ptr(out), _stream(x))

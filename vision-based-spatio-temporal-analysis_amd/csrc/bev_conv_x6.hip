@@ -1,0 +1,450 @@
+// bev_conv_x6.hip -- fp32 convolutions on the bf16 matrix cores through an exact three-way operand split.
+//
+// Same contract as bev_conv2d_f32 (the timm trunk convs of CNNEncoder._encode_single, cnn_encoder.py:26,41-46):
+//     y[m][n] = act( sum_k A[m][k] * W[k][n] + bias[n] (+ res[m][n]) )
+// with fp32 operands and fp32 accumulation.  Every fp32 value v is written EXACTLY as the sum of three bf16
+// values by round-to-nearest-even splitting:
+//     h = bf16(v),  m = bf16(v - h),  l = bf16(v - h - m)        v == h + m + l  (8 + 8 + 8 significand bits;
+// both subtractions are exact in fp32 because each residual is a multiple of ulp(v) below half an ulp of the
+// previous term), |m| <= 2^-9 |v|, |l| <= 2^-18 |v|.  A product a*b is then the sum of nine bf16 x bf16
+// products, each EXACT in fp32; the six kept here are those larger than 2^-27 |a b|:
+//     hh + hm + mh + hl + lh + mm          (dropped: ml + lm + ll <= 2^-26 |a b|, below fp32's 2^-24 rounding)
+// and all of them accumulate into the fp32 MFMA accumulator.  The result is an fp32 GEMM whose per-product error
+// (<= 2^-26 relative) is below the fp32 rounding of the running sum it is added to, so it is exactly as accurate as
+// the exact-f32 MFMA path (tests/test_conv_x6_gpu.py measures both against float64), at 6 bf16 MFMAs per 16-deep
+// k slice instead of 8 fp32 32x32x2 MFMAs per 16: v_mfma_f32_32x32x16_bf16 is 32 cycles, v_mfma_f32_32x32x2_f32
+// 64 (MI355X_MICROARCH.md), so the matrix-core time per output falls from 512 to 192 cycles (2.67x).
+// Summation order differs from the fp32 kernel: fp32-tolerance equal, not bitwise.
+//
+// Implicit GEMM, m = (image, oy, ox), n = output channel, k = (ky, kx, ci), NHWC activations with Ci % 16 == 0
+// (a K step = one tap and 16 consecutive channels), or the dual-source 1x1 form of bev_conv2d_dual_f32 (bottleneck
+// conv3 + downsample shortcut as one GEMM over K = [h | x[::s]]).  256 threads = WM x WN waves, each TM x TN MFMA
+// tiles of 32 x 32.  Per K step the block stages A (global fp32 -> registers -> split -> three bf16 LDS planes) and
+// B (weights split once at pack time: panel [Co_pad][K_pad / 16][3][16] bf16, one 96-B run per row and step);
+// LDS rows of 24 bf16 (48 B = 3 odd 16-B slots: the 16-lane ds_read_b128 fragment groups are conflict-free);
+// double-buffered LDS, two register sets prefetched two K steps ahead, one barrier per step.  Fragment map
+// (cdna_hip_programming.md §3): lane l holds A[row l & 31][k 8 (l >> 5) + j] and B[k 8 (l >> 5) + j][col l & 31].
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../../include/bev_mi355x.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int XBK = 16;   // K step
+constexpr int XROW = 24;  // bf16 per LDS row (48 B)
+
+__device__ __attribute__((aligned(16))) float g_xzero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
+
+__host__ __device__ inline int64_t kpad_x(int K) { return (K + XBK - 1) / XBK * XBK; }
+__host__ __device__ inline int64_t copad_x(int Co) { return (Co + 127) / 128 * 128; }
+
+// v == h + m + l exactly (see the header); RNE conversions (v_cvt_pk_bf16_f32), exact fp32 residuals.
+__device__ __forceinline__ void split3(float v, __bf16 &h, __bf16 &m, __bf16 &l) {
+    h = (__bf16)v;
+    const float r = v - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+// OIHW fp32 -> [Co_pad][K_pad / 16][plane h, m, l][16] bf16, k = (ky*KW + kx)*Ci + ci
+__global__ void k_pack_x6(const float *__restrict__ w, int Co, int Ci, int KH, int KW, int64_t Kp, int64_t Cop,
+                          __bf16 *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= Kp * Cop) return;
+    const int n = (int)(t / Kp);
+    const int k = (int)(t % Kp);
+    const int K = Ci * KH * KW;
+    float v = 0.0f;
+    if (n < Co && k < K) {
+        const int ci = k % Ci, r = k / Ci, kx = r % KW, ky = r / KW;
+        v = w[(((int64_t)n * Ci + ci) * KH + ky) * KW + kx];
+    }
+    __bf16 h, m, l;
+    split3(v, h, m, l);
+    const int64_t o = ((int64_t)n * (Kp / XBK) + k / XBK) * (3 * XBK) + k % XBK;
+    out[o] = h;
+    out[o + XBK] = m;
+    out[o + 2 * XBK] = l;
+}
+
+struct ConvX {
+    const float *__restrict__ x;
+    const __bf16 *__restrict__ wp;
+    const float *__restrict__ bias;
+    const float *__restrict__ res;
+    float *__restrict__ y;
+    int N, H, W, Ci, Co, KH, KW, stride, pad, dil, Ho, Wo, act, ldy, Kp;
+    int64_t M;
+    // dual-source 1x1: k in [Ci, Ci + Ci2) reads x2 [N][H2][W2][Ci2] at (oy*stride2, ox*stride2)
+    const float *__restrict__ x2;
+    int Ci2, H2, W2, stride2;
+};
+
+__device__ __forceinline__ float act_x(float t, int act) {
+    if (act == 2) return t / (1.0f + expf(-t));
+    if (act == 1) return t > 0.0f ? t : 0.0f;
+    return t;
+}
+
+// The wave's (TM*32) x (TN*32) accumulator tile goes through LDS so every lane stores whole float4 row pieces;
+// all residual loads are issued at once (the memory-bound 1x1 layers).  Same scheme as bev_conv.hip's epilogue.
+template <int TM, int TN>
+__device__ __forceinline__ void x6_epilogue(const ConvX &a, float *lds, const f32x16 (&acc)[TM][TN], int wave,
+                                            int lane, int wn, int wm, int64_t m0, int n0) {
+    const int r32 = lane & 31, h = lane >> 5;
+    constexpr int WR = TM * 32, WC = TN * 32, ER = WC + 4;
+    constexpr int C4 = WC / 4, RPI = 64 / C4, NQ = WR / RPI;
+    __syncthreads();  // every wave is done with the staging buffers
+    float *E = lds + wave * (WR * ER);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) E[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
+    const int c4 = lane % C4, rq = lane / C4;
+    const int n = n0 + wn * WC + c4 * 4;
+    const bool nvec = ((a.Co & 3) == 0) && ((a.ldy & 3) == 0) && (n + 3 < a.Co);
+    const int64_t mbase = m0 + wm * WR;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.bias) {
+        if (nvec) bv = *(const float4 *)(a.bias + n);
+        else {
+            bv.x = n < a.Co ? a.bias[n] : 0.f;
+            bv.y = n + 1 < a.Co ? a.bias[n + 1] : 0.f;
+            bv.z = n + 2 < a.Co ? a.bias[n + 2] : 0.f;
+            bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
+        }
+    }
+    float4 rv[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int64_t m = mbase + rq + RPI * q;
+        rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int row = rq + RPI * q;
+        const int64_t m = mbase + row;
+        if (m >= a.M) continue;
+        const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
+        float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
+        float *yp = a.y + m * a.ldy + n;
+        if (nvec) {
+            if (a.res) {
+                o[0] += rv[q].x;
+                o[1] += rv[q].y;
+                o[2] += rv[q].z;
+                o[3] += rv[q].w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u] = act_x(o[u], a.act);
+            *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (n + u >= a.Co) break;
+                float t = o[u];
+                if (a.res) t += a.res[m * a.Co + n + u];
+                yp[u] = act_x(t, a.act);
+            }
+        }
+    }
+}
+
+template <int WM, int WN, int TM, int TN, bool DUAL>
+__global__ __launch_bounds__(256, 2) void k_conv_x6(ConvX a) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int APL = BM * XROW, BPL = BN * XROW;  // bf16 per operand plane
+    constexpr int STAGE = 3 * (APL + BPL);            // bf16 per LDS stage
+    constexpr int AQ = BM / 64;                       // A float4 per thread and K step: rows tid / 4 + 64 q
+    // B staging: the step's BN rows x 96 B in pieces of PB bytes (16, or 8 when 16-B pieces do not divide evenly
+    // over the 256 threads), BQ whole pieces per thread -- no conditional loads
+    constexpr int PB = ((BN * 6) % 256 == 0) ? 16 : 8;
+    constexpr int PPR = 96 / PB;  // pieces per row
+    constexpr int BQ = BN * PPR / 256;
+    static_assert(BN * PPR % 256 == 0, "B pieces per thread");
+    typedef typename std::conditional<PB == 16, u32x4, u32x2>::type bpiece;  // native vectors stay in VGPRs
+    constexpr int EPIB = 4 * (TM * 32) * (TN * 32 + 4) * 4;
+    constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
+    static_assert(BM % 64 == 0, "A staging rows");
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
+    __bf16 *lds = (__bf16 *)lds_raw;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int n_tiles = (a.Co + BN - 1) / BN;
+    unsigned bid = blockIdx.x;
+    {  // XCD-aware order: the n_tiles blocks reading the same A rows run on one XCD (shared L2)
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int64_t m0 = (int64_t)(bid / n_tiles) * BM;
+    const int n0 = (bid % n_tiles) * BN;
+
+    // A staging rows: (tid >> 2) + 64 q, channel quad aq of the 16-channel K step
+    const int aq = tid & 3;
+    int64_t pb[AQ], p2[AQ];
+    int iy0[AQ], ix0[AQ];
+    bool rok[AQ];
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) {
+        const int64_t m = m0 + (tid >> 2) + 64 * q;
+        rok[q] = m < a.M;
+        const int64_t mm = rok[q] ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int64_t n = t / a.Ho;
+        if (DUAL) {
+            pb[q] = mm * a.Ci + 4 * aq;
+            p2[q] = ((n * a.H2 + (int64_t)oy * a.stride2) * a.W2 + (int64_t)ox * a.stride2) * a.Ci2 + 4 * aq;
+            iy0[q] = ix0[q] = 0;
+        } else {
+            pb[q] = n * a.H * a.W * a.Ci + 4 * aq;
+            p2[q] = 0;
+            iy0[q] = oy * a.stride - a.pad;
+            ix0[q] = ox * a.stride - a.pad;
+        }
+    }
+    const int64_t bstep = 3 * XBK;  // bf16 per (row, K step) of the panel
+    const __bf16 *brow[BQ];
+    int bdst[BQ];  // LDS offset (bf16) of the piece inside the B part of a stage
+#pragma unroll
+    for (int i = 0; i < BQ; ++i) {
+        const int pc = tid + 256 * i;
+        const int row = pc / PPR, byte = (pc % PPR) * PB;
+        brow[i] = a.wp + (int64_t)(n0 + row) * (a.Kp / XBK) * bstep + byte / 2;
+        bdst[i] = (byte / 32) * BPL + row * XROW + (byte % 32) / 2;
+    }
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+
+    f32x4 va0[AQ], va1[AQ];
+    bpiece vb0[BQ], vb1[BQ];
+    int ky = 0, kx = 0, ci0 = 0, k0 = 0;  // tap / channel (or dual k) of the step being loaded
+    int64_t kb = 0;                       // bf16 offset of that step in a panel row
+#define X6_GLOAD(VA, VB)                                                                                   \
+    do {                                                                                                   \
+        if (DUAL) {                                                                                        \
+            const bool first = k0 < a.Ci;                                                                  \
+            const float *src = first ? a.x + k0 : a.x2 + (k0 - a.Ci);                                      \
+            _Pragma("unroll") for (int q = 0; q < AQ; ++q) VA[q] =                                         \
+                *(const f32x4 *)(rok[q] ? src + (first ? pb[q] : p2[q]) : g_xzero4);                      \
+            k0 += XBK;                                                                                     \
+        } else {                                                                                           \
+            const int dy = ky * a.dil, dx = kx * a.dil;                                                    \
+            _Pragma("unroll") for (int q = 0; q < AQ; ++q) {                                               \
+                const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
+                const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
+                VA[q] = *(const f32x4 *)(in ? a.x + pb[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 : g_xzero4); \
+            }                                                                                              \
+            ci0 += XBK;                                                                                    \
+            if (ci0 == a.Ci) {                                                                             \
+                ci0 = 0;                                                                                   \
+                if (++kx == a.KW) {                                                                        \
+                    kx = 0;                                                                                \
+                    ++ky;                                                                                  \
+                }                                                                                          \
+            }                                                                                              \
+        }                                                                                                  \
+        _Pragma("unroll") for (int i = 0; i < BQ; ++i) VB[i] = *(const bpiece *)(brow[i] + kb);          \
+        kb += bstep;                                                                                       \
+    } while (0)
+#define X6_SWRITE(BUF, VA, VB)                                                                             \
+    do {                                                                                                   \
+        __bf16 *As = lds + (BUF) * STAGE;                                                                  \
+        __bf16 *Bs = As + 3 * APL;                                                                         \
+        _Pragma("unroll") for (int q = 0; q < AQ; ++q) {                                                   \
+            bf16x4 hv, mv, lv;                                                                             \
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                \
+                __bf16 h_, m_, l_;                                                                         \
+                split3(VA[q][e], h_, m_, l_);                                                              \
+                hv[e] = h_;                                                                                \
+                mv[e] = m_;                                                                                \
+                lv[e] = l_;                                                                                \
+            }                                                                                              \
+            __bf16 *d = As + ((tid >> 2) + 64 * q) * XROW + 4 * aq;                                        \
+            *(bf16x4 *)d = hv;                                                                             \
+            *(bf16x4 *)(d + APL) = mv;                                                                     \
+            *(bf16x4 *)(d + 2 * APL) = lv;                                                                 \
+        }                                                                                                  \
+        _Pragma("unroll") for (int i = 0; i < BQ; ++i) *(bpiece *)(Bs + bdst[i]) = VB[i];                \
+    } while (0)
+    const int r32 = lane & 31, h = lane >> 5;
+    // one 16-deep k slice: 6 MFMAs per (A tile, B tile) pair (hh, hm, mh, hl, lh, mm)
+#define X6_MFMA(BUF)                                                                                       \
+    do {                                                                                                   \
+        const __bf16 *As = lds + (BUF) * STAGE;                                                            \
+        const __bf16 *Bs = As + 3 * APL;                                                                   \
+        bf16x8 fa[TM][3], fb[TN][3];                                                                       \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                     \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
+                fa[i][p] = *(const bf16x8 *)(As + p * APL + (wm * TM * 32 + i * 32 + r32) * XROW + 8 * h); \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                                     \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
+                fb[j][p] = *(const bf16x8 *)(Bs + p * BPL + (wn * TN * 32 + j * 32 + r32) * XROW + 8 * h); \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                     \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                               \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0); \
+            }                                                                                              \
+    } while (0)
+
+    const int nk = a.Kp / XBK;
+    X6_GLOAD(va0, vb0);
+    if (nk > 1) X6_GLOAD(va1, vb1);
+    X6_SWRITE(0, va0, vb0);
+    __syncthreads();
+    // Invariant at the loop head: LDS buffer 0 holds step ks, register set 1 holds step ks + 1.
+    int ks = 0;
+    for (; ks + 3 < nk; ks += 2) {
+        X6_GLOAD(va0, vb0);  // step ks + 2
+        X6_MFMA(0);
+        X6_SWRITE(1, va1, vb1);  // step ks + 1 (buffer 1's readers passed the last barrier)
+        __syncthreads();
+        X6_GLOAD(va1, vb1);  // step ks + 3
+        X6_MFMA(1);
+        X6_SWRITE(0, va0, vb0);  // step ks + 2
+        __syncthreads();
+    }
+    if (ks + 2 < nk) {
+        X6_GLOAD(va0, vb0);
+        X6_MFMA(0);
+        X6_SWRITE(1, va1, vb1);
+        __syncthreads();
+        X6_MFMA(1);
+        X6_SWRITE(0, va0, vb0);
+        __syncthreads();
+        X6_MFMA(0);
+    } else if (ks + 1 < nk) {
+        X6_MFMA(0);
+        X6_SWRITE(1, va1, vb1);
+        __syncthreads();
+        X6_MFMA(1);
+    } else {
+        X6_MFMA(0);
+    }
+#undef X6_MFMA
+#undef X6_SWRITE
+#undef X6_GLOAD
+    x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
+}
+
+template <int WM, int WN, int TM, int TN, bool DUAL>
+int launch_x6(const ConvX &a, hipStream_t st) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
+    if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL((k_conv_x6<WM, WN, TM, TN, DUAL>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+int g_x6_tile = 0;  // 0 automatic, 1 = 128 x 128, 2 = 128 x 64
+
+template <bool DUAL>
+int dispatch_x6(const ConvX &a, hipStream_t st) {
+    const int t = g_x6_tile ? g_x6_tile : (a.Co <= 64 ? 2 : 1);
+    if (t == 2) return launch_x6<4, 1, 1, 2, DUAL>(a, st);
+    return launch_x6<2, 2, 2, 2, DUAL>(a, st);
+}
+
+}  // namespace
+
+namespace bev {
+int conv_x6_tune(int value) {
+    if (value < 0 || value > 2) return BEV_ERR_ARGS;
+    const int old = g_x6_tile;
+    g_x6_tile = value;
+    return old;
+}
+}  // namespace bev
+
+extern "C" {
+
+int64_t bev_conv_packed_size_x6(int Co, int Ci, int KH, int KW) {
+    if (Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;
+    return copad_x(Co) * kpad_x(Ci * KH * KW) * 3;
+}
+
+int bev_conv_pack_weights_x6(const float *w, int Co, int Ci, int KH, int KW, uint16_t *packed, void *stream) {
+    if (!w || !packed || Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;
+    const int64_t Kp = kpad_x(Ci * KH * KW), Cop = copad_x(Co), n = Kp * Cop;
+    hipLaunchKernelGGL(k_pack_x6, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, w, Co, Ci, KH,
+                       KW, Kp, Cop, (__bf16 *)packed);
+    return (int)hipGetLastError();
+}
+
+int bev_conv2d_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                      const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
+                      float *y, int ldy, int Ho, int Wo, void *stream) {
+    if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
+        stride <= 0 || pad < 0 || dilation <= 0 || act < 0 || act > 2 || ldy < Co)
+        return BEV_ERR_ARGS;
+    if (Ci % XBK != 0) return BEV_ERR_ARGS;  // one tap and 16 channels per K step
+    if (Ho != (H + 2 * pad - dilation * (KH - 1) - 1) / stride + 1 ||
+        Wo != (W + 2 * pad - dilation * (KW - 1) - 1) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
+    if (residual && ldy != Co) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvX a;
+    a.x = x;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.res = residual;
+    a.y = y;
+    a.N = N, a.H = H, a.W = W, a.Ci = Ci, a.Co = Co, a.KH = KH, a.KW = KW, a.stride = stride, a.pad = pad;
+    a.dil = dilation, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = ldy;
+    a.Kp = (int)kpad_x(Ci * KH * KW);
+    a.M = (int64_t)N * Ho * Wo;
+    a.x2 = nullptr;
+    a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    return dispatch_x6<false>(a, (hipStream_t)stream);
+}
+
+int bev_conv2d_dual_x6_f32(const float *x, int N, int Ho, int Wo, int Ci, const float *x2, int H2, int W2, int Ci2,
+                           int stride2, const uint16_t *packed, const float *bias, int Co, int act, float *y,
+                           void *stream) {
+    if (!x || !x2 || !packed || !y || N < 0 || Ho <= 0 || Wo <= 0 || Ci <= 0 || Ci2 <= 0 || H2 <= 0 || W2 <= 0 ||
+        stride2 <= 0 || Co <= 0 || act < 0 || act > 2)
+        return BEV_ERR_ARGS;
+    if (Ci % XBK != 0 || Ci2 % XBK != 0) return BEV_ERR_ARGS;
+    if (Ho != (H2 - 1) / stride2 + 1 || Wo != (W2 - 1) / stride2 + 1) return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvX a;
+    a.x = x;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.res = nullptr;
+    a.y = y;
+    a.N = N, a.H = Ho, a.W = Wo, a.Ci = Ci, a.Co = Co, a.KH = 1, a.KW = 1, a.stride = 1, a.pad = 0;
+    a.dil = 1, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = Co;
+    a.Kp = (int)kpad_x(Ci + Ci2);
+    a.M = (int64_t)N * Ho * Wo;
+    a.x2 = x2;
+    a.Ci2 = Ci2, a.H2 = H2, a.W2 = W2, a.stride2 = stride2;
+    return dispatch_x6<true>(a, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -89,7 +89,7 @@ class CNNEncoder(ViewEncoder):
             if self._feature_channels is None:
                 self._feature_channels = feat.shape[-1]
                 self.proj = nn.Conv2d(self._feature_channels, self.out_channels, kernel_size=1).to(feat.device)
-                self._fproj = FoldedConv(self.proj)
+                self._fproj = FoldedConv(self.proj, split_ok=True)
             if torch.is_grad_enabled() and (self.proj.weight.requires_grad or self.proj.bias.requires_grad):
                 return Proj1x1.apply(feat, self.proj.weight, self.proj.bias)  # trainable proj (BASELINE config 3)
             return self._fproj(feat, relu=False)

@@ -80,12 +80,16 @@ class FoldedConv:
 
     The cache is keyed on the parameters' storage and version counters, so an
     optimizer step or load_state_dict triggers a re-pack on the next call.
+    With `split_ok` (the ResNet trunk and the encoder proj) an NHWC conv with Ci % 16 == 0 runs in the
+    arithmetic bev_native.conv_arith() selects: "bf16x6" packs the split-bf16 panel (bev_conv2d_x6_f32), "f32"
+    the exact-f32 MFMA panel (bev_conv2d_f32).  The chained bottleneck kernels always take the fp32 panel.
     """
 
-    def __init__(self, conv: nn.Conv2d, bn: nn.BatchNorm2d = None):
+    def __init__(self, conv: nn.Conv2d, bn: nn.BatchNorm2d = None, split_ok: bool = False):
         self.conv, self.bn = conv, bn
-        self._key = None
-        self.packed = self.bias = None
+        self.split_ok = split_ok
+        self._keys = {}
+        self.packed = self.packed6 = self.bias = None
 
     def _tensors(self):
         ts = [self.conv.weight] + ([self.conv.bias] if self.conv.bias is not None else [])
@@ -93,15 +97,26 @@ class FoldedConv:
             ts += [self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var]
         return ts
 
-    def prepare(self, device):
+    def arith(self) -> str:
+        c = self.conv
+        if (self.split_ok and _nat.conv_arith() == "bf16x6" and c.in_channels % 16 == 0 and c.groups == 1
+                and c.dilation == (1, 1)):
+            return "bf16x6"
+        return "f32"
+
+    def prepare(self, device, arith: str = None):
+        arith = arith or self.arith()
         key = tuple((t.data_ptr(), t._version) for t in self._tensors()) + (str(device),)
-        if key == self._key:
+        if self._keys.get(arith) == key:
             return
         w, b = self.folded(device)
         with torch.no_grad():
-            self.packed = _nat.pack_conv_weight(w.contiguous())
+            if arith == "bf16x6":
+                self.packed6 = _nat.pack_conv_weight_x6(w.contiguous())
+            else:
+                self.packed = _nat.pack_conv_weight(w.contiguous())
             self.bias = b.contiguous().float()
-        self._key = key
+        self._keys[arith] = key
 
     def folded(self, device):
         """(w OIHW, b) with eval BN folded in, on `device`."""
@@ -117,11 +132,12 @@ class FoldedConv:
         return w, b
 
     def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False, ascale=None, out=None):
-        self.prepare(x.device)
+        arith = "f32" if (in_nchw or ascale is not None) else self.arith()
+        self.prepare(x.device, arith)
         c = self.conv
-        return _nat.conv2d_nhwc(x, self.packed, self.bias, c.out_channels, c.kernel_size[0], c.kernel_size[1],
-                                c.stride[0], c.padding[0], relu, residual=residual, in_nchw=in_nchw, ascale=ascale,
-                                out=out)
+        return _nat.conv2d_nhwc(x, self.packed6 if arith == "bf16x6" else self.packed, self.bias, c.out_channels,
+                                c.kernel_size[0], c.kernel_size[1], c.stride[0], c.padding[0], relu,
+                                residual=residual, in_nchw=in_nchw, ascale=ascale, out=out)
 
 
 class FoldedTail:
@@ -135,8 +151,8 @@ class FoldedTail:
 
     def __init__(self, main: FoldedConv, short: FoldedConv):
         self.main, self.short = main, short
-        self._key = None
-        self.packed = self.bias = None
+        self._keys = {}
+        self.packed = self.packed6 = self.bias = None
 
     @staticmethod
     def applies(blk) -> bool:
@@ -146,22 +162,31 @@ class FoldedTail:
                 and ds[0].padding == (0, 0) and c3.kernel_size == (1, 1) and c3.stride == (1, 1)
                 and c3.in_channels % 32 == 0 and ds[0].in_channels % 32 == 0 and ds[0].bias is None)
 
-    def prepare(self, device):
+    def arith(self) -> str:
+        return "bf16x6" if self.main.arith() == "bf16x6" and self.short.arith() == "bf16x6" else "f32"
+
+    def prepare(self, device, arith: str = None):
+        arith = arith or self.arith()
         key = tuple((t.data_ptr(), t._version) for f in (self.main, self.short) for t in f._tensors()) + (str(device),)
-        if key == self._key:
+        if self._keys.get(arith) == key:
             return
         w1, b1 = self.main.folded(device)
         w2, b2 = self.short.folded(device)
         with torch.no_grad():
             w = torch.cat([w1.reshape(w1.shape[0], -1), w2.reshape(w2.shape[0], -1)], 1)
-            self.packed = _nat.pack_conv_weight(w.reshape(w.shape[0], w.shape[1], 1, 1).contiguous())
+            w = w.reshape(w.shape[0], w.shape[1], 1, 1).contiguous()
+            if arith == "bf16x6":
+                self.packed6 = _nat.pack_conv_weight_x6(w)
+            else:
+                self.packed = _nat.pack_conv_weight(w)
             self.bias = (b1 + b2).contiguous().float()
-        self._key = key
+        self._keys[arith] = key
 
     def __call__(self, h, x, out=None):
-        self.prepare(h.device)
-        return _nat.conv2d_dual_nhwc(h, x, self.short.conv.stride[0], self.packed, self.bias,
-                                     self.main.conv.out_channels, relu=True, out=out)
+        arith = self.arith()
+        self.prepare(h.device, arith)
+        return _nat.conv2d_dual_nhwc(h, x, self.short.conv.stride[0], self.packed6 if arith == "bf16x6" else self.packed,
+                                     self.bias, self.main.conv.out_channels, relu=True, out=out)
 
 
 class FoldedChain:
@@ -185,8 +210,8 @@ class FoldedChain:
                 and c3.out_channels % 128 == 0)
 
     def prepare(self, device):
-        self.c2.prepare(device)
-        self.c3.prepare(device)
+        self.c2.prepare(device, "f32")
+        self.c3.prepare(device, "f32")
 
     def __call__(self, h, x, out=None):
         self.prepare(h.device)
@@ -217,8 +242,8 @@ class FoldedChainTail:
                 and blk.conv3.out_channels % 128 == 0)
 
     def prepare(self, device):
-        self.c2.prepare(device)
-        self.tail.prepare(device)
+        self.c2.prepare(device, "f32")
+        self.tail.prepare(device, "f32")
 
     def __call__(self, h, x, out=None):
         self.prepare(h.device)
@@ -282,7 +307,7 @@ class ResNet(nn.Module):
     def _fc(self, conv, bn):
         k = id(conv)
         if k not in self._folded:
-            self._folded[k] = FoldedConv(conv, bn)
+            self._folded[k] = FoldedConv(conv, bn, split_ok=True)
         return self._folded[k]
 
     def unexecuted_parameter_names(self, out_index: int):
@@ -416,10 +441,13 @@ class ResNet(nn.Module):
         return self._folded[k]
 
     def _block_plan(self, blk):
-        """(kind, folded executors) of one residual block on the eval path."""
-        if isinstance(blk, Bottleneck) and self.fuse_chain and FoldedChain.applies(blk):
+        """(kind, folded executors) of one residual block on the eval path.  The chained kernels are exact-f32
+        MFMA kernels: with the split-bf16 arithmetic (bev_native.conv_arith() == "bf16x6") the block runs as
+        separate split-bf16 launches (conv1, conv2, conv3 + shortcut as one dual GEMM) instead."""
+        chains = self.fuse_chain and _nat.conv_arith() == "f32"
+        if isinstance(blk, Bottleneck) and chains and FoldedChain.applies(blk):
             return "chain", [self._fc(blk.conv1, blk.bn1), self._chain(blk)]
-        if isinstance(blk, Bottleneck) and self.fuse_chain and self.fuse_shortcut and FoldedChainTail.applies(blk):
+        if isinstance(blk, Bottleneck) and chains and self.fuse_shortcut and FoldedChainTail.applies(blk):
             k = ("chaintail", id(blk))
             if k not in self._folded:
                 self._folded[k] = FoldedChainTail(self._fc(blk.conv2, blk.bn2), self._tail(blk))
