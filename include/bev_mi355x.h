@@ -54,7 +54,9 @@ int bev_abi_version(void);
  *   1 (default) = the 64-column output tiles, 2 = every tile, 0 = none (through registers); same
  *   results bit for bit.
  * BEV_TUNE_CONV_X6_TILE: output tile of the split-bf16 fp32 convs (bev_conv2d_x6_f32 / _dual_x6_f32):
- *   0 = automatic, 1 = 128x128, 2 = 128x64. */
+ *   0 = automatic, 1 = 128x128, 2 = 128x64.
+ * BEV_TUNE_CONV_X6_KERNEL: 0 (default) = 32-deep K steps with B fragments read straight from the panel when
+ *   Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel for every shape.  Same results bit for bit. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -64,6 +66,7 @@ int bev_abi_version(void);
 #define BEV_TUNE_WGRAD_MFMA 8
 #define BEV_TUNE_CONV_DMA 9
 #define BEV_TUNE_CONV_X6_TILE 10
+#define BEV_TUNE_CONV_X6_KERNEL 11
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------
@@ -324,20 +327,28 @@ int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const fl
  * their matrix-core rate.  Summation order differs from bev_conv2d_f32: fp32-tolerance equal, not bitwise.
  * ------------------------------------------------------------------------- */
 
-/* host: number of bf16 elements of a split weight panel ([Co pad 128][K pad 16 / 16][3][16]). */
+/* host: number of bf16 elements of a split weight panel (MFMA fragment order: [Co pad 128 / 32][K pad 16 / 16]
+ * [3 planes][64 lanes][8]). */
 int64_t bev_conv_packed_size_x6(int Co, int Ci, int KH, int KW);
 
 /* device: OIHW fp32 weights -> split bf16 panel (k = (ky*KW + kx)*Ci + ci), packed [size] uint16 storage. */
 int bev_conv_pack_weights_x6(const float *w, int Co, int Ci, int KH, int KW, uint16_t *packed, void *stream);
 
 /* device: y[m][n] (row pitch ldy) = act(sum_k x[m][k] * w[n][k] + bias[n] (+ residual[m][n])) in fp32 through the
- * split panel; NHWC x [N][H][W][Ci] fp32 with Ci % 16 == 0, 16-B aligned; stride / pad / dilation as
- * bev_conv2d_nhwc_ex_f32; act 0 none, 1 ReLU, 2 SiLU; bias / residual may be NULL (residual needs ldy == Co).
- * Replaces the nn.Conv2d (+ folded eval BN) layers of the timm trunk and the lazy 1x1 projection
- * (cnn_encoder.py:26,41-46) -- the same contract as bev_conv2d_f32 for NHWC inputs. */
-int bev_conv2d_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
-                      const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
-                      float *y, int ldy, int Ho, int Wo, void *stream);
+ * split panel; NHWC x [N][H][W][Ci] fp32 with Ci % 16 == 0, 16-B aligned -- or, with x NULL, the operand already
+ * split: xs [3][N][H][W][Ci] bf16 planes (h, m, l as bev_split3_f32 / a split output writes them; Ci % 32 == 0);
+ * stride / pad / dilation as bev_conv2d_nhwc_ex_f32; act 0 none, 1 ReLU, 2 SiLU; bias / residual may be NULL
+ * (residual needs ldy == Co).  Output fp32 y, or, with y NULL, the result split into ys [3][N][Ho][Wo][Co] bf16
+ * planes (ldy == Co, Co % 4 == 0) -- the pre-split operand of the next conv.  Replaces the nn.Conv2d (+ folded
+ * eval BN) layers of the timm trunk and the lazy 1x1 projection (cnn_encoder.py:26,41-46) -- the contract of
+ * bev_conv2d_f32 for NHWC inputs. */
+int bev_conv2d_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, int Ci, const uint16_t *packed,
+                      const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
+                      int dilation, int act, float *y, uint16_t *ys, int ldy, int Ho, int Wo, void *stream);
+
+/* device: split n fp32 values into planes [3][n] bf16 with x == h + m + l exactly (the operand format of
+ * bev_conv2d_x6_f32's xs). */
+int bev_split3_f32(const float *x, int64_t n, uint16_t *planes, void *stream);
 
 /* device: bev_conv2d_dual_f32 (bottleneck conv3 + downsample shortcut as one GEMM over K = [x | x2[::s2]]) through
  * the split panel of the concatenated [Co][Ci + Ci2] weights; Ci, Ci2 % 16 == 0; act as above. */

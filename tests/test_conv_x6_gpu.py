@@ -85,17 +85,42 @@ def test_x6_conv_fp32_accuracy_vs_float64(case):
 
 
 def test_x6_tiles_bit_identical():
-    """Both output tiles (BEV_TUNE_CONV_X6_TILE 1 = 128x128, 2 = 128x64) sum every output in the same K order."""
+    """Both output tiles (BEV_TUNE_CONV_X6_TILE 1 = 128x128, 2 = 128x64) and both kernels (BEV_TUNE_CONV_X6_KERNEL:
+    32-deep steps with B from the panel, 16-deep steps with B through LDS) sum every output in the same K order."""
     N, H, W, Ci, Co = 2, 19, 29, 64, 192
     x, w, b = _case(N, H, W, Ci, Co, 3, 5)
     xd, bd = _nhwc(x.float()).to(DEV), b.float().to(DEV)
     p6 = nat.pack_conv_weight_x6(w.float().to(DEV))
     outs = []
     for t in (1, 2):
-        with nat.tuned(CONV_X6_TILE=t):
-            outs.append(nat.conv2d_nhwc_x6(xd, p6, bd, Co, 3, 3, 1, 1, 1, 1))
+        for kern in (0, 1):
+            with nat.tuned(CONV_X6_TILE=t, CONV_X6_KERNEL=kern):
+                outs.append(nat.conv2d_nhwc_x6(xd, p6, bd, Co, 3, 3, 1, 1, 1, 1))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+
+
+@pytest.mark.parametrize("Ci,Co,K,stride,tile", [(64, 64, 3, 1, 0), (128, 128, 3, 2, 0), (64, 192, 3, 1, 1),
+                                                  (64, 192, 3, 1, 2), (32, 64, 1, 1, 0)])
+def test_x6_split_operand_bit_identical(Ci, Co, K, stride, tile):
+    """Pre-split operand planes (bev_split3_f32 -> k_conv_x6s, LDS-DMA staging) give bit-for-bit the result of the
+    fp32 operand split in-kernel, and a split output (ys) holds exactly the split of the fp32 output."""
+    N, H, W = 2, 23, 35
+    x, w, b = _case(N, H, W, Ci, Co, K, 77 + Ci)
+    xd, bd = _nhwc(x.float()).to(DEV), b.float().to(DEV)
+    p6 = nat.pack_conv_weight_x6(w.float().to(DEV))
+    pad = K // 2
+    xs = nat.split3(xd)
+    assert torch.equal(xs.to_float(), xd)  # exact split
+    with nat.tuned(CONV_X6_TILE=tile):
+        ref = nat.conv2d_nhwc_x6(xd, p6, bd, Co, K, K, stride, pad, 1, 1)
+        got = nat.conv2d_nhwc_x6(xs, p6, bd, Co, K, K, stride, pad, 1, 1)
+        ys = nat.conv2d_nhwc_x6(xs, p6, bd, Co, K, K, stride, pad, 1, 1, split_out=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(ys.to_float(), ref)
+    assert torch.equal(ys.planes, nat.split3(ref).planes)
 
 
 @pytest.mark.parametrize("stride2,Ci,Ci2,Co", [(1, 64, 64, 256), (2, 128, 256, 512)])

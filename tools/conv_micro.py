@@ -18,6 +18,7 @@ import bev_native as nat  # noqa: E402
 
 N = 7
 ARITH = "f32"  # --arith: panel of the plain / dual layers (bf16x6 = the split-bf16 kernels)
+SPLIT_IN = False  # --split-in: bf16x6 layers read pre-split operand planes
 # name: (Ci, Co, k, stride, H_in, W_in, residual, nchw_in)
 LAYERS = {
     "stem": (3, 64, 7, 2, 1080, 1920, False, True),
@@ -140,6 +141,8 @@ def run(name, iters):
     b = torch.randn(Co, device=dev, generator=g)
     r = torch.randn(N, Ho, Wo, Co, device=dev, generator=g) if res else None
     packed = nat.pack_conv_weight_x6(w) if (ARITH == "bf16x6" and not nchw) else nat.pack_conv_weight(w)
+    if SPLIT_IN and ARITH == "bf16x6" and not nchw and Ci % 32 == 0:
+        x = nat.split3(x)  # pre-split operand planes (k_conv_x6s)
     out = torch.empty(N, Ho, Wo, Co, device=dev)
     for _ in range(3):
         nat.conv2d_nhwc(x, packed, b, Co, k, k, s, p, True, residual=r, in_nchw=nchw, out=out)
@@ -151,7 +154,7 @@ def run(name, iters):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     flops = 2 * N * Ho * Wo * Co * Ci * k * k
-    byts = 4 * (x.numel() + out.numel() + (r.numel() if res else 0))
+    byts = 4 * (N * H * W * Ci + out.numel() + (r.numel() if res else 0))
     print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
 
 
@@ -163,9 +166,11 @@ def main():
     ap.add_argument("--values", type=int, nargs="*", default=[0], help="knob values, interleaved per round")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--arith", choices=("f32", "bf16x6"), default="f32")
+    ap.add_argument("--split-in", action="store_true")
     a = ap.parse_args()
-    global ARITH
+    global ARITH, SPLIT_IN
     ARITH = a.arith
+    SPLIT_IN = a.split_in
     knob = getattr(nat, "TUNE_" + a.knob)
     for rnd in range(a.rounds):  # interleaved rounds, same process
         for v in a.values:

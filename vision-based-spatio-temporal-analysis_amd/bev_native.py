@@ -97,7 +97,9 @@ SIGNATURES = {
     "bev_conv_wgrad_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv_packed_size_x6": (_i64, [_i, _i, _i, _i]),
     "bev_conv_pack_weights_x6": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
-    "bev_conv2d_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
+    "bev_conv2d_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _i,
+                               _vp]),
+    "bev_split3_f32": (_i, [_vp, _i64, _vp, _vp]),
     "bev_conv2d_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
 }
 
@@ -171,6 +173,7 @@ TUNE_CONV_NBUF = 7
 TUNE_WGRAD_MFMA = 8
 TUNE_CONV_DMA = 9
 TUNE_CONV_X6_TILE = 10
+TUNE_CONV_X6_KERNEL = 11
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 
@@ -446,27 +449,72 @@ def pack_conv_weight_x6(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def conv2d_nhwc_x6(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
-                   dilation: int = 1, act: int = 0, residual: torch.Tensor = None, out: torch.Tensor = None):
-    """fp32 conv through the split-bf16 panel (bev_conv2d_x6_f32): x [N,H,W,Ci] fp32 NHWC, Ci % 16 == 0 -> y
-    [N,Ho,Wo,Co] fp32 (or the first Co channels of a wider NHWC `out`)."""
+class Split3:
+    """An fp32 NHWC activation held split into three bf16 planes (planes [3, N, H, W, C] bf16, x == h + m + l
+    exactly): the pre-split operand format of bev_conv2d_x6_f32 (xs / ys)."""
+
+    def __init__(self, planes: torch.Tensor):
+        assert planes.dtype == torch.bfloat16 and planes.dim() == 5 and planes.shape[0] == 3
+        self.planes = planes
+
+    @property
+    def shape(self):
+        return tuple(self.planes.shape[1:])
+
+    @property
+    def device(self):
+        return self.planes.device
+
+    def to_float(self) -> torch.Tensor:
+        p = self.planes.float()
+        return (p[0] + p[1]) + p[2]
+
+
+def split3(x: torch.Tensor) -> Split3:
+    """fp32 tensor [N, H, W, C] -> Split3 (bev_split3_f32)."""
     x = x.contiguous()
-    _require_gpu(x, bias, residual)
+    _require_gpu(x)
+    out = torch.empty((3,) + tuple(x.shape), device=x.device, dtype=torch.bfloat16)
+    _check(lib().bev_split3_f32(_ptr(x), x.numel(), _ptr(out), _stream(x)), "bev_split3_f32")
+    return Split3(out)
+
+
+def conv2d_nhwc_x6(x, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
+                   dilation: int = 1, act: int = 0, residual: torch.Tensor = None, out: torch.Tensor = None,
+                   split_out: bool = False):
+    """fp32 conv through the split-bf16 panel (bev_conv2d_x6_f32): x [N,H,W,Ci] fp32 NHWC (Ci % 16 == 0) or a
+    Split3 (Ci % 32 == 0) -> y [N,Ho,Wo,Co] fp32 (or the first Co channels of a wider NHWC `out`), or a Split3
+    with split_out."""
+    xs = x if isinstance(x, Split3) else None
+    if xs is None:
+        x = x.contiguous()
+        _require_gpu(x)
+    _require_gpu(bias, residual)
     if not packed.is_cuda or packed.dtype != torch.bfloat16:
         raise HipError("conv2d_nhwc_x6 needs the split-bf16 weight panel on the device")
     N, H, W, Ci = x.shape
+    dev = x.device
     Ho, Wo = (H + 2 * pad - dilation * (KH - 1) - 1) // stride + 1, (W + 2 * pad - dilation * (KW - 1) - 1) // stride + 1
-    if out is None:
-        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
-    assert out.shape[:3] == (N, Ho, Wo) and out.shape[3] >= Co and out.is_contiguous() and out.dtype == torch.float32
+    ys = None
+    if split_out:
+        assert out is None
+        ys = torch.empty(3, N, Ho, Wo, Co, device=dev, dtype=torch.bfloat16)
+        ldy = Co
+    else:
+        if out is None:
+            out = torch.empty(N, Ho, Wo, Co, device=dev, dtype=torch.float32)
+        assert out.shape[:3] == (N, Ho, Wo) and out.shape[3] >= Co and out.is_contiguous() and out.dtype == torch.float32
+        ldy = out.shape[3]
     if residual is not None:
         residual = residual.contiguous()
-        assert residual.shape == (N, Ho, Wo, Co) and out.shape[3] == Co
-    with _span("conv", x):
-        rc = lib().bev_conv2d_x6_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co, KH, KW,
-                                     stride, pad, dilation, int(act), _ptr(out), out.shape[3], Ho, Wo, _stream(x))
+        assert residual.shape == (N, Ho, Wo, Co) and ldy == Co
+    with _span("conv", xs.planes if xs is not None else x):
+        rc = lib().bev_conv2d_x6_f32(None if xs is not None else _ptr(x), _ptr(xs.planes) if xs is not None else None,
+                                     N, H, W, Ci, _ptr(packed), _ptr(bias), _ptr(residual), Co, KH, KW, stride, pad,
+                                     dilation, int(act), _ptr(out), _ptr(ys), ldy, Ho, Wo,
+                                     _stream(xs.planes if xs is not None else x))
     _check(rc, "bev_conv2d_x6_f32")
-    return out
+    return Split3(ys) if split_out else out
 
 
 def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
@@ -475,11 +523,11 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
     """x: [N,H,W,Ci] NHWC (or [N,Ci,H,W] with in_nchw) -> y [N,Ho,Wo,Co] NHWC.
     ascale [N, Ci]: per-image input-channel multiplier applied in the operand load (SE excitation).
     The kernel follows the panel: fp32 (bev_conv2d_f32), split bf16 (bev_conv2d_x6_f32), fp16 (autocast)."""
-    x = x.contiguous()
     if packed.dtype == torch.bfloat16:
         if ascale is not None or in_nchw:
             raise HipError("the split-bf16 conv takes NHWC inputs without an operand channel scale")
         return conv2d_nhwc_x6(x, packed, bias, Co, KH, KW, stride, pad, 1, int(relu), residual=residual, out=out)
+    x = x.contiguous()
     if packed.dtype == torch.float16:  # autocast(float16): the fp16 matrix-core kernel
         if ascale is not None:
             raise HipError("the fp16 conv takes no operand channel scale (the SE gate is applied apart in training)")

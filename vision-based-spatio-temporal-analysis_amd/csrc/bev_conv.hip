@@ -1288,7 +1288,7 @@ int bev_tune(int knob, int value) {
         return old;
     }
     if (knob == BEV_TUNE_WGRAD_MFMA) return bev::train_tune(knob, value);
-    if (knob == BEV_TUNE_CONV_X6_TILE) return bev::conv_x6_tune(value);
+    if (knob == BEV_TUNE_CONV_X6_TILE || knob == BEV_TUNE_CONV_X6_KERNEL) return bev::conv_x6_tune(knob, value);
     return bev::warp_tune(knob, value);
 }
 

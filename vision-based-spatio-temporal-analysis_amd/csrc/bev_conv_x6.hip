@@ -56,7 +56,13 @@ __device__ __forceinline__ void split3(float v, __bf16 &h, __bf16 &m, __bf16 &l)
     l = (__bf16)(r - (float)m);
 }
 
-// OIHW fp32 -> [Co_pad][K_pad / 16][plane h, m, l][16] bf16, k = (ky*KW + kx)*Ci + ci
+// OIHW fp32 -> split panel in MFMA B-fragment order: [Co_pad / 32][K_pad / 16][plane h, m, l][lane 64][8] bf16,
+// lane l of the (32-column block, 16-deep slice, plane) fragment holds W[32 cb + (l & 31)][16 s + 8 (l >> 5) + j],
+// j = 0..7 -- one coalesced 1-KiB load per wave and fragment (k = (ky*KW + kx)*Ci + ci).
+__host__ __device__ inline int64_t frag_index(int n, int k, int p, int64_t S) {
+    return (((int64_t)(n >> 5) * S + (k >> 4)) * 3 + p) * 512 + (((k >> 3) & 1) * 32 + (n & 31)) * 8 + (k & 7);
+}
+
 __global__ void k_pack_x6(const float *__restrict__ w, int Co, int Ci, int KH, int KW, int64_t Kp, int64_t Cop,
                           __bf16 *__restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -71,10 +77,10 @@ __global__ void k_pack_x6(const float *__restrict__ w, int Co, int Ci, int KH, i
     }
     __bf16 h, m, l;
     split3(v, h, m, l);
-    const int64_t o = ((int64_t)n * (Kp / XBK) + k / XBK) * (3 * XBK) + k % XBK;
-    out[o] = h;
-    out[o + XBK] = m;
-    out[o + 2 * XBK] = l;
+    const int64_t S = Kp / XBK;
+    out[frag_index(n, k, 0, S)] = h;
+    out[frag_index(n, k, 1, S)] = m;
+    out[frag_index(n, k, 2, S)] = l;
 }
 
 struct ConvX {
@@ -88,6 +94,10 @@ struct ConvX {
     // dual-source 1x1: k in [Ci, Ci + Ci2) reads x2 [N][H2][W2][Ci2] at (oy*stride2, ox*stride2)
     const float *__restrict__ x2;
     int Ci2, H2, W2, stride2;
+    // pre-split operand / output planes: xs [3][N][H][W][Ci], ys [3][M][Co] bf16 (plane strides xps / yps)
+    const __bf16 *__restrict__ xs;
+    __bf16 *__restrict__ ys;
+    int64_t xps, yps;
 };
 
 __device__ __forceinline__ float act_x(float t, int act) {
@@ -140,6 +150,26 @@ __device__ __forceinline__ void x6_epilogue(const ConvX &a, float *lds, const f3
         if (m >= a.M) continue;
         const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
         float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
+        if (a.ys) {  // split output planes (the next conv's pre-split operand); ldy == Co, Co % 4 == 0
+            if (a.res) {
+                const float4 rr = rv[q];
+                o[0] += rr.x, o[1] += rr.y, o[2] += rr.z, o[3] += rr.w;
+            }
+            bf16x4 hv, mv, lv;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                __bf16 h_, m_, l_;
+                split3(act_x(o[u], a.act), h_, m_, l_);
+                hv[u] = h_, mv[u] = m_, lv[u] = l_;
+            }
+            __bf16 *yp = a.ys + m * a.Co + n;
+            if (n < a.Co) {
+                *(bf16x4 *)yp = hv;
+                *(bf16x4 *)(yp + a.yps) = mv;
+                *(bf16x4 *)(yp + 2 * a.yps) = lv;
+            }
+            continue;
+        }
         float *yp = a.y + m * a.ldy + n;
         if (nvec) {
             if (a.res) {
@@ -219,15 +249,16 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6(ConvX a) {
             ix0[q] = ox * a.stride - a.pad;
         }
     }
-    const int64_t bstep = 3 * XBK;  // bf16 per (row, K step) of the panel
+    const int64_t bstep = 3 * 512;  // bf16 per 16-deep slice of a 32-column block (fragment-order panel)
     const __bf16 *brow[BQ];
     int bdst[BQ];  // LDS offset (bf16) of the piece inside the B part of a stage
 #pragma unroll
     for (int i = 0; i < BQ; ++i) {
         const int pc = tid + 256 * i;
-        const int row = pc / PPR, byte = (pc % PPR) * PB;
-        brow[i] = a.wp + (int64_t)(n0 + row) * (a.Kp / XBK) * bstep + byte / 2;
-        bdst[i] = (byte / 32) * BPL + row * XROW + (byte % 32) / 2;
+        const int row = pc / PPR, byte = (pc % PPR) * PB;  // byte of the row's 96-B (plane, 16 k) run
+        const int pl = byte / 32, hk = (byte % 32) / 16, sub = (byte % 16) / 2;
+        brow[i] = a.wp + frag_index(n0 + row, 8 * hk, pl, a.Kp / XBK) + sub;
+        bdst[i] = pl * BPL + row * XROW + 8 * hk + sub;
     }
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -350,6 +381,382 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6(ConvX a) {
     x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
 }
 
+// ---------------------------------------------------------------------------
+// k_conv_x6b: Ci % 32 == 0 (every ResNet trunk layer).  K step 32 (two 16-deep slices, 48 MFMAs per wave and
+// step for a 64 x 64 wave tile: twice the work per barrier of k_conv_x6).  Only A goes through LDS (three bf16
+// planes, rows of 40 bf16 = 80 B = 5 odd 16-B slots: conflict-free fragment groups); the B fragments are read
+// straight from the fragment-order panel into registers (one coalesced 1-KiB load per fragment and plane), one
+// slice ahead of their MFMAs, so the LDS per stage is A's alone (30 KiB for 128 rows).
+// ---------------------------------------------------------------------------
+constexpr int YBK = 32;
+constexpr int YROW = 40;
+
+template <int WM, int WN, int TM, int TN, bool DUAL>
+__global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int APL = BM * YROW;                 // bf16 per A plane
+    constexpr int STAGE = 3 * APL;                 // bf16 per LDS stage
+    constexpr int AQ = BM / 32;                    // A float4 per thread and K step: rows tid / 8 + 32 q
+    constexpr int EPIB = 4 * (TM * 32) * (TN * 32 + 4) * 4;
+    constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
+    __bf16 *lds = (__bf16 *)lds_raw;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int n_tiles = (a.Co + BN - 1) / BN;
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int64_t m0 = (int64_t)(bid / n_tiles) * BM;
+    const int n0 = (bid % n_tiles) * BN;
+
+    const int aq = tid & 7;
+    int64_t pb[AQ], p2[AQ];
+    int iy0[AQ], ix0[AQ];
+    bool rok[AQ];
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) {
+        const int64_t m = m0 + (tid >> 3) + 32 * q;
+        rok[q] = m < a.M;
+        const int64_t mm = rok[q] ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int64_t n = t / a.Ho;
+        if (DUAL) {
+            pb[q] = mm * a.Ci + 4 * aq;
+            p2[q] = ((n * a.H2 + (int64_t)oy * a.stride2) * a.W2 + (int64_t)ox * a.stride2) * a.Ci2 + 4 * aq;
+            iy0[q] = ix0[q] = 0;
+        } else {
+            pb[q] = n * a.H * a.W * a.Ci + 4 * aq;
+            p2[q] = 0;
+            iy0[q] = oy * a.stride - a.pad;
+            ix0[q] = ox * a.stride - a.pad;
+        }
+    }
+    // B: this wave's fragments of column blocks (n0 + wn TN 32) / 32 + j; slice g of block cb, plane p at
+    // wb + (cb_rel * S + g) * 1536 + p * 512 (bf16), lane part l * 8
+    const int64_t S = a.Kp / XBK;
+    const __bf16 *wb = a.wp + ((int64_t)((n0 + wn * TN * 32) >> 5) * S) * 1536 + lane * 8;
+    const int nslice = a.Kp / XBK;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+
+    f32x4 va0[AQ], va1[AQ];
+    bf16x8 bs0[TN][3], bs1[TN][3];  // B fragments of the even / odd slices
+    int ky = 0, kx = 0, ci0 = 0, k0 = 0;
+#define X6B_GLOAD(VA)                                                                                      \
+    do {                                                                                                   \
+        if (DUAL) {                                                                                        \
+            const bool first = k0 < a.Ci;                                                                  \
+            const float *src = first ? a.x + k0 : a.x2 + (k0 - a.Ci);                                      \
+            _Pragma("unroll") for (int q = 0; q < AQ; ++q) VA[q] =                                         \
+                *(const f32x4 *)(rok[q] ? src + (first ? pb[q] : p2[q]) : g_xzero4);                      \
+            k0 += YBK;                                                                                     \
+        } else {                                                                                           \
+            const int dy = ky * a.dil, dx = kx * a.dil;                                                    \
+            _Pragma("unroll") for (int q = 0; q < AQ; ++q) {                                               \
+                const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
+                const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
+                VA[q] = *(const f32x4 *)(in ? a.x + pb[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 : g_xzero4); \
+            }                                                                                              \
+            ci0 += YBK;                                                                                    \
+            if (ci0 == a.Ci) {                                                                             \
+                ci0 = 0;                                                                                   \
+                if (++kx == a.KW) {                                                                        \
+                    kx = 0;                                                                                \
+                    ++ky;                                                                                  \
+                }                                                                                          \
+            }                                                                                              \
+        }                                                                                                  \
+    } while (0)
+#define X6B_SWRITE(BUF, VA)                                                                                \
+    do {                                                                                                   \
+        __bf16 *As = lds + (BUF) * STAGE;                                                                  \
+        _Pragma("unroll") for (int q = 0; q < AQ; ++q) {                                                   \
+            bf16x4 hv, mv, lv;                                                                             \
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                \
+                __bf16 h_, m_, l_;                                                                         \
+                split3(VA[q][e], h_, m_, l_);                                                              \
+                hv[e] = h_;                                                                                \
+                mv[e] = m_;                                                                                \
+                lv[e] = l_;                                                                                \
+            }                                                                                              \
+            __bf16 *d = As + ((tid >> 3) + 32 * q) * YROW + 4 * aq;                                        \
+            *(bf16x4 *)d = hv;                                                                             \
+            *(bf16x4 *)(d + APL) = mv;                                                                     \
+            *(bf16x4 *)(d + 2 * APL) = lv;                                                                 \
+        }                                                                                                  \
+    } while (0)
+#define X6B_BLOAD(BS, G)                                                                                   \
+    do {                                                                                                   \
+        const int g_ = (G) < nslice ? (G) : nslice - 1; /* past the end: a harmless re-read */             \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                                     \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
+                BS[j][p] = *(const bf16x8 *)(wb + ((int64_t)j * S + g_) * 1536 + p * 512);                \
+    } while (0)
+    const int r32 = lane & 31, h = lane >> 5;
+#define X6B_SLICE(AS, KK, BC)                                                                              \
+    do {                                                                                                   \
+        bf16x8 fa[TM][3];                                                                                  \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                     \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
+                fa[i][p] = *(const bf16x8 *)(AS + p * APL + (wm * TM * 32 + i * 32 + r32) * YROW + 16 * (KK) + 8 * h); \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                     \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                               \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], BC[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], BC[j][1], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], BC[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], BC[j][2], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], BC[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], BC[j][1], acc[i][j], 0, 0, 0); \
+            }                                                                                              \
+    } while (0)
+    // MFMAs of K step KS from LDS buffer BUF: slice 2 KS (B in bs0, slice 2 KS + 1 loaded meanwhile into bs1),
+    // slice 2 KS + 1 (B in bs1, the next step's slice 0 loaded into bs0)
+#define X6B_MFMA(BUF, KS)                                                                                  \
+    do {                                                                                                   \
+        const __bf16 *As = lds + (BUF) * STAGE;                                                            \
+        X6B_BLOAD(bs1, 2 * (KS) + 1);                                                                      \
+        X6B_SLICE(As, 0, bs0);                                                                             \
+        X6B_BLOAD(bs0, 2 * (KS) + 2);                                                                      \
+        X6B_SLICE(As, 1, bs1);                                                                             \
+    } while (0)
+
+    const int nk = a.Kp / YBK;
+    X6B_BLOAD(bs0, 0);
+    X6B_GLOAD(va0);
+    if (nk > 1) X6B_GLOAD(va1);
+    X6B_SWRITE(0, va0);
+    __syncthreads();
+    int ks = 0;
+    for (; ks + 3 < nk; ks += 2) {
+        X6B_GLOAD(va0);  // step ks + 2
+        X6B_MFMA(0, ks);
+        X6B_SWRITE(1, va1);  // step ks + 1
+        __syncthreads();
+        X6B_GLOAD(va1);  // step ks + 3
+        X6B_MFMA(1, ks + 1);
+        X6B_SWRITE(0, va0);  // step ks + 2
+        __syncthreads();
+    }
+    if (ks + 2 < nk) {
+        X6B_GLOAD(va0);
+        X6B_MFMA(0, ks);
+        X6B_SWRITE(1, va1);
+        __syncthreads();
+        X6B_MFMA(1, ks + 1);
+        X6B_SWRITE(0, va0);
+        __syncthreads();
+        X6B_MFMA(0, ks + 2);
+    } else if (ks + 1 < nk) {
+        X6B_MFMA(0, ks);
+        X6B_SWRITE(1, va1);
+        __syncthreads();
+        X6B_MFMA(1, ks + 1);
+    } else {
+        X6B_MFMA(0, ks);
+    }
+#undef X6B_MFMA
+#undef X6B_SLICE
+#undef X6B_BLOAD
+#undef X6B_SWRITE
+#undef X6B_GLOAD
+    x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
+}
+
+// ---------------------------------------------------------------------------
+// k_conv_x6s: A from PRE-SPLIT activation planes (xs [3][N][H][W][Ci] bf16, written split by the producing conv's
+// epilogue -- the 3x3 bottleneck conv2 reads the conv1 output it would otherwise split 9 times, once per tap)
+// staged global -> LDS by LDS-DMA (global_load_lds_dwordx4: no staging VGPRs, no ds_write, no split VALU).  One
+// DMA instruction moves 16 rows x 64 B of one plane; the 16-B chunk c of row r sits at chunk c ^ ((r >> 2) & 3),
+// so the 16-lane fragment groups (16 consecutive rows, one chunk) hit 16 distinct slots.  B fragments by buffer
+// loads from the fragment-order panel: the lane part of the address in the VGPR, the (block, slice, plane) part in
+// the SGPR soffset (no address VALU).  NHWC, Ci % 32 == 0.  Same per-output K order as k_conv_x6 / k_conv_x6b:
+// bit-identical results on the same split operands.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned lds_addr(const void *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__device__ __forceinline__ void dma16(const void *src, unsigned dst_any) {
+    const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)dst_any);  // wave-uniform LDS address
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(dst)
+        : "memory");
+}
+
+template <int WM, int WN, int TM, int TN>
+__global__ __launch_bounds__(256, 2) void k_conv_x6s(ConvX a) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    constexpr int APL = BM * 32;     // bf16 per A plane per stage (64-B rows)
+    constexpr int STAGE = 3 * APL;   // bf16 per stage
+    constexpr int RW = BM / 4;       // rows staged by each wave
+    constexpr int RG = RW / 16;      // 16-row DMA groups per wave and plane
+    constexpr int EPIB = 4 * (TM * 32) * (TN * 32 + 4) * 4;
+    constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
+    static_assert(RW % 16 == 0, "whole DMA groups per wave");
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
+    const __bf16 *lds = (const __bf16 *)lds_raw;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int n_tiles = (a.Co + BN - 1) / BN;
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int64_t m0 = (int64_t)(bid / n_tiles) * BM;
+    const int n0 = (bid % n_tiles) * BN;
+
+    // DMA rows of this lane: wave * RW + 16 g + (lane >> 2); physical chunk lane & 3 holds logical chunk
+    // (lane & 3) ^ ((row >> 2) & 3)
+    int64_t abase[RG];
+    int aiy[RG], aix[RG];
+    bool aok[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+        const int row = wave * RW + 16 * g + (lane >> 2);
+        const int lc = (lane & 3) ^ ((row >> 2) & 3);
+        const int64_t m = m0 + row;
+        aok[g] = m < a.M;
+        const int64_t mm = aok[g] ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int64_t n = t / a.Ho;
+        aiy[g] = oy * a.stride - a.pad;
+        aix[g] = ox * a.stride - a.pad;
+        abase[g] = ((n * a.H + aiy[g]) * a.W + aix[g]) * a.Ci + 8 * lc;
+    }
+    const unsigned lbase = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(lds_raw));
+    int ky = 0, kx = 0, ci0 = 0;
+    auto issue = [&](int buf) {
+        const int64_t toff = ((int64_t)ky * a.dil * a.W + kx * a.dil) * a.Ci + ci0;
+        const unsigned d0 = lbase + (unsigned)(buf * STAGE * 2) + (unsigned)(wave * RW * 64);
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+            const int iy = aiy[g] + ky * a.dil, ix = aix[g] + kx * a.dil;
+            const bool in = aok[g] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+            const __bf16 *src = a.xs + abase[g] + toff;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                dma16(in ? (const void *)(src + p * a.xps) : (const void *)g_xzero4,
+                      d0 + (unsigned)(p * APL * 2 + g * 1024));
+        }
+        ci0 += YBK;
+        if (ci0 == a.Ci) {
+            ci0 = 0;
+            if (++kx == a.KW) {
+                kx = 0;
+                ++ky;
+            }
+        }
+    };
+
+    const int S = a.Kp / XBK;  // 16-deep slices
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__bf16 *>(a.wp), 0, (int)(uint32_t)(copad_x(a.Co) / 32 * (int64_t)S * 3072), 0x00020000);
+    const int cb0 = (n0 + wn * TN * 32) >> 5;
+    const int vl = lane * 16;
+    bf16x8 bs0[TN][3], bs1[TN][3];
+#define X6S_BLOAD(BS, G)                                                                                   \
+    do {                                                                                                   \
+        const int g_ = (G) < S ? (G) : S - 1;                                                              \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                                     \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
+                BS[j][p] = __builtin_bit_cast(                                                             \
+                    bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, vl, (((cb0 + j) * S + g_) * 3 + p) * 1024, 0)); \
+    } while (0)
+    const int r32 = lane & 31, h = lane >> 5;
+#define X6S_SLICE(AS, KK, BC)                                                                              \
+    do {                                                                                                   \
+        bf16x8 fa[TM][3];                                                                                  \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i) {                                                   \
+            const int R = wm * TM * 32 + i * 32 + r32;                                                     \
+            const int ph = (2 * (KK) + h) ^ ((R >> 2) & 3);                                                \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
+                fa[i][p] = *(const bf16x8 *)(AS + p * APL + R * 32 + ph * 8);                              \
+        }                                                                                                  \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                     \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                               \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], BC[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], BC[j][1], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], BC[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], BC[j][2], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], BC[j][0], acc[i][j], 0, 0, 0); \
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], BC[j][1], acc[i][j], 0, 0, 0); \
+            }                                                                                              \
+    } while (0)
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
+    const int nk = a.Kp / YBK;
+    X6S_BLOAD(bs0, 0);
+    issue(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ks = 0; ks < nk; ++ks) {
+        const int cur = ks & 1;
+        if (ks + 1 < nk) issue(cur ^ 1);
+        const __bf16 *As = lds + cur * STAGE;
+        X6S_BLOAD(bs1, 2 * ks + 1);
+        X6S_SLICE(As, 0, bs0);
+        X6S_BLOAD(bs0, 2 * ks + 2);
+        X6S_SLICE(As, 1, bs1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step ks + 1 landed
+        __syncthreads();                                   // all of it; buffer cur is free again
+    }
+#undef X6S_SLICE
+#undef X6S_BLOAD
+    x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
+}
+
+template <int WM, int WN, int TM, int TN>
+int launch_x6s(const ConvX &a, hipStream_t st) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
+    if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL((k_conv_x6s<WM, WN, TM, TN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+}
+
+__global__ void k_split3(const float *__restrict__ x, int64_t n, __bf16 *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    __bf16 h, m, l;
+    split3(x[t], h, m, l);
+    out[t] = h;
+    out[t + n] = m;
+    out[t + 2 * n] = l;
+}
+
+template <int WM, int WN, int TM, int TN, bool DUAL>
+int launch_x6b(const ConvX &a, hipStream_t st) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
+    if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL((k_conv_x6b<WM, WN, TM, TN, DUAL>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+}
+
 template <int WM, int WN, int TM, int TN, bool DUAL>
 int launch_x6(const ConvX &a, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -360,10 +767,20 @@ int launch_x6(const ConvX &a, hipStream_t st) {
 }
 
 int g_x6_tile = 0;  // 0 automatic, 1 = 128 x 128, 2 = 128 x 64
+int g_x6_kernel = 0;  // 0 automatic (k_conv_x6b when Ci (and Ci2) % 32 == 0), 1 = k_conv_x6 (16-deep K steps)
 
 template <bool DUAL>
 int dispatch_x6(const ConvX &a, hipStream_t st) {
     const int t = g_x6_tile ? g_x6_tile : (a.Co <= 64 ? 2 : 1);
+    if (!DUAL && a.xs) {
+        if (t == 2) return launch_x6s<4, 1, 1, 2>(a, st);
+        return launch_x6s<2, 2, 2, 2>(a, st);
+    }
+    const bool wide = a.Ci % YBK == 0 && (!DUAL || a.Ci2 % YBK == 0) && g_x6_kernel == 0;
+    if (wide) {
+        if (t == 2) return launch_x6b<4, 1, 1, 2, DUAL>(a, st);
+        return launch_x6b<2, 2, 2, 2, DUAL>(a, st);
+    }
     if (t == 2) return launch_x6<4, 1, 1, 2, DUAL>(a, st);
     return launch_x6<2, 2, 2, 2, DUAL>(a, st);
 }
@@ -371,10 +788,11 @@ int dispatch_x6(const ConvX &a, hipStream_t st) {
 }  // namespace
 
 namespace bev {
-int conv_x6_tune(int value) {
-    if (value < 0 || value > 2) return BEV_ERR_ARGS;
-    const int old = g_x6_tile;
-    g_x6_tile = value;
+int conv_x6_tune(int knob, int value) {
+    int *slot = knob == BEV_TUNE_CONV_X6_TILE ? &g_x6_tile : &g_x6_kernel;
+    if (value < 0 || value > (knob == BEV_TUNE_CONV_X6_TILE ? 2 : 1)) return BEV_ERR_ARGS;
+    const int old = *slot;
+    *slot = value;
     return old;
 }
 }  // namespace bev
@@ -394,18 +812,19 @@ int bev_conv_pack_weights_x6(const float *w, int Co, int Ci, int KH, int KW, uin
     return (int)hipGetLastError();
 }
 
-int bev_conv2d_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
-                      const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
-                      float *y, int ldy, int Ho, int Wo, void *stream) {
-    if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
-        stride <= 0 || pad < 0 || dilation <= 0 || act < 0 || act > 2 || ldy < Co)
+int bev_conv2d_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, int Ci, const uint16_t *packed,
+                      const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
+                      int dilation, int act, float *y, uint16_t *ys, int ldy, int Ho, int Wo, void *stream) {
+    if ((!x == !xs) || !packed || (!y == !ys) || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 ||
+        KW <= 0 || stride <= 0 || pad < 0 || dilation <= 0 || act < 0 || act > 2 || ldy < Co)
         return BEV_ERR_ARGS;
-    if (Ci % XBK != 0) return BEV_ERR_ARGS;  // one tap and 16 channels per K step
+    if (Ci % (xs ? YBK : XBK) != 0) return BEV_ERR_ARGS;  // one tap and 16 (split input: 32) channels per K step
     if (Ho != (H + 2 * pad - dilation * (KH - 1) - 1) / stride + 1 ||
         Wo != (W + 2 * pad - dilation * (KW - 1) - 1) / stride + 1 || Ho <= 0 || Wo <= 0)
         return BEV_ERR_ARGS;
-    if ((((uintptr_t)x | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)xs | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
     if (residual && ldy != Co) return BEV_ERR_ARGS;
+    if (ys && (ldy != Co || Co % 4 != 0 || ((uintptr_t)ys & 7) != 0)) return BEV_ERR_ARGS;
     if (N == 0) return 0;
     ConvX a;
     a.x = x;
@@ -419,7 +838,19 @@ int bev_conv2d_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_
     a.M = (int64_t)N * Ho * Wo;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    a.xs = (const __bf16 *)xs;
+    a.ys = (__bf16 *)ys;
+    a.xps = (int64_t)N * H * W * Ci;
+    a.yps = a.M * Co;
     return dispatch_x6<false>(a, (hipStream_t)stream);
+}
+
+int bev_split3_f32(const float *x, int64_t n, uint16_t *planes, void *stream) {
+    if (!x || !planes || n < 0) return BEV_ERR_ARGS;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_split3, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, n,
+                       (__bf16 *)planes);
+    return (int)hipGetLastError();
 }
 
 int bev_conv2d_dual_x6_f32(const float *x, int N, int Ho, int Wo, int Ci, const float *x2, int H2, int W2, int Ci2,
@@ -444,6 +875,9 @@ int bev_conv2d_dual_x6_f32(const float *x, int N, int Ho, int Wo, int Ci, const 
     a.M = (int64_t)N * Ho * Wo;
     a.x2 = x2;
     a.Ci2 = Ci2, a.H2 = H2, a.W2 = W2, a.stride2 = stride2;
+    a.xs = nullptr;
+    a.ys = nullptr;
+    a.xps = a.yps = 0;
     return dispatch_x6<true>(a, (hipStream_t)stream);
 }
 

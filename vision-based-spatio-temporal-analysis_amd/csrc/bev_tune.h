@@ -10,7 +10,7 @@ int warp_tune(int knob, int value);
 // knob = BEV_TUNE_WGRAD_MFMA (bev_train.hip).
 int train_tune(int knob, int value);
 
-// BEV_TUNE_CONV_X6_TILE (bev_conv_x6.hip).
-int conv_x6_tune(int value);
+// BEV_TUNE_CONV_X6_TILE / BEV_TUNE_CONV_X6_KERNEL (bev_conv_x6.hip).
+int conv_x6_tune(int knob, int value);
 
 }  // namespace bev

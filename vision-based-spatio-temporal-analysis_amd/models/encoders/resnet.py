@@ -131,13 +131,21 @@ class FoldedConv:
                 b = bn.bias.detach().to(device) + (b - bn.running_mean.detach().to(device)) * scale
         return w, b
 
-    def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False, ascale=None, out=None):
+    def __call__(self, x, relu: bool, residual=None, in_nchw: bool = False, ascale=None, out=None,
+                 split_out: bool = False):
+        """x: NHWC fp32 (NCHW with in_nchw) or, in the bf16x6 arithmetic, a bev_native.Split3; split_out (bf16x6
+        only) returns the result as a Split3 -- the pre-split operand of the next conv."""
         arith = "f32" if (in_nchw or ascale is not None) else self.arith()
         self.prepare(x.device, arith)
         c = self.conv
-        return _nat.conv2d_nhwc(x, self.packed6 if arith == "bf16x6" else self.packed, self.bias, c.out_channels,
-                                c.kernel_size[0], c.kernel_size[1], c.stride[0], c.padding[0], relu,
-                                residual=residual, in_nchw=in_nchw, ascale=ascale, out=out)
+        if arith == "bf16x6":
+            return _nat.conv2d_nhwc_x6(x, self.packed6, self.bias, c.out_channels, c.kernel_size[0],
+                                       c.kernel_size[1], c.stride[0], c.padding[0], 1, int(relu), residual=residual,
+                                       out=out, split_out=split_out)
+        assert not split_out and not isinstance(x, _nat.Split3)
+        return _nat.conv2d_nhwc(x, self.packed, self.bias, c.out_channels, c.kernel_size[0], c.kernel_size[1],
+                                c.stride[0], c.padding[0], relu, residual=residual, in_nchw=in_nchw, ascale=ascale,
+                                out=out)
 
 
 class FoldedTail:
@@ -457,21 +465,30 @@ class ResNet(nn.Module):
         ds = self._fc(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None
         return "plain", [ds] + [self._fc(conv, bn) for conv, bn, _ in blk.convs()]
 
+    @staticmethod
+    def _split_edge(f1, f2) -> bool:
+        """conv f1's output feeds only conv f2: with both in the bf16x6 arithmetic and f2 a KxK (K > 1) conv, f1
+        writes it pre-split (f2 would otherwise split every input pixel once per tap)."""
+        return (f1.arith() == "bf16x6" and f2.arith() == "bf16x6" and f2.conv.kernel_size[0] > 1
+                and f2.conv.in_channels % 32 == 0 and f1.conv.out_channels % 4 == 0)
+
     def _block(self, blk, x, out=None):
         kind, fs = self._block_plan(blk)
         if kind in ("chain", "chaintail"):
             h = fs[0](x, relu=True)
             return fs[1](h, x, out=out)
         if kind == "tail":
-            h = fs[0](x, relu=True)
+            h = fs[0](x, relu=True, split_out=self._split_edge(fs[0], fs[1]))
             h = fs[1](h, relu=True)
             return fs[2](h, x, out=out)
         sc = fs[0](x, relu=False) if fs[0] is not None else x
         chain = blk.convs()
+        fl = fs[1:]
         y = x
-        for idx, ((conv, bn, relu), f) in enumerate(zip(chain, fs[1:])):
+        for idx, ((conv, bn, relu), f) in enumerate(zip(chain, fl)):
             last = idx == len(chain) - 1
-            y = f(y, relu=relu, residual=sc if last else None, out=out if last else None)
+            split = not last and self._split_edge(f, fl[idx + 1])
+            y = f(y, relu=relu, residual=sc if last else None, out=out if last else None, split_out=split)
         return y
 
 
