@@ -346,6 +346,14 @@ int bev_conv2d_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, i
                       const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
                       int dilation, int act, float *y, uint16_t *ys, int ldy, int Ho, int Wo, void *stream);
 
+/* device: bev_conv2d_chain_f32 (bottleneck conv2 -> conv3 + identity residual in one launch, the conv2 output kept
+ * in LDS) in the split arithmetic: packed / packed2 are the split panels of conv2 [Co][Ci][KH][KW] and conv3
+ * [Co2][Co][1][1]; NHWC x, Ci % 32 == 0, Co in {64, 128}, Co2 % 64 == 0; residual [N][Ho][Wo][Co2] (or NULL). */
+int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                            int Co, int KH, int KW, int stride, int pad, int act, const uint16_t *packed2,
+                            const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
+                            void *stream);
+
 /* device: split n fp32 values into planes [3][n] bf16 with x == h + m + l exactly (the operand format of
  * bev_conv2d_x6_f32's xs). */
 int bev_split3_f32(const float *x, int64_t n, uint16_t *planes, void *stream);

@@ -145,6 +145,25 @@ def test_x6_dual_accuracy(stride2, Ci, Ci2, Co):
     assert e <= 1e-5 * scale, (e, scale)
 
 
+@pytest.mark.parametrize("Ci,Co,Co2,stride", [(64, 64, 256, 1), (128, 128, 512, 1), (256, 64, 256, 2)])
+def test_x6_chain_bit_identical_to_two_launches(Ci, Co, Co2, stride):
+    """bev_conv2d_chain_x6_f32 (conv2 -> conv3 + residual, h2 split in LDS) == the two split-bf16 launches."""
+    g = torch.Generator().manual_seed(Ci + Co2)
+    N, H, W = 2, 25, 37
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
+    w2 = (torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5).to(DEV)
+    w3 = (torch.randn(Co2, Co, 1, 1, generator=g) / Co ** 0.5).to(DEV)
+    b2, b3 = (torch.randn(Co, generator=g) * 0.1).to(DEV), (torch.randn(Co2, generator=g) * 0.1).to(DEV)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    res = torch.randn(N, Ho, Wo, Co2, generator=g).to(DEV)
+    p2, p3 = nat.pack_conv_weight_x6(w2), nat.pack_conv_weight_x6(w3)
+    h2 = nat.conv2d_nhwc_x6(x, p2, b2, Co, 3, 3, stride, 1, 1, 1)
+    ref = nat.conv2d_nhwc_x6(h2, p3, b3, Co2, 1, 1, 1, 0, 1, 1, residual=res)
+    got = nat.conv2d_chain_nhwc(x, p2, b2, Co, 3, 3, stride, 1, 1, p3, b3, Co2, 1, residual=res)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 def test_x6_resnet50_encoder_matches_f32_path():
     """The ResNet-50 CNNEncoder (the bench's trunk) in the split-bf16 arithmetic vs the exact-f32 MFMA chains."""
     from models.encoders.cnn_encoder import CNNEncoder

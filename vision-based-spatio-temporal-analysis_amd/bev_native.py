@@ -100,6 +100,8 @@ SIGNATURES = {
     "bev_conv2d_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _i,
                                _vp]),
     "bev_split3_f32": (_i, [_vp, _i64, _vp, _vp]),
+    "bev_conv2d_chain_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
+                                     _i, _i, _vp]),
     "bev_conv2d_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
 }
 
@@ -659,7 +661,9 @@ def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: 
                       out: torch.Tensor = None):
     """act2(act(conv(x) + bias) (*) W2 + bias2 + residual) in one launch; x [N,H,W,Ci] NHWC -> [N,Ho,Wo,Co2]."""
     x = x.contiguous()
-    _require_gpu(x, packed, bias, packed2, bias2, residual)
+    _require_gpu(x, bias, bias2, residual, *([packed, packed2] if packed.dtype != torch.bfloat16 else []))
+    if not (packed.is_cuda and packed2.is_cuda and packed.dtype == packed2.dtype):
+        raise HipError("conv2d_chain_nhwc needs both weight panels on the device, in one arithmetic")
     N, H, W, Ci = x.shape
     Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
     if out is None:
@@ -667,6 +671,13 @@ def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: 
     if residual is not None:
         residual = residual.contiguous()
         assert residual.shape == out.shape
+    if packed.dtype == torch.bfloat16:  # split-bf16 arithmetic (both panels from pack_conv_weight_x6)
+        with _span("conv", x):
+            rc = lib().bev_conv2d_chain_x6_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad,
+                                               int(relu), _ptr(packed2), _ptr(bias2), Co2, _ptr(residual), int(relu2),
+                                               _ptr(out), Ho, Wo, _stream(x))
+        _check(rc, "bev_conv2d_chain_x6_f32")
+        return out
     with _span("conv", x):
         rc = lib().bev_conv2d_chain_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad,
                                         int(relu), _ptr(packed2), _ptr(bias2), Co2, _ptr(residual), int(relu2),

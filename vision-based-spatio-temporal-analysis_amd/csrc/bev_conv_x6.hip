@@ -98,6 +98,10 @@ struct ConvX {
     const __bf16 *__restrict__ xs;
     __bf16 *__restrict__ ys;
     int64_t xps, yps;
+    // chained pointwise conv (k_conv_x6b CHAIN): y = act2(h (*) W2 + bias2 + res), h = act(this conv + bias)
+    const __bf16 *__restrict__ wp2;
+    const float *__restrict__ bias2;
+    int Co2, act2;
 };
 
 __device__ __forceinline__ float act_x(float t, int act) {
@@ -106,26 +110,23 @@ __device__ __forceinline__ float act_x(float t, int act) {
     return t;
 }
 
-// The wave's (TM*32) x (TN*32) accumulator tile goes through LDS so every lane stores whole float4 row pieces;
-// all residual loads are issued at once (the memory-bound 1x1 layers).  Same scheme as bev_conv.hip's epilogue.
+// The wave's (TM*32) x (TN*32) accumulator tile goes through LDS, 32 rows per pass (4 * 32 * (TN * 32 + 4) floats
+// for the block), so every lane stores whole float4 row pieces; each pass issues all its residual loads at once (the
+// memory-bound 1x1 layers).  Same scheme as bev_conv.hip's epilogue.  With a.ys the result is stored split.
+template <int TN>
+__host__ __device__ constexpr int x6_epi_bytes() { return 4 * 32 * (TN * 32 + 4) * 4; }
+
 template <int TM, int TN>
 __device__ __forceinline__ void x6_epilogue(const ConvX &a, float *lds, const f32x16 (&acc)[TM][TN], int wave,
                                             int lane, int wn, int wm, int64_t m0, int n0) {
     const int r32 = lane & 31, h = lane >> 5;
-    constexpr int WR = TM * 32, WC = TN * 32, ER = WC + 4;
-    constexpr int C4 = WC / 4, RPI = 64 / C4, NQ = WR / RPI;
+    constexpr int WC = TN * 32, ER = WC + 4;
+    constexpr int C4 = WC / 4, RPI = 64 / C4, NQ = 32 / RPI;
     __syncthreads();  // every wave is done with the staging buffers
-    float *E = lds + wave * (WR * ER);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) E[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
+    float *E = lds + wave * (32 * ER);
     const int c4 = lane % C4, rq = lane / C4;
     const int n = n0 + wn * WC + c4 * 4;
     const bool nvec = ((a.Co & 3) == 0) && ((a.ldy & 3) == 0) && (n + 3 < a.Co);
-    const int64_t mbase = m0 + wm * WR;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
     if (a.bias) {
         if (nvec) bv = *(const float4 *)(a.bias + n);
@@ -136,58 +137,67 @@ __device__ __forceinline__ void x6_epilogue(const ConvX &a, float *lds, const f3
             bv.w = n + 3 < a.Co ? a.bias[n + 3] : 0.f;
         }
     }
-    float4 rv[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int64_t m = mbase + rq + RPI * q;
-        rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
-    }
+    for (int i = 0; i < TM; ++i) {
+        // same-wave LDS operations complete in order: the previous pass's reads precede these writes
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int row = rq + RPI * q;
-        const int64_t m = mbase + row;
-        if (m >= a.M) continue;
-        const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
-        float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
-        if (a.ys) {  // split output planes (the next conv's pre-split operand); ldy == Co, Co % 4 == 0
-            if (a.res) {
-                const float4 rr = rv[q];
-                o[0] += rr.x, o[1] += rr.y, o[2] += rr.z, o[3] += rr.w;
-            }
-            bf16x4 hv, mv, lv;
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                __bf16 h_, m_, l_;
-                split3(act_x(o[u], a.act), h_, m_, l_);
-                hv[u] = h_, mv[u] = m_, lv[u] = l_;
-            }
-            __bf16 *yp = a.ys + m * a.Co + n;
-            if (n < a.Co) {
-                *(bf16x4 *)yp = hv;
-                *(bf16x4 *)(yp + a.yps) = mv;
-                *(bf16x4 *)(yp + 2 * a.yps) = lv;
-            }
-            continue;
+            for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
+        const int64_t mbase = m0 + wm * TM * 32 + i * 32;
+        float4 rv[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int64_t m = mbase + rq + RPI * q;
+            rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
         }
-        float *yp = a.y + m * a.ldy + n;
-        if (nvec) {
-            if (a.res) {
-                o[0] += rv[q].x;
-                o[1] += rv[q].y;
-                o[2] += rv[q].z;
-                o[3] += rv[q].w;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int row = rq + RPI * q;
+            const int64_t m = mbase + row;
+            if (m >= a.M) continue;
+            const float4 v = *(const float4 *)(E + row * ER + c4 * 4);
+            float o[4] = {v.x + bv.x, v.y + bv.y, v.z + bv.z, v.w + bv.w};
+            if (a.ys) {  // split output planes (the next conv's pre-split operand); ldy == Co, Co % 4 == 0
+                if (a.res) {
+                    const float4 rr = rv[q];
+                    o[0] += rr.x, o[1] += rr.y, o[2] += rr.z, o[3] += rr.w;
+                }
+                bf16x4 hv, mv, lv;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    __bf16 h_, m_, l_;
+                    split3(act_x(o[u], a.act), h_, m_, l_);
+                    hv[u] = h_, mv[u] = m_, lv[u] = l_;
+                }
+                __bf16 *yp = a.ys + m * a.Co + n;
+                if (n < a.Co) {
+                    *(bf16x4 *)yp = hv;
+                    *(bf16x4 *)(yp + a.yps) = mv;
+                    *(bf16x4 *)(yp + 2 * a.yps) = lv;
+                }
+                continue;
             }
+            float *yp = a.y + m * a.ldy + n;
+            if (nvec) {
+                if (a.res) {
+                    o[0] += rv[q].x;
+                    o[1] += rv[q].y;
+                    o[2] += rv[q].z;
+                    o[3] += rv[q].w;
+                }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) o[u] = act_x(o[u], a.act);
-            *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
-        } else {
+                for (int u = 0; u < 4; ++u) o[u] = act_x(o[u], a.act);
+                *(float4 *)yp = make_float4(o[0], o[1], o[2], o[3]);
+            } else {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (n + u >= a.Co) break;
-                float t = o[u];
-                if (a.res) t += a.res[m * a.Co + n + u];
-                yp[u] = act_x(t, a.act);
+                for (int u = 0; u < 4; ++u) {
+                    if (n + u >= a.Co) break;
+                    float t = o[u];
+                    if (a.res) t += a.res[m * a.Co + n + u];
+                    yp[u] = act_x(t, a.act);
+                }
             }
         }
     }
@@ -206,14 +216,14 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6(ConvX a) {
     constexpr int BQ = BN * PPR / 256;
     static_assert(BN * PPR % 256 == 0, "B pieces per thread");
     typedef typename std::conditional<PB == 16, u32x4, u32x2>::type bpiece;  // native vectors stay in VGPRs
-    constexpr int EPIB = 4 * (TM * 32) * (TN * 32 + 4) * 4;
+    constexpr int EPIB = x6_epi_bytes<TN>();
     constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
     static_assert(BM % 64 == 0, "A staging rows");
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
     __bf16 *lds = (__bf16 *)lds_raw;
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
     const int wm = wave / WN, wn = wave % WN;
     const int n_tiles = (a.Co + BN - 1) / BN;
     unsigned bid = blockIdx.x;
@@ -382,6 +392,104 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6(ConvX a) {
 }
 
 // ---------------------------------------------------------------------------
+// Chained bottleneck body in the split arithmetic (bev_conv2d_chain_x6_f32): timm Bottleneck without a downsample,
+// act3(bn3(conv3(act2(bn2(conv2(h1))))) + x).  The block's BM x BN tile of h2 = act(conv2 + b2) holds EVERY channel
+// of h2 for its BM pixels (BN == Co), so it is split once into three bf16 planes in LDS ([3][BM][BN + 8]: rows of
+// odd 16-B slot counts) and conv3 (1x1, K2 = BN) runs on it there: h2 never makes its HBM round trip.  Wave w takes
+// rows 32 w .. 32 w + 31 and walks Co2 in 64-column chunks (2 MFMA tiles); the W3 fragments come from the
+// fragment-order panel by buffer loads (SGPR soffset); the chunk's residual is loaded before its MFMAs; residual and
+// output are addressed by buffer instructions (row in the VGPR offset, so rows past M read 0 / are dropped).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t x6_rsrc(const void *p, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)(uint32_t)bytes, 0x00020000);
+}
+
+template <int WM, int WN, int TM, int TN>
+__device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char *lds_raw, const f32x16 (&acc)[TM][TN],
+                                                  int wave, int lane, int wm, int wn, int64_t m0) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32, HR = BN + 8, HPL = BM * HR;
+    static_assert(BM == 128, "chain epilogue: one 32-row band per wave");
+    __bf16 *H = (__bf16 *)lds_raw;
+    const int r32 = lane & 31, hh = lane >> 5;
+    __syncthreads();  // every wave is done with the staging buffers
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn * TN * 32 + j * 32 + r32;
+            const float bj = a.bias ? a.bias[col] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                __bf16 h_, m_, l_;
+                split3(act_x(acc[i][j][r] + bj, a.act), h_, m_, l_);
+                const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                H[row * HR + col] = h_;
+                H[HPL + row * HR + col] = m_;
+                H[2 * HPL + row * HR + col] = l_;
+            }
+        }
+    __syncthreads();
+    constexpr int S2 = BN / 16;  // 16-deep slices of conv3's K
+    const int band = wave * 32;
+    const __bf16 *ap = H + (band + r32) * HR + 8 * hh;
+    const int64_t rows = (a.M - m0 < BM) ? a.M - m0 : BM;
+    const int64_t base = m0 * a.Co2;
+    const __amdgpu_buffer_rsrc_t ry = x6_rsrc(a.y + base, rows * a.Co2 * 4);
+    const __amdgpu_buffer_rsrc_t rr = x6_rsrc(a.res ? a.res + base : a.y + base, rows * a.Co2 * 4);
+    const __amdgpu_buffer_rsrc_t rw = x6_rsrc(a.wp2, copad_x(a.Co2) / 32 * (int64_t)S2 * 3072);
+    const int vo = ((band + 4 * hh) * a.Co2 + r32) * 4;  // lane part of a res / y address
+    const int vl = lane * 16;
+    const int nch = a.Co2 / 64;
+    for (int nc = 0; nc < nch; ++nc) {
+        const int c0 = 64 * nc;
+        float rv[2][16];
+        if (a.res) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    rv[j][r] = __builtin_bit_cast(
+                        float, __builtin_amdgcn_raw_buffer_load_b32(rr, vo + ((r & 3) + 8 * (r >> 2)) * a.Co2 * 4,
+                                                                    (c0 + 32 * j) * 4, 0));
+        }
+        f32x16 acc2[2] = {(f32x16){0}, (f32x16){0}};
+#pragma unroll
+        for (int t = 0; t < S2; ++t) {
+            bf16x8 fa[3], fb[2][3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) fa[p] = *(const bf16x8 *)(ap + p * HPL + 16 * t);
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    fb[j][p] = __builtin_bit_cast(
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, vl, (((c0 >> 5) + j) * S2 + t) * 3072 + p * 1024, 0));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][0], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[j][0], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][1], acc2[j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float bj = a.bias2 ? a.bias2[c0 + 32 * j + r32] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float o = acc2[j][r] + bj;
+                if (a.res) o += rv[j][r];
+                o = act_x(o, a.act2);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry,
+                                                      vo + ((r & 3) + 8 * (r >> 2)) * a.Co2 * 4, (c0 + 32 * j) * 4, 0);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_conv_x6b: Ci % 32 == 0 (every ResNet trunk layer).  K step 32 (two 16-deep slices, 48 MFMAs per wave and
 // step for a 64 x 64 wave tile: twice the work per barrier of k_conv_x6).  Only A goes through LDS (three bf16
 // planes, rows of 40 bf16 = 80 B = 5 odd 16-B slots: conflict-free fragment groups); the B fragments are read
@@ -391,19 +499,19 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6(ConvX a) {
 constexpr int YBK = 32;
 constexpr int YROW = 40;
 
-template <int WM, int WN, int TM, int TN, bool DUAL>
-__global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
+template <int WM, int WN, int TM, int TN, bool DUAL, bool CHAIN = false>
+__global__ __launch_bounds__(256, (CHAIN && WN * TN > 2) ? 1 : 2) void k_conv_x6b(ConvX a) {  // 128-wide chain: 102 KiB LDS
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int APL = BM * YROW;                 // bf16 per A plane
     constexpr int STAGE = 3 * APL;                 // bf16 per LDS stage
     constexpr int AQ = BM / 32;                    // A float4 per thread and K step: rows tid / 8 + 32 q
-    constexpr int EPIB = 4 * (TM * 32) * (TN * 32 + 4) * 4;
+    constexpr int EPIB = CHAIN ? 3 * BM * (BN + 8) * 2 : x6_epi_bytes<TN>();
     constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
     __bf16 *lds = (__bf16 *)lds_raw;
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
     const int wm = wave / WN, wn = wave % WN;
     const int n_tiles = (a.Co + BN - 1) / BN;
     unsigned bid = blockIdx.x;
@@ -570,6 +678,10 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
 #undef X6B_BLOAD
 #undef X6B_SWRITE
 #undef X6B_GLOAD
+    if constexpr (CHAIN) {
+        x6_chain_epilogue<WM, WN, TM, TN>(a, lds_raw, acc, wave, lane, wm, wn, m0);
+        return;
+    }
     x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
 }
 
@@ -599,20 +711,20 @@ __device__ __forceinline__ void dma16(const void *src, unsigned dst_any) {
 }
 
 template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(256, 2) void k_conv_x6s(ConvX a) {
+__global__ __launch_bounds__(256, 3) void k_conv_x6s(ConvX a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int APL = BM * 32;     // bf16 per A plane per stage (64-B rows)
     constexpr int STAGE = 3 * APL;   // bf16 per stage
     constexpr int RW = BM / 4;       // rows staged by each wave
     constexpr int RG = RW / 16;      // 16-row DMA groups per wave and plane
-    constexpr int EPIB = 4 * (TM * 32) * (TN * 32 + 4) * 4;
+    constexpr int EPIB = x6_epi_bytes<TN>();
     constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
     static_assert(RW % 16 == 0, "whole DMA groups per wave");
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
     const __bf16 *lds = (const __bf16 *)lds_raw;
 
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR)
     const int wm = wave / WN, wn = wave % WN;
     const int n_tiles = (a.Co + BN - 1) / BN;
     unsigned bid = blockIdx.x;
@@ -748,12 +860,12 @@ __global__ void k_split3(const float *__restrict__ x, int64_t n, __bf16 *__restr
     out[t + 2 * n] = l;
 }
 
-template <int WM, int WN, int TM, int TN, bool DUAL>
+template <int WM, int WN, int TM, int TN, bool DUAL, bool CHAIN = false>
 int launch_x6b(const ConvX &a, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL((k_conv_x6b<WM, WN, TM, TN, DUAL>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_conv_x6b<WM, WN, TM, TN, DUAL, CHAIN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     return (int)hipGetLastError();
 }
 
@@ -842,6 +954,9 @@ int bev_conv2d_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, i
     a.ys = (__bf16 *)ys;
     a.xps = (int64_t)N * H * W * Ci;
     a.yps = a.M * Co;
+    a.wp2 = nullptr;
+    a.bias2 = nullptr;
+    a.Co2 = a.act2 = 0;
     return dispatch_x6<false>(a, (hipStream_t)stream);
 }
 
@@ -878,7 +993,46 @@ int bev_conv2d_dual_x6_f32(const float *x, int N, int Ho, int Wo, int Ci, const 
     a.xs = nullptr;
     a.ys = nullptr;
     a.xps = a.yps = 0;
+    a.wp2 = nullptr;
+    a.bias2 = nullptr;
+    a.Co2 = a.act2 = 0;
     return dispatch_x6<true>(a, (hipStream_t)stream);
+}
+
+int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                            int Co, int KH, int KW, int stride, int pad, int act, const uint16_t *packed2,
+                            const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
+                            void *stream) {
+    if (!x || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+        pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2)
+        return BEV_ERR_ARGS;
+    if (Ci % YBK != 0 || (Co != 64 && Co != 128) || Co2 <= 0 || Co2 % 64 != 0 ||
+        (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvX a;
+    a.x = x;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.res = residual;
+    a.y = y;
+    a.N = N, a.H = H, a.W = W, a.Ci = Ci, a.Co = Co, a.KH = KH, a.KW = KW, a.stride = stride, a.pad = pad;
+    a.dil = 1, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = Co2;
+    a.Kp = (int)kpad_x(Ci * KH * KW);
+    a.M = (int64_t)N * Ho * Wo;
+    a.x2 = nullptr;
+    a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
+    a.xs = nullptr;
+    a.ys = nullptr;
+    a.xps = a.yps = 0;
+    a.wp2 = (const __bf16 *)packed2;
+    a.bias2 = bias2;
+    a.Co2 = Co2;
+    a.act2 = act2;
+    if (Co == 64) return launch_x6b<4, 1, 1, 2, false, true>(a, (hipStream_t)stream);
+    return launch_x6b<2, 2, 2, 2, false, true>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

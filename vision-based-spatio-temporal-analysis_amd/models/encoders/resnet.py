@@ -217,16 +217,20 @@ class FoldedChain:
                 and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.padding == (0, 0)
                 and c3.out_channels % 128 == 0)
 
-    def prepare(self, device):
-        self.c2.prepare(device, "f32")
-        self.c3.prepare(device, "f32")
+    def prepare(self, device, arith: str = "f32"):
+        self.c2.prepare(device, arith)
+        self.c3.prepare(device, arith)
 
-    def __call__(self, h, x, out=None):
-        self.prepare(h.device)
+    def __call__(self, h, x, out=None, arith: str = "f32"):
+        """arith "f32": bev_conv2d_chain_f32 (exact-f32 MFMA, bit-identical to the two launches); "bf16x6":
+        bev_conv2d_chain_x6_f32 (the split arithmetic, h2 kept split in LDS)."""
+        self.prepare(h.device, arith)
         c2 = self.c2.conv
-        return _nat.conv2d_chain_nhwc(h, self.c2.packed, self.c2.bias, c2.out_channels, c2.kernel_size[0],
-                                      c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU, self.c3.packed,
-                                      self.c3.bias, self.c3.conv.out_channels, _nat.ACT_RELU, residual=x, out=out)
+        x6 = arith == "bf16x6"
+        return _nat.conv2d_chain_nhwc(h, self.c2.packed6 if x6 else self.c2.packed, self.c2.bias, c2.out_channels,
+                                      c2.kernel_size[0], c2.kernel_size[1], c2.stride[0], c2.padding[0],
+                                      _nat.ACT_RELU, self.c3.packed6 if x6 else self.c3.packed, self.c3.bias,
+                                      self.c3.conv.out_channels, _nat.ACT_RELU, residual=x, out=out)
 
 
 class FoldedChainTail:
@@ -297,6 +301,12 @@ class ResNet(nn.Module):
         # images are independent; every layer still runs as one kernel per group; bit-identical output).
         # r02h A/B (7-cam 1080p ResNet-50 bench): 1 group 87.6, 2 groups 89.4, 3 groups 88.4 frames/s;
         # staggering the groups' start (stream_offset) did not help.
+        # bf16x6 arithmetic (bev_native.conv_arith()): the stages (1 = layer1 ...) whose bottlenecks keep the exact-f32
+        # chained kernels (conv2 output in LDS, no HBM round trip) -- measured faster where the 1x1 tails are
+        # HBM-bound -- and whether conv1 hands conv2 a pre-split operand (k_conv_x6s).
+        self.f32_chain_stages = set()
+        self.x6_chain_stages = {1}  # stages whose bottleneck bodies run as one split-arithmetic chained launch
+        self.split_edges = False
         self.stream_groups = 2
         self.stream_offset = 0  # > 0: group g waits for group g - 1 to pass this launch stage (staggered start)
         self._streams = {}
@@ -373,8 +383,13 @@ class ResNet(nn.Module):
             return
         for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
             for blk in layer:
-                for f in self._block_plan(blk)[1]:
-                    if f is not None:
+                kind, fs = self._block_plan(blk)
+                for f in fs:
+                    if f is None:
+                        continue
+                    if kind == "chain6" and isinstance(f, FoldedChain):
+                        f.prepare(device, "bf16x6")
+                    else:
                         f.prepare(device)
             if li == out_index:
                 return
@@ -452,7 +467,12 @@ class ResNet(nn.Module):
         """(kind, folded executors) of one residual block on the eval path.  The chained kernels are exact-f32
         MFMA kernels: with the split-bf16 arithmetic (bev_native.conv_arith() == "bf16x6") the block runs as
         separate split-bf16 launches (conv1, conv2, conv3 + shortcut as one dual GEMM) instead."""
-        chains = self.fuse_chain and _nat.conv_arith() == "f32"
+        stage = self._stage_of_block(blk)
+        chains = self.fuse_chain and (_nat.conv_arith() == "f32" or stage in self.f32_chain_stages)
+        if (isinstance(blk, Bottleneck) and self.fuse_chain and not chains and stage in self.x6_chain_stages
+                and FoldedChain.applies(blk) and self._fc(blk.conv2, blk.bn2).arith() == "bf16x6"
+                and self._fc(blk.conv3, blk.bn3).arith() == "bf16x6"):
+            return "chain6", [self._fc(blk.conv1, blk.bn1), self._chain(blk)]
         if isinstance(blk, Bottleneck) and chains and FoldedChain.applies(blk):
             return "chain", [self._fc(blk.conv1, blk.bn1), self._chain(blk)]
         if isinstance(blk, Bottleneck) and chains and self.fuse_shortcut and FoldedChainTail.applies(blk):
@@ -465,11 +485,16 @@ class ResNet(nn.Module):
         ds = self._fc(blk.downsample[0], blk.downsample[1]) if blk.downsample is not None else None
         return "plain", [ds] + [self._fc(conv, bn) for conv, bn, _ in blk.convs()]
 
-    @staticmethod
-    def _split_edge(f1, f2) -> bool:
+    def _stage_of_block(self, blk) -> int:
+        for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
+            if any(b is blk for b in layer):
+                return li
+        return 0
+
+    def _split_edge(self, f1, f2) -> bool:
         """conv f1's output feeds only conv f2: with both in the bf16x6 arithmetic and f2 a KxK (K > 1) conv, f1
         writes it pre-split (f2 would otherwise split every input pixel once per tap)."""
-        return (f1.arith() == "bf16x6" and f2.arith() == "bf16x6" and f2.conv.kernel_size[0] > 1
+        return (self.split_edges and f1.arith() == "bf16x6" and f2.arith() == "bf16x6" and f2.conv.kernel_size[0] > 1
                 and f2.conv.in_channels % 32 == 0 and f1.conv.out_channels % 4 == 0)
 
     def _block(self, blk, x, out=None):
@@ -477,6 +502,9 @@ class ResNet(nn.Module):
         if kind in ("chain", "chaintail"):
             h = fs[0](x, relu=True)
             return fs[1](h, x, out=out)
+        if kind == "chain6":
+            h = fs[0](x, relu=True)
+            return fs[1](h, x, out=out, arith="bf16x6")
         if kind == "tail":
             h = fs[0](x, relu=True, split_out=self._split_edge(fs[0], fs[1]))
             h = fs[1](h, relu=True)
