@@ -28,8 +28,8 @@ barrier and a MAX-reduction of the elapsed time cross ranks.  `n_gpus` is the wo
 size of the initialised process group.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
-`roofline` object for the dominant kernel family (backbone convs on fp32
-MFMA), `roofline_warp` for the IPM warp kernel (HBM-bound), and, at N = 1, a
+`roofline` object for the dominant kernel family (backbone convs; by default in
+the split-bf16 fp32 arithmetic, --conv-arith f32 for the exact-f32 MFMA kernels), `roofline_warp` for the IPM warp kernel (HBM-bound), and, at N = 1, a
 `cpu_baseline` (the reference's torch-CPU composition, timed on this host on
 a bounded sample).
 """
@@ -54,6 +54,9 @@ import torch  # noqa: E402
 BOUNDS = (-24.0, 24.0, -7.2, 7.2)
 PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TF = 157.3  # MI355X fp32 matrix spec (= vector peak)
+PEAK_BF16_MFMA_TF = 2500.0  # MI355X bf16 matrix, dense (MI355X_MICROARCH.md)
+# the split arithmetic spends 6 bf16 partial products per fp32 product: its fp32-equivalent dense peak
+PEAK_X6_TF = PEAK_BF16_MFMA_TF / 6
 
 
 def parse():
@@ -76,6 +79,9 @@ def parse():
     ap.add_argument("--stream-offset", type=int, default=None, help="ResNet inference: stagger of the stream groups")
     ap.add_argument("--cpu-iters", type=int, default=2, help="frames timed for the CPU baseline (0 = skip)")
     ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
+    ap.add_argument("--conv-arith", choices=("bf16x6", "f32"), default="bf16x6",
+                    help="trunk conv arithmetic: bf16x6 = fp32 through exact 3-way bf16 splits (default), f32 = the "
+                         "exact-f32 MFMA kernels")
     ap.add_argument("--warp-kernel", choices=("dma", "register", "wave"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
     args = ap.parse_args()
@@ -146,6 +152,14 @@ def backbone_flops(enc, H, W):
                 total += conv(blk.downsample[0], hi, wi)[0]
     total += 2 * h * w * enc.proj.in_channels * enc.proj.out_channels
     return total
+
+
+def stem_flops(enc, H, W):
+    """2 * MACs of the ResNet stem conv per image."""
+    c = enc.backbone.conv1
+    ho = (H + 2 * c.padding[0] - c.kernel_size[0]) // c.stride[0] + 1
+    wo = (W + 2 * c.padding[1] - c.kernel_size[1]) // c.stride[1] + 1
+    return 2 * ho * wo * c.out_channels * c.in_channels * c.kernel_size[0] * c.kernel_size[1]
 
 
 def backbone_bytes(enc, H, W):
@@ -272,6 +286,8 @@ def pmc_traffic(args) -> dict:
     if not default or not files:
         return {}
     d = json.load(open(files[-1]))
+    if d.get("conv_arith", "f32") != args.conv_arith:  # profiled under the other conv arithmetic
+        d.pop("conv", None)
     res = {k: d[k]["traffic_bytes"] for k in ("conv", "warp") if k in d}
     res["source"] = f"profiles/{os.path.basename(files[-1])}: {d.get('note', '')}"
     return res
@@ -338,6 +354,7 @@ def main():
     images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
     nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1, "wave": 2}[args.warp_kernel])
+    nat.set_conv_arith(args.conv_arith)
     stream = torch.cuda.current_stream(dev)
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
 
@@ -411,6 +428,11 @@ def main():
     if rank == 0:
         pmc = pmc_traffic(args)
         flops = backbone_flops(enc, H, W) * VL * B
+        # the ResNet stem (NCHW, Ci = 3) always runs the exact-f32 MFMA stem kernel; under the bf16x6 arithmetic
+        # every other trunk conv and the proj run on the bf16 matrix cores (6 partial products per fp32 product)
+        x6 = nat.conv_arith() == "bf16x6" and not args.backbone.startswith("efficient") and enc._use_timm
+        f_stem = stem_flops(enc, H, W) * VL * B if x6 else flops
+        peak_mfma = flops / (f_stem / PEAK_F32_MFMA_TF + (flops - f_stem) / PEAK_X6_TF) if x6 else PEAK_F32_MFMA_TF
         Hm = geom.homographies(Kd, Rtd, B, VL, dev)
         alg, out_b, touched = warp_alg_bytes(geom, Hm, feats.shape, (H, W), B)
         groups = int(getattr(enc.backbone, "stream_groups", 1)) if not args.backbone.startswith("efficient") else 1
@@ -418,10 +440,18 @@ def main():
         # with >1 stream group the conv launches of the groups overlap: their HIP-event spans sum to more
         # than the wall time, so the kernel time is the encoder stage's wall time (convs + max-pool)
         kern_ms = conv_ms if groups <= 1 else bb_ms
+        ach_tf = flops / (kern_ms * 1e-3) / 1e12
         roof_bb = None if args.warp_only else {
-            "kernel": "k_conv + k_stem (fp32 MFMA implicit GEMM, every backbone conv launch of one step)",
-            "bound": "mfma", "achieved": round(flops / (kern_ms * 1e-3) / 1e12, 3), "peak": PEAK_F32_MFMA_TF,
-            "unit": "TFLOP/s", "frac": round(flops / (kern_ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TF, 4),
+            "kernel": ("k_conv_x6* (fp32 as 3-way split bf16, 6 partial products on v_mfma_f32_32x32x16_bf16) + "
+                       "k_stem (exact-f32 MFMA), every backbone conv launch of one step" if x6 else
+                       "k_conv + k_stem (fp32 MFMA implicit GEMM, every backbone conv launch of one step)"),
+            "bound": "mfma", "achieved": round(ach_tf, 3), "peak": round(peak_mfma, 1),
+            "unit": "TFLOP/s", "frac": round(ach_tf / peak_mfma, 4),
+            "arith": nat.conv_arith() if x6 else "f32",
+            "peak_basis": ("algorithmic fp32 FLOPs; peak blended by FLOP share: stem at the fp32 MFMA peak 157.3, "
+                           f"the rest at bf16 dense {PEAK_BF16_MFMA_TF:.0f} / 6 = {PEAK_X6_TF:.1f}" if x6 else
+                           "fp32 MFMA dense peak"),
+            "frac_of_fp32_mfma_peak": round(ach_tf / PEAK_F32_MFMA_TF, 4),
             "traffic": pmc.get("conv"), "flops_per_step": flops, "kernel_ms_per_step": round(kern_ms, 4),
             "conv_span_sum_ms_per_step": round(conv_ms, 4), "encoder_stage_ms": round(bb_ms, 4),
             "stream_groups": groups,

@@ -30,6 +30,7 @@ def family(name: str) -> str:
 def main():
     fdir, wdir, out = sys.argv[1:4]
     groups = int(sys.argv[4]) if len(sys.argv) > 4 else 2
+    arith = sys.argv[5] if len(sys.argv) > 5 else "bf16x6"  # bench.py --conv-arith of the profiled command
     tot = defaultdict(float)
     n = defaultdict(int)
     steps = 0
@@ -54,6 +55,7 @@ def main():
     res["note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; FETCH x2 (gfx950 wide-read "
                    "correction), KiB -> bytes; warp and chained-conv stores are 4 B/lane (WRITE_SIZE uncalibrated for "
                    "that width)")
+    res["conv_arith"] = arith
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
