@@ -354,6 +354,14 @@ int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const u
                             const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
                             void *stream);
 
+/* device: bev_conv2d_chain_dual_f32 (block 0 of a stage: conv2 -> [conv3 | 1x1/s2 downsample of x2] in one launch)
+ * in the split arithmetic; packed2 = the split panel of [W3 | Wds] as [Co2][Co + Ci2][1][1]; Co == Ci2 == 64 (the
+ * layer1 shape), Ci % 32 == 0, Co2 % 64 == 0. */
+int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed,
+                                 const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
+                                 const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
+                                 const float *bias2, int Co2, int act2, float *y, int Ho, int Wo, void *stream);
+
 /* device: split n fp32 values into planes [3][n] bf16 with x == h + m + l exactly (the operand format of
  * bev_conv2d_x6_f32's xs). */
 int bev_split3_f32(const float *x, int64_t n, uint16_t *planes, void *stream);

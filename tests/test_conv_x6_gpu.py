@@ -164,6 +164,24 @@ def test_x6_chain_bit_identical_to_two_launches(Ci, Co, Co2, stride):
     assert torch.equal(got, ref)
 
 
+def test_x6_chain_dual_bit_identical_to_two_launches():
+    """bev_conv2d_chain_dual_x6_f32 (layer1 block 0: conv2 -> [conv3 | downsample], h2 split in LDS, the shortcut
+    operand split in registers) == the split conv2 launch + the split dual tail launch."""
+    g = torch.Generator().manual_seed(3)
+    N, H, W, Ci, Co, Co2 = 2, 25, 37, 64, 64, 256
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)        # conv2 input (conv1's output)
+    xb = torch.randn(N, H, W, 64, generator=g).to(DEV)       # block input (the downsample's operand)
+    w2 = (torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5).to(DEV)
+    w3 = (torch.randn(Co2, Co + 64, 1, 1, generator=g) / (Co + 64) ** 0.5).to(DEV)
+    b2, b3 = (torch.randn(Co, generator=g) * 0.1).to(DEV), (torch.randn(Co2, generator=g) * 0.1).to(DEV)
+    p2, p3 = nat.pack_conv_weight_x6(w2), nat.pack_conv_weight_x6(w3)
+    h2 = nat.conv2d_nhwc_x6(x, p2, b2, Co, 3, 3, 1, 1, 1, 1)
+    ref = nat.conv2d_dual_nhwc(h2, xb, 1, p3, b3, Co2, relu=True)
+    got = nat.conv2d_chain_dual_nhwc(x, p2, b2, Co, 3, 3, 1, 1, 1, xb, 1, p3, b3, Co2, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 def test_x6_resnet50_encoder_matches_f32_path():
     """The ResNet-50 CNNEncoder (the bench's trunk) in the split-bf16 arithmetic vs the exact-f32 MFMA chains."""
     from models.encoders.cnn_encoder import CNNEncoder

@@ -100,6 +100,8 @@ SIGNATURES = {
     "bev_conv2d_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _i,
                                _vp]),
     "bev_split3_f32": (_i, [_vp, _i64, _vp, _vp]),
+    "bev_conv2d_chain_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp,
+                                          _vp, _i, _i, _vp, _i, _i, _vp]),
     "bev_conv2d_chain_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
                                      _i, _i, _vp]),
     "bev_conv2d_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
@@ -692,12 +694,21 @@ def conv2d_chain_dual_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int,
     """act2([act(conv(x) + bias) | x2[:, ::s2, ::s2]] (*) W2 + bias2) in one launch (bottleneck with downsample)."""
     x = x.contiguous()
     x2 = x2.contiguous()
-    _require_gpu(x, packed, bias, x2, packed2, bias2)
+    _require_gpu(x, bias, x2, bias2, *([packed, packed2] if packed.dtype != torch.bfloat16 else []))
+    if not (packed.is_cuda and packed2.is_cuda and packed.dtype == packed2.dtype):
+        raise HipError("conv2d_chain_dual_nhwc needs both weight panels on the device, in one arithmetic")
     N, H, W, Ci = x.shape
     _, H2, W2, Ci2 = x2.shape
     Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
     if out is None:
         out = torch.empty(N, Ho, Wo, Co2, device=x.device, dtype=torch.float32)
+    if packed.dtype == torch.bfloat16:  # split-bf16 arithmetic
+        with _span("conv", x):
+            rc = lib().bev_conv2d_chain_dual_x6_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride,
+                                                    pad, int(relu), _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed2),
+                                                    _ptr(bias2), Co2, int(relu2), _ptr(out), Ho, Wo, _stream(x))
+        _check(rc, "bev_conv2d_chain_dual_x6_f32")
+        return out
     with _span("conv", x):
         rc = lib().bev_conv2d_chain_dual_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad,
                                              int(relu), _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed2), _ptr(bias2),

@@ -404,11 +404,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t x6_rsrc(const void *p, int64_t
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)(uint32_t)bytes, 0x00020000);
 }
 
-template <int WM, int WN, int TM, int TN>
+// X2S > 0: the dual form (block 0 of a stage, bev_conv2d_chain_dual_x6_f32): conv3's K continues with the X2S
+// 16-deep slices of the shortcut operand x2 at the lane row's strided pixel (the 1x1 downsample), split in registers
+// once per wave and reused by every chunk; the panel is the dual tail's [W3 | Wds].
+template <int WM, int WN, int TM, int TN, int X2S = 0>
 __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char *lds_raw, const f32x16 (&acc)[TM][TN],
                                                   int wave, int lane, int wm, int wn, int64_t m0) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32, HR = BN + 8, HPL = BM * HR;
-    static_assert(BM == 128, "chain epilogue: one 32-row band per wave");
+    constexpr int NB = BM / 32, WPB = 4 / NB;  // 32-row bands; waves per band (each a share of the Co2 chunks)
+    static_assert(NB * WPB == 4, "chain epilogue: 4 waves over the 32-row bands");
     __bf16 *H = (__bf16 *)lds_raw;
     const int r32 = lane & 31, hh = lane >> 5;
     __syncthreads();  // every wave is done with the staging buffers
@@ -429,18 +433,41 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
             }
         }
     __syncthreads();
-    constexpr int S2 = BN / 16;  // 16-deep slices of conv3's K
-    const int band = wave * 32;
+    constexpr int S2 = BN / 16;      // 16-deep slices of conv3's K from h2
+    constexpr int ST = S2 + X2S;     // slices of the panel
+    const int band = (wave % NB) * 32, part = wave / NB;
+    bf16x8 fx[X2S > 0 ? X2S : 1][3];  // the shortcut operand, split (dual form)
+    if constexpr (X2S > 0) {
+        int64_t m = m0 + band + r32;
+        const bool ok = m < a.M;
+        m = ok ? m : 0;
+        const int ox = (int)(m % a.Wo);
+        const int64_t q = m / a.Wo;
+        const int oy = (int)(q % a.Ho);
+        const int64_t n = q / a.Ho;
+        const float *xp = a.x2 + ((n * a.H2 + (int64_t)oy * a.stride2) * a.W2 + (int64_t)ox * a.stride2) * a.Ci2 + 8 * hh;
+#pragma unroll
+        for (int t = 0; t < X2S; ++t) {
+            f32x4 v0 = ok ? *(const f32x4 *)(xp + 16 * t) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            f32x4 v1 = ok ? *(const f32x4 *)(xp + 16 * t + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __bf16 h_, m_, l_;
+                split3(e < 4 ? v0[e] : v1[e - 4], h_, m_, l_);
+                fx[t][0][e] = h_, fx[t][1][e] = m_, fx[t][2][e] = l_;
+            }
+        }
+    }
     const __bf16 *ap = H + (band + r32) * HR + 8 * hh;
     const int64_t rows = (a.M - m0 < BM) ? a.M - m0 : BM;
     const int64_t base = m0 * a.Co2;
     const __amdgpu_buffer_rsrc_t ry = x6_rsrc(a.y + base, rows * a.Co2 * 4);
     const __amdgpu_buffer_rsrc_t rr = x6_rsrc(a.res ? a.res + base : a.y + base, rows * a.Co2 * 4);
-    const __amdgpu_buffer_rsrc_t rw = x6_rsrc(a.wp2, copad_x(a.Co2) / 32 * (int64_t)S2 * 3072);
+    const __amdgpu_buffer_rsrc_t rw = x6_rsrc(a.wp2, copad_x(a.Co2) / 32 * (int64_t)ST * 3072);
     const int vo = ((band + 4 * hh) * a.Co2 + r32) * 4;  // lane part of a res / y address
     const int vl = lane * 16;
-    const int nch = a.Co2 / 64;
-    for (int nc = 0; nc < nch; ++nc) {
+    const int nch = a.Co2 / 64 / WPB;  // this wave's 64-column chunks: [part * nch, (part + 1) * nch)
+    for (int nc = part * nch; nc < (part + 1) * nch; ++nc) {
         const int c0 = 64 * nc;
         float rv[2][16];
         if (a.res) {
@@ -454,16 +481,20 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
         }
         f32x16 acc2[2] = {(f32x16){0}, (f32x16){0}};
 #pragma unroll
-        for (int t = 0; t < S2; ++t) {
+        for (int t = 0; t < ST; ++t) {
             bf16x8 fa[3], fb[2][3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) fa[p] = *(const bf16x8 *)(ap + p * HPL + 16 * t);
+            for (int p = 0; p < 3; ++p) {
+                if constexpr (X2S > 0) fa[p] = t < S2 ? *(const bf16x8 *)(ap + p * HPL + 16 * (t < S2 ? t : 0))
+                                                      : fx[t >= S2 ? t - S2 : 0][p];
+                else fa[p] = *(const bf16x8 *)(ap + p * HPL + 16 * t);
+            }
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
                 for (int p = 0; p < 3; ++p)
                     fb[j][p] = __builtin_bit_cast(
-                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, vl, (((c0 >> 5) + j) * S2 + t) * 3072 + p * 1024, 0));
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, vl, (((c0 >> 5) + j) * ST + t) * 3072 + p * 1024, 0));
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], acc2[j], 0, 0, 0);
@@ -499,8 +530,8 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
 constexpr int YBK = 32;
 constexpr int YROW = 40;
 
-template <int WM, int WN, int TM, int TN, bool DUAL, bool CHAIN = false>
-__global__ __launch_bounds__(256, (CHAIN && WN * TN > 2) ? 1 : 2) void k_conv_x6b(ConvX a) {  // 128-wide chain: 102 KiB LDS
+template <int WM, int WN, int TM, int TN, bool DUAL, int CHAIN = 0>  // CHAIN: 0 none, 1 chain, 2 chain + shortcut
+__global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int APL = BM * YROW;                 // bf16 per A plane
     constexpr int STAGE = 3 * APL;                 // bf16 per LDS stage
@@ -678,8 +709,8 @@ __global__ __launch_bounds__(256, (CHAIN && WN * TN > 2) ? 1 : 2) void k_conv_x6
 #undef X6B_BLOAD
 #undef X6B_SWRITE
 #undef X6B_GLOAD
-    if constexpr (CHAIN) {
-        x6_chain_epilogue<WM, WN, TM, TN>(a, lds_raw, acc, wave, lane, wm, wn, m0);
+    if constexpr (CHAIN > 0) {
+        x6_chain_epilogue<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0>(a, lds_raw, acc, wave, lane, wm, wn, m0);
         return;
     }
     x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
@@ -860,7 +891,7 @@ __global__ void k_split3(const float *__restrict__ x, int64_t n, __bf16 *__restr
     out[t + 2 * n] = l;
 }
 
-template <int WM, int WN, int TM, int TN, bool DUAL, bool CHAIN = false>
+template <int WM, int WN, int TM, int TN, bool DUAL, int CHAIN = 0>
 int launch_x6b(const ConvX &a, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
@@ -1031,8 +1062,46 @@ int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const u
     a.bias2 = bias2;
     a.Co2 = Co2;
     a.act2 = act2;
-    if (Co == 64) return launch_x6b<4, 1, 1, 2, false, true>(a, (hipStream_t)stream);
-    return launch_x6b<2, 2, 2, 2, false, true>(a, (hipStream_t)stream);
+    if (Co == 64) return launch_x6b<4, 1, 1, 2, false, 1>(a, (hipStream_t)stream);
+    if (Co2 % 128 != 0) return BEV_ERR_ARGS;  // two waves share each 32-row band of the 64-row tile
+    return launch_x6b<2, 2, 1, 2, false, 1>(a, (hipStream_t)stream);  // 64 x 128: h2 planes 52 KiB of LDS
+}
+
+int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed,
+                                 const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
+                                 const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
+                                 const float *bias2, int Co2, int act2, float *y, int Ho, int Wo, void *stream) {
+    if (!x || !x2 || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+        pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2 || stride2 <= 0 || H2 <= 0 || W2 <= 0)
+        return BEV_ERR_ARGS;
+    // the layer1 block-0 shape: 64-channel h2 and a 64-channel shortcut operand (4 slices kept in registers)
+    if (Ci % YBK != 0 || Co != 64 || Ci2 != 64 || Co2 <= 0 || Co2 % 64 != 0 ||
+        (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0 ||
+        Ho != (H2 - 1) / stride2 + 1 || Wo != (W2 - 1) / stride2 + 1)
+        return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    ConvX a;
+    a.x = x;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.res = nullptr;
+    a.y = y;
+    a.N = N, a.H = H, a.W = W, a.Ci = Ci, a.Co = Co, a.KH = KH, a.KW = KW, a.stride = stride, a.pad = pad;
+    a.dil = 1, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = Co2;
+    a.Kp = (int)kpad_x(Ci * KH * KW);
+    a.M = (int64_t)N * Ho * Wo;
+    a.x2 = x2;
+    a.Ci2 = Ci2, a.H2 = H2, a.W2 = W2, a.stride2 = stride2;
+    a.xs = nullptr;
+    a.ys = nullptr;
+    a.xps = a.yps = 0;
+    a.wp2 = (const __bf16 *)packed2;
+    a.bias2 = bias2;
+    a.Co2 = Co2;
+    a.act2 = act2;
+    return launch_x6b<4, 1, 1, 2, false, 2>(a, (hipStream_t)stream);
 }
 
 }  // extern "C"

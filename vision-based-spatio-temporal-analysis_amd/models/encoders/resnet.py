@@ -253,16 +253,19 @@ class FoldedChainTail:
                 and c2.kernel_size[0] == c2.kernel_size[1] and c2.dilation == (1, 1) and c2.groups == 1
                 and blk.conv3.out_channels % 128 == 0)
 
-    def prepare(self, device):
-        self.c2.prepare(device, "f32")
-        self.tail.prepare(device, "f32")
+    def prepare(self, device, arith: str = "f32"):
+        self.c2.prepare(device, arith)
+        self.tail.prepare(device, arith)
 
-    def __call__(self, h, x, out=None):
-        self.prepare(h.device)
+    def __call__(self, h, x, out=None, arith: str = "f32"):
+        """arith "f32": bev_conv2d_chain_dual_f32; "bf16x6": bev_conv2d_chain_dual_x6_f32 (64-channel shapes)."""
+        self.prepare(h.device, arith)
         c2 = self.c2.conv
-        return _nat.conv2d_chain_dual_nhwc(h, self.c2.packed, self.c2.bias, c2.out_channels, c2.kernel_size[0],
-                                           c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU, x,
-                                           self.tail.short.conv.stride[0], self.tail.packed, self.tail.bias,
+        x6 = arith == "bf16x6"
+        return _nat.conv2d_chain_dual_nhwc(h, self.c2.packed6 if x6 else self.c2.packed, self.c2.bias, c2.out_channels,
+                                           c2.kernel_size[0], c2.kernel_size[1], c2.stride[0], c2.padding[0],
+                                           _nat.ACT_RELU, x, self.tail.short.conv.stride[0],
+                                           self.tail.packed6 if x6 else self.tail.packed, self.tail.bias,
                                            self.tail.main.conv.out_channels, _nat.ACT_RELU, out=out)
 
 
@@ -387,7 +390,7 @@ class ResNet(nn.Module):
                 for f in fs:
                     if f is None:
                         continue
-                    if kind == "chain6" and isinstance(f, FoldedChain):
+                    if kind in ("chain6", "chaintail6") and isinstance(f, (FoldedChain, FoldedChainTail)):
                         f.prepare(device, "bf16x6")
                     else:
                         f.prepare(device)
@@ -473,6 +476,14 @@ class ResNet(nn.Module):
                 and FoldedChain.applies(blk) and self._fc(blk.conv2, blk.bn2).arith() == "bf16x6"
                 and self._fc(blk.conv3, blk.bn3).arith() == "bf16x6"):
             return "chain6", [self._fc(blk.conv1, blk.bn1), self._chain(blk)]
+        if (isinstance(blk, Bottleneck) and self.fuse_chain and self.fuse_shortcut and not chains
+                and stage in self.x6_chain_stages and FoldedChainTail.applies(blk) and blk.conv2.out_channels == 64
+                and blk.downsample[0].in_channels == 64 and self._fc(blk.conv2, blk.bn2).arith() == "bf16x6"
+                and self._tail(blk).arith() == "bf16x6"):
+            k = ("chaintail", id(blk))
+            if k not in self._folded:
+                self._folded[k] = FoldedChainTail(self._fc(blk.conv2, blk.bn2), self._tail(blk))
+            return "chaintail6", [self._fc(blk.conv1, blk.bn1), self._folded[k]]
         if isinstance(blk, Bottleneck) and chains and FoldedChain.applies(blk):
             return "chain", [self._fc(blk.conv1, blk.bn1), self._chain(blk)]
         if isinstance(blk, Bottleneck) and chains and self.fuse_shortcut and FoldedChainTail.applies(blk):
@@ -502,7 +513,7 @@ class ResNet(nn.Module):
         if kind in ("chain", "chaintail"):
             h = fs[0](x, relu=True)
             return fs[1](h, x, out=out)
-        if kind == "chain6":
+        if kind in ("chain6", "chaintail6"):
             h = fs[0](x, relu=True)
             return fs[1](h, x, out=out, arith="bf16x6")
         if kind == "tail":
