@@ -64,6 +64,22 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             print(f"round {rnd} variant {b:>6}: {e0.elapsed_time(e1) / n * 1e3:8.1f} us per launch", flush=True)
+    check_exact(libs, args, out)
+
+
+def check_exact(libs, args, out):
+    """Variants without ablation bits ("0" + build suffixes) must produce the baseline's output bit for bit."""
+    ref = None
+    for b, L in libs.items():
+        if b.rstrip("nsw") not in ("0", ""):
+            continue
+        out.zero_()
+        assert L.bev_ipm_warp_fuse_ws_f32(*args) == 0
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = out.clone()
+        else:
+            print(f"variant {b}: bit-identical to the first exact variant: {torch.equal(out, ref)}", flush=True)
 
 
 if __name__ == "__main__":

@@ -465,6 +465,12 @@ __device__ unsigned long long g_warp_stamp[16384 * 6];
 #define STAMP(k) ((void)0)
 #endif
 
+#ifndef WARP_TSTORE
+#define WARP_TSTORE 0  // fused warp v2: 16-B output stores through a per-wave LDS transpose (1) or 4-B stores (0)
+#endif
+#ifndef WARP_LANESKIP
+#define WARP_LANESKIP 1  // fused warp v2: lanes with no valid tap skip the view's LDS sampling (1, r03 A/B: 1-8 % faster) or read the zero pixel (0)
+#endif
 #ifndef WARP_DMABUF
 #define WARP_DMABUF 0  // fused warp v2: footprint DMA through a buffer descriptor (1; r03m A/B: 1-8 % slower) or 64-bit global addresses (0)
 #endif
@@ -480,6 +486,16 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
         __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * N * sizeof(float)), 0x00020000);
     const int voff = cell * (int)sizeof(float);
     static_assert(N % 8 == 0, "stores in groups of 8 channels");
+    if (WARP_ABLATE & 32) {  // timing only: the same bytes as 1-KiB coalesced 16-B-per-lane stores (wrong layout)
+        const int wb = __builtin_amdgcn_readfirstlane(cell) * N * (int)sizeof(float);
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int q = 0; q < N; q += 4) {
+            const float4 v = make_float4(acc[q], acc[q + 1], acc[q + 2], acc[q + 3]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs, lane * 16, wb + q * 256, 2);
+        }
+        return;
+    }
 #pragma unroll
     for (int q0 = 0; q0 < N; q0 += 8) {
         // eight independent divisions, then their stores: the group is pinned after the previous group's
@@ -495,6 +511,43 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
             if ((WARP_ABLATE & 16) && r != 1.2345e-30f) continue;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
                                                   (int)(uint32_t)((q0 + u) * plane * sizeof(float)), 2);
+        }
+    }
+}
+
+// Output stores of a whole in-range tile through a per-wave LDS transpose (WARP_TSTORE): each lane holds one
+// cell's 64 channels, but the [C][Hb][Wb] output is contiguous along cells, so the lanes first write their values
+// (after the mean division) to LDS as [channel][wave's 64 cells], then read back 4 consecutive cells of one
+// channel and store them as ONE 16-B store: 16 1-KiB store instructions per wave instead of 64 of 256 B.
+// Two passes of 32 channels (8 KiB of LDS per wave).  Cell slot of a lane: its row inside the wave's band x TW +
+// its column.  Same values, same addresses as store_chunk: bit-identical output.
+template <int TH, int N>
+__device__ __forceinline__ void store_tile_t(float *chunk, size_t plane, int row0, int col0, int Wb, int tr, int tc,
+                                             const float (&acc)[N], int mode, double rV, unsigned char *smem,
+                                             int wave, int lane) {
+    constexpr int TW = FT_NT / TH, RB = TH / 4;  // tile width; rows per wave
+    static_assert(RB * TW == 64 && TW % 4 == 0, "one wave = 64 cells in whole 4-cell quads");
+    float *E = reinterpret_cast<float *>(smem) + wave * (32 * 64);
+    const int slot = (tr - wave * RB) * TW + tc;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * N * sizeof(float)), 0x00020000);
+    const int g = lane & 15, cq = lane >> 4;            // quad of cells, channel within the instruction's four
+    const int r = wave * RB + (4 * g) / TW, c = (4 * g) % TW;
+    const int voff = ((row0 + r) * Wb + col0 + c) * (int)sizeof(float);
+#pragma unroll
+    for (int h = 0; h < N; h += 32) {
+#pragma unroll
+        for (int u = 0; u < 32; ++u) {
+            const float a = acc[h + u];
+            E[u * 64 + slot] = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? div_rcp(a, rV) : a;
+        }
+        // same-wave LDS ops complete in order: the reads below see these writes
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int ch = 4 * k + cq;
+            const f32x4 v = *(const f32x4 *)(E + ch * 64 + 4 * g);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs, voff,
+                                                   (int)(uint32_t)((h + ch) * plane * sizeof(float)), 2);
         }
     }
 }
@@ -1077,9 +1130,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             if (!done) {
                 if (!have_t) t = taps_of(v);
                 if (WARP_ABLATE & 4) acc[0] += t.w[0] * t.w[3] + (float)(t.x0 + t.y0 + (int)t.valid);
-                else if (__ballot(t.valid != 0) != 0ull)
-                    sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
-                else zero_view<MODE>(acc, v);
+                else if (__ballot(t.valid != 0) != 0ull) {
+                    // WARP_LANESKIP: lanes without a valid tap leave the LDS reads to the others (their sample is
+                    // +0: acc + 0 == acc exactly, max(acc, 0) for the max mode)
+                    if (!WARP_LANESKIP || t.valid)
+                        sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+                    else zero_view<MODE>(acc, v);
+                } else zero_view<MODE>(acc, v);
             } else if (empty) {
                 zero_view<MODE>(acc, v);
             }
@@ -1087,7 +1144,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             __syncthreads();  // all of it landed; image of view v and red[] are free
         }
         STAMP(3);
-        if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+        if (WARP_TSTORE && pool >= 4 * 32 * 64 * 4 && (tyb + 1) * TH <= Hb && (txb + 1) * TW <= Wb && Wb % 4 == 0) {
+            store_tile_t<TH>(out + ((size_t)b * C + c0) * plane, plane, tyb * TH, txb * TW, Wb, tr, tc, acc, MODE, rV,
+                             smem, wave, lane);
+            __syncthreads();  // the transpose's LDS is free before the next chunk / frame stages into the pool
+        } else if (inside) {
+            store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+        }
         STAMP(4);
       }
     }
