@@ -55,8 +55,9 @@ int bev_abi_version(void);
  *   results bit for bit.
  * BEV_TUNE_CONV_X6_TILE: output tile of the split-bf16 fp32 convs (bev_conv2d_x6_f32 / _dual_x6_f32):
  *   0 = automatic, 1 = 128x128, 2 = 128x64.
- * BEV_TUNE_CONV_X6_KERNEL: 0 (default) = 32-deep K steps with B fragments read straight from the panel when
- *   Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel for every shape.  Same results bit for bit. */
+ * BEV_TUNE_CONV_X6_KERNEL: 0 (default) / 2 = 32-deep K steps with B fragments read straight from the panel
+ *   wherever Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel (both operands through LDS) for every shape.
+ *   Same results bit for bit. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3

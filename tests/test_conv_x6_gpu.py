@@ -93,7 +93,7 @@ def test_x6_tiles_bit_identical():
     p6 = nat.pack_conv_weight_x6(w.float().to(DEV))
     outs = []
     for t in (1, 2):
-        for kern in (0, 1):
+        for kern in (0, 1, 2):
             with nat.tuned(CONV_X6_TILE=t, CONV_X6_KERNEL=kern):
                 outs.append(nat.conv2d_nhwc_x6(xd, p6, bd, Co, 3, 3, 1, 1, 1, 1))
     torch.cuda.synchronize()

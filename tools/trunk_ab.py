@@ -27,6 +27,7 @@ VARIANTS = {
     "x6+x6chain12": ("bf16x6", set(), {1, 2}, False),
     "x6+split": ("bf16x6", set(), set(), True),
 }
+# stream-group variants of the default plan: "sg<G>"; split-kernel choice: "k<knob>" (BEV_TUNE_CONV_X6_KERNEL)
 
 
 def main():
@@ -44,7 +45,17 @@ def main():
     with torch.no_grad():
         for rnd in range(a.rounds):
             for name in a.variants:
-                arith, stages, stages6, split = VARIANTS[name]
+                knob = int(name[1:]) if name.startswith("k") else 0
+                nat.tune(nat.TUNE_CONV_X6_KERNEL, knob)
+                if name.startswith("k"):
+                    arith, stages, stages6, split = VARIANTS["x6+x6chain1"]
+                    rn.stream_groups = 2
+                elif name.startswith("sg"):
+                    arith, stages, stages6, split = VARIANTS["x6+x6chain1"]
+                    rn.stream_groups = int(name[2:])
+                else:
+                    arith, stages, stages6, split = VARIANTS[name]
+                    rn.stream_groups = 2
                 rn.f32_chain_stages, rn.x6_chain_stages, rn.split_edges = stages, stages6, split
                 with nat.conv_arith_mode(arith):
                     for _ in range(3):

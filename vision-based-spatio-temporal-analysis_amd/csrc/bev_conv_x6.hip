@@ -910,7 +910,7 @@ int launch_x6(const ConvX &a, hipStream_t st) {
 }
 
 int g_x6_tile = 0;  // 0 automatic, 1 = 128 x 128, 2 = 128 x 64
-int g_x6_kernel = 0;  // 0 automatic (k_conv_x6b when Ci (and Ci2) % 32 == 0), 1 = k_conv_x6 (16-deep K steps)
+int g_x6_kernel = 0;  // 0 automatic, 1 = k_conv_x6 (16-deep K steps) everywhere, 2 = k_conv_x6b wherever it applies
 
 template <bool DUAL>
 int dispatch_x6(const ConvX &a, hipStream_t st) {
@@ -919,7 +919,10 @@ int dispatch_x6(const ConvX &a, hipStream_t st) {
         if (t == 2) return launch_x6s<4, 1, 1, 2>(a, st);
         return launch_x6s<2, 2, 2, 2>(a, st);
     }
-    const bool wide = a.Ci % YBK == 0 && (!DUAL || a.Ci2 % YBK == 0) && g_x6_kernel == 0;
+    // automatic = the 32-deep-step kernel wherever it applies: single 1x1 layers measured faster on the 16-deep
+    // kernel in isolation, but the ResNet-50 encoder (two stream groups) is fastest with the 32-deep kernel
+    // everywhere (r03 tools/trunk_ab.py: 16.24 ms vs 16.34 with 1x1 / dual layers on the 16-deep one, 16.43 all)
+    const bool wide = a.Ci % YBK == 0 && (!DUAL || a.Ci2 % YBK == 0) && g_x6_kernel != 1;
     if (wide) {
         if (t == 2) return launch_x6b<4, 1, 1, 2, DUAL>(a, st);
         return launch_x6b<2, 2, 2, 2, DUAL>(a, st);
@@ -933,7 +936,7 @@ int dispatch_x6(const ConvX &a, hipStream_t st) {
 namespace bev {
 int conv_x6_tune(int knob, int value) {
     int *slot = knob == BEV_TUNE_CONV_X6_TILE ? &g_x6_tile : &g_x6_kernel;
-    if (value < 0 || value > (knob == BEV_TUNE_CONV_X6_TILE ? 2 : 1)) return BEV_ERR_ARGS;
+    if (value < 0 || value > 2) return BEV_ERR_ARGS;
     const int old = *slot;
     *slot = value;
     return old;
