@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--conv-arith", choices=("bf16x6", "f32"), default="bf16x6",
                     help="trunk conv arithmetic: bf16x6 = fp32 through exact 3-way bf16 splits (default), f32 = the "
                          "exact-f32 MFMA kernels")
-    ap.add_argument("--warp-kernel", choices=("dma", "register", "wave"), default="dma",
+    ap.add_argument("--warp-kernel", choices=("dma", "register", "wave", "persist"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
     args = ap.parse_args()
     if args.views is None:
@@ -353,7 +353,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(rank)
     images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
-    nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1, "wave": 2}[args.warp_kernel])
+    nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1, "wave": 2, "persist": 3}[args.warp_kernel])
     nat.set_conv_arith(args.conv_arith)
     stream = torch.cuda.current_stream(dev)
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
@@ -460,7 +460,8 @@ def main():
                        "the caller stream around the whole encoder, incl. the max-pool); per-launch spans sum "
                        "higher because launches of the two groups run concurrently")}
         ach = alg / (wp_ms * 1e-3) / 1e9
-        wk = {"dma": "k_warp_fuse_v2", "register": "k_warp_fuse", "wave": "k_warp_fuse_w"}[args.warp_kernel]
+        wk = {"dma": "k_warp_fuse_v2", "register": "k_warp_fuse", "wave": "k_warp_fuse_w",
+              "persist": "k_warp_fuse_p"}[args.warp_kernel]
         roof_wp = {"kernel": f"{wk} (IPM warp + {'sum' if args.camera_shard else 'mean'}, fused)", "bound": "hbm",
                    "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
                    "traffic": pmc.get("warp"), "alg_bytes_per_launch": alg, "out_bytes": out_b,

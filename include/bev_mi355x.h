@@ -44,7 +44,8 @@ int bev_abi_version(void);
  *   warp in KiB, 0 = automatic, else 8..150 (small pools force block decomposition).
  * BEV_TUNE_WARP_KERNEL: fused warp kernel for NHWC C % 64 == 0 features:
  *   0 = LDS-DMA kernel (default), 1 = register-staged, 2 = wave-independent LDS-DMA kernel (per-wave
- *   footprints, no workgroup barrier).
+ *   footprints, no workgroup barrier), 3 = persistent LDS-DMA kernel (C == 64 with a workspace: the next
+ *   (frame, tile)'s first footprint DMA is issued before this one's stores).
  * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.

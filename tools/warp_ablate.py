@@ -34,7 +34,7 @@ def main():
     s = feats.stride()
     # a trailing "n" times the same library without the workspace (the in-kernel corner-box prologue)
     libs = {b: ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{b.rstrip('n') or b}.so"))
-            for b in bits}
+            for b in bits}  # "p0" / "w0": copies of libwarp_ablate_0.so built as p0 / w0 (their own knob state)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ws = torch.empty(nat.lib().bev_ipm_warp_fuse_workspace_bytes(B, V, 480, 1440), device=dev, dtype=torch.uint8)
     args = (nat._ptr(feats), s[1], s[2], s[3], s[4], nat._ptr(Hm), nat._ptr(xs), nat._ptr(ys), B, V, C, Hf, Wf, sx, sy,
@@ -46,11 +46,11 @@ def main():
     # a leading "w" times the wave-independent kernel (bev_tune(BEV_TUNE_WARP_KERNEL, 2)); libwarp_ablate_w<b>.so
     # must be a separate copy of the library (its own knob state)
     for b, L in libs.items():
-        if b.startswith("w"):
+        if b.startswith("w") or b.startswith("p"):  # "p": the persistent kernel (BEV_TUNE_WARP_KERNEL 3)
             tune = getattr(L, "_ZN3bev9warp_tuneEii")  # bev::warp_tune (bev_warp.hip alone has no bev_tune)
             tune.restype = ctypes.c_int
             tune.argtypes = [ctypes.c_int, ctypes.c_int]
-            assert tune(nat.TUNE_WARP_KERNEL, 2) >= 0
+            assert tune(nat.TUNE_WARP_KERNEL, 2 if b.startswith("w") else 3) >= 0
     for rnd in range(int(os.environ.get("ROUNDS", "5"))):
         for b, L in libs.items():
             a = args_n if b.endswith("n") else args
@@ -71,7 +71,7 @@ def check_exact(libs, args, out):
     """Variants without ablation bits ("0" + build suffixes) must produce the baseline's output bit for bit."""
     ref = None
     for b, L in libs.items():
-        if b.rstrip("nsw") not in ("0", ""):
+        if b.lstrip("wp").rstrip("nsw") not in ("0", ""):
             continue
         out.zero_()
         assert L.bev_ipm_warp_fuse_ws_f32(*args) == 0

@@ -1156,6 +1156,259 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     }
 }
 
+// -------------------------------------------------------------------------
+// persistent form of k_warp_fuse_v2 (C == 64, corner boxes from the workspace; BEV_TUNE_WARP_KERNEL 3)
+// -------------------------------------------------------------------------
+// The ablation of k_warp_fuse_v2 shows its phases adding up: the ~5400 workgroups of a batch-2 launch
+// run in ~7 lock-step rounds, each computing and then storing, so the 354 MB of output stores (61 us alone) barely
+// overlap the sampling.  Here a workgroup walks (frame, tile) items with stride gridDim.x, and before it stores item
+// k it already reads item k + 1's corner boxes, issues the LDS-DMA of k + 1's first live footprint and computes that
+// view's taps: the stores then drain while the next item starts.  vmcnt counts loads, stores and LDS-DMA in issue
+// order, so the DMA must be OLDER than the stores to be waited for without them: the wait is vmcnt(63) (every
+// operation but the 63 youngest -- the stores -- is complete).  Per item the arithmetic, the view order and the
+// LDS images are exactly k_warp_fuse_v2's: bit-identical output.
+template <int MODE, int OCC, int TH>
+__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_p(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                         int64_t sW, const float *__restrict__ Hmat,
+                                                         const float *__restrict__ xs, const float *__restrict__ ys,
+                                                         int B, int V, int Hf, int Wf, float sx, float sy, int Hb,
+                                                         int Wb, float *__restrict__ out, int pool,
+                                                         const uint2 *__restrict__ boxes) {
+    constexpr int NW = FT_NT / 64;
+    constexpr int TW = FT_NT / TH;
+    constexpr int SL = 17, PS = SL * 16;
+    constexpr int C = 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int zp = pool;
+    int *red = reinterpret_cast<int *>(smem + pool + 256);
+    const int maxpix = pool / PS - 4;
+    const int ntx = (Wb + TW - 1) / TW, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
+    const int nitems = nt * B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int tr, tc;
+    tile_cell<TH>(lane, wave, tr, tc);
+    const size_t plane = (size_t)Hb * Wb;
+    const Grid grid = make_grid(Hf, Wf);
+    const double rV = recip_uniform(V);
+    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
+        dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, wave, lane, NW);
+    };
+    // per-item state
+    struct Item {
+        int b, tyb, txb, i, j;
+        bool inside;
+        float cx, cy;
+        unsigned lba, lbb;
+    };
+    auto setup = [&](int item, Item &it) {
+        it.b = item / nt;
+        int tile = item - it.b * nt;
+        {  // XCD-aware tile order within a frame, as k_warp_fuse_v2
+            const int q = nt / 8, r = nt % 8, x = tile % 8;
+            tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+        }
+        it.tyb = tile / ntx;
+        it.txb = tile - it.tyb * ntx;
+        it.i = it.tyb * TH + tr;
+        it.j = it.txb * TW + tc;
+        it.inside = (it.i < Hb) && (it.j < Wb);
+        it.cx = xs[it.inside ? it.j : 0];
+        it.cy = ys[it.inside ? it.i : 0];
+        const uint2 bx = lane < V ? boxes[((int64_t)it.b * nt + tile) * V + lane] : make_uint2(0u, 0u);
+        it.lba = bx.x;
+        it.lbb = bx.y;
+    };
+    auto box_of = [&](const Item &it, int v) {
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)it.lba, v);
+        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)it.lbb, v);
+        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
+    };
+    auto ok_of = [&](const Item &it, int v) {
+        return ((unsigned)__builtin_amdgcn_readlane((int)it.lba, v) >> 31) == 0u;
+    };
+    auto live = [&](const Item &it, int u) { return !ok_of(it, u) || box_of(it, u).x1 >= 0; };
+    auto taps_of = [&](const Item &it, int v, float ccx, float ccy) {
+        float h[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane((it.b * V + v) * 9) + q];
+        float ix, iy;
+        cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
+        Taps t = taps_from_ixy(ix, iy, grid);
+        if (!it.inside) t.valid = 0;
+        return t;
+    };
+    // head of an item: its first live view, the DMA of that view's footprint (when its corner box applies and fits)
+    // and that view's taps -- everything before the first barrier of the item
+    struct Head {
+        int v_first, offn;
+        Box bn;
+        Taps tf;
+        bool have_f;
+    };
+    auto head = [&](const Item &it, Head &hd) {
+        int u = 0;
+        while (u < V && !live(it, u)) ++u;
+        hd.v_first = u;
+        hd.bn = box_of(it, u < V ? u : 0);
+        hd.offn = -1;
+        hd.have_f = false;
+        if (u < V) {
+            const Box &bn = hd.bn;
+            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+            if (ok_of(it, u) && bn.x1 >= 0 && npix <= maxpix) {
+                hd.offn = 0;
+                dma(feats + (int64_t)(it.b * V + u) * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, 0);
+            }
+            if (ok_of(it, u)) {
+                float ccx = it.cx, ccy = it.cy;
+                asm volatile("" : "+v"(ccx), "+v"(ccy));
+                hd.tf = taps_of(it, u, ccx, ccy);
+                hd.have_f = true;
+            }
+        }
+    };
+
+    int item = blockIdx.x;
+    if (item >= nitems) return;
+    Item cur;
+    Head hd;
+    setup(item, cur);
+    head(cur, hd);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // zero pixel + image of the first live view
+    while (true) {
+        float ccx = cur.cx, ccy = cur.cy;
+        asm volatile("" : "+v"(ccx), "+v"(ccy));  // taps per view, not hoisted
+        float acc[C];
+#pragma unroll
+        for (int q = 0; q < C; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        if (hd.v_first > 0) zero_view<MODE>(acc, 0);  // views before the first live one contribute 0 (max: max(acc, 0))
+        const float *fb = feats + (int64_t)(cur.b * V) * sN;
+        auto next_live = [&](int u) {
+            ++u;
+            while (u < V && !live(cur, u)) {
+                zero_view<MODE>(acc, u);
+                ++u;
+            }
+            return u;
+        };
+        Box bn = hd.bn;
+        int offn = hd.offn;
+        bool have_f = hd.have_f;
+        for (int v = hd.v_first, vn; v < V; v = vn) {
+            vn = next_live(v);
+            Box bx = bn;
+            const int off = offn;
+            const float *f = fb + (int64_t)v * sN;
+            Taps t;
+            bool have_t = false;
+            if (have_f) {
+                t = hd.tf;
+                have_t = true;
+                have_f = false;
+            }
+            if (!ok_of(cur, v)) {
+                t = taps_of(cur, v, ccx, ccy);
+                have_t = true;
+                put_box<NW>(red, wave_box(t), wave, lane);
+                __syncthreads();
+                bx = get_box<NW>(red);
+            }
+            const bool empty = bx.x1 < 0;
+            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+            bool done = empty;
+            if (!done && off < 0) {
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                    hb = min(bh, maxpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                if (single) dma(f, bx.x0, bx.y0, bw, bw * bh, 0);
+                if (!have_t) {
+                    t = taps_of(cur, v, ccx, ccy);
+                    have_t = true;
+                }
+                int mkx = 0, mky = 0;
+                if (!single && t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
+                }
+                const bool wave_any = __ballot(t.valid != 0) != 0ull;
+                if (!single && !t.valid) zero_view<MODE>(acc, v);
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        if (!single) {
+                            __syncthreads();
+                            dma(f, sx0, sy0, sbw, sbw * sbh, 0);
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __syncthreads();
+                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
+                        if (go) sample_view<MODE, 1, 64>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        else if (single) zero_view<MODE>(acc, v);
+                    }
+                done = true;
+                __syncthreads();
+            }
+            if (vn < V) {
+                bn = box_of(cur, vn);
+                offn = -1;
+                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+                if (ok_of(cur, vn) && bn.x1 >= 0 && npix <= maxpix) {
+                    const int need = ((npix * SL + 63) >> 6) * 1024;
+                    if (done || off < 0) offn = 0;
+                    else if (off == 0) {
+                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
+                    } else if (need <= off) offn = 0;
+                    if (offn >= 0) dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, offn);
+                }
+            }
+            if (!done) {
+                if (!have_t) t = taps_of(cur, v, ccx, ccy);
+                if (__ballot(t.valid != 0) != 0ull) {
+                    if (!WARP_LANESKIP || t.valid)
+                        sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+                    else zero_view<MODE>(acc, v);
+                } else zero_view<MODE>(acc, v);
+            } else if (empty) {
+                zero_view<MODE>(acc, v);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();  // image of view v and red[] are free
+        }
+        // the next item's boxes, first footprint DMA and first taps go out BEFORE this item's stores
+        const int nitem = item + gridDim.x;
+        const bool more = nitem < nitems;
+        Item nxt;
+        Head nh;
+        if (more) {
+            setup(nitem, nxt);
+            head(nxt, nh);
+        }
+        if (cur.inside)
+            store_chunk(out + (size_t)cur.b * C * plane, plane, cur.i * Wb + cur.j, acc, MODE, rV);
+        if (!more) break;
+        asm volatile("s_waitcnt vmcnt(63)" ::: "memory");  // the DMA (older than the <= 64 stores) landed
+        __syncthreads();
+        cur = nxt;
+        hd = nh;
+        item = nitem;
+    }
+}
+
+template <int OCC>
+int launch_fuse_p(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                  const float *ys, int B, int V, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                  float *out, hipStream_t st, int pool, uint2 *boxes);
+
 // Corner boxes of every (frame, tile, view) for k_warp_fuse_v2 (FPW = 1), one thread each: the tile prologue's
 // arithmetic (corner_box + the pool-size test) moved out of the sampling kernel, whose workgroups then start
 // with one 8-byte load per view instead of a double-precision latency chain on one wave while three wait.
@@ -1626,6 +1879,32 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
     return last();
 }
 
+template <int OCC>
+int launch_fuse_p(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                  const float *ys, int B, int V, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                  float *out, hipStream_t st, int pool, uint2 *boxes) {
+    constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
+    const int nty = (Hb + TH - 1) / TH, ntiles = ((Wb + TW - 1) / TW) * nty;
+    const int maxpix = pool / (17 * 16) - 4;
+    hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0, st,
+                       Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, nty, boxes);
+    const int64_t nitems = (int64_t)ntiles * B;
+    const unsigned g = (unsigned)(nitems < (int64_t)OCC * cu_count() ? nitems : (int64_t)OCC * cu_count());
+    const size_t lds = (size_t)pool + V2_FIXED;
+    if (mode == BEV_FUSE_SUM)
+        hipLaunchKernelGGL((k_warp_fuse_p<BEV_FUSE_SUM, OCC, TH>), dim3(g), dim3(FT_NT), lds, st, feats, sN, sH, sW,
+                           Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
+    else if (mode == BEV_FUSE_MEAN)
+        hipLaunchKernelGGL((k_warp_fuse_p<BEV_FUSE_MEAN, OCC, TH>), dim3(g), dim3(FT_NT), lds, st, feats, sN, sH, sW,
+                           Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
+    else if constexpr (OCC == 2)  // MAX's extra live state spills at 3 workgroups per CU
+        hipLaunchKernelGGL((k_warp_fuse_p<BEV_FUSE_MAX, OCC, TH>), dim3(g), dim3(FT_NT), lds, st, feats, sN, sH, sW,
+                           Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
+    else
+        return BEV_ERR_ARGS;
+    return last();
+}
+
 // wave-independent kernel: 4 x (pool + zero pixel) per workgroup, OCC workgroups per CU
 template <int OCC>
 int launch_fuse_w_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
@@ -1689,7 +1968,7 @@ int warp_tune(int knob, int value) {
             break;
         case BEV_TUNE_WARP_KERNEL:
             slot = &g_warp_kernel;
-            ok = value >= 0 && value <= 2;
+            ok = value >= 0 && value <= 3;
             break;
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
@@ -1796,6 +2075,14 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
         const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
         uint2 *boxes = (workspace && workspace_bytes >= need && ((uintptr_t)workspace & 7) == 0)
                            ? reinterpret_cast<uint2 *>(workspace) : nullptr;
+        if (g_warp_kernel == 3 && boxes && C == 64 && (int64_t)B * ((Hb + 15) / 16) * ((Wb + 15) / 16) < (1ll << 31)) {
+            const int occ_pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024;
+            return mode == BEV_FUSE_MAX
+                       ? launch_fuse_p<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                          g_warp_pool_kb ? occ_pool : 72 * 1024, boxes)
+                       : launch_fuse_p<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                          occ_pool, boxes);
+        }
         if (g_warp_kernel == 2)
             return mode == BEV_FUSE_MAX
                        ? launch_fuse_w_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
