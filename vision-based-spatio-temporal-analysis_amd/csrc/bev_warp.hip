@@ -1393,10 +1393,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_p(const float *__restr
             setup(nitem, nxt);
             head(nxt, nh);
         }
+        const bool any_in = __ballot(cur.inside) != 0ull;  // the wave issues its 64 stores (else none at all)
         if (cur.inside)
             store_chunk(out + (size_t)cur.b * C * plane, plane, cur.i * Wb + cur.j, acc, MODE, rV);
         if (!more) break;
-        asm volatile("s_waitcnt vmcnt(63)" ::: "memory");  // the DMA (older than the <= 64 stores) landed
+        // the DMA is older than this wave's 64 stores: all but the 63 youngest operations = the DMA has landed
+        if (any_in) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         cur = nxt;
         hd = nh;
