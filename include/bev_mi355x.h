@@ -58,7 +58,9 @@ int bev_abi_version(void);
  *   0 = automatic, 1 = 128x128, 2 = 128x64.
  * BEV_TUNE_CONV_X6_KERNEL: 0 (default) / 2 = 32-deep K steps with B fragments read straight from the panel
  *   wherever Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel (both operands through LDS) for every shape.
- *   Same results bit for bit. */
+ *   Same results bit for bit.
+ * BEV_TUNE_CONV_H16_KERNEL: autocast fp16 convs: 0 (default) = 64-deep K steps, two steps in flight, where Ci % 64 ==
+ *   0; 1 = the 32-deep-step kernel always.  Same results bit for bit. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -69,6 +71,7 @@ int bev_abi_version(void);
 #define BEV_TUNE_CONV_DMA 9
 #define BEV_TUNE_CONV_X6_TILE 10
 #define BEV_TUNE_CONV_X6_KERNEL 11
+#define BEV_TUNE_CONV_H16_KERNEL 12
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

@@ -72,6 +72,25 @@ def test_conv_h16_vs_float64_of_rounded_operands(shape):
     _case(**shape)
 
 
+@pytest.mark.parametrize("Ci,K,stride", [(64, 3, 1), (128, 3, 2), (256, 1, 1)])
+def test_conv_h16_kernels_bit_identical(Ci, K, stride):
+    """The 64-deep-step kernel (default for Ci % 64 == 0) and the 32-deep one sum every output in the same order."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(Ci)
+    N, H, W, Co = 2, 19, 27, 192
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
+    w = (torch.randn(Co, Ci, K, K, generator=g) / (Ci * K * K) ** 0.5).to(DEV)
+    b = torch.randn(Co, generator=g).to(DEV)
+    with nat._half_mode(True):
+        packed = nat.pack_conv_weight(w)
+    outs = []
+    for kern in (0, 1):
+        with nat.tuned(CONV_H16_KERNEL=kern):
+            outs.append(nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, stride, K // 2, 1, 1))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv_h16_rejects_bad_arguments():
     import bev_native as nat
     x = torch.zeros(1, 4, 4, 48, device=DEV)

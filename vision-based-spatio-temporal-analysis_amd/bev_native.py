@@ -178,6 +178,7 @@ TUNE_WGRAD_MFMA = 8
 TUNE_CONV_DMA = 9
 TUNE_CONV_X6_TILE = 10
 TUNE_CONV_X6_KERNEL = 11
+TUNE_CONV_H16_KERNEL = 12
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 

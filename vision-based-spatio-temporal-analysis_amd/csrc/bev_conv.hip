@@ -1289,6 +1289,7 @@ int bev_tune(int knob, int value) {
     }
     if (knob == BEV_TUNE_WGRAD_MFMA) return bev::train_tune(knob, value);
     if (knob == BEV_TUNE_CONV_X6_TILE || knob == BEV_TUNE_CONV_X6_KERNEL) return bev::conv_x6_tune(knob, value);
+    if (knob == BEV_TUNE_CONV_H16_KERNEL) return bev::conv_h16_tune(value);
     return bev::warp_tune(knob, value);
 }
 

@@ -27,8 +27,10 @@ typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (uint4 arrays went to scratch)
 
 constexpr int HBM = 128, HBN = 128, HBK = 32;
+int g_h16_kernel = 0;  // BEV_TUNE_CONV_H16_KERNEL: 0 = k_conv_h16b where Ci % 64 == 0, 1 = k_conv_h16 always
 constexpr int HROW = 40;  // halves per LDS row: 32 + 8 pad = 80 B = 5 slots (odd: 16 rows -> 16 distinct slots)
 
 __device__ __attribute__((aligned(16))) float g_hzero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
     const _Float16 *wrow = a.wp + (int64_t)(n0 + (tid >> 1)) * a.Kp + 16 * (tid & 1);
 
     f32x4 ra[4];
-    uint4 rb[2];
+    u32x4 rb[2];
     int ky = 0, kx = 0, ci0 = 0;  // tap and channel offset of the K step being loaded
     int64_t kb = 0;
     auto gload = [&]() {
@@ -119,8 +121,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
             const float *src = in ? a.x + pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 + 4 * aq : g_hzero4;
             ra[q] = *(const f32x4 *)src;
         }
-        rb[0] = *(const uint4 *)(wrow + kb);
-        rb[1] = *(const uint4 *)(wrow + kb + 8);
+        rb[0] = *(const u32x4 *)(wrow + kb);
+        rb[1] = *(const u32x4 *)(wrow + kb + 8);
         kb += HBK;
         ci0 += HBK;
         if (ci0 == a.Ci) {
@@ -138,8 +140,8 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
             const h16x4 h = {(_Float16)ra[q][0], (_Float16)ra[q][1], (_Float16)ra[q][2], (_Float16)ra[q][3]};
             *(h16x4 *)(As + ((tid >> 3) + 32 * q) * HROW + 4 * aq) = h;
         }
-        *(uint4 *)(Bs + (tid >> 1) * HROW + 16 * (tid & 1)) = rb[0];
-        *(uint4 *)(Bs + (tid >> 1) * HROW + 16 * (tid & 1) + 8) = rb[1];
+        *(u32x4 *)(Bs + (tid >> 1) * HROW + 16 * (tid & 1)) = rb[0];
+        *(u32x4 *)(Bs + (tid >> 1) * HROW + 16 * (tid & 1) + 8) = rb[1];
     };
 
     f32x16 acc[2][2];
@@ -173,6 +175,161 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
         __syncthreads();
     }
     // D[row][col]: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn * 64 + j * 32 + r32;
+            if (col >= a.Co) continue;
+            const float bv = a.bias ? a.bias[col] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= a.M) continue;
+                float v = acc[i][j][r] + bv;
+                if (a.res) v += a.res[row * a.Co + col];
+                a.y[row * a.ldy + col] = act_h(v, a.act);
+            }
+        }
+}
+
+// ---- k_conv_h16b: Ci % 64 == 0 (the ResNet trunk) -----------------------------------------------------------------
+// k_conv_h16's K step of 32 gives each wave only 8 MFMAs (256 cycles) per barrier and prefetches one step ahead, so
+// the global-load latency is exposed.  Here a K step is 64 deep (one tap, 64 channels: 16 MFMAs per wave and step)
+// and the operands of steps s + 1 and s + 2 are in flight in two register sets while step s runs (ping-pong, two
+// steps per trip, no copies).  Same fragment map, same per-output K order (16-deep slices in increasing k): results
+// identical to k_conv_h16.
+constexpr int HBK2 = 64, HROW2 = 72;  // halves per LDS row: 64 + 8 pad = 144 B = 9 odd 16-B slots
+
+__global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2][(HBM + HBN) * HROW2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int ntn = (a.Co + HBN - 1) / HBN;
+    const int64_t ntm = (a.M + HBM - 1) / HBM;
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int64_t mt = bid / (unsigned)ntn;
+    const int nt = (int)(bid % (unsigned)ntn);
+    if (mt >= ntm) return;
+    const int64_t m0 = mt * HBM;
+    const int n0 = nt * HBN;
+    // A staging: rows (tid >> 2) + 64 q (q < 2), channel quads (tid & 3) + 4 u (u < 4): 64 channels per step,
+    // two rows of tap metadata per thread
+    const int aq = tid & 3;
+    int64_t pix[2];
+    int iy0[2], ix0[2];
+    bool rok[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int64_t m = m0 + (tid >> 2) + 64 * q;
+        rok[q] = m < a.M;
+        const int64_t mm = rok[q] ? m : 0;
+        const int ox = (int)(mm % a.Wo);
+        const int64_t t = mm / a.Wo;
+        const int oy = (int)(t % a.Ho);
+        const int n = (int)(t / a.Ho);
+        pix[q] = (int64_t)n * a.H * a.W * a.Ci + 4 * aq;
+        iy0[q] = oy * a.stride - a.pad;
+        ix0[q] = ox * a.stride - a.pad;
+    }
+    // B staging: weight row n0 + (tid >> 1), halves 32 (tid & 1) .. + 31 of the K step
+    const _Float16 *wrow = a.wp + (int64_t)(n0 + (tid >> 1)) * a.Kp + 32 * (tid & 1);
+    int ky = 0, kx = 0, ci0 = 0;
+    int64_t kb = 0;
+    f32x4 ra0[8], ra1[8];
+    u32x4 rb0[4], rb1[4];
+#define H16_GLOAD(RA, RB)                                                                                  \
+    do {                                                                                                   \
+        const int dy = ky * a.dil, dx = kx * a.dil;                                                        \
+        _Pragma("unroll") for (int q = 0; q < 2; ++q) {                                                    \
+            const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                                  \
+            const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;        \
+            const float *src = in ? a.x + pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 : g_hzero4;       \
+            const int st = in ? 16 : 0; /* the zero quad is re-read for every u */                         \
+            _Pragma("unroll") for (int u = 0; u < 4; ++u) RA[4 * q + u] = *(const f32x4 *)(src + st * u);  \
+        }                                                                                                  \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u) RB[u] = *(const u32x4 *)(wrow + kb + 8 * u);         \
+        kb += HBK2;                                                                                        \
+        ci0 += HBK2;                                                                                       \
+        if (ci0 == a.Ci) {                                                                                 \
+            ci0 = 0;                                                                                       \
+            if (++kx == a.KW) {                                                                            \
+                kx = 0;                                                                                    \
+                ++ky;                                                                                      \
+            }                                                                                              \
+        }                                                                                                  \
+    } while (0)
+#define H16_SWRITE(BUF, RA, RB)                                                                            \
+    do {                                                                                                   \
+        _Float16 *As = lds[BUF], *Bs = As + HBM * HROW2;                                                   \
+        _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                    \
+            const h16x4 hv = {(_Float16)RA[q][0], (_Float16)RA[q][1], (_Float16)RA[q][2], (_Float16)RA[q][3]}; \
+            *(h16x4 *)(As + ((tid >> 2) + 64 * (q >> 2)) * HROW2 + 4 * aq + 16 * (q & 3)) = hv;            \
+        }                                                                                                  \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u)                                                      \
+            *(u32x4 *)(Bs + (tid >> 1) * HROW2 + 32 * (tid & 1) + 8 * u) = RB[u];                          \
+    } while (0)
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    const int r32 = lane & 31, h = lane >> 5;
+#define H16_MFMA(BUF)                                                                                      \
+    do {                                                                                                   \
+        const _Float16 *As = lds[BUF], *Bs = As + HBM * HROW2;                                             \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk) {                                                 \
+            h16x8 fa[2], fb[2];                                                                            \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                  \
+                fa[i] = *(const h16x8 *)(As + (wm * 64 + i * 32 + r32) * HROW2 + kk * 16 + 8 * h);         \
+            _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
+                fb[j] = *(const h16x8 *)(Bs + (wn * 64 + j * 32 + r32) * HROW2 + kk * 16 + 8 * h);         \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                  \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);  \
+            __builtin_amdgcn_sched_barrier(0); /* one slice of fragments live at a time (VGPR budget) */   \
+        }                                                                                                  \
+    } while (0)
+    const int nk = a.Kp / HBK2;
+    H16_GLOAD(ra0, rb0);
+    if (nk > 1) H16_GLOAD(ra1, rb1);
+    H16_SWRITE(0, ra0, rb0);
+    __syncthreads();
+    int ks = 0;  // loop head: LDS buffer 0 holds step ks, register set 1 step ks + 1
+    for (; ks + 3 < nk; ks += 2) {
+        H16_GLOAD(ra0, rb0);
+        H16_MFMA(0);
+        H16_SWRITE(1, ra1, rb1);
+        __syncthreads();
+        H16_GLOAD(ra1, rb1);
+        H16_MFMA(1);
+        H16_SWRITE(0, ra0, rb0);
+        __syncthreads();
+    }
+    if (ks + 2 < nk) {
+        H16_GLOAD(ra0, rb0);
+        H16_MFMA(0);
+        H16_SWRITE(1, ra1, rb1);
+        __syncthreads();
+        H16_MFMA(1);
+        H16_SWRITE(0, ra0, rb0);
+        __syncthreads();
+        H16_MFMA(0);
+    } else if (ks + 1 < nk) {
+        H16_MFMA(0);
+        H16_SWRITE(1, ra1, rb1);
+        __syncthreads();
+        H16_MFMA(1);
+    } else {
+        H16_MFMA(0);
+    }
+#undef H16_MFMA
+#undef H16_SWRITE
+#undef H16_GLOAD
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -319,6 +476,15 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16(const float *__restrict__ 
 
 }  // namespace
 
+namespace bev {
+int conv_h16_tune(int value) {
+    if (value < 0 || value > 1) return BEV_ERR_ARGS;
+    const int old = g_h16_kernel;
+    g_h16_kernel = value;
+    return old;
+}
+}  // namespace bev
+
 extern "C" {
 
 int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
@@ -385,7 +551,10 @@ int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16
     a.M = (int64_t)N * Ho * Wo;
     const int64_t blocks = ((a.M + HBM - 1) / HBM) * ((Co + HBN - 1) / HBN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL(k_conv_h16, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    if (Ci % HBK2 == 0 && g_h16_kernel == 0)
+        hipLaunchKernelGGL(k_conv_h16b, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    else
+        hipLaunchKernelGGL(k_conv_h16, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
 }
 

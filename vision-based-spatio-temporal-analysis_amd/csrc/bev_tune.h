@@ -13,4 +13,7 @@ int train_tune(int knob, int value);
 // BEV_TUNE_CONV_X6_TILE / BEV_TUNE_CONV_X6_KERNEL (bev_conv_x6.hip).
 int conv_x6_tune(int knob, int value);
 
+// BEV_TUNE_CONV_H16_KERNEL (bev_conv_h16.hip).
+int conv_h16_tune(int value);
+
 }  // namespace bev
