@@ -75,9 +75,9 @@ class _ViewProjection(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             parts = []
             for v in range(V):
-                acc = _nat.conv_wgrad_ex(fl[:, v], dgn[:, v], 1, 0, 1) if B == 1 else \
-                    sum(_nat.conv_wgrad_ex(fl[b, v][None], dgn[b, v][None], 1, 0, 1) for b in range(B))
-                parts.append(acc.reshape(P, C))
+                # one weight-gradient launch over the view's B images (the kernel reduces over every pixel of the
+                # batch; conv_wgrad_ex gathers the view's slices, strided by V images, when B > 1)
+                parts.append(_nat.conv_wgrad_ex(fl[:, v], dgn[:, v], 1, 0, 1).reshape(P, C))
             # [P, V*C] storage with the parameter's strides (the per-view OIHW views are channels-last-strided;
             # DDP's bucket views compare strides exactly)
             dw = torch.cat(parts, dim=1).view(P, V * C, 1, 1)
