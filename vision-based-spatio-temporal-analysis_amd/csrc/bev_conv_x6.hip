@@ -122,11 +122,23 @@ __device__ __forceinline__ void x6_epilogue(const ConvX &a, float *lds, const f3
     const int r32 = lane & 31, h = lane >> 5;
     constexpr int WC = TN * 32, ER = WC + 4;
     constexpr int C4 = WC / 4, RPI = 64 / C4, NQ = 32 / RPI;
-    __syncthreads();  // every wave is done with the staging buffers
     float *E = lds + wave * (32 * ER);
     const int c4 = lane % C4, rq = lane / C4;
     const int n = n0 + wn * WC + c4 * 4;
     const bool nvec = ((a.Co & 3) == 0) && ((a.ldy & 3) == 0) && (n + 3 < a.Co);
+    // each pass's residual loads go out before its LDS traffic (the first pass's before the barrier)
+    float4 rv[NQ];
+    auto res_load = [&](int i) {
+        const int64_t mb = m0 + wm * TM * 32 + i * 32;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int64_t m = mb + rq + RPI * q;
+            rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
+        }
+    };
+    res_load(0);
+    __syncthreads();  // every wave is done with the staging buffers
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
     if (a.bias) {
         if (nvec) bv = *(const float4 *)(a.bias + n);
@@ -145,13 +157,7 @@ __device__ __forceinline__ void x6_epilogue(const ConvX &a, float *lds, const f3
 #pragma unroll
             for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * h) * ER + j * 32 + r32] = acc[i][j][r];
         const int64_t mbase = m0 + wm * TM * 32 + i * 32;
-        float4 rv[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int64_t m = mbase + rq + RPI * q;
-            rv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (a.res && m < a.M && nvec) rv[q] = *(const float4 *)(a.res + m * a.Co + n);
-        }
+        if (i > 0) res_load(i);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int row = rq + RPI * q;
@@ -415,6 +421,25 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
     static_assert(NB * WPB == 4, "chain epilogue: 4 waves over the 32-row bands");
     __bf16 *H = (__bf16 *)lds_raw;
     const int r32 = lane & 31, hh = lane >> 5;
+    // residual of this wave's first chunk: requested before the h2 staging, so its latency overlaps it
+    const int band = (wave % NB) * 32, part = wave / NB;
+    const int64_t rows = (a.M - m0 < BM) ? a.M - m0 : BM;
+    const int64_t base = m0 * a.Co2;
+    const __amdgpu_buffer_rsrc_t rr = x6_rsrc(a.res ? a.res + base : a.y + base, rows * a.Co2 * 4);
+    const int vo = ((band + 4 * hh) * a.Co2 + r32) * 4;  // lane part of a res / y address
+    const int nch = a.Co2 / 64 / WPB;                     // this wave's 64-column chunks: [part * nch, (part + 1) * nch)
+    float rvn[2][16];
+    auto res_load = [&](int c0) {
+        if (!a.res) return;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                rvn[j][r] = __builtin_bit_cast(
+                    float, __builtin_amdgcn_raw_buffer_load_b32(rr, vo + ((r & 3) + 8 * (r >> 2)) * a.Co2 * 4,
+                                                                (c0 + 32 * j) * 4, 0));
+    };
+    res_load(64 * part * nch);
     __syncthreads();  // every wave is done with the staging buffers
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -435,7 +460,6 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
     __syncthreads();
     constexpr int S2 = BN / 16;      // 16-deep slices of conv3's K from h2
     constexpr int ST = S2 + X2S;     // slices of the panel
-    const int band = (wave % NB) * 32, part = wave / NB;
     bf16x8 fx[X2S > 0 ? X2S : 1][3];  // the shortcut operand, split (dual form)
     if constexpr (X2S > 0) {
         int64_t m = m0 + band + r32;
@@ -459,26 +483,17 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
         }
     }
     const __bf16 *ap = H + (band + r32) * HR + 8 * hh;
-    const int64_t rows = (a.M - m0 < BM) ? a.M - m0 : BM;
-    const int64_t base = m0 * a.Co2;
     const __amdgpu_buffer_rsrc_t ry = x6_rsrc(a.y + base, rows * a.Co2 * 4);
-    const __amdgpu_buffer_rsrc_t rr = x6_rsrc(a.res ? a.res + base : a.y + base, rows * a.Co2 * 4);
     const __amdgpu_buffer_rsrc_t rw = x6_rsrc(a.wp2, copad_x(a.Co2) / 32 * (int64_t)ST * 3072);
-    const int vo = ((band + 4 * hh) * a.Co2 + r32) * 4;  // lane part of a res / y address
     const int vl = lane * 16;
-    const int nch = a.Co2 / 64 / WPB;  // this wave's 64-column chunks: [part * nch, (part + 1) * nch)
     for (int nc = part * nch; nc < (part + 1) * nch; ++nc) {
         const int c0 = 64 * nc;
         float rv[2][16];
-        if (a.res) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    rv[j][r] = __builtin_bit_cast(
-                        float, __builtin_amdgcn_raw_buffer_load_b32(rr, vo + ((r & 3) + 8 * (r >> 2)) * a.Co2 * 4,
-                                                                    (c0 + 32 * j) * 4, 0));
-        }
+            for (int r = 0; r < 16; ++r) rv[j][r] = rvn[j][r];
+        if (nc + 1 < (part + 1) * nch) res_load(c0 + 64);  // the next chunk's residual, during these MFMAs
         f32x16 acc2[2] = {(f32x16){0}, (f32x16){0}};
 #pragma unroll
         for (int t = 0; t < ST; ++t) {

@@ -308,7 +308,9 @@ class ResNet(nn.Module):
         # chained kernels (conv2 output in LDS, no HBM round trip) -- measured faster where the 1x1 tails are
         # HBM-bound -- and whether conv1 hands conv2 a pre-split operand (k_conv_x6s).
         self.f32_chain_stages = set()
-        self.x6_chain_stages = {1}  # stages whose bottleneck bodies run as one split-arithmetic chained launch
+        # stages whose bottleneck bodies run as one split-arithmetic chained launch (r03 tools/trunk_ab.py, encoder ms
+        # per 2-frame step: none 17.06, {1} 16.02-16.21, {1, 2} 15.97-16.01)
+        self.x6_chain_stages = {1, 2}
         self.split_edges = False
         self.stream_groups = 2
         self.stream_offset = 0  # > 0: group g waits for group g - 1 to pass this launch stage (staggered start)
