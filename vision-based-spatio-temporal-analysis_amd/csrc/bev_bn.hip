@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_act.h"
 
 namespace {
 
@@ -41,7 +42,7 @@ struct Stats {  // (z, z^2)
 
 // SiLU' (u) = s (1 + u (1 - s)), s = sigmoid(u) = 1 / (1 + exp(-u)) (torch's SiLU backward)
 __device__ __forceinline__ float silu_grad(float u) {
-    const float sg = 1.0f / (1.0f + expf(-u));
+    const float sg = sigmoid_hw(u);
     return sg * (1.0f + u * (1.0f - sg));
 }
 
@@ -192,8 +193,7 @@ __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__re
         }
         if (act == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
         if (act == 2)  // torch SiLU: x / (1 + exp(-x))
-            o = make_float4(o.x / (1.0f + expf(-o.x)), o.y / (1.0f + expf(-o.y)), o.z / (1.0f + expf(-o.z)),
-                            o.w / (1.0f + expf(-o.w)));
+            o = make_float4(silu_hw(o.x), silu_hw(o.y), silu_hw(o.z), silu_hw(o.w));
         *(float4 *)(y + e) = o;
     }
 }

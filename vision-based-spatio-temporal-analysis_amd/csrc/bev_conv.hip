@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_act.h"
 #include "bev_tune.h"
 
 namespace {
@@ -66,7 +67,7 @@ __global__ void k_pack(const float *__restrict__ w, int Co, int Ci, int KH, int 
 
 // Epilogue activation: 1 = ReLU, 2 = SiLU (torch: x / (1 + exp(-x)); EfficientNet trunk).
 __device__ __forceinline__ float act_fn(float t, int act) {
-    if (act == 2) return t / (1.0f + expf(-t));
+    if (act == 2) return silu_hw(t);
     return t > 0.0f ? t : 0.0f;
 }
 

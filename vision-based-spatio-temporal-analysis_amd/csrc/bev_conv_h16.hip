@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_act.h"
 
 namespace {
 
@@ -65,7 +66,7 @@ struct ConvH {
 };
 
 __device__ __forceinline__ float act_h(float t, int act) {
-    if (act == 2) return t / (1.0f + expf(-t));
+    if (act == 2) return silu_hw(t);
     if (act == 1) return t > 0.0f ? t : 0.0f;
     return t;
 }

@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_act.h"
 
 namespace {
 
@@ -105,7 +106,7 @@ struct ConvX {
 };
 
 __device__ __forceinline__ float act_x(float t, int act) {
-    if (act == 2) return t / (1.0f + expf(-t));
+    if (act == 2) return silu_hw(t);
     if (act == 1) return t > 0.0f ? t : 0.0f;
     return t;
 }

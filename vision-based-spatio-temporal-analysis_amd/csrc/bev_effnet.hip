@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "../../include/bev_mi355x.h"
+#include "bev_act.h"
 
 namespace {
 
@@ -37,7 +38,7 @@ inline int dw_ppb(int C) { return DW_STEPS * (DW_NT / dw_ch4(C)); }
 
 __device__ __forceinline__ float act_f(float t, int act) {
     if (act == 1) return t > 0.0f ? t : 0.0f;
-    if (act == 2) return t / (1.0f + expf(-t));  // torch SiLU: x / (1 + exp(-x))
+    if (act == 2) return silu_hw(t);  // torch SiLU x / (1 + exp(-x)), hardware exp2 / rcp (bev_act.h)
     return t;
 }
 
@@ -259,13 +260,13 @@ __global__ __launch_bounds__(SE_NT) void k_se_gate(const float *__restrict__ psu
     for (int j = threadIdx.x; j < rd; j += blockDim.x) {
         float t = b1[j];
         for (int c = 0; c < C; ++c) t = __builtin_fmaf(w1[(int64_t)j * C + c], mean[c], t);
-        r[j] = t / (1.0f + expf(-t));  // SiLU (conv_reduce -> act1)
+        r[j] = silu_hw(t);  // SiLU (conv_reduce -> act1)
     }
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
         float t = b2[c];
         for (int j = 0; j < rd; ++j) t = __builtin_fmaf(w2[(int64_t)c * rd + j], r[j], t);
-        gate[(int64_t)n * C + c] = 1.0f / (1.0f + expf(-t));  // conv_expand -> sigmoid gate
+        gate[(int64_t)n * C + c] = sigmoid_hw(t);  // conv_expand -> sigmoid gate
     }
 }
 
