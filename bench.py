@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--conv-arith", choices=("bf16x6", "f32"), default="bf16x6",
                     help="trunk conv arithmetic: bf16x6 = fp32 through exact 3-way bf16 splits (default), f32 = the "
                          "exact-f32 MFMA kernels")
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=V",
+                    help="set a performance knob (include/bev_mi355x.h BEV_TUNE_<NAME>) before the run; repeatable")
     ap.add_argument("--warp-kernel", choices=("dma", "register", "wave", "persist"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
     args = ap.parse_args()
@@ -354,6 +356,9 @@ def main():
     images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
     nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1, "wave": 2, "persist": 3}[args.warp_kernel])
+    for kv in args.tune:
+        name, v = kv.split("=")
+        nat.tune(getattr(nat, "TUNE_" + name.upper()), int(v))
     nat.set_conv_arith(args.conv_arith)
     stream = torch.cuda.current_stream(dev)
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]

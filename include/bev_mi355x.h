@@ -60,7 +60,9 @@ int bev_abi_version(void);
  *   wherever Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel (both operands through LDS) for every shape.
  *   Same results bit for bit.
  * BEV_TUNE_CONV_H16_KERNEL: autocast fp16 convs: 0 (default) = 64-deep K steps, two steps in flight, where Ci % 64 ==
- *   0; 1 = the 32-deep-step kernel always.  Same results bit for bit. */
+ *   0; 1 = the 32-deep-step kernel always.  Same results bit for bit.
+ * BEV_TUNE_CONV_PW_SMALL: 0 (default) = 1x1 convs with Co in {16, 24, 32, 40, 48} (EfficientNet projections) on
+ *   the MFMA tiles, 1 = on a per-pixel VALU kernel (fp32-tolerance equal; measured slower, kept for A/B). */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -72,6 +74,7 @@ int bev_abi_version(void);
 #define BEV_TUNE_CONV_X6_TILE 10
 #define BEV_TUNE_CONV_X6_KERNEL 11
 #define BEV_TUNE_CONV_H16_KERNEL 12
+#define BEV_TUNE_CONV_PW_SMALL 13
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

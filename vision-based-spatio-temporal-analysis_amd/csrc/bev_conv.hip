@@ -37,6 +37,7 @@ constexpr int BK = 32;        // K step
 constexpr int LROW = BK + 4;  // LDS row stride in floats (144 B: 9 slots, odd -> conflict-free b128 rows)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));  // native vector: promotes to VGPRs reliably
 
 // 16 zero bytes in device memory: out-of-range operand taps load from here (an unconditional load
@@ -1197,6 +1198,91 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
     return last();
 }
 
+// ---------------------------------------------------------------------------
+// Narrow pointwise convs (1x1, Co <= 48: the EfficientNet projections to 24 / 32 / 40 / 48 channels, up to
+// 518 400 pixels per image): an MFMA tile is >= 64 columns wide, so 33-62 % of its work is padding and the K loop
+// (Ci = 24 .. 288) is one to nine steps -- these layers ran at 1/3 of the HBM rate.  One thread per output pixel
+// computes its Co outputs on the VALU from the pixel's Ci inputs (two float4 loads per 8 channels, the
+// per-(image, channel) SE gate applied to them as in the MFMA loaders).  The weights are wave-uniform, so they come
+// through the scalar cache into SGPRs (s_load of 8 consecutive k of one output channel, read straight from the
+// fp32 panel [Co][Kp]) and feed packed FMAs: acc[co] = {sum over even k, sum over odd k} on v_pk_fma_f32, added at
+// the end.  Epilogue bias, residual, activation as conv_epilogue.  HBM-bound: (Ci + Co (+ Co)) floats per pixel.
+// Measured (profiles/r03h_pw_small_ab.txt, EfficientNet-B3 bench): 107.9 frames/s against 121.9 on the MFMA
+// tiles -- the per-lane rows (stride Ci floats) thrash the L1 and every 8 k the wave waits on the scalar cache
+// (55 KB of weights for 288 -> 48 does not fit it), so the layers stay on the MFMA tiles by default
+// (BEV_TUNE_CONV_PW_SMALL = 0); 1 selects this kernel.
+int g_conv_pw_small = 0;
+
+template <int CO>
+__global__ __launch_bounds__(256) void k_pw_small(ConvArgs a) {
+    const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (m >= a.M) return;
+    const int Ci = a.Ci, Kp = a.Kp;
+    const float *xp = a.x + m * Ci;
+    const float *gp = a.ascale ? a.ascale + (m / ((int64_t)a.Ho * a.Wo)) * Ci : nullptr;
+    const float *__restrict__ wp = a.wp;
+    f32x2 acc[CO];
+#pragma unroll
+    for (int co = 0; co < CO; ++co) acc[co] = (f32x2){0.f, 0.f};
+    f32x4 x0 = *(const f32x4 *)xp, x1 = *(const f32x4 *)(xp + 4);
+    for (int c0 = 0; c0 < Ci; c0 += 8) {
+        f32x4 u0 = x0, u1 = x1;
+        if (c0 + 8 < Ci) {  // next 8 channels in flight during these FMAs
+            x0 = *(const f32x4 *)(xp + c0 + 8);
+            x1 = *(const f32x4 *)(xp + c0 + 12);
+        }
+        if (gp) {
+            u0 *= *(const f32x4 *)(gp + c0);
+            u1 *= *(const f32x4 *)(gp + c0 + 4);
+        }
+        const f32x2 xa = {u0[0], u0[1]}, xb = {u0[2], u0[3]}, xc = {u1[0], u1[1]}, xd = {u1[2], u1[3]};
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+            const float *w = wp + co * Kp + c0;  // wave-uniform: scalar loads
+            acc[co] = __builtin_elementwise_fma(xa, (f32x2){w[0], w[1]}, acc[co]);
+            acc[co] = __builtin_elementwise_fma(xb, (f32x2){w[2], w[3]}, acc[co]);
+            acc[co] = __builtin_elementwise_fma(xc, (f32x2){w[4], w[5]}, acc[co]);
+            acc[co] = __builtin_elementwise_fma(xd, (f32x2){w[6], w[7]}, acc[co]);
+        }
+    }
+    float *yp = a.y + m * a.ldy;
+    const float *rp = a.res ? a.res + m * a.Co : nullptr;
+#pragma unroll
+    for (int q = 0; q < CO / 4; ++q) {
+        f32x4 o = {acc[4 * q][0] + acc[4 * q][1], acc[4 * q + 1][0] + acc[4 * q + 1][1],
+                   acc[4 * q + 2][0] + acc[4 * q + 2][1], acc[4 * q + 3][0] + acc[4 * q + 3][1]};
+        if (a.bias) o += *(const f32x4 *)(a.bias + 4 * q);
+        if (rp) o += *(const f32x4 *)(rp + 4 * q);
+        if (a.relu) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u] = act_fn(o[u], a.relu);
+        }
+        *(f32x4 *)(yp + 4 * q) = o;
+    }
+}
+
+// the layer takes k_pw_small (true) -- launched here -- or the MFMA tiles (false)
+bool try_pw_small(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
+    if (!g_conv_pw_small || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
+        a.stride != 1 || a.pad != 0 || a.in_nchw || a.ashift || a.arelu || a.dil != 1 || a.ldy != a.Co ||
+        a.Ci % 8 != 0 || a.Ci > 512 || a.Kp < a.Ci ||
+        ((((uintptr_t)a.x) | ((uintptr_t)a.y) | ((uintptr_t)a.bias) | ((uintptr_t)a.res) | ((uintptr_t)a.ascale)) & 15))
+        return false;
+    const int64_t blocks = (a.M + 255) / 256;
+    if (blocks > 0x7fffffff) return false;
+    const size_t sh = 0;
+    switch (a.Co) {
+        case 16: hipLaunchKernelGGL(k_pw_small<16>, dim3((unsigned)blocks), dim3(256), sh, st, a); break;
+        case 24: hipLaunchKernelGGL(k_pw_small<24>, dim3((unsigned)blocks), dim3(256), sh, st, a); break;
+        case 32: hipLaunchKernelGGL(k_pw_small<32>, dim3((unsigned)blocks), dim3(256), sh, st, a); break;
+        case 40: hipLaunchKernelGGL(k_pw_small<40>, dim3((unsigned)blocks), dim3(256), sh, st, a); break;
+        case 48: hipLaunchKernelGGL(k_pw_small<48>, dim3((unsigned)blocks), dim3(256), sh, st, a); break;
+        default: return false;
+    }
+    rc = last();
+    return true;
+}
+
 int g_conv_tile = 0;
 
 // XCD-aware block order (k_conv): on by default since the smaller r01f/r01g tiles put 2-4 N tiles
@@ -1216,6 +1302,8 @@ inline int conv_xcd() { return g_conv_xcd; }
 // -8..-13 %).  Small-M 128x64 launches (< 2 full rounds) keep the double
 // buffer.  BEV_TUNE_CONV_NBUF = 1|2 forces the staging depth of tiles 2 / 3.
 int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
+    int rc_pw = 0;
+    if (g_conv_tile == 0 && try_pw_small(a, loader, st, rc_pw)) return rc_pw;
     const int64_t M = a.M;
     const int Co = a.Co;
     const int nbuf_env = g_conv_nbuf;
@@ -1291,6 +1379,12 @@ int bev_tune(int knob, int value) {
     if (knob == BEV_TUNE_WGRAD_MFMA) return bev::train_tune(knob, value);
     if (knob == BEV_TUNE_CONV_X6_TILE || knob == BEV_TUNE_CONV_X6_KERNEL) return bev::conv_x6_tune(knob, value);
     if (knob == BEV_TUNE_CONV_H16_KERNEL) return bev::conv_h16_tune(value);
+    if (knob == BEV_TUNE_CONV_PW_SMALL) {
+        if (value < 0 || value > 1) return BEV_ERR_ARGS;
+        const int old = g_conv_pw_small;
+        g_conv_pw_small = value;
+        return old;
+    }
     return bev::warp_tune(knob, value);
 }
 
