@@ -80,7 +80,9 @@ DW_CASES = [  # N, C, H, W, K, stride, act
     (2, 96, 13, 11, 3, 2, 0),    # tiled, stride 2
     (1, 320, 10, 9, 5, 2, 2),    # tiled, 10 channel chunks, k5 s2
     (1, 20, 9, 12, 3, 1, 2),     # odd channel-quad count: per-pixel kernel
-    (1, 36, 11, 7, 5, 2, 0),     # odd quads, k5 s2: per-pixel kernel
+    (1, 36, 11, 7, 5, 2, 0),     # odd quads, k5 s2: row-run kernel
+    (2, 24, 13, 37, 3, 1, 2),    # row runs of 8, ragged last run
+    (1, 40, 10, 29, 3, 2, 2),    # row runs of 4 at stride 2, ragged
 ]
 
 
@@ -110,6 +112,29 @@ def test_dwconv_and_se_vs_torch_fp32(case):
     nat.channel_scale_(y, gate)
     exc = (ref * g_ref[:, :, None, None]).numpy()
     np.testing.assert_allclose(y.permute(0, 3, 1, 2).cpu().numpy(), exc, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(2, 24, 13, 37, 3, 1, 2), (1, 40, 10, 29, 3, 2, 2), (1, 144, 17, 21, 3, 2, 2),
+                                  (1, 20, 9, 12, 3, 1, 0), (1, 36, 11, 7, 5, 2, 2), (1, 28, 12, 19, 5, 1, 2),
+                                  (1, 192, 11, 19, 5, 2, 2), (1, 288, 9, 13, 5, 1, 2), (1, 384, 7, 9, 3, 1, 2)],
+                         ids=lambda c: f"c{c[1]}_k{c[4]}s{c[5]}")
+def test_dwconv_row_runs_match_per_pixel(case):
+    """k_dwconv_r (BEV_TUNE_DW_RUN=1) == k_dwconv (=0): same taps in the same order, so y is identical up to the
+    sign of an exact zero (compared after + 0.0); the SE partials sum the same outputs in another grouping
+    (per-image totals within fp32 tolerance)."""
+    import bev_native as nat
+    N, C, H, W, K, s, act = case
+    xd = _rand((N, H, W, C), 31).to(DEV)
+    wt = _rand((K * K, C), 32, 0.3).to(DEV)
+    b = _rand((C,), 33, 0.1).to(DEV)
+    with nat.tuned(DW_RUN=0):
+        y0, p0 = nat.dwconv2d_nhwc(xd, wt, b, K, s, K // 2, act, want_psum=True)
+    for run in (1, 2, 3):  # 2: every kernel row's loads issued up front (3 x 3); 3: row runs for every width
+        with nat.tuned(DW_RUN=run):
+            y1, p1 = nat.dwconv2d_nhwc(xd, wt, b, K, s, K // 2, act, want_psum=True)
+        assert torch.equal(y1 + 0.0, y0 + 0.0)
+        np.testing.assert_allclose(p1.sum(1).cpu().numpy(), p0.sum(1).cpu().numpy(), rtol=1e-5, atol=1e-4)
 
 
 @pytest.mark.gpu

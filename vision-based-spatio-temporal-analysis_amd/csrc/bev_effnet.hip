@@ -112,6 +112,126 @@ __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, i
 }
 
 
+// Row-run depthwise K x K for narrow channel counts (C / 4 <= 64 quads, where the LDS tile loses: B3's 540 x 960 C 24 /
+// C 40 and 270 x 480 C 144 stride-2 layers).  A thread owns one channel quad of R consecutive outputs of one row;
+// for each kernel row it loads the (R - 1) * S + K input pixels the run needs once into registers and applies them
+// to all R outputs, so every input quad is fetched once per kernel row and run instead of K times per output (the
+// per-pixel kernel's K * K tap loads per output were bound by the L1 / address rate, 0.28 of HBM on those layers).
+// The C / 4 lanes of a run read each pixel as one contiguous segment.  Per output the taps are applied in
+// k_dwconv's order (ky-major, kx-minor; out-of-range rows skipped, out-of-range columns read as 0, so y matches
+// k_dwconv up to the sign of an exact zero); SE partials per workgroup in a fixed order.
+// BEV_TUNE_DW_RUN: 0 keeps these layers on k_dwconv; 1 row runs; 2 (default) row runs with every kernel row's loads
+// issued up front for 3 x 3 (more VGPRs, fewer exposed latencies); 3 row runs also for the widths the LDS tile takes.
+// r03i (EfficientNet-B3 bench, profiles/r03i_dw_run_ab.txt): per-pixel -> runs -> up front: 540 x 960 C 24
+// 623 -> 421 -> 401 us, C 40 1031 -> 701 -> 671, 270 x 480 C 144 s2 1271 -> 1039 -> 980; 120.1 -> 126.5 frames/s.
+int g_dw_run = 2;
+template <int S> constexpr int dw_run_len() { return S == 1 ? 8 : 4; }
+inline int dw_run_ch4(int C) {
+    const int C4 = C / 4;
+    for (int d = 1; d <= 16; ++d)
+        if (C4 % d == 0 && C4 / d <= 64) return C4 / d;
+    return 0;
+}
+
+template <int K, int S, bool UP>
+__global__ __launch_bounds__(DW_NT) void k_dwconv_r(const float *__restrict__ x, int H, int W, int C,
+                                                    const float *__restrict__ wt, const float *__restrict__ bias,
+                                                    int pad, int act, float *__restrict__ y, int Ho, int Wo,
+                                                    float *__restrict__ psum, int nb, int CH4) {
+    constexpr int R = dw_run_len<S>(), IC = (R - 1) * S + K;
+    __shared__ float4 red[DW_NT];
+    const int PB = DW_NT / CH4;  // runs per workgroup; CH4 channel quads per workgroup (blockIdx.z chunks)
+    const int tid = threadIdx.x, pl = tid / CH4, q = blockIdx.z * CH4 + (tid - pl * CH4);
+    const int n = blockIdx.y, blk = blockIdx.x;
+    const int rpr = (Wo + R - 1) / R;
+    const int64_t ri = (int64_t)blk * PB + pl;
+    const bool active = pl < PB && ri < (int64_t)Ho * rpr;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (active) {
+        const int oy = (int)(ri / rpr), ox0 = (int)(ri - (int64_t)oy * rpr) * R;
+        const int ix0 = ox0 * S - pad;
+        float4 w[K * K];
+#pragma unroll
+        for (int t = 0; t < K * K; ++t) w[t] = *(const float4 *)(wt + (int64_t)t * C + q * 4);
+        const float4 b = *(const float4 *)(bias + q * 4);
+        float4 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = b;
+        const float *xn = x + (int64_t)n * H * W * C + q * 4;
+        float4 vu[UP ? K : 1][IC];
+        if (UP) {  // every row's loads in flight at once (out-of-range rows read as 0)
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) {
+                const int iy = oy * S - pad + ky;
+                const bool rin = iy >= 0 && iy < H;
+                const float *xr = xn + (int64_t)(rin ? iy : 0) * W * C;
+#pragma unroll
+                for (int c = 0; c < IC; ++c) {
+                    const int ix = ix0 + c;
+                    vu[UP ? ky : 0][c] = (rin && ix >= 0 && ix < W) ? *(const float4 *)(xr + (int64_t)ix * C)
+                                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky) {
+            const int iy = oy * S - pad + ky;
+            float4 v[IC];
+            if (UP) {
+#pragma unroll
+                for (int c = 0; c < IC; ++c) v[c] = vu[UP ? ky : 0][c];
+            } else {
+                if (iy < 0 || iy >= H) continue;
+                const float *xr = xn + (int64_t)iy * W * C;
+#pragma unroll
+                for (int c = 0; c < IC; ++c) {
+                    const int ix = ix0 + c;
+                    v[c] = (ix >= 0 && ix < W) ? *(const float4 *)(xr + (int64_t)ix * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+                    const float4 vv = v[r * S + kx], ww = w[ky * K + kx];
+                    acc[r].x = __builtin_fmaf(vv.x, ww.x, acc[r].x);
+                    acc[r].y = __builtin_fmaf(vv.y, ww.y, acc[r].y);
+                    acc[r].z = __builtin_fmaf(vv.z, ww.z, acc[r].z);
+                    acc[r].w = __builtin_fmaf(vv.w, ww.w, acc[r].w);
+                }
+            }
+        }
+        float *yr = y + (((int64_t)n * Ho + oy) * Wo + ox0) * C + q * 4;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (ox0 + r >= Wo) break;
+            float4 o = acc[r];
+            o.x = act_f(o.x, act);
+            o.y = act_f(o.y, act);
+            o.z = act_f(o.z, act);
+            o.w = act_f(o.w, act);
+            *(float4 *)(yr + (int64_t)r * C) = o;
+            s.x += o.x;
+            s.y += o.y;
+            s.z += o.z;
+            s.w += o.w;
+        }
+    }
+    if (psum == nullptr) return;
+    red[tid] = s;
+    __syncthreads();
+    if (pl == 0) {  // fixed order over the runs: deterministic partial
+        for (int l = 1; l < PB; ++l) {
+            const float4 t = red[l * CH4 + (tid - pl * CH4)];
+            s.x += t.x;
+            s.y += t.y;
+            s.z += t.z;
+            s.w += t.w;
+        }
+        *(float4 *)(psum + ((int64_t)n * nb + blk) * C + q * 4) = s;
+    }
+}
+
 // LDS-tiled depthwise conv: a workgroup owns an 8-row output-pixel tile x DQ channel quads (DQ = 8: 32 channels =
 // one 128-B line of every pixel, 8 columns; DQ = 4: 8 columns; DQ = 2: 16 columns).  The tile's input patch is
 // staged in LDS once (pixel stride DQ + 1 quads: conflict-free ds_read_b128 for stride 1 and 2), so the K*K taps
@@ -371,13 +491,37 @@ extern "C" {
 inline int dw_tiled_dq(int Ho, int Wo, int C, int stride) {
     const int dq = dw_dq(C);
     if (stride != 1 && stride != 2) return 0;
+    if (g_dw_run == 3 && dw_run_ch4(C) > 0) return 0;  // row runs for every width
     return (dq == 8 || (dq > 0 && (int64_t)Ho * Wo <= 65536)) ? dq : 0;
 }
+
+// k_dwconv_r: stride 1 / 2; channel quads per workgroup = C / 4 split into equal chunks of at most 64
+inline bool dw_use_run(int stride, int C) {
+    return g_dw_run && (stride == 1 || stride == 2) && (C / 4 <= 64 || (g_dw_run == 3 && dw_run_ch4(C) > 0));
+}
+inline int dw_run_blocks(int Ho, int Wo, int C, int stride) {
+    const int R = stride == 1 ? dw_run_len<1>() : dw_run_len<2>(), PB = DW_NT / dw_run_ch4(C);
+    return (int)(((int64_t)Ho * ((Wo + R - 1) / R) + PB - 1) / PB);
+}
+
+}  // namespace
+
+namespace bev {
+int dw_tune(int value) {
+    if (value < 0 || value > 3) return BEV_ERR_ARGS;
+    const int old = g_dw_run;
+    g_dw_run = value;
+    return old;
+}
+}  // namespace bev
+
+extern "C" {
 
 int bev_dwconv_psum_blocks(int Ho, int Wo, int C, int stride) {
     if (Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0 || stride <= 0) return BEV_ERR_ARGS;
     const int dq = dw_tiled_dq(Ho, Wo, C, stride);
     if (dq) return dt_tiles(Ho, Wo, dq);  // one SE partial per output tile
+    if (dw_use_run(stride, C)) return dw_run_blocks(Ho, Wo, C, stride);
     const int ppb = dw_ppb(C);
     return (int)(((int64_t)Ho * Wo + ppb - 1) / ppb);
 }
@@ -395,6 +539,32 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
     if (N == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const int dq = dw_tiled_dq(Ho, Wo, C, stride);
+    if (!dq && dw_use_run(stride, C)) {
+        const int nb = dw_run_blocks(Ho, Wo, C, stride), CH4 = dw_run_ch4(C);
+        dim3 grid(nb, N, C / 4 / CH4);
+        if (g_dw_run == 2 && K == 3) {
+            if (stride == 1)
+                hipLaunchKernelGGL((k_dwconv_r<3, 1, true>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y,
+                                   Ho, Wo, psum, nb, CH4);
+            else
+                hipLaunchKernelGGL((k_dwconv_r<3, 2, true>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y,
+                                   Ho, Wo, psum, nb, CH4);
+            return last();
+        }
+        if (K == 3 && stride == 1)
+            hipLaunchKernelGGL((k_dwconv_r<3, 1, false>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                               psum, nb, CH4);
+        else if (K == 3)
+            hipLaunchKernelGGL((k_dwconv_r<3, 2, false>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                               psum, nb, CH4);
+        else if (stride == 1)
+            hipLaunchKernelGGL((k_dwconv_r<5, 1, false>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                               psum, nb, CH4);
+        else
+            hipLaunchKernelGGL((k_dwconv_r<5, 2, false>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo,
+                               psum, nb, CH4);
+        return last();
+    }
     if (!dq) {
         const int nb = bev_dwconv_psum_blocks(Ho, Wo, C, stride), ppb = dw_ppb(C);
         const int C4 = C / 4, CH4 = dw_ch4(C);

@@ -16,4 +16,7 @@ int conv_x6_tune(int knob, int value);
 // BEV_TUNE_CONV_H16_KERNEL (bev_conv_h16.hip).
 int conv_h16_tune(int value);
 
+// BEV_TUNE_DW_RUN (bev_effnet.hip).
+int dw_tune(int value);
+
 }  // namespace bev
