@@ -64,8 +64,8 @@ int bev_abi_version(void);
  * BEV_TUNE_CONV_PW_SMALL: 0 (default) = 1x1 convs with Co in {16, 24, 32, 40, 48} (EfficientNet projections) on
  *   the MFMA tiles, 1 = on a per-pixel VALU kernel (fp32-tolerance equal; measured slower, kept for A/B).
  * BEV_TUNE_DW_RUN: depthwise convs with <= 256 channels that the LDS tile does not take: 0 = per pixel (k_dwconv),
- *   1 = row runs (k_dwconv_r), 2 (default) = row runs with the 3 x 3 rows' loads issued up front, 3 = row runs for
- *   every width (also where the LDS tile would run).  Same y up to the sign of an exact zero; the SE partial count
+ *   1 = row runs (k_dwconv_r), 2 = row runs with the 3 x 3 rows' loads issued up front, 3 (default) = 2 for every
+ *   width (also where the LDS tile k_dwconv_t ran).  Same y up to the sign of an exact zero; the SE partial count
  *   per bev_dwconv_psum_blocks, which follows the knob. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2

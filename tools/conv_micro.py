@@ -35,6 +35,15 @@ LAYERS = {
     "l2.1.c3": (128, 512, 1, 1, 135, 240, True, False),
     "proj": (512, 64, 1, 1, 135, 240, False, False),
     "g512": (512, 512, 1, 1, 135, 240, False, False),  # plain GEMM shape (M 226800 x N 512 x K 512): loop ceiling
+    # EfficientNet-B3 pointwise layers at 1080p (stride-2 stem: 540 x 960)
+    "b3.p40": (40, 24, 1, 1, 540, 960, False, False),
+    "b3.p24": (24, 24, 1, 1, 540, 960, True, False),
+    "b3.e24": (24, 144, 1, 1, 540, 960, False, False),
+    "b3.p144": (144, 32, 1, 1, 270, 480, False, False),
+    "b3.e32": (32, 192, 1, 1, 270, 480, False, False),
+    "b3.p192": (192, 32, 1, 1, 270, 480, True, False),
+    "b3.e48": (48, 288, 1, 1, 135, 240, False, False),
+    "b3.p288": (288, 48, 1, 1, 135, 240, True, False),
 }
 # fused bottleneck tails (bev_conv2d_dual_f32): name: (Ci conv3 in, Ci2 block in, Co, s2, H2, W2)
 DUAL = {

@@ -120,11 +120,13 @@ __global__ __launch_bounds__(DW_NT) void k_dwconv(const float *__restrict__ x, i
 // The C / 4 lanes of a run read each pixel as one contiguous segment.  Per output the taps are applied in
 // k_dwconv's order (ky-major, kx-minor; out-of-range rows skipped, out-of-range columns read as 0, so y matches
 // k_dwconv up to the sign of an exact zero); SE partials per workgroup in a fixed order.
-// BEV_TUNE_DW_RUN: 0 keeps these layers on k_dwconv; 1 row runs; 2 (default) row runs with every kernel row's loads
-// issued up front for 3 x 3 (more VGPRs, fewer exposed latencies); 3 row runs also for the widths the LDS tile takes.
+// BEV_TUNE_DW_RUN: 0 keeps these layers on k_dwconv; 1 row runs; 2 row runs with every kernel row's loads issued up
+// front for 3 x 3 (more VGPRs, fewer exposed latencies); 3 (default) = 2 also for the widths the LDS tile took.
 // r03i (EfficientNet-B3 bench, profiles/r03i_dw_run_ab.txt): per-pixel -> runs -> up front: 540 x 960 C 24
-// 623 -> 421 -> 401 us, C 40 1031 -> 701 -> 671, 270 x 480 C 144 s2 1271 -> 1039 -> 980; 120.1 -> 126.5 frames/s.
-int g_dw_run = 2;
+// 623 -> 421 -> 401 us, C 40 1031 -> 701 -> 671, 270 x 480 C 144 s2 1271 -> 1039 -> 980 (120.1 -> 126.8 frames/s);
+// LDS tile -> runs: 270 x 480 C 192 k3 819 -> 706, 135 x 240 C 288 k5 645 -> 439, C 192 k5 s2 1105 -> 522 us
+// (127.1 -> 136.0 frames/s).
+int g_dw_run = 3;
 template <int S> constexpr int dw_run_len() { return S == 1 ? 8 : 4; }
 inline int dw_run_ch4(int C) {
     const int C4 = C / 4;
@@ -542,7 +544,7 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
     if (!dq && dw_use_run(stride, C)) {
         const int nb = dw_run_blocks(Ho, Wo, C, stride), CH4 = dw_run_ch4(C);
         dim3 grid(nb, N, C / 4 / CH4);
-        if (g_dw_run == 2 && K == 3) {
+        if (g_dw_run >= 2 && K == 3) {
             if (stride == 1)
                 hipLaunchKernelGGL((k_dwconv_r<3, 1, true>), grid, dim3(DW_NT), 0, st, x, H, W, C, wt, bias, pad, act, y,
                                    Ho, Wo, psum, nb, CH4);
