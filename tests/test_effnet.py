@@ -175,7 +175,8 @@ def test_effnet_encoder_vs_torch_fp32(name, out_index):
 @pytest.mark.parametrize("Ci,Co,act,gated,res", [(40, 24, 0, False, False), (24, 24, 0, True, True),
                                                   (144, 32, 0, True, False), (24, 16, 2, False, True),
                                                   (288, 48, 1, True, True), (1024, 16, 0, False, False),
-                                                  (96, 40, 2, True, False)])
+                                                  (96, 40, 2, True, False), (24, 144, 2, False, False),
+                                                  (48, 288, 2, False, False), (32, 192, 2, True, True)])
 def test_pw_small_matches_mfma_tiles(Ci, Co, act, gated, res):
     """Narrow 1x1 convs on the per-pixel VALU kernel (BEV_TUNE_CONV_PW_SMALL=1) == the MFMA tiles (=0) and torch
     fp32 within fp32 tolerance (rtol/atol 1e-4; same products, accumulation order differs), with the SE gate,
@@ -188,16 +189,17 @@ def test_pw_small_matches_mfma_tiles(Ci, Co, act, gated, res):
     r = _rand((N, H, W, Co), 23).to(DEV) if res else None
     conv = torch.nn.Conv2d(Ci, Co, 1, bias=True).to(DEV)
     fc = FoldedConv(conv)
-    with nat.tuned(CONV_PW_SMALL=1):
-        a = fc(x, relu=act, residual=r, ascale=gate)
     with nat.tuned(CONV_PW_SMALL=0):
         b = fc(x, relu=act, residual=r, ascale=gate)
     xin = x * gate[:, None, None, :] if gated else x
     ref = F.conv2d(xin.permute(0, 3, 1, 2).cpu(), conv.weight.detach().cpu(), conv.bias.detach().cpu())
     ref = ref.permute(0, 2, 3, 1) + (r.cpu() if res else 0)
     ref = {0: ref, 1: torch.relu(ref), 2: F.silu(ref)}[act]
-    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(a.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    for kern in (1, 2, 3):  # 1: per-pixel VALU (Co <= 48); 2, 3: wave-streaming MFMA (Ci in {24, 32, 40, 48})
+        with nat.tuned(CONV_PW_SMALL=kern):
+            a = fc(x, relu=act, residual=r, ascale=gate)
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(a.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.gpu

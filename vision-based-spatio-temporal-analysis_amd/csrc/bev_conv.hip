@@ -1209,9 +1209,9 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
 // the end.  Epilogue bias, residual, activation as conv_epilogue.  HBM-bound: (Ci + Co (+ Co)) floats per pixel.
 // Measured (profiles/r03h_pw_small_ab.txt, EfficientNet-B3 bench): 107.9 frames/s against 121.9 on the MFMA
 // tiles -- the per-lane rows (stride Ci floats) thrash the L1 and every 8 k the wave waits on the scalar cache
-// (55 KB of weights for 288 -> 48 does not fit it), so the layers stay on the MFMA tiles by default
-// (BEV_TUNE_CONV_PW_SMALL = 0); 1 selects this kernel.
-int g_conv_pw_small = 0;
+// (55 KB of weights for 288 -> 48 does not fit it), so the layers stay on the MFMA tiles (BEV_TUNE_CONV_PW_SMALL
+// 0) or k_pw_mfma below (2, default; 3); 1 selects this kernel.
+int g_conv_pw_small = 2;
 
 template <int CO>
 __global__ __launch_bounds__(256) void k_pw_small(ConvArgs a) {
@@ -1261,9 +1261,87 @@ __global__ __launch_bounds__(256) void k_pw_small(ConvArgs a) {
     }
 }
 
+// Wave-streaming 1x1 conv for tiny K (Ci in {24, 32, 40, 48}: EfficientNet's 24 -> 144 expansion and 40 / 24 -> 24
+// projections at 540 x 960), BEV_TUNE_CONV_PW_SMALL = 2.  The tiled kernels spend one K step per tile between an
+// operand load and an epilogue (nothing to overlap: 0.3 of HBM).  Here every wave owns 32 pixels and is independent
+// (no LDS, no barrier): lane (i = pixel, h = k half) loads its pixel's k in [h K/2, (h + 1) K/2) straight into
+// registers (float4 pieces of one contiguous row) and the matching weight row piece of output channel i of each
+// 32-channel block, so MFMA k-slot h of step s multiplies x[m][h K/2 + s] by W[co][h K/2 + s] -- a permutation
+// of the k order (fp32-tolerance equal to the tiles); D[(r & 3) + 8 (r >> 2) + 4 h][lane & 31] gets bias,
+// residual, activation and is stored 32 channels (128 B) per half-wave.
+template <int KH2>
+__global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 31, h = lane >> 5;
+    const int64_t mw = ((int64_t)blockIdx.x * 4 + wave) * 32;  // the wave's first pixel
+    if (mw >= a.M) return;
+    const int64_t m = mw + i < a.M ? mw + i : a.M - 1;
+    const int Ci = a.Ci;
+    float av[KH2];
+    {
+        const float *xp = a.x + m * Ci + h * KH2;
+        const float *gp = a.ascale ? a.ascale + (m / ((int64_t)a.Ho * a.Wo)) * Ci + h * KH2 : nullptr;
+#pragma unroll
+        for (int u = 0; u < KH2 / 4; ++u) {
+            f32x4 v = *(const f32x4 *)(xp + 4 * u);
+            if (gp) v *= *(const f32x4 *)(gp + 4 * u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) av[4 * u + e] = v[e];
+        }
+    }
+    const int nbt = (a.Co + 31) / 32;
+    for (int nb = 0; nb < nbt; ++nb) {
+        const int co = nb * 32 + i;  // B column of this lane; also the output channel of its D column
+        const float *wr = a.wp + (int64_t)co * a.Kp + h * KH2;  // panel rows are zero-padded to 128
+        float bv[KH2];
+#pragma unroll
+        for (int u = 0; u < KH2 / 4; ++u) {
+            const f32x4 v = *(const f32x4 *)(wr + 4 * u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bv[4 * u + e] = v[e];
+        }
+        f32x16 acc = {};
+#pragma unroll
+        for (int st = 0; st < KH2; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], bv[st], acc, 0, 0, 0);
+        if (co >= a.Co) continue;
+        const float b = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t mo = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (mo >= a.M) continue;
+            float o = acc[r] + b;
+            if (a.res) o += a.res[mo * a.Co + co];
+            if (a.relu) o = act_fn(o, a.relu);
+            a.y[mo * a.ldy + co] = o;
+        }
+    }
+}
+
+// Taken (BEV_TUNE_CONV_PW_SMALL = 2, default) where it measured faster: narrow outputs without a residual --
+// r03j micro (profiles/r03j_b3_pointwise_micro.txt, 7 x 1080p): 40 -> 24 482 -> 257 us; with a residual (24 -> 24,
+// per-lane scalar residual loads) 353 -> 510, and the wide expansions 24 -> 144 / 32 -> 192 / 48 -> 288 within
+// +-5 % of the tiles.  3 = every tiny-K 1x1 layer.
+bool try_pw_mfma(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
+    if (g_conv_pw_small < 2 || (g_conv_pw_small == 2 && (a.res || a.Co > 32)) || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
+        a.stride != 1 || a.pad != 0 || a.in_nchw || a.ashift || a.arelu || a.dil != 1 || a.Kp < a.Ci ||
+        !(a.Ci == 24 || a.Ci == 32 || a.Ci == 40 || a.Ci == 48) ||
+        ((((uintptr_t)a.x) | ((uintptr_t)a.wp) | ((uintptr_t)a.ascale)) & 15))
+        return false;
+    const int64_t blocks = (a.M + 127) / 128;
+    if (blocks > 0x7fffffff) return false;
+    const dim3 g((unsigned)blocks), b(256);
+    switch (a.Ci) {
+        case 24: hipLaunchKernelGGL(k_pw_mfma<12>, g, b, 0, st, a); break;
+        case 32: hipLaunchKernelGGL(k_pw_mfma<16>, g, b, 0, st, a); break;
+        case 40: hipLaunchKernelGGL(k_pw_mfma<20>, g, b, 0, st, a); break;
+        default: hipLaunchKernelGGL(k_pw_mfma<24>, g, b, 0, st, a); break;
+    }
+    rc = last();
+    return true;
+}
+
 // the layer takes k_pw_small (true) -- launched here -- or the MFMA tiles (false)
 bool try_pw_small(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
-    if (!g_conv_pw_small || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
+    if (g_conv_pw_small != 1 || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
         a.stride != 1 || a.pad != 0 || a.in_nchw || a.ashift || a.arelu || a.dil != 1 || a.ldy != a.Co ||
         a.Ci % 8 != 0 || a.Ci > 512 || a.Kp < a.Ci ||
         ((((uintptr_t)a.x) | ((uintptr_t)a.y) | ((uintptr_t)a.bias) | ((uintptr_t)a.res) | ((uintptr_t)a.ascale)) & 15))
@@ -1304,6 +1382,7 @@ inline int conv_xcd() { return g_conv_xcd; }
 int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
     int rc_pw = 0;
     if (g_conv_tile == 0 && try_pw_small(a, loader, st, rc_pw)) return rc_pw;
+    if (g_conv_tile == 0 && try_pw_mfma(a, loader, st, rc_pw)) return rc_pw;
     const int64_t M = a.M;
     const int Co = a.Co;
     const int nbuf_env = g_conv_nbuf;
@@ -1328,6 +1407,11 @@ int launch_tiled(const ConvArgs &a, int loader, hipStream_t st) {
         // parallelism.  r01f A/B over ResNet-50: every such layer -1..-19 % (proj 209 -> 170 us,
         // layer1 conv1 400 -> 352 us); 3x3 layers and the dual-source tails are slower with it.
         if (a.KH == 1 && a.KW == 1 && (loader == 1 || loader == 6) && M >= 200000) tile = 4;
+        // The same for the contiguous-row loader (Ci % 4 == 0: EfficientNet's 24 / 40 / 144-channel inputs) when
+        // the output is narrow or K is not tiny: r03i micro (profiles/r03i_b3_pointwise_tile_micro.txt, 7 x 1080p
+        // B3 layers) 40 -> 24 480 -> 420 us, 24 -> 24 375 -> 338, 144 -> 32 236 -> 204, 48 -> 288 164 -> 141;
+        // 24 -> 144 is slower with it (968 -> 1030) and keeps 128 x 64.
+        if (a.KH == 1 && a.KW == 1 && loader == 4 && M >= 200000 && (Co <= 64 || a.Ci >= 48)) tile = 4;
     }
     if (tile == 2)
         return nbuf1_for(2) ? launch_conv<4, 1, 1, 2, 1>(a, loader, st) : launch_conv<4, 1, 1, 2>(a, loader, st);
@@ -1381,7 +1465,7 @@ int bev_tune(int knob, int value) {
     if (knob == BEV_TUNE_CONV_H16_KERNEL) return bev::conv_h16_tune(value);
     if (knob == BEV_TUNE_DW_RUN) return bev::dw_tune(value);
     if (knob == BEV_TUNE_CONV_PW_SMALL) {
-        if (value < 0 || value > 1) return BEV_ERR_ARGS;
+        if (value < 0 || value > 3) return BEV_ERR_ARGS;
         const int old = g_conv_pw_small;
         g_conv_pw_small = value;
         return old;
