@@ -1270,6 +1270,32 @@ __global__ __launch_bounds__(256) void k_pw_small(ConvArgs a) {
 // of the k order (fp32-tolerance equal to the tiles); D[(r & 3) + 8 (r >> 2) + 4 h][lane & 31] gets bias,
 // residual, activation and is stored 32 channels (128 B) per half-wave.
 template <int KH2>
+__device__ __forceinline__ void pw_load_b(const ConvArgs &a, int co, int h, float (&bv)[KH2]) {
+    const float *wr = a.wp + (int64_t)co * a.Kp + h * KH2;  // panel rows are zero-padded to 128
+#pragma unroll
+    for (int u = 0; u < KH2 / 4; ++u) {
+        const f32x4 v = *(const f32x4 *)(wr + 4 * u);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[4 * u + e] = v[e];
+    }
+}
+
+__device__ __forceinline__ void pw_store(const ConvArgs &a, const f32x16 &acc, int64_t mw, int h, int co) {
+    if (co >= a.Co) return;
+    const float b = a.bias ? a.bias[co] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t mo = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (mo >= a.M) continue;
+        float o = acc[r] + b;
+        if (a.res) o += a.res[mo * a.Co + co];
+        if (a.relu) o = act_fn(o, a.relu);
+        a.y[mo * a.ldy + co] = o;
+    }
+}
+
+// NP output blocks of 32 channels per pass: NP independent MFMA chains interleaved (NP = 1 launched: see below)
+template <int KH2, int NP>
 __global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 31, h = lane >> 5;
     const int64_t mw = ((int64_t)blockIdx.x * 4 + wave) * 32;  // the wave's first pixel
@@ -1289,30 +1315,20 @@ __global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
         }
     }
     const int nbt = (a.Co + 31) / 32;
-    for (int nb = 0; nb < nbt; ++nb) {
-        const int co = nb * 32 + i;  // B column of this lane; also the output channel of its D column
-        const float *wr = a.wp + (int64_t)co * a.Kp + h * KH2;  // panel rows are zero-padded to 128
-        float bv[KH2];
+    for (int nb = 0; nb < nbt; nb += NP) {
+        float bv[NP][KH2];
+        f32x16 acc[NP];
 #pragma unroll
-        for (int u = 0; u < KH2 / 4; ++u) {
-            const f32x4 v = *(const f32x4 *)(wr + 4 * u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) bv[4 * u + e] = v[e];
+        for (int p = 0; p < NP; ++p) {
+            pw_load_b<KH2>(a, (nb + p) * 32 + i, h, bv[p]);  // rows past Co: zero padding (< copad)
+            acc[p] = (f32x16){};
         }
-        f32x16 acc = {};
 #pragma unroll
-        for (int st = 0; st < KH2; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], bv[st], acc, 0, 0, 0);
-        if (co >= a.Co) continue;
-        const float b = a.bias ? a.bias[co] : 0.f;
+        for (int st = 0; st < KH2; ++st)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int64_t mo = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (mo >= a.M) continue;
-            float o = acc[r] + b;
-            if (a.res) o += a.res[mo * a.Co + co];
-            if (a.relu) o = act_fn(o, a.relu);
-            a.y[mo * a.ldy + co] = o;
-        }
+            for (int p = 0; p < NP; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], bv[p][st], acc[p], 0, 0, 0);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) pw_store(a, acc[p], mw, h, (nb + p) * 32 + i);
     }
 }
 
@@ -1329,11 +1345,13 @@ bool try_pw_mfma(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
     const int64_t blocks = (a.M + 127) / 128;
     if (blocks > 0x7fffffff) return false;
     const dim3 g((unsigned)blocks), b(256);
-    switch (a.Ci) {
-        case 24: hipLaunchKernelGGL(k_pw_mfma<12>, g, b, 0, st, a); break;
-        case 32: hipLaunchKernelGGL(k_pw_mfma<16>, g, b, 0, st, a); break;
-        case 40: hipLaunchKernelGGL(k_pw_mfma<20>, g, b, 0, st, a); break;
-        default: hipLaunchKernelGGL(k_pw_mfma<24>, g, b, 0, st, a); break;
+    {  // NP = 2 (two chains in flight, 188 VGPRs) measured slower on 24 -> 144: 953 -> 1230 us (r03m)
+        switch (a.Ci) {
+            case 24: hipLaunchKernelGGL((k_pw_mfma<12, 1>), g, b, 0, st, a); break;
+            case 32: hipLaunchKernelGGL((k_pw_mfma<16, 1>), g, b, 0, st, a); break;
+            case 40: hipLaunchKernelGGL((k_pw_mfma<20, 1>), g, b, 0, st, a); break;
+            default: hipLaunchKernelGGL((k_pw_mfma<24, 1>), g, b, 0, st, a); break;
+        }
     }
     rc = last();
     return true;
