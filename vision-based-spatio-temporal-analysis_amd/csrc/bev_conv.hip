@@ -1283,12 +1283,18 @@ __device__ __forceinline__ void pw_load_b(const ConvArgs &a, int co, int h, floa
 __device__ __forceinline__ void pw_store(const ConvArgs &a, const f32x16 &acc, int64_t mw, int h, int co) {
     if (co >= a.Co) return;
     const float b = a.bias ? a.bias[co] : 0.f;
+    float rv[16];  // every residual load issued before the first store (the compiler cannot reorder them past it)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t mo = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
+        rv[r] = (a.res && mo < a.M) ? a.res[mo * a.Co + co] : 0.f;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int64_t mo = mw + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (mo >= a.M) continue;
         float o = acc[r] + b;
-        if (a.res) o += a.res[mo * a.Co + co];
+        if (a.res) o += rv[r];
         if (a.relu) o = act_fn(o, a.relu);
         a.y[mo * a.ldy + co] = o;
     }
@@ -1332,12 +1338,12 @@ __global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
     }
 }
 
-// Taken (BEV_TUNE_CONV_PW_SMALL = 2, default) where it measured faster: narrow outputs without a residual --
-// r03j micro (profiles/r03j_b3_pointwise_micro.txt, 7 x 1080p): 40 -> 24 482 -> 257 us; with a residual (24 -> 24,
-// per-lane scalar residual loads) 353 -> 510, and the wide expansions 24 -> 144 / 32 -> 192 / 48 -> 288 within
-// +-5 % of the tiles.  3 = every tiny-K 1x1 layer.
+// Taken (BEV_TUNE_CONV_PW_SMALL = 2, default) where it measured faster: narrow outputs (Co <= 32) -- r03j micro
+// (profiles/r03j_b3_pointwise_micro.txt, 7 x 1080p): 40 -> 24 482 -> 257 us (24 -> 24 + residual lost, 353 -> 510,
+// while each residual load waited behind the previous store; now all 16 are issued first); the wide expansions
+// 24 -> 144 / 32 -> 192 / 48 -> 288 are within +-5 % of the tiles.  3 = every tiny-K 1x1 layer.
 bool try_pw_mfma(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
-    if (g_conv_pw_small < 2 || (g_conv_pw_small == 2 && (a.res || a.Co > 32)) || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
+    if (g_conv_pw_small < 2 || (g_conv_pw_small == 2 && a.Co > 32) || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
         a.stride != 1 || a.pad != 0 || a.in_nchw || a.ashift || a.arelu || a.dil != 1 || a.Kp < a.Ci ||
         !(a.Ci == 24 || a.Ci == 32 || a.Ci == 40 || a.Ci == 48) ||
         ((((uintptr_t)a.x) | ((uintptr_t)a.wp) | ((uintptr_t)a.ascale)) & 15))
