@@ -62,9 +62,10 @@ int bev_abi_version(void);
  * BEV_TUNE_CONV_H16_KERNEL: autocast fp16 convs: 0 (default) = 64-deep K steps, two steps in flight, where Ci % 64 ==
  *   0; 1 = the 32-deep-step kernel always.  Same results bit for bit.
  * BEV_TUNE_CONV_PW_SMALL: narrow / tiny-K 1x1 convs (EfficientNet): 0 = the MFMA tiles; 1 = Co in
- *   {16, 24, 32, 40, 48} on a per-pixel VALU kernel (measured slower, kept for A/B); 2 (default) = Ci in
- *   {24, 32, 40, 48}, Co <= 32 on a wave-streaming MFMA kernel (k_pw_mfma); 3 = every Ci in
- *   {24, 32, 40, 48} 1x1 on k_pw_mfma.  All fp32-tolerance equal.
+ *   {16, 24, 32, 40, 48} on a per-pixel VALU kernel (measured slower, kept for A/B); 2 (default) = 1x1 with
+ *   Ci in {24, 32, 40, 48} and Co <= 32 on a wave-streaming MFMA kernel (k_pw_mfma, float4 epilogue through
+ *   LDS); 3 = every 1x1 with Ci in {24, 32, 40, 48} on it (faster inference); 4 = as 2 with dword stores.
+ *   All fp32-tolerance equal.
  * BEV_TUNE_DW_RUN: depthwise convs with <= 256 channels that the LDS tile does not take: 0 = per pixel (k_dwconv),
  *   1 = row runs (k_dwconv_r), 2 = row runs with the 3 x 3 rows' loads issued up front, 3 (default) = 2 for every
  *   width (also where the LDS tile k_dwconv_t ran).  Same y up to the sign of an exact zero; the SE partial count

@@ -195,7 +195,7 @@ def test_pw_small_matches_mfma_tiles(Ci, Co, act, gated, res):
     ref = F.conv2d(xin.permute(0, 3, 1, 2).cpu(), conv.weight.detach().cpu(), conv.bias.detach().cpu())
     ref = ref.permute(0, 2, 3, 1) + (r.cpu() if res else 0)
     ref = {0: ref, 1: torch.relu(ref), 2: F.silu(ref)}[act]
-    for kern in (1, 2, 3):  # 1: per-pixel VALU (Co <= 48); 2, 3: wave-streaming MFMA (Ci in {24, 32, 40, 48})
+    for kern in (1, 2, 3, 4):  # 1: per-pixel VALU (Co <= 48); 2-4: wave-streaming MFMA (Ci in {24, 32, 40, 48})
         with nat.tuned(CONV_PW_SMALL=kern):
             a = fc(x, relu=act, residual=r, ascale=gate)
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-4)

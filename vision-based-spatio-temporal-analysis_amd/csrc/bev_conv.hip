@@ -101,6 +101,7 @@ struct ConvArgs {
     const float *__restrict__ wp2;
     const float *__restrict__ bias2;
     int Co2, Kp2, relu2;
+    int pwvec;  // k_pw_mfma: float4 epilogue through LDS (set by try_pw_mfma)
 };
 
 // Per-thread view of the A tile rows it loads: rows (tid >> 3) + 32 r, one 16-B quad.
@@ -1210,7 +1211,7 @@ int launch_conv(const ConvArgs &a, int loader, hipStream_t st) {
 // Measured (profiles/r03h_pw_small_ab.txt, EfficientNet-B3 bench): 107.9 frames/s against 121.9 on the MFMA
 // tiles -- the per-lane rows (stride Ci floats) thrash the L1 and every 8 k the wave waits on the scalar cache
 // (55 KB of weights for 288 -> 48 does not fit it), so the layers stay on the MFMA tiles (BEV_TUNE_CONV_PW_SMALL
-// 0) or k_pw_mfma below (2, default; 3); 1 selects this kernel.
+// 0) or k_pw_mfma below (2, default; 3; 4); 1 selects this kernel.
 int g_conv_pw_small = 2;
 
 template <int CO>
@@ -1269,6 +1270,7 @@ __global__ __launch_bounds__(256) void k_pw_small(ConvArgs a) {
 // 32-channel block, so MFMA k-slot h of step s multiplies x[m][h K/2 + s] by W[co][h K/2 + s] -- a permutation
 // of the k order (fp32-tolerance equal to the tiles); D[(r & 3) + 8 (r >> 2) + 4 h][lane & 31] gets bias,
 // residual, activation and is stored 32 channels (128 B) per half-wave.
+
 template <int KH2>
 __device__ __forceinline__ void pw_load_b(const ConvArgs &a, int co, int h, float (&bv)[KH2]) {
     const float *wr = a.wp + (int64_t)co * a.Kp + h * KH2;  // panel rows are zero-padded to 128
@@ -1300,10 +1302,44 @@ __device__ __forceinline__ void pw_store(const ConvArgs &a, const f32x16 &acc, i
     }
 }
 
+// Vector epilogue (Co % 4 == 0, 16-B aligned y / res / bias, ldy % 4 == 0): the 32 x 32 block goes through a
+// wave-private LDS tile and leaves as float4 rows -- 4 store instructions per block instead of 16 dword ones.
+__device__ __forceinline__ void pw_store_v(const ConvArgs &a, const f32x16 &acc, int64_t mw, int lane, int nb,
+                                           float *E) {
+    constexpr int ER = 36;  // row stride (floats): float4 reads of 8 lanes per row spread over the banks
+    const int h = lane >> 5, c = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) E[((r & 3) + 8 * (r >> 2) + 4 * h) * ER + c] = acc[r];
+    const int c4 = lane & 7, co = nb * 32 + 4 * c4;
+    if (co >= a.Co) return;
+    const f32x4 b = a.bias ? *(const f32x4 *)(a.bias + co) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    f32x4 rv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t mo = mw + (lane >> 3) + 8 * q;
+        rv[q] = (a.res && mo < a.M) ? *(const f32x4 *)(a.res + mo * a.Co + co) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int pr = (lane >> 3) + 8 * q;
+        const int64_t mo = mw + pr;
+        if (mo >= a.M) continue;
+        f32x4 o = *(const f32x4 *)(E + pr * ER + 4 * c4) + b;
+        if (a.res) o += rv[q];
+        if (a.relu) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = act_fn(o[e], a.relu);
+        }
+        *(f32x4 *)(a.y + mo * a.ldy + co) = o;
+    }
+}
+
 // NP output blocks of 32 channels per pass: NP independent MFMA chains interleaved (NP = 1 launched: see below)
 template <int KH2, int NP>
 __global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
+    __shared__ __attribute__((aligned(16))) float epi[4][32 * 36];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 31, h = lane >> 5;
+    const bool vec = a.pwvec != 0;
     const int64_t mw = ((int64_t)blockIdx.x * 4 + wave) * 32;  // the wave's first pixel
     if (mw >= a.M) return;
     const int64_t m = mw + i < a.M ? mw + i : a.M - 1;
@@ -1334,16 +1370,22 @@ __global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
 #pragma unroll
             for (int p = 0; p < NP; ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[st], bv[p][st], acc[p], 0, 0, 0);
 #pragma unroll
-        for (int p = 0; p < NP; ++p) pw_store(a, acc[p], mw, h, (nb + p) * 32 + i);
+        for (int p = 0; p < NP; ++p) {
+            if (vec) pw_store_v(a, acc[p], mw, lane, nb + p, epi[wave]);
+            else pw_store(a, acc[p], mw, h, (nb + p) * 32 + i);
+        }
     }
 }
 
-// Taken (BEV_TUNE_CONV_PW_SMALL = 2, default) where it measured faster: narrow outputs (Co <= 32) -- r03j micro
-// (profiles/r03j_b3_pointwise_micro.txt, 7 x 1080p): 40 -> 24 482 -> 257 us (24 -> 24 + residual lost, 353 -> 510,
-// while each residual load waited behind the previous store; now all 16 are issued first); the wide expansions
-// 24 -> 144 / 32 -> 192 / 48 -> 288 are within +-5 % of the tiles.  3 = every tiny-K 1x1 layer.
+// BEV_TUNE_CONV_PW_SMALL: 2 (default) = narrow outputs (Co <= 32) only, 3 = every tiny-K 1x1 layer, 4 = narrow only
+// with the dword epilogue.  3 is faster for inference but not the default: its k order on the wide expansions
+// moves one EfficientNet-B0 training gradient (test_effnet_trunk_backward_vs_torch_autograd, blocks.0.0.bn2.bias)
+// to 1.007e-3 relative against float64 autograd, past the test's 1e-3 bound (r03q).  r03p micro (profiles/r03p_pw_mfma_vec_ab.txt, 7 x 1080p, us; tiles -> dword epilogue ->
+// float4 epilogue): 40 -> 24 420 -> 344 -> 270, 24 -> 24 + residual 337 -> 294 -> 223, 24 -> 144 927 -> (921) -> 747,
+// 32 -> 192 287 -> 242.  (r03j: with the dword epilogue the wide expansions were within +-5 % of the tiles, and each
+// residual load waited behind the previous store until all 16 were issued first.)
 bool try_pw_mfma(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
-    if (g_conv_pw_small < 2 || (g_conv_pw_small == 2 && a.Co > 32) || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
+    if (g_conv_pw_small < 2 || (g_conv_pw_small != 3 && a.Co > 32) || !(loader == 1 || loader == 4 || loader == 6) || a.KH != 1 || a.KW != 1 ||
         a.stride != 1 || a.pad != 0 || a.in_nchw || a.ashift || a.arelu || a.dil != 1 || a.Kp < a.Ci ||
         !(a.Ci == 24 || a.Ci == 32 || a.Ci == 40 || a.Ci == 48) ||
         ((((uintptr_t)a.x) | ((uintptr_t)a.wp) | ((uintptr_t)a.ascale)) & 15))
@@ -1351,12 +1393,15 @@ bool try_pw_mfma(const ConvArgs &a, int loader, hipStream_t st, int &rc) {
     const int64_t blocks = (a.M + 127) / 128;
     if (blocks > 0x7fffffff) return false;
     const dim3 g((unsigned)blocks), b(256);
+    ConvArgs av = a;  // float4 epilogue when the output rows allow it (knob 4: dword stores, for A/B)
+    av.pwvec = g_conv_pw_small != 4 && a.Co % 4 == 0 && a.ldy % 4 == 0 &&
+               ((((uintptr_t)a.y) | ((uintptr_t)a.res) | ((uintptr_t)a.bias)) & 15) == 0;
     {  // NP = 2 (two chains in flight, 188 VGPRs) measured slower on 24 -> 144: 953 -> 1230 us (r03m)
         switch (a.Ci) {
-            case 24: hipLaunchKernelGGL((k_pw_mfma<12, 1>), g, b, 0, st, a); break;
-            case 32: hipLaunchKernelGGL((k_pw_mfma<16, 1>), g, b, 0, st, a); break;
-            case 40: hipLaunchKernelGGL((k_pw_mfma<20, 1>), g, b, 0, st, a); break;
-            default: hipLaunchKernelGGL((k_pw_mfma<24, 1>), g, b, 0, st, a); break;
+            case 24: hipLaunchKernelGGL((k_pw_mfma<12, 1>), g, b, 0, st, av); break;
+            case 32: hipLaunchKernelGGL((k_pw_mfma<16, 1>), g, b, 0, st, av); break;
+            case 40: hipLaunchKernelGGL((k_pw_mfma<20, 1>), g, b, 0, st, av); break;
+            default: hipLaunchKernelGGL((k_pw_mfma<24, 1>), g, b, 0, st, av); break;
         }
     }
     rc = last();
@@ -1489,7 +1534,7 @@ int bev_tune(int knob, int value) {
     if (knob == BEV_TUNE_CONV_H16_KERNEL) return bev::conv_h16_tune(value);
     if (knob == BEV_TUNE_DW_RUN) return bev::dw_tune(value);
     if (knob == BEV_TUNE_CONV_PW_SMALL) {
-        if (value < 0 || value > 3) return BEV_ERR_ARGS;
+        if (value < 0 || value > 4) return BEV_ERR_ARGS;
         const int old = g_conv_pw_small;
         g_conv_pw_small = value;
         return old;
