@@ -86,6 +86,10 @@ def parse():
                     help="set a performance knob (include/bev_mi355x.h BEV_TUNE_<NAME>) before the run; repeatable")
     ap.add_argument("--warp-kernel", choices=("dma", "register", "wave", "persist"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="orchestration check on the CPU (gloo): the rank spawning, barriers, timing and MAX "
+                         "reduction of this script with a placeholder step (rank r sleeps (r + 1) x 5 ms); no hot "
+                         "path runs and the line is marked so.  Used by tests/test_dist_gloo.py")
     args = ap.parse_args()
     if args.views is None:
         args.views = 16 if args.camera_shard else 7
@@ -309,6 +313,64 @@ def workload(args, world):
             f"mean -> {args.bev[0]}x{args.bev[1]} BEV")
 
 
+def timed_steps(step, steps: int, sync, world: int):
+    """The contract's timed region: barrier + sync, exactly `steps` steps, barrier + sync, then the MAX of the
+    elapsed time over the ranks (all_reduce MAX on the default group).  Returns (elapsed_s, own_elapsed_s)."""
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        sync()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+    barrier()
+    own = time.perf_counter() - t0
+    elapsed = own
+    if world > 1:
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.distributed.get_backend() == "nccl" \
+            else torch.device("cpu")
+        t = torch.tensor([own], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, own
+
+
+def dry_run(args, world: int, rank: int) -> None:
+    """--dry-run: the multi-rank orchestration of main() on the CPU with the gloo backend and a placeholder
+    step, so that the N > 1 path (spawn_ranks, barriers, MAX over ranks, frame accounting) runs where no GPU
+    exists.  Rank r's step sleeps (r + 1) x 5 ms: the MAX-reduced time must be the slowest rank's."""
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+        world = torch.distributed.get_world_size()
+    delay = 0.005 * (rank + 1)
+
+    def step(record):
+        time.sleep(delay)
+
+    for _ in range(args.warmup):
+        step(False)
+    elapsed, own = timed_steps(step, args.steps, lambda: None, world)
+    owns = [own]
+    if world > 1:
+        g = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        torch.distributed.all_gather(g, torch.tensor([own], dtype=torch.float64))
+        owns = [float(x.item()) for x in g]
+    frames = world * args.batch * args.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "dry-run (bench.py orchestration only; no hot path ran)", "value": round(frames / elapsed, 3),
+            "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "none", "data": "none (placeholder step)",
+            "config": {"workload": "placeholder", "frames_per_gpu_per_step": args.batch,
+                       "frames_per_step": world * args.batch, "backend": "gloo" if world > 1 else "none"},
+            "frames": frames, "elapsed_s": elapsed, "rank_elapsed_s": owns}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -321,6 +383,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if args.dry_run:
+        return dry_run(args, world, rank)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if dist:
@@ -397,16 +461,8 @@ def main():
 
     barrier()
     nat.spans_start()  # HIP events around every conv / warp launch, on the launch stream
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed, _ = timed_steps(step, args.steps, lambda: torch.cuda.synchronize(dev), world)
     spans = nat.spans_stop()
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     h2d = None
     if world == 1 and not args.warp_only:

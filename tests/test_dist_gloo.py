@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from conftest import GOLDEN, PKG
+from conftest import GOLDEN, PKG, REPO
 
 ORACLE_DIR = os.path.join(os.path.dirname(GOLDEN), "..", "oracle")
 
@@ -93,3 +93,30 @@ def test_camera_sharded_reduce_scatter(world):
                 assert np.abs(full - ref).max() <= 1e-5 * scale, mode
             rows = -(-ref.shape[2] // world)
             np.testing.assert_array_equal(sl, full[:, :, rank * rows:(rank + 1) * rows])
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_orchestration_dry_run(world):
+    """bench.py's multi-rank path itself (spawn_ranks -> torch.distributed.run -> one process per rank, the
+    barrier-bracketed timed region, the MAX reduction of the elapsed time, rank 0's JSON line) on the CPU with
+    gloo and a placeholder step: the same code the driver's 8-GPU run executes, minus the hot path."""
+    import json
+    import subprocess
+    import sys
+    steps, batch = 5, 2
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--gpus", str(world), "--steps", str(steps),
+           "--warmup", "1", "--batch", str(batch)]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["steps"] == steps
+    assert d["frames"] == world * batch * steps
+    assert len(d["rank_elapsed_s"]) == world
+    assert d["elapsed_s"] == max(d["rank_elapsed_s"])  # MAX over ranks
+    # the slowest rank sleeps world x 5 ms per step: the reported time per step covers it
+    assert d["ms_per_step"] >= 5.0 * world
+    assert abs(d["value"] - d["frames"] / d["elapsed_s"]) <= 1e-3 * d["value"]
