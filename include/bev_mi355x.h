@@ -46,7 +46,7 @@ int bev_abi_version(void);
  *   0 = LDS-DMA kernel (default), 1 = register-staged, 2 = wave-independent LDS-DMA kernel (per-wave
  *   footprints, no workgroup barrier), 3 = persistent LDS-DMA kernel (C == 64 with a workspace: the next
  *   (frame, tile)'s first footprint DMA is issued before this one's stores).
- * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats, 0 = 8192.
+ * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats (<= 12288), 0 = 12288.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.
  * BEV_TUNE_WGRAD_MFMA: conv weight gradient on the MFMA with natural-layout operands copied by LDS-DMA
@@ -150,11 +150,23 @@ int bev_ipm_taps_f32(const float *Hmat, const float *xs, const float *ys, int N,
 int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C, int Hf,
                          int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, void *stream);
 
+/* The same with the gradient's element strides (sN, sC, sH, sW): dense NCHW (sW == 1) or dense channels-last
+ * NHWC (sC == 1, the layout CNNEncoder hands over); anything else is BEV_ERR_ARGS.  Hf, Wf < 16383. */
+int bev_ipm_warp_bwd_ex_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C,
+                            int Hf, int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, int64_t sN, int64_t sC,
+                            int64_t sH, int64_t sW, void *stream);
+
 /* Backward of bev_ipm_warp_fuse_f32 for mode SUM / MEAN: gout [B][C][Hb][Wb],
- * gfeats [B*V][C][Hf][Wf] contiguous, OVERWRITTEN. */
+ * gfeats [B*V][C][Hf][Wf] contiguous, OVERWRITTEN.  Replaces autograd through geometry.py:161 and
+ * fusion.py:19-21 (d mean / d x_v = gout / V). */
 int bev_ipm_warp_fuse_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int B, int V,
                               int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode, float *gfeats,
                               void *stream);
+
+/* The same with the gradient's element strides (dense NCHW or dense NHWC, as bev_ipm_warp_bwd_ex_f32). */
+int bev_ipm_warp_fuse_bwd_ex_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int B,
+                                 int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                                 float *gfeats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, void *stream);
 
 /* ---------------------------------------------------------------------------
  * View fusion on materialised per-view maps (SimpleFusion / AttentionFusion)
@@ -162,6 +174,11 @@ int bev_ipm_warp_fuse_bwd_f32(const float *gout, const float *Hmat, const float 
  * (bev_maps.sum(1) / .mean(1) / .max(1).values; AttentionFusion fusion.py:36).
  * ------------------------------------------------------------------------- */
 int bev_view_fuse_f32(const float *x, int B, int V, int64_t M, int mode, float *out, void *stream);
+
+/* Backward of the max fusion (fusion.py:22, autograd of bev_maps.max(dim=1).values): gx [B][V][M] (written in full)
+ * = gout [B][M] at the view torch's max(dim) selects -- the first NaN, else the first maximal element (ties to the
+ * lowest view) -- and 0 at every other view.  x [B][V][M] are the fused maps of the forward. */
+int bev_view_max_bwd_f32(const float *x, const float *gout, int B, int V, int64_t M, float *gx, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Backbone (CNNEncoder, cnn_encoder.py:39-70): convolutions on MFMA.

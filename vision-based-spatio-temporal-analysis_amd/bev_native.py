@@ -45,8 +45,13 @@ SIGNATURES = {
                                       _i, _vp, _vp, _i64, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_ipm_warp_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
+    "bev_ipm_warp_bwd_ex_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _i64, _i64, _i64, _i64,
+                                     _vp]),
     "bev_ipm_warp_fuse_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _vp]),
+    "bev_ipm_warp_fuse_bwd_ex_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _i64, _i64,
+                                          _i64, _i64, _vp]),
     "bev_view_fuse_f32": (_i, [_vp, _i, _i, _i64, _i, _vp, _vp]),
+    "bev_view_max_bwd_f32": (_i, [_vp, _vp, _i, _i, _i64, _vp, _vp]),
     "bev_conv_packed_size": (_i64, [_i, _i, _i, _i]),
     "bev_conv_pack_weights_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
@@ -389,25 +394,44 @@ def taps(H, xs, ys, Hf, Wf, img_hw):
     return x0y0, wts, valid
 
 
-def warp_bwd(gout, H, xs, ys, Hf, Wf, img_hw):
+def _grad_maps(lead, C, Hf, Wf, dev, channels_last):
+    """Gradient buffer [*lead, C, Hf, Wf]: dense NCHW, or a channels-last view of [*lead, Hf, Wf, C] storage (the
+    layout CNNEncoder hands its features over in, so the gradient needs no transpose on its way back)."""
+    if not channels_last:
+        return torch.empty(*lead, C, Hf, Wf, device=dev, dtype=torch.float32)
+    nl = len(lead)
+    buf = torch.empty(*lead, Hf, Wf, C, device=dev, dtype=torch.float32)
+    return buf.permute(*range(nl), nl + 2, nl, nl + 1)
+
+
+def warp_bwd(gout, H, xs, ys, Hf, Wf, img_hw, channels_last=True):
+    """d feats of the per-view warp (k_warp_bwd_runs); [N,C,Hf,Wf], channels-last storage by default."""
     gout = gout.contiguous()
     _require_gpu(gout, H, xs, ys)
     N, C, Hb, Wb = gout.shape
     sx, sy = _scales(Hf, Wf, img_hw)
-    g = torch.empty(N, C, Hf, Wf, device=gout.device, dtype=torch.float32)
-    _check(lib().bev_ipm_warp_bwd_f32(_ptr(gout), _ptr(H), _ptr(xs), _ptr(ys), N, C, Hf, Wf, sx, sy, Hb, Wb, _ptr(g),
-                                      _stream(gout)), "bev_ipm_warp_bwd_f32")
+    g = _grad_maps((N,), C, Hf, Wf, gout.device, channels_last)
+    s = g.stride()
+    with _span("warp_bwd", gout):
+        rc = lib().bev_ipm_warp_bwd_ex_f32(_ptr(gout), _ptr(H), _ptr(xs), _ptr(ys), N, C, Hf, Wf, sx, sy, Hb, Wb,
+                                           _ptr(g), s[0], s[1], s[2], s[3], _stream(gout))
+    _check(rc, "bev_ipm_warp_bwd_ex_f32")
     return g
 
 
-def warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode):
+def warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode, channels_last=True):
+    """d feats of the fused warp + sum / mean (k_warp_bwd_runs); [B,V,C,Hf,Wf], channels-last storage by
+    default."""
     gout = gout.contiguous()
     _require_gpu(gout, H, xs, ys)
     B, C, Hb, Wb = gout.shape
     sx, sy = _scales(Hf, Wf, img_hw)
-    g = torch.empty(B, V, C, Hf, Wf, device=gout.device, dtype=torch.float32)
-    _check(lib().bev_ipm_warp_fuse_bwd_f32(_ptr(gout), _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf, Wf, sx, sy, Hb, Wb,
-                                           FUSE_MODES[mode], _ptr(g), _stream(gout)), "bev_ipm_warp_fuse_bwd_f32")
+    g = _grad_maps((B, V), C, Hf, Wf, gout.device, channels_last)
+    s = g.stride()
+    with _span("warp_bwd", gout):
+        rc = lib().bev_ipm_warp_fuse_bwd_ex_f32(_ptr(gout), _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf, Wf, sx, sy, Hb,
+                                                Wb, FUSE_MODES[mode], _ptr(g), s[1], s[2], s[3], s[4], _stream(gout))
+    _check(rc, "bev_ipm_warp_fuse_bwd_ex_f32")
     return g
 
 
@@ -420,6 +444,18 @@ def view_fuse(x: torch.Tensor, mode: str) -> torch.Tensor:
     out = torch.empty((B,) + tuple(x.shape[2:]), device=x.device, dtype=torch.float32)
     _check(lib().bev_view_fuse_f32(_ptr(x), B, V, M, FUSE_MODES[mode], _ptr(out), _stream(x)), "bev_view_fuse_f32")
     return out
+
+
+def view_max_bwd(x: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """Gradient of the max over dim 1 of x [B,V,...] for the upstream gradient g [B,...] (torch's index rule)."""
+    x = x.contiguous()
+    g = g.contiguous().float()
+    _require_gpu(x, g)
+    B, V = x.shape[:2]
+    M = x[0, 0].numel() if B * V > 0 else 0
+    gx = torch.empty_like(x, dtype=torch.float32)
+    _check(lib().bev_view_max_bwd_f32(_ptr(x), _ptr(g), B, V, M, _ptr(gx), _stream(x)), "bev_view_max_bwd_f32")
+    return gx
 
 
 # ---------------------------------------------------------------------------

@@ -7,6 +7,10 @@ namespace bev {
 // knob = BEV_TUNE_WARP_* (include/bev_mi355x.h); returns the previous value or BEV_ERR_ARGS.
 int warp_tune(int knob, int value);
 
+// LDS image of the warp backward (bev_warp_bwd.hip) in floats: BEV_TUNE_WARP_BWD_POOL, 0 = the maximum.
+constexpr int WARP_BWD_POOL_MAX = 12288;  // 48 KiB: three workgroups per CU
+int warp_bwd_pool_floats();
+
 // knob = BEV_TUNE_WGRAD_MFMA (bev_train.hip).
 int train_tune(int knob, int value);
 

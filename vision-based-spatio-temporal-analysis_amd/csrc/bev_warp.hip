@@ -13,8 +13,9 @@
 //                    footprints staged by LDS-DMA, one workgroup barrier per view
 //   k_warp_fuse      the same reduction for any strides / channel count,
 //                    register-staged footprint images (NCHW, C % 64 != 0)
-//   k_warp_bwd_lds   d out / d feats (LDS-reduced scatter, float atomics)
+//   (the backward, d out / d feats, is bev_warp_bwd.hip)
 //   k_view_fuse      SimpleFusion on materialised maps      (fusion.py:19-22)
+//   k_view_max_bwd   backward of the max over views (torch max(dim) index rule)
 //
 // Every fused kernel computes a cell's bilinear taps once per view with the
 // bit-exact recipe (bev_geometry.h), stages the tile's source footprint in LDS
@@ -1671,96 +1672,6 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_w(const float *__restr
 }
 
 // -------------------------------------------------------------------------
-// backward (grad w.r.t. feats)
-// -------------------------------------------------------------------------
-// Backward with the scatter reduced in LDS first.  One workgroup owns a
-// TILE_H x TILE_W tile of BEV cells of one feature map (grid z = b*V + v).  The
-// tile's exact tap footprint (bbox of its valid taps) is an LDS image of
-// CC-channel planes [CC][npix]; every cell adds w * grad for its 4 taps with
-// LDS float atomics (ds_add_f32: ~3 cells per source pixel collide here, not in
-// L2), then the image is flushed with ONE global float atomic per non-zero
-// (pixel, channel) -- coalesced along footprint rows of the NCHW gradient.
-// Global contention is left only on the edges shared by neighbouring tiles.
-// CC = the largest of 16/8/4/2/1 whose image fits the 32 KiB pool; footprints
-// larger than 8192 pixels (tiles at the horizon) scatter straight to global.
-// Summation order differs from the per-tap atomics (float addition is not
-// associative): equal to the reference's backward within fp32 tolerance.
-constexpr int BW_POOL = 8192;  // floats (32 KiB)
-
-__global__ __launch_bounds__(NT) void k_warp_bwd_lds(const float *__restrict__ gout, const float *__restrict__ Hmat,
-                                                     const float *__restrict__ xs, const float *__restrict__ ys,
-                                                     int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
-                                                     int Wb, float scale, int per_view_gout,
-                                                     float *__restrict__ gfeats, int pool) {
-    __shared__ float img[BW_POOL];  // pool <= BW_POOL floats of it are used (tests force small pools)
-    __shared__ int red[4 * TILE_H];
-    const int tid = threadIdx.y * TILE_W + threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int j = blockIdx.x * TILE_W + threadIdx.x;
-    const int i = blockIdx.y * TILE_H + threadIdx.y;
-    const int n = blockIdx.z;
-    const bool inside = (i < Hb) && (j < Wb);
-    float h[9];
-    load_h(Hmat, n, h);
-    const Grid grid = make_grid(Hf, Wf);
-    Taps t = cell_taps(h, xs[inside ? j : 0], ys[inside ? i : 0], grid, sx, sy);
-    if (!inside) t.valid = 0;
-    put_box<TILE_H>(red, wave_box(t), wave, lane);
-    __syncthreads();
-    const Box bx = get_box<TILE_H>(red);
-    if (bx.x1 < 0) return;  // no valid tap in the tile (uniform)
-    const int bw = bx.x1 - bx.x0 + 1, npix = bw * (bx.y1 - bx.y0 + 1);
-
-    const size_t plane = (size_t)Hb * Wb, fplane = (size_t)Hf * Wf;
-    const int src = per_view_gout ? n : n / V;
-    const double rscale = 1.0 / (double)scale;
-    const float *g = gout + (size_t)src * C * plane + (size_t)(inside ? i : 0) * Wb + (inside ? j : 0);
-    float *gf = gfeats + (size_t)n * C * fplane;
-
-    if (npix > pool) {  // horizon tile: direct scatter
-        if (!t.valid) return;
-        const size_t base = (size_t)t.y0 * Wf + t.x0;
-        for (int c = 0; c < C; ++c) {
-            float go = g[(size_t)c * plane];
-            if (scale != 1.0f) go = div_rcp(go, rscale);
-            float *p = gf + (size_t)c * fplane + base;
-            if (t.valid & 1) unsafeAtomicAdd(p, t.w[0] * go);
-            if (t.valid & 2) unsafeAtomicAdd(p + 1, t.w[1] * go);
-            if (t.valid & 4) unsafeAtomicAdd(p + Wf, t.w[2] * go);
-            if (t.valid & 8) unsafeAtomicAdd(p + Wf + 1, t.w[3] * go);
-        }
-        return;
-    }
-    int CC = 16;
-    while (CC > 1 && CC * npix > pool) CC >>= 1;
-    const int q = (t.y0 - bx.y0) * bw + (t.x0 - bx.x0);  // LDS index of the nw tap (valid lanes)
-    for (int c0 = 0; c0 < C; c0 += CC) {
-        const int cc_n = min(CC, C - c0), tot = cc_n * npix;
-        for (int k = tid; k < tot; k += NT) img[k] = 0.0f;
-        __syncthreads();
-        if (t.valid) {
-            for (int cc = 0; cc < cc_n; ++cc) {
-                float go = g[(size_t)(c0 + cc) * plane];
-                if (scale != 1.0f) go = div_rcp(go, rscale);
-                float *p = img + cc * npix + q;
-                if (t.valid & 1) atomicAdd(p, t.w[0] * go);
-                if (t.valid & 2) atomicAdd(p + 1, t.w[1] * go);
-                if (t.valid & 4) atomicAdd(p + bw, t.w[2] * go);
-                if (t.valid & 8) atomicAdd(p + bw + 1, t.w[3] * go);
-            }
-        }
-        __syncthreads();
-        for (int k = tid; k < tot; k += NT) {
-            const float val = img[k];
-            if (val != 0.0f) {
-                const int cc = k / npix, p = k - cc * npix, py = p / bw, px = p - py * bw;
-                unsafeAtomicAdd(gf + (size_t)(c0 + cc) * fplane + (size_t)(bx.y0 + py) * Wf + bx.x0 + px, val);
-            }
-        }
-        __syncthreads();  // the image is re-zeroed by the next chunk
-    }
-}
-
-// -------------------------------------------------------------------------
 // SimpleFusion on materialised maps: x [B][V][M] -> out [B][M]
 // -------------------------------------------------------------------------
 template <int MODE>
@@ -1783,13 +1694,36 @@ __global__ void k_view_fuse(const float *__restrict__ x, int V, int64_t M, float
     }
 }
 
+// Backward of the max over views (fusion.py:22, bev_maps.max(dim=1).values): the gradient goes to the view torch's
+// CPU max(dim) returns as the index -- the first NaN if any element is NaN, else the first maximal element (ties,
+// -0 vs +0 included, go to the lowest view) -- and every other view gets 0.  gx [B][V][M], all of it written.
+__global__ void k_view_max_bwd(const float *__restrict__ x, const float *__restrict__ g, int V, int64_t M,
+                               float *__restrict__ gx) {
+    const int b = blockIdx.y;
+    const float *xb = x + (size_t)b * V * M;
+    float *gb = gx + (size_t)b * V * M;
+    for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (int64_t)gridDim.x * blockDim.x) {
+        float best = xb[m];
+        int arg = 0;
+        for (int v = 1; v < V; ++v) {
+            const float t = xb[(size_t)v * M + m];
+            if (best == best && (t > best || t != t)) {  // nan_max's choice; a NaN best is kept
+                best = t;
+                arg = v;
+            }
+        }
+        const float gm = g[(size_t)b * M + m];
+        for (int v = 0; v < V; ++v) gb[(size_t)v * M + m] = (v == arg) ? gm : 0.0f;
+    }
+}
+
 inline int err(hipError_t e) { return (int)e; }
 inline int last() { return (int)hipGetLastError(); }
 
 // ---- performance knobs (bev_tune; results never depend on them) -------------
 int g_warp_pool_kb = 0;  // BEV_TUNE_WARP_POOL_KB: LDS image pool / ring per workgroup, 0 = automatic
 int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 LDS-DMA kernel (k_warp_fuse_v2, default), 1 register-staged
-int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = BW_POOL
+int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = WARP_BWD_POOL_MAX
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
 
@@ -1961,6 +1895,8 @@ inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW
 }  // namespace
 
 namespace bev {
+int warp_bwd_pool_floats() { return g_warp_bwd_pool > 0 ? g_warp_bwd_pool : WARP_BWD_POOL_MAX; }
+
 int warp_tune(int knob, int value) {
     int *slot = nullptr;
     bool ok = false;
@@ -1975,7 +1911,7 @@ int warp_tune(int knob, int value) {
             break;
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
-            ok = value >= 0 && value <= BW_POOL;
+            ok = value >= 0 && value <= WARP_BWD_POOL_MAX;
             break;
         default:
             return BEV_ERR_ARGS;
@@ -2103,36 +2039,12 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
     return launch_fuse_ck<64>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
 }
 
-static int bwd_pool() { return g_warp_bwd_pool > 0 ? g_warp_bwd_pool : BW_POOL; }
-
-int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C, int Hf,
-                         int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, void *stream) {
-    if (N < 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || N > 65535) return BEV_ERR_ARGS;
-    hipStream_t st = (hipStream_t)stream;
-    if (N == 0 || C == 0) return 0;
-    hipError_t e = hipMemsetAsync(gfeats, 0, sizeof(float) * (size_t)N * C * Hf * Wf, st);
-    if (e != hipSuccess) return err(e);
-    if (Hb == 0 || Wb == 0) return 0;
-    dim3 grid((Wb + TILE_W - 1) / TILE_W, (Hb + TILE_H - 1) / TILE_H, N), block(TILE_W, TILE_H);
-    hipLaunchKernelGGL(k_warp_bwd_lds, grid, block, 0, st, gout, Hmat, xs, ys, 1, C, Hf, Wf, sx, sy, Hb, Wb, 1.0f, 1,
-                       gfeats, bwd_pool());
-    return last();
-}
-
-int bev_ipm_warp_fuse_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int B, int V,
-                              int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode, float *gfeats,
-                              void *stream) {
-    if (B < 0 || V <= 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B * V > 65535) return BEV_ERR_ARGS;
-    if (mode != BEV_FUSE_SUM && mode != BEV_FUSE_MEAN) return BEV_ERR_ARGS;
-    hipStream_t st = (hipStream_t)stream;
-    if (B == 0 || C == 0) return 0;
-    hipError_t e = hipMemsetAsync(gfeats, 0, sizeof(float) * (size_t)B * V * C * Hf * Wf, st);
-    if (e != hipSuccess) return err(e);
-    if (Hb == 0 || Wb == 0) return 0;
-    dim3 grid((Wb + TILE_W - 1) / TILE_W, (Hb + TILE_H - 1) / TILE_H, B * V), block(TILE_W, TILE_H);
-    const float scale = mode == BEV_FUSE_MEAN ? (float)V : 1.0f;
-    hipLaunchKernelGGL(k_warp_bwd_lds, grid, block, 0, st, gout, Hmat, xs, ys, V, C, Hf, Wf, sx, sy, Hb, Wb, scale, 0,
-                       gfeats, bwd_pool());
+int bev_view_max_bwd_f32(const float *x, const float *gout, int B, int V, int64_t M, float *gx, void *stream) {
+    if (B < 0 || V <= 0 || M < 0 || B > 65535) return BEV_ERR_ARGS;
+    if (B == 0 || M == 0) return 0;
+    int64_t blocks = (M + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_view_max_bwd, dim3((unsigned)blocks, B), dim3(256), 0, (hipStream_t)stream, x, gout, V, M, gx);
     return last();
 }
 

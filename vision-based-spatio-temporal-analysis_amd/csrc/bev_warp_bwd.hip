@@ -1,0 +1,374 @@
+// bev_warp_bwd.hip -- backward of the IPM warp (+ view sum / mean) w.r.t. the features, for gfx950 (MI355X).
+//
+// Replaces autograd through geometry.py:161 (grid_sampler_2d_backward, input gradient only: the grid comes from
+// the calibration, which carries no gradient) and, for the fused path, fusion.py:19-21 (sum / mean over views:
+// d mean / d x_v = gout / V).  For every source pixel p of view v and channel c:
+//     gfeats[v][c][p] = sum over BEV cells q and taps t of q with tap(q, t) == p, valid:  w_t(q) * g_v[c][q]
+// with g_v = gout (sum) or gout / V (mean), or the view's own gout (per-view warp).  The taps and weights are
+// the forward's bit-exact recipe (bev_geometry.h).  Float addition order differs from torch's scatter (float
+// atomics): equal to the reference's backward within fp32 tolerance, not bit for bit.
+//
+// k_warp_bwd_runs -- one workgroup per (frame, 16 x 16 BEV tile), ALL views of the frame in one workgroup, so the
+// fused gradient gout is read from HBM once (not once per view).  Lane mapping ("runs"): a 16-lane DPP row owns
+// one tile row = a run of 16 consecutive cells along the BEV x axis; lane l holds channels {l, l+16, l+32, l+48}
+// of a 64-channel chunk for all 16 cells of the run (64 VGPRs), and computes the taps of cell l.  The row walks
+// its 16 cells in order; cell k's tap key and weights come from lane k by DPP row broadcast (row_newbcast, folded
+// into the FMAs), and the four tap gradients w_t * g are accumulated in registers while consecutive cells share
+// the same 2x2 source quad -- on the Appendix-B rig 80 % of the cells have their left neighbour's quad (DESIGN.md
+// §4) -- and are added to the LDS image of the tile's footprint only when the quad changes: ~4x fewer LDS
+// atomics than one per (cell, tap, channel), and each ds_add_f32 instruction of a row covers 16 consecutive
+// channel dwords of one pixel.  The image ([pixel][64 channels + pad]) then goes to the gradient with one float
+// atomic per touched (pixel, channel), coalesced along channels for NHWC gradients (one 256-B wave instruction
+// per pixel) or along x for NCHW.  Footprints larger than the LDS pool (horizon tiles) add their quad sums
+// straight to global memory.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bev_geometry.h"
+#include "bev_tune.h"
+#include "../../include/bev_mi355x.h"
+
+using namespace bev;
+
+namespace {
+
+constexpr int RB_NT = 256;     // 4 waves = 16 DPP rows = 16 runs
+constexpr int RB_T = 16;       // tile = 16 rows x 16 cells
+constexpr int RB_PSW = 68;     // LDS image pixel stride in dwords (64 channels + 4: rows of neighbouring pixels
+                               // start 4 banks apart)
+
+static inline int rb_err(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+// lane k of this lane's 16-lane DPP row, to every lane of the row
+template <int K>
+__device__ __forceinline__ int row_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ float row_bcast_f(float v) {
+    return __builtin_bit_cast(float, row_bcast<K>(__builtin_bit_cast(int, v)));
+}
+
+// Quad key of a cell: (x0 + 1) | (y0 + 1) << 14 | valid << 28; 0 = no valid tap (never equal to a real key).
+__device__ __forceinline__ int quad_key(const Taps &t) {
+    if (!t.valid) return 0;
+    return (t.x0 + 1) | ((t.y0 + 1) << 14) | ((int)t.valid << 28);
+}
+__device__ __forceinline__ int key_x0(int k) { return (k & 0x3fff) - 1; }
+__device__ __forceinline__ int key_y0(int k) { return ((k >> 14) & 0x3fff) - 1; }
+__device__ __forceinline__ unsigned key_valid(int k) { return ((unsigned)k >> 28) & 15u; }
+
+struct Box4 {
+    int x0, y0, x1, y1;
+};
+
+// Where a run's four tap sums go.  IMG: the LDS image of the tile footprint, at the byte addresses the run's first
+// cell computed for its taps (an invalid tap points at a trash pixel that is never flushed).  !IMG (footprint larger
+// than the pool): the global gradient, by float atomics on the valid taps.
+struct GSink {
+    float *gf;           // global gradient of this view at the chunk's first channel
+    int64_t sC, sH, sW;  // its element strides
+    int lane16, cmax;
+};
+
+template <bool IMG>
+__device__ __forceinline__ void run_flush(int key, const int (&a)[4], const float (&q)[4][4], unsigned char *smem,
+                                          const GSink &gs) {
+    if constexpr (IMG) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                __hip_atomic_fetch_add(reinterpret_cast<float *>(smem + a[t]) + 16 * m, q[t][m], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        const unsigned vb = key_valid(key);
+        const int x0 = key_x0(key), y0 = key_y0(key);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (!(vb & (1u << t))) continue;
+            float *p = gs.gf + (int64_t)(y0 + (t >> 1)) * gs.sH + (int64_t)(x0 + (t & 1)) * gs.sW;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if (gs.lane16 + 16 * m < gs.cmax) unsafeAtomicAdd(p + (int64_t)(gs.lane16 + 16 * m) * gs.sC, q[t][m]);
+        }
+    }
+}
+
+// Step K of a row's walk: accumulate cell K's four tap gradients (key / weights / tap addresses from lane K by DPP
+// row broadcast); when cell K ends its run (cell K + 1 has another quad, or K is the last cell), add the run's sums
+// to the image at cell K's tap addresses and restart them.  The branch is uniform inside the row; the restart is a
+// select, so the accumulators carry no control-flow merges.
+template <bool IMG, int K>
+__device__ __forceinline__ void walk_step(const float (&g)[16][4], float (&q)[4][4], int &key, int (&a)[4],
+                                          float (&w)[4], unsigned char *smem, const GSink &gs) {
+    // the broadcast sources are "redefined" at every step, so the compiler cannot hoist all 16 steps' broadcasts
+    // to the top of the walk (9 x 16 extra live VGPRs)
+    asm volatile("" : "+v"(key), "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
+                 "+v"(a[3]));
+    const int kk = row_bcast<K>(key);
+    int kn = 0;
+    if constexpr (K + 1 < 16) kn = row_bcast<K + 1>(key);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const float wt = row_bcast_f<K>(w[t]);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[t][m] = __builtin_fmaf(wt, g[K][m], q[t][m]);
+    }
+    const bool end = kn != kk;
+    if (end && kk != 0) {
+        int at[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) at[t] = row_bcast<K>(a[t]);
+        run_flush<IMG>(kk, at, q, smem, gs);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[t][m] = end ? 0.0f : q[t][m];
+}
+
+template <bool IMG, int K>
+__device__ __forceinline__ void walk_from(const float (&g)[16][4], float (&q)[4][4], int &key, int (&a)[4],
+                                          float (&w)[4], unsigned char *smem, const GSink &gs) {
+    walk_step<IMG, K>(g, q, key, a, w, smem, gs);
+    if constexpr (K + 1 < 16) walk_from<IMG, K + 1>(g, q, key, a, w, smem, gs);
+}
+
+// One row's walk over its 16 cells for one view.
+template <bool IMG>
+__device__ __forceinline__ void walk_row(const float (&g)[16][4], int key, const int (&a0)[4], const float (&w0)[4],
+                                         unsigned char *smem, const GSink &gs) {
+    int a[4] = {a0[0], a0[1], a0[2], a0[3]};
+    float w[4] = {w0[0], w0[1], w0[2], w0[3]};
+    float q[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) q[t][m] = 0.0f;
+    walk_from<IMG, 0>(g, q, key, a, w, smem, gs);
+}
+
+// Exact bbox of the valid taps of the workgroup's cells (wave shuffles + LDS exchange).
+__device__ __forceinline__ Box4 block_box(const Taps &t, int *red, int wave, int lane) {
+    int x0 = 0x7fffffff, y0 = 0x7fffffff, x1 = -1, y1 = -1;
+    if (t.valid) {
+        x0 = (t.valid & 5) ? t.x0 : t.x0 + 1;
+        x1 = (t.valid & 10) ? t.x0 + 1 : t.x0;
+        y0 = (t.valid & 3) ? t.y0 : t.y0 + 1;
+        y1 = (t.valid & 12) ? t.y0 + 1 : t.y0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        x0 = min(x0, __shfl_xor(x0, o));
+        y0 = min(y0, __shfl_xor(y0, o));
+        x1 = max(x1, __shfl_xor(x1, o));
+        y1 = max(y1, __shfl_xor(y1, o));
+    }
+    if (lane == 0) {
+        red[wave] = x0;
+        red[4 + wave] = y0;
+        red[8 + wave] = x1;
+        red[12 + wave] = y1;
+    }
+    __syncthreads();
+    Box4 b{red[0], red[4], red[8], red[12]};
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+        b.x0 = min(b.x0, red[w]);
+        b.y0 = min(b.y0, red[4 + w]);
+        b.x1 = max(b.x1, red[8 + w]);
+        b.y1 = max(b.y1, red[12 + w]);
+    }
+    return b;
+}
+
+// grid (tiles, B); gout [B][Cg][Hb][Wb] (per_view: [B*V][C][Hb][Wb]), gfeats element strides (sN, sC, sH, sW)
+__global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict__ gout, const float *__restrict__ Hmat,
+                                                         const float *__restrict__ xs, const float *__restrict__ ys,
+                                                         int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                                                         int Wb, int mean, int per_view, float *__restrict__ gfeats,
+                                                         int64_t sN, int64_t sC, int64_t sH, int64_t sW, int pool) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float *img = reinterpret_cast<float *>(smem);
+    int *red = reinterpret_cast<int *>(smem + pool);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15;
+    const int ntx = (Wb + RB_T - 1) / RB_T;
+    const int ty = blockIdx.x / ntx, tx = blockIdx.x - ty * ntx;
+    const int b = blockIdx.y;
+    const int row = wave * 4 + (lane >> 4);  // the run (tile row) of this lane's DPP row
+    const int i = ty * RB_T + row, j0 = tx * RB_T, j = j0 + l16;
+    const bool inside = i < Hb && j < Wb, row_in = i < Hb;
+    const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
+    const Grid grid = make_grid(Hf, Wf);
+    const int64_t plane = (int64_t)Hb * Wb;
+    const bool vec = row_in && (Wb % 4 == 0) && j0 + RB_T <= Wb;
+    const double rV = recip_uniform(V);
+    const int maxpix = pool / (RB_PSW * 4) - 1;  // + the trash pixel
+
+    for (int c0 = 0; c0 < C; c0 += 64) {
+        const int cmax = min(64, C - c0);
+        float g[16][4];
+        auto load_g = [&](const float *src) {  // src = gradient map of this frame (or view) [C][Hb][Wb]
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const int c = c0 + l16 + 16 * m;
+                const float *p = src + (int64_t)(c < C ? c : 0) * plane + (int64_t)(row_in ? i : 0) * Wb + j0;
+                if (vec && c < C) {
+#pragma unroll
+                    for (int k4 = 0; k4 < 4; ++k4) {
+                        const float4 v = *reinterpret_cast<const float4 *>(p + 4 * k4);
+                        g[4 * k4][m] = v.x;
+                        g[4 * k4 + 1][m] = v.y;
+                        g[4 * k4 + 2][m] = v.z;
+                        g[4 * k4 + 3][m] = v.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) g[k][m] = (row_in && c < C && j0 + k < Wb) ? p[k] : 0.0f;
+                }
+                if (mean) {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) g[k][m] = div_rcp(g[k][m], rV);  // gout / V, IEEE-exact
+                }
+            }
+        };
+        if (!per_view) load_g(gout + (int64_t)b * C * plane);
+
+        for (int v = 0; v < V; ++v) {
+            const int n = b * V + v;
+            float h[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane(n * 9) + q];
+            Taps t = cell_taps(h, cx, cy, grid, sx, sy);
+            if (!inside) t.valid = 0;
+            const Box4 bx = block_box(t, red, wave, lane);  // one barrier; red[] reused next view after two more
+            if (bx.x1 < 0) {
+                __syncthreads();  // red[] is read by every wave before the next view rewrites it
+                continue;
+            }
+            const int bw = bx.x1 - bx.x0 + 1, npix = bw * (bx.y1 - bx.y0 + 1);
+            const bool use_img = npix <= maxpix;
+            if (use_img) {
+                float4 *z = reinterpret_cast<float4 *>(img);
+                for (int k = tid; k < (npix + 1) * (RB_PSW / 4); k += RB_NT) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+            if (per_view) load_g(gout + (int64_t)n * C * plane);
+            __syncthreads();  // image zeroed; red[] consumed
+
+            const int key = quad_key(t);
+            const GSink gs{gfeats + (int64_t)n * sN + (int64_t)c0 * sC, sC, sH, sW, l16, cmax};
+            if (use_img) {
+                // byte addresses of this cell's four taps in the image (lane's channel offset included); invalid
+                // taps -> the trash pixel after the image
+                const int trash = npix * RB_PSW * 4 + l16 * 4;
+                const int px = t.x0 - bx.x0, py = t.y0 - bx.y0;
+                int a[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    a[u] = (t.valid & (1u << u)) ? ((py + (u >> 1)) * bw + px + (u & 1)) * (RB_PSW * 4) + l16 * 4
+                                                 : trash;
+                walk_row<true>(g, key, a, t.w, smem, gs);
+            } else {
+                const int a[4] = {0, 0, 0, 0};
+                walk_row<false>(g, key, a, t.w, smem, gs);
+            }
+
+            if (use_img) {
+                __syncthreads();  // every row's quad sums are in the image
+                float *gfv = gfeats + (int64_t)n * sN + (int64_t)c0 * sC;
+                if (sC == 1) {  // channels contiguous: one pixel per wave instruction, lane = channel
+                    for (int p0 = wave * 4; p0 < npix; p0 += 16) {  // 4 pixels per wave in flight
+                        float val[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) val[u] = (p0 + u < npix) ? img[(p0 + u) * RB_PSW + lane] : 0.0f;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int p = p0 + u, py = p / bw, px = p - py * bw;
+                            if (val[u] != 0.0f && lane < cmax)
+                                unsafeAtomicAdd(gfv + (int64_t)(bx.y0 + py) * sH + (int64_t)(bx.x0 + px) * sW + lane,
+                                                val[u]);
+                        }
+                    }
+                } else {  // lanes along x: for each (channel, footprint row), 64 consecutive pixels per step
+                    const int bh = npix / bw;
+                    for (int r = wave; r < cmax * bh; r += 4) {
+                        const int c = r / bh, py = r - c * bh;
+                        for (int px = lane; px < bw; px += 64) {
+                            const float val = img[(py * bw + px) * RB_PSW + c];
+                            if (val != 0.0f)
+                                unsafeAtomicAdd(gfv + (int64_t)c * sC + (int64_t)(bx.y0 + py) * sH +
+                                                    (int64_t)(bx.x0 + px) * sW,
+                                                val);
+                        }
+                    }
+                }
+            }
+            __syncthreads();  // the image is free for the next view
+        }
+    }
+}
+
+}  // namespace
+
+// Shared launcher: zero the gradient, then one workgroup per (frame, tile).
+static int warp_bwd_runs(const float *gout, const float *Hmat, const float *xs, const float *ys, int B, int V, int C,
+                         int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mean, int per_view, float *gfeats,
+                         int64_t sN, int64_t sC, int64_t sH, int64_t sW, hipStream_t st) {
+    // zero the [B*V] maps (any strides that cover a dense block: NCHW or NHWC)
+    const int64_t n_el = (int64_t)B * V * C * Hf * Wf;
+    hipError_t e = hipMemsetAsync(gfeats, 0, sizeof(float) * (size_t)n_el, st);
+    if (e != hipSuccess) return rb_err(e);
+    if (Hb == 0 || Wb == 0) return 0;
+    const int ntiles = ((Wb + RB_T - 1) / RB_T) * ((Hb + RB_T - 1) / RB_T);
+    const int pool = (warp_bwd_pool_floats() * 4) & ~15;  // LDS image bytes (default 48 KiB: 3 workgroups per CU)
+    hipLaunchKernelGGL(k_warp_bwd_runs, dim3(ntiles, B), dim3(RB_NT), pool + 16 * sizeof(int), st, gout, Hmat, xs, ys,
+                       V, C, Hf, Wf, sx, sy, Hb, Wb, mean, per_view, gfeats, sN, sC, sH, sW, pool);
+    return rb_err(hipGetLastError());
+}
+
+static bool dense_nchw_or_nhwc(int C, int Hf, int Wf, int64_t sN, int64_t sC, int64_t sH, int64_t sW) {
+    const int64_t P = (int64_t)Hf * Wf;
+    const bool nchw = sW == 1 && sH == Wf && sC == P && sN == C * P;
+    const bool nhwc = sC == 1 && sW == C && sH == (int64_t)Wf * C && sN == C * P;
+    return nchw || nhwc;
+}
+
+extern "C" {
+
+int bev_ipm_warp_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C, int Hf,
+                         int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, void *stream) {
+    return bev_ipm_warp_bwd_ex_f32(gout, Hmat, xs, ys, N, C, Hf, Wf, sx, sy, Hb, Wb, gfeats, (int64_t)C * Hf * Wf,
+                                   (int64_t)Hf * Wf, Wf, 1, stream);
+}
+
+int bev_ipm_warp_bwd_ex_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int N, int C,
+                            int Hf, int Wf, float sx, float sy, int Hb, int Wb, float *gfeats, int64_t sN, int64_t sC,
+                            int64_t sH, int64_t sW, void *stream) {
+    if (N < 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || N > 65535) return BEV_ERR_ARGS;
+    if (Hf >= 16383 || Wf >= 16383 || !dense_nchw_or_nhwc(C, Hf, Wf, sN, sC, sH, sW)) return BEV_ERR_ARGS;
+    if (N == 0 || C == 0) return 0;
+    // per-view gradient maps: one "frame" per map, V = 1
+    return warp_bwd_runs(gout, Hmat, xs, ys, N, 1, C, Hf, Wf, sx, sy, Hb, Wb, 0, 1, gfeats, sN, sC, sH, sW,
+                         (hipStream_t)stream);
+}
+
+int bev_ipm_warp_fuse_bwd_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int B, int V,
+                              int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode, float *gfeats,
+                              void *stream) {
+    return bev_ipm_warp_fuse_bwd_ex_f32(gout, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, gfeats,
+                                        (int64_t)C * Hf * Wf, (int64_t)Hf * Wf, Wf, 1, stream);
+}
+
+int bev_ipm_warp_fuse_bwd_ex_f32(const float *gout, const float *Hmat, const float *xs, const float *ys, int B,
+                                 int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                                 float *gfeats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, void *stream) {
+    if (B < 0 || V <= 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B > 65535) return BEV_ERR_ARGS;
+    if (mode != BEV_FUSE_SUM && mode != BEV_FUSE_MEAN) return BEV_ERR_ARGS;
+    if (Hf >= 16383 || Wf >= 16383 || !dense_nchw_or_nhwc(C, Hf, Wf, sN, sC, sH, sW)) return BEV_ERR_ARGS;
+    if (B == 0 || C == 0) return 0;
+    return warp_bwd_runs(gout, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode == BEV_FUSE_MEAN, 0, gfeats, sN, sC,
+                         sH, sW, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -31,7 +31,7 @@ class _FuseFn(torch.autograd.Function):
         ctx.mode = mode
         ctx.V = x.shape[1]
         if mode == "max":
-            ctx.save_for_backward(x, out)
+            ctx.save_for_backward(x)
         return out
 
     @staticmethod
@@ -42,11 +42,9 @@ class _FuseFn(torch.autograd.Function):
             return g.unsqueeze(1).expand(g.shape[0], V, *g.shape[1:]), None
         if ctx.mode == "mean":
             return (g / V).unsqueeze(1).expand(g.shape[0], V, *g.shape[1:]), None
-        x, out = ctx.saved_tensors
-        idx = (x == out.unsqueeze(1)).to(torch.uint8).argmax(dim=1, keepdim=True)  # first maximal view
-        gx = torch.zeros_like(x)
-        gx.scatter_(1, idx, g.unsqueeze(1))
-        return gx, None
+        x, = ctx.saved_tensors
+        # to the view torch's max(dim) returns: the first NaN, else the first maximal element (bev_view_max_bwd_f32)
+        return _nat.view_max_bwd(x, g), None
 
 
 class FusionModule(nn.Module):

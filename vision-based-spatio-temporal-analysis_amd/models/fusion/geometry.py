@@ -144,19 +144,30 @@ class _WarpFuseFn(torch.autograd.Function):
     @staticmethod
     @_nat.amp_fwd
     def forward(ctx, feats5, H, xs, ys, img_hw, mode):
-        ctx.save_for_backward(H, xs, ys)
+        if mode == "max":  # the backward re-samples the views to find each element's maximal one
+            ctx.save_for_backward(H, xs, ys, feats5)
+        else:
+            ctx.save_for_backward(H, xs, ys)
         ctx.meta = (feats5.shape[1], feats5.shape[3], feats5.shape[4], img_hw, mode)
         return _nat.warp_fuse(feats5, H, xs, ys, img_hw, mode)
 
     @staticmethod
     @_nat.amp_bwd
     def backward(ctx, gout):
-        H, xs, ys = ctx.saved_tensors
         V, Hf, Wf, img_hw, mode = ctx.meta
-        if mode not in ("sum", "mean"):
-            raise NotImplementedError("backward of the fused max reduction is not implemented; "
-                                      "use forward() + SimpleFusion('max') for training")
-        return _nat.warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode), None, None, None, None, None
+        if mode in ("sum", "mean"):
+            H, xs, ys = ctx.saved_tensors
+            return _nat.warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode), None, None, None, None, None
+        # max (fusion.py:22 after geometry.py:161): the per-view samples again (bit-identical to the forward's),
+        # the gradient to the view torch's max(dim) picks, then the per-view warp backward
+        H, xs, ys, feats5 = ctx.saved_tensors
+        B, C = feats5.shape[0], feats5.shape[2]
+        f4 = feats5.reshape(B * V, C, Hf, Wf)
+        per_view = _nat.warp(f4, H, xs, ys, img_hw).view(B, V, C, gout.shape[2], gout.shape[3])
+        gv = _nat.view_max_bwd(per_view, gout)
+        del per_view
+        gf = _nat.warp_bwd(gv.view(B * V, C, gout.shape[2], gout.shape[3]), H, xs, ys, Hf, Wf, img_hw)
+        return gf.view(B, V, C, Hf, Wf), None, None, None, None, None
 
 
 class GeometryTransformer(nn.Module):

@@ -61,7 +61,11 @@ class _ViewProjection(torch.autograd.Function):
         fl, weight = ctx.saved_tensors
         B, V, Hf, Wf, C = fl.shape
         P = weight.shape[0]
-        dgn = _nat.nchw_to_nhwc(dg.reshape(B * V, P, Hf, Wf)).view(B, V, Hf, Wf, P)
+        dgl = dg.permute(0, 1, 3, 4, 2)
+        if dgl.is_contiguous():  # the fused-warp backward hands its gradient over channels-last: no transpose
+            dgn = dgl
+        else:
+            dgn = _nat.nchw_to_nhwc(dg.reshape(B * V, P, Hf, Wf)).view(B, V, Hf, Wf, P)
         dfeat = dw = None
         w = weight.detach().float().view(P, V, C)
         if ctx.needs_input_grad[0]:
