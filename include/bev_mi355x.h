@@ -40,12 +40,12 @@ int bev_abi_version(void);
  * BEV_ERR_ARGS for an unknown knob / out-of-range value.
  * BEV_TUNE_CONV_TILE: 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64
  *   output tiles for bev_conv2d_f32.
- * BEV_TUNE_WARP_POOL_KB: LDS footprint-image pool (ring) per workgroup of the fused
- *   warp in KiB, 0 = automatic, else 8..150 (small pools force block decomposition).
+ * BEV_TUNE_WARP_POOL_KB: LDS footprint-image pool per workgroup of the fused warp in KiB, 0 = automatic,
+ *   else 1..150 (small pools force one-view batches / direct views in the default kernel and block
+ *   decomposition in the per-view LDS-DMA kernel, which uses at least 8).
  * BEV_TUNE_WARP_KERNEL: fused warp kernel for NHWC C % 64 == 0 features:
- *   0 = LDS-DMA kernel (default), 1 = register-staged, 2 = wave-independent LDS-DMA kernel (per-wave
- *   footprints, no workgroup barrier), 3 = persistent LDS-DMA kernel (C == 64 with a workspace: the next
- *   (frame, tile)'s first footprint DMA is issued before this one's stores).
+ *   0 = default (DPP-row kernel with batched footprint staging for SUM / MEAN with a workspace, else the
+ *   per-view LDS-DMA kernel), 1 = register-staged, 2 = per-view LDS-DMA kernel.
  * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats (<= 12288), 0 = 12288.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.

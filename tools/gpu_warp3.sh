@@ -1,0 +1,17 @@
+# Fused-warp pass: LDS atomic micro, every warp GPU test, warp-only bench of the default (v3) and v2 kernels, the
+# full bench line, and a kernel trace of the full bench.
+# usage (on the box): bash tools/gpu_warp3.sh <tag>
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/$1; mkdir -p $O
+if [ -x tools/lds_atomic_micro ]; then timeout -k 10 60 ./tools/lds_atomic_micro > $O/lds_atomic_micro.txt 2>&1 || exit $?; fi
+timeout -k 10 900 python -u -m pytest tests/test_warp_gpu.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/warp_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/warp_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/warp_bwd_micro.py > $O/bwd_micro.txt 2>&1 || exit $?
+for k in rows dma; do
+  timeout -k 10 300 python -u bench.py --warp-only --steps 30 --warmup 5 --cpu-iters 0 --warp-kernel $k > $O/warp_only_$k.log 2>&1 || exit $?
+done
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --cpu-iters 0 > $O/bench.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1 || exit $?
+exit 0

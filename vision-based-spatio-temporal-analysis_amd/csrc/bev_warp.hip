@@ -48,6 +48,10 @@
 
 using namespace bev;
 
+// V = 1..64 for which Markstein's fp32 division by V (+ NaN fix-up) equals a / V for every float but -0
+// (tools/verify_div_markstein_fix.c, exhaustive): bit V - 1.
+#define MARKSTEIN_EXACT_V 0xd5555555d555d5dfull
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -374,6 +378,7 @@ __global__ __launch_bounds__(FT_NT, 2) void k_warp_fuse(const float *__restrict_
 // -------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
+typedef int v4i_t __attribute__((ext_vector_type(4)));
 
 
 __device__ __forceinline__ unsigned lds_base(const unsigned char *p) {
@@ -411,44 +416,6 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
     }
 }
 
-// The same DMA through a buffer descriptor based at the block origin (byte strides sH4 / sW4 < 2^24, every
-// byte offset of the feature map < 2^31 -- the launcher checks): per lane only 24-bit integer products and a
-// 32-bit offset, no 64-bit address arithmetic (slot / 17 as (slot * 61681) >> 20, exact for slot < 69632,
-// i.e. footprints < 4096 pixels).  The pad slot (sl == 16) re-reads channel group 0 (any in-range address).
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-template <int S = 17>
-__device__ __forceinline__ void dma_block_buf(const float *__restrict__ f, int sH4, int sW4, int sx0, int sy0, int sbw,
-                                              int npix, unsigned char *smem, int off, int wave, int lane,
-                                              int nwaves = FT_NT / 64) {
-    static_assert(S == 17, "slot decomposition assumes 17 slots per pixel");
-    if (WARP_ABLATE & 2) return;
-    const int ninstr = (npix * S + 63) >> 6;
-    const float inv_bw = 1.0f / (float)sbw;
-    const uint64_t a = (uint64_t)(uintptr_t)f + (uint64_t)((int64_t)sy0 * sH4 + (int64_t)sx0 * sW4);
-    const v4i_t rsrc = {__builtin_amdgcn_readfirstlane((int)(uint32_t)a),
-                        __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu)), 0x7fffffff, 0x00020000};
-    for (int k = wave; k < ninstr; k += nwaves) {
-        const unsigned slot = (unsigned)(k * 64 + lane);
-        const unsigned p = __umul24(slot, 61681u) >> 20;
-        const unsigned sl = slot - ((p << 4) + p);
-        int q = (int)((float)p * inv_bw);
-        int r = (int)p - (int)__umul24((unsigned)q, (unsigned)sbw);
-        const bool hi = r >= sbw, lo = r < 0;
-        q += (int)hi - (int)lo;
-        r += (lo ? sbw : 0) - (hi ? sbw : 0);
-        unsigned voff = __umul24((unsigned)q, (unsigned)sH4) + __umul24((unsigned)r, (unsigned)sW4) + ((sl & 15u) << 4);
-        voff = ((int)p < npix) ? voff : 0u;  // tail lanes: any in-range address
-        const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_base(smem) + off + k * 1024));
-        unsigned keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %1, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(voff), "s"(dst), "s"(rsrc)
-            : "memory");
-    }
-}
-
 #ifndef WARP_PIPE
 #define WARP_PIPE 1  // fused warp v2: LDS sampling software-pipelined by one 4-channel group (1) or not (0)
 #endif
@@ -466,16 +433,9 @@ __device__ unsigned long long g_warp_stamp[16384 * 6];
 #define STAMP(k) ((void)0)
 #endif
 
-#ifndef WARP_TSTORE
-#define WARP_TSTORE 0  // fused warp v2: 16-B output stores through a per-wave LDS transpose (1) or 4-B stores (0)
-#endif
 #ifndef WARP_LANESKIP
 #define WARP_LANESKIP 1  // fused warp v2: lanes with no valid tap skip the view's LDS sampling (1, r03 A/B: 1-8 % faster) or read the zero pixel (0)
 #endif
-#ifndef WARP_DMABUF
-#define WARP_DMABUF 0  // fused warp v2: footprint DMA through a buffer descriptor (1; r03m A/B: 1-8 % slower) or 64-bit global addresses (0)
-#endif
-
 // Output stores of a 64-channel chunk through a buffer descriptor: SGPR base of
 // the chunk, per-lane byte offset of the cell, SGPR byte offset of the channel
 // plane -> no per-store address arithmetic.  The dispatcher guarantees the
@@ -512,43 +472,6 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
             if ((WARP_ABLATE & 16) && r != 1.2345e-30f) continue;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
                                                   (int)(uint32_t)((q0 + u) * plane * sizeof(float)), 2);
-        }
-    }
-}
-
-// Output stores of a whole in-range tile through a per-wave LDS transpose (WARP_TSTORE): each lane holds one
-// cell's 64 channels, but the [C][Hb][Wb] output is contiguous along cells, so the lanes first write their values
-// (after the mean division) to LDS as [channel][wave's 64 cells], then read back 4 consecutive cells of one
-// channel and store them as ONE 16-B store: 16 1-KiB store instructions per wave instead of 64 of 256 B.
-// Two passes of 32 channels (8 KiB of LDS per wave).  Cell slot of a lane: its row inside the wave's band x TW +
-// its column.  Same values, same addresses as store_chunk: bit-identical output.
-template <int TH, int N>
-__device__ __forceinline__ void store_tile_t(float *chunk, size_t plane, int row0, int col0, int Wb, int tr, int tc,
-                                             const float (&acc)[N], int mode, double rV, unsigned char *smem,
-                                             int wave, int lane) {
-    constexpr int TW = FT_NT / TH, RB = TH / 4;  // tile width; rows per wave
-    static_assert(RB * TW == 64 && TW % 4 == 0, "one wave = 64 cells in whole 4-cell quads");
-    float *E = reinterpret_cast<float *>(smem) + wave * (32 * 64);
-    const int slot = (tr - wave * RB) * TW + tc;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * N * sizeof(float)), 0x00020000);
-    const int g = lane & 15, cq = lane >> 4;            // quad of cells, channel within the instruction's four
-    const int r = wave * RB + (4 * g) / TW, c = (4 * g) % TW;
-    const int voff = ((row0 + r) * Wb + col0 + c) * (int)sizeof(float);
-#pragma unroll
-    for (int h = 0; h < N; h += 32) {
-#pragma unroll
-        for (int u = 0; u < 32; ++u) {
-            const float a = acc[h + u];
-            E[u * 64 + slot] = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? div_rcp(a, rV) : a;
-        }
-        // same-wave LDS ops complete in order: the reads below see these writes
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int ch = 4 * k + cq;
-            const f32x4 v = *(const f32x4 *)(E + ch * 64 + 4 * g);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs, voff,
-                                                   (int)(uint32_t)((h + ch) * plane * sizeof(float)), 2);
         }
     }
 }
@@ -830,20 +753,13 @@ __device__ __forceinline__ void tile_cell(int lane, int wave, int &r, int &c) {
     }
 }
 
-// Frames per workgroup (FPW = 2, tcache >= 0): a static rig gives every frame of a batch the same homographies
-// (Wildtrack's cameras do not move), so the workgroup of a tile runs the frames one after the other and the
-// second pass reads each cell's taps from an LDS record written by the first instead of recomputing them:
-// (x0, y0) as int16 (-32768: no valid tap along that axis) + the fractional offsets we = ix - floor(ix) and
-// n = iy - floor(iy), from which the weights and validity bits are rebuilt with the same fp32 operations
-// (bit-identical).  The geometry is compared per view in the prologue; frames that differ take a full pass.
-// The same records serve every further 64-channel chunk of a frame.
-template <int MODE, int OCC, int TH = 8, int FPW = 1>
+template <int MODE, int OCC, int TH = 8>
 __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                           int64_t sW, const float *__restrict__ Hmat,
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
                                                           int B, int V, int C, int Hf, int Wf, float sx, float sy,
                                                           int Hb, int Wb, float *__restrict__ out, int pool,
-                                                          int tcache, const uint2 *__restrict__ boxes) {
+                                                          const uint2 *__restrict__ boxes) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
     constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
@@ -864,55 +780,41 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     STAMP(0);
     int tr, tc;
     tile_cell<TH>(lane, wave, tr, tc);
-    // footprint DMA: buffer-descriptor form when the byte strides fit 24 bits and the map 2^31 bytes (uniform)
-    const bool bufdma = WARP_DMABUF && sH * 4 < (1 << 24) && sW * 4 < (1 << 24) &&
-                        ((int64_t)Hf * sH + (int64_t)Wf * sW) * 4 < (1ll << 31);
     auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
-        if (bufdma) dma_block_buf<SL>(fp, (int)sH * 4, (int)sW * 4, x0, y0, w, n, smem, o, wave, lane, NW);
-        else dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, wave, lane, NW);
+        dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, wave, lane, NW);
     };
     const int i = tyb * TH + tr;
     const int j = txb * TW + tc;
-    const int b0 = blockIdx.y * FPW;
+    const int b = blockIdx.y;
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
     const Grid grid = make_grid(Hf, Wf);
     const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
-    unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes, [2 V] same flag
-    unsigned *tc0 = reinterpret_cast<unsigned *>(smem + (tcache >= 0 ? tcache : 0));  // [V][256] packed x0, y0
-    float2 *tc1 = reinterpret_cast<float2 *>(tc0 + V * FT_NT);                         // [V][256] (we, n)
+    unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes
 
     // corner boxes of this tile for frame bb, lane v <-> view v, packed in two VGPRs (wave 0 computes them in
     // double, the others read them): lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16
-    // (x1 + 1 == 0: empty).  With FPW = 2 wave 0 also compares frame bb + 1's homographies with bb's.
+    // (x1 + 1 == 0: empty).
     unsigned lba = 0, lbb = 0;
-    bool same = false;
-    auto prologue = [&](int bb, bool check_next) {
-        if (WARP_HSCALAR && boxes != nullptr) {  // precomputed by k_warp_boxes (FPW = 1): every wave reads them
+    auto prologue = [&](int bb) {
+        if (WARP_HSCALAR && boxes != nullptr) {  // precomputed by k_warp_boxes: every wave reads them
             const uint2 bx = lane < V ? boxes[((int64_t)bb * nt + tile) * V + lane] : make_uint2(0u, 0u);
             lba = bx.x;
             lbb = bx.y;
-            same = false;
             return;
         }
         if (wave == 0) {
             const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
             const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
             Box cb{0x7fffffff, 0x7fffffff, -1, -1};
-            bool ok = true, eq = true;
+            bool ok = true;
             if (lane < V) {
                 float hv[9];
                 load_h(Hmat, bb * V + lane, hv);
 #pragma unroll
                 for (int q = 0; q < 9; ++q) htab[lane * 9 + q] = hv[q];  // visible after the barrier below
-                if (check_next) {
-                    float hn[9];
-                    load_h(Hmat, (bb + 1) * V + lane, hn);
-#pragma unroll
-                    for (int q = 0; q < 9; ++q) eq = eq && (__float_as_uint(hn[q]) == __float_as_uint(hv[q]));
-                }
                 cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok);
                 // large footprints: the exact per-cell box (usually much smaller near the
                 // horizon, where adjacent cell rows map far apart) decides the staging
@@ -923,15 +825,12 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 btab[2 * lane] = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
                 btab[2 * lane + 1] = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
             }
-            const bool all_eq = check_next && __ballot(lane < V && !eq) == 0ull;
-            if (lane == 0) btab[2 * V2_MAXV] = all_eq ? 1u : 0u;
         }
         __syncthreads();
         lba = lane < V ? btab[2 * lane] : 0u;
         lbb = lane < V ? btab[2 * lane + 1] : 0u;
-        same = btab[2 * V2_MAXV] != 0u;
     };
-    prologue(b0, FPW > 1 && b0 + 1 < B && tcache >= 0);
+    prologue(b);
     STAMP(1);
     auto box_of = [&](int v) {
         const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
@@ -941,27 +840,9 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
 
     float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
-    bool cache_rd = false;     // this chunk reads the tap records (written by an earlier chunk / frame)
-    int hbase = b0 * V;        // homography row of view 0 of the frame being sampled
+    const int hbase = b * V;   // homography row of view 0 of this frame
     auto taps_of = [&](int v) {
         Taps t;
-        if (cache_rd) {
-            const unsigned pk = tc0[v * FT_NT + tid];
-            const float2 f = tc1[v * FT_NT + tid];
-            const int x0s = (int)(short)(pk & 0xffffu), y0s = (int)(short)(pk >> 16);
-            const float e = 1.0f - f.x, s = 1.0f - f.y;  // taps_from_ixy's arithmetic
-            t.w[0] = s * e;
-            t.w[1] = s * f.x;
-            t.w[2] = f.y * e;
-            t.w[3] = f.y * f.x;
-            const bool vx0 = x0s >= 0 && x0s < Wf, vx1 = x0s >= -1 && x0s + 1 < Wf;
-            const bool vy0 = y0s >= 0 && y0s < Hf, vy1 = y0s >= -1 && y0s + 1 < Hf;
-            t.valid = (unsigned)(vx0 & vy0) | ((unsigned)(vx1 & vy0) << 1) | ((unsigned)(vx0 & vy1) << 2) |
-                      ((unsigned)(vx1 & vy1) << 3);
-            t.x0 = (vx0 | vx1) ? x0s : 0;
-            t.y0 = (vy0 | vy1) ? y0s : 0;
-            return t;
-        }
         float h[9];
 #pragma unroll
         for (int q = 0; q < 9; ++q) {  // wave-uniform address: scalar loads (no LDS cycles on the sampling path)
@@ -974,13 +855,6 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         float ix, iy;
         cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
         t = taps_from_ixy(ix, iy, grid);
-        if (FPW > 1 && tcache >= 0) {
-            const float xw = __builtin_floorf(ix), yn = __builtin_floorf(iy);
-            const bool xv = xw >= -1.0f && xw < grid.fWf, yv = yn >= -1.0f && yn < grid.fHf;  // vx0 | vx1, vy0 | vy1
-            const int x0s = (inside && xv) ? t.x0 : -32768, y0s = (inside && yv) ? t.y0 : -32768;
-            tc0[v * FT_NT + tid] = ((unsigned)x0s & 0xffffu) | ((unsigned)y0s << 16);
-            tc1[v * FT_NT + tid] = make_float2(ix - xw, iy - yn);
-        }
         if (WARP_ABLATE & 8) {
             const Box bb = box_of(v);
             t.x0 = bb.x0 + (lane & 1);
@@ -992,16 +866,8 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         return t;
     };
 
-    for (int pass = 0; pass < FPW; ++pass) {
-      const int b = b0 + pass;
-      if (b >= B) break;
-      hbase = b * V;
-      if (pass > 0 && !same) {  // this frame's geometry differs: its own boxes and homographies
-          __syncthreads();
-          prologue(b, false);
-      }
+    {
       for (int c0 = 0; c0 < C; c0 += 64) {
-        cache_rd = FPW > 1 && tcache >= 0 && (c0 > 0 || (pass > 0 && same));
         ccx = cx;
         ccy = cy;
         asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep taps per chunk (no hoisting + spills)
@@ -1145,11 +1011,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             __syncthreads();  // all of it landed; image of view v and red[] are free
         }
         STAMP(3);
-        if (WARP_TSTORE && pool >= 4 * 32 * 64 * 4 && (tyb + 1) * TH <= Hb && (txb + 1) * TW <= Wb && Wb % 4 == 0) {
-            store_tile_t<TH>(out + ((size_t)b * C + c0) * plane, plane, tyb * TH, txb * TW, Wb, tr, tc, acc, MODE, rV,
-                             smem, wave, lane);
-            __syncthreads();  // the transpose's LDS is free before the next chunk / frame stages into the pool
-        } else if (inside) {
+        if (inside) {
             store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
         }
         STAMP(4);
@@ -1157,265 +1019,6 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     }
 }
 
-// -------------------------------------------------------------------------
-// persistent form of k_warp_fuse_v2 (C == 64, corner boxes from the workspace; BEV_TUNE_WARP_KERNEL 3)
-// -------------------------------------------------------------------------
-// The ablation of k_warp_fuse_v2 shows its phases adding up: the ~5400 workgroups of a batch-2 launch
-// run in ~7 lock-step rounds, each computing and then storing, so the 354 MB of output stores (61 us alone) barely
-// overlap the sampling.  Here a workgroup walks (frame, tile) items with stride gridDim.x, and before it stores item
-// k it already reads item k + 1's corner boxes, issues the LDS-DMA of k + 1's first live footprint and computes that
-// view's taps: the stores then drain while the next item starts.  vmcnt counts loads, stores and LDS-DMA in issue
-// order, so the DMA must be OLDER than the stores to be waited for without them: the wait is vmcnt(63) (every
-// operation but the 63 youngest -- the stores -- is complete).  Per item the arithmetic, the view order and the
-// LDS images are exactly k_warp_fuse_v2's: bit-identical output.
-template <int MODE, int OCC, int TH>
-__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_p(const float *__restrict__ feats, int64_t sN, int64_t sH,
-                                                         int64_t sW, const float *__restrict__ Hmat,
-                                                         const float *__restrict__ xs, const float *__restrict__ ys,
-                                                         int B, int V, int Hf, int Wf, float sx, float sy, int Hb,
-                                                         int Wb, float *__restrict__ out, int pool,
-                                                         const uint2 *__restrict__ boxes) {
-    constexpr int NW = FT_NT / 64;
-    constexpr int TW = FT_NT / TH;
-    constexpr int SL = 17, PS = SL * 16;
-    constexpr int C = 64;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int zp = pool;
-    int *red = reinterpret_cast<int *>(smem + pool + 256);
-    const int maxpix = pool / PS - 4;
-    const int ntx = (Wb + TW - 1) / TW, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
-    const int nitems = nt * B;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int tr, tc;
-    tile_cell<TH>(lane, wave, tr, tc);
-    const size_t plane = (size_t)Hb * Wb;
-    const Grid grid = make_grid(Hf, Wf);
-    const double rV = recip_uniform(V);
-    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
-        dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, wave, lane, NW);
-    };
-    // per-item state
-    struct Item {
-        int b, tyb, txb, i, j;
-        bool inside;
-        float cx, cy;
-        unsigned lba, lbb;
-    };
-    auto setup = [&](int item, Item &it) {
-        it.b = item / nt;
-        int tile = item - it.b * nt;
-        {  // XCD-aware tile order within a frame, as k_warp_fuse_v2
-            const int q = nt / 8, r = nt % 8, x = tile % 8;
-            tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
-        }
-        it.tyb = tile / ntx;
-        it.txb = tile - it.tyb * ntx;
-        it.i = it.tyb * TH + tr;
-        it.j = it.txb * TW + tc;
-        it.inside = (it.i < Hb) && (it.j < Wb);
-        it.cx = xs[it.inside ? it.j : 0];
-        it.cy = ys[it.inside ? it.i : 0];
-        const uint2 bx = lane < V ? boxes[((int64_t)it.b * nt + tile) * V + lane] : make_uint2(0u, 0u);
-        it.lba = bx.x;
-        it.lbb = bx.y;
-    };
-    auto box_of = [&](const Item &it, int v) {
-        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)it.lba, v);
-        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)it.lbb, v);
-        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
-    };
-    auto ok_of = [&](const Item &it, int v) {
-        return ((unsigned)__builtin_amdgcn_readlane((int)it.lba, v) >> 31) == 0u;
-    };
-    auto live = [&](const Item &it, int u) { return !ok_of(it, u) || box_of(it, u).x1 >= 0; };
-    auto taps_of = [&](const Item &it, int v, float ccx, float ccy) {
-        float h[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane((it.b * V + v) * 9) + q];
-        float ix, iy;
-        cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
-        Taps t = taps_from_ixy(ix, iy, grid);
-        if (!it.inside) t.valid = 0;
-        return t;
-    };
-    // head of an item: its first live view, the DMA of that view's footprint (when its corner box applies and fits)
-    // and that view's taps -- everything before the first barrier of the item
-    struct Head {
-        int v_first, offn;
-        Box bn;
-        Taps tf;
-        bool have_f;
-    };
-    auto head = [&](const Item &it, Head &hd) {
-        int u = 0;
-        while (u < V && !live(it, u)) ++u;
-        hd.v_first = u;
-        hd.bn = box_of(it, u < V ? u : 0);
-        hd.offn = -1;
-        hd.have_f = false;
-        if (u < V) {
-            const Box &bn = hd.bn;
-            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-            if (ok_of(it, u) && bn.x1 >= 0 && npix <= maxpix) {
-                hd.offn = 0;
-                dma(feats + (int64_t)(it.b * V + u) * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, 0);
-            }
-            if (ok_of(it, u)) {
-                float ccx = it.cx, ccy = it.cy;
-                asm volatile("" : "+v"(ccx), "+v"(ccy));
-                hd.tf = taps_of(it, u, ccx, ccy);
-                hd.have_f = true;
-            }
-        }
-    };
-
-    int item = blockIdx.x;
-    if (item >= nitems) return;
-    Item cur;
-    Head hd;
-    setup(item, cur);
-    head(cur, hd);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // zero pixel + image of the first live view
-    while (true) {
-        float ccx = cur.cx, ccy = cur.cy;
-        asm volatile("" : "+v"(ccx), "+v"(ccy));  // taps per view, not hoisted
-        float acc[C];
-#pragma unroll
-        for (int q = 0; q < C; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
-        if (hd.v_first > 0) zero_view<MODE>(acc, 0);  // views before the first live one contribute 0 (max: max(acc, 0))
-        const float *fb = feats + (int64_t)(cur.b * V) * sN;
-        auto next_live = [&](int u) {
-            ++u;
-            while (u < V && !live(cur, u)) {
-                zero_view<MODE>(acc, u);
-                ++u;
-            }
-            return u;
-        };
-        Box bn = hd.bn;
-        int offn = hd.offn;
-        bool have_f = hd.have_f;
-        for (int v = hd.v_first, vn; v < V; v = vn) {
-            vn = next_live(v);
-            Box bx = bn;
-            const int off = offn;
-            const float *f = fb + (int64_t)v * sN;
-            Taps t;
-            bool have_t = false;
-            if (have_f) {
-                t = hd.tf;
-                have_t = true;
-                have_f = false;
-            }
-            if (!ok_of(cur, v)) {
-                t = taps_of(cur, v, ccx, ccy);
-                have_t = true;
-                put_box<NW>(red, wave_box(t), wave, lane);
-                __syncthreads();
-                bx = get_box<NW>(red);
-            }
-            const bool empty = bx.x1 < 0;
-            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
-            bool done = empty;
-            if (!done && off < 0) {
-                int wb = bw, hb = bh, nbx = 1, nby = 1;
-                if (bw * bh > maxpix) {
-                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
-                    hb = min(bh, maxpix / wb);
-                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
-                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
-                }
-                const bool single = (nbx == 1) && (nby == 1);
-                if (single) dma(f, bx.x0, bx.y0, bw, bw * bh, 0);
-                if (!have_t) {
-                    t = taps_of(cur, v, ccx, ccy);
-                    have_t = true;
-                }
-                int mkx = 0, mky = 0;
-                if (!single && t.valid) {
-                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
-                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
-                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
-                }
-                const bool wave_any = __ballot(t.valid != 0) != 0ull;
-                if (!single && !t.valid) zero_view<MODE>(acc, v);
-                for (int ky = 0; ky < nby; ++ky)
-                    for (int kx = 0; kx < nbx; ++kx) {
-                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
-                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
-                        if (!single) {
-                            __syncthreads();
-                            dma(f, sx0, sy0, sbw, sbw * sbh, 0);
-                        }
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        __syncthreads();
-                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
-                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE, 1, 64>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
-                        else if (single) zero_view<MODE>(acc, v);
-                    }
-                done = true;
-                __syncthreads();
-            }
-            if (vn < V) {
-                bn = box_of(cur, vn);
-                offn = -1;
-                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-                if (ok_of(cur, vn) && bn.x1 >= 0 && npix <= maxpix) {
-                    const int need = ((npix * SL + 63) >> 6) * 1024;
-                    if (done || off < 0) offn = 0;
-                    else if (off == 0) {
-                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
-                    } else if (need <= off) offn = 0;
-                    if (offn >= 0) dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, offn);
-                }
-            }
-            if (!done) {
-                if (!have_t) t = taps_of(cur, v, ccx, ccy);
-                if (__ballot(t.valid != 0) != 0ull) {
-                    if (!WARP_LANESKIP || t.valid)
-                        sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
-                    else zero_view<MODE>(acc, v);
-                } else zero_view<MODE>(acc, v);
-            } else if (empty) {
-                zero_view<MODE>(acc, v);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();  // image of view v and red[] are free
-        }
-        // the next item's boxes, first footprint DMA and first taps go out BEFORE this item's stores
-        const int nitem = item + gridDim.x;
-        const bool more = nitem < nitems;
-        Item nxt;
-        Head nh;
-        if (more) {
-            setup(nitem, nxt);
-            head(nxt, nh);
-        }
-        const bool any_in = __ballot(cur.inside) != 0ull;  // the wave issues its 64 stores (else none at all)
-        if (cur.inside)
-            store_chunk(out + (size_t)cur.b * C * plane, plane, cur.i * Wb + cur.j, acc, MODE, rV);
-        if (!more) break;
-        // the DMA is older than this wave's 64 stores: all but the 63 youngest operations = the DMA has landed
-        if (any_in) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        cur = nxt;
-        hd = nh;
-        item = nitem;
-    }
-}
-
-template <int OCC>
-int launch_fuse_p(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                  const float *ys, int B, int V, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
-                  float *out, hipStream_t st, int pool, uint2 *boxes);
-
-// Corner boxes of every (frame, tile, view) for k_warp_fuse_v2 (FPW = 1), one thread each: the tile prologue's
-// arithmetic (corner_box + the pool-size test) moved out of the sampling kernel, whose workgroups then start
-// with one 8-byte load per view instead of a double-precision latency chain on one wave while three wait.
 template <int TH, int TW = FT_NT / TH>
 __global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hmat, const float *__restrict__ xs,
                                                     const float *__restrict__ ys, int V, int Hf, int Wf, float sx,
@@ -1444,230 +1047,257 @@ __global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hm
 }
 
 // -------------------------------------------------------------------------
-// fused warp + reduce, wave-independent (k_warp_fuse_w): no workgroup barrier
+// fused warp + sum / mean v3: DPP row runs (default for NHWC features with C % 64 == 0, modes SUM / MEAN)
 // -------------------------------------------------------------------------
-// The workgroup's four waves share nothing but the launch: wave w owns the 4 x 16 cells of rows 4w .. 4w + 3 of
-// the 16 x 16 tile (the same cells, lanes, taps, sampling order and stores as k_warp_fuse_v2<.., 16, 1>, hence
-// bit-identical results), and stages, for each view, the footprint of ITS cells into its own slice of LDS (pool
-// `wpool` bytes + a zero pixel).  Its own LDS-DMA completes under its own vmcnt, so the per-view workgroup barrier
-// of v2 is gone: the waves drift apart and hide each other's DMA / tap / sampling latency.  Footprints are
-// per-wave corner boxes (k_warp_boxes over 4 x 16 tiles; in-lane if no workspace); the ring anchors consecutive
-// images at opposite ends of the pool; a footprint larger than what is free is staged synchronously, in
-// overlapping blocks when larger than the pool; tiles where the corner bound does not apply reduce their exact
-// per-cell box by shuffles.  Staging volume ~2x v2's (smaller tiles overlap more), LDS-read and VALU work equal.
-template <int MODE, int OCC>
-__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_w(const float *__restrict__ feats, int64_t sN, int64_t sH,
-                                                         int64_t sW, const float *__restrict__ Hmat,
-                                                         const float *__restrict__ xs, const float *__restrict__ ys,
-                                                         int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                                                         int Hb, int Wb, float *__restrict__ out, int wpool,
-                                                         const uint2 *__restrict__ boxes) {
-    constexpr int TH = 16, TW = 16, SL = 17, PS = SL * 16;
+// Workgroup = one (frame, 16 x 16 BEV tile), 4 waves, wave w = tile rows 4w .. 4w + 3, one 16-lane DPP row per tile
+// row.  Lane l of a row computes the taps of cell l of its row (once per view, the bit-exact recipe) and holds, for
+// ALL 16 cells of the row, the 4 channels 4l .. 4l + 3 of the 64-channel chunk: acc[16][4].  A row walks its cells
+// k = 0..15: cell k's quad key, tap addresses and weights come from lane k by DPP row broadcast (row_newbcast), the
+// row reads the quad's four 256-B pixels with one ds_read_b128 per tap (lane l: bytes 16l .. 16l + 15 -- every
+// 16-lane LDS group reads whole pixels, conflict-free on the unpadded 256-B pixel layout), and the bilinear combine is
+// the reference's FMA chain per channel.  Consecutive cells usually share a quad (Appendix-B rig: 80 % have their
+// left neighbour's): the reads are skipped whenever no row of the wave enters a new quad (wave-uniform ballot) --
+// half of the steps on the rig, so half the LDS reads of one read per (cell, view, tap).
+// Footprints: conservative corner boxes from k_warp_boxes (workspace).  The views of a tile are staged in batches:
+// as many consecutive views as fit the pool, each box row one contiguous NHWC run moved by LDS-DMA (4 pixels per
+// 1-KiB instruction, no per-lane index arithmetic), ONE vmcnt wait + barrier per batch, then the batch's views are
+// walked in view order (the reference's v = 0..V-1 accumulation from +0).  Views whose box does not apply (w sign
+// change / |w| near 1e-6) or does not fit the pool read their taps straight from global memory (same walk).
+// Output: each lane stores its 4 channel planes x 16 cells as 16-B non-temporal stores; the mean divides by V in
+// fp32 (Markstein's correction step, exact for the verified V -- tools/verify_div_markstein_fix.c) or through
+// div_rcp.  Bit-identical to k_warp_fuse_v2 (same taps, weights, FMA chain, view order, division result).
+constexpr int W3_PIX = 256;  // staged bytes per pixel (one unpadded 64-channel chunk)
+
+template <int K>
+__device__ __forceinline__ int rbc(int v) {  // lane K of this lane's 16-lane DPP row
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);
+}
+template <int K>
+__device__ __forceinline__ float rbcf(float v) {
+    return __builtin_bit_cast(float, rbc<K>(__builtin_bit_cast(int, v)));
+}
+
+// one lane's cell for one view, broadcast along its row during the walk
+struct CellTap {
+    int key;    // (x0 + 1) | (y0 + 1) << 14 | valid << 28; 0 = no valid tap (never a real key; -1 neither)
+    int a[4];   // staged: LDS byte address of each tap (the zero pixel if invalid); direct: element offset or -1
+    float w[4]; // bilinear weights nw, ne, sw, se (all 0 when no tap is valid)
+};
+
+template <int K>
+__device__ __forceinline__ void w3_step(float (&acc)[16][4], f32x4 (&qv)[4], int &cur, CellTap &c,
+                                        const unsigned char *smem, __amdgpu_buffer_rsrc_t rs, bool direct, int l16) {
+    // the broadcast sources are re-defined per step: no hoisting of all 16 steps' broadcasts (register pressure)
+    asm volatile("" : "+v"(c.key), "+v"(c.a[0]), "+v"(c.a[1]), "+v"(c.a[2]), "+v"(c.a[3]), "+v"(c.w[0]),
+                 "+v"(c.w[1]), "+v"(c.w[2]), "+v"(c.w[3]));
+    const int kk = rbc<K>(c.key);
+    if (__ballot(kk != cur) != 0ull) {  // wave-uniform: some row enters a new quad -> every row reads its quad
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int at = rbc<K>(c.a[t]);
+            if (direct) {  // (uniform) buffer loads: an invalid tap's out-of-range offset reads 0
+                const int vo = at >= 0 ? at * 4 + 16 * l16 : 0x7ffffff0;
+                qv[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0));
+            } else {
+                qv[t] = *reinterpret_cast<const f32x4 *>(smem + at + 16 * l16);
+            }
+        }
+    }
+    cur = kk;
+    const float w0 = rbcf<K>(c.w[0]), w1 = rbcf<K>(c.w[1]), w2 = rbcf<K>(c.w[2]), w3 = rbcf<K>(c.w[3]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // grid_sampler_2d's chain (bilerp), then the view sum
+        float s = qv[0][u] * w0;
+        s = __builtin_fmaf(qv[1][u], w1, s);
+        s = __builtin_fmaf(qv[2][u], w2, s);
+        s = __builtin_fmaf(qv[3][u], w3, s);
+        acc[K][u] = acc[K][u] + s;
+    }
+    // and the step's sums are complete here: without this the compiler defers the FMAs of many steps (keeping
+    // their broadcast weights and quads live -- spills)
+    asm volatile("" : "+v"(acc[K][0]), "+v"(acc[K][1]), "+v"(acc[K][2]), "+v"(acc[K][3]));
+}
+
+template <int K>
+__device__ __forceinline__ void w3_walk(float (&acc)[16][4], f32x4 (&qv)[4], int &cur, CellTap &c,
+                                        const unsigned char *smem, __amdgpu_buffer_rsrc_t rs, bool direct, int l16) {
+    w3_step<K>(acc, qv, cur, c, smem, rs, direct, l16);
+    if constexpr (K + 1 < 16) w3_walk<K + 1>(acc, qv, cur, c, smem, rs, direct, l16);
+}
+
+// Stage one view's box (bx0, by0, bw x bh pixels of the map at chunk channel 0) into LDS at byte offset img: row r at
+// img + r * bw4 * 256 (bw4 = bw rounded up to 4 pixels), 4 pixels per LDS-DMA instruction, rows round-robin over
+// the waves.  Lane l moves bytes 16 (l & 15) .. of pixel 4i + (l >> 4) of the row.
+__device__ __forceinline__ void w3_stage(const float *__restrict__ map, int64_t sH, int64_t sW, int bx0, int by0,
+                                         int bw, int bh, unsigned char *smem, int img, int wave, int lane) {
+    if (WARP_ABLATE & 2) return;
+    const int bw4 = (bw + 3) & ~3, nins = bw4 >> 2;
+    const int px = lane >> 4, cb = (lane & 15) * 4;
+    for (int r = wave; r < bh; r += FT_NT / 64) {
+        const float *row = map + (int64_t)(by0 + r) * sH + (int64_t)bx0 * sW + cb;
+        const int dst0 = (int)lds_base(smem) + img + r * bw4 * W3_PIX;
+        for (int i = 0; i < nins; ++i) {
+            const int x = 4 * i + px;
+            const unsigned dst = (unsigned)__builtin_amdgcn_readfirstlane(dst0 + i * 1024);
+            if (x < bw) {
+                const float *src = row + (int64_t)x * sW;
+                unsigned keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                    "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "v"(src), "s"(dst)
+                    : "memory");
+            }
+        }
+    }
+}
+
+// a / V in fp32: Markstein's correction step + the NaN fix-up (exact for every float but -0 when V is in the verified
+// set; the view sum is never -0), else div_rcp through double.
+__device__ __forceinline__ float w3_div(float a, float vf, float r, double rV, bool fast) {
+    if (fast) {
+        const float q0 = a * r;
+        const float q = __builtin_fmaf(__builtin_fmaf(-q0, vf, a), r, q0);
+        return q != q ? q0 : q;
+    }
+    return div_rcp(a, rV);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(FT_NT, 3) void k_warp_fuse_v3(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                           int64_t sW, const float *__restrict__ Hmat,
+                                                           const float *__restrict__ xs, const float *__restrict__ ys,
+                                                           int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                                                           int Hb, int Wb, float *__restrict__ out, int pool,
+                                                           const uint2 *__restrict__ boxes, int fastdiv) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int ib = wave * (wpool + 256);  // this wave's pool (byte offset in smem), zero pixel after it
-    const int zp = ib + wpool;
-    const int maxpix = wpool / PS - 4;
-    const int ntx = (Wb + TW - 1) / TW, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
+    const int zp = pool;  // the zero pixel (256 B) after the pool
+    const int ntx = (Wb + 15) / 16, nty = (Hb + 15) / 16, nt = ntx * nty;
     int tile = blockIdx.x;
-    {
+    {  // XCD-aware order: neighbouring tiles (shared source pixels) on one XCD's L2
         const int q = nt / 8, r = nt % 8, x = tile % 8;
         tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
     }
-    const int tyb = tile / ntx, txb = tile - tyb * ntx;
-    const int wtile = (tyb * 4 + wave) * ntx + txb;  // this wave's 4 x 16 box tile
-    STAMP(0);
-    int tr, tc;
-    tile_cell<TH>(lane, wave, tr, tc);
-    const bool bufdma = WARP_DMABUF && sH * 4 < (1 << 24) && sW * 4 < (1 << 24) &&
-                        ((int64_t)Hf * sH + (int64_t)Wf * sW) * 4 < (1ll << 31);
-    auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
-        if (bufdma) dma_block_buf<SL>(fp, (int)sH * 4, (int)sW * 4, x0, y0, w, n, smem, o, 0, lane, 1);
-        else dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, 0, lane, 1);
-    };
-    const int i = tyb * TH + tr;
-    const int j = txb * TW + tc;
+    const int ty = tile / ntx, tx = tile - ty * ntx;
     const int b = blockIdx.y;
-    const bool inside = (i < Hb) && (j < Wb);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l16 = lane & 15;
+    const int i = ty * 16 + wave * 4 + (lane >> 4), j0 = tx * 16, j = j0 + l16;
+    const bool inside = i < Hb && j < Wb;
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
-    const size_t plane = (size_t)Hb * Wb;
     const Grid grid = make_grid(Hf, Wf);
-    const double rV = recip_uniform(V);
-    if (lane < 16) *(float4 *)(smem + zp + lane * 16) = make_float4(0.f, 0.f, 0.f, 0.f);  // read after, same wave
-
-    // per-wave corner boxes, lane v <-> view v (v2's packing)
-    unsigned lba = 0, lbb = 0;
-    if (boxes != nullptr) {
-        const uint2 bx = lane < V ? boxes[((int64_t)b * (nt * 4) + wtile) * V + lane] : make_uint2(0u, 0u);
-        lba = bx.x;
-        lbb = bx.y;
-    } else if (lane < V) {
-        const int ia = tyb * TH + 4 * wave, ibr = min(ia + 3, Hb - 1);
-        const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
-        Box cb{0x7fffffff, 0x7fffffff, -1, -1};
-        bool ok = true;
-        if (ia < Hb) {
-            float hv[9];
-            load_h(Hmat, b * V + lane, hv);
-            cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ibr], sx, sy, Wf, Hf, ok);
-            if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
-        }
-        const bool emp = cb.x1 < 0;
-        lba = (emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u);
-        lbb = emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16);
-    }
-    STAMP(1);
+    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+    // boxes of this (frame, tile): lane v of every wave holds view v's (k_warp_boxes format)
+    uint2 bxv = make_uint2(0u, 0u);
+    if (lane < V) bxv = boxes[((int64_t)b * nt + tile) * V + lane];
     auto box_of = [&](int v) {
-        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
-        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)bxv.x, v);
+        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)bxv.y, v);
         return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
     };
-    auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
-    const int hbase = b * V;
-    float ccx = cx, ccy = cy;
-    auto taps_of = [&](int v) {
-        float h[9];
-#pragma unroll
-        for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane((hbase + v) * 9) + q];
-        float ix, iy;
-        cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
-        Taps t = taps_from_ixy(ix, iy, grid);
-        if (WARP_ABLATE & 8) {
-            const Box bb = box_of(v);
-            t.x0 = bb.x0 + (lane & 1);
-            t.y0 = bb.y0;
-            t.valid = (bb.x1 > bb.x0 + 1 && bb.y1 > bb.y0) ? 15u : 0u;
-            t.w[0] = t.w[1] = t.w[2] = t.w[3] = 0.25f;
-        }
-        if (!inside) t.valid = 0;
-        return t;
-    };
+    auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)bxv.x, v) >> 31) == 0u; };
+    auto need_of = [&](const Box &bo) { return (bo.y1 - bo.y0 + 1) * (((bo.x1 - bo.x0 + 1) + 3) & ~3) * W3_PIX; };
+    const float vf = (float)V, rf = (float)(1.0 / (double)V);
+    const double rV = recip_uniform(V);
+    const size_t plane = (size_t)Hb * Wb;
 
     for (int c0 = 0; c0 < C; c0 += 64) {
-        ccx = cx;
-        ccy = cy;
-        asm volatile("" : "+v"(ccx), "+v"(ccy));  // taps per chunk (no hoisting + spills)
-        float acc[64];
+        float acc[16][4];
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        for (int k = 0; k < 16; ++k)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[k][u] = 0.0f;
         const float *fb = feats + (int64_t)(b * V) * sN + c0;
-        auto live = [&](int u) { return !ok_of(u) || box_of(u).x1 >= 0; };
-        auto next_live = [&](int u) {
-            ++u;
-            while (u < V && !live(u)) {
-                zero_view<MODE>(acc, u);
-                ++u;
+        for (int v = 0; v < V;) {
+            // ---- stage a batch: consecutive views while their images fit the pool ----
+            int off = 0, u = v;
+            for (; u < V; ++u) {
+                const Box bo = box_of(u);
+                if (bo.x1 < 0 || !ok_of(u)) continue;  // empty (no work) or direct (no staging)
+                const int need = need_of(bo);
+                if (need > pool) continue;  // direct
+                if (off + need > pool) break;
+                w3_stage(fb + (int64_t)u * sN, sH, sW, bo.x0, bo.y0, bo.x1 - bo.x0 + 1, bo.y1 - bo.y0 + 1, smem, off,
+                         wave, lane);
+                off += need;
             }
-            return u;
-        };
-        const int v_first = next_live(-1);
-        Box bn = box_of(v_first < V ? v_first : 0);
-        int offn = -1;
-        if (v_first < V) {
-            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-            if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
-                offn = ib;
-                dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, ib);
+            const int vend = u;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA landed
+            __syncthreads();                                  // every wave's (and the zero pixel)
+            // ---- walk the batch's views in view order ----
+            off = 0;
+            for (u = v; u < vend; ++u) {
+                const Box bo = box_of(u);
+                if (bo.x1 < 0) continue;  // the tile misses this view: +0 for every cell, exact to skip
+                const int need = need_of(bo);
+                const bool direct = !ok_of(u) || need > pool;
+                const int img = off;
+                if (!direct) off += need;
+                float h[9];
+#pragma unroll
+                for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane((b * V + u) * 9) + q];
+                float ix, iy;
+                cell_ixy(h, cx, cy, grid, sx, sy, ix, iy);
+                Taps t = taps_from_ixy(ix, iy, grid);
+                if (!inside) t.valid = 0;
+                CellTap c;
+                c.key = t.valid ? (t.x0 + 1) | ((t.y0 + 1) << 14) | ((int)t.valid << 28) : 0;
+                const bool any = t.valid != 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) c.w[q] = any ? t.w[q] : 0.0f;
+                if (direct) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        c.a[q] = (t.valid & (1u << q))
+                                     ? (int)((int64_t)(t.y0 + (q >> 1)) * sH + (int64_t)(t.x0 + (q & 1)) * sW)
+                                     : -1;
+                } else {
+                    const int bw4 = ((bo.x1 - bo.x0 + 1) + 3) & ~3;
+                    const int p0 = img + ((t.y0 - bo.y0) * bw4 + (t.x0 - bo.x0)) * W3_PIX;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        c.a[q] = (t.valid & (1u << q)) ? p0 + ((q >> 1) * bw4 + (q & 1)) * W3_PIX : zp;
+                }
+                f32x4 qv[4];
+                int cur = -1;
+                if (WARP_ABLATE & 4) continue;
+                // direct views: the view's map at this chunk as a buffer (bytes: every pixel's 64 channels)
+                const int nbytes = direct ? (int)(((int64_t)(Hf - 1) * sH + (int64_t)(Wf - 1) * sW + 64) * 4) : 0;
+                const __amdgpu_buffer_rsrc_t rs =
+                    __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(fb + (int64_t)u * sN), 0, nbytes, 0x00020000);
+                w3_walk<0>(acc, qv, cur, c, smem, rs, direct, l16);
             }
+            __syncthreads();  // the pool is free for the next batch
+            v = vend;
         }
-        Taps tf;
-        bool have_f = false;
-        if (v_first < V && ok_of(v_first)) {
-            tf = taps_of(v_first);
-            have_f = true;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's own DMA: visible to its own reads
-        STAMP(2);
-
-        for (int v = v_first, vn; v < V; v = vn) {
-            vn = next_live(v);
-            Box bx = bn;
-            const int off = offn;
-            const float *f = fb + (int64_t)v * sN;
-            Taps t;
-            bool have_t = false;
-            if (have_f) {
-                t = tf;
-                have_t = true;
-                have_f = false;
-            }
-            if (!ok_of(v)) {  // exact per-cell box of this wave's cells (shuffle reduction, no exchange)
-                t = taps_of(v);
-                have_t = true;
-                bx = wave_box(t);
-            }
-            const bool empty = bx.x1 < 0;
-            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
-            bool done = empty;
-            if (!done && off < 0) {
-                // synchronous staging (overlapping blocks if larger than the pool); the pool's previous
-                // images have been read: every earlier ds_read's result was consumed by its FMAs
-                int wb = bw, hb = bh, nbx = 1, nby = 1;
-                if (bw * bh > maxpix) {
-                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
-                    hb = min(bh, maxpix / wb);
-                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
-                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
-                }
-                const bool single = (nbx == 1) && (nby == 1);
-                if (single) dma(f, bx.x0, bx.y0, bw, bw * bh, ib);
-                if (!have_t) {
-                    t = taps_of(v);
-                    have_t = true;
-                }
-                int mkx = 0, mky = 0;
-                if (!single && t.valid) {
-                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
-                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
-                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
-                }
-                const bool wave_any = __ballot(t.valid != 0) != 0ull;
-                if (!single && !t.valid) zero_view<MODE>(acc, v);
-                for (int ky = 0; ky < nby; ++ky)
-                    for (int kx = 0; kx < nbx; ++kx) {
-                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
-                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
-                        if (!single) {
-                            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous block's reads returned
-                            dma(f, sx0, sy0, sbw, sbw * sbh, ib);
+        // ---- output: channel planes 4 l16 .. 4 l16 + 3, cells j0 .. j0 + 15 of row i ----
+        if (i < Hb && !(WARP_ABLATE & 16)) {
+            float *ob = out + ((size_t)b * C + c0 + 4 * l16) * plane + (size_t)i * Wb + j0;
+            const bool mean = MODE == BEV_FUSE_MEAN && !(WARP_ABLATE & 1);
+            if (j0 + 16 <= Wb && (Wb & 3) == 0) {
+#pragma unroll
+                for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        f32x4 o;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float a = acc[4 * m + e][uu];
+                            o[e] = mean ? w3_div(a, vf, rf, rV, fastdiv != 0) : a;
                         }
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
-                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE, 1, 64>(acc, t, mine, v, smem, ib, sx0, sy0, sbw, zp);
-                        else if (single) zero_view<MODE>(acc, v);
+                        __builtin_nontemporal_store(o, reinterpret_cast<f32x4 *>(ob + uu * plane + 4 * m));
                     }
-                done = true;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the pool is free for the next DMA
+            } else {
+#pragma unroll
+                for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+                    for (int k = 0; k < 16; ++k)
+                        if (j0 + k < Wb) {
+                            const float a = acc[k][uu];
+                            ob[uu * plane + k] = mean ? w3_div(a, vf, rf, rV, fastdiv != 0) : a;
+                        }
             }
-            // look ahead: DMA of the next live view beside the live image of view v
-            if (vn < V) {
-                bn = box_of(vn);
-                offn = -1;
-                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-                if (ok_of(vn) && bn.x1 >= 0 && npix <= maxpix) {
-                    const int need = ((npix * SL + 63) >> 6) * 1024;
-                    if (done || off < 0) offn = ib;
-                    else if (off == ib) {
-                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= wpool) offn = ib + wpool - need;
-                    } else if (need <= off - ib) offn = ib;
-                    if (offn >= 0) dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, offn);
-                }
-            }
-            if (!done) {
-                if (!have_t) t = taps_of(v);
-                if (WARP_ABLATE & 4) acc[0] += t.w[0] * t.w[3] + (float)(t.x0 + t.y0 + (int)t.valid);
-                else if (__ballot(t.valid != 0) != 0ull)
-                    sample_view_pipe<MODE, 64>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
-                else zero_view<MODE>(acc, v);
-            } else if (empty) {
-                zero_view<MODE>(acc, v);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // view v + 1's image landed
         }
-        STAMP(3);
-        if (inside) store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
-        STAMP(4);
     }
 }
 
@@ -1722,7 +1352,8 @@ inline int last() { return (int)hipGetLastError(); }
 
 // ---- performance knobs (bev_tune; results never depend on them) -------------
 int g_warp_pool_kb = 0;  // BEV_TUNE_WARP_POOL_KB: LDS image pool / ring per workgroup, 0 = automatic
-int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 LDS-DMA kernel (k_warp_fuse_v2, default), 1 register-staged
+int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 default (k_warp_fuse_v3 where it applies), 1 register-staged
+                         // k_warp_fuse, 2 per-view LDS-DMA k_warp_fuse_v2
 int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = WARP_BWD_POOL_MAX
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
@@ -1778,118 +1409,72 @@ int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
 #ifndef WARP_TILE_H
 #define WARP_TILE_H 16  // fused-warp tile: 16 x 16 (default) or 8 x 32 cells (A/B builds)
 #endif
-#ifndef WARP_PAIR
-#define WARP_PAIR 0  // frames per workgroup with the LDS tap records: 0 off (default), 1 on (A/B builds; r03d:
-                     // 176 vs 131 us for the batch-2 bench launch -- half the workgroups, a tail and a smaller pool)
-#endif
 #ifndef WARP_OCC
 #define WARP_OCC 3   // workgroups per CU the default (mean / sum) kernel is compiled and sized for
 #endif
 constexpr int V2_FIXED = 256 + 4 * (FT_NT / 64) * (int)sizeof(int) + V2_MAXV * 9 * (int)sizeof(float) +
-                         (2 * V2_MAXV + 4) * (int)sizeof(unsigned);  // zero pixel, red, htab, btab + flag
-constexpr int V2_TC_MAXV = 8;  // tap records only for rigs of up to 8 cameras (12 B per cell and view)
+                         (2 * V2_MAXV + 4) * (int)sizeof(unsigned);  // zero pixel, red, htab, btab
 
-template <int OCC, int FPW>
+template <int OCC>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                       int mode, float *out, hipStream_t st, int pool, int tc_bytes, uint2 *boxes) {
+                       int mode, float *out, hipStream_t st, int pool, uint2 *boxes) {
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
-    dim3 grid(ntiles, (B + FPW - 1) / FPW), block(FT_NT);
-    const int tcache = tc_bytes > 0 ? pool + V2_FIXED : -1;
-    const size_t lds = (size_t)pool + V2_FIXED + (tc_bytes > 0 ? tc_bytes : 0);
-    if (FPW != 1 || !WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (frame pairs / LDS homographies)
+    dim3 grid(ntiles, B), block(FT_NT);
+    const size_t lds = (size_t)pool + V2_FIXED;
+    if (!WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (LDS homographies)
     if (boxes) {
         const int maxpix = pool / (17 * 16) - 4;  // the kernel's own pool test
         hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                            st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes);
     }
     if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache, boxes);
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
     else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache, boxes);
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
     else
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH, FPW>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, tcache, boxes);
+        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
     return last();
 }
 
-template <int OCC>
-int launch_fuse_p(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                  const float *ys, int B, int V, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
-                  float *out, hipStream_t st, int pool, uint2 *boxes) {
-    constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
-    const int nty = (Hb + TH - 1) / TH, ntiles = ((Wb + TW - 1) / TW) * nty;
-    const int maxpix = pool / (17 * 16) - 4;
-    hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0, st,
-                       Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, nty, boxes);
-    const int64_t nitems = (int64_t)ntiles * B;
-    const unsigned g = (unsigned)(nitems < (int64_t)OCC * cu_count() ? nitems : (int64_t)OCC * cu_count());
-    const size_t lds = (size_t)pool + V2_FIXED;
-    if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_p<BEV_FUSE_SUM, OCC, TH>), dim3(g), dim3(FT_NT), lds, st, feats, sN, sH, sW,
-                           Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_p<BEV_FUSE_MEAN, OCC, TH>), dim3(g), dim3(FT_NT), lds, st, feats, sN, sH, sW,
-                           Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
-    else if constexpr (OCC == 2)  // MAX's extra live state spills at 3 workgroups per CU
-        hipLaunchKernelGGL((k_warp_fuse_p<BEV_FUSE_MAX, OCC, TH>), dim3(g), dim3(FT_NT), lds, st, feats, sN, sH, sW,
-                           Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
-    else
-        return BEV_ERR_ARGS;
-    return last();
-}
+// V for which k_warp_fuse_v3's fp32 mean division (w3_div) is exact for every input but -0: bit V - 1, from the
+// exhaustive check tools/verify_div_markstein_fix.c (other V divide through double, div_rcp).
+constexpr uint64_t W3_FASTDIV_V = MARKSTEIN_EXACT_V;
 
-// wave-independent kernel: 4 x (pool + zero pixel) per workgroup, OCC workgroups per CU
-template <int OCC>
-int launch_fuse_w_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
-                      const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
-                      float *out, hipStream_t st, uint2 *boxes) {
-    const int ntx = (Wb + 15) / 16, nty = (Hb + 15) / 16;
-    const int wpool = g_warp_pool_kb ? g_warp_pool_kb * 1024 / 4 : ((163840 / OCC - 64) / 4 - 256) & ~1023;
-    if (wpool < 4096) return BEV_ERR_ARGS;
-    if (boxes) {
-        const int maxpix = wpool / (17 * 16) - 4;
-        hipLaunchKernelGGL((k_warp_boxes<4, 16>), dim3((unsigned)(((int64_t)ntx * nty * 4 * V + 255) / 256), B),
-                           dim3(256), 0, st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, nty * 4, boxes);
-    }
-    dim3 grid(ntx * nty, B), block(FT_NT);
-    const size_t lds = (size_t)4 * (wpool + 256);
+int launch_fuse_v3(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
+                   const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb, int mode,
+                   float *out, hipStream_t st, uint2 *boxes) {
+    const int ntx = (Wb + 15) / 16, nty = (Hb + 15) / 16, ntiles = ntx * nty;
+    // 3 workgroups per CU: pool + zero pixel <= 160 KiB / 3
+    const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : ((163840 / 3 - 256 - 64) & ~1023);
+    hipLaunchKernelGGL((k_warp_boxes<16, 16>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
+                       st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, pool / W3_PIX, nty, boxes);
+    const int fastdiv = (V >= 1 && V <= 64 && ((W3_FASTDIV_V >> (V - 1)) & 1)) ? 1 : 0;
+    const size_t lds = (size_t)pool + 256;
     if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_w<BEV_FUSE_SUM, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B,
-                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, wpool, boxes);
-    else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_w<BEV_FUSE_MEAN, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys,
-                           B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, wpool, boxes);
-    else if constexpr (OCC == 2)  // MAX's extra live state spills at 3 workgroups per CU
-        hipLaunchKernelGGL((k_warp_fuse_w<BEV_FUSE_MAX, OCC>), grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B,
-                           V, C, Hf, Wf, sx, sy, Hb, Wb, out, wpool, boxes);
+        hipLaunchKernelGGL(k_warp_fuse_v3<BEV_FUSE_SUM>, dim3(ntiles, B), dim3(FT_NT), lds, st, feats, sN, sH, sW, Hmat,
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, fastdiv);
     else
-        return BEV_ERR_ARGS;
+        hipLaunchKernelGGL(k_warp_fuse_v3<BEV_FUSE_MEAN>, dim3(ntiles, B), dim3(FT_NT), lds, st, feats, sN, sH, sW,
+                           Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, fastdiv);
     return last();
 }
 
 inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                           int Hb, int Wb, int mode, float *out, hipStream_t st, uint2 *boxes) {
+    const int kb = g_warp_pool_kb > 0 && g_warp_pool_kb < 8 ? 8 : g_warp_pool_kb;  // v2 needs >= 8 KiB
     if (mode == BEV_FUSE_MAX)  // MAX's extra live state spills at 3 workgroups per CU
-        return launch_fuse_v2_occ<2, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                        st, g_warp_pool_kb ? g_warp_pool_kb * 1024 : 72 * 1024, 0, boxes);
-    // tap records: worth it when a workgroup runs two frames or several 64-channel chunks
-    const int tc_bytes = V * FT_NT * 12;
-    const bool pair = WARP_PAIR && V <= V2_TC_MAXV && (B > 1 || C > 64);
-    // 3 workgroups per CU: pool + fixed + records <= 160 KiB / 3 (the pool shrinks by the records)
-    const int budget = 163840 / 3 - V2_FIXED - 64;
-    const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : ((pair ? budget - tc_bytes : 49 * 1024) & ~1023);
-    if (pair && pool >= 16 * 1024 && pool + V2_FIXED + tc_bytes <= 160 * 1024)
-        return launch_fuse_v2_occ<3, 2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                        pool, tc_bytes, boxes);
-    return launch_fuse_v2_occ<WARP_OCC, 1>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                           st, g_warp_pool_kb ? g_warp_pool_kb * 1024 :
-                                           ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) < 49 * 1024 ?
-                                           ((163840 / WARP_OCC - V2_FIXED - 64) & ~1023) : 49 * 1024, 0, boxes);
+        return launch_fuse_v2_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                     kb ? kb * 1024 : 72 * 1024, boxes);
+    const int pool3 = (163840 / WARP_OCC - V2_FIXED - 64) & ~1023;
+    return launch_fuse_v2_occ<WARP_OCC>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
+                                        st, kb ? kb * 1024 : (pool3 < 49 * 1024 ? pool3 : 49 * 1024),
+                                        boxes);
 }
 
 }  // namespace
@@ -1903,11 +1488,11 @@ int warp_tune(int knob, int value) {
     switch (knob) {
         case BEV_TUNE_WARP_POOL_KB:
             slot = &g_warp_pool_kb;
-            ok = value == 0 || (value >= 8 && value <= 150);
+            ok = value >= 0 && value <= 150;  // v3 takes any pool; v2 clamps to >= 8 KiB
             break;
         case BEV_TUNE_WARP_KERNEL:
             slot = &g_warp_kernel;
-            ok = value >= 0 && value <= 3;
+            ok = value >= 0 && value <= 2;
             break;
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
@@ -1980,11 +1565,11 @@ int bev_ipm_warp_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int
 
 int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb) {
     if (B < 0 || V <= 0 || Hb < 0 || Wb < 0) return BEV_ERR_ARGS;
-    // the larger of the two box tables: v2's (TH x TW tiles) and the wave-independent kernel's (4 x 16)
+    // per-(frame, tile, view) footprint boxes (16 x 16 tiles, v2 and v3; A/B builds of v2 with 8 x 32 tiles have as
+    // many)
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
-    const int64_t v2 = (((int64_t)Wb + TW - 1) / TW) * (((int64_t)Hb + TH - 1) / TH);
-    const int64_t wv = (((int64_t)Wb + 15) / 16) * (((int64_t)Hb + 15) / 16) * 4;
-    return (int64_t)B * (v2 > wv ? v2 : wv) * V * (int64_t)sizeof(uint2);
+    const int64_t nt = (((int64_t)Wb + TW - 1) / TW) * (((int64_t)Hb + TH - 1) / TH);
+    return (int64_t)B * nt * V * (int64_t)sizeof(uint2);
 }
 
 int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
@@ -2009,25 +1594,14 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
                         ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) &&
                         (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) && (sN % 4 == 0) &&
                         (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32);
-    if (dma_ok && g_warp_kernel != 1)
-    {
+    if (dma_ok && g_warp_kernel != 1) {
         const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
         uint2 *boxes = (workspace && workspace_bytes >= need && ((uintptr_t)workspace & 7) == 0)
                            ? reinterpret_cast<uint2 *>(workspace) : nullptr;
-        if (g_warp_kernel == 3 && boxes && C == 64 && (int64_t)B * ((Hb + 15) / 16) * ((Wb + 15) / 16) < (1ll << 31)) {
-            const int occ_pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : 49 * 1024;
-            return mode == BEV_FUSE_MAX
-                       ? launch_fuse_p<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                          g_warp_pool_kb ? occ_pool : 72 * 1024, boxes)
-                       : launch_fuse_p<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                          occ_pool, boxes);
-        }
-        if (g_warp_kernel == 2)
-            return mode == BEV_FUSE_MAX
-                       ? launch_fuse_w_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                              st, boxes)
-                       : launch_fuse_w_occ<3>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                              st, boxes);
+        // default: the DPP-row kernel (sum / mean, footprint boxes in the workspace); 2: the per-view LDS-DMA kernel
+        if (g_warp_kernel == 0 && boxes && mode != BEV_FUSE_MAX && (int64_t)Hf * sH + (int64_t)Wf * sW < (1ll << 31))
+            return launch_fuse_v3(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
+                                  boxes);
         return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st, boxes);
     }
     if (C <= 4)

@@ -6,21 +6,23 @@
 //     gfeats[v][c][p] = sum over BEV cells q and taps t of q with tap(q, t) == p, valid:  w_t(q) * g_v[c][q]
 // with g_v = gout (sum) or gout / V (mean), or the view's own gout (per-view warp).  The taps and weights are
 // the forward's bit-exact recipe (bev_geometry.h).  Float addition order differs from torch's scatter (float
-// atomics): equal to the reference's backward within fp32 tolerance, not bit for bit.
+// atomics across tiles): equal to the reference's backward within fp32 tolerance, not bit for bit.
 //
 // k_warp_bwd_runs -- one workgroup per (frame, 16 x 16 BEV tile), ALL views of the frame in one workgroup, so the
 // fused gradient gout is read from HBM once (not once per view).  Lane mapping ("runs"): a 16-lane DPP row owns
-// one tile row = a run of 16 consecutive cells along the BEV x axis; lane l holds channels {l, l+16, l+32, l+48}
-// of a 64-channel chunk for all 16 cells of the run (64 VGPRs), and computes the taps of cell l.  The row walks
-// its 16 cells in order; cell k's tap key and weights come from lane k by DPP row broadcast (row_newbcast, folded
-// into the FMAs), and the four tap gradients w_t * g are accumulated in registers while consecutive cells share
+// one tile row = a run of 16 consecutive cells along the BEV x axis; lane l holds channels 4l .. 4l + 3 of a
+// 64-channel chunk for all 16 cells of the run (64 VGPRs), and computes the taps of cell l.  The row walks its 16
+// cells in order; cell k's tap key, weights and image addresses come from lane k by DPP row broadcast
+// (row_newbcast), and the four tap gradients w_t * g are accumulated in registers while consecutive cells share
 // the same 2x2 source quad -- on the Appendix-B rig 80 % of the cells have their left neighbour's quad (DESIGN.md
-// §4) -- and are added to the LDS image of the tile's footprint only when the quad changes: ~4x fewer LDS
-// atomics than one per (cell, tap, channel), and each ds_add_f32 instruction of a row covers 16 consecutive
-// channel dwords of one pixel.  The image ([pixel][64 channels + pad]) then goes to the gradient with one float
-// atomic per touched (pixel, channel), coalesced along channels for NHWC gradients (one 256-B wave instruction
-// per pixel) or along x for NCHW.  Footprints larger than the LDS pool (horizon tiles) add their quad sums
-// straight to global memory.
+// §4) -- and are added to the LDS image of the tile's footprint only when the quad changes.
+// No LDS float atomics: on gfx950 a ds_add_f32 wave instruction costs ~40x a ds_add_u32 / ~160x a ds_write_b32
+// (tools/lds_atomic_micro.hip, profiles/r04c_lds_atomic_micro.txt).  Instead every wave owns a copy of the image and
+// its four rows add their run sums by plain read-modify-write (ds_read_b128 + add + ds_write_b128), one row at a
+// time (the rows of a wave may hit the same pixel; a wave's LDS operations complete in order).  The four copies are
+// summed per (pixel, channel) and go to the gradient with one global float atomic per touched (pixel, channel),
+// coalesced along channels for NHWC gradients (one 256-B wave instruction per pixel) or along x for NCHW.
+// Footprints whose four copies do not fit the LDS pool (horizon tiles) add their run sums straight to global memory.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,10 +34,9 @@ using namespace bev;
 
 namespace {
 
-constexpr int RB_NT = 256;     // 4 waves = 16 DPP rows = 16 runs
-constexpr int RB_T = 16;       // tile = 16 rows x 16 cells
-constexpr int RB_PSW = 68;     // LDS image pixel stride in dwords (64 channels + 4: rows of neighbouring pixels
-                               // start 4 banks apart)
+constexpr int RB_NT = 256;   // 4 waves = 16 DPP rows = 16 runs
+constexpr int RB_T = 16;     // tile = 16 rows x 16 cells
+constexpr int RB_PIX = 256;  // image bytes per pixel (64 channels, unpadded: a row's b128 access is one pixel)
 
 static inline int rb_err(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
@@ -58,29 +59,29 @@ __device__ __forceinline__ int key_x0(int k) { return (k & 0x3fff) - 1; }
 __device__ __forceinline__ int key_y0(int k) { return ((k >> 14) & 0x3fff) - 1; }
 __device__ __forceinline__ unsigned key_valid(int k) { return ((unsigned)k >> 28) & 15u; }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 struct Box4 {
     int x0, y0, x1, y1;
 };
 
-// Where a run's four tap sums go.  IMG: the LDS image of the tile footprint, at the byte addresses the run's first
-// cell computed for its taps (an invalid tap points at a trash pixel that is never flushed).  !IMG (footprint larger
-// than the pool): the global gradient, by float atomics on the valid taps.
+// Where a run's four tap sums go: the wave's copy of the LDS image (byte addresses of the four taps from the run's
+// last cell, lane offset included; an invalid tap points at the copy's trash pixel, never flushed), or without an
+// image (footprint too large) the global gradient, by float atomics on the valid taps.
 struct GSink {
     float *gf;           // global gradient of this view at the chunk's first channel
     int64_t sC, sH, sW;  // its element strides
     int lane16, cmax;
 };
 
-template <bool IMG>
-__device__ __forceinline__ void run_flush(int key, const int (&a)[4], const float (&q)[4][4], unsigned char *smem,
-                                          const GSink &gs) {
-    if constexpr (IMG) {
+__device__ __forceinline__ void run_flush(bool img, int key, const int (&a)[4], const f32x4 (&q)[4],
+                                          unsigned char *smem, const GSink &gs) {
+    if (img) {  // uniform in the row
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                __hip_atomic_fetch_add(reinterpret_cast<float *>(smem + a[t]) + 16 * m, q[t][m], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int t = 0; t < 4; ++t) {
+            f32x4 *p = reinterpret_cast<f32x4 *>(smem + a[t]);
+            *p = *p + q[t];
+        }
     } else {
         const unsigned vb = key_valid(key);
         const int x0 = key_x0(key), y0 = key_y0(key);
@@ -89,19 +90,19 @@ __device__ __forceinline__ void run_flush(int key, const int (&a)[4], const floa
             if (!(vb & (1u << t))) continue;
             float *p = gs.gf + (int64_t)(y0 + (t >> 1)) * gs.sH + (int64_t)(x0 + (t & 1)) * gs.sW;
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
-                if (gs.lane16 + 16 * m < gs.cmax) unsafeAtomicAdd(p + (int64_t)(gs.lane16 + 16 * m) * gs.sC, q[t][m]);
+            for (int u = 0; u < 4; ++u)
+                if (4 * gs.lane16 + u < gs.cmax) unsafeAtomicAdd(p + (int64_t)(4 * gs.lane16 + u) * gs.sC, q[t][u]);
         }
     }
 }
 
-// Step K of a row's walk: accumulate cell K's four tap gradients (key / weights / tap addresses from lane K by DPP
-// row broadcast); when cell K ends its run (cell K + 1 has another quad, or K is the last cell), add the run's sums
-// to the image at cell K's tap addresses and restart them.  The branch is uniform inside the row; the restart is a
-// select, so the accumulators carry no control-flow merges.
-template <bool IMG, int K>
-__device__ __forceinline__ void walk_step(const float (&g)[16][4], float (&q)[4][4], int &key, int (&a)[4],
-                                          float (&w)[4], unsigned char *smem, const GSink &gs) {
+// Step K of a row's walk: accumulate cell K's four tap gradients (key / weights from lane K by DPP row broadcast);
+// when cell K ends its run (cell K + 1 has another quad, or K is the last cell), add the run's sums at cell K's tap
+// addresses -- the rows of the wave one after the other -- and restart them.  The restart is a select, so the
+// accumulators carry no control-flow merges.
+template <int K>
+__device__ __forceinline__ void walk_step(const float (&g)[16][4], f32x4 (&q)[4], int &key, int (&a)[4],
+                                          float (&w)[4], bool img, int rw, unsigned char *smem, const GSink &gs) {
     // the broadcast sources are "redefined" at every step, so the compiler cannot hoist all 16 steps' broadcasts
     // to the top of the walk (9 x 16 extra live VGPRs)
     asm volatile("" : "+v"(key), "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(a[0]), "+v"(a[1]), "+v"(a[2]),
@@ -113,40 +114,45 @@ __device__ __forceinline__ void walk_step(const float (&g)[16][4], float (&q)[4]
     for (int t = 0; t < 4; ++t) {
         const float wt = row_bcast_f<K>(w[t]);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) q[t][m] = __builtin_fmaf(wt, g[K][m], q[t][m]);
+        for (int u = 0; u < 4; ++u) q[t][u] = __builtin_fmaf(wt, g[K][u], q[t][u]);
     }
     const bool end = kn != kk;
-    if (end && kk != 0) {
+    const bool fl = end && kk != 0;
+    if (__ballot(fl) != 0ull) {  // wave-uniform
         int at[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) at[t] = row_bcast<K>(a[t]);
-        run_flush<IMG>(kk, at, q, smem, gs);
+#pragma unroll 1
+        for (int r = 0; r < 4; ++r) {  // one row at a time: plain read-modify-write of the wave's image copy
+            // compiler barrier: per thread the rows' accesses look independent, but row r + 1 must read what row r
+            // wrote (the hardware keeps a wave's LDS operations in order)
+            asm volatile("" ::: "memory");
+            if (rw == r && fl) run_flush(img, kk, at, q, smem, gs);
+        }
+        asm volatile("" ::: "memory");
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) q[t][m] = end ? 0.0f : q[t][m];
+    for (int t = 0; t < 4; ++t) q[t] = end ? (f32x4){0.0f, 0.0f, 0.0f, 0.0f} : q[t];
+    // the step's sums exist here (no deferral of many steps' FMAs: register pressure)
+    asm volatile("" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]));
 }
 
-template <bool IMG, int K>
-__device__ __forceinline__ void walk_from(const float (&g)[16][4], float (&q)[4][4], int &key, int (&a)[4],
-                                          float (&w)[4], unsigned char *smem, const GSink &gs) {
-    walk_step<IMG, K>(g, q, key, a, w, smem, gs);
-    if constexpr (K + 1 < 16) walk_from<IMG, K + 1>(g, q, key, a, w, smem, gs);
+template <int K>
+__device__ __forceinline__ void walk_from(const float (&g)[16][4], f32x4 (&q)[4], int &key, int (&a)[4],
+                                          float (&w)[4], bool img, int rw, unsigned char *smem, const GSink &gs) {
+    walk_step<K>(g, q, key, a, w, img, rw, smem, gs);
+    if constexpr (K + 1 < 16) walk_from<K + 1>(g, q, key, a, w, img, rw, smem, gs);
 }
 
 // One row's walk over its 16 cells for one view.
-template <bool IMG>
 __device__ __forceinline__ void walk_row(const float (&g)[16][4], int key, const int (&a0)[4], const float (&w0)[4],
-                                         unsigned char *smem, const GSink &gs) {
+                                         bool img, int rw, unsigned char *smem, const GSink &gs) {
     int a[4] = {a0[0], a0[1], a0[2], a0[3]};
     float w[4] = {w0[0], w0[1], w0[2], w0[3]};
-    float q[4][4];
+    f32x4 q[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) q[t][m] = 0.0f;
-    walk_from<IMG, 0>(g, q, key, a, w, smem, gs);
+    for (int t = 0; t < 4; ++t) q[t] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+    walk_from<0>(g, q, key, a, w, img, rw, smem, gs);
 }
 
 // Exact bbox of the valid taps of the workgroup's cells (wave shuffles + LDS exchange).
@@ -184,7 +190,7 @@ __device__ __forceinline__ Box4 block_box(const Taps &t, int *red, int wave, int
 }
 
 // grid (tiles, B); gout [B][Cg][Hb][Wb] (per_view: [B*V][C][Hb][Wb]), gfeats element strides (sN, sC, sH, sW)
-__global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict__ gout, const float *__restrict__ Hmat,
+__global__ __launch_bounds__(RB_NT, 2) void k_warp_bwd_runs(const float *__restrict__ gout, const float *__restrict__ Hmat,
                                                          const float *__restrict__ xs, const float *__restrict__ ys,
                                                          int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
                                                          int Wb, int mean, int per_view, float *__restrict__ gfeats,
@@ -204,7 +210,8 @@ __global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict
     const int64_t plane = (int64_t)Hb * Wb;
     const bool vec = row_in && (Wb % 4 == 0) && j0 + RB_T <= Wb;
     const double rV = recip_uniform(V);
-    const int maxpix = pool / (RB_PSW * 4) - 1;  // + the trash pixel
+    const int maxpix = pool / (4 * RB_PIX) - 1;  // four copies, each + its trash pixel
+    const int rw = lane >> 4;                     // the lane's row within its wave
 
     for (int c0 = 0; c0 < C; c0 += 64) {
         const int cmax = min(64, C - c0);
@@ -212,7 +219,7 @@ __global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict
         auto load_g = [&](const float *src) {  // src = gradient map of this frame (or view) [C][Hb][Wb]
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
-                const int c = c0 + l16 + 16 * m;
+                const int c = c0 + 4 * l16 + m;
                 const float *p = src + (int64_t)(c < C ? c : 0) * plane + (int64_t)(row_in ? i : 0) * Wb + j0;
                 if (vec && c < C) {
 #pragma unroll
@@ -249,30 +256,26 @@ __global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict
             }
             const int bw = bx.x1 - bx.x0 + 1, npix = bw * (bx.y1 - bx.y0 + 1);
             const bool use_img = npix <= maxpix;
+            const int cpy = (npix + 1) * RB_PIX;  // bytes of one image copy (+ its trash pixel)
             if (use_img) {
                 float4 *z = reinterpret_cast<float4 *>(img);
-                for (int k = tid; k < (npix + 1) * (RB_PSW / 4); k += RB_NT) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int k = tid; k < 4 * cpy / 16; k += RB_NT) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
             if (per_view) load_g(gout + (int64_t)n * C * plane);
             __syncthreads();  // image zeroed; red[] consumed
 
             const int key = quad_key(t);
             const GSink gs{gfeats + (int64_t)n * sN + (int64_t)c0 * sC, sC, sH, sW, l16, cmax};
-            if (use_img) {
-                // byte addresses of this cell's four taps in the image (lane's channel offset included); invalid
-                // taps -> the trash pixel after the image
-                const int trash = npix * RB_PSW * 4 + l16 * 4;
-                const int px = t.x0 - bx.x0, py = t.y0 - bx.y0;
-                int a[4];
+            // byte addresses of this cell's four taps in its wave's image copy (lane's channels included);
+            // invalid taps -> the copy's trash pixel
+            const int cb = wave * cpy + l16 * 16;
+            const int px = t.x0 - bx.x0, py = t.y0 - bx.y0;
+            int a[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    a[u] = (t.valid & (1u << u)) ? ((py + (u >> 1)) * bw + px + (u & 1)) * (RB_PSW * 4) + l16 * 4
-                                                 : trash;
-                walk_row<true>(g, key, a, t.w, smem, gs);
-            } else {
-                const int a[4] = {0, 0, 0, 0};
-                walk_row<false>(g, key, a, t.w, smem, gs);
-            }
+            for (int u = 0; u < 4; ++u)
+                a[u] = use_img && (t.valid & (1u << u)) ? cb + ((py + (u >> 1)) * bw + px + (u & 1)) * RB_PIX
+                                                        : cb + npix * RB_PIX;
+            walk_row(g, key, a, t.w, use_img, rw, smem, gs);
 
             if (use_img) {
                 __syncthreads();  // every row's quad sums are in the image
@@ -281,7 +284,13 @@ __global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict
                     for (int p0 = wave * 4; p0 < npix; p0 += 16) {  // 4 pixels per wave in flight
                         float val[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) val[u] = (p0 + u < npix) ? img[(p0 + u) * RB_PSW + lane] : 0.0f;
+                        for (int u = 0; u < 4; ++u) {
+                            val[u] = 0.0f;
+                            if (p0 + u < npix) {
+#pragma unroll
+                                for (int w = 0; w < 4; ++w) val[u] += img[(w * cpy) / 4 + (p0 + u) * 64 + lane];
+                            }
+                        }
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const int p = p0 + u, py = p / bw, px = p - py * bw;
@@ -295,7 +304,9 @@ __global__ __launch_bounds__(RB_NT) void k_warp_bwd_runs(const float *__restrict
                     for (int r = wave; r < cmax * bh; r += 4) {
                         const int c = r / bh, py = r - c * bh;
                         for (int px = lane; px < bw; px += 64) {
-                            const float val = img[(py * bw + px) * RB_PSW + c];
+                            float val = 0.0f;
+#pragma unroll
+                            for (int w = 0; w < 4; ++w) val += img[(w * cpy) / 4 + (py * bw + px) * 64 + c];
                             if (val != 0.0f)
                                 unsafeAtomicAdd(gfv + (int64_t)c * sC + (int64_t)(bx.y0 + py) * sH +
                                                     (int64_t)(bx.x0 + px) * sW,
