@@ -77,7 +77,7 @@ def parse():
     ap.add_argument("--stream-groups", type=int, default=None, help="ResNet inference: image groups on separate "
                     "streams (default: the model's)")
     ap.add_argument("--stream-offset", type=int, default=None, help="ResNet inference: stagger of the stream groups")
-    ap.add_argument("--cpu-iters", type=int, default=2, help="frames timed for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-iters", type=int, default=3, help="frames timed for the CPU baseline (median; 0 = skip)")
     ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
     ap.add_argument("--conv-arith", choices=("bf16x6", "f32"), default="bf16x6",
                     help="trunk conv arithmetic: bf16x6 = fp32 through exact 3-way bf16 splits (default), f32 = the "
@@ -246,10 +246,21 @@ def cpu_baseline(enc, args, K, Rt):
         times.append(t_enc + time.perf_counter() - t1)
     t = float(np.median(times))
     enc_note = (f"trunk timed on {v_enc} of the {V} cameras and scaled x{V // v_enc}, " if v_enc != V else "")
+    # the reference's warp + mean (geometry.py grid_sample loop + fusion.py mean) on ONE host thread
+    torch.set_num_threads(1)
+    t1 = time.perf_counter()
+    reference_composition_cpu(feats[:, :V].contiguous(), torch.from_numpy(K[:1]), torch.from_numpy(Rt[:1]), (H, W),
+                              args.bev[0], args.bev[1], BOUNDS)
+    warp_1t = time.perf_counter() - t1
+    torch.set_num_threads(threads)
     return {"value": round(1.0 / t, 4), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"{args.cpu_iters} frame(s) of the same workload ({V}x3x{H}x{W} -> {args.backbone} "
                       f"layer2 + proj C={args.channels} -> grid_sample warp -> mean), {enc_note}median {t:.2f} "
-                      "s/frame, torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
+                      "s/frame, torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)",
+            "per_frame_s": [round(x, 3) for x in times],
+            "warp_mean_1thread": {"value": round(1.0 / warp_1t, 4), "unit": "frames/s", "cores": 1,
+                                  "sample": f"1 frame: the {V}-view grid_sample warp + mean alone (geometry.py:120-162, "
+                                            f"fusion.py:21) on one host thread, {warp_1t:.2f} s"}}
 
 
 def cpu_k1(args, K, Rt):

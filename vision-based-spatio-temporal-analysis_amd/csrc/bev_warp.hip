@@ -1070,7 +1070,7 @@ constexpr int W3_PIX = 256;  // staged bytes per pixel (one unpadded 64-channel 
 
 template <int K>
 __device__ __forceinline__ int rbc(int v) {  // lane K of this lane's 16-lane DPP row
-    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, true);  // bound_ctrl: no "old" operand to set up
 }
 template <int K>
 __device__ __forceinline__ float rbcf(float v) {
@@ -1092,15 +1092,18 @@ __device__ __forceinline__ void w3_step(float (&acc)[16][4], f32x4 (&qv)[4], int
                  "+v"(c.w[1]), "+v"(c.w[2]), "+v"(c.w[3]));
     const int kk = rbc<K>(c.key);
     if (__ballot(kk != cur) != 0ull) {  // wave-uniform: some row enters a new quad -> every row reads its quad
+        int at[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int at = rbc<K>(c.a[t]);
-            if (direct) {  // (uniform) buffer loads: an invalid tap's out-of-range offset reads 0
-                const int vo = at >= 0 ? at * 4 + 16 * l16 : 0x7ffffff0;
+        for (int t = 0; t < 4; ++t) at[t] = rbc<K>(c.a[t]);
+        if (direct) {  // (uniform) buffer loads: an invalid tap's out-of-range offset reads 0
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int vo = at[t] >= 0 ? at[t] * 4 + 16 * l16 : 0x7ffffff0;
                 qv[t] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0));
-            } else {
-                qv[t] = *reinterpret_cast<const f32x4 *>(smem + at + 16 * l16);
             }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) qv[t] = *reinterpret_cast<const f32x4 *>(smem + at[t] + 16 * l16);
         }
     }
     cur = kk;

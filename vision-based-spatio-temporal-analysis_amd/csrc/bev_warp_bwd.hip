@@ -43,7 +43,7 @@ static inline int rb_err(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 // lane k of this lane's 16-lane DPP row, to every lane of the row
 template <int K>
 __device__ __forceinline__ int row_bcast(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, false);
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xf, 0xf, true);  // bound_ctrl: no "old" operand to set up
 }
 template <int K>
 __device__ __forceinline__ float row_bcast_f(float v) {

@@ -49,6 +49,11 @@ class _ViewProjection(torch.autograd.Function):
             fl = fl.contiguous()
         g = torch.empty(B, V, Hf, Wf, P, device=feats.device, dtype=torch.float32)
         zero = torch.zeros(P, device=feats.device)
+        if _nat.half_convs():
+            # under autocast(float16) the projection runs in the fp16 arithmetic its backward uses (dgrad / wgrad
+            # under the same half mode): pack the per-view slices here, in that precision
+            wv = weight.detach().float().view(P, V, C)
+            panels = [_nat.pack_conv_weight(wv[:, v].contiguous().view(P, C, 1, 1)) for v in range(V)]
         for v in range(V):
             for b in range(B):
                 _nat.conv2d_nhwc_ex(fl[b, v][None], panels[v], zero, P, 1, 0, out=g[b, v][None])
