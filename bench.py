@@ -84,9 +84,9 @@ def parse():
                          "exact-f32 MFMA kernels")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V",
                     help="set a performance knob (include/bev_mi355x.h BEV_TUNE_<NAME>) before the run; repeatable")
-    ap.add_argument("--warp-kernel", choices=("rows", "register", "dma"), default="rows",
-                    help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results): rows = "
-                         "k_warp_fuse_v3 (default), register = k_warp_fuse, dma = k_warp_fuse_v2")
+    ap.add_argument("--warp-kernel", choices=("dma", "register", "rows"), default="dma",
+                    help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results): dma = "
+                         "k_warp_fuse_v2 (default), register = k_warp_fuse, rows = k_warp_fuse_v3")
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration check on the CPU (gloo): the rank spawning, barriers, timing and MAX "
                          "reduction of this script with a placeholder step (rank r sleeps (r + 1) x 5 ms); no hot "
@@ -299,7 +299,7 @@ def pmc_traffic(args) -> dict:
     file's numbers (named in `traffic_source`), not counters read by this run."""
     default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone,
                args.camera_shard, args.warp_kernel) == \
-        (7, 64, (1080, 1920), (480, 1440), 2, "resnet50", False, "rows")
+        (7, 64, (1080, 1920), (480, 1440), 2, "resnet50", False, "dma")
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
     if not default or not files:
         return {}
@@ -431,7 +431,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(rank)
     images = torch.randn(B, VL, 3, H, W, device=dev, generator=gen)
 
-    nat.tune(nat.TUNE_WARP_KERNEL, {"rows": 0, "register": 1, "dma": 2}[args.warp_kernel])
+    nat.tune(nat.TUNE_WARP_KERNEL, {"dma": 0, "register": 1, "rows": 3}[args.warp_kernel])
     for kv in args.tune:
         name, v = kv.split("=")
         nat.tune(getattr(nat, "TUNE_" + name.upper()), int(v))

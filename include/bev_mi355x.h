@@ -44,9 +44,9 @@ int bev_abi_version(void);
  *   else 1..150 (small pools force one-view batches / direct views in the default kernel and block
  *   decomposition in the per-view LDS-DMA kernel, which uses at least 8).
  * BEV_TUNE_WARP_KERNEL: fused warp kernel for NHWC C % 64 == 0 features:
- *   0 = default (DPP-row kernel with batched footprint staging for SUM / MEAN with a workspace, else the
- *   per-view LDS-DMA kernel), 1 = register-staged, 2 = per-view LDS-DMA kernel.
- * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats (<= 12288), 0 = 12288.
+ *   0 = default (= 2), 1 = register-staged, 2 = per-view LDS-DMA kernel, 3 = DPP-row kernel with batched
+ *   footprint staging (SUM / MEAN with a workspace; else 2).
+ * BEV_TUNE_WARP_BWD_POOL: LDS image of the warp backward in floats (<= 19968), 0 = 19968.
  * BEV_TUNE_CONV_XCD: 1 (default) = XCD-aware conv block order, 0 = plain.
  * BEV_TUNE_CONV_NBUF: 0 = automatic, 1 / 2 = LDS staging depth of the 128x64 / 64x128 conv tiles.
  * BEV_TUNE_WGRAD_MFMA: conv weight gradient on the MFMA with natural-layout operands copied by LDS-DMA
@@ -345,6 +345,18 @@ int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16
                        const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
                        float *y, int ldy, int Ho, int Wo, void *stream);
 
+/* host: number of 128-row tiles of the BatchNorm statistics bev_conv2d_h16_bnstats_f32 writes for M output rows. */
+int64_t bev_conv_h16_stat_tiles(int64_t M);
+
+/* device: bev_conv2d_h16_f32 (act 0, no residual, ldy == Co; Ci % 64 == 0) that also writes the BatchNorm batch
+ * statistics of its output, so the train-mode BN after the conv does not read it back: tile_stats
+ * [bev_conv_h16_stat_tiles(M)][Co][2] = per 128-row tile and channel (sum, sum of squared deviations from the tile
+ * mean), fp32; combine with bev_batchnorm_finalize_tiles_f32.  Replaces the conv -> BatchNorm2d(train) pair of the
+ * timm trunk under autocast (cnn_encoder.py:26, train.py:238-247). */
+int bev_conv2d_h16_bnstats_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                               int Co, int KH, int KW, int stride, int pad, int dilation, float *y, int Ho, int Wo,
+                               float *tile_stats, void *stream);
+
 /* Weight gradient of a convolution under autocast(float16): dW[co][(ky*KW + kx)*Ci + ci] =
  * sum over output pixels of f16(dz) * f16(x) with fp32 accumulation (the fp16 matrix cores), dW [Co][KH*KW*Ci]
  * fp32 (zeroed by the call).  x [N,H,W,Ci], dz [N,Ho,Wo,Co] NHWC fp32, Ci % 4 == 0, Co % 4 == 0, 16-B aligned.
@@ -461,12 +473,21 @@ int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, flo
                                 const float *beta, float *running_mean, float *running_var, float *mean, float *rstd,
                                 float *scale, float *shift, void *workspace, void *stream);
 
-/* device: y = act(z * scale + shift (+ residual [M][C])), per channel; act 0 none, 1 ReLU, 2 SiLU. */
+/* device: bev_batchnorm_train_fwd_f32's outputs (mean, rstd, scale, shift, running-stat update) from per-tile
+ * partials (sum, M2 about the tile mean) [ntiles][C][2] of z [M][C] in tiles of rows_per_tile rows (the last
+ * one ragged), combined in double (Chan et al.'s pairwise update). */
+int bev_batchnorm_finalize_tiles_f32(const float *tile_stats, int ntiles, int rows_per_tile, int64_t M, int C,
+                                     float eps, float momentum, const float *gamma, const float *beta,
+                                     float *running_mean, float *running_var, float *mean, float *rstd, float *scale,
+                                     float *shift, void *stream);
+
+/* device: y = act(fmaf(z, scale, shift) (+ residual [M][C])), per channel; act 0 none, 1 ReLU, 2 SiLU. */
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                             const float *residual, int act, float *y, void *stream);
 
 /* device: backward of y = act(batchnorm(z) (+ residual)): act 1 (ReLU) takes its mask from the forward output
- * y, act 2 (SiLU) recomputes u = z * scale + shift; frozen = 1 for running statistics (the mean / variance are
+ * y, act 3 (ReLU of a layer WITHOUT residual; dres must be NULL, y is not read) recomputes it exactly as
+ * fmaf(z, scale, shift) > 0, act 2 (SiLU) recomputes u = fmaf(z, scale, shift); frozen = 1 for running statistics (the mean / variance are
  * constants: dz = gamma * rstd * g).  dz [M][C], dres [M][C] (the gradient reaching the residual; may be NULL),
  * dgamma, dbeta [C], all OVERWRITTEN. */
 int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,

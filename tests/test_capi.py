@@ -86,7 +86,7 @@ def test_tune_knobs_host_only(lib):
     no GPU involved (knobs are read at launch)."""
     import bev_native as nat
     assert lib.bev_tune(99, 0) == -1
-    for knob, good, bad in ((nat.TUNE_CONV_TILE, 3, 5), (nat.TUNE_WARP_POOL_KB, 16, 151), (nat.TUNE_WARP_KERNEL, 1, 4),
+    for knob, good, bad in ((nat.TUNE_CONV_TILE, 3, 5), (nat.TUNE_WARP_POOL_KB, 16, 151), (nat.TUNE_WARP_KERNEL, 1, 5),
                             (nat.TUNE_WARP_BWD_POOL, 96, 1 << 20),
                             (nat.TUNE_CONV_XCD, 0, 2), (nat.TUNE_CONV_NBUF, 1, 3), (nat.TUNE_CONV_DMA, 2, 3),
                             (nat.TUNE_WGRAD_MFMA, 0, 3), (nat.TUNE_CONV_X6_TILE, 2, 3),

@@ -432,6 +432,71 @@ def test_batchnorm_train_kernels_vs_torch(case):
     chk(grv, rv, 1e-5, "running_var")
 
 
+BNSTAT_CASES = [(2, 64, 64, 31, 45, 3, 1), (1, 128, 256, 20, 33, 1, 1), (3, 64, 128, 17, 26, 3, 2),
+                (1, 256, 64, 9, 14, 1, 1), (2, 64, 320, 16, 8, 3, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", BNSTAT_CASES, ids=[f"n{c[0]}ci{c[1]}co{c[2]}_{c[3]}x{c[4]}_k{c[5]}s{c[6]}"
+                                                    for c in BNSTAT_CASES])
+def test_conv_h16_epilogue_batchnorm_stats(case):
+    """The autocast trunk conv with the train-mode BN statistics in its epilogue (bev_conv2d_h16_bnstats_f32 +
+    bev_batchnorm_finalize_tiles_f32, what ConvBNTrain runs under autocast): z bit-identical to the plain fp16
+    conv (same kernel, same K order), and mean / rstd / scale / shift / running stats equal to the separate pass
+    over z (bev_batchnorm_train_fwd_f32) and to float64 statistics of z -- ragged row tiles (M % 128), Co of 64..320
+    (partial 128-column tiles), 1x1 and 3x3, stride 1 / 2."""
+    import bev_native as nat
+    N, Ci, Co, H, W, k, st = case
+    g = torch.Generator().manual_seed(Ci + Co + H)
+    x = (torch.randn(N, H, W, Ci, generator=g) + 0.3).to(DEV)
+    w = (torch.randn(Co, Ci, k, k, generator=g) / (Ci * k * k) ** 0.5).to(DEV)
+    gamma, beta = (torch.rand(Co, generator=g) + 0.5).to(DEV), (torch.randn(Co, generator=g) * 0.3).to(DEV)
+    rm0, rv0 = torch.rand(Co, generator=g).to(DEV), (torch.rand(Co, generator=g) + 0.5).to(DEV)
+    p = k // 2
+    with nat._half_mode(True):  # what a native Function sets under autocast(float16)
+        packed = nat.pack_conv_weight(w)
+    assert packed.dtype == torch.float16
+    z0 = nat.conv2d_nhwc_h16(x, packed, torch.zeros(Co, device=DEV), Co, k, k, st, p)
+    z, tiles = nat.conv2d_nhwc_h16_bnstats(x, packed, Co, k, k, st, p)
+    assert torch.equal(z, z0)
+    M = z.numel() // Co
+    assert tiles.shape == ((M + 127) // 128, Co, 2)
+    rm1, rv1, rm2, rv2 = rm0.clone(), rv0.clone(), rm0.clone(), rv0.clone()
+    a = nat.batchnorm_finalize_tiles(tiles, M, gamma, beta, rm1, rv1, 1e-5, 0.1)
+    b = nat.batchnorm_train_fwd(z, gamma, beta, rm2, rv2, 1e-5, 0.1)
+    zd = z.double().reshape(M, Co)
+    mu, var = zd.mean(0), zd.var(0, unbiased=False)
+    for name, u, v in zip(("mean", "rstd", "scale", "shift"), a, b):
+        np.testing.assert_allclose(u.cpu().numpy(), v.cpu().numpy(), rtol=2e-6, atol=2e-6 * float(v.abs().max()),
+                                   err_msg=name)
+    np.testing.assert_allclose(a[0].double().cpu().numpy(), mu.cpu().numpy(), rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(a[1].double().cpu().numpy(), (1 / torch.sqrt(var + 1e-5)).cpu().numpy(), rtol=1e-6)
+    np.testing.assert_allclose(rm1.cpu().numpy(), rm2.cpu().numpy(), rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(rv1.cpu().numpy(), rv2.cpu().numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_batchnorm_bwd_relu_mask_from_z():
+    """bev_batchnorm_bwd_f32 act 3 (ReLU without residual, mask recomputed from z as fmaf(z, scale, shift) > 0)
+    == act 1 (mask from the saved output y of bev_batchnorm_apply_f32) bit for bit -- including elements whose
+    pre-activation rounds to exactly 0 or a tiny value of either sign; act 3 with a residual is rejected."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(5)
+    N, H, W, C = 2, 19, 23, 64
+    z = torch.randn(N, H, W, C, generator=g).to(DEV)
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.3).to(DEV)
+    mean, rstd, scale, shift = nat.batchnorm_train_fwd(z, gamma, beta, None, None, 1e-5, 0.1)
+    z.view(-1, C)[::7] = -shift / scale  # pre-activations at / around the ReLU kink
+    dy = torch.randn(N, H, W, C, generator=g).to(DEV)
+    y = nat.batchnorm_apply(z, scale, shift, None, 1)
+    a = nat.batchnorm_bwd(dy, y, z, mean, rstd, gamma, False, 1, scale, shift)
+    b = nat.batchnorm_bwd(dy, None, z, mean, rstd, gamma, False, nat.ACT_RELU_FROM_Z, scale, shift)
+    for u, v in zip((a[0], a[2], a[3]), (b[0], b[2], b[3])):
+        assert torch.equal(u, v)
+    with pytest.raises(nat.HipError):
+        nat.batchnorm_bwd(dy, None, z, mean, rstd, gamma, True, nat.ACT_RELU_FROM_Z, scale, shift)
+
+
 DW_CASES = [(2, 96, 17, 23, 3, 1), (1, 144, 20, 31, 3, 2), (2, 40, 13, 11, 5, 1), (1, 240, 18, 22, 5, 2),
             (1, 1152, 5, 7, 3, 1)]
 

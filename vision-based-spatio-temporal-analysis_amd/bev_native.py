@@ -100,6 +100,10 @@ SIGNATURES = {
     "bev_conv_pack_weights_h16": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
     "bev_conv_wgrad_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_conv_h16_stat_tiles": (_i64, [_i64]),
+    "bev_conv2d_h16_bnstats_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
+    "bev_batchnorm_finalize_tiles_f32": (_i, [_vp, _i, _i, _i64, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                               _vp]),
     "bev_conv_packed_size_x6": (_i64, [_i, _i, _i, _i]),
     "bev_conv_pack_weights_x6": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _i,
@@ -602,6 +606,47 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
 
 
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2  # `relu` argument of conv2d_nhwc / dwconv2d_nhwc
+ACT_RELU_FROM_Z = 3  # batchnorm_bwd only: ReLU of a layer without residual, mask recomputed from z (y not read)
+H16_STAT_ROWS = 128  # rows per BatchNorm statistics tile of conv2d_nhwc_h16_bnstats
+
+
+def conv2d_nhwc_h16_bnstats(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: int, stride: int, pad: int):
+    """The fp16-operand conv of a train-mode BatchNorm layer (no bias, no activation; Ci % 64 == 0) with the BN batch
+    statistics taken in its epilogue: -> (z [N,Ho,Wo,Co] fp32, tile partials [tiles, Co, 2] = per 128-row tile
+    (sum, sum of squared deviations from the tile mean)) for batchnorm_finalize_tiles."""
+    x = x.contiguous()
+    _require_gpu(x)
+    if not packed.is_cuda or packed.dtype != torch.float16:
+        raise HipError("conv2d_nhwc_h16_bnstats needs the fp16 weight panel on the device")
+    N, H, W, Ci = x.shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    z = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    nt = lib().bev_conv_h16_stat_tiles(N * Ho * Wo)
+    _check(0 if nt > 0 else nt, "bev_conv_h16_stat_tiles")
+    tiles = torch.empty(nt, Co, 2, device=x.device, dtype=torch.float32)
+    with _span("conv", x):
+        rc = lib().bev_conv2d_h16_bnstats_f32(_ptr(x), N, H, W, Ci, _ptr(packed), None, Co, KH, KW, stride, pad, 1,
+                                              _ptr(z), Ho, Wo, _ptr(tiles), _stream(x))
+    _check(rc, "bev_conv2d_h16_bnstats_f32")
+    return z, tiles
+
+
+def batchnorm_finalize_tiles(tiles: torch.Tensor, M: int, gamma, beta, running_mean, running_var, eps: float,
+                             momentum: float):
+    """batchnorm_train_fwd's outputs (mean, rstd, scale, shift; running stats updated in place if given) from the
+    per-tile partials of conv2d_nhwc_h16_bnstats over M rows."""
+    _require_gpu(tiles, gamma, beta, running_mean, running_var)
+    nt, C, _ = tiles.shape
+    dev = tiles.device
+    mean, rstd, scale, shift = (torch.empty(C, device=dev) for _ in range(4))
+    with _span("batchnorm", tiles):
+        rc = lib().bev_batchnorm_finalize_tiles_f32(_ptr(tiles), nt, H16_STAT_ROWS, M, C, float(eps), float(momentum),
+                                                    _ptr(gamma.detach().contiguous()),
+                                                    _ptr(beta.detach().contiguous()), _ptr(running_mean),
+                                                    _ptr(running_var), _ptr(mean), _ptr(rstd), _ptr(scale),
+                                                    _ptr(shift), _stream(tiles))
+    _check(rc, "bev_batchnorm_finalize_tiles_f32")
+    return mean, rstd, scale, shift
 
 
 def conv2d_nhwc_h16(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
@@ -1029,7 +1074,8 @@ def batchnorm_apply(z: torch.Tensor, scale, shift, residual=None, act: int = 0) 
 def batchnorm_bwd(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_dres: bool, act: int = 1,
                   scale=None, shift=None, frozen: bool = False):
     """-> (dz, dres or None, dgamma, dbeta) of y = act(batchnorm(z) (+ res)).  act 1 needs the forward output y,
-    act 2 (SiLU) the forward's scale / shift; frozen: running statistics (no batch-statistic terms)."""
+    act 2 (SiLU) and 3 (ReLU without residual, mask from z) the forward's scale / shift; frozen: running statistics
+    (no batch-statistic terms)."""
     dy = dy.contiguous()
     _require_gpu(dy, y, z, mean, rstd, gamma, scale, shift)
     C = z.shape[-1]

@@ -46,7 +46,8 @@ __device__ __forceinline__ float silu_grad(float u) {
     return sg * (1.0f + u * (1.0f - sg));
 }
 
-// g = dy * act'(u) for the 4 channels c .. c+3 of element i (act 1: y > 0; act 2: u = z * scale + shift)
+// g = dy * act'(u) for the 4 channels c .. c+3 of element i (act 1: y > 0 from the saved output; act 3: ReLU of a
+// layer without residual, y > 0 recomputed from z so y is not read; act 2: u = z * scale + shift)
 __device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const float *y, const float4 v,
                                          const float *scale, const float *shift, int act, int64_t i, int c) {
     g[0] = d.x;
@@ -58,10 +59,14 @@ __device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const fl
         const float ov[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
+    } else if (act == 3) {  // ReLU without residual: y > 0 <=> z * scale + shift > 0, k_bn_apply's exact fmaf
+        const float zv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = fmaf(zv[u], scale[c + u], shift[c + u]) > 0.f ? g[u] : 0.f;
     } else if (act == 2) {
         const float zv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) g[u] *= silu_grad(zv[u] * scale[c + u] + shift[c + u]);
+        for (int u = 0; u < 4; ++u) g[u] *= silu_grad(fmaf(zv[u], scale[c + u], shift[c + u]));
     }
 }
 
@@ -175,6 +180,63 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize(const double *__r
     }
 }
 
+// BatchNorm statistics from the conv epilogue's per-tile partials (k_conv_h16b with stats): tile k holds
+// n_k = min(rows, M - k rows) rows of every channel as (sum, M2 about the tile mean) in fp32.  Chan et al.'s
+// pairwise update in double: n = nA + nB, d = meanB - meanA, mean = meanA + d nB / n, M2 = M2A + M2B + d^2 nA nB / n;
+// 16 tile phases per channel, then the phases in order.  Same outputs and running-stat rule as k_bn_finalize.
+struct Chan {
+    double n, mean, m2;
+    __device__ void add(double nb, double meanb, double m2b) {
+        if (nb <= 0.0) return;
+        const double nn = n + nb, d = meanb - mean;
+        mean += d * (nb / nn);
+        m2 += m2b + d * d * (n * nb / nn);
+        n = nn;
+    }
+};
+
+__global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize_tiles(const float *__restrict__ part, int ntiles, int rows,
+                                                                      int64_t M, int C, float eps, float momentum,
+                                                                      const float *__restrict__ gamma,
+                                                                      const float *__restrict__ beta,
+                                                                      float *__restrict__ running_mean,
+                                                                      float *__restrict__ running_var,
+                                                                      float *__restrict__ mean, float *__restrict__ rstd,
+                                                                      float *__restrict__ scale, float *__restrict__ shift) {
+    __shared__ double red[FIN_P][FIN_C][3];
+    const int cl = threadIdx.x % FIN_C, ph = threadIdx.x / FIN_C, c = blockIdx.x * FIN_C + cl;
+    Chan acc{0.0, 0.0, 0.0};
+    if (c < C) {
+        for (int k = ph; k < ntiles; k += FIN_P) {
+            const int64_t left = M - (int64_t)k * rows;
+            const double nk = (double)(left < rows ? left : rows);
+            const float *o = part + ((size_t)k * C + c) * 2;
+            acc.add(nk, (double)o[0] / nk, (double)o[1]);
+        }
+    }
+    red[ph][cl][0] = acc.n;
+    red[ph][cl][1] = acc.mean;
+    red[ph][cl][2] = acc.m2;
+    __syncthreads();
+    if (ph != 0 || c >= C) return;
+    Chan t{0.0, 0.0, 0.0};
+    for (int p = 0; p < FIN_P; ++p) t.add(red[p][cl][0], red[p][cl][1], red[p][cl][2]);
+    const double mu = t.mean;
+    double var = t.m2 / (double)M;
+    var = var > 0.0 ? var : 0.0;
+    const float r = (float)(1.0 / __builtin_sqrt(var + (double)eps));
+    const float sc = gamma[c] * r;
+    mean[c] = (float)mu;
+    rstd[c] = r;
+    scale[c] = sc;
+    shift[c] = beta[c] - (float)mu * sc;
+    if (running_mean) {
+        const float unb = (float)(M > 1 ? t.m2 / (double)(M - 1) : var);
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mu;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+}
+
 // IT: uint32_t when the element count fits (no 64-bit divisions in the channel decode), else int64_t
 template <typename IT>
 __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__restrict__ scale,
@@ -186,7 +248,7 @@ __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__re
         const int c = 4 * (int)(i % C4);
         const float4 v = *(const float4 *)(z + e);
         const float4 s = *(const float4 *)(scale + c), h = *(const float4 *)(shift + c);
-        float4 o = make_float4(v.x * s.x + h.x, v.y * s.y + h.y, v.z * s.z + h.z, v.w * s.w + h.w);
+        float4 o = make_float4(fmaf(v.x, s.x, h.x), fmaf(v.y, s.y, h.y), fmaf(v.z, s.z, h.z), fmaf(v.w, s.w, h.w));
         if (res) {
             const float4 r = *(const float4 *)(res + e);
             o = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
@@ -320,6 +382,19 @@ int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, flo
     return (int)hipGetLastError();
 }
 
+int bev_batchnorm_finalize_tiles_f32(const float *tile_stats, int ntiles, int rows_per_tile, int64_t M, int C,
+                                     float eps, float momentum, const float *gamma, const float *beta,
+                                     float *running_mean, float *running_var, float *mean, float *rstd, float *scale,
+                                     float *shift, void *stream) {
+    if (!tile_stats || !gamma || !beta || !mean || !rstd || !scale || !shift || M <= 0 || C <= 0 ||
+        rows_per_tile <= 0 || ntiles != (M + rows_per_tile - 1) / rows_per_tile || (!running_mean) != (!running_var))
+        return BEV_ERR_ARGS;
+    hipLaunchKernelGGL(k_bn_finalize_tiles, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, (hipStream_t)stream,
+                       tile_stats, ntiles, rows_per_tile, M, C, eps, momentum, gamma, beta, running_mean, running_var,
+                       mean, rstd, scale, shift);
+    return (int)hipGetLastError();
+}
+
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                             const float *residual, int act, float *y, void *stream) {
     if (!z || !scale || !shift || !y || !bn_shape_ok(M, C) || act < 0 || act > 2) return BEV_ERR_ARGS;
@@ -338,7 +413,8 @@ int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64
                           int frozen, float *dz, float *dres, float *dgamma, float *dbeta, void *workspace,
                           void *stream) {
     if (!dy || !z || !mean || !rstd || !gamma || !dz || !dgamma || !dbeta || !workspace || !bn_shape_ok(M, C) ||
-        act < 0 || act > 2 || (act == 1 && !y) || (act == 2 && (!scale || !shift)))
+        act < 0 || act > 3 || (act == 1 && !y) || ((act == 2 || act == 3) && (!scale || !shift)) ||
+        (act == 3 && dres))  // act 3: ReLU recomputed from z, only for a layer without residual
         return BEV_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;
     const int nb = row_blocks(M);

@@ -61,6 +61,7 @@ struct ConvH {
     const float *__restrict__ bias;
     const float *__restrict__ res;
     float *__restrict__ y;
+    float *__restrict__ stats;  // k_conv_h16b: per (row tile, channel) BatchNorm partials (sum, M2) of the output, or null
     int N, H, W, Ci, Co, KH, KW, stride, pad, dil, Ho, Wo, act, ldy, Kp;
     int64_t M;
 };
@@ -202,6 +203,72 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
 // identical to k_conv_h16.
 constexpr int HBK2 = 64, HROW2 = 72;  // halves per LDS row: 64 + 8 pad = 144 B = 9 odd 16-B slots
 
+// BatchNorm statistics of the conv output z = acc + bias (training forward, BN with batch statistics), fused into
+// the epilogue so z is not read back: per output column of the 128 x 128 tile, over the tile's valid rows,
+// (sum, M2 = sum (z - sum / n)^2) in fp32 -> stats[(row tile) * Co + col][2]; bev_batchnorm_finalize_tiles_f32
+// combines the tiles in double (Chan et al.'s pairwise update).  Two-pass around the tile mean, so the variance
+// has no E[z^2] - E[z]^2 cancellation.  Column col = n0 + wn 64 + j 32 + r32 is held by 32 rows of each lane,
+// the lane pair (h = 0, 1) and the two wm waves: lane sums, one xor-32 exchange, one LDS exchange.
+__device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&acc)[2][2], _Float16 *ldsh, int64_t m0,
+                                               int n0, int wm, int wn, int r32, int h) {
+    float *red = reinterpret_cast<float *>(ldsh);  // [2 wm][128 cols]
+    const int64_t nv64 = a.M - m0;
+    const int nv = nv64 < HBM ? (int)nv64 : HBM;
+    float mean[2], sum[2];
+    __syncthreads();  // the last K step's fragment reads of this buffer are done
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = wn * 64 + j * 32 + r32;
+        const float bv = (a.bias && n0 + c < a.Co) ? a.bias[n0 + c] : 0.0f;
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row < nv) s += acc[i][j][r] + bv;
+            }
+        s += __shfl_xor(s, 32);
+        if (h == 0) red[wm * 128 + c] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = wn * 64 + j * 32 + r32;
+        sum[j] = red[c] + red[128 + c];
+        mean[j] = sum[j] / (float)nv;
+    }
+    __syncthreads();  // sums consumed before the M2 exchange reuses red
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = wn * 64 + j * 32 + r32;
+        const float bv = (a.bias && n0 + c < a.Co) ? a.bias[n0 + c] : 0.0f;
+        float q = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float d = acc[i][j][r] + bv - mean[j];
+                if (row < nv) q = fmaf(d, d, q);
+            }
+        q += __shfl_xor(q, 32);
+        if (h == 0) red[wm * 128 + c] = q;
+    }
+    __syncthreads();
+    if (wm == 0 && h == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int c = wn * 64 + j * 32 + r32;
+            if (n0 + c < a.Co) {
+                float *o = a.stats + ((m0 / HBM) * a.Co + n0 + c) * 2;
+                o[0] = sum[j];
+                o[1] = red[c] + red[128 + c];
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
     __shared__ __attribute__((aligned(16))) _Float16 lds[2][(HBM + HBN) * HROW2];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -331,6 +398,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
 #undef H16_MFMA
 #undef H16_SWRITE
 #undef H16_GLOAD
+    if (a.stats) h16_tile_stats(a, acc, lds[0], m0, n0, wm, wn, r32, h);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -527,9 +595,9 @@ int bev_conv_pack_weights_h16(const float *w, int Co, int Ci, int KH, int KW, ui
     return (int)hipGetLastError();
 }
 
-int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
-                       const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
-                       float *y, int ldy, int Ho, int Wo, void *stream) {
+static int conv_h16(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                    const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act, float *y,
+                    int ldy, int Ho, int Wo, float *stats, void *stream) {
     if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
         stride <= 0 || pad < 0 || dilation <= 0 || act < 0 || act > 2 || ldy < Co)
         return BEV_ERR_ARGS;
@@ -539,6 +607,8 @@ int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16
         return BEV_ERR_ARGS;
     if ((((uintptr_t)x | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
     if (residual && ldy != Co) return BEV_ERR_ARGS;
+    const bool wide = Ci % HBK2 == 0 && g_h16_kernel == 0;
+    if (stats && (!wide || act != 0 || residual)) return BEV_ERR_ARGS;  // statistics of the raw conv output, k_conv_h16b
     if (N == 0) return 0;
     ConvH a;
     a.x = x;
@@ -546,17 +616,35 @@ int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16
     a.bias = bias;
     a.res = residual;
     a.y = y;
+    a.stats = stats;
     a.N = N, a.H = H, a.W = W, a.Ci = Ci, a.Co = Co, a.KH = KH, a.KW = KW, a.stride = stride, a.pad = pad;
     a.dil = dilation, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = ldy;
     a.Kp = (int)kpad_h(Ci * KH * KW);
     a.M = (int64_t)N * Ho * Wo;
     const int64_t blocks = ((a.M + HBM - 1) / HBM) * ((Co + HBN - 1) / HBN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    if (Ci % HBK2 == 0 && g_h16_kernel == 0)
+    if (wide)
         hipLaunchKernelGGL(k_conv_h16b, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(k_conv_h16, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
+}
+
+int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                       const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
+                       float *y, int ldy, int Ho, int Wo, void *stream) {
+    return conv_h16(x, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, dilation, act, y, ldy, Ho, Wo,
+                    nullptr, stream);
+}
+
+int64_t bev_conv_h16_stat_tiles(int64_t M) { return M > 0 ? (M + HBM - 1) / HBM : BEV_ERR_ARGS; }
+
+int bev_conv2d_h16_bnstats_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+                               int Co, int KH, int KW, int stride, int pad, int dilation, float *y, int Ho, int Wo,
+                               float *tile_stats, void *stream) {
+    if (!tile_stats) return BEV_ERR_ARGS;
+    return conv_h16(x, N, H, W, Ci, packed, bias, nullptr, Co, KH, KW, stride, pad, dilation, 0, y, Co, Ho, Wo,
+                    tile_stats, stream);
 }
 
 }  // extern "C"

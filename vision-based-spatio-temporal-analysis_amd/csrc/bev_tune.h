@@ -8,7 +8,7 @@ namespace bev {
 int warp_tune(int knob, int value);
 
 // LDS image of the warp backward (bev_warp_bwd.hip) in floats: BEV_TUNE_WARP_BWD_POOL, 0 = the maximum.
-constexpr int WARP_BWD_POOL_MAX = 12288;  // 48 KiB: three workgroups per CU
+constexpr int WARP_BWD_POOL_MAX = 19968;  // 78 KiB: two workgroups per CU (k_warp_bwd_runs holds 256 VGPRs)
 int warp_bwd_pool_floats();
 
 // knob = BEV_TUNE_WGRAD_MFMA (bev_train.hip).

@@ -1108,14 +1108,21 @@ __device__ __forceinline__ void w3_step(float (&acc)[16][4], f32x4 (&qv)[4], int
     }
     cur = kk;
     const float w0 = rbcf<K>(c.w[0]), w1 = rbcf<K>(c.w[1]), w2 = rbcf<K>(c.w[2]), w3 = rbcf<K>(c.w[3]);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {  // grid_sampler_2d's chain (bilerp), then the view sum
-        float s = qv[0][u] * w0;
-        s = __builtin_fmaf(qv[1][u], w1, s);
-        s = __builtin_fmaf(qv[2][u], w2, s);
-        s = __builtin_fmaf(qv[3][u], w3, s);
-        acc[K][u] = acc[K][u] + s;
-    }
+    // grid_sampler_2d's chain (bilerp) per channel, then the view sum -- as packed fp32 (v_pk_mul / v_pk_fma /
+    // v_pk_add: two channels per instruction, each half the scalar op exactly)
+    const f32x2 W0 = (f32x2){w0, w0}, W1 = (f32x2){w1, w1}, W2 = (f32x2){w2, w2}, W3 = (f32x2){w3, w3};
+    f32x2 a = qv[0].xy * W0, b = qv[0].zw * W0;
+    a = __builtin_elementwise_fma(qv[1].xy, W1, a);
+    b = __builtin_elementwise_fma(qv[1].zw, W1, b);
+    a = __builtin_elementwise_fma(qv[2].xy, W2, a);
+    b = __builtin_elementwise_fma(qv[2].zw, W2, b);
+    a = __builtin_elementwise_fma(qv[3].xy, W3, a);
+    b = __builtin_elementwise_fma(qv[3].zw, W3, b);
+    const f32x2 s0 = (f32x2){acc[K][0], acc[K][1]} + a, s1 = (f32x2){acc[K][2], acc[K][3]} + b;
+    acc[K][0] = s0.x;
+    acc[K][1] = s0.y;
+    acc[K][2] = s1.x;
+    acc[K][3] = s1.y;
     // and the step's sums are complete here: without this the compiler defers the FMAs of many steps (keeping
     // their broadcast weights and quads live -- spills)
     asm volatile("" : "+v"(acc[K][0]), "+v"(acc[K][1]), "+v"(acc[K][2]), "+v"(acc[K][3]));
@@ -1193,6 +1200,9 @@ __global__ __launch_bounds__(FT_NT, 3) void k_warp_fuse_v3(const float *__restri
     // boxes of this (frame, tile): lane v of every wave holds view v's (k_warp_boxes format)
     uint2 bxv = make_uint2(0u, 0u);
     if (lane < V) bxv = boxes[((int64_t)b * nt + tile) * V + lane];
+    // consume the load here: its wait would otherwise sit at the head of the staging loop and, every iteration,
+    // also wait for the LDS-DMA issued so far (the compiler cannot see those in the asm) -- serialising the views
+    asm volatile("" : "+v"(bxv.x), "+v"(bxv.y));
     auto box_of = [&](int v) {
         const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)bxv.x, v);
         const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)bxv.y, v);
@@ -1288,7 +1298,9 @@ __global__ __launch_bounds__(FT_NT, 3) void k_warp_fuse_v3(const float *__restri
                             const float a = acc[4 * m + e][uu];
                             o[e] = mean ? w3_div(a, vf, rf, rV, fastdiv != 0) : a;
                         }
-                        __builtin_nontemporal_store(o, reinterpret_cast<f32x4 *>(ob + uu * plane + 4 * m));
+                        // plain stores: a lane's 64-B run of one channel row is 4 of these, merged in L2 (16-B
+                        // non-temporal stores from 64 different rows per instruction went to HBM as partial writes)
+                        *reinterpret_cast<f32x4 *>(ob + uu * plane + 4 * m) = o;
                     }
             } else {
 #pragma unroll
@@ -1355,8 +1367,8 @@ inline int last() { return (int)hipGetLastError(); }
 
 // ---- performance knobs (bev_tune; results never depend on them) -------------
 int g_warp_pool_kb = 0;  // BEV_TUNE_WARP_POOL_KB: LDS image pool / ring per workgroup, 0 = automatic
-int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 default (k_warp_fuse_v3 where it applies), 1 register-staged
-                         // k_warp_fuse, 2 per-view LDS-DMA k_warp_fuse_v2
+int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 default (= 2), 1 register-staged k_warp_fuse, 2 per-view LDS-DMA
+                         // k_warp_fuse_v2, 3 DPP-row k_warp_fuse_v3 (sum / mean with a workspace)
 int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = WARP_BWD_POOL_MAX
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
@@ -1495,7 +1507,7 @@ int warp_tune(int knob, int value) {
             break;
         case BEV_TUNE_WARP_KERNEL:
             slot = &g_warp_kernel;
-            ok = value >= 0 && value <= 2;
+            ok = value >= 0 && value <= 3;
             break;
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
@@ -1601,8 +1613,9 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
         const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
         uint2 *boxes = (workspace && workspace_bytes >= need && ((uintptr_t)workspace & 7) == 0)
                            ? reinterpret_cast<uint2 *>(workspace) : nullptr;
-        // default: the DPP-row kernel (sum / mean, footprint boxes in the workspace); 2: the per-view LDS-DMA kernel
-        if (g_warp_kernel == 0 && boxes && mode != BEV_FUSE_MAX && (int64_t)Hf * sH + (int64_t)Wf * sW < (1ll << 31))
+        // default: the per-view LDS-DMA kernel; 3: the DPP-row kernel (sum / mean, footprint boxes in the workspace;
+        // measured slower at the bench geometry, profiles/r04g_warp_v3_vs_v2.txt)
+        if (g_warp_kernel == 3 && boxes && mode != BEV_FUSE_MAX && (int64_t)Hf * sH + (int64_t)Wf * sW < (1ll << 31))
             return launch_fuse_v3(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
                                   boxes);
         return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st, boxes);

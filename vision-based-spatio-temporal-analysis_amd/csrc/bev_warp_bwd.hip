@@ -60,6 +60,7 @@ __device__ __forceinline__ int key_y0(int k) { return ((k >> 14) & 0x3fff) - 1; 
 __device__ __forceinline__ unsigned key_valid(int k) { return ((unsigned)k >> 28) & 15u; }
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct Box4 {
     int x0, y0, x1, y1;
@@ -77,10 +78,19 @@ struct GSink {
 __device__ __forceinline__ void run_flush(bool img, int key, const int (&a)[4], const f32x4 (&q)[4],
                                           unsigned char *smem, const GSink &gs) {
     if (img) {  // uniform in the row
+        // the four taps are distinct pixels (or the trash pixel, never read back): all reads, ONE wait, all writes
+        // (a read-wait-write per tap costs four LDS round trips)
+        f32x4 *p[4];
+        f32x4 o[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            f32x4 *p = reinterpret_cast<f32x4 *>(smem + a[t]);
-            *p = *p + q[t];
+            p[t] = reinterpret_cast<f32x4 *>(smem + a[t] + 16 * gs.lane16);
+            o[t] = *p[t];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const f32x2 lo = o[t].xy + q[t].xy, hi = o[t].zw + q[t].zw;  // v_pk_add_f32
+            *p[t] = (f32x4){lo.x, lo.y, hi.x, hi.y};
         }
     } else {
         const unsigned vb = key_valid(key);
@@ -110,11 +120,13 @@ __device__ __forceinline__ void walk_step(const float (&g)[16][4], f32x4 (&q)[4]
     const int kk = row_bcast<K>(key);
     int kn = 0;
     if constexpr (K + 1 < 16) kn = row_bcast<K + 1>(key);
+    const f32x2 g01 = (f32x2){g[K][0], g[K][1]}, g23 = (f32x2){g[K][2], g[K][3]};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 4; ++t) {  // packed fp32: two channels per v_pk_fma_f32 (each half fmaf exactly)
         const float wt = row_bcast_f<K>(w[t]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) q[t][u] = __builtin_fmaf(wt, g[K][u], q[t][u]);
+        const f32x2 W = (f32x2){wt, wt};
+        const f32x2 lo = __builtin_elementwise_fma(W, g01, q[t].xy), hi = __builtin_elementwise_fma(W, g23, q[t].zw);
+        q[t] = (f32x4){lo.x, lo.y, hi.x, hi.y};
     }
     const bool end = kn != kk;
     const bool fl = end && kk != 0;
@@ -266,9 +278,10 @@ __global__ __launch_bounds__(RB_NT, 2) void k_warp_bwd_runs(const float *__restr
 
             const int key = quad_key(t);
             const GSink gs{gfeats + (int64_t)n * sN + (int64_t)c0 * sC, sC, sH, sW, l16, cmax};
-            // byte addresses of this cell's four taps in its wave's image copy (lane's channels included);
+            // byte addresses of this cell's four taps in its wave's image copy, WITHOUT the lane's channel
+            // offset (the addresses are row-broadcast from the owning lane; run_flush adds 16 * lane16);
             // invalid taps -> the copy's trash pixel
-            const int cb = wave * cpy + l16 * 16;
+            const int cb = wave * cpy;
             const int px = t.x0 - bx.x0, py = t.y0 - bx.y0;
             int a[4];
 #pragma unroll

@@ -16,9 +16,11 @@ BatchNorm follows the module's own mode, as torch does:
 * `bn.training` (model.train(), what the reference's train.py:222 runs): BATCH statistics --
   `ConvBNTrain`: z = conv(x, W) (MFMA), per-channel batch mean / variance of z
   (bev_batchnorm_train_fwd_f32, which also updates running_mean / running_var with the momentum
-  rule and counts num_batches_tracked), y = act(z * scale + shift (+ residual))
-  (bev_batchnorm_apply_f32); backward bev_batchnorm_bwd_f32 (dz, d residual, dgamma, dbeta) then
-  the conv dgrad / wgrad above.
+  rule and counts num_batches_tracked; under autocast the fp16 conv writes per-tile partials in its
+  epilogue instead, bev_conv2d_h16_bnstats_f32 + bev_batchnorm_finalize_tiles_f32, so z is not read
+  back), y = act(z * scale + shift (+ residual)) (bev_batchnorm_apply_f32); backward
+  bev_batchnorm_bwd_f32 (dz, d residual, dgamma, dbeta; a ReLU layer without residual takes its mask
+  from z, so y is neither saved nor read) then the conv dgrad / wgrad above.
 * `bn.eval()` inside a training model (the usual way to freeze BN when fine-tuning): running
   statistics folded into the conv -- `ConvBNAct`: W_f = W * s, b_f = beta - mean * s with
   s = gamma / sqrt(var + eps), so dW = dWf * s, dgamma = (sum dWf * W - mean * dbf) / sqrt(var + eps),
@@ -35,6 +37,9 @@ import bev_native as _nat
 
 __all__ = ["ConvBNAct", "ConvBNTrain", "DWConvBNTrain", "SqueezeExcite", "ConvAct", "MaxPool", "conv_bn_act",
            "conv_act"]
+
+
+EPILOGUE_BN_STATS = True  # autocast: train-mode BN statistics from the fp16 conv's epilogue (else a pass over z)
 
 
 def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
@@ -94,16 +99,21 @@ class ConvBNAct(torch.autograd.Function):
         return dx, dw, dgamma, dbf, None, None, None, None, (dz if has_res else None)
 
 
-def _bn_affine(bn: nn.BatchNorm2d, z: torch.Tensor, gamma, beta):
+def _bn_affine(bn: nn.BatchNorm2d, z: torch.Tensor, gamma, beta, tiles: torch.Tensor = None):
     """(mean, rstd, scale, shift, frozen) of BN over NHWC z: batch statistics (+ running-stat update) when the
-    module is training, its running statistics (constants) when it is in eval()."""
+    module is training -- from the conv epilogue's per-tile partials when given (`tiles`, z is not read), else by a
+    pass over z -- and its running statistics (constants) when it is in eval()."""
     if bn.training:
         track = bn.track_running_stats and bn.running_mean is not None
         if track:
             bn.num_batches_tracked.add_(1)
         momentum = bn.momentum if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
-        mean, rstd, scale, shift = _nat.batchnorm_train_fwd(z, gamma, beta, bn.running_mean if track else None,
-                                                            bn.running_var if track else None, bn.eps, momentum)
+        rm, rv = (bn.running_mean, bn.running_var) if track else (None, None)
+        if tiles is not None:
+            mean, rstd, scale, shift = _nat.batchnorm_finalize_tiles(tiles, z.numel() // z.shape[-1], gamma, beta, rm,
+                                                                     rv, bn.eps, momentum)
+        else:
+            mean, rstd, scale, shift = _nat.batchnorm_train_fwd(z, gamma, beta, rm, rv, bn.eps, momentum)
         return mean, rstd, scale, shift, False
     with torch.no_grad():
         mean = bn.running_mean.detach().float().contiguous()
@@ -123,11 +133,18 @@ class ConvBNTrain(torch.autograd.Function):
         k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
         w = weight.detach().float().contiguous()
         Co = conv.out_channels
-        z = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(w), torch.zeros(Co, device=x.device), Co, k, k, st, p, False,
-                             in_nchw=in_nchw)
-        mean, rstd, scale, shift, frozen = _bn_affine(bn, z, gamma, beta)
+        packed = _nat.pack_conv_weight(w)
+        tiles = None
+        if (EPILOGUE_BN_STATS and packed.dtype == torch.float16 and bn.training and not in_nchw and x.shape[-1] % 64 == 0
+                and conv.dilation[0] == 1):  # autocast: the fp16 conv takes the BN statistics in its epilogue
+            z, tiles = _nat.conv2d_nhwc_h16_bnstats(x, packed, Co, k, k, st, p)
+        else:
+            z = _nat.conv2d_nhwc(x, packed, torch.zeros(Co, device=x.device), Co, k, k, st, p, False, in_nchw=in_nchw)
+        mean, rstd, scale, shift, frozen = _bn_affine(bn, z, gamma, beta, tiles)
         y = _nat.batchnorm_apply(z, scale, shift, residual, act)
-        ctx.save_for_backward(x, z, y if act == 1 else None, w, mean, rstd, gamma, scale, shift)
+        # ReLU without residual: the backward recomputes the mask from z (y > 0 <=> fmaf(z, scale, shift) > 0)
+        ctx.save_for_backward(x, z, y if (act == 1 and residual is not None) else None, w, mean, rstd, gamma, scale,
+                              shift)
         ctx.meta = (k, st, p, in_nchw, residual is not None, int(act), frozen)
         return y
 
@@ -136,7 +153,8 @@ class ConvBNTrain(torch.autograd.Function):
     def backward(ctx, dy):
         x, z, y, w, mean, rstd, gamma, scale, shift = ctx.saved_tensors
         k, st, p, in_nchw, has_res, act, frozen = ctx.meta
-        dz, dres, dgamma, dbeta = _nat.batchnorm_bwd(dy.float(), y, z, mean, rstd, gamma, has_res, act, scale, shift,
+        bact = _nat.ACT_RELU_FROM_Z if (act == 1 and not has_res) else act
+        dz, dres, dgamma, dbeta = _nat.batchnorm_bwd(dy.float(), y, z, mean, rstd, gamma, has_res, bact, scale, shift,
                                                      frozen)
         xn = _nat.nchw_to_nhwc(x) if in_nchw else x
         H, W = xn.shape[1], xn.shape[2]

@@ -35,6 +35,9 @@ from .fusion.geometry import GeometryTransformer, _WarpFuseFn
 from .heads.detector import BEVDetector, _ceil_to
 
 
+AMP_FWD_HALF_PANELS = True  # autocast: the projection's forward packs fp16 panels (its backward's arithmetic)
+
+
 class _ViewProjection(torch.autograd.Function):
     """g[b, v] = W_v (1x1) f[b, v] for channels-last per-camera maps f [B,V,C,Hf,Wf]; returns the projected
     maps as a [B,V,P,Hf,Wf] view of a [B,V,Hf,Wf,P] buffer (the layout the fused warp reads)."""
@@ -49,7 +52,7 @@ class _ViewProjection(torch.autograd.Function):
             fl = fl.contiguous()
         g = torch.empty(B, V, Hf, Wf, P, device=feats.device, dtype=torch.float32)
         zero = torch.zeros(P, device=feats.device)
-        if _nat.half_convs():
+        if _nat.half_convs() and AMP_FWD_HALF_PANELS:
             # under autocast(float16) the projection runs in the fp16 arithmetic its backward uses (dgrad / wgrad
             # under the same half mode): pack the per-view slices here, in that precision
             wv = weight.detach().float().view(P, V, C)
