@@ -325,6 +325,12 @@ int bev_colsum_f32(const float *dz, int64_t M, int C, float *db, void *stream);
 int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride, int pad,
                                int Ho, int Wo, float *dx, void *stream);
 
+/* The same dx (bit-identical) in two passes for C % 4 == 0, k * k <= 255: each window's argmax tap is found once and
+ * kept as a byte in argmax [N][Ho][Wo][C] (uint8 workspace, 4-B aligned), then every input gathers the dy of the
+ * windows whose byte names it.  Replaces MaxPool2d's backward of timm's stem pool (cnn_encoder.py:26). */
+int bev_maxpool2d_bwd_ws_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride,
+                                  int pad, int Ho, int Wo, float *dx, uint8_t *argmax, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Mixed precision (train.py:238-247, configs/wildtrack.yaml:45 USE_AMP): the convolutions a training step
  * runs under torch.autocast(float16) -- fp16 operands (round to nearest even, as autocast's casts), fp32
@@ -350,7 +356,7 @@ int64_t bev_conv_h16_stat_tiles(int64_t M);
 
 /* device: bev_conv2d_h16_f32 (act 0, no residual, ldy == Co; Ci % 64 == 0) that also writes the BatchNorm batch
  * statistics of its output, so the train-mode BN after the conv does not read it back: tile_stats
- * [bev_conv_h16_stat_tiles(M)][Co][2] = per 128-row tile and channel (sum, sum of squared deviations from the tile
+ * [Co][bev_conv_h16_stat_tiles(M)][2] = per channel and 128-row tile (sum, sum of squared deviations from the tile
  * mean), fp32; combine with bev_batchnorm_finalize_tiles_f32.  Replaces the conv -> BatchNorm2d(train) pair of the
  * timm trunk under autocast (cnn_encoder.py:26, train.py:238-247). */
 int bev_conv2d_h16_bnstats_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
@@ -474,20 +480,21 @@ int bev_batchnorm_train_fwd_f32(const float *z, int64_t M, int C, float eps, flo
                                 float *scale, float *shift, void *workspace, void *stream);
 
 /* device: bev_batchnorm_train_fwd_f32's outputs (mean, rstd, scale, shift, running-stat update) from per-tile
- * partials (sum, M2 about the tile mean) [ntiles][C][2] of z [M][C] in tiles of rows_per_tile rows (the last
- * one ragged), combined in double (Chan et al.'s pairwise update). */
+ * partials (sum, M2 about the tile mean) [C][ntiles][2] of z [M][C] in tiles of rows_per_tile rows (the last
+ * one ragged), combined in double: mean = sum of sums / M, M2 = sum of (M2_k + n_k (mean_k - mean)^2). */
 int bev_batchnorm_finalize_tiles_f32(const float *tile_stats, int ntiles, int rows_per_tile, int64_t M, int C,
                                      float eps, float momentum, const float *gamma, const float *beta,
                                      float *running_mean, float *running_var, float *mean, float *rstd, float *scale,
                                      float *shift, void *stream);
 
-/* device: y = act(fmaf(z, scale, shift) (+ residual [M][C])), per channel; act 0 none, 1 ReLU, 2 SiLU. */
+/* device: y = act(z * scale + shift (+ residual [M][C])), per channel (product and sum each rounded to fp32);
+ * act 0 none, 1 ReLU, 2 SiLU. */
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                             const float *residual, int act, float *y, void *stream);
 
 /* device: backward of y = act(batchnorm(z) (+ residual)): act 1 (ReLU) takes its mask from the forward output
  * y, act 3 (ReLU of a layer WITHOUT residual; dres must be NULL, y is not read) recomputes it exactly as
- * fmaf(z, scale, shift) > 0, act 2 (SiLU) recomputes u = fmaf(z, scale, shift); frozen = 1 for running statistics (the mean / variance are
+ * z * scale + shift > 0 (apply's rounding), act 2 (SiLU) recomputes u = z * scale + shift; frozen = 1 for running statistics (the mean / variance are
  * constants: dz = gamma * rstd * g).  dz [M][C], dres [M][C] (the gradient reaching the residual; may be NULL),
  * dgamma, dbeta [C], all OVERWRITTEN. */
 int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,

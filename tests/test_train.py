@@ -366,6 +366,25 @@ def test_maxpool_bwd_vs_torch_ties(N, C, H, W):
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,C,H,W", [(2, 64, 37, 53), (1, 8, 16, 16), (3, 4, 9, 7)])
+def test_maxpool_bwd_two_pass_bit_identical(N, C, H, W):
+    """bev_maxpool2d_bwd_ws_nhwc_f32 (argmax bytes, then the gather: what maxpool_bwd_nhwc runs for C % 4 == 0)
+    == the single-pass bev_maxpool2d_bwd_nhwc_f32 bit for bit, with tied maxima and NaNs in the windows."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.randint(-2, 3, (N, H, W, C), generator=g).float()
+    x.view(-1)[::97] = float("nan")
+    dy = torch.randn(N, (H - 1) // 2 + 1, (W - 1) // 2 + 1, C, generator=g)
+    xd, dyd = x.to(DEV), dy.to(DEV)
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    one = torch.empty_like(xd)
+    assert nat.lib().bev_maxpool2d_bwd_nhwc_f32(nat._ptr(xd), nat._ptr(dyd), N, H, W, C, 3, 2, 1, Ho, Wo,
+                                                nat._ptr(one), nat._stream(xd)) == 0
+    two = nat.maxpool_bwd_nhwc(xd, dyd, 3, 2, 1)
+    assert torch.equal(one.view(torch.int32), two.view(torch.int32))
+
+
 BN_CASES = [(2, 64, 13, 17, 1, True, False), (1, 384, 9, 11, 1, False, False), (3, 24, 7, 5, 0, False, False),
             (2, 512, 40, 60, 1, True, False), (1, 4, 1, 3, 0, True, False), (2, 144, 11, 13, 2, False, False),
             (1, 96, 9, 7, 2, False, True), (2, 64, 6, 9, 1, True, True)]
@@ -460,7 +479,7 @@ def test_conv_h16_epilogue_batchnorm_stats(case):
     z, tiles = nat.conv2d_nhwc_h16_bnstats(x, packed, Co, k, k, st, p)
     assert torch.equal(z, z0)
     M = z.numel() // Co
-    assert tiles.shape == ((M + 127) // 128, Co, 2)
+    assert tiles.shape == (Co, (M + 127) // 128, 2)
     rm1, rv1, rm2, rv2 = rm0.clone(), rv0.clone(), rm0.clone(), rv0.clone()
     a = nat.batchnorm_finalize_tiles(tiles, M, gamma, beta, rm1, rv1, 1e-5, 0.1)
     b = nat.batchnorm_train_fwd(z, gamma, beta, rm2, rv2, 1e-5, 0.1)
@@ -477,7 +496,7 @@ def test_conv_h16_epilogue_batchnorm_stats(case):
 
 @pytest.mark.gpu
 def test_batchnorm_bwd_relu_mask_from_z():
-    """bev_batchnorm_bwd_f32 act 3 (ReLU without residual, mask recomputed from z as fmaf(z, scale, shift) > 0)
+    """bev_batchnorm_bwd_f32 act 3 (ReLU without residual, mask recomputed from z as z * scale + shift > 0)
     == act 1 (mask from the saved output y of bev_batchnorm_apply_f32) bit for bit -- including elements whose
     pre-activation rounds to exactly 0 or a tiny value of either sign; act 3 with a residual is rejected."""
     import bev_native as nat

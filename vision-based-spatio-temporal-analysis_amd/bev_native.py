@@ -62,6 +62,7 @@ SIGNATURES = {
     "bev_conv_wgrad_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_colsum_f32": (_i, [_vp, _i64, _i, _vp, _vp]),
     "bev_maxpool2d_bwd_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_maxpool2d_bwd_ws_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_conv2d_chain_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
                                   _i, _i, _vp]),
@@ -613,7 +614,7 @@ H16_STAT_ROWS = 128  # rows per BatchNorm statistics tile of conv2d_nhwc_h16_bns
 def conv2d_nhwc_h16_bnstats(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: int, stride: int, pad: int):
     """The fp16-operand conv of a train-mode BatchNorm layer (no bias, no activation; Ci % 64 == 0) with the BN batch
     statistics taken in its epilogue: -> (z [N,Ho,Wo,Co] fp32, tile partials [tiles, Co, 2] = per 128-row tile
-    (sum, sum of squared deviations from the tile mean)) for batchnorm_finalize_tiles."""
+    (sum, sum of squared deviations from the tile mean), channel-major [Co, tiles, 2]) for batchnorm_finalize_tiles."""
     x = x.contiguous()
     _require_gpu(x)
     if not packed.is_cuda or packed.dtype != torch.float16:
@@ -623,7 +624,7 @@ def conv2d_nhwc_h16_bnstats(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: 
     z = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
     nt = lib().bev_conv_h16_stat_tiles(N * Ho * Wo)
     _check(0 if nt > 0 else nt, "bev_conv_h16_stat_tiles")
-    tiles = torch.empty(nt, Co, 2, device=x.device, dtype=torch.float32)
+    tiles = torch.empty(Co, nt, 2, device=x.device, dtype=torch.float32)
     with _span("conv", x):
         rc = lib().bev_conv2d_h16_bnstats_f32(_ptr(x), N, H, W, Ci, _ptr(packed), None, Co, KH, KW, stride, pad, 1,
                                               _ptr(z), Ho, Wo, _ptr(tiles), _stream(x))
@@ -636,7 +637,7 @@ def batchnorm_finalize_tiles(tiles: torch.Tensor, M: int, gamma, beta, running_m
     """batchnorm_train_fwd's outputs (mean, rstd, scale, shift; running stats updated in place if given) from the
     per-tile partials of conv2d_nhwc_h16_bnstats over M rows."""
     _require_gpu(tiles, gamma, beta, running_mean, running_var)
-    nt, C, _ = tiles.shape
+    C, nt, _ = tiles.shape
     dev = tiles.device
     mean, rstd, scale, shift = (torch.empty(C, device=dev) for _ in range(4))
     with _span("batchnorm", tiles):
@@ -876,6 +877,11 @@ def maxpool_bwd_nhwc(x: torch.Tensor, dy: torch.Tensor, k: int, stride: int, pad
     N, H, W, C = x.shape
     Ho, Wo = dy.shape[1], dy.shape[2]
     dx = torch.empty_like(x)
+    if C % 4 == 0 and k * k <= 255:  # window argmax bytes once, then the gather (bit-identical, ~16x fewer loads)
+        arg = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.uint8)
+        _check(lib().bev_maxpool2d_bwd_ws_nhwc_f32(_ptr(x), _ptr(dy), N, H, W, C, k, stride, pad, Ho, Wo, _ptr(dx),
+                                                   _ptr(arg), _stream(x)), "bev_maxpool2d_bwd_ws_nhwc_f32")
+        return dx
     _check(lib().bev_maxpool2d_bwd_nhwc_f32(_ptr(x), _ptr(dy), N, H, W, C, k, stride, pad, Ho, Wo, _ptr(dx),
                                             _stream(x)), "bev_maxpool2d_bwd_nhwc_f32")
     return dx

@@ -7,9 +7,12 @@
 //                                  the momentum rule and the unbiased variance (torch's train-mode BN)
 //             k_bn_apply           y = act(z*scale + shift (+ residual)), act = none / ReLU / SiLU (float4)
 //   backward  k_bn_partial<Grads>  per channel (sum g, sum g*xhat), g = dy * act'(u) (ReLU: y > 0 from the
-//                                  saved output; SiLU: u = z*scale + shift recomputed), xhat = (z - mean) * rstd
+//                                  saved output, or -- no residual -- u = z*scale + shift > 0 recomputed from
+//                                  z (act 3); SiLU: u recomputed), xhat = (z - mean) * rstd
 //             k_bn_bwd_finalize    k1 = sum g / M, k2 = sum g xhat / M, dbeta, dgamma
 //             k_bn_bwd_apply       dz = gamma * rstd * (g - k1 - xhat * k2); d(residual) = g
+//   Under autocast the forward statistics come from the fp16 conv's epilogue instead (bev_conv2d_h16_bnstats_f32):
+//             k_bn_finalize_tiles  per-tile (sum, M2 about the tile mean) combined in double (two passes)
 //   A BN module in eval() inside a training model ("frozen": running statistics) uses the same apply and
 //   backward with k1 = k2 = 0 (its statistics are constants).
 //
@@ -40,6 +43,10 @@ struct Stats {  // (z, z^2)
     }
 };
 
+// u = z * scale + shift, two roundings (the library builds with -ffp-contract=off: no fma) -- the one expression
+// k_bn_apply writes and the backward's recomputed ReLU mask / SiLU argument use, so they agree bit for bit
+__device__ __forceinline__ float bn_u(float z, float s, float h) { return z * s + h; }
+
 // SiLU' (u) = s (1 + u (1 - s)), s = sigmoid(u) = 1 / (1 + exp(-u)) (torch's SiLU backward)
 __device__ __forceinline__ float silu_grad(float u) {
     const float sg = sigmoid_hw(u);
@@ -59,14 +66,14 @@ __device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const fl
         const float ov[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
-    } else if (act == 3) {  // ReLU without residual: y > 0 <=> z * scale + shift > 0, k_bn_apply's exact fmaf
+    } else if (act == 3) {  // ReLU without residual: y > 0 <=> u > 0, u exactly as k_bn_apply computed it
         const float zv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) g[u] = fmaf(zv[u], scale[c + u], shift[c + u]) > 0.f ? g[u] : 0.f;
+        for (int u = 0; u < 4; ++u) g[u] = bn_u(zv[u], scale[c + u], shift[c + u]) > 0.f ? g[u] : 0.f;
     } else if (act == 2) {
         const float zv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) g[u] *= silu_grad(fmaf(zv[u], scale[c + u], shift[c + u]));
+        for (int u = 0; u < 4; ++u) g[u] *= silu_grad(bn_u(zv[u], scale[c + u], shift[c + u]));
     }
 }
 
@@ -180,49 +187,47 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize(const double *__r
     }
 }
 
-// BatchNorm statistics from the conv epilogue's per-tile partials (k_conv_h16b with stats): tile k holds
-// n_k = min(rows, M - k rows) rows of every channel as (sum, M2 about the tile mean) in fp32.  Chan et al.'s
-// pairwise update in double: n = nA + nB, d = meanB - meanA, mean = meanA + d nB / n, M2 = M2A + M2B + d^2 nA nB / n;
-// 16 tile phases per channel, then the phases in order.  Same outputs and running-stat rule as k_bn_finalize.
-struct Chan {
-    double n, mean, m2;
-    __device__ void add(double nb, double meanb, double m2b) {
-        if (nb <= 0.0) return;
-        const double nn = n + nb, d = meanb - mean;
-        mean += d * (nb / nn);
-        m2 += m2b + d * d * (n * nb / nn);
-        n = nn;
-    }
-};
-
-__global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize_tiles(const float *__restrict__ part, int ntiles, int rows,
-                                                                      int64_t M, int C, float eps, float momentum,
-                                                                      const float *__restrict__ gamma,
-                                                                      const float *__restrict__ beta,
-                                                                      float *__restrict__ running_mean,
-                                                                      float *__restrict__ running_var,
-                                                                      float *__restrict__ mean, float *__restrict__ rstd,
-                                                                      float *__restrict__ scale, float *__restrict__ shift) {
-    __shared__ double red[FIN_P][FIN_C][3];
-    const int cl = threadIdx.x % FIN_C, ph = threadIdx.x / FIN_C, c = blockIdx.x * FIN_C + cl;
-    Chan acc{0.0, 0.0, 0.0};
-    if (c < C) {
-        for (int k = ph; k < ntiles; k += FIN_P) {
-            const int64_t left = M - (int64_t)k * rows;
-            const double nk = (double)(left < rows ? left : rows);
-            const float *o = part + ((size_t)k * C + c) * 2;
-            acc.add(nk, (double)o[0] / nk, (double)o[1]);
-        }
-    }
-    red[ph][cl][0] = acc.n;
-    red[ph][cl][1] = acc.mean;
-    red[ph][cl][2] = acc.m2;
+// BatchNorm statistics from the conv epilogue's per-tile partials (k_conv_h16b with stats): channel c's tiles
+// part[c][k] = (sum, M2 about the tile mean) over n_k = min(rows, M - k rows) rows, fp32.  One workgroup per
+// channel, two passes over its (contiguous) tiles in double: mean = sum_k sum_k / M, then
+// M2 = sum_k (M2_k + n_k (mean_k - mean)^2) -- the exact combination (Chan et al.), no per-tile division chain.
+// Same outputs and running-stat rule as k_bn_finalize.
+constexpr int FT_T = 256;
+__device__ __forceinline__ double ft_block_sum(double v, double *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();  // red[] free (previous use consumed)
+    if (lane == 0) red[w] = v;
     __syncthreads();
-    if (ph != 0 || c >= C) return;
-    Chan t{0.0, 0.0, 0.0};
-    for (int p = 0; p < FIN_P; ++p) t.add(red[p][cl][0], red[p][cl][1], red[p][cl][2]);
-    const double mu = t.mean;
-    double var = t.m2 / (double)M;
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(FT_T) void k_bn_finalize_tiles(const float *__restrict__ part, int ntiles, int rows,
+                                                              int64_t M, int C, float eps, float momentum,
+                                                              const float *__restrict__ gamma,
+                                                              const float *__restrict__ beta,
+                                                              float *__restrict__ running_mean,
+                                                              float *__restrict__ running_var,
+                                                              float *__restrict__ mean, float *__restrict__ rstd,
+                                                              float *__restrict__ scale, float *__restrict__ shift) {
+    __shared__ double red[4];
+    const int c = blockIdx.x;
+    const float2 *pc = reinterpret_cast<const float2 *>(part) + (size_t)c * ntiles;
+    double s = 0.0;
+    for (int k = threadIdx.x; k < ntiles; k += FT_T) s += (double)pc[k].x;
+    const double mu = ft_block_sum(s, red) / (double)M;
+    double q = 0.0;
+    for (int k = threadIdx.x; k < ntiles; k += FT_T) {
+        const int64_t left = M - (int64_t)k * rows;
+        const double nk = (double)(left < rows ? left : rows);
+        const float2 t = pc[k];
+        const double d = (double)t.x / nk - mu;
+        q += (double)t.y + nk * d * d;
+    }
+    const double m2 = ft_block_sum(q, red);
+    if (threadIdx.x != 0) return;
+    double var = m2 / (double)M;
     var = var > 0.0 ? var : 0.0;
     const float r = (float)(1.0 / __builtin_sqrt(var + (double)eps));
     const float sc = gamma[c] * r;
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_finalize_tiles(const float
     scale[c] = sc;
     shift[c] = beta[c] - (float)mu * sc;
     if (running_mean) {
-        const float unb = (float)(M > 1 ? t.m2 / (double)(M - 1) : var);
+        const float unb = (float)(M > 1 ? m2 / (double)(M - 1) : var);
         running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mu;
         running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
     }
@@ -248,7 +253,7 @@ __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__re
         const int c = 4 * (int)(i % C4);
         const float4 v = *(const float4 *)(z + e);
         const float4 s = *(const float4 *)(scale + c), h = *(const float4 *)(shift + c);
-        float4 o = make_float4(fmaf(v.x, s.x, h.x), fmaf(v.y, s.y, h.y), fmaf(v.z, s.z, h.z), fmaf(v.w, s.w, h.w));
+        float4 o = make_float4(bn_u(v.x, s.x, h.x), bn_u(v.y, s.y, h.y), bn_u(v.z, s.z, h.z), bn_u(v.w, s.w, h.w));
         if (res) {
             const float4 r = *(const float4 *)(res + e);
             o = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
@@ -389,7 +394,7 @@ int bev_batchnorm_finalize_tiles_f32(const float *tile_stats, int ntiles, int ro
     if (!tile_stats || !gamma || !beta || !mean || !rstd || !scale || !shift || M <= 0 || C <= 0 ||
         rows_per_tile <= 0 || ntiles != (M + rows_per_tile - 1) / rows_per_tile || (!running_mean) != (!running_var))
         return BEV_ERR_ARGS;
-    hipLaunchKernelGGL(k_bn_finalize_tiles, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_bn_finalize_tiles, dim3(C), dim3(FT_T), 0, (hipStream_t)stream,
                        tile_stats, ntiles, rows_per_tile, M, C, eps, momentum, gamma, beta, running_mean, running_var,
                        mean, rstd, scale, shift);
     return (int)hipGetLastError();

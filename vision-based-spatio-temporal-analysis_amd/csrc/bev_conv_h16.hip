@@ -184,12 +184,18 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
             const int col = n0 + wn * 64 + j * 32 + r32;
             if (col >= a.Co) continue;
             const float bv = a.bias ? a.bias[col] : 0.0f;
+            float rv[16];  // all residual loads first: interleaved with the stores they would serialise (y may alias)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                rv[r] = (a.res && row < a.M) ? a.res[row * a.Co + col] : 0.0f;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (row >= a.M) continue;
                 float v = acc[i][j][r] + bv;
-                if (a.res) v += a.res[row * a.Co + col];
+                if (a.res) v += rv[r];
                 a.y[row * a.ldy + col] = act_h(v, a.act);
             }
         }
@@ -205,8 +211,8 @@ constexpr int HBK2 = 64, HROW2 = 72;  // halves per LDS row: 64 + 8 pad = 144 B 
 
 // BatchNorm statistics of the conv output z = acc + bias (training forward, BN with batch statistics), fused into
 // the epilogue so z is not read back: per output column of the 128 x 128 tile, over the tile's valid rows,
-// (sum, M2 = sum (z - sum / n)^2) in fp32 -> stats[(row tile) * Co + col][2]; bev_batchnorm_finalize_tiles_f32
-// combines the tiles in double (Chan et al.'s pairwise update).  Two-pass around the tile mean, so the variance
+// (sum, M2 = sum (z - sum / n)^2) in fp32 -> stats[col][row tile][2] (channel-major: the finalize reads each
+// channel's tiles contiguously); bev_batchnorm_finalize_tiles_f32 combines the tiles in double.  Two-pass around the tile mean, so the variance
 // has no E[z^2] - E[z]^2 cancellation.  Column col = n0 + wn 64 + j 32 + r32 is held by 32 rows of each lane,
 // the lane pair (h = 0, 1) and the two wm waves: lane sums, one xor-32 exchange, one LDS exchange.
 __device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&acc)[2][2], _Float16 *ldsh, int64_t m0,
@@ -261,7 +267,7 @@ __device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&ac
         for (int j = 0; j < 2; ++j) {
             const int c = wn * 64 + j * 32 + r32;
             if (n0 + c < a.Co) {
-                float *o = a.stats + ((m0 / HBM) * a.Co + n0 + c) * 2;
+                float *o = a.stats + ((int64_t)(n0 + c) * ((a.M + HBM - 1) / HBM) + m0 / HBM) * 2;
                 o[0] = sum[j];
                 o[1] = red[c] + red[128 + c];
             }
@@ -406,12 +412,18 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
             const int col = n0 + wn * 64 + j * 32 + r32;
             if (col >= a.Co) continue;
             const float bv = a.bias ? a.bias[col] : 0.0f;
+            float rv[16];  // all residual loads first: interleaved with the stores they would serialise (y may alias)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                rv[r] = (a.res && row < a.M) ? a.res[row * a.Co + col] : 0.0f;
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (row >= a.M) continue;
                 float v = acc[i][j][r] + bv;
-                if (a.res) v += a.res[row * a.Co + col];
+                if (a.res) v += rv[r];
                 a.y[row * a.ldy + col] = act_h(v, a.act);
             }
         }

@@ -11,7 +11,8 @@
 //                  k_wgrad_v4 = float4 staging without index divisions when Ci % 4 == 0 and Co % 4 == 0)
 //   k_colsum       db[co] = sum_m dz[m][co]
 //   k_maxpool_bwd  dx = sum of dy over the windows whose first maximum is this input (gather, no atomics;
-//                  k_maxpool_bwd_v4: four channels per thread when C % 4 == 0)
+//                  k_maxpool_bwd_v4: four channels per thread when C % 4 == 0; bev_maxpool2d_bwd_ws_nhwc_f32:
+//                  window argmax bytes once, then the gather -- k_maxpool_argmax_v4 + k_maxpool_bwd_idx_v4)
 //
 // All tensors NHWC fp32.  Float atomics in k_wgrad / k_colsum: the last bits of the weight gradients
 // may vary run to run (summation order); the activations' gradients are deterministic.
@@ -697,6 +698,81 @@ inline unsigned grid_for(int64_t n) {
     return (unsigned)(b < 256 * 64 ? (b > 0 ? b : 1) : 256 * 64);
 }
 
+// Two-pass max-pool backward for C % 4 == 0 (the trunk's 3x3 / 2 stem pool): k_maxpool_argmax_v4 scans every window
+// once with k_maxpool_bwd_v4's rule (first valid tap, then v > best or v NaN) and stores the winning tap ky * k + kx
+// per (output, channel) as one byte; k_maxpool_bwd_idx_v4 gathers, per input, dy of the windows whose byte names it,
+// in the same (oy, ox) order -- bit-identical to k_maxpool_bwd_v4, which re-scans every covering window per input
+// (4 windows x 9 taps of float4 loads per input for 3x3 / 2, against 2.25 here).
+__global__ __launch_bounds__(256) void k_maxpool_argmax_v4(const float *__restrict__ x, int N, int H, int W, int C,
+                                                           int k, int s, int p, int Ho, int Wo,
+                                                           uchar4 *__restrict__ arg) {
+    const int C4 = C >> 2;
+    const int64_t total = (int64_t)N * Ho * Wo * C4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % C4);
+        int64_t t = i / C4;
+        const int ox = (int)(t % Wo);
+        t /= Wo;
+        const int oy = (int)(t % Ho);
+        const int n = (int)(t / Ho);
+        int bi[4] = {-1, -1, -1, -1};
+        float best[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+        for (int ky = 0; ky < k; ++ky) {
+            const int yy = oy * s - p + ky;
+            if (yy < 0 || yy >= H) continue;
+            for (int kx = 0; kx < k; ++kx) {
+                const int xx = ox * s - p + kx;
+                if (xx < 0 || xx >= W) continue;
+                const float4 q = ((const float4 *)x)[(((int64_t)n * H + yy) * W + xx) * C4 + c4];
+                const float v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (bi[u] < 0) bi[u] = ky * k + kx;
+                    if (v[u] > best[u] || v[u] != v[u]) {
+                        best[u] = v[u];
+                        bi[u] = ky * k + kx;
+                    }
+                }
+            }
+        }
+        arg[i] = make_uchar4((unsigned char)bi[0], (unsigned char)bi[1], (unsigned char)bi[2], (unsigned char)bi[3]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_maxpool_bwd_idx_v4(const uchar4 *__restrict__ arg,
+                                                            const float *__restrict__ dy, int N, int H, int W, int C,
+                                                            int k, int s, int p, int Ho, int Wo,
+                                                            float *__restrict__ dx) {
+    const int C4 = C >> 2;
+    const int64_t total = (int64_t)N * H * W * C4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int c4 = (int)(i % C4);
+        int64_t t = i / C4;
+        const int ix = (int)(t % W);
+        t /= W;
+        const int iy = (int)(t % H);
+        const int n = (int)(t / H);
+        float g[4] = {0.f, 0.f, 0.f, 0.f};
+        const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(Ho - 1, (iy + p) / s);
+        const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(Wo - 1, (ix + p) / s);
+        for (int oy = oy_lo; oy <= oy_hi; ++oy)
+            for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+                const int me = (iy - (oy * s - p)) * k + (ix - (ox * s - p));
+                const int64_t o = (((int64_t)n * Ho + oy) * Wo + ox) * C4 + c4;
+                const uchar4 a = arg[o];
+                const bool h0 = a.x == me, h1 = a.y == me, h2 = a.z == me, h3 = a.w == me;
+                if (h0 || h1 || h2 || h3) {
+                    const float4 d = ((const float4 *)dy)[o];
+                    if (h0) g[0] += d.x;
+                    if (h1) g[1] += d.y;
+                    if (h2) g[2] += d.z;
+                    if (h3) g[3] += d.w;
+                }
+            }
+        ((float4 *)dx)[i] = make_float4(g[0], g[1], g[2], g[3]);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -807,6 +883,24 @@ int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, in
     else
         hipLaunchKernelGGL(k_maxpool_bwd, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, x, dy, N, H, W, C,
                            k, stride, pad, Ho, Wo, dx);
+    return last();
+}
+
+int bev_maxpool2d_bwd_ws_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride,
+                                  int pad, int Ho, int Wo, float *dx, uint8_t *argmax, void *stream) {
+    if (!x || !dy || !dx || !argmax || N < 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || k <= 0 || k * k > 255 ||
+        stride <= 0 || pad < 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx) & 15) != 0 || ((uintptr_t)argmax & 3) != 0) return BEV_ERR_ARGS;
+    const int64_t total = (int64_t)N * H * W * C;
+    if (total == 0) return 0;
+    const int64_t outs = (int64_t)N * Ho * Wo * C;
+    hipLaunchKernelGGL(k_maxpool_argmax_v4, dim3(grid_for(outs / 4)), dim3(256), 0, (hipStream_t)stream, x, N, H, W, C,
+                       k, stride, pad, Ho, Wo, (uchar4 *)argmax);
+    hipLaunchKernelGGL(k_maxpool_bwd_idx_v4, dim3(grid_for(total / 4)), dim3(256), 0, (hipStream_t)stream,
+                       (const uchar4 *)argmax, dy, N, H, W, C, k, stride, pad, Ho, Wo, dx);
     return last();
 }
 

@@ -434,9 +434,10 @@ class ResNet(nn.Module):
 
     def _forward_train(self, x: torch.Tensor, out_index: int) -> torch.Tensor:
         """Training: the same graph with one autograd node per conv + BN (+ residual) (+ ReLU)
-        and native backward kernels (trunk_grad.py; batch-statistics or frozen BN per module mode).  No bottleneck-tail fusion (the shortcut's
-        gradient is a separate conv backward)."""
-        from .trunk_grad import MaxPool, conv_bn_act
+        and native backward kernels (trunk_grad.py; batch-statistics or frozen BN per module mode).  No
+        bottleneck-tail fusion in the forward; in the backward an identity block's shortcut gradient is added in its
+        first conv's dgrad epilogue (trunk_grad.GradSink), a downsample block's is a separate conv backward."""
+        from .trunk_grad import GradSink, MaxPool, conv_bn_act
         y = conv_bn_act(self.conv1, self.bn1, x, relu=True, in_nchw=True)
         if out_index == 0:
             return y
@@ -447,10 +448,13 @@ class ResNet(nn.Module):
                 if blk.downsample is not None:
                     sc = conv_bn_act(blk.downsample[0], blk.downsample[1], y, relu=False)
                 chain = blk.convs()
+                # identity shortcut: the residual's gradient goes to the first conv's dgrad epilogue (GradSink)
+                sink = GradSink() if blk.downsample is None else None
                 h = y
                 for idx, (conv, bn, relu) in enumerate(chain):
                     last = idx == len(chain) - 1
-                    h = conv_bn_act(conv, bn, h, relu=relu, residual=sc if last else None)
+                    h = conv_bn_act(conv, bn, h, relu=relu, residual=sc if last else None,
+                                    sink_in=sink if idx == 0 else None, sink_out=sink if last else None)
                 y = h
             if li == out_index:
                 return y
