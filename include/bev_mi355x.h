@@ -60,7 +60,8 @@ int bev_abi_version(void);
  *   wherever Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel (both operands through LDS) for every shape.
  *   Same results bit for bit.
  * BEV_TUNE_CONV_H16_KERNEL: autocast fp16 convs: 0 (default) = 64-deep K steps, two steps in flight, where Ci % 64 ==
- *   0; 1 = the 32-deep-step kernel always.  Same results bit for bit.
+ *   0, and the 64-pixel-step weight gradient; 1 = the 32-deep-step conv and 32-pixel-step weight gradient always.
+ *   Same conv results bit for bit; weight gradients equal to fp32 tolerance (pixel chunks differ).
  * BEV_TUNE_CONV_PW_SMALL: narrow / tiny-K 1x1 convs (EfficientNet): 0 = the MFMA tiles; 1 = Co in
  *   {16, 24, 32, 40, 48} on a per-pixel VALU kernel (measured slower, kept for A/B); 2 (default) = 1x1 with
  *   Ci in {24, 32, 40, 48} and Co <= 32 on a wave-streaming MFMA kernel (k_pw_mfma, float4 epilogue through

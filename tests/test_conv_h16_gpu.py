@@ -143,10 +143,13 @@ def test_amp_functions_take_half_convs_only_under_autocast():
     dict(N=2, H=16, W=19, Ci=128, Co=36, K=3, stride=1, pad=2, dil=2),
     dict(N=3, H=9, W=11, Ci=96, Co=8, K=1, stride=1, pad=0, dil=1),
     dict(N=1, H=40, W=40, Ci=256, Co=64, K=1, stride=1, pad=0, dil=1),
-], ids=lambda d: f"{d['Ci']}to{d['Co']}k{d['K']}s{d['stride']}d{d['dil']}")
-def test_wgrad_h16_vs_float64_of_rounded_operands(shape):
+    dict(N=1, H=110, W=110, Ci=256, Co=256, K=3, stride=1, pad=1, dil=1),  # 7 K steps per workgroup in the 64-px kernel
+], ids=lambda d: f"{d['Ci']}to{d['Co']}k{d['K']}s{d['stride']}d{d['dil']}h{d['H']}")
+@pytest.mark.parametrize("kern", [0, 1], ids=["wgrad64", "wgrad32"])
+def test_wgrad_h16_vs_float64_of_rounded_operands(shape, kern):
     """conv_wgrad_ex under half_convs(): fp16 operands, fp32 sums (split over pixels, float atomics) against the
-    float64 weight gradient of the fp16-rounded operands; relative to sum |terms| < 2e-6."""
+    float64 weight gradient of the fp16-rounded operands; relative to sum |terms| < 2e-6.  kern: bev_tune
+    CONV_H16_KERNEL 0 = k_wgrad_h16b (64-pixel steps, two in flight), 1 = k_wgrad_h16 (32-pixel steps)."""
     import bev_native as nat
     N, H, W, Ci, Co, K = shape["N"], shape["H"], shape["W"], shape["Ci"], shape["Co"], shape["K"]
     st, pad, dil = shape["stride"], shape["pad"], shape["dil"]
@@ -155,7 +158,7 @@ def test_wgrad_h16_vs_float64_of_rounded_operands(shape):
     Ho = (H + 2 * pad - dil * (K - 1) - 1) // st + 1
     Wo = (W + 2 * pad - dil * (K - 1) - 1) // st + 1
     dz = torch.randn(N, Ho, Wo, Co, generator=g) * 1e-3
-    with nat._half_mode(True):
+    with nat._half_mode(True), nat.tuned(CONV_H16_KERNEL=kern):
         dw = nat.conv_wgrad_ex(x.to(DEV), dz.to(DEV), K, pad, dil, stride=st)
     torch.cuda.synchronize()
     xh, dh = x.half().double().permute(0, 3, 1, 2), dz.half().double().permute(0, 3, 1, 2)

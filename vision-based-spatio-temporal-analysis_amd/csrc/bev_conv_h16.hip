@@ -31,7 +31,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));  // native vector: stays in VGPRs (uint4 arrays went to scratch)
 
 constexpr int HBM = 128, HBN = 128, HBK = 32;
-int g_h16_kernel = 0;  // BEV_TUNE_CONV_H16_KERNEL: 0 = k_conv_h16b where Ci % 64 == 0, 1 = k_conv_h16 always
+int g_h16_kernel = 0;  // BEV_TUNE_CONV_H16_KERNEL: 0 = k_conv_h16b where Ci % 64 == 0 and k_wgrad_h16b, 1 = k_conv_h16
+                       // and k_wgrad_h16 always
 constexpr int HROW = 40;  // halves per LDS row: 32 + 8 pad = 80 B = 5 slots (odd: 16 rows -> 16 distinct slots)
 
 __device__ __attribute__((aligned(16))) float g_hzero4[4] = {0.f, 0.f, 0.f, 0.f};  // never written
@@ -555,6 +556,163 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16(const float *__restrict__ 
         }
 }
 
+// ---- k_wgrad_h16b: 64 pixels per K step, two steps of operands in flight -----------------------------------------
+// k_wgrad_h16's 32-pixel step gives a wave 8 MFMAs (~256 cycles) per barrier with one step of loads in flight: the
+// global-load latency is exposed (the weight gradient was 15 % of the AMP training step).  Here a step is 64 pixels
+// (16 MFMAs per wave) and, as in k_conv_h16b, the loads of steps s + 1 and s + 2 sit in two register sets while
+// step s runs.  Staging: thread (rg = tid >> 5, q = tid & 31) loads pixel rows 8 rg .. 8 rg + 7 of channel quad q
+// of both operands and writes each channel's 8 pixels as ONE ds_write_b128 ([channel][pixel] rows of 72 halves:
+// 9 odd 16-B slots, conflict-free fragment reads).  Same per-element products; pixel chunks per workgroup are
+// multiples of 64 (fp32-tolerance equal to k_wgrad_h16, float atomics across chunks as there).
+constexpr int WMS2 = 64, WROW2 = 72;
+
+__global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__ x, const float *__restrict__ dz,
+                                                        int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
+                                                        int K, int stride, int pad, int dil, int64_t mchunk, int ctiles,
+                                                        int ntiles, float *__restrict__ dW) {
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2][2 * WT * WROW2];
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int tile = (int)(bid % (unsigned)ntiles);
+    const int64_t split = bid / (unsigned)ntiles;
+    const int co0 = (tile % ctiles) * WT, k0 = (tile / ctiles) * WT;
+    const int64_t M = (int64_t)N * Ho * Wo;
+    const int64_t mb = split * mchunk, me = mb + mchunk < M ? mb + mchunk : M;
+    if (mb >= me) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int rg = tid >> 5, q = tid & 31;  // staging: pixel rows 8 rg .. 8 rg + 7, channel quad q
+    const int co = co0 + 4 * q;
+    const bool co_ok = co < Co;
+    const int k = k0 + 4 * q;
+    const bool k_ok = k < K;
+    const int tap = k_ok ? k / Ci : 0, ci = k - tap * Ci, ky = tap / KW, kx = tap - ky * KW;
+    const int dyo = ky * dil - pad, dxo = kx * dil - pad;
+    int px, py, pn;  // (column, row, image) of this thread's first pixel row of the next step to load
+    {
+        const int64_t m = mb + 8 * rg, t = m / Wo;
+        px = (int)(m - t * Wo);
+        py = (int)(t % Ho);
+        pn = (int)(t / Ho);
+    }
+    int64_t ms = mb;
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+#define WG16_LOAD(RA, RB)                                                                                      \
+    do {                                                                                                       \
+        int x1 = px, y1 = py, n1 = pn;                                                                         \
+        _Pragma("unroll") for (int r = 0; r < 8; ++r) {                                                        \
+            const int64_t m = ms + 8 * rg + r;                                                                 \
+            const bool mok = m < me;                                                                           \
+            RA[r] = (mok && co_ok) ? *(const f32x4 *)(dz + m * Co + co) : z4;                                  \
+            const int iy = y1 * stride + dyo, ix = x1 * stride + dxo;                                          \
+            const bool in = mok && k_ok && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;           \
+            RB[r] = in ? *(const f32x4 *)(x + (((int64_t)n1 * H + iy) * W + ix) * Ci + ci) : z4;               \
+            if (++x1 == Wo) {                                                                                  \
+                x1 = 0;                                                                                        \
+                if (++y1 == Ho) {                                                                              \
+                    y1 = 0;                                                                                    \
+                    ++n1;                                                                                      \
+                }                                                                                              \
+            }                                                                                                  \
+        }                                                                                                      \
+        ms += WMS2;                                                                                            \
+        px += WMS2;                                                                                            \
+        while (px >= Wo) {                                                                                     \
+            px -= Wo;                                                                                          \
+            if (++py == Ho) {                                                                                  \
+                py = 0;                                                                                        \
+                ++pn;                                                                                          \
+            }                                                                                                  \
+        }                                                                                                      \
+    } while (0)
+#define WG16_STORE(BUF, RA, RB)                                                                                \
+    do {                                                                                                       \
+        _Float16 *As = lds[BUF], *Bs = As + WT * WROW2;                                                        \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                                        \
+            h16x8 ha, hb;                                                                                      \
+            _Pragma("unroll") for (int r = 0; r < 8; ++r) {                                                    \
+                ha[r] = (_Float16)RA[r][c];                                                                    \
+                hb[r] = (_Float16)RB[r][c];                                                                    \
+            }                                                                                                  \
+            *(h16x8 *)(As + (4 * q + c) * WROW2 + 8 * rg) = ha;                                                \
+            *(h16x8 *)(Bs + (4 * q + c) * WROW2 + 8 * rg) = hb;                                                \
+        }                                                                                                      \
+    } while (0)
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    const int r32 = lane & 31, h = lane >> 5;
+#define WG16_MFMA(BUF)                                                                                         \
+    do {                                                                                                       \
+        const _Float16 *As = lds[BUF], *Bs = As + WT * WROW2;                                                  \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk) {                                                     \
+            h16x8 fa[2], fb[2];                                                                                \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                      \
+                fa[i] = *(const h16x8 *)(As + (wm * 64 + i * 32 + r32) * WROW2 + kk * 16 + 8 * h);             \
+            _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                      \
+                fb[j] = *(const h16x8 *)(Bs + (wn * 64 + j * 32 + r32) * WROW2 + kk * 16 + 8 * h);             \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                      \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);      \
+            __builtin_amdgcn_sched_barrier(0);                                                                 \
+        }                                                                                                      \
+    } while (0)
+    f32x4 ra0[8], rb0[8], ra1[8], rb1[8];
+    const int nk = (int)((me - mb + WMS2 - 1) / WMS2);
+    WG16_LOAD(ra0, rb0);
+    if (nk > 1) WG16_LOAD(ra1, rb1);
+    WG16_STORE(0, ra0, rb0);
+    __syncthreads();
+    int ks = 0;  // loop head: LDS buffer 0 holds step ks, register set 1 step ks + 1
+    for (; ks + 3 < nk; ks += 2) {
+        WG16_LOAD(ra0, rb0);
+        WG16_MFMA(0);
+        WG16_STORE(1, ra1, rb1);
+        __syncthreads();
+        WG16_LOAD(ra1, rb1);
+        WG16_MFMA(1);
+        WG16_STORE(0, ra0, rb0);
+        __syncthreads();
+    }
+    if (ks + 2 < nk) {
+        WG16_LOAD(ra0, rb0);
+        WG16_MFMA(0);
+        WG16_STORE(1, ra1, rb1);
+        __syncthreads();
+        WG16_MFMA(1);
+        WG16_STORE(0, ra0, rb0);
+        __syncthreads();
+        WG16_MFMA(0);
+    } else if (ks + 1 < nk) {
+        WG16_MFMA(0);
+        WG16_STORE(1, ra1, rb1);
+        __syncthreads();
+        WG16_MFMA(1);
+    } else {
+        WG16_MFMA(0);
+    }
+#undef WG16_MFMA
+#undef WG16_STORE
+#undef WG16_LOAD
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int kc = k0 + wn * 64 + j * 32 + r32;
+            if (kc >= K) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int cr = co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (cr < Co) atomicAdd(dW + (int64_t)cr * K + kc, acc[i][j][r]);
+            }
+        }
+}
+
 }  // namespace
 
 namespace bev {
@@ -583,13 +741,19 @@ int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const fl
     if (hipMemsetAsync(dW, 0, (size_t)Co * K * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
     if (M == 0) return 0;
     const int ct = (Co + WT - 1) / WT, kt = (K + WT - 1) / WT, nt = ct * kt;
+    const bool deep = g_h16_kernel == 0;  // k_wgrad_h16b (64-pixel steps, two in flight); 1: k_wgrad_h16
+    const int step = deep ? WMS2 : WMS;
     int64_t sp = 1024 / nt + 1;  // >= ~1024 workgroups
     int64_t mc = (M + sp - 1) / sp;
-    mc = ((mc + WMS - 1) / WMS) * WMS;
+    mc = ((mc + step - 1) / step) * step;
     sp = (M + mc - 1) / mc;
     if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL(k_wgrad_h16, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K,
-                       stride, pad, dilation, mc, ct, nt, dW);
+    if (deep)
+        hipLaunchKernelGGL(k_wgrad_h16b, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW,
+                           K, stride, pad, dilation, mc, ct, nt, dW);
+    else
+        hipLaunchKernelGGL(k_wgrad_h16, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW,
+                           K, stride, pad, dilation, mc, ct, nt, dW);
     return (int)hipGetLastError();
 }
 
