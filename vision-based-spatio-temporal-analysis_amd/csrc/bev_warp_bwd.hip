@@ -22,7 +22,8 @@
 // time (the rows of a wave may hit the same pixel; a wave's LDS operations complete in order).  The four copies are
 // summed per (pixel, channel) and go to the gradient with one global float atomic per touched (pixel, channel),
 // coalesced along channels for NHWC gradients (one 256-B wave instruction per pixel) or along x for NCHW.
-// Footprints whose four copies do not fit the LDS pool (horizon tiles) add their run sums straight to global memory.
+// A footprint whose four copies do not fit the LDS pool is done in two halves of the tile (two waves each, two copies
+// of the half's own box); only a half whose box still does not fit adds its run sums straight to global memory.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(RB_NT, 2) void k_warp_bwd_runs(const float *__restr
     const int64_t plane = (int64_t)Hb * Wb;
     const bool vec = row_in && (Wb % 4 == 0) && j0 + RB_T <= Wb;
     const double rV = recip_uniform(V);
-    const int maxpix = pool / (4 * RB_PIX) - 1;  // four copies, each + its trash pixel
+    const int maxpix = pool / (4 * RB_PIX) - 1;  // four copies, each + its trash pixel (whole-tile footprints)
     const int rw = lane >> 4;                     // the lane's row within its wave
 
     for (int c0 = 0; c0 < C; c0 += 64) {
@@ -261,74 +262,98 @@ __global__ __launch_bounds__(RB_NT, 2) void k_warp_bwd_runs(const float *__restr
             for (int q = 0; q < 9; ++q) h[q] = Hmat[__builtin_amdgcn_readfirstlane(n * 9) + q];
             Taps t = cell_taps(h, cx, cy, grid, sx, sy);
             if (!inside) t.valid = 0;
-            const Box4 bx = block_box(t, red, wave, lane);  // one barrier; red[] reused next view after two more
-            if (bx.x1 < 0) {
+            const Box4 bxt = block_box(t, red, wave, lane);  // one barrier; red[] reused after the next barrier
+            if (bxt.x1 < 0) {
                 __syncthreads();  // red[] is read by every wave before the next view rewrites it
                 continue;
             }
-            const int bw = bx.x1 - bx.x0 + 1, npix = bw * (bx.y1 - bx.y0 + 1);
-            const bool use_img = npix <= maxpix;
-            const int cpy = (npix + 1) * RB_PIX;  // bytes of one image copy (+ its trash pixel)
-            if (use_img) {
-                float4 *z = reinterpret_cast<float4 *>(img);
-                for (int k = tid; k < 4 * cpy / 16; k += RB_NT) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
             if (per_view) load_g(gout + (int64_t)n * C * plane);
-            __syncthreads();  // image zeroed; red[] consumed
+            // A footprint too large for four per-wave copies is done in two halves of the tile (waves 0-1, then
+            // 2-3), each with its own (smaller) box and two copies of twice the size -- instead of adding every run
+            // straight to global memory.
+            const int npt = (bxt.x1 - bxt.x0 + 1) * (bxt.y1 - bxt.y0 + 1);
+            const int parts = npt <= maxpix ? 1 : 2;
+            for (int part = 0; part < parts; ++part) {
+                const bool active = parts == 1 || (wave >> 1) == part;
+                Taps tp = t;
+                if (!active) tp.valid = 0;
+                Box4 bx = bxt;
+                if (parts > 1) {
+                    __syncthreads();  // red[] consumed before block_box rewrites it
+                    bx = block_box(tp, red, wave, lane);
+                    if (bx.x1 < 0) {
+                        __syncthreads();
+                        continue;
+                    }
+                }
+                const int ncop = parts == 1 ? 4 : 2, copy = parts == 1 ? wave : (wave & 1);
+                const int bw = bx.x1 - bx.x0 + 1, npix = bw * (bx.y1 - bx.y0 + 1);
+                const bool use_img = npix <= pool / (ncop * RB_PIX) - 1;
+                const int cpy = (npix + 1) * RB_PIX;  // bytes of one image copy (+ its trash pixel)
+                if (use_img) {
+                    float4 *z = reinterpret_cast<float4 *>(img);
+                    for (int k = tid; k < ncop * cpy / 16; k += RB_NT) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+                __syncthreads();  // image zeroed; red[] consumed
 
-            const int key = quad_key(t);
-            const GSink gs{gfeats + (int64_t)n * sN + (int64_t)c0 * sC, sC, sH, sW, l16, cmax};
-            // byte addresses of this cell's four taps in its wave's image copy, WITHOUT the lane's channel
-            // offset (the addresses are row-broadcast from the owning lane; run_flush adds 16 * lane16);
-            // invalid taps -> the copy's trash pixel
-            const int cb = wave * cpy;
-            const int px = t.x0 - bx.x0, py = t.y0 - bx.y0;
-            int a[4];
+                if (active) {  // wave-uniform
+                    const int key = quad_key(tp);
+                    const GSink gs{gfeats + (int64_t)n * sN + (int64_t)c0 * sC, sC, sH, sW, l16, cmax};
+                    // byte addresses of this cell's four taps in its wave's image copy, WITHOUT the lane's channel
+                    // offset (the addresses are row-broadcast from the owning lane; run_flush adds 16 * lane16);
+                    // invalid taps -> the copy's trash pixel
+                    const int cb = copy * cpy;
+                    const int px = tp.x0 - bx.x0, py = tp.y0 - bx.y0;
+                    int a[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                a[u] = use_img && (t.valid & (1u << u)) ? cb + ((py + (u >> 1)) * bw + px + (u & 1)) * RB_PIX
-                                                        : cb + npix * RB_PIX;
-            walk_row(g, key, a, t.w, use_img, rw, smem, gs);
+                    for (int u = 0; u < 4; ++u)
+                        a[u] = use_img && (tp.valid & (1u << u)) ? cb + ((py + (u >> 1)) * bw + px + (u & 1)) * RB_PIX
+                                                                 : cb + npix * RB_PIX;
+                    walk_row(g, key, a, tp.w, use_img, rw, smem, gs);
+                }
 
-            if (use_img) {
-                __syncthreads();  // every row's quad sums are in the image
-                float *gfv = gfeats + (int64_t)n * sN + (int64_t)c0 * sC;
-                if (sC == 1) {  // channels contiguous: one pixel per wave instruction, lane = channel
-                    for (int p0 = wave * 4; p0 < npix; p0 += 16) {  // 4 pixels per wave in flight
-                        float val[4];
+                if (use_img) {
+                    __syncthreads();  // every row's quad sums are in the image
+                    float *gfv = gfeats + (int64_t)n * sN + (int64_t)c0 * sC;
+                    if (sC == 1) {  // channels contiguous: one pixel per wave instruction, lane = channel
+                        for (int p0 = wave * 4; p0 < npix; p0 += 16) {  // 4 pixels per wave in flight
+                            float val[4];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            val[u] = 0.0f;
-                            if (p0 + u < npix) {
+                            for (int u = 0; u < 4; ++u) {
+                                val[u] = 0.0f;
+                                if (p0 + u < npix) {
 #pragma unroll
-                                for (int w = 0; w < 4; ++w) val[u] += img[(w * cpy) / 4 + (p0 + u) * 64 + lane];
+                                    for (int w = 0; w < 4; ++w)
+                                        if (w < ncop) val[u] += img[(w * cpy) / 4 + (p0 + u) * 64 + lane];
+                                }
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const int p = p0 + u, qy = p / bw, qx = p - qy * bw;
+                                if (val[u] != 0.0f && lane < cmax)
+                                    unsafeAtomicAdd(gfv + (int64_t)(bx.y0 + qy) * sH + (int64_t)(bx.x0 + qx) * sW + lane,
+                                                    val[u]);
                             }
                         }
+                    } else {  // lanes along x: for each (channel, footprint row), 64 consecutive pixels per step
+                        const int bh = npix / bw;
+                        for (int r = wave; r < cmax * bh; r += 4) {
+                            const int c = r / bh, qy = r - c * bh;
+                            for (int qx = lane; qx < bw; qx += 64) {
+                                float val = 0.0f;
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int p = p0 + u, py = p / bw, px = p - py * bw;
-                            if (val[u] != 0.0f && lane < cmax)
-                                unsafeAtomicAdd(gfv + (int64_t)(bx.y0 + py) * sH + (int64_t)(bx.x0 + px) * sW + lane,
-                                                val[u]);
-                        }
-                    }
-                } else {  // lanes along x: for each (channel, footprint row), 64 consecutive pixels per step
-                    const int bh = npix / bw;
-                    for (int r = wave; r < cmax * bh; r += 4) {
-                        const int c = r / bh, py = r - c * bh;
-                        for (int px = lane; px < bw; px += 64) {
-                            float val = 0.0f;
-#pragma unroll
-                            for (int w = 0; w < 4; ++w) val += img[(w * cpy) / 4 + (py * bw + px) * 64 + c];
-                            if (val != 0.0f)
-                                unsafeAtomicAdd(gfv + (int64_t)c * sC + (int64_t)(bx.y0 + py) * sH +
-                                                    (int64_t)(bx.x0 + px) * sW,
-                                                val);
+                                for (int w = 0; w < 4; ++w)
+                                    if (w < ncop) val += img[(w * cpy) / 4 + (qy * bw + qx) * 64 + c];
+                                if (val != 0.0f)
+                                    unsafeAtomicAdd(gfv + (int64_t)c * sC + (int64_t)(bx.y0 + qy) * sH +
+                                                        (int64_t)(bx.x0 + qx) * sW,
+                                                    val);
+                            }
                         }
                     }
                 }
+                __syncthreads();  // the image is free for the next part / view
             }
-            __syncthreads();  // the image is free for the next view
         }
     }
 }
