@@ -60,8 +60,9 @@ int bev_abi_version(void);
  *   wherever Ci (and Ci2) % 32 == 0, 1 = the 16-deep-step kernel (both operands through LDS) for every shape.
  *   Same results bit for bit.
  * BEV_TUNE_CONV_H16_KERNEL: autocast fp16 convs: 0 (default) = 64-deep K steps, two steps in flight, where Ci % 64 ==
- *   0, and the 64-pixel-step weight gradient; 1 = the 32-deep-step conv and 32-pixel-step weight gradient always.
- *   Same conv results bit for bit; weight gradients equal to fp32 tolerance (pixel chunks differ).
+ *   0 (64-column tiles for Co <= 64), and the 64-pixel-step weight gradient; 1 = the 32-deep-step conv and
+ *   32-pixel-step weight gradient always; 2 = as 0 with 128-column tiles always.  Same conv results bit for bit;
+ *   weight gradients equal to fp32 tolerance (pixel chunks differ).
  * BEV_TUNE_CONV_PW_SMALL: narrow / tiny-K 1x1 convs (EfficientNet): 0 = the MFMA tiles; 1 = Co in
  *   {16, 24, 32, 40, 48} on a per-pixel VALU kernel (measured slower, kept for A/B); 2 (default) = 1x1 with
  *   Ci in {24, 32, 40, 48} and Co <= 32 on a wave-streaming MFMA kernel (k_pw_mfma, float4 epilogue through
@@ -313,6 +314,10 @@ int bev_relu_bwd_f32(const float *dy, const float *y, float *dz, int64_t n, void
 int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd, int Wd,
                         float *out, void *stream);
 
+/* bev_dilate_nhwc_f32 for elements of elem_bytes 4 (fp32) or 2 (fp16 storage): a copy, any 4-channel quad type. */
+int bev_dilate_nhwc_ex(const void *dz, int elem_bytes, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd,
+                       int Wd, void *out, void *stream);
+
 /* dW [Co][KH*KW*Ci] (k = (ky*KW + kx)*Ci + ci, OVERWRITTEN) = sum over output pixels of
  * dz[m][co] * im2col(x)[m][k] (conv weight gradient; float atomics across m-splits). */
 int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,
@@ -364,12 +369,25 @@ int bev_conv2d_h16_bnstats_f32(const float *x, int N, int H, int W, int Ci, cons
                                int Co, int KH, int KW, int stride, int pad, int dilation, float *y, int Ho, int Wo,
                                float *tile_stats, void *stream);
 
+/* bev_conv2d_h16_f32 / _bnstats_f32 in one entry, with the operand x optionally STORED in fp16 (x_half = 1: uint16
+ * storage of _Float16, 8-B aligned, Ci % 64 == 0) -- the values the fp32-operand kernel rounds x to while staging,
+ * so the result is bit-identical; tile_stats may be NULL (else act 0, no residual, ldy == Co). */
+int bev_conv2d_h16_ex_f32(const void *x, int x_half, int N, int H, int W, int Ci, const uint16_t *packed,
+                          const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
+                          int dilation, int act, float *y, int ldy, int Ho, int Wo, float *tile_stats, void *stream);
+
 /* Weight gradient of a convolution under autocast(float16): dW[co][(ky*KW + kx)*Ci + ci] =
  * sum over output pixels of f16(dz) * f16(x) with fp32 accumulation (the fp16 matrix cores), dW [Co][KH*KW*Ci]
  * fp32 (zeroed by the call).  x [N,H,W,Ci], dz [N,Ho,Wo,Co] NHWC fp32, Ci % 4 == 0, Co % 4 == 0, 16-B aligned.
  * Replaces the conv weight gradient autograd computes for the reference's autocast branch (train.py:238-247). */
 int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
                            int KH, int KW, int stride, int pad, int dilation, float *dW, void *stream);
+
+/* bev_conv_wgrad_h16_f32 with x and / or dz optionally stored in fp16 (x_half / dz_half = 1; 8-B aligned): the
+ * values the fp32-operand kernel rounds them to, so the products are identical. */
+int bev_conv_wgrad_h16_ex_f32(const void *x, int x_half, int N, int H, int W, int Ci, const void *dz, int dz_half,
+                              int Ho, int Wo, int Co, int KH, int KW, int stride, int pad, int dilation, float *dW,
+                              void *stream);
 
 /* ---------------------------------------------------------------------------
  * fp32 convolutions on the bf16 matrix cores (exact three-way operand split; bev_conv_x6.hip)
@@ -493,6 +511,11 @@ int bev_batchnorm_finalize_tiles_f32(const float *tile_stats, int ntiles, int ro
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                             const float *residual, int act, float *y, void *stream);
 
+/* bev_batchnorm_apply_f32 with y stored in fp16 when y_half = 1 (round to nearest even) -- for an output whose only
+ * readers round it to fp16 anyway (the autocast convs' operands), so storing it rounded changes no result. */
+int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                               const float *residual, int act, void *y, int y_half, void *stream);
+
 /* device: backward of y = act(batchnorm(z) (+ residual)): act 1 (ReLU) takes its mask from the forward output
  * y, act 3 (ReLU of a layer WITHOUT residual; dres must be NULL, y is not read) recomputes it exactly as
  * z * scale + shift > 0 (apply's rounding), act 2 (SiLU) recomputes u = z * scale + shift; frozen = 1 for running statistics (the mean / variance are
@@ -502,6 +525,12 @@ int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64
                           const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
                           int frozen, float *dz, float *dres, float *dgamma, float *dbeta, void *workspace,
                           void *stream);
+
+/* bev_batchnorm_bwd_f32 with dz stored in fp16 when dz_half = 1 (for a dz read only by fp16-operand kernels). */
+int bev_batchnorm_bwd_ex_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
+                             const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
+                             int frozen, void *dz, int dz_half, float *dres, float *dgamma, float *dbeta,
+                             void *workspace, void *stream);
 
 /* host: workspace bytes of bev_channel_sums_f32 (-1: C % 4 != 0 or an empty shape). */
 int64_t bev_channel_sums_workspace_bytes(int N, int64_t P, int C);

@@ -72,23 +72,32 @@ def test_conv_h16_vs_float64_of_rounded_operands(shape):
     _case(**shape)
 
 
-@pytest.mark.parametrize("Ci,K,stride", [(64, 3, 1), (128, 3, 2), (256, 1, 1)])
-def test_conv_h16_kernels_bit_identical(Ci, K, stride):
-    """The 64-deep-step kernel (default for Ci % 64 == 0) and the 32-deep one sum every output in the same order."""
+@pytest.mark.parametrize("Ci,K,stride,Co", [(64, 3, 1, 192), (128, 3, 2, 192), (256, 1, 1, 192), (64, 3, 1, 64),
+                                            (256, 1, 1, 40), (128, 3, 2, 64)])
+def test_conv_h16_kernels_bit_identical(Ci, K, stride, Co):
+    """The 64-deep-step kernel (default for Ci % 64 == 0; 64-column tiles when Co <= 64), the same with 128-column
+    tiles always (CONV_H16_KERNEL 2) and the 32-deep one (1) sum every output in the same order; and fp16-stored
+    operands (bev_conv2d_h16_ex_f32 x_half) give the same bits as the fp32 operand they round."""
     import bev_native as nat
-    g = torch.Generator().manual_seed(Ci)
-    N, H, W, Co = 2, 19, 27, 192
+    g = torch.Generator().manual_seed(Ci + Co)
+    N, H, W = 2, 19, 27
     x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
     w = (torch.randn(Co, Ci, K, K, generator=g) / (Ci * K * K) ** 0.5).to(DEV)
     b = torch.randn(Co, generator=g).to(DEV)
     with nat._half_mode(True):
         packed = nat.pack_conv_weight(w)
     outs = []
-    for kern in (0, 1):
+    for kern in (0, 1, 2):
         with nat.tuned(CONV_H16_KERNEL=kern):
             outs.append(nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, stride, K // 2, 1, 1))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    # fp16-stored operand (the conv_h16_any path), default and 128-column kernels, against the fp32 operand
+    z0 = nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, stride, K // 2, 1, 0)
+    for kern in (0, 2):
+        with nat.tuned(CONV_H16_KERNEL=kern):
+            z = nat.conv2d_h16_any(x.half(), packed, Co, K, K, stride, K // 2, bias=b)
+        assert torch.equal(z, z0)
 
 
 def test_conv_h16_rejects_bad_arguments():

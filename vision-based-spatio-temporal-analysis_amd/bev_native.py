@@ -102,6 +102,13 @@ SIGNATURES = {
     "bev_conv2d_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _vp]),
     "bev_conv_wgrad_h16_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv_h16_stat_tiles": (_i64, [_i64]),
+    "bev_conv2d_h16_ex_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i,
+                                   _vp, _vp]),
+    "bev_conv_wgrad_h16_ex_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_batchnorm_apply_ex_f32": (_i, [_vp, _i64, _i, _vp, _vp, _vp, _i, _vp, _i, _vp]),
+    "bev_batchnorm_bwd_ex_f32": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp,
+                                      _vp, _vp]),
+    "bev_dilate_nhwc_ex": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_h16_bnstats_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_batchnorm_finalize_tiles_f32": (_i, [_vp, _i, _i, _i64, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                _vp]),
@@ -275,6 +282,12 @@ def _half_mode(on: bool):
         yield
     finally:
         _AMP_LOCAL.half = prev
+
+
+def amp_half_active() -> bool:
+    """True where a native Function called now would run its convolutions in the fp16 AMP arithmetic."""
+    return bool(torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16
+                and AMP_HALF_CONVS)
 
 
 def amp_fwd(fn):
@@ -630,6 +643,100 @@ def conv2d_nhwc_h16_bnstats(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: 
                                               _ptr(z), Ho, Wo, _ptr(tiles), _stream(x))
     _check(rc, "bev_conv2d_h16_bnstats_f32")
     return z, tiles
+
+
+# ---- fp16-STORED operands of the autocast convs (bit-identical: the kernels round these operands to fp16 anyway) ----
+def _require_gpu_h(*ts):
+    """Like _require_gpu, but fp16 tensors are accepted (operands stored in the precision the kernel computes in)."""
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise HipError("libbev_mi355x kernels need ROCm device tensors (got a CPU tensor); "
+                           "this package has no CPU fallback")
+        if t.dtype not in (torch.float32, torch.float16):
+            raise HipError(f"fp32 / fp16 tensors expected, got {t.dtype}")
+
+
+def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: int, stride: int, pad: int,
+                   stats: bool = False, residual: torch.Tensor = None, bias: torch.Tensor = None):
+    """The autocast fp16 conv with x [N,H,W,Ci] stored in fp32 or fp16 (Ci % 64 == 0 for fp16) -> z fp32
+    [N,Ho,Wo,Co] (+ residual), and with `stats` the BatchNorm tile partials (conv2d_nhwc_h16_bnstats)."""
+    x = x.contiguous()
+    _require_gpu_h(x)
+    _require_gpu(residual, bias)
+    if not packed.is_cuda or packed.dtype != torch.float16:
+        raise HipError("conv2d_h16_any needs the fp16 weight panel on the device")
+    N, H, W, Ci = x.shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    z = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    tiles = None
+    if stats:
+        nt = lib().bev_conv_h16_stat_tiles(N * Ho * Wo)
+        _check(0 if nt > 0 else nt, "bev_conv_h16_stat_tiles")
+        tiles = torch.empty(Co, nt, 2, device=x.device, dtype=torch.float32)
+    if residual is not None:
+        residual = residual.contiguous()
+    with _span("conv", x):
+        rc = lib().bev_conv2d_h16_ex_f32(_ptr(x), int(x.dtype == torch.float16), N, H, W, Ci, _ptr(packed),
+                                         _ptr(bias), _ptr(residual), Co, KH, KW, stride, pad, 1, 0, _ptr(z), Co, Ho,
+                                         Wo, _ptr(tiles), _stream(x))
+    _check(rc, "bev_conv2d_h16_ex_f32")
+    return (z, tiles) if stats else z
+
+
+def conv_wgrad_h16_any(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stride: int, pad: int) -> torch.Tensor:
+    """The autocast weight gradient with x / dz stored in fp32 or fp16 (Ci, Co % 4 == 0) -> dW [Co, Ci, KH, KW]."""
+    x, dz = x.contiguous(), dz.contiguous()
+    _require_gpu_h(x, dz)
+    N, H, W, Ci = x.shape
+    _, Ho, Wo, Co = dz.shape
+    dW = torch.empty(Co, KH, KW, Ci, device=x.device, dtype=torch.float32)
+    _check(lib().bev_conv_wgrad_h16_ex_f32(_ptr(x), int(x.dtype == torch.float16), N, H, W, Ci, _ptr(dz),
+                                           int(dz.dtype == torch.float16), Ho, Wo, Co, KH, KW, stride, pad, 1,
+                                           _ptr(dW), _stream(x)), "bev_conv_wgrad_h16_ex_f32")
+    return dW.permute(0, 3, 1, 2).contiguous()
+
+
+def dilate_nhwc_any(dz: torch.Tensor, s: int, top: int, left: int, Hd: int, Wd: int) -> torch.Tensor:
+    dz = dz.contiguous()
+    _require_gpu_h(dz)
+    N, Ho, Wo, C = dz.shape
+    out = torch.empty(N, Hd, Wd, C, device=dz.device, dtype=dz.dtype)
+    _check(lib().bev_dilate_nhwc_ex(_ptr(dz), dz.element_size(), N, Ho, Wo, C, s, top, left, Hd, Wd, _ptr(out),
+                                    _stream(dz)), "bev_dilate_nhwc_ex")
+    return out
+
+
+def batchnorm_apply_half(z: torch.Tensor, scale, shift, act: int = 0) -> torch.Tensor:
+    """batchnorm_apply (no residual) with the output stored in fp16: for a y whose only readers are fp16-operand
+    kernels (the next autocast conv and its weight gradient), which round it to exactly these values."""
+    _require_gpu(z, scale, shift)
+    assert z.is_contiguous()
+    C = z.shape[-1]
+    y = torch.empty(z.shape, device=z.device, dtype=torch.float16)
+    _check(lib().bev_batchnorm_apply_ex_f32(_ptr(z), z.numel() // C, C, _ptr(scale), _ptr(shift), None, int(act),
+                                            _ptr(y), 1, _stream(z)), "bev_batchnorm_apply_ex_f32")
+    return y
+
+
+def batchnorm_bwd_half(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_dres: bool, act: int = 1,
+                       scale=None, shift=None, frozen: bool = False):
+    """batchnorm_bwd with dz stored in fp16 (for a dz read only by the fp16-operand dgrad / weight gradient)."""
+    dy = dy.contiguous()
+    _require_gpu(dy, y, z, mean, rstd, gamma, scale, shift)
+    C = z.shape[-1]
+    M = z.numel() // C
+    dz = torch.empty(z.shape, device=z.device, dtype=torch.float16)
+    dres = torch.empty_like(z) if want_dres else None
+    dg = torch.empty(C, device=z.device)
+    db = torch.empty(C, device=z.device)
+    ws = _bn_workspace(M, C, z.device)
+    _check(lib().bev_batchnorm_bwd_ex_f32(_ptr(dy), _ptr(y), _ptr(z), M, C, _ptr(mean), _ptr(rstd),
+                                          _ptr(gamma.detach().contiguous()), _ptr(scale), _ptr(shift), int(act),
+                                          int(frozen), _ptr(dz), 1, _ptr(dres), _ptr(dg), _ptr(db), _ptr(ws),
+                                          _stream(z)), "bev_batchnorm_bwd_ex_f32")
+    return dz, dres, dg, db
 
 
 def batchnorm_finalize_tiles(tiles: torch.Tensor, M: int, gamma, beta, running_mean, running_var, eps: float,

@@ -243,10 +243,17 @@ __global__ __launch_bounds__(FT_T) void k_bn_finalize_tiles(const float *__restr
 }
 
 // IT: uint32_t when the element count fits (no 64-bit divisions in the channel decode), else int64_t
-template <typename IT>
+// store 4 values: fp32, or fp16 (RNE) when the only readers are fp16-operand kernels (bit-identical to their rounding)
+__device__ __forceinline__ void st4(float *p, int64_t e, float4 o) { *(float4 *)(p + e) = o; }
+__device__ __forceinline__ void st4(_Float16 *p, int64_t e, float4 o) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    *(h4 *)(p + e) = (h4){(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
+}
+
+template <typename IT, typename OT>
 __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__restrict__ scale,
                            const float *__restrict__ shift, const float *__restrict__ res, int act,
-                           float *__restrict__ y, IT total4) {
+                           OT *__restrict__ y, IT total4) {
     const IT C4 = (IT)(C / 4);
     for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
         const int64_t e = 4 * (int64_t)i;
@@ -261,7 +268,7 @@ __global__ void k_bn_apply(const float *__restrict__ z, int C, const float *__re
         if (act == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
         if (act == 2)  // torch SiLU: x / (1 + exp(-x))
             o = make_float4(silu_hw(o.x), silu_hw(o.y), silu_hw(o.z), silu_hw(o.w));
-        *(float4 *)(y + e) = o;
+        st4(y, e, o);
     }
 }
 
@@ -279,12 +286,12 @@ __global__ __launch_bounds__(FIN_C * FIN_P) void k_bn_bwd_finalize(const double 
     coef[2 * c + 1] = frozen ? 0.f : (float)(b / (double)M);
 }
 
-template <typename IT>
+template <typename IT, typename OT>
 __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__restrict__ y, const float *__restrict__ z,
                                int C, const float *__restrict__ mean, const float *__restrict__ rstd,
                                const float *__restrict__ gamma, const float *__restrict__ scale,
                                const float *__restrict__ shift, int act, const float *__restrict__ coef,
-                               float *__restrict__ dz, float *__restrict__ dres, IT total4) {
+                               OT *__restrict__ dz, float *__restrict__ dres, IT total4) {
     const IT C4 = (IT)(C / 4);
     for (IT i = (IT)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (IT)gridDim.x * blockDim.x) {
         const int64_t e = 4 * (int64_t)i;
@@ -300,7 +307,7 @@ __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__rest
             const float xh = (zv[u] - mean[c]) * rstd[c];
             o[u] = gamma[c] * rstd[c] * (g[u] - coef[2 * c] - xh * coef[2 * c + 1]);
         }
-        *(float4 *)(dz + e) = make_float4(o[0], o[1], o[2], o[3]);
+        st4(dz, e, make_float4(o[0], o[1], o[2], o[3]));
         if (dres) *(float4 *)(dres + e) = make_float4(g[0], g[1], g[2], g[3]);
     }
 }
@@ -400,23 +407,37 @@ int bev_batchnorm_finalize_tiles_f32(const float *tile_stats, int ntiles, int ro
     return (int)hipGetLastError();
 }
 
-int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
-                            const float *residual, int act, float *y, void *stream) {
+int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                               const float *residual, int act, void *y, int y_half, void *stream) {
     if (!z || !scale || !shift || !y || !bn_shape_ok(M, C) || act < 0 || act > 2) return BEV_ERR_ARGS;
     const int64_t total4 = M * C / 4;
-    if (total4 < ((int64_t)1 << 32) - 65536 * 256)
-        hipLaunchKernelGGL(k_bn_apply<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C,
-                           scale, shift, residual, act, y, (uint32_t)total4);
+    const dim3 g(stream_blocks(total4));
+    hipStream_t st = (hipStream_t)stream;
+    const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
+    if (y_half && small)
+        hipLaunchKernelGGL((k_bn_apply<uint32_t, _Float16>), g, dim3(256), 0, st, z, C, scale, shift, residual, act,
+                           (_Float16 *)y, (uint32_t)total4);
+    else if (y_half)
+        hipLaunchKernelGGL((k_bn_apply<int64_t, _Float16>), g, dim3(256), 0, st, z, C, scale, shift, residual, act,
+                           (_Float16 *)y, total4);
+    else if (small)
+        hipLaunchKernelGGL((k_bn_apply<uint32_t, float>), g, dim3(256), 0, st, z, C, scale, shift, residual, act,
+                           (float *)y, (uint32_t)total4);
     else
-        hipLaunchKernelGGL(k_bn_apply<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, (hipStream_t)stream, z, C,
-                           scale, shift, residual, act, y, total4);
+        hipLaunchKernelGGL((k_bn_apply<int64_t, float>), g, dim3(256), 0, st, z, C, scale, shift, residual, act,
+                           (float *)y, total4);
     return (int)hipGetLastError();
 }
 
-int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
-                          const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
-                          int frozen, float *dz, float *dres, float *dgamma, float *dbeta, void *workspace,
-                          void *stream) {
+int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                            const float *residual, int act, float *y, void *stream) {
+    return bev_batchnorm_apply_ex_f32(z, M, C, scale, shift, residual, act, y, 0, stream);
+}
+
+int bev_batchnorm_bwd_ex_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
+                             const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
+                             int frozen, void *dz, int dz_half, float *dres, float *dgamma, float *dbeta,
+                             void *workspace, void *stream) {
     if (!dy || !z || !mean || !rstd || !gamma || !dz || !dgamma || !dbeta || !workspace || !bn_shape_ok(M, C) ||
         act < 0 || act > 3 || (act == 1 && !y) || ((act == 2 || act == 3) && (!scale || !shift)) ||
         (act == 3 && dres))  // act 3: ReLU recomputed from z, only for a layer without residual
@@ -430,13 +451,29 @@ int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st, part, nb, M, C,
                        frozen, coef, dgamma, dbeta);
     const int64_t total4 = M * C / 4;
-    if (total4 < ((int64_t)1 << 32) - 65536 * 256)
-        hipLaunchKernelGGL(k_bn_bwd_apply<uint32_t>, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean,
-                           rstd, gamma, scale, shift, act, coef, dz, dres, (uint32_t)total4);
+    const dim3 g(stream_blocks(total4));
+    const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
+    if (dz_half && small)
+        hipLaunchKernelGGL((k_bn_bwd_apply<uint32_t, _Float16>), g, dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,
+                           scale, shift, act, coef, (_Float16 *)dz, dres, (uint32_t)total4);
+    else if (dz_half)
+        hipLaunchKernelGGL((k_bn_bwd_apply<int64_t, _Float16>), g, dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,
+                           scale, shift, act, coef, (_Float16 *)dz, dres, total4);
+    else if (small)
+        hipLaunchKernelGGL((k_bn_bwd_apply<uint32_t, float>), g, dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,
+                           scale, shift, act, coef, (float *)dz, dres, (uint32_t)total4);
     else
-        hipLaunchKernelGGL(k_bn_bwd_apply<int64_t>, dim3(stream_blocks(total4)), dim3(256), 0, st, dy, y, z, C, mean,
-                           rstd, gamma, scale, shift, act, coef, dz, dres, total4);
+        hipLaunchKernelGGL((k_bn_bwd_apply<int64_t, float>), g, dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,
+                           scale, shift, act, coef, (float *)dz, dres, total4);
     return (int)hipGetLastError();
+}
+
+int bev_batchnorm_bwd_f32(const float *dy, const float *y, const float *z, int64_t M, int C, const float *mean,
+                          const float *rstd, const float *gamma, const float *scale, const float *shift, int act,
+                          int frozen, float *dz, float *dres, float *dgamma, float *dbeta, void *workspace,
+                          void *stream) {
+    return bev_batchnorm_bwd_ex_f32(dy, y, z, M, C, mean, rstd, gamma, scale, shift, act, frozen, dz, 0, dres, dgamma,
+                                    dbeta, workspace, stream);
 }
 
 int64_t bev_channel_sums_workspace_bytes(int N, int64_t P, int C) {

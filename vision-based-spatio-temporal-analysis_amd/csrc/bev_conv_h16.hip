@@ -58,6 +58,7 @@ __global__ void k_pack_h16(const float *__restrict__ w, int Co, int Ci, int KH, 
 
 struct ConvH {
     const float *__restrict__ x;
+    const _Float16 *__restrict__ xh;  // k_conv_h16b<true>: the operand stored in fp16 (what the kernel rounds x to)
     const _Float16 *__restrict__ wp;
     const float *__restrict__ bias;
     const float *__restrict__ res;
@@ -216,9 +217,11 @@ constexpr int HBK2 = 64, HROW2 = 72;  // halves per LDS row: 64 + 8 pad = 144 B 
 // channel's tiles contiguously); bev_batchnorm_finalize_tiles_f32 combines the tiles in double.  Two-pass around the tile mean, so the variance
 // has no E[z^2] - E[z]^2 cancellation.  Column col = n0 + wn 64 + j 32 + r32 is held by 32 rows of each lane,
 // the lane pair (h = 0, 1) and the two wm waves: lane sums, one xor-32 exchange, one LDS exchange.
-__device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&acc)[2][2], _Float16 *ldsh, int64_t m0,
+template <int BN, int TI>
+__device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&acc)[TI][2], _Float16 *ldsh, int64_t m0,
                                                int n0, int wm, int wn, int r32, int h) {
-    float *red = reinterpret_cast<float *>(ldsh);  // [2 wm][128 cols]
+    constexpr int NRW = BN == 128 ? 2 : 4, WROWS = BN == 128 ? 64 : 32;  // row-waves sharing a column, rows each
+    float *red = reinterpret_cast<float *>(ldsh);  // [NRW][BN cols]
     const int64_t nv64 = a.M - m0;
     const int nv = nv64 < HBM ? (int)nv64 : HBM;
     float mean[2], sum[2];
@@ -229,20 +232,23 @@ __device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&ac
         const float bv = (a.bias && n0 + c < a.Co) ? a.bias[n0 + c] : 0.0f;
         float s = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int row = wm * WROWS + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (row < nv) s += acc[i][j][r] + bv;
             }
         s += __shfl_xor(s, 32);
-        if (h == 0) red[wm * 128 + c] = s;
+        if (h == 0) red[wm * BN + c] = s;
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int c = wn * 64 + j * 32 + r32;
-        sum[j] = red[c] + red[128 + c];
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NRW; ++w) t += red[w * BN + c];
+        sum[j] = t;
         mean[j] = sum[j] / (float)nv;
     }
     __syncthreads();  // sums consumed before the M2 exchange reuses red
@@ -252,15 +258,15 @@ __device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&ac
         const float bv = (a.bias && n0 + c < a.Co) ? a.bias[n0 + c] : 0.0f;
         float q = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int row = wm * WROWS + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 const float d = acc[i][j][r] + bv - mean[j];
                 if (row < nv) q = fmaf(d, d, q);
             }
         q += __shfl_xor(q, 32);
-        if (h == 0) red[wm * 128 + c] = q;
+        if (h == 0) red[wm * BN + c] = q;
     }
     __syncthreads();
     if (wm == 0 && h == 0) {
@@ -268,19 +274,29 @@ __device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&ac
         for (int j = 0; j < 2; ++j) {
             const int c = wn * 64 + j * 32 + r32;
             if (n0 + c < a.Co) {
+                float t = 0.0f;
+#pragma unroll
+                for (int w = 0; w < NRW; ++w) t += red[w * BN + c];
                 float *o = a.stats + ((int64_t)(n0 + c) * ((a.M + HBM - 1) / HBM) + m0 / HBM) * 2;
                 o[0] = sum[j];
-                o[1] = red[c] + red[128 + c];
+                o[1] = t;
             }
         }
     }
 }
 
+// HIN: the operand arrives in fp16 (a.xh) -- the value the fp32 path rounds it to while staging, so the result is
+// bit-identical; 8-B loads instead of 16 and no conversion.
+// BN: output columns per workgroup.  128: 2 x 2 waves of 64 x 64 (2 x 2 MFMA tiles each); 64 (outputs of <= 64
+// channels: no zero half of the panel loaded or multiplied): 4 x 1 waves of 32 x 64 (1 x 2 tiles).  Per output the
+// K order is the same, so both give identical conv results.
+template <bool HIN, int BN>
 __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
-    __shared__ __attribute__((aligned(16))) _Float16 lds[2][(HBM + HBN) * HROW2];
+    constexpr int TI = BN == 128 ? 2 : 1, WROWS = BN == 128 ? 64 : 32, NBU = BN == 128 ? 4 : 2;
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2][(HBM + BN) * HROW2];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int ntn = (a.Co + HBN - 1) / HBN;
+    const int wm = BN == 128 ? wave >> 1 : wave, wn = BN == 128 ? wave & 1 : 0;
+    const int ntn = (a.Co + BN - 1) / BN;
     const int64_t ntm = (a.M + HBM - 1) / HBM;
     unsigned bid = blockIdx.x;
     {
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
     const int nt = (int)(bid % (unsigned)ntn);
     if (mt >= ntm) return;
     const int64_t m0 = mt * HBM;
-    const int n0 = nt * HBN;
+    const int n0 = nt * BN;
     // A staging: rows (tid >> 2) + 64 q (q < 2), channel quads (tid & 3) + 4 u (u < 4): 64 channels per step,
     // two rows of tap metadata per thread
     const int aq = tid & 3;
@@ -311,23 +327,32 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
         iy0[q] = oy * a.stride - a.pad;
         ix0[q] = ox * a.stride - a.pad;
     }
-    // B staging: weight row n0 + (tid >> 1), halves 32 (tid & 1) .. + 31 of the K step
-    const _Float16 *wrow = a.wp + (int64_t)(n0 + (tid >> 1)) * a.Kp + 32 * (tid & 1);
+    // B staging: weight row n0 + (tid >> 1), halves 32 (tid & 1) .. + 31 of the K step (BN 64: row n0 + (tid >> 2),
+    // halves 16 (tid & 3) .. + 15)
+    const int brow = BN == 128 ? tid >> 1 : tid >> 2, bcol = BN == 128 ? 32 * (tid & 1) : 16 * (tid & 3);
+    const _Float16 *wrow = a.wp + (int64_t)(n0 + brow) * a.Kp + bcol;
     int ky = 0, kx = 0, ci0 = 0;
     int64_t kb = 0;
     f32x4 ra0[8], ra1[8];
-    u32x4 rb0[4], rb1[4];
-#define H16_GLOAD(RA, RB)                                                                                  \
+    h16x4 rh0[8], rh1[8];
+    u32x4 rb0[NBU], rb1[NBU];
+#define H16_GLOAD(RA, RH, RB)                                                                              \
     do {                                                                                                   \
         const int dy = ky * a.dil, dx = kx * a.dil;                                                        \
         _Pragma("unroll") for (int q = 0; q < 2; ++q) {                                                    \
             const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                                  \
             const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;        \
-            const float *src = in ? a.x + pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 : g_hzero4;       \
+            const int64_t e = pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0;                              \
             const int st = in ? 16 : 0; /* the zero quad is re-read for every u */                         \
-            _Pragma("unroll") for (int u = 0; u < 4; ++u) RA[4 * q + u] = *(const f32x4 *)(src + st * u);  \
+            if constexpr (HIN) {                                                                           \
+                const _Float16 *src = in ? a.xh + e : (const _Float16 *)g_hzero4;                          \
+                _Pragma("unroll") for (int u = 0; u < 4; ++u) RH[4 * q + u] = *(const h16x4 *)(src + st * u); \
+            } else {                                                                                       \
+                const float *src = in ? a.x + e : g_hzero4;                                                \
+                _Pragma("unroll") for (int u = 0; u < 4; ++u) RA[4 * q + u] = *(const f32x4 *)(src + st * u); \
+            }                                                                                              \
         }                                                                                                  \
-        _Pragma("unroll") for (int u = 0; u < 4; ++u) RB[u] = *(const u32x4 *)(wrow + kb + 8 * u);         \
+        _Pragma("unroll") for (int u = 0; u < NBU; ++u) RB[u] = *(const u32x4 *)(wrow + kb + 8 * u);       \
         kb += HBK2;                                                                                        \
         ci0 += HBK2;                                                                                       \
         if (ci0 == a.Ci) {                                                                                 \
@@ -338,19 +363,21 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
             }                                                                                              \
         }                                                                                                  \
     } while (0)
-#define H16_SWRITE(BUF, RA, RB)                                                                            \
+#define H16_SWRITE(BUF, RA, RH, RB)                                                                        \
     do {                                                                                                   \
         _Float16 *As = lds[BUF], *Bs = As + HBM * HROW2;                                                   \
         _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                    \
-            const h16x4 hv = {(_Float16)RA[q][0], (_Float16)RA[q][1], (_Float16)RA[q][2], (_Float16)RA[q][3]}; \
+            h16x4 hv;                                                                                      \
+            if constexpr (HIN) hv = RH[q];                                                                 \
+            else hv = (h16x4){(_Float16)RA[q][0], (_Float16)RA[q][1], (_Float16)RA[q][2], (_Float16)RA[q][3]}; \
             *(h16x4 *)(As + ((tid >> 2) + 64 * (q >> 2)) * HROW2 + 4 * aq + 16 * (q & 3)) = hv;            \
         }                                                                                                  \
-        _Pragma("unroll") for (int u = 0; u < 4; ++u)                                                      \
-            *(u32x4 *)(Bs + (tid >> 1) * HROW2 + 32 * (tid & 1) + 8 * u) = RB[u];                          \
+        _Pragma("unroll") for (int u = 0; u < NBU; ++u)                                                    \
+            *(u32x4 *)(Bs + brow * HROW2 + bcol + 8 * u) = RB[u];                                          \
     } while (0)
-    f32x16 acc[2][2];
+    f32x16 acc[TI][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
     const int r32 = lane & 31, h = lane >> 5;
@@ -358,45 +385,45 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
     do {                                                                                                   \
         const _Float16 *As = lds[BUF], *Bs = As + HBM * HROW2;                                             \
         _Pragma("unroll") for (int kk = 0; kk < 4; ++kk) {                                                 \
-            h16x8 fa[2], fb[2];                                                                            \
-            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                  \
-                fa[i] = *(const h16x8 *)(As + (wm * 64 + i * 32 + r32) * HROW2 + kk * 16 + 8 * h);         \
+            h16x8 fa[TI], fb[2];                                                                           \
+            _Pragma("unroll") for (int i = 0; i < TI; ++i)                                                 \
+                fa[i] = *(const h16x8 *)(As + (wm * WROWS + i * 32 + r32) * HROW2 + kk * 16 + 8 * h);      \
             _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
                 fb[j] = *(const h16x8 *)(Bs + (wn * 64 + j * 32 + r32) * HROW2 + kk * 16 + 8 * h);         \
-            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                  \
+            _Pragma("unroll") for (int i = 0; i < TI; ++i)                                                 \
                 _Pragma("unroll") for (int j = 0; j < 2; ++j)                                              \
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);  \
             __builtin_amdgcn_sched_barrier(0); /* one slice of fragments live at a time (VGPR budget) */   \
         }                                                                                                  \
     } while (0)
     const int nk = a.Kp / HBK2;
-    H16_GLOAD(ra0, rb0);
-    if (nk > 1) H16_GLOAD(ra1, rb1);
-    H16_SWRITE(0, ra0, rb0);
+    H16_GLOAD(ra0, rh0, rb0);
+    if (nk > 1) H16_GLOAD(ra1, rh1, rb1);
+    H16_SWRITE(0, ra0, rh0, rb0);
     __syncthreads();
     int ks = 0;  // loop head: LDS buffer 0 holds step ks, register set 1 step ks + 1
     for (; ks + 3 < nk; ks += 2) {
-        H16_GLOAD(ra0, rb0);
+        H16_GLOAD(ra0, rh0, rb0);
         H16_MFMA(0);
-        H16_SWRITE(1, ra1, rb1);
+        H16_SWRITE(1, ra1, rh1, rb1);
         __syncthreads();
-        H16_GLOAD(ra1, rb1);
+        H16_GLOAD(ra1, rh1, rb1);
         H16_MFMA(1);
-        H16_SWRITE(0, ra0, rb0);
+        H16_SWRITE(0, ra0, rh0, rb0);
         __syncthreads();
     }
     if (ks + 2 < nk) {
-        H16_GLOAD(ra0, rb0);
+        H16_GLOAD(ra0, rh0, rb0);
         H16_MFMA(0);
-        H16_SWRITE(1, ra1, rb1);
+        H16_SWRITE(1, ra1, rh1, rb1);
         __syncthreads();
         H16_MFMA(1);
-        H16_SWRITE(0, ra0, rb0);
+        H16_SWRITE(0, ra0, rh0, rb0);
         __syncthreads();
         H16_MFMA(0);
     } else if (ks + 1 < nk) {
         H16_MFMA(0);
-        H16_SWRITE(1, ra1, rb1);
+        H16_SWRITE(1, ra1, rh1, rb1);
         __syncthreads();
         H16_MFMA(1);
     } else {
@@ -405,9 +432,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
 #undef H16_MFMA
 #undef H16_SWRITE
 #undef H16_GLOAD
-    if (a.stats) h16_tile_stats(a, acc, lds[0], m0, n0, wm, wn, r32, h);
+    if (a.stats) h16_tile_stats<BN, TI>(a, acc, lds[0], m0, n0, wm, wn, r32, h);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = n0 + wn * 64 + j * 32 + r32;
@@ -416,12 +443,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
             float rv[16];  // all residual loads first: interleaved with the stores they would serialise (y may alias)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int64_t row = m0 + wm * WROWS + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 rv[r] = (a.res && row < a.M) ? a.res[row * a.Co + col] : 0.0f;
             }
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int64_t row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int64_t row = m0 + wm * WROWS + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (row >= a.M) continue;
                 float v = acc[i][j][r] + bv;
                 if (a.res) v += rv[r];
@@ -564,8 +591,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16(const float *__restrict__ 
 // of both operands and writes each channel's 8 pixels as ONE ds_write_b128 ([channel][pixel] rows of 72 halves:
 // 9 odd 16-B slots, conflict-free fragment reads).  Same per-element products; pixel chunks per workgroup are
 // multiples of 64 (fp32-tolerance equal to k_wgrad_h16, float atomics across chunks as there).
+// XH / DH: x / dz arrive in fp16 (the values the fp32 path rounds them to: bit-identical products).
 constexpr int WMS2 = 64, WROW2 = 72;
 
+template <bool XH, bool DH>
 __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__ x, const float *__restrict__ dz,
                                                         int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
                                                         int K, int stride, int pad, int dil, int64_t mchunk, int ctiles,
@@ -606,10 +635,17 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
         _Pragma("unroll") for (int r = 0; r < 8; ++r) {                                                        \
             const int64_t m = ms + 8 * rg + r;                                                                 \
             const bool mok = m < me;                                                                           \
-            RA[r] = (mok && co_ok) ? *(const f32x4 *)(dz + m * Co + co) : z4;                                  \
+            if constexpr (DH)                                                                                  \
+                RA##h[r] = (mok && co_ok) ? *(const h16x4 *)((const _Float16 *)dz + m * Co + co) : h4z;        \
+            else                                                                                               \
+                RA[r] = (mok && co_ok) ? *(const f32x4 *)(dz + m * Co + co) : z4;                              \
             const int iy = y1 * stride + dyo, ix = x1 * stride + dxo;                                          \
             const bool in = mok && k_ok && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;           \
-            RB[r] = in ? *(const f32x4 *)(x + (((int64_t)n1 * H + iy) * W + ix) * Ci + ci) : z4;               \
+            const int64_t xe = (((int64_t)n1 * H + iy) * W + ix) * Ci + ci;                                    \
+            if constexpr (XH)                                                                                  \
+                RB##h[r] = in ? *(const h16x4 *)((const _Float16 *)x + xe) : h4z;                              \
+            else                                                                                               \
+                RB[r] = in ? *(const f32x4 *)(x + xe) : z4;                                                    \
             if (++x1 == Wo) {                                                                                  \
                 x1 = 0;                                                                                        \
                 if (++y1 == Ho) {                                                                              \
@@ -634,8 +670,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
         _Pragma("unroll") for (int c = 0; c < 4; ++c) {                                                        \
             h16x8 ha, hb;                                                                                      \
             _Pragma("unroll") for (int r = 0; r < 8; ++r) {                                                    \
-                ha[r] = (_Float16)RA[r][c];                                                                    \
-                hb[r] = (_Float16)RB[r][c];                                                                    \
+                if constexpr (DH) ha[r] = RA##h[r][c];                                                         \
+                else ha[r] = (_Float16)RA[r][c];                                                               \
+                if constexpr (XH) hb[r] = RB##h[r][c];                                                         \
+                else hb[r] = (_Float16)RB[r][c];                                                               \
             }                                                                                                  \
             *(h16x8 *)(As + (4 * q + c) * WROW2 + 8 * rg) = ha;                                                \
             *(h16x8 *)(Bs + (4 * q + c) * WROW2 + 8 * rg) = hb;                                                \
@@ -663,6 +701,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
         }                                                                                                      \
     } while (0)
     f32x4 ra0[8], rb0[8], ra1[8], rb1[8];
+    h16x4 ra0h[8], rb0h[8], ra1h[8], rb1h[8];
+    const h16x4 h4z = {(_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f, (_Float16)0.0f};
     const int nk = (int)((me - mb + WMS2 - 1) / WMS2);
     WG16_LOAD(ra0, rb0);
     if (nk > 1) WG16_LOAD(ra1, rb1);
@@ -717,7 +757,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
 
 namespace bev {
 int conv_h16_tune(int value) {
-    if (value < 0 || value > 1) return BEV_ERR_ARGS;
+    if (value < 0 || value > 2) return BEV_ERR_ARGS;
     const int old = g_h16_kernel;
     g_h16_kernel = value;
     return old;
@@ -726,12 +766,15 @@ int conv_h16_tune(int value) {
 
 extern "C" {
 
-int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
-                           int KH, int KW, int stride, int pad, int dilation, float *dW, void *stream) {
+int bev_conv_wgrad_h16_ex_f32(const void *xv, int x_half, int N, int H, int W, int Ci, const void *dzv, int dz_half,
+                              int Ho, int Wo, int Co, int KH, int KW, int stride, int pad, int dilation, float *dW,
+                              void *stream) {
+    const float *x = (const float *)xv, *dz = (const float *)dzv;
     if (!x || !dz || !dW || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
         pad < 0 || dilation <= 0)
         return BEV_ERR_ARGS;
-    if (Ci % 4 != 0 || Co % 4 != 0 || (((uintptr_t)x | (uintptr_t)dz) & 15) != 0) return BEV_ERR_ARGS;
+    if (Ci % 4 != 0 || Co % 4 != 0 || (((uintptr_t)x | (uintptr_t)dz) & 7) != 0) return BEV_ERR_ARGS;
+    if ((!x_half && ((uintptr_t)x & 15) != 0) || (!dz_half && ((uintptr_t)dz & 15) != 0)) return BEV_ERR_ARGS;
     if (Ho != (H + 2 * pad - dilation * (KH - 1) - 1) / stride + 1 ||
         Wo != (W + 2 * pad - dilation * (KW - 1) - 1) / stride + 1 || Ho <= 0 || Wo <= 0)
         return BEV_ERR_ARGS;
@@ -741,22 +784,31 @@ int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const fl
     if (hipMemsetAsync(dW, 0, (size_t)Co * K * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
     if (M == 0) return 0;
     const int ct = (Co + WT - 1) / WT, kt = (K + WT - 1) / WT, nt = ct * kt;
-    const bool deep = g_h16_kernel == 0;  // k_wgrad_h16b (64-pixel steps, two in flight); 1: k_wgrad_h16
+    const bool deep = g_h16_kernel != 1 || x_half || dz_half;  // k_wgrad_h16b (64-pixel steps, two in flight); 1:
+                                                               // k_wgrad_h16 (fp32 operands only)
     const int step = deep ? WMS2 : WMS;
     int64_t sp = 1024 / nt + 1;  // >= ~1024 workgroups
     int64_t mc = (M + sp - 1) / sp;
     mc = ((mc + step - 1) / step) * step;
     sp = (M + mc - 1) / mc;
     if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    if (deep)
-        hipLaunchKernelGGL(k_wgrad_h16b, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW,
-                           K, stride, pad, dilation, mc, ct, nt, dW);
+    if (deep) {
+        auto kern = x_half ? (dz_half ? k_wgrad_h16b<true, true> : k_wgrad_h16b<true, false>)
+                           : (dz_half ? k_wgrad_h16b<false, true> : k_wgrad_h16b<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K,
+                           stride, pad, dilation, mc, ct, nt, dW);
+    }
     else
         hipLaunchKernelGGL(k_wgrad_h16, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW,
                            K, stride, pad, dilation, mc, ct, nt, dW);
     return (int)hipGetLastError();
 }
 
+
+int bev_conv_wgrad_h16_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co,
+                           int KH, int KW, int stride, int pad, int dilation, float *dW, void *stream) {
+    return bev_conv_wgrad_h16_ex_f32(x, 0, N, H, W, Ci, dz, 0, Ho, Wo, Co, KH, KW, stride, pad, dilation, dW, stream);
+}
 
 int64_t bev_conv_packed_size_h16(int Co, int Ci, int KH, int KW) {
     if (Co <= 0 || Ci <= 0 || KH <= 0 || KW <= 0) return BEV_ERR_ARGS;
@@ -771,9 +823,10 @@ int bev_conv_pack_weights_h16(const float *w, int Co, int Ci, int KH, int KW, ui
     return (int)hipGetLastError();
 }
 
-static int conv_h16(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
+static int conv_h16(const void *xv, int x_half, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
                     const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act, float *y,
                     int ldy, int Ho, int Wo, float *stats, void *stream) {
+    const float *x = (const float *)xv;
     if (!x || !packed || !y || N < 0 || H <= 0 || W <= 0 || Ci <= 0 || Co <= 0 || KH <= 0 || KW <= 0 ||
         stride <= 0 || pad < 0 || dilation <= 0 || act < 0 || act > 2 || ldy < Co)
         return BEV_ERR_ARGS;
@@ -783,11 +836,14 @@ static int conv_h16(const float *x, int N, int H, int W, int Ci, const uint16_t 
         return BEV_ERR_ARGS;
     if ((((uintptr_t)x | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
     if (residual && ldy != Co) return BEV_ERR_ARGS;
-    const bool wide = Ci % HBK2 == 0 && g_h16_kernel == 0;
+    const bool wide = Ci % HBK2 == 0 && g_h16_kernel != 1;
     if (stats && (!wide || act != 0 || residual)) return BEV_ERR_ARGS;  // statistics of the raw conv output, k_conv_h16b
+    if (x_half && !wide) return BEV_ERR_ARGS;                         // fp16 operands: k_conv_h16b only
+    if (x_half && ((uintptr_t)x & 7) != 0) return BEV_ERR_ARGS;
     if (N == 0) return 0;
     ConvH a;
-    a.x = x;
+    a.x = x_half ? nullptr : x;
+    a.xh = x_half ? (const _Float16 *)xv : nullptr;
     a.wp = (const _Float16 *)packed;
     a.bias = bias;
     a.res = residual;
@@ -797,10 +853,16 @@ static int conv_h16(const float *x, int N, int H, int W, int Ci, const uint16_t 
     a.dil = dilation, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = ldy;
     a.Kp = (int)kpad_h(Ci * KH * KW);
     a.M = (int64_t)N * Ho * Wo;
-    const int64_t blocks = ((a.M + HBM - 1) / HBM) * ((Co + HBN - 1) / HBN);
+    const bool n64 = wide && Co <= 64 && g_h16_kernel != 2;  // 2: the 128-column tile always (A/B, same results)
+    const int64_t blocks = ((a.M + HBM - 1) / HBM) * (n64 ? 1 : (Co + HBN - 1) / HBN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    if (wide)
-        hipLaunchKernelGGL(k_conv_h16b, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+    const dim3 g((unsigned)blocks), b(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (wide) {
+        void (*kern)(ConvH) = n64 ? (x_half ? k_conv_h16b<true, 64> : k_conv_h16b<false, 64>)
+                                  : (x_half ? k_conv_h16b<true, 128> : k_conv_h16b<false, 128>);
+        hipLaunchKernelGGL(kern, g, b, 0, st, a);
+    }
     else
         hipLaunchKernelGGL(k_conv_h16, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
@@ -809,7 +871,7 @@ static int conv_h16(const float *x, int N, int H, int W, int Ci, const uint16_t 
 int bev_conv2d_h16_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
                        const float *residual, int Co, int KH, int KW, int stride, int pad, int dilation, int act,
                        float *y, int ldy, int Ho, int Wo, void *stream) {
-    return conv_h16(x, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, dilation, act, y, ldy, Ho, Wo,
+    return conv_h16(x, 0, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, dilation, act, y, ldy, Ho, Wo,
                     nullptr, stream);
 }
 
@@ -819,8 +881,15 @@ int bev_conv2d_h16_bnstats_f32(const float *x, int N, int H, int W, int Ci, cons
                                int Co, int KH, int KW, int stride, int pad, int dilation, float *y, int Ho, int Wo,
                                float *tile_stats, void *stream) {
     if (!tile_stats) return BEV_ERR_ARGS;
-    return conv_h16(x, N, H, W, Ci, packed, bias, nullptr, Co, KH, KW, stride, pad, dilation, 0, y, Co, Ho, Wo,
+    return conv_h16(x, 0, N, H, W, Ci, packed, bias, nullptr, Co, KH, KW, stride, pad, dilation, 0, y, Co, Ho, Wo,
                     tile_stats, stream);
+}
+
+int bev_conv2d_h16_ex_f32(const void *x, int x_half, int N, int H, int W, int Ci, const uint16_t *packed,
+                          const float *bias, const float *residual, int Co, int KH, int KW, int stride, int pad,
+                          int dilation, int act, float *y, int ldy, int Ho, int Wo, float *tile_stats, void *stream) {
+    return conv_h16(x, x_half, N, H, W, Ci, packed, bias, residual, Co, KH, KW, stride, pad, dilation, act, y, ldy, Ho,
+                    Wo, tile_stats, stream);
 }
 
 }  // extern "C"

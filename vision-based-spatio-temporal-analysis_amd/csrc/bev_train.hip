@@ -42,9 +42,11 @@ __global__ __launch_bounds__(256) void k_relu_bwd(const float *__restrict__ dy, 
     }
 }
 
-// out [N][Hd][Wd][C] (zero everywhere else): out[n][top + oy*s][left + ox*s][c] = dz[n][oy][ox][c]
-__global__ __launch_bounds__(256) void k_dilate(const float *__restrict__ dz, int N, int Ho, int Wo, int C, int s,
-                                                int top, int left, int Hd, int Wd, float *__restrict__ out) {
+// out [N][Hd][Wd][C] (zero everywhere else): out[n][top + oy*s][left + ox*s][c] = dz[n][oy][ox][c]; Q = one
+// channel quad (float4 for fp32, uint2 for fp16 elements: a copy, so any 4-element type)
+template <typename Q>
+__global__ __launch_bounds__(256) void k_dilate(const Q *__restrict__ dz, int N, int Ho, int Wo, int C, int s,
+                                                int top, int left, int Hd, int Wd, Q *__restrict__ out) {
     const int64_t total = (int64_t)N * Hd * Wd * (C / 4);
     const int C4 = C / 4;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -55,10 +57,10 @@ __global__ __launch_bounds__(256) void k_dilate(const float *__restrict__ dz, in
         const int y = (int)(t % Hd);
         const int n = (int)(t / Hd);
         const int yy = y - top, xx = x - left;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        Q v = {};
         if (yy >= 0 && xx >= 0 && yy % s == 0 && xx % s == 0 && yy / s < Ho && xx / s < Wo)
-            v = ((const float4 *)dz)[(((int64_t)n * Ho + yy / s) * Wo + xx / s) * C4 + c4];
-        ((float4 *)out)[i] = v;
+            v = dz[(((int64_t)n * Ho + yy / s) * Wo + xx / s) * C4 + c4];
+        out[i] = v;
     }
 }
 
@@ -784,16 +786,25 @@ int bev_relu_bwd_f32(const float *dy, const float *y, float *dz, int64_t n, void
     return last();
 }
 
-int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd, int Wd,
-                        float *out, void *stream) {
+int bev_dilate_nhwc_ex(const void *dz, int elem_bytes, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd,
+                       int Wd, void *out, void *stream) {
     if (!dz || !out || N < 0 || Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0 || s <= 0 || top < 0 || left < 0 ||
-        top + s * (Ho - 1) >= Hd || left + s * (Wo - 1) >= Wd)
+        top + s * (Ho - 1) >= Hd || left + s * (Wo - 1) >= Wd || (elem_bytes != 4 && elem_bytes != 2))
         return BEV_ERR_ARGS;
     const int64_t total = (int64_t)N * Hd * Wd * (C / 4);
     if (total == 0) return 0;
-    hipLaunchKernelGGL(k_dilate, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, dz, N, Ho, Wo, C, s, top,
-                       left, Hd, Wd, out);
+    if (elem_bytes == 4)
+        hipLaunchKernelGGL(k_dilate<float4>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                           (const float4 *)dz, N, Ho, Wo, C, s, top, left, Hd, Wd, (float4 *)out);
+    else
+        hipLaunchKernelGGL(k_dilate<uint2>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
+                           (const uint2 *)dz, N, Ho, Wo, C, s, top, left, Hd, Wd, (uint2 *)out);
     return last();
+}
+
+int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd, int Wd,
+                        float *out, void *stream) {
+    return bev_dilate_nhwc_ex(dz, 4, N, Ho, Wo, C, s, top, left, Hd, Wd, out, stream);
 }
 
 int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float *dz, int Ho, int Wo, int Co, int KH,

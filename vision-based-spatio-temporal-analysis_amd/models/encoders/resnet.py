@@ -299,6 +299,7 @@ class ResNet(nn.Module):
         self._folded = {}
         self.fuse_shortcut = True  # bottleneck conv3 + downsample as one dual-source GEMM
         self.fuse_chain = True  # bottleneck conv2 -> conv3 (+ identity) in one launch (h2 stays in LDS)
+        self.h16_blocks = True  # AMP training: bottlenecks as one node with fp16-stored inner tensors (bit-identical)
         # Inference: split the images into this many groups, each run on its own HIP stream, so the
         # HBM- / latency-bound 1x1 layers of one group overlap the MFMA-bound 3x3 layers of another (the
         # images are independent; every layer still runs as one kernel per group; bit-identical output).
@@ -437,7 +438,7 @@ class ResNet(nn.Module):
         and native backward kernels (trunk_grad.py; batch-statistics or frozen BN per module mode).  No
         bottleneck-tail fusion in the forward; in the backward an identity block's shortcut gradient is added in its
         first conv's dgrad epilogue (trunk_grad.GradSink), a downsample block's is a separate conv backward."""
-        from .trunk_grad import GradSink, MaxPool, conv_bn_act
+        from .trunk_grad import BottleneckTrainH16, GradSink, MaxPool, bottleneck_h16_ok, conv_bn_act
         y = conv_bn_act(self.conv1, self.bn1, x, relu=True, in_nchw=True)
         if out_index == 0:
             return y
@@ -447,6 +448,11 @@ class ResNet(nn.Module):
                 sc = y
                 if blk.downsample is not None:
                     sc = conv_bn_act(blk.downsample[0], blk.downsample[1], y, relu=False)
+                if self.h16_blocks and bottleneck_h16_ok(blk):  # AMP: one node, fp16-stored inner tensors
+                    y = BottleneckTrainH16.apply(y, None if blk.downsample is None else sc, blk.conv1.weight,
+                                                 blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
+                                                 blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, blk)
+                    continue
                 chain = blk.convs()
                 # identity shortcut: the residual's gradient goes to the first conv's dgrad epilogue (GradSink)
                 sink = GradSink() if blk.downsample is None else None

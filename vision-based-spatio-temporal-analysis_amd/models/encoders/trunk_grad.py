@@ -272,6 +272,98 @@ class SqueezeExcite(torch.autograd.Function):
         return dy, dw1, db1, dw2, db2
 
 
+def _dgrad_h16(dz: torch.Tensor, wf: torch.Tensor, H: int, W: int, stride: int, pad: int,
+               residual: torch.Tensor = None) -> torch.Tensor:
+    """_dgrad under autocast with dz stored in fp16 (the fp16 conv rounds it to exactly these values)."""
+    Co, Ci, K, _ = wf.shape
+    packed = _nat.pack_conv_weight(wf.flip(2, 3).transpose(0, 1).contiguous())
+    q = K - 1 - pad
+    if stride == 1:
+        return _nat.conv2d_h16_any(dz, packed, Ci, K, K, 1, q, residual=residual)
+    N, Ho, Wo, _ = dz.shape
+    ry, rx = (H + 2 * pad - K) % stride, (W + 2 * pad - K) % stride
+    Hd, Wd = stride * (Ho - 1) + 1 + 2 * q + ry, stride * (Wo - 1) + 1 + 2 * q + rx
+    d = _nat.dilate_nhwc_any(dz, stride, q, q, Hd, Wd)
+    return _nat.conv2d_h16_any(d, packed, Ci, K, K, 1, 0, residual=residual)
+
+
+class BottleneckTrainH16(torch.autograd.Function):
+    """One timm Bottleneck (conv1 1x1 -> BN -> ReLU -> conv2 3x3 -> BN -> ReLU -> conv3 1x1 -> BN, + shortcut, ReLU)
+    in training with batch-statistics BN under autocast(float16), as ONE autograd node, so the tensors that live
+    between its layers can be stored in the precision their readers compute in:
+      * y1, y2 (the ReLU outputs feeding conv2 / conv3) are read only by the fp16 convs and their weight gradients,
+        which round them to fp16 -- stored in fp16 (`batchnorm_apply_half`);
+      * dz1..dz3 (BN backward outputs) are read only by the fp16 dgrad convs and weight gradients -- fp16
+        (`batchnorm_bwd_half`);
+    both are exactly the values the fp32-stored path rounds them to, so every result is bit-identical to the
+    per-layer `ConvBNTrain` chain (`tests/test_train_amp_gpu.py::test_bottleneck_h16_block_bit_identical`), with
+    half the bytes on those tensors.  The statistics come from the conv epilogues, the ReLU masks of y1 / y2 from
+    z, and an identity shortcut's gradient is added in conv1's dgrad epilogue.  `sc`: the shortcut tensor (the
+    downsample branch's output), or None for the identity (x)."""
+
+    @staticmethod
+    @_nat.amp_fwd
+    def forward(ctx, x, sc, w1, g1, b1, w2, g2, b2, w3, g3, b3, blk):
+        assert _nat.half_convs()
+        layers = ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2), (blk.conv3, blk.bn3))
+        ws = (w1, w2, w3)
+        gb = ((g1, b1), (g2, b2), (g3, b3))
+        h = x
+        saved, meta = [], []
+        for i, ((conv, bn), w, (g, b)) in enumerate(zip(layers, ws, gb)):
+            k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+            wd = w.detach().float().contiguous()
+            Co = conv.out_channels
+            z, tiles = _nat.conv2d_h16_any(h, _nat.pack_conv_weight(wd), Co, k, k, st, p, stats=True)
+            mean, rstd, scale, shift, _ = _bn_affine(bn, z, g, b, tiles)
+            if i < 2:
+                y = _nat.batchnorm_apply_half(z, scale, shift, 1)
+            else:
+                y = _nat.batchnorm_apply(z, scale, shift, x if sc is None else sc, 1)
+            saved += [h, z, wd, mean, rstd, g, scale, shift]
+            meta.append((k, st, p))
+            h = y
+        ctx.save_for_backward(*saved, h)
+        ctx.meta = (meta, sc is not None)
+        return h
+
+    @staticmethod
+    @_nat.amp_bwd
+    def backward(ctx, dy):
+        t = ctx.saved_tensors
+        meta, has_sc = ctx.meta
+        y3 = t[24]
+        g = dy.contiguous().float()
+        grads = [None] * 3
+        dres = None
+        for i in (2, 1, 0):
+            h, z, wd, mean, rstd, gamma, scale, shift = t[8 * i: 8 * i + 8]
+            k, st, p = meta[i]
+            if i == 2:
+                dz, dres, dgm, dbt = _nat.batchnorm_bwd_half(g, y3, z, mean, rstd, gamma, True, 1, scale, shift)
+            else:
+                dz, _, dgm, dbt = _nat.batchnorm_bwd_half(g, None, z, mean, rstd, gamma, False,
+                                                          _nat.ACT_RELU_FROM_Z, scale, shift)
+            dw = _nat.conv_wgrad_h16_any(h, dz, k, k, st, p)
+            res = dres if (i == 0 and not has_sc) else None
+            need = i > 0 or ctx.needs_input_grad[0]
+            g = _dgrad_h16(dz, wd, h.shape[1], h.shape[2], st, p, residual=res) if need else None
+            grads[i] = (dw, dgm, dbt)
+        dx = g
+        return (dx, dres if has_sc else None, *grads[0], *grads[1], *grads[2], None)
+
+
+def bottleneck_h16_ok(blk) -> bool:
+    """The BottleneckTrainH16 node applies: a 3-conv bottleneck, every BN in training mode, AMP fp16 convs active,
+    channel counts the fp16-operand kernels take (Ci % 64), no dilation."""
+    if not _nat.amp_half_active() or not hasattr(blk, "conv3"):
+        return False
+    convs = (blk.conv1, blk.conv2, blk.conv3)
+    return (all(bn.training for bn in (blk.bn1, blk.bn2, blk.bn3))
+            and all(c.in_channels % 64 == 0 and c.dilation[0] == 1 and c.groups == 1 and c.bias is None
+                    for c in convs))
+
+
 def conv_bn_act(conv: nn.Conv2d, bn: nn.BatchNorm2d, x, relu: bool, residual=None, in_nchw: bool = False,
                 sink_in: GradSink = None, sink_out: GradSink = None):
     """One ResNet layer in training: batch-statistics BN when `bn.training`, else the folded frozen BN.  sink_out
