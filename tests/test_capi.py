@@ -90,7 +90,7 @@ def test_tune_knobs_host_only(lib):
                             (nat.TUNE_WARP_BWD_POOL, 96, 1 << 20),
                             (nat.TUNE_CONV_XCD, 0, 2), (nat.TUNE_CONV_NBUF, 1, 3), (nat.TUNE_CONV_DMA, 2, 3),
                             (nat.TUNE_WGRAD_MFMA, 0, 3), (nat.TUNE_CONV_X6_TILE, 2, 3),
-                            (nat.TUNE_CONV_X6_KERNEL, 1, 3), (nat.TUNE_CONV_H16_KERNEL, 1, 3),
+                            (nat.TUNE_CONV_X6_KERNEL, 1, 3), (nat.TUNE_CONV_H16_KERNEL, 1, 4),
                             (nat.TUNE_CONV_PW_SMALL, 0, 5),
                             (nat.TUNE_DW_RUN, 1, 4)):
         old = lib.bev_tune(knob, good)

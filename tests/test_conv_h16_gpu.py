@@ -76,7 +76,8 @@ def test_conv_h16_vs_float64_of_rounded_operands(shape):
                                             (256, 1, 1, 40), (128, 3, 2, 64)])
 def test_conv_h16_kernels_bit_identical(Ci, K, stride, Co):
     """The 64-deep-step kernel (default for Ci % 64 == 0; 64-column tiles when Co <= 64), the same with 128-column
-    tiles always (CONV_H16_KERNEL 2) and the 32-deep one (1) sum every output in the same order; and fp16-stored
+    tiles always (CONV_H16_KERNEL 2) or 64-column tiles always (3), and the 32-deep one (1) sum every output in the
+    same order; and fp16-stored
     operands (bev_conv2d_h16_ex_f32 x_half) give the same bits as the fp32 operand they round."""
     import bev_native as nat
     g = torch.Generator().manual_seed(Ci + Co)
@@ -87,11 +88,11 @@ def test_conv_h16_kernels_bit_identical(Ci, K, stride, Co):
     with nat._half_mode(True):
         packed = nat.pack_conv_weight(w)
     outs = []
-    for kern in (0, 1, 2):
+    for kern in (0, 1, 2, 3):
         with nat.tuned(CONV_H16_KERNEL=kern):
             outs.append(nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, stride, K // 2, 1, 1))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
     # fp16-stored operand (the conv_h16_any path), default and 128-column kernels, against the fp32 operand
     z0 = nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, stride, K // 2, 1, 0)
     for kern in (0, 2):

@@ -31,9 +31,13 @@ def main():
     ap.add_argument("--backbone", default="resnet50")
     ap.add_argument("--amp", action="store_true")
     ap.add_argument("--fp32-kernels", action="store_true")
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=V", help="bev_tune knob (A/B); repeatable")
     a = ap.parse_args()
     import bev_native
     bev_native.AMP_HALF_CONVS = not a.fp32_kernels
+    for kv in a.tune:
+        name, v = kv.split("=")
+        bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))
     scaler = torch.amp.GradScaler("cuda") if a.amp else None
     dev = torch.device("cuda:0")
     V, H, W = 7, 1080, 1920
@@ -98,6 +102,7 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     print(json.dumps({"what": "bevnet train step" if a.bevnet else "hot-path train step", "backbone": a.backbone,
+                      "tune": a.tune,
                       "amp": a.amp, "half_convs": a.amp and not a.fp32_kernels,
                       "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
                       "loss": float(loss)}), flush=True)

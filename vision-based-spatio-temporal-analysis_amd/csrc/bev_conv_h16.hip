@@ -757,7 +757,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
 
 namespace bev {
 int conv_h16_tune(int value) {
-    if (value < 0 || value > 2) return BEV_ERR_ARGS;
+    if (value < 0 || value > 3) return BEV_ERR_ARGS;
     const int old = g_h16_kernel;
     g_h16_kernel = value;
     return old;
@@ -853,8 +853,9 @@ static int conv_h16(const void *xv, int x_half, int N, int H, int W, int Ci, con
     a.dil = dilation, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = ldy;
     a.Kp = (int)kpad_h(Ci * KH * KW);
     a.M = (int64_t)N * Ho * Wo;
-    const bool n64 = wide && Co <= 64 && g_h16_kernel != 2;  // 2: the 128-column tile always (A/B, same results)
-    const int64_t blocks = ((a.M + HBM - 1) / HBM) * (n64 ? 1 : (Co + HBN - 1) / HBN);
+    // 64-column tiles for Co <= 64 (2: the 128-column tile always; 3: 64-column tiles always -- A/B, same results)
+    const bool n64 = wide && ((Co <= 64 && g_h16_kernel != 2) || g_h16_kernel == 3);
+    const int64_t blocks = ((a.M + HBM - 1) / HBM) * (n64 ? (Co + 63) / 64 : (Co + HBN - 1) / HBN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
     const dim3 g((unsigned)blocks), b(256);
     hipStream_t st = (hipStream_t)stream;
