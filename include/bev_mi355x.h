@@ -476,11 +476,21 @@ int bev_groupnorm_fwd_f32(const float *x, int N, int64_t P, int C, int G, float 
 int bev_groupnorm_apply_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift, int relu,
                             float *y, void *stream);
 
+/* bev_groupnorm_apply_f32 with y stored in fp16 when y_half = 1 (an output read only by fp16-operand convs, which
+ * round it to exactly these values). */
+int bev_groupnorm_apply_ex_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift,
+                               int relu, void *y, int y_half, void *stream);
+
 /* device: backward of y = relu?(groupnorm(x)) (the forward's mean, rstd, scale, shift): dx [N][P][C],
  * dgamma, dbeta [C], all OVERWRITTEN. */
 int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
                           const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
                           float *dx, float *dgamma, float *dbeta, void *workspace, void *stream);
+
+/* bev_groupnorm_bwd_f32 with dx stored in fp16 when dx_half = 1 (read only by the fp16 dgrad / weight gradient). */
+int bev_groupnorm_bwd_ex_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
+                             const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
+                             void *dx, int dx_half, float *dgamma, float *dbeta, void *workspace, void *stream);
 
 /* ---------------------------------------------------------------------------
  * BatchNorm with batch statistics (training the trunk in model.train(), reference train.py:222;

@@ -208,6 +208,7 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
 
     trunk_masks, head_masks = [], []
     bn_apply, bn_apply_half, gn_apply = nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply
+    gn_apply_half = nat.groupnorm_apply_half
 
     def rec_bn(z, scale, shift, residual=None, act=0):
         out = bn_apply(z, scale, shift, residual, act)
@@ -227,7 +228,15 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
             head_masks.append((out > 0).permute(0, 3, 1, 2).double().cpu())
         return out
 
+    def rec_gn_half(x, scale, shift, relu):  # fp16-stored output: the fp32 decision x * s + h > 0 (two roundings)
+        out = gn_apply_half(x, scale, shift, relu)
+        if relu:
+            u = x * scale[:, None, None, :] + shift[:, None, None, :]
+            head_masks.append((u > 0).permute(0, 3, 1, 2).double().cpu())
+        return out
+
     nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = rec_bn, rec_bn_half, rec_gn
+    nat.groupnorm_apply_half = rec_gn_half
     scaler = torch.amp.GradScaler("cuda") if amp else None
     try:
         model.zero_grad(set_to_none=True)
@@ -242,6 +251,7 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
             losses["total_loss"].backward()
     finally:
         nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = bn_apply, bn_apply_half, gn_apply
+        nat.groupnorm_apply_half = gn_apply_half
     if amp:
         opt = torch.optim.SGD(model.parameters(), lr=0.0)
         scaler.unscale_(opt)
@@ -373,6 +383,46 @@ def test_bottleneck_h16_block_bit_identical():
     assert n_bn > 40 and n_conv > 20
     for k in b0:
         assert torch.equal(b0[k], b1[k]), k
+
+
+@pytest.mark.timeout(300)
+def test_head_h16_node_bit_identical():
+    """BEVDetector training under autocast with the head as one _HeadTrainH16 node (fp16-stored GroupNorm + ReLU
+    outputs and GroupNorm backward outputs) vs the per-layer _HeadConv / _GroupNormReLU chain (fp32-stored): the five
+    outputs, the input gradient and the GroupNorm parameter gradients bit-identical; conv weight / bias gradients
+    (float atomics) to fp32 summation noise.  in_channels 66 (operand padded to 96 channels), dilation 2 in the
+    middle conv, B = 2."""
+    from models.heads.detector import BEVDetector
+    torch.manual_seed(11)
+    head = BEVDetector(in_channels=66, bev_bounds=(-6.0, 6.0, -2.0, 2.0), bev_size=(48, 88)).to(DEV)
+    with torch.no_grad():  # non-trivial GroupNorm affines and head weights
+        for n, p in head.named_parameters():
+            if "stem.1" in n or "stem.4" in n or "stem.7" in n or "offset_head.weight" in n:
+                p.add_(torch.randn(p.shape, device=DEV) * 0.1)
+    x0 = torch.randn(2, 66, 48, 88, device=DEV)
+    g = [torch.randn(2, c, 48, 88, device=DEV, generator=torch.Generator(device=DEV).manual_seed(c)) for c in (1, 2, 2)]
+    results = []
+    for node in (False, True):
+        head.h16_node = node
+        head.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        with _autocast():
+            out = head(x)
+        loss = sum((out[k].float() * gk).sum() for k, gk in zip(("heatmap_logits", "offset_raw", "size_raw"), g))
+        loss.backward()
+        results.append(({k: v.detach().float().clone() for k, v in out.items()}, x.grad.detach().clone(),
+                        {k: p.grad.detach().clone() for k, p in head.named_parameters()}))
+    head.h16_node = True
+    (o0, gx0, gr0), (o1, gx1, gr1) = results
+    for k in o0:
+        assert torch.equal(o0[k], o1[k]), k
+    assert torch.equal(gx0, gx1)
+    for k in gr0:
+        if k.startswith("stem.1") or k.startswith("stem.4") or k.startswith("stem.7"):  # GroupNorm gamma / beta
+            assert torch.equal(gr0[k], gr1[k]), k
+        else:
+            scale = float(gr0[k].abs().max())
+            assert float((gr0[k] - gr1[k]).abs().max()) <= 2e-6 * scale + 1e-30, k
 
 
 def _free_port():

@@ -109,6 +109,9 @@ SIGNATURES = {
     "bev_batchnorm_bwd_ex_f32": (_i, [_vp, _vp, _vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _vp, _vp, _vp,
                                       _vp, _vp]),
     "bev_dilate_nhwc_ex": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_groupnorm_apply_ex_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp, _i, _vp, _i, _vp]),
+    "bev_groupnorm_bwd_ex_f32": (_i, [_vp, _vp, _i, _i64, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp,
+                                      _vp]),
     "bev_conv2d_h16_bnstats_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_batchnorm_finalize_tiles_f32": (_i, [_vp, _i, _i, _i64, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                                _vp]),
@@ -659,7 +662,7 @@ def _require_gpu_h(*ts):
 
 
 def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: int, stride: int, pad: int,
-                   stats: bool = False, residual: torch.Tensor = None, bias: torch.Tensor = None):
+                   stats: bool = False, residual: torch.Tensor = None, bias: torch.Tensor = None, dilation: int = 1):
     """The autocast fp16 conv with x [N,H,W,Ci] stored in fp32 or fp16 (Ci % 64 == 0 for fp16) -> z fp32
     [N,Ho,Wo,Co] (+ residual), and with `stats` the BatchNorm tile partials (conv2d_nhwc_h16_bnstats)."""
     x = x.contiguous()
@@ -668,7 +671,8 @@ def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: 
     if not packed.is_cuda or packed.dtype != torch.float16:
         raise HipError("conv2d_h16_any needs the fp16 weight panel on the device")
     N, H, W, Ci = x.shape
-    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    Ho = (H + 2 * pad - dilation * (KH - 1) - 1) // stride + 1
+    Wo = (W + 2 * pad - dilation * (KW - 1) - 1) // stride + 1
     z = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
     tiles = None
     if stats:
@@ -679,13 +683,14 @@ def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: 
         residual = residual.contiguous()
     with _span("conv", x):
         rc = lib().bev_conv2d_h16_ex_f32(_ptr(x), int(x.dtype == torch.float16), N, H, W, Ci, _ptr(packed),
-                                         _ptr(bias), _ptr(residual), Co, KH, KW, stride, pad, 1, 0, _ptr(z), Co, Ho,
-                                         Wo, _ptr(tiles), _stream(x))
+                                         _ptr(bias), _ptr(residual), Co, KH, KW, stride, pad, dilation, 0, _ptr(z), Co,
+                                         Ho, Wo, _ptr(tiles), _stream(x))
     _check(rc, "bev_conv2d_h16_ex_f32")
     return (z, tiles) if stats else z
 
 
-def conv_wgrad_h16_any(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stride: int, pad: int) -> torch.Tensor:
+def conv_wgrad_h16_any(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stride: int, pad: int,
+                       dilation: int = 1) -> torch.Tensor:
     """The autocast weight gradient with x / dz stored in fp32 or fp16 (Ci, Co % 4 == 0) -> dW [Co, Ci, KH, KW]."""
     x, dz = x.contiguous(), dz.contiguous()
     _require_gpu_h(x, dz)
@@ -693,7 +698,7 @@ def conv_wgrad_h16_any(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stri
     _, Ho, Wo, Co = dz.shape
     dW = torch.empty(Co, KH, KW, Ci, device=x.device, dtype=torch.float32)
     _check(lib().bev_conv_wgrad_h16_ex_f32(_ptr(x), int(x.dtype == torch.float16), N, H, W, Ci, _ptr(dz),
-                                           int(dz.dtype == torch.float16), Ho, Wo, Co, KH, KW, stride, pad, 1,
+                                           int(dz.dtype == torch.float16), Ho, Wo, Co, KH, KW, stride, pad, dilation,
                                            _ptr(dW), _stream(x)), "bev_conv_wgrad_h16_ex_f32")
     return dW.permute(0, 3, 1, 2).contiguous()
 
@@ -737,6 +742,34 @@ def batchnorm_bwd_half(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, 
                                           int(frozen), _ptr(dz), 1, _ptr(dres), _ptr(dg), _ptr(db), _ptr(ws),
                                           _stream(z)), "bev_batchnorm_bwd_ex_f32")
     return dz, dres, dg, db
+
+
+def groupnorm_apply_half(x: torch.Tensor, scale, shift, relu: bool) -> torch.Tensor:
+    """groupnorm_apply with the output stored in fp16 (read only by the next fp16 conv and its weight gradient)."""
+    _require_gpu(x, scale, shift)
+    assert x.is_contiguous()
+    N, C = x.shape[0], x.shape[-1]
+    y = torch.empty(x.shape, device=x.device, dtype=torch.float16)
+    _check(lib().bev_groupnorm_apply_ex_f32(_ptr(x), N, x.numel() // (N * C), C, _ptr(scale), _ptr(shift), int(relu),
+                                            _ptr(y), 1, _stream(x)), "bev_groupnorm_apply_ex_f32")
+    return y
+
+
+def groupnorm_bwd_half(x: torch.Tensor, dy: torch.Tensor, G: int, mean, rstd, gamma, scale, shift, relu: bool):
+    """groupnorm_bwd with dx stored in fp16 (read only by the conv's fp16 dgrad and weight gradient)."""
+    x, dy = x.contiguous(), dy.contiguous().float()
+    _require_gpu(x, dy, mean, rstd, gamma, scale, shift)
+    N, C = x.shape[0], x.shape[-1]
+    P = x.numel() // (N * C)
+    dx = torch.empty(x.shape, device=x.device, dtype=torch.float16)
+    dg = torch.empty(C, device=x.device)
+    db = torch.empty(C, device=x.device)
+    ws = _gn_workspace(N, P, C, G, x.device)
+    _check(lib().bev_groupnorm_bwd_ex_f32(_ptr(x), _ptr(dy), N, P, C, G, _ptr(mean), _ptr(rstd),
+                                          _ptr(gamma.detach().contiguous()), _ptr(scale), _ptr(shift), int(relu),
+                                          _ptr(dx), 1, _ptr(dg), _ptr(db), _ptr(ws), _stream(x)),
+           "bev_groupnorm_bwd_ex_f32")
+    return dx, dg, db
 
 
 def batchnorm_finalize_tiles(tiles: torch.Tensor, M: int, gamma, beta, running_mean, running_var, eps: float,

@@ -86,8 +86,16 @@ __global__ void k_gn_finalize(const double *__restrict__ part, int nb, int64_t P
     }
 }
 
+// 4 values out: fp32, or fp16 (RNE) for an output read only by fp16-operand kernels (bit-identical to their rounding)
+__device__ __forceinline__ void gn_st4(float *p, int64_t e, float4 o) { *(float4 *)(p + e) = o; }
+__device__ __forceinline__ void gn_st4(_Float16 *p, int64_t e, float4 o) {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    *(h4 *)(p + e) = (h4){(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
+}
+
+template <typename OT>
 __global__ void k_gn_apply(const float *__restrict__ x, int64_t P, int C, const float *__restrict__ scale,
-                           const float *__restrict__ shift, int relu, float *__restrict__ y, int64_t total4) {
+                           const float *__restrict__ shift, int relu, OT *__restrict__ y, int64_t total4) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e = 4 * i;
         const int c = (int)(e % C);
@@ -96,7 +104,7 @@ __global__ void k_gn_apply(const float *__restrict__ x, int64_t P, int C, const 
         const float4 s = *(const float4 *)(scale + (size_t)n * C + c), h = *(const float4 *)(shift + (size_t)n * C + c);
         float4 o = make_float4(v.x * s.x + h.x, v.y * s.y + h.y, v.z * s.z + h.z, v.w * s.w + h.w);
         if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
-        *(float4 *)(y + e) = o;
+        gn_st4(y, e, o);
     }
 }
 
@@ -201,11 +209,12 @@ __global__ void k_gn_bwd_finalize(const double *__restrict__ part, const double 
     }
 }
 
+template <typename OT>
 __global__ void k_gn_bwd_apply(const float *__restrict__ x, const float *__restrict__ dy, int64_t P, int C, int G,
                                const float *__restrict__ mean, const float *__restrict__ rstd,
                                const float *__restrict__ gamma, const float *__restrict__ scale,
                                const float *__restrict__ shift, int relu, const float *__restrict__ coef,
-                               float *__restrict__ dx, int64_t total4) {
+                               OT *__restrict__ dx, int64_t total4) {
     const int cpg = C / G;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e = 4 * i;
@@ -223,7 +232,7 @@ __global__ void k_gn_bwd_apply(const float *__restrict__ x, const float *__restr
             const float xh = (xv[u] - mean[ng]) * rstd[ng];
             o[u] = rstd[ng] * (gr * gamma[c] - coef[2 * ng] - xh * coef[2 * ng + 1]);
         }
-        *(float4 *)(dx + e) = make_float4(o[0], o[1], o[2], o[3]);
+        gn_st4(dx, e, make_float4(o[0], o[1], o[2], o[3]));
     }
 }
 
@@ -259,20 +268,29 @@ int bev_groupnorm_fwd_f32(const float *x, int N, int64_t P, int C, int G, float 
     return (int)hipGetLastError();
 }
 
-int bev_groupnorm_apply_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift, int relu,
-                            float *y, void *stream) {
+int bev_groupnorm_apply_ex_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift,
+                               int relu, void *y, int y_half, void *stream) {
     if (!x || !scale || !shift || !y || N <= 0 || P <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
     const int64_t total4 = (int64_t)N * P * C / 4;
     int64_t blocks = (total4 + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_gn_apply, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, P, C, scale, shift,
-                       relu, y, total4);
+    if (y_half)
+        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, P, C,
+                           scale, shift, relu, (_Float16 *)y, total4);
+    else
+        hipLaunchKernelGGL(k_gn_apply<float>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, P, C, scale,
+                           shift, relu, (float *)y, total4);
     return (int)hipGetLastError();
 }
 
-int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
-                          const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
-                          float *dx, float *dgamma, float *dbeta, void *workspace, void *stream) {
+int bev_groupnorm_apply_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift, int relu,
+                            float *y, void *stream) {
+    return bev_groupnorm_apply_ex_f32(x, N, P, C, scale, shift, relu, y, 0, stream);
+}
+
+int bev_groupnorm_bwd_ex_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
+                             const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
+                             void *dx, int dx_half, float *dgamma, float *dbeta, void *workspace, void *stream) {
     if (!x || !dy || !mean || !rstd || !gamma || !scale || !shift || !dx || !dgamma || !dbeta || !workspace ||
         !gn_shape_ok(N, P, C, G))
         return BEV_ERR_ARGS;
@@ -290,9 +308,20 @@ int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int
     const int64_t total4 = (int64_t)N * P * C / 4;
     int64_t blocks = (total4 + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(k_gn_bwd_apply, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, P, C, G, mean, rstd, gamma,
-                       scale, shift, relu, coef, dx, total4);
+    if (dx_half)
+        hipLaunchKernelGGL(k_gn_bwd_apply<_Float16>, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, P, C, G, mean,
+                           rstd, gamma, scale, shift, relu, coef, (_Float16 *)dx, total4);
+    else
+        hipLaunchKernelGGL(k_gn_bwd_apply<float>, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, P, C, G, mean, rstd,
+                           gamma, scale, shift, relu, coef, (float *)dx, total4);
     return (int)hipGetLastError();
+}
+
+int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int C, int G, const float *mean,
+                          const float *rstd, const float *gamma, const float *scale, const float *shift, int relu,
+                          float *dx, float *dgamma, float *dbeta, void *workspace, void *stream) {
+    return bev_groupnorm_bwd_ex_f32(x, dy, N, P, C, G, mean, rstd, gamma, scale, shift, relu, dx, 0, dgamma, dbeta,
+                                    workspace, stream);
 }
 
 }  // extern "C"

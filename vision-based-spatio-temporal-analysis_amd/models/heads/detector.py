@@ -112,6 +112,86 @@ class _GroupNormReLU(torch.autograd.Function):
         return dz, dg, db, None
 
 
+class _HeadTrainH16(torch.autograd.Function):
+    """The whole training head under autocast(float16) as ONE autograd node: 3 x [conv -> GroupNorm -> ReLU] -> the
+    heads conv, with the tensors that live between its layers stored in the precision their readers compute in --
+    each GroupNorm + ReLU output (read only by the next fp16 conv and its weight gradient) and each GroupNorm
+    backward output (read only by its conv's fp16 dgrad and weight gradient) in fp16: exactly the values the
+    fp32-stored per-layer path (_HeadConv / _GroupNormReLU) rounds them to, so every result is bit-identical to it
+    (`tests/test_train_amp_gpu.py::test_head_h16_node_bit_identical`) with half the bytes on those tensors."""
+
+    @staticmethod
+    @_nat.amp_fwd
+    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wh, bh, head):
+        assert _nat.half_convs()
+        convs, gns = head._convs()
+        ws, gbs = (w1, w2, w3), ((g1, b1), (g2, b2), (g3, b3))
+        a = x
+        saved, meta = [], []
+        for i, (conv, gn) in enumerate(zip(convs, gns)):
+            Co, Ci, K, _ = ws[i].shape
+            cp = a.shape[-1]
+            w = ws[i].detach().float()
+            if cp > Ci:
+                w = F.pad(w, (0, 0, 0, 0, 0, cp - Ci))
+            w = w.contiguous()
+            dil = conv.dilation[0]
+            pad = dil * (K // 2)
+            packed = _nat.pack_conv_weight(w)
+            if a.dtype == torch.float16:
+                z = _nat.conv2d_h16_any(a, packed, Co, K, K, 1, pad, dilation=dil)
+            else:
+                z = _nat.conv2d_nhwc_ex(a, packed, torch.zeros(Co, device=a.device), Co, K, pad, dil)
+            g, b = gbs[i]
+            mean, rstd, scale, shift = _nat.groupnorm_fwd(z, _GROUPS, g, b, gn.eps)
+            saved += [a, w, z, g, mean, rstd, scale, shift]
+            meta.append((dil, Ci))
+            a = _nat.groupnorm_apply_half(z, scale, shift, True)
+        w = wh.detach().float().contiguous()
+        bb = bh.detach().float().contiguous()
+        y = _nat.conv2d_h16_any(a, _nat.pack_conv_weight(w), w.shape[0], 3, 3, 1, 1, bias=bb)
+        ctx.save_for_backward(*saved, a, w)
+        ctx.meta = meta
+        return y
+
+    @staticmethod
+    @_nat.amp_bwd
+    def backward(ctx, dy):
+        t = ctx.saved_tensors
+        a3, wh = t[24], t[25]
+        dy = dy.contiguous().float()
+        Co_h, cp, K, _ = wh.shape
+        # heads conv: colsum bias gradient, dgrad on the fp32 gradient, weight gradient (output channels padded to 4)
+        dbh = _nat.colsum(dy)
+        dyp = F.pad(dy, (0, (-Co_h) % 4)).contiguous()
+        dwh = _nat.conv_wgrad_h16_any(a3, dyp, K, K, 1, 1)[:Co_h]
+        wt = wh.flip(2, 3).transpose(0, 1).contiguous()
+        da = _nat.conv2d_nhwc_ex(dy, _nat.pack_conv_weight(wt), torch.zeros(cp, device=dy.device), cp, K, 1, 1)
+        grads = [None] * 3
+        for i in (2, 1, 0):
+            a, w, z, g, mean, rstd, scale, shift = t[8 * i: 8 * i + 8]
+            dil, Ci = ctx.meta[i]
+            Co, cpi, K, _ = w.shape
+            pad = dil * (K // 2)
+            dz, dg, db = _nat.groupnorm_bwd_half(z, da, _GROUPS, mean, rstd, g, scale, shift, True)
+            dw = _nat.conv_wgrad_h16_any(a, dz, K, K, 1, pad, dil)[:, :Ci]
+            if i > 0 or ctx.needs_input_grad[0]:
+                wt = w.flip(2, 3).transpose(0, 1).contiguous()
+                da = _nat.conv2d_h16_any(dz, _nat.pack_conv_weight(wt), cpi, K, K, 1, pad, dilation=dil)
+            else:
+                da = None
+            grads[i] = (dw, dg, db)
+        return (da, *grads[0], *grads[1], *grads[2], dwh, dbh, None)
+
+
+def _head_h16_ok(head) -> bool:
+    """_HeadTrainH16 applies: AMP fp16 convs active and the layers' channels fit the fp16-operand kernels."""
+    if not _nat.amp_half_active():
+        return False
+    convs, _ = head._convs()
+    return all(c.out_channels % 64 == 0 for c in convs) and head.input_channels_padded % 32 == 0
+
+
 class BEVDetector(nn.Module):
     def __init__(self, in_channels: int = 32, bev_bounds: Tuple[float, float, float, float] = (-6.0, 6.0, -2.0, 2.0),
                  bev_size: Tuple[int, int] = (64, 64), default_box_wh: Tuple[float, float] = (0.6, 0.6)):
@@ -137,6 +217,7 @@ class BEVDetector(nn.Module):
         with torch.no_grad():
             self.size_head.bias.copy_(torch.log(torch.tensor(cells, dtype=torch.float32)))
         self._panels = [_Packed() for _ in range(3)]
+        self.h16_node = True  # AMP training: the head as one node with fp16-stored inner tensors (bit-identical)
 
     # ---- layout helpers -----------------------------------------------------------------------
     @property
@@ -165,7 +246,12 @@ class BEVDetector(nn.Module):
         """x [B, H, W, input_channels_padded] NHWC (channels >= in_channels zero)."""
         convs, gns = self._convs()
         train = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
-        if train:
+        if train and self.h16_node and _head_h16_ok(self):  # AMP: one node, fp16-stored inner tensors (bit-identical)
+            w, b = self._head_params()
+            (c1, c2, c3), (n1, n2, n3) = convs, gns
+            y = _HeadTrainH16.apply(x, c1.weight, n1.weight, n1.bias, c2.weight, n2.weight, n2.bias, c3.weight,
+                                    n3.weight, n3.bias, w, b, self)
+        elif train:
             a = x
             for conv, gn in zip(convs, gns):
                 z = _HeadConv.apply(a, conv.weight, None, conv.dilation[0])
