@@ -672,6 +672,8 @@ def test_effnet_trunk_backward_vs_torch_autograd(name, bn_mode):
         assert k in got, k
         errs[k] = (got[k].double() - p.grad).abs().max().item() / max(p.grad.abs().max().item(), floor)
     assert len(errs) > 30
+    worst = sorted(errs.items(), key=lambda t: -t[1])[:3]
+    print(f"effnet trunk gradient worst relative errors ({name}, {bn_mode}): {worst}")
     assert max(errs.values()) < 1e-3, sorted(errs.items(), key=lambda t: -t[1])[:6]
     moved = 0
     for k, b in enc_c.named_buffers():

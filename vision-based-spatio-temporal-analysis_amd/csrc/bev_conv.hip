@@ -1380,7 +1380,8 @@ __global__ __launch_bounds__(256) void k_pw_mfma(ConvArgs a) {
 // BEV_TUNE_CONV_PW_SMALL: 2 (default) = narrow outputs (Co <= 32) only, 3 = every tiny-K 1x1 layer, 4 = narrow only
 // with the dword epilogue.  3 is faster for inference but not the default: its k order on the wide expansions
 // moves one EfficientNet-B0 training gradient (test_effnet_trunk_backward_vs_torch_autograd, blocks.0.0.bn2.bias)
-// to 1.007e-3 relative against float64 autograd, past the test's 1e-3 bound (r03q).  r03p micro (profiles/r03p_pw_mfma_vec_ab.txt, 7 x 1080p, us; tiles -> dword epilogue ->
+// to 1.007e-3 relative against float64 autograd, past the test's 1e-3 bound (r03q); the default path's worst in that
+// test is 5.74e-4 (b0, batch statistics: blocks.0.0.bn2.bias; b3 5.06e-4; frozen BN ~1e-6; gpurun_out r04t, round 4).  r03p micro (profiles/r03p_pw_mfma_vec_ab.txt, 7 x 1080p, us; tiles -> dword epilogue ->
 // float4 epilogue): 40 -> 24 420 -> 344 -> 270, 24 -> 24 + residual 337 -> 294 -> 223, 24 -> 144 927 -> (921) -> 747,
 // 32 -> 192 287 -> 242.  (r03j: with the dword epilogue the wide expansions were within +-5 % of the tiles, and each
 // residual load waited behind the previous store until all 16 were issued first.)

@@ -68,7 +68,13 @@ __device__ __forceinline__ void cell_ixy(const float h[9], float x, float y, con
     // u0 / ws and u1 / ws as IEEE f32 divisions, through ONE double reciprocal of ws: rcp_f64 refined by two
     // Newton steps is within ~2^-53 of 1/ws, so (double)u0 * rws lies within 2^-51 (relative) of the exact
     // quotient, inside div_rcp's 2^-49 midpoint margin -> the same float as u0 / ws (12 VALU instead of the
-    // two 13-instruction f32 division sequences).
+    // two 13-instruction f32 division sequences).  Why the margin suffices (normal quotients): a float rounds
+    // differently only if q = u0 / ws lies within 2^-51 of a rounding midpoint m (25 significant bits, odd at that
+    // width).  q == m exactly would need u0 = m * ws, an odd 25-bit times a >= 1-bit odd significand in 24 bits:
+    // impossible; and q != m gives |q - m| = |u0 - m ws| / |ws| >= 2^-49 |q| (u0 - m ws is a nonzero multiple of
+    // the product's last bit).  Covered by the argument, not exhaustively checked: subnormal quotients (|u0|
+    // below ~1e-38 |ws|; the geometry's u0 are pixel-scale or exactly 0, and 0 * rws keeps IEEE's sign) and
+    // ws = +-inf (handled explicitly above).  |ws| >= 1e-6 by the clamp, so rws never overflows.
     const double wd = (double)ws;
     double rws = __builtin_amdgcn_rcp(wd);
     rws = __builtin_fma(rws, __builtin_fma(-wd, rws, 1.0), rws);
