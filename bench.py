@@ -87,6 +87,10 @@ def parse():
     ap.add_argument("--warp-kernel", choices=("dma", "register", "rows"), default="dma",
                     help="fused warp kernel (bev_tune BEV_TUNE_WARP_KERNEL; A/B only, same results): dma = "
                          "k_warp_fuse_v2 (default), register = k_warp_fuse, rows = k_warp_fuse_v3")
+    ap.add_argument("--warp-touch", choices=("none", "tlb", "full", "sleep"), default="none",
+                    help="experiment: read the encoder's features before the warp (tlb: one float per 4 KiB page, "
+                         "full: every byte) or idle the GPU ~60 us (sleep), inside the timed geometry stage; "
+                         "profiles/r04u_warp_touch_ab.txt")
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration check on the CPU (gloo): the rank spawning, barriers, timing and MAX "
                          "reduction of this script with a placeholder step (rank r sleeps (r + 1) x 5 ms); no hot "
@@ -451,6 +455,11 @@ def main():
                 feats = enc(images)
             if record:
                 e1.record(stream)
+            if args.warp_touch == "sleep":  # experiment: an idle gap (~60 us of GPU sleep) instead of a read
+                torch.cuda._sleep(150000)
+            elif args.warp_touch != "none":  # experiment (--warp-touch): warm TLB / caches for the warp's gathers
+                flat = feats.as_strided((feats.numel(),), (1,))
+                step.sink = (flat[::1024] if args.warp_touch == "tlb" else flat).sum()
             if args.camera_shard:
                 bev = bev_dist.camera_sharded_forward(geom, feats, Kd, Rtd, (H, W), V, "mean")
             else:
