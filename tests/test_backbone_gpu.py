@@ -227,6 +227,20 @@ def test_maxpool_and_layouts_exact():
     assert torch.equal(y.permute(0, 3, 1, 2).cpu(), F.max_pool2d(x, 3, 2, 1))
 
 
+@pytest.mark.parametrize("shape,k,s,p", [((2, 64, 31, 45), 3, 2, 1), ((1, 12, 17, 9), 2, 2, 0), ((3, 4, 8, 11), 3, 1, 1),
+                                         ((1, 64, 540, 960), 3, 2, 1)])
+def test_maxpool_rows_kernel_exact(shape, k, s, p):
+    """k_maxpool_rows (the float4 row-grid kernel) vs torch max_pool2d, NaNs included (torch propagates them)."""
+    import bev_native as nat
+    x = _rand(shape, 11)
+    x.view(-1)[:: 997] = float("nan")
+    y = nat.maxpool_nhwc(nat.nchw_to_nhwc(x.to(DEV)), k, s, p)
+    ref = F.max_pool2d(x, k, s, p)
+    got = y.permute(0, 3, 1, 2).cpu()
+    assert torch.equal(torch.isnan(got), torch.isnan(ref))
+    assert torch.equal(torch.nan_to_num(got, nan=7.0), torch.nan_to_num(ref, nan=7.0))
+
+
 def test_fallback_encoder_matches_reference_fixture():
     """cnn_encoder.py:31-37 (the branch the reference takes without timm) vs its recorded outputs."""
     from models.encoders.cnn_encoder import CNNEncoder

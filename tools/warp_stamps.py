@@ -58,8 +58,19 @@ def main():
         span = a[:, 4].max() - a[:, 0].min()
         print(f"{name}: {nwg} workgroups, span {span} cyc; per workgroup mean cycles: prologue {d[:, 0].mean():.0f}, "
               f"first DMA {d[:, 1].mean():.0f}, view loop {d[:, 2].mean():.0f}, store {d[:, 3].mean():.0f}, "
-              f"lifetime {life.mean():.0f} (p10 {np.percentile(life, 10):.0f}, p90 {np.percentile(life, 90):.0f}); "
-              f"sum of lifetimes / span = {life.sum() / span:.1f} concurrent", flush=True)
+              f"lifetime {life.mean():.0f} (p10 {np.percentile(life, 10):.0f}, p90 {np.percentile(life, 90):.0f})",
+              flush=True)
+        # per XCD (linear workgroup id mod 8; one s_memtime clock per XCD): its span, slot utilisation at
+        # 3 workgroups x 32 CUs, and when the last quarter / last workgroup started relative to the span
+        for x in range(8):
+            sel = np.arange(nwg) % 8 == x
+            t0, t1 = a[sel, 0].min(), a[sel, 4].max()
+            sp = t1 - t0
+            starts = np.sort(a[sel, 0] - t0)
+            ends = np.sort(a[sel, 4] - t0)
+            print(f"  xcd {x}: span {sp} cyc, busy slots {life[sel].sum() / sp:.1f} of 96, "
+                  f"start of last wg {starts[-1] / sp:.2f}, end of first wg {ends[0] / sp:.2f}, "
+                  f"75% done at {ends[int(0.75 * len(ends))] / sp:.2f}", flush=True)
 
 
 if __name__ == "__main__":
