@@ -71,7 +71,10 @@ int bev_abi_version(void);
  * BEV_TUNE_DW_RUN: depthwise convs with <= 256 channels that the LDS tile does not take: 0 = per pixel (k_dwconv),
  *   1 = row runs (k_dwconv_r), 2 = row runs with the 3 x 3 rows' loads issued up front, 3 (default) = 2 for every
  *   width (also where the LDS tile k_dwconv_t ran).  Same y up to the sign of an exact zero; the SE partial count
- *   per bev_dwconv_psum_blocks, which follows the knob. */
+ *   per bev_dwconv_psum_blocks, which follows the knob.
+ * BEV_TUNE_CONV_X6_NT: 1 = non-temporal (streaming) activation loads in the split-arithmetic 1x1 / 3x3 convs with
+ *   Co <= 64 tiles, 0 (default) = cached loads.  For the LAST reader of a large tensor: CNNEncoder sets it around its
+ *   projection so the feature maps that conv writes stay in the Infinity Cache for the warp.  Same results. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -85,6 +88,7 @@ int bev_abi_version(void);
 #define BEV_TUNE_CONV_H16_KERNEL 12
 #define BEV_TUNE_CONV_PW_SMALL 13
 #define BEV_TUNE_DW_RUN 14
+#define BEV_TUNE_CONV_X6_NT 16
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

@@ -227,6 +227,21 @@ def test_maxpool_and_layouts_exact():
     assert torch.equal(y.permute(0, 3, 1, 2).cpu(), F.max_pool2d(x, 3, 2, 1))
 
 
+def test_encoder_proj_streaming_loads_same_result():
+    """CNNEncoder's projection with non-temporal activation loads (proj_stream_nt, BEV_TUNE_CONV_X6_NT) gives the
+    same bits as with cached loads (same kernel arithmetic), at a full 1080p camera."""
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(3)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(DEV)
+    x = _rand((1, 2, 3, 1080, 1920), 4).to(DEV)
+    with torch.no_grad():
+        enc.proj_stream_nt = True
+        a = enc(x)
+        enc.proj_stream_nt = False
+        b = enc(x)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("shape,k,s,p", [((2, 64, 31, 45), 3, 2, 1), ((1, 12, 17, 9), 2, 2, 0), ((3, 4, 8, 11), 3, 1, 1),
                                          ((1, 64, 540, 960), 3, 2, 1)])
 def test_maxpool_rows_kernel_exact(shape, k, s, p):

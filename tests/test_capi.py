@@ -92,7 +92,7 @@ def test_tune_knobs_host_only(lib):
                             (nat.TUNE_WGRAD_MFMA, 0, 3), (nat.TUNE_CONV_X6_TILE, 2, 3),
                             (nat.TUNE_CONV_X6_KERNEL, 1, 3), (nat.TUNE_CONV_H16_KERNEL, 1, 4),
                             (nat.TUNE_CONV_PW_SMALL, 0, 5),
-                            (nat.TUNE_DW_RUN, 1, 4)):
+                            (nat.TUNE_DW_RUN, 1, 4), (nat.TUNE_CONV_X6_NT, 1, 2)):
         old = lib.bev_tune(knob, good)
         assert old >= 0
         assert lib.bev_tune(knob, bad) == -1

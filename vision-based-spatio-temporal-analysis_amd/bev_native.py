@@ -201,6 +201,7 @@ TUNE_CONV_X6_KERNEL = 11
 TUNE_CONV_H16_KERNEL = 12
 TUNE_CONV_PW_SMALL = 13
 TUNE_DW_RUN = 14
+TUNE_CONV_X6_NT = 16
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 

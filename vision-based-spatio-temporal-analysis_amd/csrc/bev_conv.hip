@@ -1531,7 +1531,8 @@ int bev_tune(int knob, int value) {
         return old;
     }
     if (knob == BEV_TUNE_WGRAD_MFMA) return bev::train_tune(knob, value);
-    if (knob == BEV_TUNE_CONV_X6_TILE || knob == BEV_TUNE_CONV_X6_KERNEL) return bev::conv_x6_tune(knob, value);
+    if (knob == BEV_TUNE_CONV_X6_TILE || knob == BEV_TUNE_CONV_X6_KERNEL || knob == BEV_TUNE_CONV_X6_NT)
+        return bev::conv_x6_tune(knob, value);
     if (knob == BEV_TUNE_CONV_H16_KERNEL) return bev::conv_h16_tune(value);
     if (knob == BEV_TUNE_DW_RUN) return bev::dw_tune(value);
     if (knob == BEV_TUNE_CONV_PW_SMALL) {

@@ -103,6 +103,7 @@ struct ConvX {
     const __bf16 *__restrict__ wp2;
     const float *__restrict__ bias2;
     int Co2, act2;
+    int nta = 0;  // 1: A (activation) loads non-temporal (BEV_TUNE_CONV_X6_NT, the last layer of a trunk)
 };
 
 __device__ __forceinline__ float act_x(float t, int act) {
@@ -546,7 +547,8 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
 constexpr int YBK = 32;
 constexpr int YROW = 40;
 
-template <int WM, int WN, int TM, int TN, bool DUAL, int CHAIN = 0>  // CHAIN: 0 none, 1 chain, 2 chain + shortcut
+// CHAIN: 0 none, 1 chain, 2 chain + shortcut; NT: non-temporal activation loads (BEV_TUNE_CONV_X6_NT)
+template <int WM, int WN, int TM, int TN, bool DUAL, int CHAIN = 0, bool NT = false>
 __global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int APL = BM * YROW;                 // bf16 per A plane
@@ -621,7 +623,9 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
             _Pragma("unroll") for (int q = 0; q < AQ; ++q) {                                               \
                 const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
                 const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
-                VA[q] = *(const f32x4 *)(in ? a.x + pb[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 : g_xzero4); \
+                const f32x4 *ap_ = (const f32x4 *)(in ? a.x + pb[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0 : g_xzero4); \
+                if (NT) VA[q] = __builtin_nontemporal_load(ap_);                                          \
+                else VA[q] = *ap_;                                                                        \
             }                                                                                              \
             ci0 += YBK;                                                                                    \
             if (ci0 == a.Ci) {                                                                             \
@@ -907,12 +911,12 @@ __global__ void k_split3(const float *__restrict__ x, int64_t n, __bf16 *__restr
     out[t + 2 * n] = l;
 }
 
-template <int WM, int WN, int TM, int TN, bool DUAL, int CHAIN = 0>
+template <int WM, int WN, int TM, int TN, bool DUAL, int CHAIN = 0, bool NT = false>
 int launch_x6b(const ConvX &a, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL((k_conv_x6b<WM, WN, TM, TN, DUAL, CHAIN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_conv_x6b<WM, WN, TM, TN, DUAL, CHAIN, NT>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     return (int)hipGetLastError();
 }
 
@@ -926,10 +930,13 @@ int launch_x6(const ConvX &a, hipStream_t st) {
 }
 
 int g_x6_tile = 0;  // 0 automatic, 1 = 128 x 128, 2 = 128 x 64
+int g_x6_nt = 0;    // BEV_TUNE_CONV_X6_NT: 1 = non-temporal activation loads in the 32-deep kernels
 int g_x6_kernel = 0;  // 0 automatic, 1 = k_conv_x6 (16-deep K steps) everywhere, 2 = k_conv_x6b wherever it applies
 
 template <bool DUAL>
-int dispatch_x6(const ConvX &a, hipStream_t st) {
+int dispatch_x6(const ConvX &a0, hipStream_t st) {
+    ConvX a = a0;
+    a.nta = g_x6_nt;
     const int t = g_x6_tile ? g_x6_tile : (a.Co <= 64 ? 2 : 1);
     if (!DUAL && a.xs) {
         if (t == 2) return launch_x6s<4, 1, 1, 2>(a, st);
@@ -940,6 +947,7 @@ int dispatch_x6(const ConvX &a, hipStream_t st) {
     // everywhere (r03 tools/trunk_ab.py: 16.24 ms vs 16.34 with 1x1 / dual layers on the 16-deep one, 16.43 all)
     const bool wide = a.Ci % YBK == 0 && (!DUAL || a.Ci2 % YBK == 0) && g_x6_kernel != 1;
     if (wide) {
+        if (t == 2 && !DUAL && a.nta) return launch_x6b<4, 1, 1, 2, false, 0, true>(a, st);
         if (t == 2) return launch_x6b<4, 1, 1, 2, DUAL>(a, st);
         return launch_x6b<2, 2, 2, 2, DUAL>(a, st);
     }
@@ -951,8 +959,8 @@ int dispatch_x6(const ConvX &a, hipStream_t st) {
 
 namespace bev {
 int conv_x6_tune(int knob, int value) {
-    int *slot = knob == BEV_TUNE_CONV_X6_TILE ? &g_x6_tile : &g_x6_kernel;
-    if (value < 0 || value > 2) return BEV_ERR_ARGS;
+    int *slot = knob == BEV_TUNE_CONV_X6_TILE ? &g_x6_tile : knob == BEV_TUNE_CONV_X6_NT ? &g_x6_nt : &g_x6_kernel;
+    if (value < 0 || value > 2 || (knob == BEV_TUNE_CONV_X6_NT && value > 1)) return BEV_ERR_ARGS;
     const int old = *slot;
     *slot = value;
     return old;

@@ -25,6 +25,7 @@ and never moves it; here it is created on the input's device.
 """
 from __future__ import annotations
 
+
 import torch
 import torch.nn as nn
 
@@ -74,6 +75,7 @@ class CNNEncoder(ViewEncoder):
             )
         self._fb = None
         self._fproj = None
+        self.proj_stream_nt = True  # non-temporal activation loads in the inference projection (see forward)
 
     def _trunk_frozen(self) -> bool:
         return not any(p.requires_grad for p in self.backbone.parameters())
@@ -92,6 +94,15 @@ class CNNEncoder(ViewEncoder):
                 self._fproj = FoldedConv(self.proj, split_ok=True)
             if torch.is_grad_enabled() and (self.proj.weight.requires_grad or self.proj.bias.requires_grad):
                 return Proj1x1.apply(feat, self.proj.weight, self.proj.bias)  # trainable proj (BASELINE config 3)
+            if self.proj_stream_nt:
+                # The projection is the last reader of the trunk output (~8x the feature maps' bytes): streamed
+                # with non-temporal loads it no longer evicts the maps it writes from the Infinity Cache, and the
+                # warp that follows reads them from there (bench: warp 179.5 -> 136.4 us, profiles/r04nt_proj_ab.txt)
+                old = _nat.tune(_nat.TUNE_CONV_X6_NT, 1)
+                try:
+                    return self._fproj(feat, relu=False)
+                finally:
+                    _nat.tune(_nat.TUNE_CONV_X6_NT, old)
             return self._fproj(feat, relu=False)
         c0, c2 = self.backbone[0], self.backbone[2]
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.backbone.parameters()):
