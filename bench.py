@@ -91,9 +91,6 @@ def parse():
                     help="experiment: read the encoder's features before the warp (tlb: one float per 4 KiB page, "
                          "full: every byte) or idle the GPU ~60 us (sleep), inside the timed geometry stage; "
                          "profiles/r04u_warp_touch_ab.txt")
-    ap.add_argument("--prepare-warp", type=int, default=0, choices=(0, 1),
-                    help="1: the warp's homographies + footprint boxes are computed on a side stream while the encoder "
-                         "runs (GeometryTransformer.prepare_fused), every step; 0: inside the geometry stage")
     ap.add_argument("--dry-run", action="store_true",
                     help="orchestration check on the CPU (gloo): the rank spawning, barriers, timing and MAX "
                          "reduction of this script with a placeholder step (rank r sleeps (r + 1) x 5 ms); no hot "
@@ -446,18 +443,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
 
-    side = torch.cuda.Stream(dev)  # the warp's feature-independent pre-pass (homographies, footprint boxes)
-
     def step(record):
         with torch.no_grad():
             e0 = e1 = e2 = None
             if record:
                 e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
                 e0.record(stream)
-            plan = None
-            if args.prepare_warp and not args.camera_shard and step.fshape is not None:
-                # overlaps the encoder on a side stream, every step (the feature shape is the first step's)
-                plan = geom.prepare_fused(step.fshape, Kd, Rtd, (H, W), "mean", device=dev, stream=side)
             if args.warp_only and step.feats is not None:
                 feats = step.feats
             else:
@@ -472,17 +463,15 @@ def main():
             if args.camera_shard:
                 bev = bev_dist.camera_sharded_forward(geom, feats, Kd, Rtd, (H, W), V, "mean")
             else:
-                bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean", plan=plan)
+                bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean")
             if record:
                 e2.record(stream)
                 ev.append((e0, e1, e2))
             return feats, bev
 
     step.feats = None
-    step.fshape = None
     feats, bev = step(False)
     step.feats = feats
-    step.fshape = tuple(feats.shape)
     for _ in range(args.warmup):
         step(False)
 

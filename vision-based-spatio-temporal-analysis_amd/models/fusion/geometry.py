@@ -143,13 +143,13 @@ class _WarpFn(torch.autograd.Function):
 class _WarpFuseFn(torch.autograd.Function):
     @staticmethod
     @_nat.amp_fwd
-    def forward(ctx, feats5, H, xs, ys, img_hw, mode, boxes=None):
+    def forward(ctx, feats5, H, xs, ys, img_hw, mode):
         if mode == "max":  # the backward re-samples the views to find each element's maximal one
             ctx.save_for_backward(H, xs, ys, feats5)
         else:
             ctx.save_for_backward(H, xs, ys)
         ctx.meta = (feats5.shape[1], feats5.shape[3], feats5.shape[4], img_hw, mode)
-        return _nat.warp_fuse(feats5, H, xs, ys, img_hw, mode, boxes=boxes)
+        return _nat.warp_fuse(feats5, H, xs, ys, img_hw, mode)
 
     @staticmethod
     @_nat.amp_bwd
@@ -157,7 +157,7 @@ class _WarpFuseFn(torch.autograd.Function):
         V, Hf, Wf, img_hw, mode = ctx.meta
         if mode in ("sum", "mean"):
             H, xs, ys = ctx.saved_tensors
-            return _nat.warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode), None, None, None, None, None, None
+            return _nat.warp_fuse_bwd(gout, H, xs, ys, V, Hf, Wf, img_hw, mode), None, None, None, None, None
         # max (fusion.py:22 after geometry.py:161): the per-view samples again (bit-identical to the forward's),
         # the gradient to the view torch's max(dim) picks, then the per-view warp backward
         H, xs, ys, feats5 = ctx.saved_tensors
@@ -167,14 +167,7 @@ class _WarpFuseFn(torch.autograd.Function):
         gv = _nat.view_max_bwd(per_view, gout)
         del per_view
         gf = _nat.warp_bwd(gv.view(B * V, C, gout.shape[2], gout.shape[3]), H, xs, ys, Hf, Wf, img_hw)
-        return gf.view(B, V, C, Hf, Wf), None, None, None, None, None, None
-
-
-class FusedPlan:
-    """Homographies + footprint boxes of one fused-warp call, computed ahead (GeometryTransformer.prepare_fused)."""
-
-    def __init__(self, H, xs, ys, hw, boxes, event, key):
-        self.H, self.xs, self.ys, self.hw, self.boxes, self.event, self.key = H, xs, ys, hw, boxes, event, key
+        return gf.view(B, V, C, Hf, Wf), None, None, None, None, None
 
 
 class GeometryTransformer(nn.Module):
@@ -306,39 +299,10 @@ class GeometryTransformer(nn.Module):
         return out.view(B, V, C, self.bev_h, self.bev_w)
 
     def forward_fused(self, feats: torch.Tensor, intrinsics, extrinsics, img_size: Tuple[int, int] = (1080, 1920),
-                      mode: str = "mean", plan: "FusedPlan" = None) -> torch.Tensor:
-        """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev].
-
-        `plan` (from `prepare_fused` with the same calibration, image size, feature shape and mode): the homographies
-        and footprint boxes were computed ahead, e.g. on a side stream while the encoder ran; the caller orders that
-        work before this call (`plan.event`)."""
-        if plan is not None:
-            assert plan.key == (tuple(feats.shape), tuple(img_size), mode), "plan made for another call"
-            if plan.event is not None:
-                torch.cuda.current_stream(feats.device).wait_event(plan.event)
-            return _WarpFuseFn.apply(feats, plan.H, plan.xs, plan.ys, plan.hw, mode, plan.boxes)
+                      mode: str = "mean") -> torch.Tensor:
+        """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev]."""
         H, xs, ys, hw = self._sampling(feats, intrinsics, extrinsics, img_size)
         return _WarpFuseFn.apply(feats, H, xs, ys, hw, mode)
-
-    def prepare_fused(self, feats_shape, intrinsics, extrinsics, img_size: Tuple[int, int] = (1080, 1920),
-                      mode: str = "mean", device=None, stream=None) -> "FusedPlan":
-        """The feature-independent part of `forward_fused` -- homographies (geometry.py:143) and the fused kernel's
-        per-(frame, tile, view) footprint boxes -- issued on `stream` (default: the current one) and marked by an
-        event, so it can overlap the encoder.  Same results as `forward_fused` without a plan."""
-        B, V, C, Hf, Wf = feats_shape
-        device = torch.device(device) if device is not None else torch.device("cuda")
-        stream = stream if stream is not None else torch.cuda.current_stream(device)
-        stream.wait_stream(torch.cuda.current_stream(device))  # the calibration tensors were made on the caller's
-        with torch.cuda.stream(stream):
-            probe = torch.empty((), device=device).expand(B, V, C, Hf, Wf)  # shape / device only
-            H, xs, ys, hw = self._sampling(probe, intrinsics, extrinsics, img_size)
-            boxes = _nat.warp_fuse_boxes(H, xs, ys, B, V, Hf, Wf, hw, mode)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        for t in (H, xs, ys, boxes):
-            if t is not None:
-                t.record_stream(torch.cuda.current_stream(device))
-        return FusedPlan(H, xs, ys, hw, boxes, ev, (tuple(feats_shape), tuple(img_size), mode))
 
 
 # north_star vocabulary alias
