@@ -547,7 +547,10 @@ def main():
                    "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
                    "traffic": pmc.get("warp"), "alg_bytes_per_launch": alg, "out_bytes": out_b,
                    "touched_src_pixels": touched, "avg_us": round(wp_ms * 1e3, 2),
-                   "geometry_stage_us": round(stage_wp_ms * 1e3, 2)}
+                   "geometry_stage_us": round(stage_wp_ms * 1e3, 2),
+                   "timing": "HIP events on the launch stream around the fused kernel launch alone (its footprint-box "
+                             "pre-pass, k_warp_boxes, and the homographies run before the span, inside the geometry "
+                             "stage)"}
         label, wl = workload(args, world)
         roof_bb_hbm = None
         if not args.warp_only and args.backbone.startswith("efficientnet"):

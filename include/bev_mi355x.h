@@ -140,6 +140,19 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
                              const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                              int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
                              void *stream);
+/* The footprint-box pre-pass of bev_ipm_warp_fuse_ws_f32 on its own (so it can run on a side stream, e.g. while the
+ * encoder runs: it needs only the homographies), and the fused warp that takes the boxes from the workspace instead of
+ * recomputing them.  bev_ipm_warp_fuse_pre_f32 requires a prior bev_ipm_warp_fuse_boxes_f32 on the same workspace with
+ * the same Hmat / xs / ys / B / V / Hf / Wf / sx / sy / Hb / Wb / mode and tuning knobs, ordered before it (same stream
+ * or an event); otherwise it is bev_ipm_warp_fuse_ws_f32.  Same results.  Replaces the same reference ops
+ * (geometry.py:120-162 + fusion.py:17-22). */
+int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float *ys, int B, int V, int Hf, int Wf,
+                                float sx, float sy, int Hb, int Wb, int mode, void *workspace, int64_t workspace_bytes,
+                                void *stream);
+int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                              const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                              int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
+                              void *stream);
 
 /* Bilinear corners for index-exactness checks: x0y0 [N][Hb][Wb][2] int32
  * (0 when both taps of an axis are out of range), wts [N][Hb][Wb][4] (nw, ne,

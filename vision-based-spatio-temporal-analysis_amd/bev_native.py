@@ -43,6 +43,9 @@ SIGNATURES = {
     "bev_ipm_warp_fuse_workspace_bytes": (_i64, [_i, _i, _i, _i]),
     "bev_ipm_warp_fuse_ws_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
                                       _i, _vp, _vp, _i64, _vp]),
+    "bev_ipm_warp_fuse_pre_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
+                                      _i, _vp, _vp, _i64, _vp]),
+    "bev_ipm_warp_fuse_boxes_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _i64, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_ipm_warp_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
     "bev_ipm_warp_bwd_ex_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _i64, _i64, _i64, _i64,
@@ -380,8 +383,24 @@ def warp(feats: torch.Tensor, H: torch.Tensor, xs: torch.Tensor, ys: torch.Tenso
     return out
 
 
-def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, out: torch.Tensor = None):
-    """feats [B,V,C,Hf,Wf] (any strides within a map; maps b*V+v) -> out [B,C,Hb,Wb]."""
+def warp_fuse_boxes(H: torch.Tensor, xs, ys, B: int, V: int, Hf: int, Wf: int, img_hw, mode: str) -> torch.Tensor:
+    """The fused warp's footprint-box pre-pass alone (bev_ipm_warp_fuse_boxes_f32) into a new workspace, on the
+    current stream; pass it to `warp_fuse(..., boxes=)` with the same geometry and mode."""
+    _require_gpu(H, xs, ys)
+    Hb, Wb = ys.numel(), xs.numel()
+    sx, sy = _scales(Hf, Wf, img_hw)
+    nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
+    ws = torch.empty(max(nws, 8), device=H.device, dtype=torch.uint8)
+    rc = lib().bev_ipm_warp_fuse_boxes_f32(_ptr(H), _ptr(xs), _ptr(ys), B, V, Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode],
+                                           _ptr(ws), nws, _stream(H))
+    _check(rc, "bev_ipm_warp_fuse_boxes_f32")
+    return ws
+
+
+def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, out: torch.Tensor = None,
+              boxes: torch.Tensor = None):
+    """feats [B,V,C,Hf,Wf] (any strides within a map; maps b*V+v) -> out [B,C,Hb,Wb].  `boxes`: a workspace filled
+    by `warp_fuse_boxes` for this geometry and mode (the pre-pass is then not launched again)."""
     _require_gpu(feats, H, xs, ys)
     B, V, C, Hf, Wf = feats.shape
     if B * V > 0 and feats.stride(0) != V * feats.stride(1):
@@ -391,14 +410,21 @@ def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, o
     if out is None:
         out = torch.empty(B, C, Hb, Wb, device=feats.device, dtype=torch.float32)
     s = feats.stride()
-    # the per-(frame, tile, view) footprint boxes go to a stream-ordered workspace (a small launch of their own)
+    # the per-(frame, tile, view) footprint boxes go to a stream-ordered workspace: for the LDS-DMA kernels (NHWC,
+    # C % 64 == 0) a launch of their own BEFORE the timed span, so "warp_fuse" spans time the fused kernel alone
+    # (as rocprofv3 lists it); other layouts let the library decide
     nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
-    ws = torch.empty(max(nws, 8), device=feats.device, dtype=torch.uint8)
+    if boxes is None and s[2] == 1 and C % 64 == 0 and V <= 64 and Hf < 16384 and Wf < 16384 and B * Hb * Wb > 0:
+        boxes = warp_fuse_boxes(H, xs, ys, B, V, Hf, Wf, img_hw, mode)
+    if boxes is not None:
+        assert boxes.numel() >= nws and boxes.device == feats.device, "boxes workspace for another geometry"
+        fn, ws = lib().bev_ipm_warp_fuse_pre_f32, boxes
+    else:
+        fn, ws = lib().bev_ipm_warp_fuse_ws_f32, torch.empty(max(nws, 8), device=feats.device, dtype=torch.uint8)
     with _span("warp_fuse", feats):
-        rc = lib().bev_ipm_warp_fuse_ws_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C,
-                                            Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _ptr(ws), nws,
-                                            _stream(feats))
-    _check(rc, "bev_ipm_warp_fuse_ws_f32")
+        rc = fn(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf, Wf, sx, sy, Hb, Wb,
+                FUSE_MODES[mode], _ptr(out), _ptr(ws), nws, _stream(feats))
+    _check(rc, "bev_ipm_warp_fuse")
     return out
 
 

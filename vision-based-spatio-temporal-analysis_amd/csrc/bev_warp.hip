@@ -1433,13 +1433,13 @@ constexpr int V2_FIXED = 256 + 4 * (FT_NT / 64) * (int)sizeof(int) + V2_MAXV * 9
 template <int OCC>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                       int mode, float *out, hipStream_t st, int pool, uint2 *boxes) {
+                       int mode, float *out, hipStream_t st, int pool, uint2 *boxes, bool boxes_ready) {
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
     dim3 grid(ntiles, B), block(FT_NT);
     const size_t lds = (size_t)pool + V2_FIXED;
     if (!WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (LDS homographies)
-    if (boxes) {
+    if (boxes && !boxes_ready) {  // else bev_ipm_warp_fuse_boxes_f32 wrote them (same geometry, pool and knobs)
         const int maxpix = pool / (17 * 16) - 4;  // the kernel's own pool test
         hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                            st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes);
@@ -1479,18 +1479,28 @@ int launch_fuse_v3(const float *feats, int64_t sN, int64_t sH, int64_t sW, const
     return last();
 }
 
+// LDS image pool of k_warp_fuse_v2 for `mode` (the corner boxes' fit test depends on it)
+inline int v2_pool_bytes(int mode) {
+    const int kb = g_warp_pool_kb > 0 && g_warp_pool_kb < 8 ? 8 : g_warp_pool_kb;  // v2 needs >= 8 KiB
+    if (mode == BEV_FUSE_MAX) return kb ? kb * 1024 : 72 * 1024;  // MAX: 2 workgroups per CU
+    const int pool3 = (163840 / WARP_OCC - V2_FIXED - 64) & ~1023;
+    return kb ? kb * 1024 : (pool3 < 49 * 1024 ? pool3 : 49 * 1024);
+}
+
 inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                          int Hb, int Wb, int mode, float *out, hipStream_t st, uint2 *boxes) {
-    const int kb = g_warp_pool_kb > 0 && g_warp_pool_kb < 8 ? 8 : g_warp_pool_kb;  // v2 needs >= 8 KiB
+                          int Hb, int Wb, int mode, float *out, hipStream_t st, uint2 *boxes, bool boxes_ready = false) {
     if (mode == BEV_FUSE_MAX)  // MAX's extra live state spills at 3 workgroups per CU
         return launch_fuse_v2_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                     kb ? kb * 1024 : 72 * 1024, boxes);
-    const int pool3 = (163840 / WARP_OCC - V2_FIXED - 64) & ~1023;
+                                     v2_pool_bytes(mode), boxes, boxes_ready);
     return launch_fuse_v2_occ<WARP_OCC>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                        st, kb ? kb * 1024 : (pool3 < 49 * 1024 ? pool3 : 49 * 1024),
-                                        boxes);
+                                        st, v2_pool_bytes(mode), boxes, boxes_ready);
 }
+
+int warp_fuse_impl(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                   const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                   int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes, void *stream,
+                   bool boxes_ready);
 
 }  // namespace
 
@@ -1598,6 +1608,43 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
                              const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                              int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
                              void *stream) {
+    return warp_fuse_impl(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, workspace,
+                          workspace_bytes, stream, false);
+}
+
+int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                              const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                              int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
+                              void *stream) {
+    return warp_fuse_impl(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, workspace,
+                          workspace_bytes, stream, true);
+}
+
+int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float *ys, int B, int V, int Hf, int Wf,
+                                float sx, float sy, int Hb, int Wb, int mode, void *workspace, int64_t workspace_bytes,
+                                void *stream) {
+    if (!Hmat || !xs || !ys || B < 0 || V <= 0 || V > V2_MAXV || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B > 65535)
+        return BEV_ERR_ARGS;
+    if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX || Hf >= 16384 || Wf >= 16384) return BEV_ERR_ARGS;
+    const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
+    if (!workspace || workspace_bytes < need || ((uintptr_t)workspace & 7) != 0) return BEV_ERR_ARGS;
+    if (B == 0 || Hb == 0 || Wb == 0) return 0;
+    constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
+    const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
+    const int maxpix = v2_pool_bytes(mode) / (17 * 16) - 4;  // k_warp_fuse_v2's own pool test
+    hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
+                       (hipStream_t)stream, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH,
+                       reinterpret_cast<uint2 *>(workspace));
+    return last();
+}
+
+}  // extern "C"
+
+namespace {
+int warp_fuse_impl(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                   const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
+                   int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes, void *stream,
+                   bool boxes_ready) {
     if (B < 0 || V <= 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B > 65535) return BEV_ERR_ARGS;
     if ((int64_t)Hf * Wf >= (1 << 22)) return BEV_ERR_ARGS;  // fast_div range of the footprint index
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
@@ -1618,7 +1665,8 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
         if (g_warp_kernel == 3 && boxes && mode != BEV_FUSE_MAX && (int64_t)Hf * sH + (int64_t)Wf * sW < (1ll << 31))
             return launch_fuse_v3(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
                                   boxes);
-        return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st, boxes);
+        return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st, boxes,
+                              boxes_ready);
     }
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
@@ -1628,6 +1676,9 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
         return launch_fuse_ck<32>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
     return launch_fuse_ck<64>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);
 }
+}  // namespace
+
+extern "C" {
 
 int bev_view_max_bwd_f32(const float *x, const float *gout, int B, int V, int64_t M, float *gx, void *stream) {
     if (B < 0 || V <= 0 || M < 0 || B > 65535) return BEV_ERR_ARGS;
