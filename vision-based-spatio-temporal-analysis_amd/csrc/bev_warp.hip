@@ -416,6 +416,9 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
     }
 }
 
+#ifndef WARP_STORE_AUX
+#define WARP_STORE_AUX 2  // fused warp output stores: buffer cache policy (2 = nt, streaming; 0 = default)
+#endif
 #ifndef WARP_PIPE
 #define WARP_PIPE 1  // fused warp v2: LDS sampling software-pipelined by one 4-channel group (1) or not (0)
 #endif
@@ -471,7 +474,8 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
             const float r = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? div_rcp(a[u], rV) : a[u];
             if ((WARP_ABLATE & 16) && r != 1.2345e-30f) continue;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
-                                                  (int)(uint32_t)((q0 + u) * plane * sizeof(float)), 2);
+                                                  (int)(uint32_t)((q0 + u) * plane * sizeof(float)),
+                                                  WARP_STORE_AUX);
         }
     }
 }
