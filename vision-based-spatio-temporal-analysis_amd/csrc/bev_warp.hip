@@ -45,6 +45,9 @@
 #ifndef WARP_OPT
 #define WARP_OPT 1
 #endif
+#ifndef WARP_DMA_POLICY
+#define WARP_DMA_POLICY ""  // footprint LDS-DMA cache policy suffix (A/B builds: " nt")
+#endif
 
 using namespace bev;
 
@@ -409,7 +412,7 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
         unsigned keep;
         asm volatile(
             "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            "global_load_lds_dwordx4 %1, off" WARP_DMA_POLICY "\n\ts_mov_b32 m0, %0"
             : "=&s"(keep)
             : "v"(src), "s"(dst)
             : "memory");
