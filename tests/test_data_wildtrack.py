@@ -1,7 +1,8 @@
 """Wildtrack data path (reference project/data/wildtrack_loader.py, transforms.py).
 
-The reference module is not importable here (it imports torchvision at module scope, absent in this
-image), so its behaviour is pinned by known answers built from the dataset's published file formats:
+The reference helpers themselves are pinned bit for bit by tests/test_wildtrack_golden.py (fixtures recorded
+from the reference module with a raising torchvision stub for its unused module-scope import).  This file adds
+known answers built from the dataset's published file formats:
 OpenCV-storage intrinsics (`camera_matrix` with a `<data>` child) and Rodrigues extrinsics
 (`rvec` / `tvec` in centimetres -> the reference's >100 "millimetre" rule divides by 1000), and the
 Wildtrack annotation list (per-view boxes, bottom centre projected through inv(K [r1 r2 t])).

@@ -386,6 +386,43 @@ def test_bottleneck_h16_block_bit_identical():
 
 
 @pytest.mark.timeout(300)
+def test_bottleneck_h16_under_kernel_knob_1():
+    """bev_tune CONV_H16_KERNEL = 1 (the 32-deep fp16 conv, an A/B knob) under autocast with the default
+    BottleneckTrainH16 nodes and epilogue BatchNorm statistics: the calls that only k_conv_h16b serves (statistics
+    in the epilogue, fp16-stored operands) keep it, every other call takes the 32-deep kernel, and since both kernels
+    sum each output in the same K order the forward output and the BatchNorm parameter gradients are bit-identical
+    to the default knob (round-4 ADVICE: the knob used to make those calls fail with BEV_ERR_ARGS)."""
+    import bev_native as nat
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(4)
+    enc = CNNEncoder(out_channels=32, backbone="resnet50", pretrained=False).to(DEV)
+    x0 = torch.randn(1, 2, 3, 104, 168, device=DEV)
+    with torch.no_grad():
+        enc.eval()(x0)
+    enc.train()
+    assert enc.backbone.h16_blocks
+    state = copy.deepcopy(enc.state_dict())
+    results = []
+    for kern in (0, 1):
+        enc.load_state_dict(state)
+        enc.zero_grad(set_to_none=True)
+        with nat.tuned(CONV_H16_KERNEL=kern), _autocast():
+            out = enc(x0)
+            g = torch.randn(out.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(6))
+            out.float().backward(g)
+        torch.cuda.synchronize()
+        grads = {k: p.grad.detach().clone() for k, p in enc.named_parameters() if p.grad is not None}
+        results.append((out.detach().float().clone(), grads))
+    (o0, g0), (o1, g1) = results
+    assert torch.equal(o0, o1)
+    assert g0.keys() == g1.keys() and len(g0) > 60
+    for k in g0:
+        assert torch.isfinite(g1[k]).all(), k
+        if k.split(".")[-2].startswith("bn") or "downsample.1." in k:
+            assert torch.equal(g0[k], g1[k]), k
+
+
+@pytest.mark.timeout(300)
 def test_head_h16_node_bit_identical():
     """BEVDetector training under autocast with the head as one _HeadTrainH16 node (fp16-stored GroupNorm + ReLU
     outputs and GroupNorm backward outputs) vs the per-layer _HeadConv / _GroupNormReLU chain (fp32-stored): the five

@@ -836,7 +836,9 @@ static int conv_h16(const void *xv, int x_half, int N, int H, int W, int Ci, con
         return BEV_ERR_ARGS;
     if ((((uintptr_t)x | (uintptr_t)packed) & 15) != 0) return BEV_ERR_ARGS;
     if (residual && ldy != Co) return BEV_ERR_ARGS;
-    const bool wide = Ci % HBK2 == 0 && g_h16_kernel != 1;
+    // CONV_H16_KERNEL 1 (the 32-deep kernel, A/B) applies only where that kernel can run: epilogue statistics
+    // and fp16-stored operands exist on k_conv_h16b alone, so those calls keep it (as the weight gradient does)
+    const bool wide = Ci % HBK2 == 0 && (g_h16_kernel != 1 || stats != nullptr || x_half);
     if (stats && (!wide || act != 0 || residual)) return BEV_ERR_ARGS;  // statistics of the raw conv output, k_conv_h16b
     if (x_half && !wide) return BEV_ERR_ARGS;                         // fp16 operands: k_conv_h16b only
     if (x_half && ((uintptr_t)x & 7) != 0) return BEV_ERR_ARGS;

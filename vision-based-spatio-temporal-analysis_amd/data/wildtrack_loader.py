@@ -118,9 +118,11 @@ def _parse_float_list(text: Optional[str]) -> List[float]:
 
 
 def _reshape(vals: List[float], rows: int, cols: int) -> torch.Tensor:
-    if len(vals) < rows * cols:
-        raise ValueError(f"Not enough values to reshape: need {rows*cols}, got {len(vals)}")
-    return torch.tensor(vals[: rows * cols], dtype=torch.float32).reshape(rows, cols)
+    """The first rows*cols values as a float32 [rows, cols] matrix (extra values are ignored)."""
+    n = rows * cols
+    if n > len(vals):
+        raise ValueError(f"Not enough values to reshape: need {n}, got {len(vals)}")
+    return torch.tensor(vals[:n], dtype=torch.float32).view(rows, cols)
 
 
 def _try_get_matrix(root: ET.Element, tag_names: List[str], shape: Tuple[int, int]) -> Optional[torch.Tensor]:
