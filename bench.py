@@ -590,6 +590,9 @@ def main():
                                             "includes the reduce-scatter and the /V"
         if pmc:
             line["traffic_source"] = pmc["source"]
+        prov = nat.provenance()  # the library this run loaded, and whether it was built from this tree's sources
+        line["build"] = {"lib_source_hash": prov["lib_source_hash"], "tree_source_hash": prov["tree_source_hash"],
+                         "matches_tree": prov["matches_tree"]}
         if h2d:
             line["h2d_inclusive"] = h2d
         if args.warp_only:

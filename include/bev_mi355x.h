@@ -36,6 +36,10 @@ extern "C" {
 /* ABI version (bumped on any signature change). */
 int bev_abi_version(void);
 
+/* host: provenance -- the first 16 hex digits of sha256 over the library's HIP sources and headers (the
+ * Makefile's SRCS then HDRS), fixed at build time; bev_native.source_hash() recomputes it from a source tree. */
+const char *bev_build_source_hash(void);
+
 /* host: performance knobs (no effect on results); returns the previous value, or
  * BEV_ERR_ARGS for an unknown knob / out-of-range value.
  * BEV_TUNE_CONV_TILE: 0 = automatic, 1 = 128x128, 2 = 128x64, 3 = 64x128, 4 = 64x64

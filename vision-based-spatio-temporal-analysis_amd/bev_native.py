@@ -34,6 +34,7 @@ _d = ctypes.c_double
 # name -> (restype, argtypes); must match include/bev_mi355x.h
 SIGNATURES = {
     "bev_abi_version": (_i, []),
+    "bev_build_source_hash": (ctypes.c_char_p, []),
     "bev_tune": (_i, [_i, _i]),
     "bev_linspace_f32": (_i, [_d, _d, _i, _vp]),
     "bev_homography_f32": (_i, [_vp, _vp, _i, _vp, _vp]),
@@ -188,6 +189,32 @@ def lib():
             raise ImportError(f"libbev_mi355x.so ABI {v} != expected {ABI_VERSION}; rebuild")
         _lib = L
     return _lib
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) of the library's sources and headers in the Makefile's order (SRCS, then HDRS):
+    the digest the Makefile compiles into bev_build_source_hash()."""
+    import hashlib
+    mk = open(os.path.join(HERE, "Makefile")).read()
+    files = []
+    for var in ("SRCS", "HDRS"):
+        line = next(l for l in mk.splitlines() if l.startswith(var + " ="))
+        files += line.split("=", 1)[1].split()
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(HERE, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def provenance() -> dict:
+    """Which sources the loaded library was built from, and whether they are the sources in this tree."""
+    built = lib().bev_build_source_hash().decode()
+    try:
+        tree = source_hash()
+    except OSError:
+        tree = None
+    return {"lib": LIB_PATH, "lib_source_hash": built, "tree_source_hash": tree, "matches_tree": built == tree}
 
 
 # performance knobs (include/bev_mi355x.h BEV_TUNE_*); results never depend on them
