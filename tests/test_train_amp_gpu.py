@@ -542,3 +542,153 @@ def test_bevnet_r50_ddp_world2_trainable_trunk_amp():
     assert all(np.isfinite(res[r][2]).all() for r in (0, 1))
     # the scale both ranks hold: 65536 unless a step met an fp16 inf (fp16 convs), then halved -- on both ranks
     assert res[0][5] == res[1][5] and res[0][5] in (65536.0, 32768.0, 16384.0)
+
+
+K3_TRAINABLE_REF = ("encoder.backbone.layer2.3.", "encoder.proj.", "proj.", "detector.")
+
+
+def k3_reference_step(model_cpu_state, cfg, imgs, K, Rt, t_ref, boxes, trunk_masks, head_masks, scale, half):
+    """The reference graph of one K3 training step at full geometry, in float64 and float32 on the CPU, with the
+    native run's ReLU decisions (bool masks, in execution order) and, under AMP, the native fp16 operand
+    roundings (_H16Conv).  Only the parameters the full-geometry test compares take gradients -- the head, the BEV
+    projection, the encoder projection and the last trunk block (K3_TRAINABLE_REF) -- so autograd stops at
+    layer2's last block and the float64 trunk runs forward only below it.  Returns {dtype: (outputs, losses,
+    {name: grad})}."""
+    import bevnet_ref
+    res = {}
+    if half:
+        _H16Conv.scale = scale
+        torch.nn.functional.conv2d = _h16_conv2d
+    try:
+        for dt in (torch.float64, torch.float32):
+            net = model_cpu_state(dt)
+            net.train()
+            for k, p in net.named_parameters():
+                p.requires_grad_(k.startswith(K3_TRAINABLE_REF))
+            net._build_training_targets = lambda _t: t_ref
+            it = iter(trunk_masks)
+            out = bevnet_ref.bevnet_train_forward(net, imgs.to(dt), K, Rt, trunk_act=lambda t: t * next(it).to(dt),
+                                                  head_masks=[m.to(dt) for m in head_masks])
+            ls = net.loss(out, [{"boxes_world": b.to(dt)} for b in boxes], cfg["LOSS"])
+            ls["total_loss"].backward()
+            print(f"k3_reference_step: {dt} forward + backward done", flush=True)  # progress (pytest -s)
+            grads = {k: p.grad.detach().clone() for k, p in net.named_parameters() if p.grad is not None}
+            res[dt] = ({k: out[k].detach() for k in ("heatmap_logits", "offset_raw", "size_raw", "bev_feat")},
+                       {k: ls[k].detach().reshape(1) for k in ("heatmap_loss", "offset_loss", "size_loss", "total_loss")},
+                       grads)
+            del net, out, ls
+    finally:
+        torch.nn.functional.conv2d = _ORIG_CONV
+    return res
+
+
+@pytest.mark.timeout(1200)
+def test_bevnet_r50_amp_step_full_geometry():
+    """One K3 training step at the geometry tools/train_step_bench.py --bevnet --amp times (BASELINE configs[2]
+    shape: B = 1 frame, 7 cameras x 3 x 1080 x 1920, ResNet-50 trunk trainable with batch-statistics BN, FEAT_DIM
+    64, BEV 480 x 1440, BEV_PROJ_CH 128 = configs/wildtrack.yaml:14; autocast float16 + GradScaler, train.py:238-247)
+    vs the float64 / float32 torch restatement of the reference graph: the outputs, the four losses and the
+    gradients of the head, the BEV projection, the encoder projection and the last trunk block, with
+    test_bevnet_r50_training_step_vs_float64_reference's bar (error <= 4 x the fp32 reference's own error + floor).
+    Covers at full size what the reduced-size test cannot: the fp16 conv tiles and the BatchNorm epilogue-statistics
+    partial counts over 7 x 270 x 480 pixels, the 512-channel head over 691 k cells, the fused-warp backward on
+    the bench rig."""
+    import bev_dist
+    import bev_native as nat
+    from models.model_wrapper import BEVNet
+    torch.manual_seed(0)
+    cfg = {"MODEL": {"BACKBONE": "resnet50", "PRETRAINED": False, "FEAT_DIM": 64, "OUT_INDEX": 2,
+                     "BEV_SIZE": [32, 480, 1440], "BEV_BOUNDS": [-24.0, 24.0, -7.2, 7.2], "BEV_PROJ_CH": 128},
+           "LOSS": {}, "EVAL": {"CONF_THRESH": 0.99, "NMS_DIST_M": 0.5}}
+    B, V, H, W = 1, 7, 1080, 1920
+    imgs, K, Rt, boxes = _r50_batch(B, V, H, W, seed=2)
+    batch = {"images": imgs.to(DEV), "calib": {"intrinsic": K.to(DEV), "extrinsic": Rt.to(DEV)}}
+    targets = [{"boxes_world": b.to(DEV)} for b in boxes]
+    model = BEVNet(cfg).to(DEV)
+    bev_dist.materialize_lazy(model, batch)
+    _randomize_bn(model, 9)
+    model.train()
+
+    trunk_masks, head_masks = [], []
+    bn_apply, bn_apply_half, gn_apply = nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply
+    gn_apply_half = nat.groupnorm_apply_half
+
+    def rec_bn(z, scale, shift, residual=None, act=0):
+        out = bn_apply(z, scale, shift, residual, act)
+        if act == 1:
+            trunk_masks.append((out > 0).permute(0, 3, 1, 2).cpu())
+        return out
+
+    def rec_bn_half(z, scale, shift, act=0):
+        out = bn_apply_half(z, scale, shift, act)
+        if act == 1:
+            trunk_masks.append(((z * scale + shift) > 0).permute(0, 3, 1, 2).cpu())
+        return out
+
+    def rec_gn(x, scale, shift, relu):
+        out = gn_apply(x, scale, shift, relu)
+        if relu:
+            head_masks.append((out > 0).permute(0, 3, 1, 2).cpu())
+        return out
+
+    def rec_gn_half(x, scale, shift, relu):
+        out = gn_apply_half(x, scale, shift, relu)
+        if relu:
+            u = x * scale[:, None, None, :] + shift[:, None, None, :]
+            head_masks.append((u > 0).permute(0, 3, 1, 2).cpu())
+        return out
+
+    nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = rec_bn, rec_bn_half, rec_gn
+    nat.groupnorm_apply_half = rec_gn_half
+    scaler = torch.amp.GradScaler("cuda")
+    try:
+        model.zero_grad(set_to_none=True)
+        with _autocast():
+            preds = model(batch)
+            losses = model.loss(preds, targets, cfg["LOSS"])
+        scaler.scale(losses["total_loss"]).backward()
+    finally:
+        nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = bn_apply, bn_apply_half, gn_apply
+        nat.groupnorm_apply_half = gn_apply_half
+    opt = torch.optim.SGD(model.parameters(), lr=0.0)
+    scaler.unscale_(opt)
+    torch.cuda.synchronize()
+    print("full-geometry K3: native AMP step done", flush=True)  # progress (pytest -s)
+    assert len(trunk_masks) > 20 and len(head_masks) == 3
+    t_ref = {k: v.detach().cpu() for k, v in model._build_training_targets(targets).items()}
+    got_out = {k: preds[k].detach().float().cpu() for k in ("heatmap_logits", "offset_raw", "size_raw", "bev_feat")}
+    got_ls = {k: losses[k].detach().float().cpu().reshape(1) for k in ("heatmap_loss", "offset_loss", "size_loss",
+                                                                         "total_loss")}
+    got = {k: p.grad.detach().double().cpu() for k, p in model.named_parameters()
+           if p.grad is not None and k.startswith(K3_TRAINABLE_REF)}
+    state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    del preds, losses
+    half = nat.AMP_HALF_CONVS
+
+    def ref_copy(dt):
+        m = _reference_copy(model, cfg, dt)
+        m.load_state_dict(state, strict=True)
+        return m
+
+    res = k3_reference_step(ref_copy, cfg, imgs, K, Rt, t_ref, boxes, trunk_masks, head_masks,
+                            float(scaler.get_scale()), half)
+    (o64, l64, g64), (o32, l32, g32) = res[torch.float64], res[torch.float32]
+    worst = []
+
+    def bounded(native, r64, r32, what, floor=1e-5):
+        scale = max(float(r64.abs().max()), 1e-30)
+        e_nat = float((native.double() - r64.double()).abs().max()) / scale
+        e_32 = float((r32.double() - r64.double()).abs().max()) / scale
+        worst.append((e_nat / (e_32 + 1e-12), what, e_nat, e_32))
+        assert e_nat <= 4.0 * e_32 + floor, (what, e_nat, e_32)
+
+    loss_floor = 3e-4 if half else 1e-5  # as the reduced-size test (fp16 rounding flips summed over 691 k cells)
+    for k in got_out:
+        bounded(got_out[k], o64[k], o32[k], k)
+    for k in got_ls:
+        bounded(got_ls[k], l64[k], l32[k], k, loss_floor)
+    assert set(g64) == set(got), sorted(set(g64) ^ set(got))
+    for k in g64:
+        bounded(got[k], g64[k], g32[k], "grad " + k, loss_floor if g64[k].numel() <= 8 else 1e-5)
+    assert len(g64) >= 20
+    print("worst native / fp32-reference error ratios:", sorted(worst, reverse=True)[:3])

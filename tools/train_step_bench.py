@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--bevnet", action="store_true")
     ap.add_argument("--backbone", default="resnet50")
     ap.add_argument("--amp", action="store_true")
+    ap.add_argument("--proj-ch", type=int, default=128, help="BEVNet BEV_PROJ_CH (configs/wildtrack.yaml:14: 128)")
     ap.add_argument("--fp32-kernels", action="store_true")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V", help="bev_tune knob (A/B); repeatable")
     a = ap.parse_args()
@@ -47,7 +48,7 @@ def main():
     if a.bevnet:
         from models.model_wrapper import BEVNet
         cfg = {"MODEL": {"BACKBONE": a.backbone, "PRETRAINED": False, "FEAT_DIM": 64, "OUT_INDEX": 2,
-                         "BEV_SIZE": [32, 480, 1440], "BEV_BOUNDS": [-24.0, 24.0, -7.2, 7.2], "BEV_PROJ_CH": 64},
+                         "BEV_SIZE": [32, 480, 1440], "BEV_BOUNDS": [-24.0, 24.0, -7.2, 7.2], "BEV_PROJ_CH": a.proj_ch},
                "LOSS": {}, "EVAL": {"CONF_THRESH": 0.99}}
         model = BEVNet(cfg).to(dev)
         batch = {"images": images, "calib": {"intrinsic": Kd, "extrinsic": Rtd}}
@@ -102,7 +103,8 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     print(json.dumps({"what": "bevnet train step" if a.bevnet else "hot-path train step", "backbone": a.backbone,
-                      "tune": a.tune,
+                      "tune": a.tune, "bev": [480, 1440], "cameras": V, "img": [H, W], "feat_dim": 64,
+                      "bev_proj_ch": a.proj_ch if a.bevnet else None,
                       "amp": a.amp, "half_convs": a.amp and not a.fp32_kernels,
                       "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
                       "loss": float(loss)}), flush=True)
