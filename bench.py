@@ -504,6 +504,7 @@ def main():
     # conv kernels only, per step (EfficientNet: + its depthwise convs, which the FLOP count includes)
     conv_ms = float(np.sum(spans.get("conv", [0.0])) + np.sum(spans.get("dwconv", [0.0]))) / args.steps
     wp_ms = float(np.mean(spans["warp_fuse"]))  # the fused warp kernel only
+    box_ms = float(np.mean(spans["warp_boxes"])) if spans.get("warp_boxes") else 0.0  # its footprint-box pre-pass
     frames = (B if args.camera_shard else world * B) * args.steps
     value = frames / elapsed
 
@@ -547,6 +548,8 @@ def main():
                    "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4),
                    "traffic": pmc.get("warp"), "alg_bytes_per_launch": alg, "out_bytes": out_b,
                    "touched_src_pixels": touched, "avg_us": round(wp_ms * 1e3, 2),
+                   "boxes_prepass_us": round(box_ms * 1e3, 2),
+                   "frac_incl_prepass": round(alg / ((wp_ms + box_ms) * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                    "geometry_stage_us": round(stage_wp_ms * 1e3, 2),
                    "timing": "HIP events on the launch stream around the fused kernel launch alone (its footprint-box "
                              "pre-pass, k_warp_boxes, and the homographies run before the span, inside the geometry "

@@ -136,7 +136,7 @@ int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH
                           int Hb, int Wb, int mode, float *out, void *stream);
 
 /* bev_ipm_warp_fuse_f32 with a caller-owned device workspace of at least
- * bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb) bytes (8-B aligned, stream-ordered like the output): the
+ * bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb) bytes (16-B aligned, stream-ordered like the output): the
  * fused kernel's per-(frame, tile, view) footprint boxes are then computed by a separate small launch instead of
  * inside every workgroup (same results, bit for bit).  A null or short workspace = bev_ipm_warp_fuse_f32. */
 int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb);
@@ -148,8 +148,10 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
  * encoder runs: it needs only the homographies), and the fused warp that takes the boxes from the workspace instead of
  * recomputing them.  bev_ipm_warp_fuse_pre_f32 requires a prior bev_ipm_warp_fuse_boxes_f32 on the same workspace with
  * the same Hmat / xs / ys / B / V / Hf / Wf / sx / sy / Hb / Wb / mode and tuning knobs, ordered before it (same stream
- * or an event); otherwise it is bev_ipm_warp_fuse_ws_f32.  Same results.  Replaces the same reference ops
- * (geometry.py:120-162 + fusion.py:17-22). */
+ * or an event); otherwise it is bev_ipm_warp_fuse_ws_f32.  Same results.  The workspace starts with a 16-B header
+ * recording the fit test (LDS pool), V and tile shape the boxes were made for; a fused launch whose own differ (another
+ * mode's pool, a changed pool knob) ignores the boxes and derives its footprints itself -- still the same results.
+ * Replaces the same reference ops (geometry.py:120-162 + fusion.py:17-22). */
 int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float *ys, int B, int V, int Hf, int Wf,
                                 float sx, float sy, int Hb, int Wb, int mode, void *workspace, int64_t workspace_bytes,
                                 void *stream);
@@ -157,6 +159,17 @@ int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_
                               const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                               int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
                               void *stream);
+/* bev_ipm_warp_fuse_pre_f32 (boxes_ready != 0) or _ws_f32 (boxes_ready == 0) writing the fused map in
+ * rank-chunk-major row order for the camera-shard exchange: out [ceil(Hb / rows_per_chunk)][B][C][rows_per_chunk][Wb],
+ * BEV row r of frame b at chunk r / rows_per_chunk, row r % rows_per_chunk -- the layout reduce_scatter over BEV rows
+ * takes as is (bev_dist.reduce_partial_bev), so the partial map is not permuted by a copy.  Rows past Hb in the last
+ * chunk are not written.  rows_per_chunk >= Hb is the plain [B][C][Hb][Wb] layout.  Same values as the plain call.
+ * Needs the LDS-DMA kernel's layout (NHWC C % 64 == 0 ...) and a whole output < 2 GiB; else BEV_ERR_ARGS.  Replaces
+ * geometry.py:120-162 + fusion.py:17-22 per rank, and the partial-map permute of the exchange. */
+int bev_ipm_warp_fuse_chunked_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW,
+                                  const float *Hmat, const float *xs, const float *ys, int B, int V, int C, int Hf,
+                                  int Wf, float sx, float sy, int Hb, int Wb, int mode, int rows_per_chunk, float *out,
+                                  void *workspace, int64_t workspace_bytes, int boxes_ready, void *stream);
 
 /* Bilinear corners for index-exactness checks: x0y0 [N][Hb][Wb][2] int32
  * (0 when both taps of an axis are out of range), wts [N][Hb][Wb][4] (nw, ne,

@@ -52,7 +52,17 @@ def _worker(rank, world, port, result_q):
                 (B, C) + per_view.shape[3:], -np.inf if mode == "max" else 0.0, np.float32)
             full = bev_dist.reduce_partial_bev(torch.from_numpy(partial), V, mode, gather=True)
             sl = bev_dist.reduce_partial_bev(torch.from_numpy(partial), V, mode, gather=False)
-            out[mode] = (full.numpy(), sl.numpy(), o.fuse(per_view, mode))
+            # the same partial in the rank-chunk-major layout the fused kernel writes for device groups
+            # (bev_ipm_warp_fuse_chunked_f32): [world, B, C, rows_per_rank, Wb], padding rows zero
+            Hb = partial.shape[2]
+            rpr = bev_dist.rows_per_rank(Hb, world)
+            pad = np.zeros((B, C, rpr * world, partial.shape[3]), np.float32)
+            pad[:, :, :Hb] = partial
+            ck = torch.from_numpy(np.ascontiguousarray(pad.reshape(B, C, world, rpr, -1).transpose(2, 0, 1, 3, 4)))
+            full_c = bev_dist.reduce_partial_bev(ck, V, mode, gather=True, bev_h=Hb)
+            sl_c = bev_dist.reduce_partial_bev(ck, V, mode, gather=False, bev_h=Hb)
+            same = bool(torch.equal(full_c, full) and torch.equal(sl_c, sl))
+            out[mode] = (full.numpy(), sl.numpy(), o.fuse(per_view, mode), same)
         result_q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -85,7 +95,8 @@ def test_camera_sharded_reduce_scatter(world):
         p.join(60)
         assert p.exitcode == 0
     for rank in range(world):
-        for mode, (full, sl, ref) in res[rank].items():
+        for mode, (full, sl, ref, same_chunked) in res[rank].items():
+            assert same_chunked, (mode, "chunk-major partial gives another result")
             scale = max(np.abs(ref).max(), 1e-30)
             if mode == "max":
                 assert np.array_equal(full, ref), mode  # max is order-independent

@@ -24,10 +24,11 @@ def main():
         c = per[max(per)]
         w = c["SQ_WAVES"]
         gui = c["GRBM_GUI_ACTIVE"] / 8.0
-        print(f"{os.path.basename(d):>5}: gui {gui:9.0f} cyc  valu/wave {c['SQ_INSTS_VALU'] / w:7.0f}  "
-              f"valu-cyc/wave {4 * c['SQ_ACTIVE_INST_VALU'] / w:8.0f}  lds/wave {c['SQ_INSTS_LDS'] / w:6.0f}  "
-              f"lds-cyc/wave {4 * c['SQ_ACTIVE_INST_LDS'] / w:7.0f}  conflicts/wave {c['SQ_LDS_BANK_CONFLICT'] / w:6.0f}  "
-              f"wave-cyc {4 * c['SQ_WAVE_CYCLES'] / w:8.0f}")
+        g = lambda k, s=1.0: f"{s * c[k] / w:8.0f}" if k in c else "       -"
+        print(f"{os.path.basename(d):>5}: gui {gui:9.0f} cyc  wave-cyc {g('SQ_WAVE_CYCLES', 4)}  valu {g('SQ_INSTS_VALU')}  "
+              f"valu-cyc {g('SQ_ACTIVE_INST_VALU', 4)}  lds {g('SQ_INSTS_LDS')}  lds-cyc {g('SQ_ACTIVE_INST_LDS', 4)}  "
+              f"conflicts {g('SQ_LDS_BANK_CONFLICT')}  salu {g('SQ_INSTS_SALU')}  smem {g('SQ_INSTS_SMEM')}  "
+              f"wait-any {g('SQ_WAIT_ANY', 4)}  wait-inst {g('SQ_WAIT_INST_ANY', 4)}  (per wave)")
 
 
 if __name__ == "__main__":

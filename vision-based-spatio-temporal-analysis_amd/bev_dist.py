@@ -31,8 +31,8 @@ from typing import Optional, Tuple
 import torch
 import torch.distributed as dist
 
-__all__ = ["frame_shard", "camera_shard", "reduce_partial_bev", "camera_sharded_forward", "materialize_lazy",
-           "ddp_wrap", "train_step"]
+__all__ = ["frame_shard", "camera_shard", "rows_per_rank", "reduce_partial_bev", "camera_sharded_forward",
+           "materialize_lazy", "ddp_wrap", "train_step"]
 
 
 def frame_shard(num_frames: int, rank: int, world: int) -> range:
@@ -50,32 +50,47 @@ def camera_shard(num_views: int, rank: int, world: int) -> Tuple[int, int]:
     return rg.start, rg.stop
 
 
-def reduce_partial_bev(partial: torch.Tensor, num_views: int, mode: str = "mean",
-                       group: Optional[dist.ProcessGroup] = None, gather: bool = False) -> torch.Tensor:
-    """Combine per-rank partial BEV maps [B, C, Hb, Wb] into the fused result.
+def rows_per_rank(Hb: int, world: int) -> int:
+    """BEV rows of each rank's slice of the reduce-scatter (ceil; the last slices shorter when world does not
+    divide Hb)."""
+    return -(-Hb // world)
 
-    `partial` is this rank's SUM over its cameras (mode sum/mean) or MAX over
-    them (mode max).  Returns this rank's row slice of the fused map (rows
-    [r * ceil(Hb / world), ...), the last slices shorter when Hb is not a
-    multiple of the group size), or the whole map when `gather` (one extra
-    all-gather).  One reduce-scatter over BEV rows is the only exchange.
+
+def reduce_partial_bev(partial: torch.Tensor, num_views: int, mode: str = "mean",
+                       group: Optional[dist.ProcessGroup] = None, gather: bool = False,
+                       bev_h: Optional[int] = None) -> torch.Tensor:
+    """Combine per-rank partial BEV maps into the fused result.
+
+    `partial` is this rank's SUM over its cameras (mode sum/mean) or MAX over them (mode max), either as a map
+    [B, C, Hb, Wb] or already in rank-chunk-major row order [world, B, C, rows_per_rank(Hb, world), Wb] with zero
+    padding rows (GeometryTransformer.forward_fused(rows_per_chunk=...), the fused kernel writing that order
+    directly; then `bev_h` = Hb).  Returns this rank's row slice of the fused map (rows [r * rpr, ...)), or the
+    whole map when `gather` (one extra all-gather).  One reduce-scatter over BEV rows is the only exchange; a
+    map-layout partial is first permuted into chunk order (one extra read + write of it).
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if partial.is_cuda and dist.get_backend(group) == "gloo":
         # gloo has no device collectives here: exchange through host memory (CPU-process-group tests and
         # hosts without RCCL); RCCL groups exchange device buffers directly over xGMI
-        out = reduce_partial_bev(partial.cpu(), num_views, mode, group, gather)
+        out = reduce_partial_bev(partial.cpu(), num_views, mode, group, gather, bev_h)
         return out.to(partial.device)
-    B, C, Hb, Wb = partial.shape
-    rpr = -(-Hb // world)  # rows per rank (ceil); the map is zero-padded to world * rpr rows
-    if rpr * world != Hb:
-        partial = torch.nn.functional.pad(partial, (0, 0, 0, rpr * world - Hb))
-    # rows-major chunks so that rank r's slice is the r-th contiguous chunk
-    x = partial.reshape(B, C, world, rpr, Wb).permute(2, 0, 1, 3, 4).contiguous()
+    if partial.dim() == 5:  # chunk-major already
+        if bev_h is None or partial.shape[0] != world or partial.shape[3] != rows_per_rank(bev_h, world):
+            raise ValueError("chunked partial: [world, B, C, rows_per_rank(bev_h, world), Wb] with bev_h given")
+        _, B, C, rpr, Wb = partial.shape
+        Hb = bev_h
+        x = partial
+    else:
+        B, C, Hb, Wb = partial.shape
+        rpr = rows_per_rank(Hb, world)  # the map is zero-padded to world * rpr rows
+        if rpr * world != Hb:
+            partial = torch.nn.functional.pad(partial, (0, 0, 0, rpr * world - Hb))
+        # rows-major chunks so that rank r's slice is the r-th contiguous chunk
+        x = partial.reshape(B, C, world, rpr, Wb).permute(2, 0, 1, 3, 4).contiguous()
     out = torch.empty(B, C, rpr, Wb, dtype=partial.dtype, device=partial.device)
     op = dist.ReduceOp.MAX if mode == "max" else dist.ReduceOp.SUM
-    dist.reduce_scatter_tensor(out, x.view(world * B, C, rpr, Wb), op=op, group=group)
+    dist.reduce_scatter_tensor(out, x.reshape(world * B, C, rpr, Wb), op=op, group=group)
     if mode == "mean":
         out = out / float(num_views)
     if not gather:
@@ -91,13 +106,23 @@ def camera_sharded_forward(geom, feats_local: torch.Tensor, K_local, Rt_local, i
                            gather: bool = False) -> torch.Tensor:
     """K5 path: this rank's cameras -> fused partial (HIP kernel) -> reduce-scatter over BEV rows.
     Without an initialised process group this process holds every camera: the fused kernel computes
-    the reduction directly (bit-identical to the reference)."""
+    the reduction directly (bit-identical to the reference).  On a device (RCCL) group the fused kernel writes its
+    partial in rank-chunk-major row order, so the reduce-scatter takes it without a permute copy."""
     if not dist.is_available() or not dist.is_initialized():
         if feats_local.shape[1] != num_views:
             raise ValueError("camera_sharded_forward without a process group needs all cameras")
         return geom.forward_fused(feats_local, K_local, Rt_local, img_size, mode)
     part_mode = "max" if mode == "max" else "sum"
-    partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
+    world = dist.get_world_size(group)
+    chunked = world > 1 and feats_local.is_cuda and dist.get_backend(group) != "gloo" and not (
+        torch.is_grad_enabled() and feats_local.requires_grad)
+    if chunked:
+        rpr = rows_per_rank(geom.bev_h, world)
+        partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode, rows_per_chunk=rpr)
+        if partial.dim() == 5:
+            return reduce_partial_bev(partial, num_views, mode, group, gather, bev_h=geom.bev_h)
+    else:
+        partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
     return reduce_partial_bev(partial, num_views, mode, group, gather)
 
 

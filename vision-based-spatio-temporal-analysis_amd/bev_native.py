@@ -19,7 +19,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -47,6 +47,8 @@ SIGNATURES = {
     "bev_ipm_warp_fuse_pre_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
                                       _i, _vp, _vp, _i64, _vp]),
     "bev_ipm_warp_fuse_boxes_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _i64, _vp]),
+    "bev_ipm_warp_fuse_chunked_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
+                                           _i, _i, _i, _vp, _vp, _i64, _i, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_ipm_warp_bwd_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _vp]),
     "bev_ipm_warp_bwd_ex_f32": (_i, [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _vp, _i64, _i64, _i64, _i64,
@@ -418,16 +420,21 @@ def warp_fuse_boxes(H: torch.Tensor, xs, ys, B: int, V: int, Hf: int, Wf: int, i
     sx, sy = _scales(Hf, Wf, img_hw)
     nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
     ws = torch.empty(max(nws, 8), device=H.device, dtype=torch.uint8)
-    rc = lib().bev_ipm_warp_fuse_boxes_f32(_ptr(H), _ptr(xs), _ptr(ys), B, V, Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode],
-                                           _ptr(ws), nws, _stream(H))
+    with _span("warp_boxes", H):
+        rc = lib().bev_ipm_warp_fuse_boxes_f32(_ptr(H), _ptr(xs), _ptr(ys), B, V, Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode],
+                                               _ptr(ws), nws, _stream(H))
     _check(rc, "bev_ipm_warp_fuse_boxes_f32")
     return ws
 
 
 def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, out: torch.Tensor = None,
-              boxes: torch.Tensor = None):
+              boxes: torch.Tensor = None, rows_per_chunk: int = None):
     """feats [B,V,C,Hf,Wf] (any strides within a map; maps b*V+v) -> out [B,C,Hb,Wb].  `boxes`: a workspace filled
-    by `warp_fuse_boxes` for this geometry and mode (the pre-pass is then not launched again)."""
+    by `warp_fuse_boxes` for this geometry and mode (the pre-pass is then not launched again).
+    `rows_per_chunk` (< Hb): the rank-chunk-major layout of bev_ipm_warp_fuse_chunked_f32 instead,
+    out [ceil(Hb / rpr), B, C, rpr, Wb] with the rows past Hb zero (the camera-shard reduce-scatter's input)."""
+    if rows_per_chunk is not None and rows_per_chunk < ys.numel():
+        return _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, int(rows_per_chunk), boxes)
     _require_gpu(feats, H, xs, ys)
     B, V, C, Hf, Wf = feats.shape
     if B * V > 0 and feats.stride(0) != V * feats.stride(1):
@@ -452,6 +459,31 @@ def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, o
         rc = fn(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf, Wf, sx, sy, Hb, Wb,
                 FUSE_MODES[mode], _ptr(out), _ptr(ws), nws, _stream(feats))
     _check(rc, "bev_ipm_warp_fuse")
+    return out
+
+
+def _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, rpr, boxes=None):
+    _require_gpu(feats, H, xs, ys)
+    B, V, C, Hf, Wf = feats.shape
+    if B * V > 0 and feats.stride(0) != V * feats.stride(1):
+        feats = feats.contiguous()
+    Hb, Wb = ys.numel(), xs.numel()
+    sx, sy = _scales(Hf, Wf, img_hw)
+    nck = -(-Hb // rpr)
+    out = torch.empty(nck, B, C, rpr, Wb, device=feats.device, dtype=torch.float32)
+    if nck * rpr > Hb:
+        out[-1, :, :, Hb - (nck - 1) * rpr:].zero_()  # padding rows: no cell writes them
+    s = feats.stride()
+    nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
+    ready = boxes is not None
+    if boxes is None and s[2] == 1 and C % 64 == 0 and V <= 64 and Hf < 16384 and Wf < 16384 and B * Hb * Wb > 0:
+        boxes, ready = warp_fuse_boxes(H, xs, ys, B, V, Hf, Wf, img_hw, mode), True
+    ws = boxes if boxes is not None else torch.empty(max(nws, 8), device=feats.device, dtype=torch.uint8)
+    with _span("warp_fuse", feats):
+        rc = lib().bev_ipm_warp_fuse_chunked_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B,
+                                                 V, C, Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], rpr, _ptr(out),
+                                                 _ptr(ws), nws, int(ready), _stream(feats))
+    _check(rc, "bev_ipm_warp_fuse_chunked_f32")
     return out
 
 

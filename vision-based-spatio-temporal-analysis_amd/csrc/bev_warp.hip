@@ -419,6 +419,67 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
     }
 }
 
+#ifndef WARP_DMA_ROWS
+#define WARP_DMA_ROWS 1  // fused warp v2 staging: 3 pixels of one box row per LDS-DMA instruction, no VALU (1) or dma_block
+#endif
+
+// The same image as dma_block (pixel p = py * sbw + px at `off` + 272 p, 17 slots of 16 B: 64 channels + pad) from
+// one LDS-DMA instruction per 3 pixels of a box row.  Lane l moves chunk l % 17 of pixel l / 17 of the instruction
+// (the pad slot and lanes 51-63 stay idle), so its global byte offset from the instruction's first pixel is a
+// per-lane constant; the pixel address itself is an SGPR base (global_load_lds_dwordx4 with saddr) and M0 the
+// instruction's first slot -- the per-instruction work is scalar.  Instructions are dealt round-robin over the
+// waves (row-major), so every wave issues about sbh * ceil(sbw / 3) / nwaves of them.  Element offsets are 32-bit
+// (the launcher checks that a feature map fits).
+__device__ __forceinline__ void dma_rows(const float *__restrict__ f, int sH, int sW, int sx0, int sy0, int sbw,
+                                         int sbh, unsigned char *smem, int off, int wave, int lane,
+                                         int nwaves = FT_NT / 64) {
+    if (WARP_ABLATE & 2) return;
+    const int lp = (lane * 241) >> 12;  // lane / 17 for lane < 64
+    const int ls = lane - 17 * lp;
+    const bool slot_ok = lp < 3 && ls < 16;
+    const unsigned voff = (unsigned)((lp * sW + ls * 4) * (int)sizeof(float));
+    const int per_row = (sbw + 2) / 3;
+    const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_base(smem) + (unsigned)off));
+    int py = 0, i = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: the loop runs on the scalar unit
+    while (i >= per_row && py < sbh) {  // instruction `wave` of the row-major order
+        i -= per_row;
+        ++py;
+    }
+    for (; py < sbh;) {
+        const int rem = sbw - 3 * i;  // pixels left in the row from this instruction's first (>= 1)
+        const float *src = f + (sy0 + py) * sH + (sx0 + 3 * i) * sW;
+        const unsigned dst = lds0 + (unsigned)((py * sbw + 3 * i) * 272);
+        if (slot_ok && lp < rem) {
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %1, %3" WARP_DMA_POLICY "\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"(voff), "s"(dst), "s"(src)
+                : "memory");
+        }
+        i += nwaves;
+        while (i >= per_row && py < sbh) {
+            i -= per_row;
+            ++py;
+        }
+    }
+}
+
+// bytes of the output from element `base` on, as a buffer bound (clamped to 32 bits: a chunk of 64 planes is < 4 GiB)
+__device__ __forceinline__ uint32_t out_range(size_t total_bytes, size_t base) {
+    const size_t r = total_bytes - base * sizeof(float);
+    return r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
+}
+
+#ifndef WARP_STAGE_ALL
+#define WARP_STAGE_ALL 1  // fused warp v2: all live views staged at once when they fit the pool (1) or always per view
+#endif
+// LDS bytes of an np-pixel footprint image (17-slot pixels); dma_block rounds to its 1-KiB instructions
+__device__ __forceinline__ int stage_bytes(int np) {
+    return WARP_DMA_ROWS ? np * 272 : ((np * 17 + 63) >> 6) * 1024;
+}
+
 #ifndef WARP_STORE_AUX
 #define WARP_STORE_AUX 2  // fused warp output stores: buffer cache policy (2 = nt, streaming; 0 = default)
 #endif
@@ -429,14 +490,29 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
 #define WARP_STAMP 0  // timing builds only (tools/warp_stamps.py): per-workgroup s_memtime stamps of the v2 phases
 #endif
 #if WARP_STAMP
-__device__ unsigned long long g_warp_stamp[16384 * 6];
-#define STAMP(k)                                                                                             \
+// per workgroup: [0..4] phases, [5] HW_ID | XCC_ID << 32, [6 + 3 v + k] view v < 6: taps done, sampled, barrier
+constexpr int STAMP_N = 24;
+__device__ unsigned long long g_warp_stamp[16384 * STAMP_N];
+#define STAMP_AT(k)                                                                                          \
     do {                                                                                                     \
         const unsigned sb_ = blockIdx.x + blockIdx.y * gridDim.x;                                            \
-        if (threadIdx.x == 0 && sb_ < 16384) g_warp_stamp[sb_ * 6 + (k)] = __builtin_amdgcn_s_memtime();      \
+        if (threadIdx.x == 0 && sb_ < 16384) g_warp_stamp[sb_ * STAMP_N + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#define STAMP(k)                                                                                             \
+    do {                                                                                                     \
+        STAMP_AT(k);                                                                                         \
+        const unsigned sb_ = blockIdx.x + blockIdx.y * gridDim.x;                                            \
+        if ((k) == 0 && threadIdx.x == 0 && sb_ < 16384)                                                     \
+            g_warp_stamp[sb_ * STAMP_N + 5] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |  \
+                                              ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32); \
+    } while (0)
+#define STAMP_VIEW(n, k) \
+    do {                 \
+        if ((n) < 6) STAMP_AT(6 + 3 * (n) + (k)); \
     } while (0)
 #else
 #define STAMP(k) ((void)0)
+#define STAMP_VIEW(n, k) ((void)0)
 #endif
 
 #ifndef WARP_LANESKIP
@@ -446,15 +522,43 @@ __device__ unsigned long long g_warp_stamp[16384 * 6];
 // the chunk, per-lane byte offset of the cell, SGPR byte offset of the channel
 // plane -> no per-store address arithmetic.  The dispatcher guarantees the
 // chunk (64 planes) spans < 4 GiB.  aux 2 = nt (streaming, written once).
+#ifndef WARP_MEAN_FP32
+#define WARP_MEAN_FP32 0  // fused warp v2 mean: Markstein fp32 division for the exhaustively verified V (1, A/B: slower), or div_rcp (0)
+#endif
+// acc / V for the mean: for V with bit V - 1 of MARKSTEIN_EXACT_V, q0 = a * RN(1/V) and one correction step
+// q0 + RN(a - q0 V) * RN(1/V) (two FMAs) is the correctly rounded quotient for every float but -0 (the view sum is
+// never -0) -- tools/verify_div_markstein_fix.c, exhaustive over all 2^32 inputs; infinities give NaN in the
+// correction, which the fix-up maps back to q0 (= +-inf, the IEEE quotient).  Other V: div_rcp through double.
+struct MeanDiv {
+    float vf, rf;
+    double rV;
+    bool fast;
+};
+__device__ __forceinline__ MeanDiv mean_div_of(int V) {
+    MeanDiv m;
+    m.vf = (float)V;
+    m.rV = recip_uniform(V);
+    m.rf = (float)m.rV;
+    m.fast = WARP_MEAN_FP32 && V >= 1 && V <= 64 && ((MARKSTEIN_EXACT_V >> (V - 1)) & 1ull);
+    return m;
+}
+__device__ __forceinline__ float mean_div(float a, const MeanDiv &m) {
+    if (m.fast) {
+        const float q0 = a * m.rf;
+        const float q = __builtin_fmaf(__builtin_fmaf(-q0, m.vf, a), m.rf, q0);
+        return q != q ? q0 : q;
+    }
+    return div_rcp(a, m.rV);
+}
+
 template <int N>
-__device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell, const float (&acc)[N], int mode,
-                                            double rV) {
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)(uint32_t)(plane * N * sizeof(float)), 0x00020000);
-    const int voff = cell * (int)sizeof(float);
+__device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int voff, const float (&acc)[N], int mode,
+                                            const MeanDiv &md, uint32_t range) {
+    // range: bytes addressable from `chunk` (the buffer's bound: an offset past it drops the store)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(chunk, 0, (int)range, 0x00020000);
     static_assert(N % 8 == 0, "stores in groups of 8 channels");
     if (WARP_ABLATE & 32) {  // timing only: the same bytes as 1-KiB coalesced 16-B-per-lane stores (wrong layout)
-        const int wb = __builtin_amdgcn_readfirstlane(cell) * N * (int)sizeof(float);
+        const int wb = __builtin_amdgcn_readfirstlane(voff) * N;
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int q = 0; q < N; q += 4) {
@@ -474,7 +578,7 @@ __device__ __forceinline__ void store_chunk(float *chunk, size_t plane, int cell
                      "+v"(a[7])::"memory");
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const float r = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? div_rcp(a[u], rV) : a[u];
+            const float r = (mode == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) ? mean_div(a[u], md) : a[u];
             if ((WARP_ABLATE & 16) && r != 1.2345e-30f) continue;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, voff,
                                                   (int)(uint32_t)((q0 + u) * plane * sizeof(float)),
@@ -607,6 +711,11 @@ __device__ __forceinline__ void zero_view(float (&acc)[N], int v) {
 // channels' four ds_read_b128 are in flight during this group's FMAs) ->
 // vmcnt(0) + one barrier.
 constexpr double EPS32 = 5.9604644775390625e-08;  // 2^-24
+// Footprint-box workspace: a 16-B header {BOX_MAGIC, maxpix, V, TH} (the fit test and tiling the boxes were made
+// for, written by k_warp_boxes) and then the boxes.  The fused kernel checks the header and, on a mismatch (boxes
+// made for another mode's pool, another pool knob, another V or tile shape), ignores the boxes and computes its own.
+constexpr unsigned BOX_MAGIC = 0x42455642u;  // "BVEB"
+constexpr int BOX_HDR = 16;                   // header bytes before the boxes
 constexpr int V2_MAXV = 64;                         // one view per lane
 
 // Conservative tap bbox of the BEV rectangle [xa, xb] x [ya, yb] (cell
@@ -726,9 +835,17 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t,
         if (g < NG - 1) {
             n0 = *(const f32x4 *)(a0 + (g + 1) * 16);
             n1 = *(const f32x4 *)(a1 + (g + 1) * 16);
-            n2 = *(const f32x4 *)(a2 + (g + 1) * 16);
-            n3 = *(const f32x4 *)(a3 + (g + 1) * 16);
+            if (WARP_ABLATE & 128) {  // timing only: half the LDS reads, the same arithmetic
+                n2 = n0;
+                n3 = n1;
+            } else {
+                n2 = *(const f32x4 *)(a2 + (g + 1) * 16);
+                n3 = *(const f32x4 *)(a3 + (g + 1) * 16);
+            }
         }
+        if ((WARP_ABLATE & 256) && (g & 1)) {  // timing only: half the arithmetic, the same LDS reads
+            acc[4 * g] += c0.x + c1.y + c2.z + c3.w;
+        } else
         bilerp4<MODE>(acc, 4 * g, c0, c1, c2, c3, t.w);
         __builtin_amdgcn_sched_barrier(0);  // at most two groups of reads in flight
         if (g < NG - 1) {
@@ -766,7 +883,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
                                                           int B, int V, int C, int Hf, int Wf, float sx, float sy,
                                                           int Hb, int Wb, float *__restrict__ out, int pool,
-                                                          const uint2 *__restrict__ boxes) {
+                                                          const uint2 *boxes, int rpr) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
     constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
@@ -787,8 +904,9 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     STAMP(0);
     int tr, tc;
     tile_cell<TH>(lane, wave, tr, tc);
-    auto dma = [&](const float *fp, int x0, int y0, int w, int n, int o) {
-        dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, n, smem, o, wave, lane, NW);
+    auto dma = [&](const float *fp, int x0, int y0, int w, int h, int o) {
+        if (WARP_DMA_ROWS) dma_rows(fp, (int)sH, (int)sW, x0, y0, w, h, smem, o, wave, lane, NW);
+        else dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, w * h, smem, o, wave, lane, NW);
     };
     const int i = tyb * TH + tr;
     const int j = txb * TW + tc;
@@ -796,10 +914,21 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
+    // output layout: [B][C][Hb][Wb] (rpr == Hb), or rank-chunk-major [ceil(Hb / rpr)][B][C][rpr][Wb] for the camera-shard
+    // reduce-scatter (BEV row r -> chunk r / rpr, its row r % rpr); the chunk is a per-lane byte offset (the launcher
+    // checks the whole output is < 2 GiB), the (frame, channel) base and the channel plane stay uniform
+    const size_t oplane = (size_t)rpr * Wb;
+    const int ck = inside ? i / rpr : 0;
+    const int ovoff = (int)(((size_t)ck * B * C * oplane + (size_t)(i - ck * rpr) * Wb + j) * sizeof(float));
+    const size_t orange = (size_t)((Hb + rpr - 1) / rpr) * B * C * oplane * sizeof(float);  // whole output, bytes
     const Grid grid = make_grid(Hf, Wf);
-    const double rV = recip_uniform(V);  // mean: acc / V via div_rcp (exact)
+    const MeanDiv md = mean_div_of(V);  // mean: acc / V (exact)
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes
+    if (boxes != nullptr) {  // boxes made for this kernel's fit test and tiling? (else: computed here)
+        const uint4 hd = reinterpret_cast<const uint4 *>(boxes)[-1];
+        if (hd.x != BOX_MAGIC || (int)hd.y != maxpix || (int)hd.z != V || (int)hd.w != TH) boxes = nullptr;
+    }
 
     // corner boxes of this tile for frame bb, lane v <-> view v, packed in two VGPRs (wave 0 computes them in
     // double, the others read them): lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16
@@ -895,6 +1024,53 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             }
             return u;
         };
+        if (WARP_STAGE_ALL) {
+            // ---- every live view's footprint at once: when all corner boxes apply and the images fit the pool
+            // together, they are staged back to back up front and the views are sampled with ONE wait + barrier
+            // per tile (instead of one per view) -- same taps, same view order, same arithmetic
+            int need = 0;  // lane v < V: view v's image bytes (0: empty view; huge: the corner box does not apply)
+            if (lane < V) {
+                const int x0 = (int)(lba & 0xffffu), y0 = (int)((lba >> 16) & 0x7fffu);
+                const int x1 = (int)(lbb & 0xffffu) - 1, y1 = (int)(lbb >> 16) - 1;
+                const int np = (x1 - x0 + 1) * (y1 - y0 + 1);
+                need = (lba >> 31) ? (1 << 26) : (x1 < 0 ? 0 : stage_bytes(np));
+            }
+            int tot = need;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+            tot = __builtin_amdgcn_readfirstlane(tot);
+            if (tot <= pool) {
+                int off = 0;
+                for (int u = 0; u < V; ++u) {
+                    const Box bx = box_of(u);
+                    if (bx.x1 < 0) continue;
+                    const int w = bx.x1 - bx.x0 + 1, h = bx.y1 - bx.y0 + 1;
+                    dma(fb + (int64_t)u * sN, bx.x0, bx.y0, w, h, off);
+                    off += stage_bytes(w * h);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();  // every image and the zero pixel
+                off = 0;
+                for (int u = 0; u < V; ++u) {
+                    const Box bx = box_of(u);
+                    if (bx.x1 < 0) {
+                        zero_view<MODE>(acc, u);
+                        continue;
+                    }
+                    const int w = bx.x1 - bx.x0 + 1;
+                    const Taps t = taps_of(u);
+                    if (__ballot(t.valid != 0) != 0ull && (!WARP_LANESKIP || t.valid))
+                        sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, w, zp, zp);
+                    else
+                        zero_view<MODE>(acc, u);
+                    off += stage_bytes(w * (bx.y1 - bx.y0 + 1));
+                }
+                if (inside) store_chunk(out + ((size_t)b * C + c0) * oplane, oplane, ovoff, acc, MODE, md,
+                                        out_range(orange, ((size_t)b * C + c0) * oplane));
+                if (c0 + 64 < C) __syncthreads();  // the next chunk re-stages the pool
+                continue;
+            }
+        }
         const int v_first = next_live(-1);
         // prologue: DMA of the first live view (if its corner box applies and fits)
         Box bn = box_of(v_first < V ? v_first : 0);
@@ -903,7 +1079,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
             if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
                 offn = 0;
-                dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, 0);
+                dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, 0);
             }
         }
         // the first live view's taps while its footprint lands (exact-bbox views reduce their taps first)
@@ -917,6 +1093,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         __syncthreads();  // zero pixel + image of the first live view
         STAMP(2);
 
+        int nview = 0;  // live views done (timing stamps)
         for (int v = v_first, vn; v < V; v = vn) {
             vn = next_live(v);
             Box bx = bn;
@@ -952,7 +1129,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 const bool single = (nbx == 1) && (nby == 1);
                 if (single)  // the common case: start the copy (the pool is free since the last
                              // end-of-view barrier), compute the taps while it lands
-                    dma(f, bx.x0, bx.y0, bw, bw * bh, 0);
+                    dma(f, bx.x0, bx.y0, bw, bh, 0);
                 if (!have_t) {
                     t = taps_of(v);
                     have_t = true;
@@ -971,7 +1148,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
                         if (!single) {
                             __syncthreads();  // earlier LDS images are no longer read
-                            dma(f, sx0, sy0, sbw, sbw * sbh, 0);
+                            dma(f, sx0, sy0, sbw, sbh, 0);
                         }
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         __syncthreads();
@@ -997,12 +1174,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
                     } else if (need <= off) offn = 0;
                     if (offn >= 0)
-                        dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, npix, offn);
+                        dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, offn);
                 }
             }
             // ---- sample view v from its prefetched image ------------------------------
             if (!done) {
                 if (!have_t) t = taps_of(v);
+                STAMP_VIEW(nview, 0);
                 if (WARP_ABLATE & 4) acc[0] += t.w[0] * t.w[3] + (float)(t.x0 + t.y0 + (int)t.valid);
                 else if (__ballot(t.valid != 0) != 0ull) {
                     // WARP_LANESKIP: lanes without a valid tap leave the LDS reads to the others (their sample is
@@ -1014,12 +1192,16 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             } else if (empty) {
                 zero_view<MODE>(acc, v);
             }
+            STAMP_VIEW(nview, 1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
             __syncthreads();  // all of it landed; image of view v and red[] are free
+            STAMP_VIEW(nview, 2);
+            ++nview;
         }
         STAMP(3);
         if (inside) {
-            store_chunk(out + ((size_t)b * C + c0) * plane, plane, i * Wb + j, acc, MODE, rV);
+            store_chunk(out + ((size_t)b * C + c0) * oplane, oplane, ovoff, acc, MODE, md,
+                                        out_range(orange, ((size_t)b * C + c0) * oplane));
         }
         STAMP(4);
       }
@@ -1034,6 +1216,8 @@ __global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hm
     const int ntx = (Wb + TW - 1) / TW, nt = ntx * nty;  // nty >= ceil(Hb / TH) box-tile rows (extra rows: empty)
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int b = blockIdx.y;
+    if (t == 0 && b == 0)
+        reinterpret_cast<uint4 *>(boxes)[-1] = make_uint4(BOX_MAGIC, (unsigned)maxpix, (unsigned)V, (unsigned)TH);
     if (t >= (int64_t)nt * V) return;
     const int tile = (int)(t / V), v = (int)(t - (int64_t)tile * V);
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
@@ -1440,7 +1624,7 @@ constexpr int V2_FIXED = 256 + 4 * (FT_NT / 64) * (int)sizeof(int) + V2_MAXV * 9
 template <int OCC>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
-                       int mode, float *out, hipStream_t st, int pool, uint2 *boxes, bool boxes_ready) {
+                       int mode, float *out, hipStream_t st, int pool, uint2 *boxes, bool boxes_ready, int rpr) {
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
     dim3 grid(ntiles, B), block(FT_NT);
@@ -1453,13 +1637,13 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
     }
     if (mode == BEV_FUSE_SUM)
         hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, rpr);
     else if (mode == BEV_FUSE_MEAN)
         hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, rpr);
     else
         hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes);
+                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, rpr);
     return last();
 }
 
@@ -1496,18 +1680,18 @@ inline int v2_pool_bytes(int mode) {
 
 inline int launch_fuse_v2(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat,
                           const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
-                          int Hb, int Wb, int mode, float *out, hipStream_t st, uint2 *boxes, bool boxes_ready = false) {
+                          int Hb, int Wb, int mode, float *out, hipStream_t st, uint2 *boxes, bool boxes_ready, int rpr) {
     if (mode == BEV_FUSE_MAX)  // MAX's extra live state spills at 3 workgroups per CU
         return launch_fuse_v2_occ<2>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
-                                     v2_pool_bytes(mode), boxes, boxes_ready);
+                                     v2_pool_bytes(mode), boxes, boxes_ready, rpr);
     return launch_fuse_v2_occ<WARP_OCC>(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out,
-                                        st, v2_pool_bytes(mode), boxes, boxes_ready);
+                                        st, v2_pool_bytes(mode), boxes, boxes_ready, rpr);
 }
 
 int warp_fuse_impl(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
                    const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
                    int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes, void *stream,
-                   bool boxes_ready);
+                   bool boxes_ready, int rpr);
 
 }  // namespace
 
@@ -1542,11 +1726,11 @@ int warp_tune(int knob, int value) {
 
 extern "C" {
 
-int bev_abi_version(void) { return 6; }
+int bev_abi_version(void) { return 7; }
 
 #if WARP_STAMP
 int bev_warp_stamp_read(unsigned long long *host, int n) {  // timing builds only
-    if (n > 16384 * 6) n = 16384 * 6;
+    if (n > 16384 * STAMP_N) n = 16384 * STAMP_N;
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_warp_stamp), (size_t)n * sizeof(unsigned long long), 0,
                                     hipMemcpyDeviceToHost);
 }
@@ -1601,7 +1785,7 @@ int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb) {
     // many)
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int64_t nt = (((int64_t)Wb + TW - 1) / TW) * (((int64_t)Hb + TH - 1) / TH);
-    return (int64_t)B * nt * V * (int64_t)sizeof(uint2);
+    return BOX_HDR + (int64_t)B * nt * V * (int64_t)sizeof(uint2);
 }
 
 int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
@@ -1616,7 +1800,7 @@ int bev_ipm_warp_fuse_ws_f32(const float *feats, int64_t sN, int64_t sC, int64_t
                              int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
                              void *stream) {
     return warp_fuse_impl(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, workspace,
-                          workspace_bytes, stream, false);
+                          workspace_bytes, stream, false, Hb);
 }
 
 int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
@@ -1624,7 +1808,16 @@ int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_
                               int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
                               void *stream) {
     return warp_fuse_impl(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, workspace,
-                          workspace_bytes, stream, true);
+                          workspace_bytes, stream, true, Hb);
+}
+
+int bev_ipm_warp_fuse_chunked_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW,
+                                  const float *Hmat, const float *xs, const float *ys, int B, int V, int C, int Hf,
+                                  int Wf, float sx, float sy, int Hb, int Wb, int mode, int rows_per_chunk, float *out,
+                                  void *workspace, int64_t workspace_bytes, int boxes_ready, void *stream) {
+    if (rows_per_chunk <= 0 || Hb <= 0) return BEV_ERR_ARGS;
+    return warp_fuse_impl(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, workspace,
+                          workspace_bytes, stream, boxes_ready != 0, rows_per_chunk < Hb ? rows_per_chunk : Hb);
 }
 
 int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float *ys, int B, int V, int Hf, int Wf,
@@ -1634,14 +1827,14 @@ int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float 
         return BEV_ERR_ARGS;
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX || Hf >= 16384 || Wf >= 16384) return BEV_ERR_ARGS;
     const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
-    if (!workspace || workspace_bytes < need || ((uintptr_t)workspace & 7) != 0) return BEV_ERR_ARGS;
+    if (!workspace || workspace_bytes < need || ((uintptr_t)workspace & 15) != 0) return BEV_ERR_ARGS;
     if (B == 0 || Hb == 0 || Wb == 0) return 0;
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
     const int maxpix = v2_pool_bytes(mode) / (17 * 16) - 4;  // k_warp_fuse_v2's own pool test
     hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                        (hipStream_t)stream, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH,
-                       reinterpret_cast<uint2 *>(workspace));
+                       reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR));
     return last();
 }
 
@@ -1651,7 +1844,7 @@ namespace {
 int warp_fuse_impl(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
                    const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb,
                    int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes, void *stream,
-                   bool boxes_ready) {
+                   bool boxes_ready, int rpr) {
     if (B < 0 || V <= 0 || C < 0 || Hf <= 0 || Wf <= 0 || Hb < 0 || Wb < 0 || B > 65535) return BEV_ERR_ARGS;
     if ((int64_t)Hf * Wf >= (1 << 22)) return BEV_ERR_ARGS;  // fast_div range of the footprint index
     if (mode < BEV_FUSE_SUM || mode > BEV_FUSE_MAX) return BEV_ERR_ARGS;
@@ -1663,17 +1856,24 @@ int warp_fuse_impl(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
                         ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) &&
                         (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) && (sN % 4 == 0) &&
                         (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32);
+    if (rpr != Hb) {  // rank-chunk-major output: the LDS-DMA kernel only, whole output < 2 GiB (per-lane offsets)
+        const int64_t nck = ((int64_t)Hb + rpr - 1) / rpr;
+        if (!dma_ok || g_warp_kernel == 1 || nck * rpr * (int64_t)B * C * Wb * (int64_t)sizeof(float) >= (1ll << 31))
+            return BEV_ERR_ARGS;
+    }
     if (dma_ok && g_warp_kernel != 1) {
         const int64_t need = bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb);
-        uint2 *boxes = (workspace && workspace_bytes >= need && ((uintptr_t)workspace & 7) == 0)
-                           ? reinterpret_cast<uint2 *>(workspace) : nullptr;
+        uint2 *boxes = (workspace && workspace_bytes >= need && ((uintptr_t)workspace & 15) == 0)
+                           ? reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR)
+                           : nullptr;
         // default: the per-view LDS-DMA kernel; 3: the DPP-row kernel (sum / mean, footprint boxes in the workspace;
         // measured slower at the bench geometry, profiles/r04g_warp_v3_vs_v2.txt)
-        if (g_warp_kernel == 3 && boxes && mode != BEV_FUSE_MAX && (int64_t)Hf * sH + (int64_t)Wf * sW < (1ll << 31))
+        if (g_warp_kernel == 3 && boxes && mode != BEV_FUSE_MAX && rpr == Hb &&
+            (int64_t)Hf * sH + (int64_t)Wf * sW < (1ll << 31))
             return launch_fuse_v3(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st,
                                   boxes);
         return launch_fuse_v2(feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st, boxes,
-                              boxes_ready);
+                              boxes_ready, rpr);
     }
     if (C <= 4)
         return launch_fuse_ck<4>(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, st);

@@ -56,7 +56,10 @@ class GradSink:
     """Carries a bottleneck's identity-shortcut gradient from its last conv node to its first conv node, which the
     backward runs later (it is upstream): the first conv's input-gradient conv then adds it in its epilogue instead
     of autograd summing the block input's two gradients in a separate pass (a full read-read-write of the block
-    input's size: 0.2-0.5 ms per block at the bench size)."""
+    input's size: 0.2-0.5 ms per block at the bench size).  It assumes the backward runs through the whole block
+    (conv3's node sets the hand-off, conv1's node consumes it); after a partial backward that stops between the two
+    (torch.autograd.grad with inputs inside the block) the hand-off is simply not consumed -- the gradient it carries
+    belongs to the block input, which that backward does not ask for -- and the block's next forward clears it."""
     __slots__ = ("grad",)
 
     def __init__(self):
@@ -89,6 +92,8 @@ class ConvBNAct(torch.autograd.Function):
     def forward(ctx, x, weight, gamma, beta, conv, bn, relu: bool, in_nchw: bool, residual, sink_in=None,
                 sink_out=None):
         ctx.sinks = (sink_in, sink_out)
+        if sink_in is not None:
+            sink_in.grad = None  # a stale hand-off of an earlier, partial backward (conv1's backward never ran)
         wf, bf, s, r = _fold(conv, bn)
         k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
         y = _nat.conv2d_nhwc(x, _nat.pack_conv_weight(wf), bf, conv.out_channels, k, k, st, p, relu,
@@ -157,6 +162,8 @@ class ConvBNTrain(torch.autograd.Function):
     def forward(ctx, x, weight, gamma, beta, conv, bn, act: int, in_nchw: bool, residual, sink_in=None,
                 sink_out=None):
         ctx.sinks = (sink_in, sink_out)
+        if sink_in is not None:
+            sink_in.grad = None  # a stale hand-off of an earlier, partial backward (conv1's backward never ran)
         k, st, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
         w = weight.detach().float().contiguous()
         Co = conv.out_channels

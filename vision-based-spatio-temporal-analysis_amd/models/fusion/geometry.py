@@ -22,7 +22,7 @@ the product; the CPU restatement lives in oracle/ for testing only).
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -299,9 +299,16 @@ class GeometryTransformer(nn.Module):
         return out.view(B, V, C, self.bev_h, self.bev_w)
 
     def forward_fused(self, feats: torch.Tensor, intrinsics, extrinsics, img_size: Tuple[int, int] = (1080, 1920),
-                      mode: str = "mean") -> torch.Tensor:
-        """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev]."""
+                      mode: str = "mean", rows_per_chunk: Optional[int] = None) -> torch.Tensor:
+        """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev].
+        rows_per_chunk (< H_bev, inference only): the same values in rank-chunk-major row order,
+        [ceil(H_bev / rows_per_chunk), B, C, rows_per_chunk, W_bev] (padding rows zero) -- the layout the camera-shard
+        reduce-scatter over BEV rows consumes without a permute (bev_dist.camera_sharded_forward)."""
         H, xs, ys, hw = self._sampling(feats, intrinsics, extrinsics, img_size)
+        if rows_per_chunk is not None and rows_per_chunk < self.bev_h:
+            if torch.is_grad_enabled() and feats.requires_grad:
+                raise RuntimeError("forward_fused(rows_per_chunk=...) is an inference layout (no autograd)")
+            return _nat.warp_fuse(feats, H, xs, ys, hw, mode, rows_per_chunk=rows_per_chunk)
         return _WarpFuseFn.apply(feats, H, xs, ys, hw, mode)
 
 
