@@ -25,6 +25,8 @@ def main():
     bits = sys.argv[1:] or ["0"]
     dev = torch.device("cuda")
     B, V, C, H, W, Hf, Wf = 2, 7, 64, 1080, 1920, 135, 240
+    if os.environ.get("GEOM") == "k5":  # BASELINE configs[4]: 16 cameras at 4K, one frame, SUM (the per-rank partial)
+        B, V, H, W, Hf, Wf = 1, 16, 2160, 3840, 270, 480
     feats = torch.randn(B, V, Hf, Wf, C, device=dev).permute(0, 1, 4, 2, 3)
     geom = GeometryTransformer(480, 1440, BOUNDS)
     K, Rt = bev_rig.rig(V, H, W, B)
@@ -33,12 +35,12 @@ def main():
     out = torch.empty(B, C, 480, 1440, device=dev)
     s = feats.stride()
     # a trailing "n" times the same library without the workspace (the in-kernel corner-box prologue)
-    libs = {b: ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{b.rstrip('n') or b}.so"))
+    libs = {b: ctypes.CDLL(os.path.join(REPO, "tools", "_ablate", f"libwarp_ablate_{(b.rstrip('n') or b).split('_p')[0]}.so"))
             for b in bits}  # "p0" / "w0": copies of libwarp_ablate_0.so built as p0 / w0 (their own knob state)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ws = torch.empty(nat.lib().bev_ipm_warp_fuse_workspace_bytes(B, V, 480, 1440), device=dev, dtype=torch.uint8)
     args = (nat._ptr(feats), s[1], s[2], s[3], s[4], nat._ptr(Hm), nat._ptr(xs), nat._ptr(ys), B, V, C, Hf, Wf, sx, sy,
-            480, 1440, 1, nat._ptr(out), nat._ptr(ws), ws.numel(), st)
+            480, 1440, 0 if os.environ.get("GEOM") == "k5" else 1, nat._ptr(out), nat._ptr(ws), ws.numel(), st)
     for L in libs.values():
         L.bev_ipm_warp_fuse_ws_f32.restype = ctypes.c_int
         L.bev_ipm_warp_fuse_ws_f32.argtypes = nat.SIGNATURES["bev_ipm_warp_fuse_ws_f32"][1]
@@ -51,6 +53,14 @@ def main():
             tune.restype = ctypes.c_int
             tune.argtypes = [ctypes.c_int, ctypes.c_int]
             assert tune(nat.TUNE_WARP_KERNEL, 2 if b.startswith("w") else 3) >= 0
+    pool_kb = os.environ.get("POOL_KB")  # a variant name containing "_p<KB>" sets that LDS pool (BEV_TUNE_WARP_POOL_KB)
+    for b, L in libs.items():
+        if "_p" in b:
+            tune = getattr(L, "_ZN3bev9warp_tuneEii")
+            tune.restype = ctypes.c_int
+            tune.argtypes = [ctypes.c_int, ctypes.c_int]
+            assert tune(nat.TUNE_WARP_POOL_KB, int(b.split("_p")[1].split("_")[0])) >= 0
+    del pool_kb
     for rnd in range(int(os.environ.get("ROUNDS", "5"))):
         for b, L in libs.items():
             a = args_n if b.endswith("n") else args

@@ -420,7 +420,7 @@ __device__ __forceinline__ void dma_block(const float *__restrict__ f, int sH, i
 }
 
 #ifndef WARP_DMA_ROWS
-#define WARP_DMA_ROWS 1  // fused warp v2 staging: 3 pixels of one box row per LDS-DMA instruction, no VALU (1) or dma_block
+#define WARP_DMA_ROWS 0  // fused warp v2 staging: 3 pixels of one box row per LDS-DMA instruction (1, A/B: neutral on K2, +4 % on K5) or dma_block (0)
 #endif
 
 // The same image as dma_block (pixel p = py * sbw + px at `off` + 272 p, 17 slots of 16 B: 64 channels + pad) from
@@ -473,7 +473,7 @@ __device__ __forceinline__ uint32_t out_range(size_t total_bytes, size_t base) {
 }
 
 #ifndef WARP_STAGE_ALL
-#define WARP_STAGE_ALL 1  // fused warp v2: all live views staged at once when they fit the pool (1) or always per view
+#define WARP_STAGE_ALL 0  // fused warp v2: all live views staged at once when they fit the pool (1, A/B: neutral) or per view (0)
 #endif
 // LDS bytes of an np-pixel footprint image (17-slot pixels); dma_block rounds to its 1-KiB instructions
 __device__ __forceinline__ int stage_bytes(int np) {
@@ -877,13 +877,13 @@ __device__ __forceinline__ void tile_cell(int lane, int wave, int &r, int &c) {
     }
 }
 
-template <int MODE, int OCC, int TH = 8>
+template <int MODE, int OCC, int TH = 8, bool CHUNK = false>
 __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                           int64_t sW, const float *__restrict__ Hmat,
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
                                                           int B, int V, int C, int Hf, int Wf, float sx, float sy,
                                                           int Hb, int Wb, float *__restrict__ out, int pool,
-                                                          const uint2 *boxes, int rpr) {
+                                                          const uint2 *__restrict__ boxes_in, int rpr) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
     constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
@@ -917,18 +917,30 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     // output layout: [B][C][Hb][Wb] (rpr == Hb), or rank-chunk-major [ceil(Hb / rpr)][B][C][rpr][Wb] for the camera-shard
     // reduce-scatter (BEV row r -> chunk r / rpr, its row r % rpr); the chunk is a per-lane byte offset (the launcher
     // checks the whole output is < 2 GiB), the (frame, channel) base and the channel plane stay uniform
-    const size_t oplane = (size_t)rpr * Wb;
-    const int ck = inside ? i / rpr : 0;
-    const int ovoff = (int)(((size_t)ck * B * C * oplane + (size_t)(i - ck * rpr) * Wb + j) * sizeof(float));
-    const size_t orange = (size_t)((Hb + rpr - 1) / rpr) * B * C * oplane * sizeof(float);  // whole output, bytes
+    // (CHUNK only: the plain layout keeps the round-4 addressing -- no extra live registers in the default kernel)
+    const size_t oplane = CHUNK ? (size_t)rpr * Wb : plane;
+    auto store_out = [&](int c0, const float (&acc)[64], const MeanDiv &md) {
+        if (!CHUNK) {
+            store_chunk(out + ((size_t)b * C + c0) * plane, plane, (i * Wb + j) * (int)sizeof(float), acc, MODE, md,
+                        (uint32_t)(plane * 64 * sizeof(float)));
+            return;
+        }
+        const int ck = i / rpr;
+        const int ovoff = (int)(((size_t)ck * B * C * oplane + (size_t)(i - ck * rpr) * Wb + j) * sizeof(float));
+        const size_t orange = (size_t)((Hb + rpr - 1) / rpr) * B * C * oplane * sizeof(float);  // whole output
+        store_chunk(out + ((size_t)b * C + c0) * oplane, oplane, ovoff, acc, MODE, md,
+                    out_range(orange, ((size_t)b * C + c0) * oplane));
+    };
     const Grid grid = make_grid(Hf, Wf);
     const MeanDiv md = mean_div_of(V);  // mean: acc / V (exact)
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes
-    if (boxes != nullptr) {  // boxes made for this kernel's fit test and tiling? (else: computed here)
-        const uint4 hd = reinterpret_cast<const uint4 *>(boxes)[-1];
-        if (hd.x != BOX_MAGIC || (int)hd.y != maxpix || (int)hd.z != V || (int)hd.w != TH) boxes = nullptr;
+    bool box_hdr_ok = false;  // boxes made for this kernel's fit test and tiling? (else: computed here)
+    if (boxes_in != nullptr) {
+        const uint4 hd = reinterpret_cast<const uint4 *>(boxes_in)[-1];
+        box_hdr_ok = hd.x == BOX_MAGIC && (int)hd.y == maxpix && (int)hd.z == V && (int)hd.w == TH;
     }
+    const uint2 *__restrict__ boxes = box_hdr_ok ? boxes_in : nullptr;
 
     // corner boxes of this tile for frame bb, lane v <-> view v, packed in two VGPRs (wave 0 computes them in
     // double, the others read them): lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16
@@ -1065,8 +1077,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         zero_view<MODE>(acc, u);
                     off += stage_bytes(w * (bx.y1 - bx.y0 + 1));
                 }
-                if (inside) store_chunk(out + ((size_t)b * C + c0) * oplane, oplane, ovoff, acc, MODE, md,
-                                        out_range(orange, ((size_t)b * C + c0) * oplane));
+                if (inside) store_out(c0, acc, md);
                 if (c0 + 64 < C) __syncthreads();  // the next chunk re-stages the pool
                 continue;
             }
@@ -1200,8 +1211,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         }
         STAMP(3);
         if (inside) {
-            store_chunk(out + ((size_t)b * C + c0) * oplane, oplane, ovoff, acc, MODE, md,
-                                        out_range(orange, ((size_t)b * C + c0) * oplane));
+            store_out(c0, acc, md);
         }
         STAMP(4);
       }
@@ -1635,15 +1645,17 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
         hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                            st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes);
     }
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
+                           out, pool, boxes, rpr);
+    };
+    const bool ck = rpr < Hb;  // rank-chunk-major output (camera-shard partials)
     if (mode == BEV_FUSE_SUM)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, rpr);
+        ck ? go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, true>) : go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, false>);
     else if (mode == BEV_FUSE_MEAN)
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, rpr);
+        ck ? go(k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, true>) : go(k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, false>);
     else
-        hipLaunchKernelGGL((k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH>), grid, block, lds, st, feats, sN, sH, sW, Hmat,
-                           xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, out, pool, boxes, rpr);
+        ck ? go(k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH, true>) : go(k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH, false>);
     return last();
 }
 
