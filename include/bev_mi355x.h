@@ -632,6 +632,15 @@ int bev_decode_nms_large_f32(const int32_t *cand_idx, const float *cand_score, c
 int bev_image_normalize_u8_f32(const uint8_t *src, int N, int H, int W, const float *mean, const float *std,
                                float *out, void *stream);
 
+/* BEVNet head operand (model_wrapper.py:69-75 -- proj bias add, pos-enc concat; the reference's torch.cat of the
+ * projection [B,P,Hb,Wb] and pos_enc [2,Hb,Wb]): x [B][Hb][Wb][cp] channels-last = (s + bias, pos, 0...) per cell, s the
+ * fused warp-sum of the projected views [B][P][Hb][Wb]; cp >= P + 2 (the head's padded input width), P <= 512.  The
+ * backward moves the first P channels of the head-input gradient gx [B][Hb][Wb][cp] back to gs [B][P][Hb][Wb] (the
+ * warp-sum's gradient).  Values bit-identical to torch's add + cat / slice + permute. */
+int bev_head_operand_f32(const float *s, const float *bias, const float *pos, int B, int P, int Hb, int Wb, int cp,
+                         float *x, void *stream);
+int bev_head_operand_bwd_f32(const float *gx, int B, int P, int Hb, int Wb, int cp, float *gs, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

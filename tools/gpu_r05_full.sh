@@ -12,4 +12,8 @@ timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --camera-shard --steps 10 --warmup 2 --cpu-iters 0 > $O/cam.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --backbone efficientnet_b3 --steps 20 --warmup 3 --cpu-iters 0 > $O/effb3.log 2>&1 || exit $?
+if [ -n "${TRAIN:-}" ]; then
+  timeout -k 10 300 python -u tools/train_step_bench.py --steps 5 --bevnet --amp > $O/train_amp.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tprof -o run -- python3 tools/train_step_bench.py --steps 3 --warmup 1 --bevnet --amp > $O/tprof.log 2>&1 || exit $?
+fi
 exit 0

@@ -47,6 +47,8 @@ SIGNATURES = {
     "bev_ipm_warp_fuse_pre_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i, _i,
                                       _i, _vp, _vp, _i64, _vp]),
     "bev_ipm_warp_fuse_boxes_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _i64, _vp]),
+    "bev_head_operand_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_head_operand_bwd_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_ipm_warp_fuse_chunked_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
                                            _i, _i, _i, _vp, _vp, _i64, _i, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
@@ -485,6 +487,28 @@ def _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, rpr, boxes=None):
                                                  _ptr(ws), nws, int(ready), _stream(feats))
     _check(rc, "bev_ipm_warp_fuse_chunked_f32")
     return out
+
+
+def head_operand(s: torch.Tensor, bias: torch.Tensor, pos: torch.Tensor, cp: int) -> torch.Tensor:
+    """s [B,P,Hb,Wb] contiguous, bias [P], pos [2,Hb,Wb] -> x [B,Hb,Wb,cp] channels-last (s + bias, pos, zeros)."""
+    _require_gpu(s, bias, pos)
+    s, bias, pos = s.contiguous(), bias.contiguous().float(), pos.contiguous().float()
+    B, P, Hb, Wb = s.shape
+    x = torch.empty(B, Hb, Wb, cp, device=s.device, dtype=torch.float32)
+    _check(lib().bev_head_operand_f32(_ptr(s), _ptr(bias), _ptr(pos), B, P, Hb, Wb, cp, _ptr(x), _stream(s)),
+           "bev_head_operand_f32")
+    return x
+
+
+def head_operand_bwd(gx: torch.Tensor, P: int) -> torch.Tensor:
+    """gx [B,Hb,Wb,cp] (channels contiguous) -> gs [B,P,Hb,Wb] = gx[..., :P] in NCHW."""
+    _require_gpu(gx)
+    gx = gx.contiguous()
+    B, Hb, Wb, cp = gx.shape
+    gs = torch.empty(B, P, Hb, Wb, device=gx.device, dtype=torch.float32)
+    _check(lib().bev_head_operand_bwd_f32(_ptr(gx), B, P, Hb, Wb, cp, _ptr(gs), _stream(gx)),
+           "bev_head_operand_bwd_f32")
+    return gs
 
 
 def taps(H, xs, ys, Hf, Wf, img_hw):

@@ -209,7 +209,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16(ConvH a) {
 // and the operands of steps s + 1 and s + 2 are in flight in two register sets while step s runs (ping-pong, two
 // steps per trip, no copies).  Same fragment map, same per-output K order (16-deep slices in increasing k): results
 // identical to k_conv_h16.
-constexpr int HBK2 = 64, HROW2 = 72;  // halves per LDS row: 64 + 8 pad = 144 B = 9 odd 16-B slots
+constexpr int HBK2 = 64, HROW2 = 72;
+// H16B_LINES 1: the fp16 operand and the weight panel are staged with eight lanes per 128-B K-step row, so every
+// wave load instruction reads whole lines (round 5); 0: the round-4 maps (4 / 2 lanes per row, 32-64 B pieces).
+#ifndef H16B_LINES
+#define H16B_LINES 1
+#endif  // halves per LDS row: 64 + 8 pad = 144 B = 9 odd 16-B slots
 
 // BatchNorm statistics of the conv output z = acc + bias (training forward, BN with batch statistics), fused into
 // the epilogue so z is not read back: per output column of the 128 x 128 tile, over the tile's valid rows,
@@ -308,51 +313,73 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
     if (mt >= ntm) return;
     const int64_t m0 = mt * HBM;
     const int n0 = nt * BN;
-    // A staging: rows (tid >> 2) + 64 q (q < 2), channel quads (tid & 3) + 4 u (u < 4): 64 channels per step,
-    // two rows of tap metadata per thread
-    const int aq = tid & 3;
-    int64_t pix[2];
-    int iy0[2], ix0[2];
-    bool rok[2];
+    // A staging.  fp32 operand: rows (tid >> 2) + 64 q (q < 2), channel quads (tid & 3) + 4 u (u < 4), 16-B loads.
+    // fp16 operand (H16B_LINES): rows (tid >> 3) + 32 q (q < 4), halves 8 (tid & 7) .. + 7 -- eight lanes read one
+    // pixel's 128-B K step, so each wave load is 8 whole lines instead of 16 rows x 32 B.
+    constexpr bool LN = HIN && H16B_LINES;
+    constexpr int NQ = LN ? 4 : 2, ARS = LN ? 32 : 64;
+    const int aq = LN ? (tid & 7) : (tid & 3), arow = LN ? (tid >> 3) : (tid >> 2);
+    int64_t pix[NQ];
+    int iy0[NQ], ix0[NQ];
+    bool rok[NQ];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int64_t m = m0 + (tid >> 2) + 64 * q;
+    for (int q = 0; q < NQ; ++q) {
+        const int64_t m = m0 + arow + ARS * q;
         rok[q] = m < a.M;
         const int64_t mm = rok[q] ? m : 0;
         const int ox = (int)(mm % a.Wo);
         const int64_t t = mm / a.Wo;
         const int oy = (int)(t % a.Ho);
         const int n = (int)(t / a.Ho);
-        pix[q] = (int64_t)n * a.H * a.W * a.Ci + 4 * aq;
+        pix[q] = (int64_t)n * a.H * a.W * a.Ci + (LN ? 8 : 4) * aq;
         iy0[q] = oy * a.stride - a.pad;
         ix0[q] = ox * a.stride - a.pad;
     }
-    // B staging: weight row n0 + (tid >> 1), halves 32 (tid & 1) .. + 31 of the K step (BN 64: row n0 + (tid >> 2),
-    // halves 16 (tid & 3) .. + 15)
-    const int brow = BN == 128 ? tid >> 1 : tid >> 2, bcol = BN == 128 ? 32 * (tid & 1) : 16 * (tid & 3);
+    // B staging (H16B_LINES): weight rows n0 + (tid >> 3) + 32 u (u < NBU), halves 8 (tid & 7) .. + 7 of the K step
+    // (whole 128-B lines per wave load).  Otherwise row n0 + (tid >> 1), halves 32 (tid & 1) .. + 31 (BN 64: row
+    // n0 + (tid >> 2), halves 16 (tid & 3) .. + 15).
+    const int brow = H16B_LINES ? tid >> 3 : BN == 128 ? tid >> 1 : tid >> 2;
+    const int bcol = H16B_LINES ? 8 * (tid & 7) : BN == 128 ? 32 * (tid & 1) : 16 * (tid & 3);
+    const int64_t bstep = H16B_LINES ? 32 * (int64_t)a.Kp : 8;  // halves between a thread's NBU weight loads
+    const int bls = H16B_LINES ? 32 * HROW2 : 8;                 // ... and between its LDS stores
     const _Float16 *wrow = a.wp + (int64_t)(n0 + brow) * a.Kp + bcol;
     int ky = 0, kx = 0, ci0 = 0;
     int64_t kb = 0;
     f32x4 ra0[8], ra1[8];
-    h16x4 rh0[8], rh1[8];
+    h16x8 rh0[4], rh1[4];  // LN: one 16-B line piece per row q; else pairs of the old map's 8-B quads
     u32x4 rb0[NBU], rb1[NBU];
 #define H16_GLOAD(RA, RH, RB)                                                                              \
     do {                                                                                                   \
         const int dy = ky * a.dil, dx = kx * a.dil;                                                        \
-        _Pragma("unroll") for (int q = 0; q < 2; ++q) {                                                    \
-            const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                                  \
-            const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;        \
-            const int64_t e = pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0;                              \
-            const int st = in ? 16 : 0; /* the zero quad is re-read for every u */                         \
-            if constexpr (HIN) {                                                                           \
-                const _Float16 *src = in ? a.xh + e : (const _Float16 *)g_hzero4;                          \
-                _Pragma("unroll") for (int u = 0; u < 4; ++u) RH[4 * q + u] = *(const h16x4 *)(src + st * u); \
-            } else {                                                                                       \
-                const float *src = in ? a.x + e : g_hzero4;                                                \
-                _Pragma("unroll") for (int u = 0; u < 4; ++u) RA[4 * q + u] = *(const f32x4 *)(src + st * u); \
+        if constexpr (LN) {                                                                                \
+            _Pragma("unroll") for (int q = 0; q < NQ; ++q) {                                               \
+                const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
+                const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
+                const int64_t e = pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0;                          \
+                RH[q] = *(const h16x8 *)(in ? a.xh + e : (const _Float16 *)g_hzero4);                      \
+            }                                                                                              \
+        } else {                                                                                           \
+            _Pragma("unroll") for (int q = 0; q < 2; ++q) {                                                \
+                const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
+                const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
+                const int64_t e = pix[q] + ((int64_t)iy * a.W + ix) * a.Ci + ci0;                          \
+                const int st = in ? 16 : 0; /* the zero quad is re-read for every u */                     \
+                if constexpr (HIN) {                                                                       \
+                    const _Float16 *src = in ? a.xh + e : (const _Float16 *)g_hzero4;                      \
+                    _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                        \
+                        const h16x4 v = *(const h16x4 *)(src + st * u);                                    \
+                        RH[(4 * q + u) >> 1][4 * (u & 1) + 0] = v[0];                                      \
+                        RH[(4 * q + u) >> 1][4 * (u & 1) + 1] = v[1];                                      \
+                        RH[(4 * q + u) >> 1][4 * (u & 1) + 2] = v[2];                                      \
+                        RH[(4 * q + u) >> 1][4 * (u & 1) + 3] = v[3];                                      \
+                    }                                                                                      \
+                } else {                                                                                   \
+                    const float *src = in ? a.x + e : g_hzero4;                                            \
+                    _Pragma("unroll") for (int u = 0; u < 4; ++u) RA[4 * q + u] = *(const f32x4 *)(src + st * u); \
+                }                                                                                          \
             }                                                                                              \
         }                                                                                                  \
-        _Pragma("unroll") for (int u = 0; u < NBU; ++u) RB[u] = *(const u32x4 *)(wrow + kb + 8 * u);       \
+        _Pragma("unroll") for (int u = 0; u < NBU; ++u) RB[u] = *(const u32x4 *)(wrow + kb + bstep * u);  \
         kb += HBK2;                                                                                        \
         ci0 += HBK2;                                                                                       \
         if (ci0 == a.Ci) {                                                                                 \
@@ -366,14 +393,20 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
 #define H16_SWRITE(BUF, RA, RH, RB)                                                                        \
     do {                                                                                                   \
         _Float16 *As = lds[BUF], *Bs = As + HBM * HROW2;                                                   \
-        _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                    \
-            h16x4 hv;                                                                                      \
-            if constexpr (HIN) hv = RH[q];                                                                 \
-            else hv = (h16x4){(_Float16)RA[q][0], (_Float16)RA[q][1], (_Float16)RA[q][2], (_Float16)RA[q][3]}; \
-            *(h16x4 *)(As + ((tid >> 2) + 64 * (q >> 2)) * HROW2 + 4 * aq + 16 * (q & 3)) = hv;            \
+        if constexpr (LN) {                                                                                \
+            _Pragma("unroll") for (int q = 0; q < NQ; ++q)                                                 \
+                *(h16x8 *)(As + (arow + 32 * q) * HROW2 + 8 * aq) = RH[q];                                 \
+        } else {                                                                                           \
+            _Pragma("unroll") for (int q = 0; q < 8; ++q) {                                                \
+                h16x4 hv;                                                                                  \
+                if constexpr (HIN) hv = (h16x4){RH[q >> 1][4 * (q & 1)], RH[q >> 1][4 * (q & 1) + 1],      \
+                                                RH[q >> 1][4 * (q & 1) + 2], RH[q >> 1][4 * (q & 1) + 3]}; \
+                else hv = (h16x4){(_Float16)RA[q][0], (_Float16)RA[q][1], (_Float16)RA[q][2], (_Float16)RA[q][3]}; \
+                *(h16x4 *)(As + (arow + 64 * (q >> 2)) * HROW2 + 4 * aq + 16 * (q & 3)) = hv;              \
+            }                                                                                              \
         }                                                                                                  \
         _Pragma("unroll") for (int u = 0; u < NBU; ++u)                                                    \
-            *(u32x4 *)(Bs + brow * HROW2 + bcol + 8 * u) = RB[u];                                          \
+            *(u32x4 *)(Bs + brow * HROW2 + bcol + bls * u) = RB[u];                                        \
     } while (0)
     f32x16 acc[TI][2];
 #pragma unroll

@@ -244,6 +244,122 @@ bool gn_shape_ok(int N, int64_t P, int C, int G) {
     return GN_T % QP == 0 && (C / G) % 4 == 0 && N <= 65535;
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// BEVNet head operand (model_wrapper.py:69-75): x[b, h, w, :] = [proj(concat)(b, :, h, w) + bias, pos_enc(:, h, w),
+// 0 ... 0] -- the fused warp-sum output (NCHW) plus the BEV projection's bias, the 2 positional channels and the
+// zero pad, written channels-last with `cp` channels per cell (what the head's convs read).  One workgroup per
+// (frame, BEV row, 64-cell run): the run's P channel rows are read coalesced along w into an LDS tile [64][P + 1],
+// the cells' cp channels are written coalesced (the 64 cells' rows form one contiguous block).  The backward
+// (k_head_operand_bwd) transposes the first P channels of the gradient back to NCHW the same way.  Values are
+// moved unchanged except the one fp32 add s + bias (the reference's own rounding of proj's bias add).
+constexpr int HO_T = 256, HO_RUN = 64;
+
+__global__ __launch_bounds__(HO_T) void k_head_operand(const float *__restrict__ s, const float *__restrict__ bias,
+                                                       const float *__restrict__ pos, int P, int Hb, int Wb, int cp,
+                                                       float *__restrict__ x) {
+    extern __shared__ float tile[];  // [HO_RUN][P + 1]
+    const int w0 = blockIdx.x * HO_RUN, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+    const int nw = min(HO_RUN, Wb - w0);
+    const size_t plane = (size_t)Hb * Wb;
+    for (int e = tid; e < P * HO_RUN; e += HO_T) {
+        const int c = e / HO_RUN, k = e - c * HO_RUN;
+        if (k < nw) tile[k * (P + 1) + c] = s[((size_t)b * P + c) * plane + (size_t)h * Wb + w0 + k] + bias[c];
+    }
+    __syncthreads();
+    float *xr = x + (((size_t)b * Hb + h) * Wb + w0) * cp;
+    for (int e = tid; e < nw * cp; e += HO_T) {
+        const int k = e / cp, c = e - k * cp;
+        float v = 0.0f;
+        if (c < P) v = tile[k * (P + 1) + c];
+        else if (c < P + 2) v = pos[(size_t)(c - P) * plane + (size_t)h * Wb + w0 + k];
+        xr[e] = v;
+    }
+}
+
+__global__ __launch_bounds__(HO_T) void k_head_operand_bwd(const float *__restrict__ gx, int P, int Hb, int Wb,
+                                                           int cp, float *__restrict__ gs) {
+    extern __shared__ float tile[];  // [HO_RUN][P + 1]
+    const int w0 = blockIdx.x * HO_RUN, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+    const int nw = min(HO_RUN, Wb - w0);
+    const size_t plane = (size_t)Hb * Wb;
+    const float *gr = gx + (((size_t)b * Hb + h) * Wb + w0) * cp;
+    for (int e = tid; e < nw * cp; e += HO_T) {
+        const int k = e / cp, c = e - k * cp;
+        if (c < P) tile[k * (P + 1) + c] = gr[e];
+    }
+    __syncthreads();
+    for (int e = tid; e < P * HO_RUN; e += HO_T) {
+        const int c = e / HO_RUN, k = e - c * HO_RUN;
+        if (k < nw) gs[((size_t)b * P + c) * plane + (size_t)h * Wb + w0 + k] = tile[k * (P + 1) + c];
+    }
+}
+
+// 16-B forms (Wb % 4 == 0, cp % 4 == 0, 16-B aligned buffers -- the bench geometry): sixteen lanes read one
+// channel row's 64 cells as float4 (256 B), the cells' block of 64 cp-channel rows is written as float4.  The
+// scalar forms above move 4 B per lane and divide by cp per element: 420 / 317 us at 480 x 1440 x P 128 (r05o).
+__global__ __launch_bounds__(HO_T) void k_head_operand_v4(const float *__restrict__ s, const float *__restrict__ bias,
+                                                          const float *__restrict__ pos, int P, int Hb, int Wb,
+                                                          int cp, float *__restrict__ x) {
+    extern __shared__ float tile[];  // [HO_RUN][P + 1]
+    const int w0 = blockIdx.x * HO_RUN, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+    const int nw = min(HO_RUN, Wb - w0), nq = nw / 4;  // Wb % 4 == 0: whole quads
+    const size_t plane = (size_t)Hb * Wb;
+    const float *sb = s + (size_t)b * P * plane + (size_t)h * Wb + w0;
+    for (int e = tid; e < P * (HO_RUN / 4); e += HO_T) {
+        const int c = e / (HO_RUN / 4), k4 = e % (HO_RUN / 4);
+        if (k4 < nq) {
+            const float4 v = *(const float4 *)(sb + (size_t)c * plane + 4 * k4);
+            const float bc = bias[c];
+            float *t = tile + 4 * k4 * (P + 1) + c;
+            t[0] = v.x + bc;
+            t[P + 1] = v.y + bc;
+            t[2 * (P + 1)] = v.z + bc;
+            t[3 * (P + 1)] = v.w + bc;
+        }
+    }
+    __syncthreads();
+    const int cq = cp / 4;
+    float4 *xr = reinterpret_cast<float4 *>(x + (((size_t)b * Hb + h) * Wb + w0) * cp);
+    const float *pr = pos + (size_t)h * Wb + w0;
+    for (int e = tid; e < nw * cq; e += HO_T) {
+        const int k = e / cq, c = 4 * (e - k * cq);
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int cc = c + u;
+            v[u] = cc < P ? tile[k * (P + 1) + cc] : cc < P + 2 ? pr[(size_t)(cc - P) * plane + k] : 0.0f;
+        }
+        xr[e] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+__global__ __launch_bounds__(HO_T) void k_head_operand_bwd_v4(const float *__restrict__ gx, int P, int Hb, int Wb,
+                                                              int cp, float *__restrict__ gs) {
+    extern __shared__ float tile[];  // [HO_RUN][P + 1]
+    const int w0 = blockIdx.x * HO_RUN, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+    const int nw = min(HO_RUN, Wb - w0), nq = nw / 4, cq = cp / 4, pq = (P + 3) / 4;
+    const size_t plane = (size_t)Hb * Wb;
+    const float4 *gr = reinterpret_cast<const float4 *>(gx + (((size_t)b * Hb + h) * Wb + w0) * cp);
+    for (int e = tid; e < nw * pq; e += HO_T) {
+        const int k = e / pq, c = 4 * (e - k * pq);
+        const float4 v = gr[(size_t)k * cq + c / 4];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (c + u < P) tile[k * (P + 1) + c + u] = vv[u];
+    }
+    __syncthreads();
+    float *gb = gs + (size_t)b * P * plane + (size_t)h * Wb + w0;
+    for (int e = tid; e < P * (HO_RUN / 4); e += HO_T) {
+        const int c = e / (HO_RUN / 4), k4 = e % (HO_RUN / 4);
+        if (k4 < nq) {
+            const float *t = tile + 4 * k4 * (P + 1) + c;
+            *(float4 *)(gb + (size_t)c * plane + 4 * k4) = make_float4(t[0], t[P + 1], t[2 * (P + 1)], t[3 * (P + 1)]);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -322,6 +438,34 @@ int bev_groupnorm_bwd_f32(const float *x, const float *dy, int N, int64_t P, int
                           float *dx, float *dgamma, float *dbeta, void *workspace, void *stream) {
     return bev_groupnorm_bwd_ex_f32(x, dy, N, P, C, G, mean, rstd, gamma, scale, shift, relu, dx, 0, dgamma, dbeta,
                                     workspace, stream);
+}
+
+int bev_head_operand_f32(const float *s, const float *bias, const float *pos, int B, int P, int Hb, int Wb, int cp,
+                         float *x, void *stream) {
+    if (!s || !bias || !pos || !x || B < 0 || P <= 0 || Hb < 0 || Wb < 0 || cp < P + 2 || B > 65535 || Hb > 65535 ||
+        P > 512)
+        return BEV_ERR_ARGS;
+    if (B == 0 || Hb == 0 || Wb == 0) return 0;
+    const size_t lds = (size_t)HO_RUN * (P + 1) * sizeof(float);
+    const dim3 grid((Wb + HO_RUN - 1) / HO_RUN, Hb, B);
+    if (Wb % 4 == 0 && cp % 4 == 0 && (((uintptr_t)s | (uintptr_t)pos | (uintptr_t)x) & 15) == 0)
+        hipLaunchKernelGGL(k_head_operand_v4, grid, dim3(HO_T), lds, (hipStream_t)stream, s, bias, pos, P, Hb, Wb, cp, x);
+    else
+        hipLaunchKernelGGL(k_head_operand, grid, dim3(HO_T), lds, (hipStream_t)stream, s, bias, pos, P, Hb, Wb, cp, x);
+    return (int)hipGetLastError();
+}
+
+int bev_head_operand_bwd_f32(const float *gx, int B, int P, int Hb, int Wb, int cp, float *gs, void *stream) {
+    if (!gx || !gs || B < 0 || P <= 0 || Hb < 0 || Wb < 0 || cp < P || B > 65535 || Hb > 65535 || P > 512)
+        return BEV_ERR_ARGS;
+    if (B == 0 || Hb == 0 || Wb == 0) return 0;
+    const size_t lds = (size_t)HO_RUN * (P + 1) * sizeof(float);
+    const dim3 grid((Wb + HO_RUN - 1) / HO_RUN, Hb, B);
+    if (Wb % 4 == 0 && cp % 4 == 0 && (((uintptr_t)gx | (uintptr_t)gs) & 15) == 0)
+        hipLaunchKernelGGL(k_head_operand_bwd_v4, grid, dim3(HO_T), lds, (hipStream_t)stream, gx, P, Hb, Wb, cp, gs);
+    else
+        hipLaunchKernelGGL(k_head_operand_bwd, grid, dim3(HO_T), lds, (hipStream_t)stream, gx, P, Hb, Wb, cp, gs);
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -472,6 +472,10 @@ __device__ __forceinline__ uint32_t out_range(size_t total_bytes, size_t base) {
     return r > 0xffffffffull ? 0xffffffffu : (uint32_t)r;
 }
 
+#ifndef WARP_TAPS_AHEAD
+#define WARP_TAPS_AHEAD 0  // fused warp v2: the next live view's taps computed before the end-of-view wait (1), inside
+                           // this view's LDS sampling after group WARP_TAPS_AHEAD - 2 (>= 2), or at its start (0)
+#endif
 #ifndef WARP_STAGE_ALL
 #define WARP_STAGE_ALL 0  // fused warp v2: all live views staged at once when they fit the pool (1, A/B: neutral) or per view (0)
 #endif
@@ -809,9 +813,13 @@ __device__ __forceinline__ void bilerp4(float (&acc)[N], int q0, const f32x4 &nw
 // each group's reads are issued right before its use -- fewer live registers, the
 // max reduction's choice).  Invalid taps read the zero pixel `zp` (the nw tap: `zp0`,
 // see k_warp_fuse_pc's blocked views).
-template <int MODE, int N, bool PIPE = true>
+struct NoMid {
+    __device__ __forceinline__ void operator()() const {}
+};
+// `mid` runs between LDS groups MID_G and MID_G + 1 (the next view's taps while this view's reads are in flight)
+template <int MODE, int N, bool PIPE = true, int MID_G = -1, class Mid = NoMid>
 __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t, const unsigned char *smem, int ib,
-                                                 int sx0, int sy0, int sbw, int zp, int zp0) {
+                                                 int sx0, int sy0, int sbw, int zp, int zp0, Mid mid = Mid()) {
     constexpr int PS = (N / 4 + 1) * 16, NG = N / 4;
     const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * PS;
     const unsigned char *a0 = smem + ((t.valid & 1) ? pb : zp0);
@@ -824,6 +832,7 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t,
             const f32x4 c0 = *(const f32x4 *)(a0 + g * 16), c1 = *(const f32x4 *)(a1 + g * 16);
             const f32x4 c2 = *(const f32x4 *)(a2 + g * 16), c3 = *(const f32x4 *)(a3 + g * 16);
             bilerp4<MODE>(acc, 4 * g, c0, c1, c2, c3, t.w);
+            if (g == MID_G) mid();
             __builtin_amdgcn_sched_barrier(0);
         }
         return;
@@ -847,6 +856,7 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t,
             acc[4 * g] += c0.x + c1.y + c2.z + c3.w;
         } else
         bilerp4<MODE>(acc, 4 * g, c0, c1, c2, c3, t.w);
+        if (g == MID_G) mid();
         __builtin_amdgcn_sched_barrier(0);  // at most two groups of reads in flight
         if (g < NG - 1) {
             c0 = n0;
@@ -1196,7 +1206,15 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 else if (__ballot(t.valid != 0) != 0ull) {
                     // WARP_LANESKIP: lanes without a valid tap leave the LDS reads to the others (their sample is
                     // +0: acc + 0 == acc exactly, max(acc, 0) for the max mode)
-                    if (!WARP_LANESKIP || t.valid)
+                    if (WARP_TAPS_AHEAD && vn < V && ok_of(vn)) {
+                        // the next view's taps inside this view's sampling, by every lane (a lane without a valid tap
+                        // reads the zero pixel: its sample is +0, i.e. acc + 0 == acc, or max(acc, +0) -- what the
+                        // lane skip gives)
+                        sample_view_pipe<MODE, 64, WARP_PIPE != 0, WARP_TAPS_AHEAD - 2>(
+                            acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp, [&]() { tf = taps_of(vn); });
+                        if (WARP_TAPS_AHEAD == 1) tf = taps_of(vn);  // after the sampling, before the DMA wait
+                        have_f = true;
+                    } else if (!WARP_LANESKIP || t.valid)
                         sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
                     else zero_view<MODE>(acc, v);
                 } else zero_view<MODE>(acc, v);

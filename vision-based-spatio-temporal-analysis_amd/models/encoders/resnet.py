@@ -446,12 +446,17 @@ class ResNet(nn.Module):
         for li, layer in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
             for blk in layer:
                 sc = y
+                h16 = self.h16_blocks and bottleneck_h16_ok(blk)
+                # downsample block as one H16 node: the node's input gradient (conv1's dgrad) goes to the downsample
+                # conv's dgrad epilogue (GradSink) instead of autograd adding the block input's two gradients
+                ds_sink = GradSink() if (h16 and blk.downsample is not None) else None
                 if blk.downsample is not None:
-                    sc = conv_bn_act(blk.downsample[0], blk.downsample[1], y, relu=False)
-                if self.h16_blocks and bottleneck_h16_ok(blk):  # AMP: one node, fp16-stored inner tensors
+                    sc = conv_bn_act(blk.downsample[0], blk.downsample[1], y, relu=False, sink_in=ds_sink)
+                if h16:  # AMP: one node, fp16-stored inner tensors
                     y = BottleneckTrainH16.apply(y, None if blk.downsample is None else sc, blk.conv1.weight,
                                                  blk.bn1.weight, blk.bn1.bias, blk.conv2.weight, blk.bn2.weight,
-                                                 blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, blk)
+                                                 blk.bn2.bias, blk.conv3.weight, blk.bn3.weight, blk.bn3.bias, blk,
+                                                 ds_sink)
                     continue
                 chain = blk.convs()
                 # identity shortcut: the residual's gradient goes to the first conv's dgrad epilogue (GradSink)

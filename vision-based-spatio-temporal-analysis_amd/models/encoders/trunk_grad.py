@@ -306,12 +306,15 @@ class BottleneckTrainH16(torch.autograd.Function):
     per-layer `ConvBNTrain` chain (`tests/test_train_amp_gpu.py::test_bottleneck_h16_block_bit_identical`), with
     half the bytes on those tensors.  The statistics come from the conv epilogues, the ReLU masks of y1 / y2 from
     z, and an identity shortcut's gradient is added in conv1's dgrad epilogue.  `sc`: the shortcut tensor (the
-    downsample branch's output), or None for the identity (x)."""
+    downsample branch's output), or None for the identity (x).  `x_sink` (downsample blocks): the node's gradient of x
+    is handed to the downsample conv's node (which consumes it as its dgrad epilogue's residual; that node's backward
+    runs after this one, since it needs d sc), instead of autograd summing the two gradients of x in a separate pass."""
 
     @staticmethod
     @_nat.amp_fwd
-    def forward(ctx, x, sc, w1, g1, b1, w2, g2, b2, w3, g3, b3, blk):
+    def forward(ctx, x, sc, w1, g1, b1, w2, g2, b2, w3, g3, b3, blk, x_sink=None):
         assert _nat.half_convs()
+        ctx.x_sink = x_sink  # downsample block: x's gradient from this node goes to the downsample conv's dgrad
         layers = ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2), (blk.conv3, blk.bn3))
         ws = (w1, w2, w3)
         gb = ((g1, b1), (g2, b2), (g3, b3))
@@ -357,7 +360,9 @@ class BottleneckTrainH16(torch.autograd.Function):
             g = _dgrad_h16(dz, wd, h.shape[1], h.shape[2], st, p, residual=res) if need else None
             grads[i] = (dw, dgm, dbt)
         dx = g
-        return (dx, dres if has_sc else None, *grads[0], *grads[1], *grads[2], None)
+        if ctx.x_sink is not None and dx is not None:  # added in the downsample conv's dgrad epilogue instead
+            ctx.x_sink.grad, dx = dx, None
+        return (dx, dres if has_sc else None, *grads[0], *grads[1], *grads[2], None, None)
 
 
 def bottleneck_h16_ok(blk) -> bool:

@@ -38,6 +38,27 @@ from .heads.detector import BEVDetector, _ceil_to
 AMP_FWD_HALF_PANELS = True  # autocast: the projection's forward packs fp16 panels (its backward's arithmetic)
 
 
+class _HeadOperand(torch.autograd.Function):
+    """x [B,Hb,Wb,cp] channels-last head operand = (s + bias, pos_enc, zeros) per cell (model_wrapper.py:69-75: the
+    BEV projection's bias add and the pos-enc concat), s [B,P,Hb,Wb] the fused warp-sum of the projected views: one
+    native transpose pass (bev_head_operand_f32) instead of torch's add, permuted cat and, backward, slice + permute;
+    the values are the same (one fp32 add).  Gradients: s gets gx[..., :P] back in NCHW, bias its sum over (b, h, w)
+    (torch's reduction of the broadcast add's gradient); pos_enc is a buffer."""
+
+    @staticmethod
+    @_nat.amp_fwd
+    def forward(ctx, s, bias, pos, cp):
+        ctx.P = s.shape[1]
+        return _nat.head_operand(s, bias, pos, cp)
+
+    @staticmethod
+    @_nat.amp_bwd
+    def backward(ctx, gx):
+        gs = _nat.head_operand_bwd(gx, ctx.P)
+        gb = gs.sum((0, 2, 3)) if ctx.needs_input_grad[1] else None
+        return gs, gb, None, None
+
+
 class _ViewProjection(torch.autograd.Function):
     """g[b, v] = W_v (1x1) f[b, v] for channels-last per-camera maps f [B,V,C,Hf,Wf]; returns the projected
     maps as a [B,V,P,Hf,Wf] view of a [B,V,Hf,Wf,P] buffer (the layout the fused warp reads)."""
@@ -159,7 +180,7 @@ class BEVNet(nn.Module):
             return self.fusion(per_view.view(B, V, C, self.bev_h, self.bev_w))
         g = _ViewProjection.apply(feats, self.proj.weight, self._view_panels(V, C))
         s = _WarpFuseFn.apply(g, H, xs, ys, img_hw, "sum")
-        return s + self.proj.bias.view(1, -1, 1, 1)
+        return s, self.proj.bias  # the bias is added where the head operand is assembled (_HeadOperand)
 
     def forward(self, batch: Dict) -> Dict:
         images = batch["images"]  # [B, V, 3, H, W]
@@ -170,16 +191,24 @@ class BEVNet(nn.Module):
         # quirk Q1: network-input size; warp_impl='kornia' -> grid_sample semantics unless KORNIA_AVAILABLE
         H, xs, ys, hw = self.geom._sampling(feats, K, Rt, (Hi, Wi))
         main = self._bev_main(feats, H, xs, ys, hw)
+        bias = None
+        if isinstance(main, tuple):
+            main, bias = main
         P = main.shape[1]
         if self.detector is None:
             self.detector = BEVDetector(in_channels=P + 2, bev_bounds=self.bounds, bev_size=(self.bev_h, self.bev_w),
                                         default_box_wh=self.default_box_wh).to(main.device)
         cp = self.detector.input_channels_padded
-        pos = self.pos_enc.permute(1, 2, 0).unsqueeze(0).expand(B, -1, -1, -1)
-        parts = [main.permute(0, 2, 3, 1), pos]
-        if cp > P + 2:
-            parts.append(main.new_zeros(B, self.bev_h, self.bev_w, cp - P - 2))
-        x = torch.cat(parts, dim=-1)  # [B, Hb, Wb, cp] channels-last head operand
+        if bias is not None and P <= 512 and main.is_cuda:
+            x = _HeadOperand.apply(main, bias, self.pos_enc, cp)  # [B, Hb, Wb, cp] channels-last head operand
+        else:
+            if bias is not None:
+                main = main + bias.view(1, -1, 1, 1)
+            pos = self.pos_enc.permute(1, 2, 0).unsqueeze(0).expand(B, -1, -1, -1)
+            parts = [main.permute(0, 2, 3, 1), pos]
+            if cp > P + 2:
+                parts.append(main.new_zeros(B, self.bev_h, self.bev_w, cp - P - 2))
+            x = torch.cat(parts, dim=-1)  # [B, Hb, Wb, cp] channels-last head operand
         det = self.detector.forward_nhwc(x)
         boxes, scores = self.detector.decode(det["heatmap"], det["offset"], det["size"],
                                              conf_thresh=self.conf_thresh, nms_dist_m=self.nms_dist_m)
