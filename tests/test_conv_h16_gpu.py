@@ -181,3 +181,38 @@ def test_wgrad_h16_vs_float64_of_rounded_operands(shape, kern):
     raw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (Co, Ci, K, K), dz.double().permute(0, 3, 1, 2),
                                       st, pad, dil)
     assert float((raw - ref).abs().max()) > 10 * float(err.max())
+
+
+@pytest.mark.parametrize("shape", [
+    dict(N=2, H=20, W=24, Ci=64, Co=128, K=3, stride=1, pad=1, dil=1),
+    dict(N=1, H=33, W=17, Ci=32, Co=200, K=3, stride=2, pad=1, dil=1),
+    dict(N=1, H=24, W=72, Ci=160, Co=512, K=3, stride=1, pad=1, dil=1),   # the head's conv1: taps inside 128-k tiles
+    dict(N=1, H=16, W=70, Ci=512, Co=128, K=3, stride=1, pad=2, dil=2),   # head conv2 (dilated)
+    dict(N=2, H=16, W=19, Ci=128, Co=36, K=3, stride=1, pad=2, dil=2),    # Co % 8 != 0: the register-transpose kernel
+    dict(N=3, H=9, W=11, Ci=96, Co=8, K=1, stride=1, pad=0, dil=1),
+    dict(N=1, H=45, W=60, Ci=256, Co=64, K=1, stride=2, pad=0, dil=1),    # the trunk's strided 1x1 downsample
+    dict(N=1, H=110, W=110, Ci=64, Co=64, K=3, stride=1, pad=1, dil=1),   # many 64-pixel steps per workgroup
+], ids=lambda d: f"{d['Ci']}to{d['Co']}k{d['K']}s{d['stride']}d{d['dil']}h{d['H']}")
+@pytest.mark.parametrize("x_half", [True, False], ids=["xh", "xf"])
+def test_wgrad_h16_fp16_gradient_vs_float64(shape, x_half):
+    """conv_wgrad_h16_any with the gradient stored in fp16 (the AMP training step's dgrad / BatchNorm-backward
+    outputs) and x in fp16 or fp32: k_wgrad_h16c (natural [pixel][channel] LDS images, transposing
+    ds_read_b64_tr_b16 fragment reads) where Ci, Co % 8 == 0, else k_wgrad_h16b; against the float64 weight gradient
+    of the fp16 operands, relative to sum |terms| < 2e-6."""
+    import bev_native as nat
+    N, H, W, Ci, Co, K = shape["N"], shape["H"], shape["W"], shape["Ci"], shape["Co"], shape["K"]
+    st, pad, dil = shape["stride"], shape["pad"], shape["dil"]
+    g = torch.Generator().manual_seed(Ci + Co + K)
+    x = torch.randn(N, H, W, Ci, generator=g)
+    Ho = (H + 2 * pad - dil * (K - 1) - 1) // st + 1
+    Wo = (W + 2 * pad - dil * (K - 1) - 1) // st + 1
+    dz = (torch.randn(N, Ho, Wo, Co, generator=g) * 1e-3).half()
+    xd = x.to(DEV).half() if x_half else x.to(DEV)
+    dw = nat.conv_wgrad_h16_any(xd, dz.to(DEV), K, K, st, pad, dilation=dil)
+    torch.cuda.synchronize()
+    xh, dh = x.half().double().permute(0, 3, 1, 2), dz.double().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(xh, (Co, Ci, K, K), dh, st, pad, dil)
+    mag = torch.nn.grad.conv2d_weight(xh.abs(), (Co, Ci, K, K), dh.abs(), st, pad, dil)
+    err = (dw.cpu().double() - ref).abs()
+    assert dw.shape == (Co, Ci, K, K)
+    assert float((err / (mag + 1e-12)).max()) < 2e-6

@@ -23,13 +23,16 @@ def main():
                 continue
             d = int(r["Dispatch_Id"])
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
-            names[d] = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:60]
+            names[d] = (r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][:50] + " grid "
+                        + r.get("Grid_Size", "?"))
         for d, c in per.items():
             w = c.get("SQ_WAVES", 0) or 1
             for k, v in c.items():
-                agg[names[d]][k].append(v if k in ("GRBM_GUI_ACTIVE", "SQ_WAVES") or k.startswith("TCC") else
+                agg[names[d]][k].append(v if k in ("GRBM_GUI_ACTIVE", "SQ_WAVES", "FETCH_SIZE", "WRITE_SIZE") or k.startswith("TCC") else
                                         v * (4 if k in QUAD else 1) / w)
     for n, c in agg.items():
+        if "conv" not in n and "wgrad" not in n and sub == "":
+            continue
         print(n)
         for k in sorted(c):
             v = c[k]

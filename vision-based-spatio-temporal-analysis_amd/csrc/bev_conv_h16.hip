@@ -214,6 +214,9 @@ constexpr int HBK2 = 64, HROW2 = 72;
 // wave load instruction reads whole lines (round 5); 0: the round-4 maps (4 / 2 lanes per row, 32-64 B pieces).
 #ifndef H16B_LINES
 #define H16B_LINES 1
+#endif
+#ifndef H16B_BUF
+#define H16B_BUF 1
 #endif  // halves per LDS row: 64 + 8 pad = 144 B = 9 odd 16-B slots
 
 // BatchNorm statistics of the conv output z = acc + bias (training forward, BN with batch statistics), fused into
@@ -295,7 +298,12 @@ __device__ __forceinline__ void h16_tile_stats(const ConvH &a, const f32x16 (&ac
 // BN: output columns per workgroup.  128: 2 x 2 waves of 64 x 64 (2 x 2 MFMA tiles each); 64 (outputs of <= 64
 // channels: no zero half of the panel loaded or multiplied): 4 x 1 waves of 32 x 64 (1 x 2 tiles).  Per output the
 // K order is the same, so both give identical conv results.
-template <bool HIN, int BN>
+// BUF (fp16 operand, H16B_LINES, operand and panel < 2 GiB): the staging loads are raw buffer loads with 32-bit
+// offsets -- per row a constant base, per K step one uniform tap offset (SGPR), and taps outside the image read
+// through an out-of-range offset, which the buffer returns as zeros; the weight panel's K step is the SGPR soffset.
+// Same values in LDS, so results are identical to the pointer form (r05q counters: ~7 VALU per MFMA there, mostly
+// 64-bit address arithmetic).
+template <bool HIN, int BN, bool BUF = false>
 __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
     constexpr int TI = BN == 128 ? 2 : 1, WROWS = BN == 128 ? 64 : 32, NBU = BN == 128 ? 4 : 2;
     __shared__ __attribute__((aligned(16))) _Float16 lds[2][(HBM + BN) * HROW2];
@@ -343,6 +351,22 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
     const int64_t bstep = H16B_LINES ? 32 * (int64_t)a.Kp : 8;  // halves between a thread's NBU weight loads
     const int bls = H16B_LINES ? 32 * HROW2 : 8;                 // ... and between its LDS stores
     const _Float16 *wrow = a.wp + (int64_t)(n0 + brow) * a.Kp + bcol;
+    static_assert(!BUF || LN, "buffer staging: fp16 operand, whole-line map");
+    __amdgpu_buffer_rsrc_t rsx, rsw;
+    int xrb[NQ], wvo[NBU];  // BUF: byte offsets of row q's (0, 0) tap piece / of weight load u at K step 0
+    if constexpr (BUF) {
+        rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(a.xh), 0,
+                                                (int)((int64_t)a.N * a.H * a.W * a.Ci * 2), 0x00020000);
+        rsw = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16 *>(a.wp), 0,
+                                                (int)(copad_h(a.Co) * (int64_t)a.Kp * 2), 0x00020000);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int n = (int)((pix[q] - 8 * aq) / ((int64_t)a.H * a.W * a.Ci));
+            xrb[q] = (((n * a.H + iy0[q]) * a.W + ix0[q]) * a.Ci + 8 * aq) * 2;
+        }
+#pragma unroll
+        for (int u = 0; u < NBU; ++u) wvo[u] = ((n0 + brow + 32 * u) * a.Kp + bcol) * 2;
+    }
     int ky = 0, kx = 0, ci0 = 0;
     int64_t kb = 0;
     f32x4 ra0[8], ra1[8];
@@ -351,7 +375,15 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
 #define H16_GLOAD(RA, RH, RB)                                                                              \
     do {                                                                                                   \
         const int dy = ky * a.dil, dx = kx * a.dil;                                                        \
-        if constexpr (LN) {                                                                                \
+        if constexpr (BUF) {                                                                               \
+            const int toff = ((dy * a.W + dx) * a.Ci + ci0) * 2; /* uniform */                             \
+            _Pragma("unroll") for (int q = 0; q < NQ; ++q) {                                               \
+                const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
+                const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
+                RH[q] = __builtin_bit_cast(h16x8, __builtin_amdgcn_raw_buffer_load_b128(                   \
+                                                      rsx, in ? xrb[q] + toff : (int)0x80000000, 0, 0));   \
+            }                                                                                              \
+        } else if constexpr (LN) {                                                                         \
             _Pragma("unroll") for (int q = 0; q < NQ; ++q) {                                               \
                 const int iy = iy0[q] + dy, ix = ix0[q] + dx;                                              \
                 const bool in = rok[q] && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;    \
@@ -379,7 +411,12 @@ __global__ __launch_bounds__(256, 2) void k_conv_h16b(ConvH a) {
                 }                                                                                          \
             }                                                                                              \
         }                                                                                                  \
-        _Pragma("unroll") for (int u = 0; u < NBU; ++u) RB[u] = *(const u32x4 *)(wrow + kb + bstep * u);  \
+        if constexpr (BUF) {                                                                               \
+            _Pragma("unroll") for (int u = 0; u < NBU; ++u) RB[u] = __builtin_bit_cast(                    \
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsw, wvo[u], (int)kb * 2, 0));                \
+        } else {                                                                                           \
+            _Pragma("unroll") for (int u = 0; u < NBU; ++u) RB[u] = *(const u32x4 *)(wrow + kb + bstep * u); \
+        }                                                                                                  \
         kb += HBK2;                                                                                        \
         ci0 += HBK2;                                                                                       \
         if (ci0 == a.Ci) {                                                                                 \
@@ -786,6 +823,203 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
         }
 }
 
+// ---- k_wgrad_h16c: natural [pixel][channel] LDS images read back with the transposing ds_read_b64_tr_b16 --------
+// k_wgrad_h16b transposes in registers (each thread gathers 8 pixels of a channel into one ds_write_b128): ~20 VALU
+// per MFMA and 0.20 MFMA utilisation in its counters (profiles/r05q_conv_h16_pmc.txt).  Here each thread loads 16-B
+// pieces of pixel rows -- dz[m][co0 + 8 c .. + 7] and the tap's x[pixel][ci .. ci + 7] -- and stores them unchanged
+// into [64 pixels][128 channels] images (256-B rows, XOR-swizzled 16-B chunks, cdna_hip_programming.md T10 (b):
+// conflict-free for the 32x32x16 transposed reads); the MFMA fragments (8 consecutive pixels of one channel per
+// lane) are two ds_read_b64_tr_b16 each.  Same tiles, pixel chunks and per-slice pixel order as k_wgrad_h16b, so
+// every workgroup's partial tile is bit-identical to it; only the float-atomic order across chunks varies (as
+// there).  dz in fp16; x in fp16 (XH) or fp32 (rounded to fp16 in the staging write, as k_wgrad_h16b does).
+// Requires Ci % 8 == 0 and Co % 8 == 0 (a 16-B piece inside one tap / one output row) and 16-B aligned operands.
+#ifndef H16_WGRAD_TR
+#define H16_WGRAD_TR 1
+#endif
+typedef short s16x4v __attribute__((vector_size(8)));
+
+__device__ __forceinline__ h16x4 lds_tr16(const _Float16 *p) {
+    return __builtin_bit_cast(
+        h16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4v *)(_Float16 *)p));
+}
+
+__device__ __forceinline__ int tr_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+template <bool XH>
+__global__ __launch_bounds__(256, 2) void k_wgrad_h16c(const float *__restrict__ x, const _Float16 *__restrict__ dz,
+                                                        int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
+                                                        int K, int stride, int pad, int dil, int64_t mchunk, int ctiles,
+                                                        int ntiles, float *__restrict__ dW) {
+    constexpr int IMG = WMS2 * WT;  // halves per operand image: 64 pixel rows x 128 channels
+    __shared__ __attribute__((aligned(16))) _Float16 lds[2][2 * IMG];
+    unsigned bid = blockIdx.x;
+    {
+        const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
+        bid = (xc < r ? xc * (q + 1) : r * (q + 1) + (xc - r) * q) + bid / 8;
+    }
+    const int tile = (int)(bid % (unsigned)ntiles);
+    const int split = (int)(bid / (unsigned)ntiles);
+    const int co0 = (tile % ctiles) * WT, k0 = (tile / ctiles) * WT;
+    const int M = N * Ho * Wo;  // the launcher checks that every offset fits in 31 bits
+    const int mb = split * (int)mchunk, me = mb + (int)mchunk < M ? mb + (int)mchunk : M;
+    if (mb >= me) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    // staging: ONE pixel row per thread and step, prow = tid >> 2, its 16-B pieces cq + 4 u (u < 4), cq = tid & 3:
+    // one address per operand and step; four lanes cover 64 contiguous bytes of a row per load instruction
+    const int prow = tid >> 2, cq = tid & 3;
+    int dzo = (mb + prow) * Co + co0 + 8 * cq;  // dz offset of piece 0 (pieces u at + 32 u halves)
+    unsigned cmask = 0;                         // pieces inside [0, Co) / [0, K)
+    int xoff[4], xdy[4], xdx[4];                // per piece: offset from the pixel's (0, 0) tap, tap displacement
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int c = co0 + 8 * (cq + 4 * u), k = k0 + 8 * (cq + 4 * u);
+        if (c < Co) cmask |= 1u << u;
+        const bool kok = k < K;
+        if (kok) cmask |= 16u << u;
+        const int tap = kok ? k / Ci : 0, ci = k - tap * Ci, ky = tap / KW, kx = tap - ky * KW;
+        xdy[u] = ky * dil - pad;
+        xdx[u] = kx * dil - pad;
+        xoff[u] = (xdy[u] * W + xdx[u]) * Ci + ci;
+    }
+    int px, py, pn;  // (column, row, image) of this thread's pixel row in the next step to load
+    {
+        const int m = mb + prow, t = m / Wo;
+        px = m - t * Wo;
+        py = t % Ho;
+        pn = t / Ho;
+    }
+    int ms = mb;
+    const int soff = tr_swz(prow);  // rows prow: chunk c of the row sits at c ^ soff
+    const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+    const h16x8 hz = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f,
+                      (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+#define WG16C_LOAD(RD, RX, RF)                                                                                 \
+    do {                                                                                                       \
+        const bool mok = ms + prow < me;                                                                       \
+        const int iy0 = py * stride, ix0 = px * stride;                                                        \
+        const int xb = ((pn * H + iy0) * W + ix0) * Ci;                                                        \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                        \
+            RD[u] = (mok && (cmask >> u & 1)) ? *(const h16x8 *)(dz + dzo + 32 * u) : hz;                      \
+            const int iy = iy0 + xdy[u], ix = ix0 + xdx[u];                                                    \
+            const bool in = mok && (cmask >> (4 + u) & 1) && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W; \
+            if constexpr (XH) {                                                                                \
+                RX[u] = in ? *(const h16x8 *)((const _Float16 *)x + (xb + xoff[u])) : hz;                      \
+            } else {                                                                                           \
+                RF[2 * u] = in ? *(const f32x4 *)(x + (xb + xoff[u])) : z4;                                    \
+                RF[2 * u + 1] = in ? *(const f32x4 *)(x + (xb + xoff[u] + 4)) : z4;                            \
+            }                                                                                                  \
+        }                                                                                                      \
+        dzo += WMS2 * Co;                                                                                      \
+        ms += WMS2;                                                                                            \
+        px += WMS2;                                                                                            \
+        while (px >= Wo) {                                                                                     \
+            px -= Wo;                                                                                          \
+            if (++py == Ho) {                                                                                  \
+                py = 0;                                                                                        \
+                ++pn;                                                                                          \
+            }                                                                                                  \
+        }                                                                                                      \
+    } while (0)
+#define WG16C_STORE(BUF, RD, RX, RF)                                                                           \
+    do {                                                                                                       \
+        _Float16 *Ds = lds[BUF] + prow * WT, *Xs = Ds + IMG;                                                   \
+        _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                        \
+            const int o = 8 * ((cq + 4 * u) ^ soff);                                                           \
+            *(h16x8 *)(Ds + o) = RD[u];                                                                        \
+            if constexpr (XH) {                                                                                \
+                *(h16x8 *)(Xs + o) = RX[u];                                                                    \
+            } else {                                                                                           \
+                const f32x4 a_ = RF[2 * u], b_ = RF[2 * u + 1];                                                \
+                *(h16x8 *)(Xs + o) = (h16x8){(_Float16)a_[0], (_Float16)a_[1], (_Float16)a_[2], (_Float16)a_[3], \
+                                             (_Float16)b_[0], (_Float16)b_[1], (_Float16)b_[2], (_Float16)b_[3]}; \
+            }                                                                                                  \
+        }                                                                                                      \
+    } while (0)
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+    // transposed fragment reads: 16-lane group g = lane >> 4 reads rows kk 16 + 8 (g >> 1) + {0..3} and {4..7} of
+    // the 16 columns cb + 16 (g & 1) ..; lane 4 q + p of the group addresses row q, columns 4 p .. 4 p + 3
+    const int li = lane & 15, g = lane >> 4, q = li >> 2, p = li & 3;
+    const int rq = 8 * (g >> 1) + q;                                                    // row within a 16-row slice
+    const int cg = 2 * (g & 1) + (p >> 1), sw0 = tr_swz(rq), sw1 = tr_swz(rq + 4), hp = 4 * (p & 1);
+    const int r32 = lane & 31, h = lane >> 5;
+#define WG16C_FRAG(IMGP, KK, CB, F)                                                                            \
+    do {                                                                                                       \
+        const int ch_ = (CB) / 8 + cg;                                                                         \
+        const h16x4 lo_ = lds_tr16((IMGP) + ((KK) * 16 + rq) * WT + 8 * (ch_ ^ sw0) + hp);                     \
+        const h16x4 hi_ = lds_tr16((IMGP) + ((KK) * 16 + rq + 4) * WT + 8 * (ch_ ^ sw1) + hp);                 \
+        F = __builtin_shufflevector(lo_, hi_, 0, 1, 2, 3, 4, 5, 6, 7);                                         \
+    } while (0)
+#define WG16C_MFMA(BUF)                                                                                        \
+    do {                                                                                                       \
+        const _Float16 *Ds = lds[BUF], *Xs = Ds + IMG;                                                         \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk) {                                                     \
+            h16x8 fa[2], fb[2];                                                                                \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i) WG16C_FRAG(Ds, kk, wm * 64 + i * 32, fa[i]);         \
+            _Pragma("unroll") for (int j = 0; j < 2; ++j) WG16C_FRAG(Xs, kk, wn * 64 + j * 32, fb[j]);         \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                      \
+                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);      \
+            __builtin_amdgcn_sched_barrier(0);                                                                 \
+        }                                                                                                      \
+    } while (0)
+    h16x8 rd0[4], rd1[4], rx0[4], rx1[4];
+    f32x4 rf0[8], rf1[8];
+    const int nk = (int)((me - mb + WMS2 - 1) / WMS2);
+    WG16C_LOAD(rd0, rx0, rf0);
+    if (nk > 1) WG16C_LOAD(rd1, rx1, rf1);
+    WG16C_STORE(0, rd0, rx0, rf0);
+    __syncthreads();
+    int ks = 0;  // loop head: LDS buffer 0 holds step ks, register set 1 step ks + 1
+    for (; ks + 3 < nk; ks += 2) {
+        WG16C_LOAD(rd0, rx0, rf0);
+        WG16C_MFMA(0);
+        WG16C_STORE(1, rd1, rx1, rf1);
+        __syncthreads();
+        WG16C_LOAD(rd1, rx1, rf1);
+        WG16C_MFMA(1);
+        WG16C_STORE(0, rd0, rx0, rf0);
+        __syncthreads();
+    }
+    if (ks + 2 < nk) {
+        WG16C_LOAD(rd0, rx0, rf0);
+        WG16C_MFMA(0);
+        WG16C_STORE(1, rd1, rx1, rf1);
+        __syncthreads();
+        WG16C_MFMA(1);
+        WG16C_STORE(0, rd0, rx0, rf0);
+        __syncthreads();
+        WG16C_MFMA(0);
+    } else if (ks + 1 < nk) {
+        WG16C_MFMA(0);
+        WG16C_STORE(1, rd1, rx1, rf1);
+        __syncthreads();
+        WG16C_MFMA(1);
+    } else {
+        WG16C_MFMA(0);
+    }
+#undef WG16C_MFMA
+#undef WG16C_FRAG
+#undef WG16C_STORE
+#undef WG16C_LOAD
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int kc = k0 + wn * 64 + j * 32 + r32;
+            if (kc >= K) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int cr = co0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (cr < Co) atomicAdd(dW + (int64_t)cr * K + kc, acc[i][j][r]);
+            }
+        }
+}
+
 }  // namespace
 
 namespace bev {
@@ -825,7 +1059,14 @@ int bev_conv_wgrad_h16_ex_f32(const void *xv, int x_half, int N, int H, int W, i
     mc = ((mc + step - 1) / step) * step;
     sp = (M + mc - 1) / mc;
     if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    if (deep) {
+    const bool tr = H16_WGRAD_TR && deep && dz_half && Ci % 8 == 0 && Co % 8 == 0 &&
+                    (((uintptr_t)x | (uintptr_t)dz) & 15) == 0 && M * Co < ((int64_t)1 << 31) - WMS2 * Co &&
+                    (int64_t)N * H * W * Ci < ((int64_t)1 << 31);  // k_wgrad_h16c: 32-bit offsets
+    if (tr) {
+        auto kern = x_half ? k_wgrad_h16c<true> : k_wgrad_h16c<false>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, (const _Float16 *)dz, N, H, W, Ci,
+                           Ho, Wo, Co, KW, K, stride, pad, dilation, mc, ct, nt, dW);
+    } else if (deep) {
         auto kern = x_half ? (dz_half ? k_wgrad_h16b<true, true> : k_wgrad_h16b<true, false>)
                            : (dz_half ? k_wgrad_h16b<false, true> : k_wgrad_h16b<false, false>);
         hipLaunchKernelGGL(kern, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, dz, N, H, W, Ci, Ho, Wo, Co, KW, K,
@@ -895,8 +1136,15 @@ static int conv_h16(const void *xv, int x_half, int N, int H, int W, int Ci, con
     const dim3 g((unsigned)blocks), b(256);
     hipStream_t st = (hipStream_t)stream;
     if (wide) {
-        void (*kern)(ConvH) = n64 ? (x_half ? k_conv_h16b<true, 64> : k_conv_h16b<false, 64>)
-                                  : (x_half ? k_conv_h16b<true, 128> : k_conv_h16b<false, 128>);
+        // 32-bit buffer offsets: operand and panel below 2 GiB (every in-image byte offset, and the out-of-range
+        // sentinel 2^31 above them all)
+        const bool buf = H16B_BUF && H16B_LINES && x_half &&
+                         (int64_t)N * H * W * Ci * 2 < ((int64_t)1 << 31) - 16 &&
+                         copad_h(Co) * (int64_t)a.Kp * 2 < ((int64_t)1 << 31) - 16;
+        void (*kern)(ConvH) = n64 ? (x_half ? (buf ? k_conv_h16b<true, 64, true> : k_conv_h16b<true, 64>)
+                                            : k_conv_h16b<false, 64>)
+                                  : (x_half ? (buf ? k_conv_h16b<true, 128, true> : k_conv_h16b<true, 128>)
+                                            : k_conv_h16b<false, 128>);
         hipLaunchKernelGGL(kern, g, b, 0, st, a);
     }
     else
