@@ -313,6 +313,71 @@ __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__rest
 }
 
 
+// Row-block forms of the two streaming passes (round 5), used when 256 % (C / 4) == 0 (every ResNet trunk width):
+// grid = blocks of BNQ_ROWS rows, thread = (channel quad q, row phase), the quad's per-channel constants in registers
+// for the whole block -- the grid-stride forms above decode the channel per float4 and re-load 4-7 per-channel
+// values per element.  Same arithmetic per element, so identical results.
+constexpr int BNQ_ROWS = 256;
+
+template <typename OT>
+__global__ __launch_bounds__(256) void k_bn_apply_q(const float *__restrict__ z, int64_t M, int C,
+                                                    const float *__restrict__ scale, const float *__restrict__ shift,
+                                                    const float *__restrict__ res, int act, OT *__restrict__ y) {
+    const int tid = threadIdx.x, QP = C / 4, q = tid % QP, ph = tid / QP, nph = 256 / QP;
+    const int64_t r0 = (int64_t)blockIdx.x * BNQ_ROWS, r1 = r0 + BNQ_ROWS < M ? r0 + BNQ_ROWS : M;
+    const float4 s = *(const float4 *)(scale + 4 * q), h = *(const float4 *)(shift + 4 * q);
+    for (int64_t r = r0 + ph; r < r1; r += nph) {
+        const int64_t e = r * C + 4 * q;
+        const float4 v = *(const float4 *)(z + e);
+        float4 o = make_float4(bn_u(v.x, s.x, h.x), bn_u(v.y, s.y, h.y), bn_u(v.z, s.z, h.z), bn_u(v.w, s.w, h.w));
+        if (res) {
+            const float4 rr = *(const float4 *)(res + e);
+            o = make_float4(o.x + rr.x, o.y + rr.y, o.z + rr.z, o.w + rr.w);
+        }
+        if (act == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+        if (act == 2) o = make_float4(silu_hw(o.x), silu_hw(o.y), silu_hw(o.z), silu_hw(o.w));
+        st4(y, e, o);
+    }
+}
+
+template <typename OT>
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_q(const float *__restrict__ dy, const float *__restrict__ y,
+                                                        const float *__restrict__ z, int64_t M, int C,
+                                                        const float *__restrict__ mean, const float *__restrict__ rstd,
+                                                        const float *__restrict__ gamma,
+                                                        const float *__restrict__ scale,
+                                                        const float *__restrict__ shift, int act,
+                                                        const float *__restrict__ coef, OT *__restrict__ dz,
+                                                        float *__restrict__ dres) {
+    const int tid = threadIdx.x, QP = C / 4, q = tid % QP, ph = tid / QP, nph = 256 / QP;
+    const int64_t r0 = (int64_t)blockIdx.x * BNQ_ROWS, r1 = r0 + BNQ_ROWS < M ? r0 + BNQ_ROWS : M;
+    const int c0 = 4 * q;
+    float mu[4], rs[4], gr[4], k1[4], k2[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        mu[u] = mean[c0 + u];
+        rs[u] = rstd[c0 + u];
+        gr[u] = gamma[c0 + u] * rstd[c0 + u];
+        k1[u] = coef[2 * (c0 + u)];
+        k2[u] = coef[2 * (c0 + u) + 1];
+    }
+    for (int64_t r = r0 + ph; r < r1; r += nph) {
+        const int64_t e = r * C + c0;
+        const float4 d = *(const float4 *)(dy + e), v = *(const float4 *)(z + e);
+        float g[4];
+        act_grad(g, d, y, v, scale, shift, act, e, c0);
+        const float zv[4] = {v.x, v.y, v.z, v.w};
+        float o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float xh = (zv[u] - mu[u]) * rs[u];
+            o[u] = gr[u] * (g[u] - k1[u] - xh * k2[u]);
+        }
+        st4(dz, e, make_float4(o[0], o[1], o[2], o[3]));
+        if (dres) *(float4 *)(dres + e) = make_float4(g[0], g[1], g[2], g[3]);
+    }
+}
+
 // ---- per-image channel sums and channel affine (SqueezeExcite training) -------------------------------
 struct Prod {  // (x * x2, unused)
     const float *x, *x2;
@@ -413,6 +478,16 @@ int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *sc
     const int64_t total4 = M * C / 4;
     const dim3 g(stream_blocks(total4));
     hipStream_t st = (hipStream_t)stream;
+    if (256 % (C / 4) == 0) {
+        const dim3 gq((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS));
+        if (y_half)
+            hipLaunchKernelGGL(k_bn_apply_q<_Float16>, gq, dim3(256), 0, st, z, M, C, scale, shift, residual, act,
+                               (_Float16 *)y);
+        else
+            hipLaunchKernelGGL(k_bn_apply_q<float>, gq, dim3(256), 0, st, z, M, C, scale, shift, residual, act,
+                               (float *)y);
+        return (int)hipGetLastError();
+    }
     const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
     if (y_half && small)
         hipLaunchKernelGGL((k_bn_apply<uint32_t, _Float16>), g, dim3(256), 0, st, z, C, scale, shift, residual, act,
@@ -452,6 +527,16 @@ int bev_batchnorm_bwd_ex_f32(const float *dy, const float *y, const float *z, in
                        frozen, coef, dgamma, dbeta);
     const int64_t total4 = M * C / 4;
     const dim3 g(stream_blocks(total4));
+    if (256 % (C / 4) == 0) {
+        const dim3 gq((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS));
+        if (dz_half)
+            hipLaunchKernelGGL(k_bn_bwd_apply_q<_Float16>, gq, dim3(256), 0, st, dy, y, z, M, C, mean, rstd, gamma,
+                               scale, shift, act, coef, (_Float16 *)dz, dres);
+        else
+            hipLaunchKernelGGL(k_bn_bwd_apply_q<float>, gq, dim3(256), 0, st, dy, y, z, M, C, mean, rstd, gamma,
+                               scale, shift, act, coef, (float *)dz, dres);
+        return (int)hipGetLastError();
+    }
     const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
     if (dz_half && small)
         hipLaunchKernelGGL((k_bn_bwd_apply<uint32_t, _Float16>), g, dim3(256), 0, st, dy, y, z, C, mean, rstd, gamma,

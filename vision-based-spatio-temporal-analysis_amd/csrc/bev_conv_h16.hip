@@ -831,7 +831,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16b(const float *__restrict__
 // conflict-free for the 32x32x16 transposed reads); the MFMA fragments (8 consecutive pixels of one channel per
 // lane) are two ds_read_b64_tr_b16 each.  Same tiles, pixel chunks and per-slice pixel order as k_wgrad_h16b, so
 // every workgroup's partial tile is bit-identical to it; only the float-atomic order across chunks varies (as
-// there).  dz in fp16; x in fp16 (XH) or fp32 (rounded to fp16 in the staging write, as k_wgrad_h16b does).
+// there).  dz (DH) and x (XH) in fp16, or fp32 rounded to fp16 in the staging write (as k_wgrad_h16b does).
 // Requires Ci % 8 == 0 and Co % 8 == 0 (a 16-B piece inside one tap / one output row) and 16-B aligned operands.
 #ifndef H16_WGRAD_TR
 #define H16_WGRAD_TR 1
@@ -845,13 +845,15 @@ __device__ __forceinline__ h16x4 lds_tr16(const _Float16 *p) {
 
 __device__ __forceinline__ int tr_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-template <bool XH>
-__global__ __launch_bounds__(256, 2) void k_wgrad_h16c(const float *__restrict__ x, const _Float16 *__restrict__ dz,
+template <bool XH, bool DH>
+__global__ __launch_bounds__(256, 2) void k_wgrad_h16c(const float *__restrict__ x, const void *__restrict__ dzv,
                                                         int N, int H, int W, int Ci, int Ho, int Wo, int Co, int KW,
                                                         int K, int stride, int pad, int dil, int64_t mchunk, int ctiles,
                                                         int ntiles, float *__restrict__ dW) {
     constexpr int IMG = WMS2 * WT;  // halves per operand image: 64 pixel rows x 128 channels
     __shared__ __attribute__((aligned(16))) _Float16 lds[2][2 * IMG];
+    const _Float16 *dz = (const _Float16 *)dzv;  // DH: fp16 gradient; else fp32 (dzf), rounded while staging
+    const float *dzf = (const float *)dzv;
     unsigned bid = blockIdx.x;
     {
         const unsigned nb = gridDim.x, q = nb / 8, r = nb % 8, xc = bid % 8;
@@ -894,13 +896,19 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16c(const float *__restrict__
     const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
     const h16x8 hz = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f,
                       (_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
-#define WG16C_LOAD(RD, RX, RF)                                                                                 \
+#define WG16C_LOAD(RD, RX, RF, RG)                                                                             \
     do {                                                                                                       \
         const bool mok = ms + prow < me;                                                                       \
         const int iy0 = py * stride, ix0 = px * stride;                                                        \
         const int xb = ((pn * H + iy0) * W + ix0) * Ci;                                                        \
         _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                        \
-            RD[u] = (mok && (cmask >> u & 1)) ? *(const h16x8 *)(dz + dzo + 32 * u) : hz;                      \
+            const bool dok = mok && (cmask >> u & 1);                                                          \
+            if constexpr (DH) {                                                                                \
+                RD[u] = dok ? *(const h16x8 *)(dz + dzo + 32 * u) : hz;                                        \
+            } else {                                                                                           \
+                RG[2 * u] = dok ? *(const f32x4 *)(dzf + dzo + 32 * u) : z4;                                   \
+                RG[2 * u + 1] = dok ? *(const f32x4 *)(dzf + dzo + 32 * u + 4) : z4;                           \
+            }                                                                                                  \
             const int iy = iy0 + xdy[u], ix = ix0 + xdx[u];                                                    \
             const bool in = mok && (cmask >> (4 + u) & 1) && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W; \
             if constexpr (XH) {                                                                                \
@@ -921,12 +929,18 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16c(const float *__restrict__
             }                                                                                                  \
         }                                                                                                      \
     } while (0)
-#define WG16C_STORE(BUF, RD, RX, RF)                                                                           \
+#define WG16C_STORE(BUF, RD, RX, RF, RG)                                                                       \
     do {                                                                                                       \
         _Float16 *Ds = lds[BUF] + prow * WT, *Xs = Ds + IMG;                                                   \
         _Pragma("unroll") for (int u = 0; u < 4; ++u) {                                                        \
             const int o = 8 * ((cq + 4 * u) ^ soff);                                                           \
-            *(h16x8 *)(Ds + o) = RD[u];                                                                        \
+            if constexpr (DH) {                                                                                \
+                *(h16x8 *)(Ds + o) = RD[u];                                                                    \
+            } else {                                                                                           \
+                const f32x4 c_ = RG[2 * u], d_ = RG[2 * u + 1];                                                \
+                *(h16x8 *)(Ds + o) = (h16x8){(_Float16)c_[0], (_Float16)c_[1], (_Float16)c_[2], (_Float16)c_[3], \
+                                             (_Float16)d_[0], (_Float16)d_[1], (_Float16)d_[2], (_Float16)d_[3]}; \
+            }                                                                                                  \
             if constexpr (XH) {                                                                                \
                 *(h16x8 *)(Xs + o) = RX[u];                                                                    \
             } else {                                                                                           \
@@ -968,35 +982,35 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_h16c(const float *__restrict__
         }                                                                                                      \
     } while (0)
     h16x8 rd0[4], rd1[4], rx0[4], rx1[4];
-    f32x4 rf0[8], rf1[8];
+    f32x4 rf0[8], rf1[8], rg0[8], rg1[8];
     const int nk = (int)((me - mb + WMS2 - 1) / WMS2);
-    WG16C_LOAD(rd0, rx0, rf0);
-    if (nk > 1) WG16C_LOAD(rd1, rx1, rf1);
-    WG16C_STORE(0, rd0, rx0, rf0);
+    WG16C_LOAD(rd0, rx0, rf0, rg0);
+    if (nk > 1) WG16C_LOAD(rd1, rx1, rf1, rg1);
+    WG16C_STORE(0, rd0, rx0, rf0, rg0);
     __syncthreads();
     int ks = 0;  // loop head: LDS buffer 0 holds step ks, register set 1 step ks + 1
     for (; ks + 3 < nk; ks += 2) {
-        WG16C_LOAD(rd0, rx0, rf0);
+        WG16C_LOAD(rd0, rx0, rf0, rg0);
         WG16C_MFMA(0);
-        WG16C_STORE(1, rd1, rx1, rf1);
+        WG16C_STORE(1, rd1, rx1, rf1, rg1);
         __syncthreads();
-        WG16C_LOAD(rd1, rx1, rf1);
+        WG16C_LOAD(rd1, rx1, rf1, rg1);
         WG16C_MFMA(1);
-        WG16C_STORE(0, rd0, rx0, rf0);
+        WG16C_STORE(0, rd0, rx0, rf0, rg0);
         __syncthreads();
     }
     if (ks + 2 < nk) {
-        WG16C_LOAD(rd0, rx0, rf0);
+        WG16C_LOAD(rd0, rx0, rf0, rg0);
         WG16C_MFMA(0);
-        WG16C_STORE(1, rd1, rx1, rf1);
+        WG16C_STORE(1, rd1, rx1, rf1, rg1);
         __syncthreads();
         WG16C_MFMA(1);
-        WG16C_STORE(0, rd0, rx0, rf0);
+        WG16C_STORE(0, rd0, rx0, rf0, rg0);
         __syncthreads();
         WG16C_MFMA(0);
     } else if (ks + 1 < nk) {
         WG16C_MFMA(0);
-        WG16C_STORE(1, rd1, rx1, rf1);
+        WG16C_STORE(1, rd1, rx1, rf1, rg1);
         __syncthreads();
         WG16C_MFMA(1);
     } else {
@@ -1059,12 +1073,13 @@ int bev_conv_wgrad_h16_ex_f32(const void *xv, int x_half, int N, int H, int W, i
     mc = ((mc + step - 1) / step) * step;
     sp = (M + mc - 1) / mc;
     if (sp * nt >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    const bool tr = H16_WGRAD_TR && deep && dz_half && Ci % 8 == 0 && Co % 8 == 0 &&
+    const bool tr = H16_WGRAD_TR && deep && Ci % 8 == 0 && Co % 8 == 0 &&
                     (((uintptr_t)x | (uintptr_t)dz) & 15) == 0 && M * Co < ((int64_t)1 << 31) - WMS2 * Co &&
                     (int64_t)N * H * W * Ci < ((int64_t)1 << 31);  // k_wgrad_h16c: 32-bit offsets
     if (tr) {
-        auto kern = x_half ? k_wgrad_h16c<true> : k_wgrad_h16c<false>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, (const _Float16 *)dz, N, H, W, Ci,
+        auto kern = x_half ? (dz_half ? k_wgrad_h16c<true, true> : k_wgrad_h16c<true, false>)
+                           : (dz_half ? k_wgrad_h16c<false, true> : k_wgrad_h16c<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)(sp * nt)), dim3(256), 0, st, x, (const void *)dz, N, H, W, Ci,
                            Ho, Wo, Co, KW, K, stride, pad, dilation, mc, ct, nt, dW);
     } else if (deep) {
         auto kern = x_half ? (dz_half ? k_wgrad_h16b<true, true> : k_wgrad_h16b<true, false>)

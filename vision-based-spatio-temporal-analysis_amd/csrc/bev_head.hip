@@ -23,7 +23,10 @@
 namespace {
 
 constexpr int GN_T = 256;
-constexpr int GN_PIX_PER_BLOCK = 2048;
+// Pixels per partial block.  Round 5: 512 (was 2048 -> 338 workgroups for the 691 k-cell head maps, ~1.3 per CU: the
+// partial passes ran at 2.3-3.4 TB/s, latency-bound on their serial double chains); the finalizes reduce the
+// partials in parallel (one workgroup per (image, group) / per 16 channels) instead of one thread per output.
+constexpr int GN_PIX_PER_BLOCK = 512;
 
 // thread -> (channel quad q, pixel phase): QP = C / 4 quads per pixel, 256 % QP == 0
 __global__ __launch_bounds__(GN_T) void k_gn_partial(const float *__restrict__ x, int64_t P, int C, int G,
@@ -33,54 +36,92 @@ __global__ __launch_bounds__(GN_T) void k_gn_partial(const float *__restrict__ x
     const int QP = C / 4, q = tid % QP, ph = tid / QP, nph = GN_T / QP;
     const int64_t p0 = (int64_t)blk * GN_PIX_PER_BLOCK, p1 = p0 + GN_PIX_PER_BLOCK < P ? p0 + GN_PIX_PER_BLOCK : P;
     const float *xb = x + (size_t)n * P * C;
-    double s = 0.0, ss = 0.0;
-    for (int64_t p = p0 + ph; p < p1; p += nph) {
-        const float4 v = *(const float4 *)(xb + p * C + 4 * q);
-        s += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
-        ss += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    double s0 = 0.0, ss0 = 0.0, s1 = 0.0, ss1 = 0.0;  // two independent chains (pixels p, p + nph)
+    int64_t p = p0 + ph;
+    for (; p + nph < p1; p += 2 * nph) {
+        const float4 v = *(const float4 *)(xb + p * C + 4 * q), w = *(const float4 *)(xb + (p + nph) * C + 4 * q);
+        s0 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+        ss0 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+        s1 += (double)w.x + (double)w.y + (double)w.z + (double)w.w;
+        ss1 += (double)w.x * w.x + (double)w.y * w.y + (double)w.z * w.z + (double)w.w * w.w;
     }
-    red[tid][0] = s;
-    red[tid][1] = ss;
+    if (p < p1) {
+        const float4 v = *(const float4 *)(xb + p * C + 4 * q);
+        s0 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+        ss0 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+    }
+    red[tid][0] = s0 + s1;
+    red[tid][1] = ss0 + ss1;
     __syncthreads();
-    // group g = channels [g * cpg, (g+1) * cpg) = quads [g * cpg / 4, ...); sum over its quads and phases
-    const int cpg = C / G, qpg = cpg / 4;
-    for (int g = tid; g < G; g += GN_T) {
+    // per quad: sum over the phases (fixed order), then per group over its quads
+    if (tid < QP) {
         double a = 0.0, b = 0.0;
-        for (int t = 0; t < GN_T; ++t) {
-            const int qq = t % QP;
-            if (qq / qpg == g) {
-                a += red[t][0];
-                b += red[t][1];
-            }
+        for (int t = tid; t < GN_T; t += QP) {
+            a += red[t][0];
+            b += red[t][1];
         }
-        double *o = part + (((size_t)n * nb + blk) * G + g) * 2;
+        red[tid][0] = a;  // row tid is read only by this thread above (t == tid first)
+        red[tid][1] = b;
+    }
+    __syncthreads();
+    const int qpg = C / G / 4;
+    if (tid < G) {
+        double a = 0.0, b = 0.0;
+        for (int t = tid * qpg; t < (tid + 1) * qpg; ++t) {
+            a += red[t][0];
+            b += red[t][1];
+        }
+        double *o = part + (((size_t)n * nb + blk) * G + tid) * 2;
         o[0] = a;
         o[1] = b;
     }
 }
 
-__global__ void k_gn_finalize(const double *__restrict__ part, int nb, int64_t P, int C, int G, float eps,
-                              const float *__restrict__ gamma, const float *__restrict__ beta,
-                              float *__restrict__ mean, float *__restrict__ rstd, float *__restrict__ scale,
-                              float *__restrict__ shift) {
-    const int n = blockIdx.x, c = threadIdx.x;  // blockDim.x == C (<= 1024)
-    const int cpg = C / G, g = c / cpg;
+// fixed-order block sum of two doubles over GN_T threads
+__device__ __forceinline__ void gn_block_sum2(double &a, double &b, double (*red)[2]) {
+    const int tid = threadIdx.x;
+    red[tid][0] = a;
+    red[tid][1] = b;
+    __syncthreads();
+    for (int o = GN_T / 2; o > 0; o >>= 1) {
+        if (tid < o) {
+            red[tid][0] += red[tid + o][0];
+            red[tid][1] += red[tid + o][1];
+        }
+        __syncthreads();
+    }
+    a = red[0][0];
+    b = red[0][1];
+}
+
+// one workgroup per (image, group): the nb partials summed in parallel, then the group's channels' affine
+__global__ __launch_bounds__(GN_T) void k_gn_finalize(const double *__restrict__ part, int nb, int64_t P, int C, int G,
+                                                      float eps, const float *__restrict__ gamma,
+                                                      const float *__restrict__ beta, float *__restrict__ mean,
+                                                      float *__restrict__ rstd, float *__restrict__ scale,
+                                                      float *__restrict__ shift) {
+    __shared__ double red[GN_T][2];
+    const int n = blockIdx.x / G, g = blockIdx.x % G, cpg = C / G;
     double a = 0.0, b = 0.0;
-    for (int k = 0; k < nb; ++k) {
+    for (int k = threadIdx.x; k < nb; k += GN_T) {
         const double *o = part + (((size_t)n * nb + k) * G + g) * 2;
         a += o[0];
         b += o[1];
     }
+    gn_block_sum2(a, b, red);
     const double cnt = (double)P * cpg;
     const double mu = a / cnt;
     double var = b / cnt - mu * mu;
     var = var > 0.0 ? var : 0.0;
     const float r = (float)(1.0 / __builtin_sqrt(var + (double)eps));
     const float m = (float)mu;
-    const float sc = r * gamma[c];
-    scale[(size_t)n * C + c] = sc;
-    shift[(size_t)n * C + c] = beta[c] - m * sc;
-    if (c % cpg == 0) {
+    for (int j = threadIdx.x; j < cpg; j += GN_T) {
+        const int c = g * cpg + j;
+        const float sc = r * gamma[c];
+        scale[(size_t)n * C + c] = sc;
+        shift[(size_t)n * C + c] = beta[c] - m * sc;
+    }
+    if (threadIdx.x == 0) {
         mean[(size_t)n * G + g] = m;
         rstd[(size_t)n * G + g] = r;
     }
@@ -93,15 +134,24 @@ __device__ __forceinline__ void gn_st4(_Float16 *p, int64_t e, float4 o) {
     *(h4 *)(p + e) = (h4){(_Float16)o.x, (_Float16)o.y, (_Float16)o.z, (_Float16)o.w};
 }
 
+// Streaming passes: grid (pixel blocks of GN_APPLY_PIX, images), thread = (channel quad q, pixel phase), the quad's
+// per-channel constants held in registers for the whole block (the round-4 form decoded (image, channel) with
+// 64-bit divisions and re-loaded the constants for every float4: 1.3 ms for the 1.4 GB map's backward apply).
+constexpr int GN_APPLY_PIX = 256;
+
 template <typename OT>
-__global__ void k_gn_apply(const float *__restrict__ x, int64_t P, int C, const float *__restrict__ scale,
-                           const float *__restrict__ shift, int relu, OT *__restrict__ y, int64_t total4) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = 4 * i;
-        const int c = (int)(e % C);
-        const int n = (int)(e / ((int64_t)P * C));
+__global__ __launch_bounds__(GN_T) void k_gn_apply(const float *__restrict__ x, int64_t P, int C,
+                                                   const float *__restrict__ scale, const float *__restrict__ shift,
+                                                   int relu, OT *__restrict__ y) {
+    const int n = blockIdx.y, tid = threadIdx.x;
+    const int QP = C / 4, q = tid % QP, ph = tid / QP, nph = GN_T / QP;
+    const int64_t p0 = (int64_t)blockIdx.x * GN_APPLY_PIX;
+    const int64_t p1 = p0 + GN_APPLY_PIX < P ? p0 + GN_APPLY_PIX : P;
+    const float4 s = *(const float4 *)(scale + (size_t)n * C + 4 * q), h = *(const float4 *)(shift + (size_t)n * C + 4 * q);
+    const size_t base = (size_t)n * P * C + 4 * q;
+    for (int64_t p = p0 + ph; p < p1; p += nph) {
+        const int64_t e = base + p * C;
         const float4 v = *(const float4 *)(x + e);
-        const float4 s = *(const float4 *)(scale + (size_t)n * C + c), h = *(const float4 *)(shift + (size_t)n * C + c);
         float4 o = make_float4(v.x * s.x + h.x, v.y * s.y + h.y, v.z * s.z + h.z, v.w * s.w + h.w);
         if (relu) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
         gn_st4(y, e, o);
@@ -179,58 +229,84 @@ __global__ __launch_bounds__(GN_T) void k_gn_bwd_partial(const float *__restrict
     }
 }
 
-// coef [N][G][2] = (mean(g gamma), mean(g gamma xhat)); dgamma / dbeta [C] (sums over images and blocks)
-__global__ void k_gn_bwd_finalize(const double *__restrict__ part, const double *__restrict__ cpart, int N, int nb,
-                                  int64_t P, int C, int G, float *__restrict__ coef, float *__restrict__ dgamma,
-                                  float *__restrict__ dbeta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < C) {
-        double a = 0.0, b = 0.0;
-        for (int n = 0; n < N; ++n)
-            for (int k = 0; k < nb; ++k) {
-                const double *o = cpart + (((size_t)n * nb + k) * C + c) * 2;
-                a += o[0];
-                b += o[1];
-            }
-        dgamma[c] = (float)a;
-        dbeta[c] = (float)b;
-    }
-    if (c < N * G) {
-        const int n = c / G, g = c % G;
-        double a = 0.0, b = 0.0;
-        for (int k = 0; k < nb; ++k) {
-            const double *o = part + (((size_t)n * nb + k) * G + g) * 2;
+// dgamma / dbeta [C]: sums of cpart over images and blocks, 16 channels x 16 phases per workgroup
+constexpr int GF_C = 16, GF_P = 16;
+__global__ __launch_bounds__(GF_C * GF_P) void k_gn_bwd_fin_chan(const double *__restrict__ cpart, int N, int nb,
+                                                                 int C, float *__restrict__ dgamma,
+                                                                 float *__restrict__ dbeta) {
+    __shared__ double red[GF_P][GF_C][2];
+    const int cl = threadIdx.x % GF_C, ph = threadIdx.x / GF_C, c = blockIdx.x * GF_C + cl;
+    double a = 0.0, b = 0.0;
+    if (c < C)
+        for (int k = ph; k < N * nb; k += GF_P) {  // k = n * nb + block
+            const double *o = cpart + ((size_t)k * C + c) * 2;
             a += o[0];
             b += o[1];
         }
+    red[ph][cl][0] = a;
+    red[ph][cl][1] = b;
+    __syncthreads();
+    if (ph != 0 || c >= C) return;
+    for (int t = 1; t < GF_P; ++t) {
+        a += red[t][cl][0];
+        b += red[t][cl][1];
+    }
+    dgamma[c] = (float)a;
+    dbeta[c] = (float)b;
+}
+
+// coef [N][G][2] = (mean(g gamma), mean(g gamma xhat)): one workgroup per (image, group)
+__global__ __launch_bounds__(GN_T) void k_gn_bwd_fin_group(const double *__restrict__ part, int nb, int64_t P, int C,
+                                                           int G, float *__restrict__ coef) {
+    __shared__ double red[GN_T][2];
+    const int n = blockIdx.x / G, g = blockIdx.x % G;
+    double a = 0.0, b = 0.0;
+    for (int k = threadIdx.x; k < nb; k += GN_T) {
+        const double *o = part + (((size_t)n * nb + k) * G + g) * 2;
+        a += o[0];
+        b += o[1];
+    }
+    gn_block_sum2(a, b, red);
+    if (threadIdx.x == 0) {
         const double cnt = (double)P * (C / G);
-        coef[(size_t)c * 2] = (float)(a / cnt);
-        coef[(size_t)c * 2 + 1] = (float)(b / cnt);
+        coef[(size_t)blockIdx.x * 2] = (float)(a / cnt);
+        coef[(size_t)blockIdx.x * 2 + 1] = (float)(b / cnt);
     }
 }
 
 template <typename OT>
-__global__ void k_gn_bwd_apply(const float *__restrict__ x, const float *__restrict__ dy, int64_t P, int C, int G,
-                               const float *__restrict__ mean, const float *__restrict__ rstd,
-                               const float *__restrict__ gamma, const float *__restrict__ scale,
-                               const float *__restrict__ shift, int relu, const float *__restrict__ coef,
-                               OT *__restrict__ dx, int64_t total4) {
-    const int cpg = C / G;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t e = 4 * i;
-        const int c0 = (int)(e % C);
-        const int n = (int)(e / ((int64_t)P * C));
+__global__ __launch_bounds__(GN_T) void k_gn_bwd_apply(const float *__restrict__ x, const float *__restrict__ dy,
+                                                       int64_t P, int C, int G, const float *__restrict__ mean,
+                                                       const float *__restrict__ rstd,
+                                                       const float *__restrict__ gamma,
+                                                       const float *__restrict__ scale,
+                                                       const float *__restrict__ shift, int relu,
+                                                       const float *__restrict__ coef, OT *__restrict__ dx) {
+    const int n = blockIdx.y, tid = threadIdx.x;
+    const int QP = C / 4, q = tid % QP, ph = tid / QP, nph = GN_T / QP;
+    const int64_t p0 = (int64_t)blockIdx.x * GN_APPLY_PIX;
+    const int64_t p1 = p0 + GN_APPLY_PIX < P ? p0 + GN_APPLY_PIX : P;
+    const size_t ng = (size_t)n * G + (4 * q) / (C / G);  // the quad's group ((C / G) % 4 == 0)
+    const float mu = mean[ng], rs = rstd[ng], k1 = coef[2 * ng], k2 = coef[2 * ng + 1];
+    float sc[4], sh[4], ga[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int c = 4 * q + u;
+        sc[u] = scale[(size_t)n * C + c];
+        sh[u] = shift[(size_t)n * C + c];
+        ga[u] = gamma[c];
+    }
+    const size_t base = (size_t)n * P * C + 4 * q;
+    for (int64_t p = p0 + ph; p < p1; p += nph) {
+        const int64_t e = base + p * C;
         const float4 v = *(const float4 *)(x + e), d = *(const float4 *)(dy + e);
         const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
         float o[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int c = c0 + u, g = c / cpg;
-            const size_t ng = (size_t)n * G + g;
-            const float sc = scale[(size_t)n * C + c], sh = shift[(size_t)n * C + c];
-            const float gr = (relu && !(xv[u] * sc + sh > 0.f)) ? 0.f : dv[u];
-            const float xh = (xv[u] - mean[ng]) * rstd[ng];
-            o[u] = rstd[ng] * (gr * gamma[c] - coef[2 * ng] - xh * coef[2 * ng + 1]);
+            const float gr = (relu && !(xv[u] * sc[u] + sh[u] > 0.f)) ? 0.f : dv[u];
+            const float xh = (xv[u] - mu) * rs;
+            o[u] = rs * (gr * ga[u] - k1 - xh * k2);
         }
         gn_st4(dx, e, make_float4(o[0], o[1], o[2], o[3]));
     }
@@ -379,23 +455,22 @@ int bev_groupnorm_fwd_f32(const float *x, int N, int64_t P, int C, int G, float 
     const int nb = nblocks(P);
     double *part = (double *)workspace;
     hipLaunchKernelGGL(k_gn_partial, dim3(nb, N), dim3(GN_T), 0, st, x, P, C, G, part);
-    hipLaunchKernelGGL(k_gn_finalize, dim3(N), dim3(C), 0, st, part, nb, P, C, G, eps, gamma, beta, mean, rstd, scale,
-                       shift);
+    hipLaunchKernelGGL(k_gn_finalize, dim3(N * G), dim3(GN_T), 0, st, part, nb, P, C, G, eps, gamma, beta, mean, rstd,
+                       scale, shift);
     return (int)hipGetLastError();
 }
 
 int bev_groupnorm_apply_ex_f32(const float *x, int N, int64_t P, int C, const float *scale, const float *shift,
                                int relu, void *y, int y_half, void *stream) {
-    if (!x || !scale || !shift || !y || N <= 0 || P <= 0 || C <= 0 || C % 4 != 0) return BEV_ERR_ARGS;
-    const int64_t total4 = (int64_t)N * P * C / 4;
-    int64_t blocks = (total4 + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
+    if (!x || !scale || !shift || !y || N <= 0 || N > 65535 || P <= 0 || C <= 0 || C % 4 != 0 || GN_T % (C / 4) != 0)
+        return BEV_ERR_ARGS;
+    const dim3 grid((unsigned)((P + GN_APPLY_PIX - 1) / GN_APPLY_PIX), N);
     if (y_half)
-        hipLaunchKernelGGL(k_gn_apply<_Float16>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, P, C,
-                           scale, shift, relu, (_Float16 *)y, total4);
+        hipLaunchKernelGGL(k_gn_apply<_Float16>, grid, dim3(GN_T), 0, (hipStream_t)stream, x, P, C, scale, shift, relu,
+                           (_Float16 *)y);
     else
-        hipLaunchKernelGGL(k_gn_apply<float>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, P, C, scale,
-                           shift, relu, (float *)y, total4);
+        hipLaunchKernelGGL(k_gn_apply<float>, grid, dim3(GN_T), 0, (hipStream_t)stream, x, P, C, scale, shift, relu,
+                           (float *)y);
     return (int)hipGetLastError();
 }
 
@@ -418,18 +493,16 @@ int bev_groupnorm_bwd_ex_f32(const float *x, const float *dy, int N, int64_t P, 
     hipLaunchKernelGGL(k_gn_bwd_partial, dim3(nb, N), dim3(GN_T), 0, st, x, dy, P, C, G, mean, rstd, gamma, scale,
                        shift, relu, part, cpart);
     float *coef = (float *)(cpart + (size_t)N * nb * C * 2);
-    const int nt = (C > N * G ? C : N * G);
-    hipLaunchKernelGGL(k_gn_bwd_finalize, dim3((nt + 255) / 256), dim3(256), 0, st, part, cpart, N, nb, P, C, G, coef,
+    hipLaunchKernelGGL(k_gn_bwd_fin_chan, dim3((C + GF_C - 1) / GF_C), dim3(GF_C * GF_P), 0, st, cpart, N, nb, C,
                        dgamma, dbeta);
-    const int64_t total4 = (int64_t)N * P * C / 4;
-    int64_t blocks = (total4 + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_gn_bwd_fin_group, dim3(N * G), dim3(GN_T), 0, st, part, nb, P, C, G, coef);
+    const dim3 grid((unsigned)((P + GN_APPLY_PIX - 1) / GN_APPLY_PIX), N);
     if (dx_half)
-        hipLaunchKernelGGL(k_gn_bwd_apply<_Float16>, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, P, C, G, mean,
-                           rstd, gamma, scale, shift, relu, coef, (_Float16 *)dx, total4);
+        hipLaunchKernelGGL(k_gn_bwd_apply<_Float16>, grid, dim3(GN_T), 0, st, x, dy, P, C, G, mean, rstd, gamma, scale,
+                           shift, relu, coef, (_Float16 *)dx);
     else
-        hipLaunchKernelGGL(k_gn_bwd_apply<float>, dim3((unsigned)blocks), dim3(256), 0, st, x, dy, P, C, G, mean, rstd,
-                           gamma, scale, shift, relu, coef, (float *)dx, total4);
+        hipLaunchKernelGGL(k_gn_bwd_apply<float>, grid, dim3(GN_T), 0, st, x, dy, P, C, G, mean, rstd, gamma, scale,
+                           shift, relu, coef, (float *)dx);
     return (int)hipGetLastError();
 }
 
