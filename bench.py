@@ -296,7 +296,7 @@ def cpu_k1(args, K, Rt):
                       "torch CPU fp32 (oracle/backbone_ref.py + oracle.reference_composition_cpu)"}
 
 
-def pmc_traffic(args) -> dict:
+def pmc_traffic(args, world: int = 1) -> dict:
     """HBM bytes from the committed rocprofv3 PMC passes of this same command (tools/pmc_traffic.py):
     conv = bytes per step over all backbone conv launches, warp = bytes per fused-warp launch.
     Only reported for the default workload those passes ran; {} otherwise.  These are the profile
@@ -304,8 +304,13 @@ def pmc_traffic(args) -> dict:
     default = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone,
                args.camera_shard, args.warp_kernel) == \
         (7, 64, (1080, 1920), (480, 1440), 2, "resnet50", False, "dma")
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic.json")))
-    if not default or not files:
+    # the camera-shard line (BASELINE configs[4]) at world 1: its own passes (tools/gpu_r05_warp_pmc.sh cam_fetch /
+    # cam_write -> tools/pmc_traffic.py -> profiles/r*_pmc_traffic_k5.json)
+    k5 = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.backbone, args.camera_shard,
+          args.warp_kernel, world) == (16, 64, (2160, 3840), (480, 1440), "resnet50", True, "dma", 1)
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic_k5.json" if k5 else
+                                          "r*_pmc_traffic.json")))
+    if not (default or k5) or not files:
         return {}
     d = json.load(open(files[-1]))
     if d.get("conv_arith", "f32") != args.conv_arith:  # profiled under the other conv arithmetic
@@ -509,7 +514,7 @@ def main():
     value = frames / elapsed
 
     if rank == 0:
-        pmc = pmc_traffic(args)
+        pmc = pmc_traffic(args, world)
         flops = backbone_flops(enc, H, W) * VL * B
         # the ResNet stem (NCHW, Ci = 3) always runs the exact-f32 MFMA stem kernel; under the bf16x6 arithmetic
         # every other trunk conv and the proj run on the bf16 matrix cores (6 partial products per fp32 product)
