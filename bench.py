@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--conv-arith", choices=("bf16x6", "f32"), default="bf16x6",
                     help="trunk conv arithmetic: bf16x6 = fp32 through exact 3-way bf16 splits (default), f32 = the "
                          "exact-f32 MFMA kernels")
+    ap.add_argument("--stem-f32", action="store_true", help="ResNet: the exact-f32 stem kernel instead of the "
+                    "split-arithmetic one (A/B only; resnet.STEM_X6)")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V",
                     help="set a performance knob (include/bev_mi355x.h BEV_TUNE_<NAME>) before the run; repeatable")
     ap.add_argument("--warp-kernel", choices=("dma", "register", "rows"), default="dma",
@@ -432,6 +434,9 @@ def main():
     if hasattr(enc.backbone, "stream_groups"):
         if args.stream_groups is not None:
             enc.backbone.stream_groups = args.stream_groups
+        if args.stem_f32:
+            import models.encoders.resnet as _resnet
+            _resnet.STEM_X6 = False
         if args.stream_offset is not None:
             enc.backbone.stream_offset = args.stream_offset
     geom = GeometryTransformer(args.bev[0], args.bev[1], BOUNDS)
@@ -516,10 +521,12 @@ def main():
     if rank == 0:
         pmc = pmc_traffic(args, world)
         flops = backbone_flops(enc, H, W) * VL * B
-        # the ResNet stem (NCHW, Ci = 3) always runs the exact-f32 MFMA stem kernel; under the bf16x6 arithmetic
-        # every other trunk conv and the proj run on the bf16 matrix cores (6 partial products per fp32 product)
+        # under the bf16x6 arithmetic every trunk conv and the proj run on the bf16 matrix cores (6 partial products
+        # per fp32 product); the ResNet stem too (k_stem_x6) unless --stem-f32 keeps the exact-f32 MFMA stem kernel
         x6 = nat.conv_arith() == "bf16x6" and not args.backbone.startswith("efficient") and enc._use_timm
-        f_stem = stem_flops(enc, H, W) * VL * B if x6 else flops
+        import models.encoders.resnet as _resnet
+        stem6 = x6 and _resnet.STEM_X6
+        f_stem = 0 if stem6 else stem_flops(enc, H, W) * VL * B if x6 else flops
         peak_mfma = flops / (f_stem / PEAK_F32_MFMA_TF + (flops - f_stem) / PEAK_X6_TF) if x6 else PEAK_F32_MFMA_TF
         Hm = geom.homographies(Kd, Rtd, B, VL, dev)
         alg, out_b, touched = warp_alg_bytes(geom, Hm, feats.shape, (H, W), B)
@@ -530,13 +537,17 @@ def main():
         kern_ms = conv_ms if groups <= 1 else bb_ms
         ach_tf = flops / (kern_ms * 1e-3) / 1e12
         roof_bb = None if args.warp_only else {
-            "kernel": ("k_conv_x6* (fp32 as 3-way split bf16, 6 partial products on v_mfma_f32_32x32x16_bf16) + "
+            "kernel": ("k_conv_x6* + k_stem_x6 (fp32 as 3-way split bf16, 6 partial products on "
+                       "v_mfma_f32_32x32x16_bf16), every backbone conv launch of one step" if stem6 else
+                       "k_conv_x6* (fp32 as 3-way split bf16, 6 partial products on v_mfma_f32_32x32x16_bf16) + "
                        "k_stem (exact-f32 MFMA), every backbone conv launch of one step" if x6 else
                        "k_conv + k_stem (fp32 MFMA implicit GEMM, every backbone conv launch of one step)"),
             "bound": "mfma", "achieved": round(ach_tf, 3), "peak": round(peak_mfma, 1),
             "unit": "TFLOP/s", "frac": round(ach_tf / peak_mfma, 4),
             "arith": nat.conv_arith() if x6 else "f32",
-            "peak_basis": ("algorithmic fp32 FLOPs; peak blended by FLOP share: stem at the fp32 MFMA peak 157.3, "
+            "peak_basis": (f"algorithmic fp32 FLOPs at bf16 dense {PEAK_BF16_MFMA_TF:.0f} / 6 = {PEAK_X6_TF:.1f}"
+                           if stem6 else
+                           "algorithmic fp32 FLOPs; peak blended by FLOP share: stem at the fp32 MFMA peak 157.3, "
                            f"the rest at bf16 dense {PEAK_BF16_MFMA_TF:.0f} / 6 = {PEAK_X6_TF:.1f}" if x6 else
                            "fp32 MFMA dense peak"),
             "frac_of_fp32_mfma_peak": round(ach_tf / PEAK_F32_MFMA_TF, 4),

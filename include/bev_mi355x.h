@@ -348,6 +348,12 @@ int bev_relu_bwd_f32(const float *dy, const float *y, float *dz, int64_t n, void
 int bev_dilate_nhwc_f32(const float *dz, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd, int Wd,
                         float *out, void *stream);
 
+/* out [N][H][W][C] = residual (or 0 when NULL) + (y [N][Ho][Wo][C] placed at (s*oy, s*ox), zero elsewhere): the input
+ * gradient of a 1x1 / stride-s / pad-0 conv from y = dz W (the zero-inserted dgrad without the zeros' work);
+ * 256 % (C / 4) == 0, 16-B aligned. */
+int bev_place_strided_f32(const float *y, int N, int Ho, int Wo, int C, int s, int H, int W, const float *residual,
+                          float *out, void *stream);
+
 /* bev_dilate_nhwc_f32 for elements of elem_bytes 4 (fp32) or 2 (fp16 storage): a copy, any 4-channel quad type. */
 int bev_dilate_nhwc_ex(const void *dz, int elem_bytes, int N, int Ho, int Wo, int C, int s, int top, int left, int Hd,
                        int Wd, void *out, void *stream);
@@ -465,6 +471,13 @@ int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, co
                                  const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
                                  const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
                                  const float *bias2, int Co2, int act2, float *y, int Ho, int Wo, void *stream);
+
+/* device: the ResNet stem (timm conv1: 7x7, stride 2, pad 3, Ci = 3; cnn_encoder.py:26, the first layer of
+ * CNNEncoder._encode_single) in the split arithmetic: x NCHW [N][3][H][W] fp32 images, packed = the split panel of
+ * the (BN-folded) [Co][3][7][7] weights (bev_conv_pack_weights_x6, 16-B aligned), Co <= 64; y NHWC [N][Ho][Wo][Co]
+ * = act(conv + bias), act 0 / 1 (ReLU).  fp32-tolerance equal to the exact-f32 stem of bev_conv2d_f32. */
+int bev_conv2d_stem_x6_f32(const float *x, int N, int H, int W, const uint16_t *packed, const float *bias, int Co,
+                           int relu, float *y, int Ho, int Wo, void *stream);
 
 /* device: split n fp32 values into planes [3][n] bf16 with x == h + m + l exactly (the operand format of
  * bev_conv2d_x6_f32's xs). */

@@ -196,3 +196,24 @@ def test_x6_resnet50_encoder_matches_f32_path():
     torch.cuda.synchronize()
     scale = ref.abs().max().item()
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4 * scale)
+
+
+@pytest.mark.parametrize("N,H,W,Co,relu", [(2, 45, 140, 64, True), (1, 1080, 1920, 64, True), (1, 33, 70, 40, False)],
+                         ids=["ragged", "bench-frame", "co40-norelu"])
+def test_stem_x6_vs_float64_and_exact_stem(N, H, W, Co, relu):
+    """The ResNet stem on the split arithmetic (bev_conv2d_stem_x6_f32: 7x7 / s2 / p3 over NCHW Ci = 3) against the
+    float64 conv of the fp32 operands, with the x6 bar (max error <= 1e-5 max|ref|) and no less accurate than the
+    exact-f32 stem kernel (bev_conv2d_f32 with the NCHW loader) within 4x -- ragged tiles (Ho, Wo not multiples of
+    8 / 64), one full 1080p image, and Co < 64."""
+    x, w, b = _case(N, H, W, 3, Co, 7, 99 + Co)
+    x32, w32, b32 = x.float(), w.float(), b.float()
+    ref = _nhwc(_ref(x32.double(), w32.double(), b32.double(), 2, 3, 1, 1 if relu else 0))
+    xd, bd = x32.to(DEV), b32.to(DEV)
+    y6 = nat.conv2d_stem_x6(xd, nat.pack_conv_weight_x6(w32.to(DEV)), bd, Co, relu)
+    yf = nat.conv2d_nhwc(xd, nat.pack_conv_weight(w32.to(DEV)), bd, Co, 7, 7, 2, 3, relu, in_nchw=True)
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    e6, ef = (y6.cpu().double() - ref).abs(), (yf.cpu().double() - ref).abs()
+    assert torch.isfinite(y6).all()
+    assert e6.max().item() <= 1e-5 * scale, (e6.max().item(), scale)
+    assert e6.max().item() <= 4 * ef.max().item() + 1e-7 * scale, (e6.max().item(), ef.max().item())

@@ -681,3 +681,32 @@ def test_effnet_trunk_backward_vs_torch_autograd(name, bn_mode):
             assert (stats1[k].double() - b).abs().max().item() <= 1e-4 * max(b.abs().max().item(), 1e-12), k
             moved += int(not torch.equal(stats1[k], stats0[k]))
     assert (moved > 0) == (bn_mode == "batch")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,H,W,Ci,Co,res", [(2, 17, 23, 64, 128, True), (1, 40, 30, 256, 512, False),
+                                            (3, 9, 12, 32, 64, True)])
+def test_dgrad_1x1_strided_placement(N, H, W, Ci, Co, res):
+    """Input gradient of a 1x1 / stride-2 conv (the downsample) as dz W on the Ho x Wo pixels placed at the strided
+    positions (bev_place_strided_f32, + the residual gradient) against torch.nn.grad.conv2d_input in float64 --
+    including odd H / W (the last row / column of x receives no gradient) -- and equal to the zero-inserted
+    (dilated) form it replaces."""
+    import bev_native as nat
+    from models.encoders import trunk_grad
+    g = torch.Generator().manual_seed(H * W + Ci)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    dz = torch.randn(N, Ho, Wo, Co, generator=g)
+    w = torch.randn(Co, Ci, 1, 1, generator=g) / Ci ** 0.5
+    r = torch.randn(N, H, W, Ci, generator=g) if res else None
+    got = trunk_grad._dgrad(dz.to(DEV), w.to(DEV), H, W, 2, 0, residual=r.to(DEV) if res else None)
+    ref = torch.nn.grad.conv2d_input((N, Ci, H, W), w.double(), dz.double().permute(0, 3, 1, 2), stride=2)
+    ref = ref.permute(0, 2, 3, 1) + (r.double() if res else 0)
+    torch.cuda.synchronize()
+    scale = float(ref.abs().max())
+    assert float((got.cpu().double() - ref).abs().max()) <= 1e-5 * scale
+    d = nat.dilate_nhwc(dz.to(DEV), 2, 0, 0, 2 * (Ho - 1) + 1 + (H - 1) % 2, 2 * (Wo - 1) + 1 + (W - 1) % 2)
+    wt = nat.pack_conv_weight(w.flip(2, 3).transpose(0, 1).contiguous().to(DEV))
+    old = nat.conv2d_nhwc(d, wt, torch.zeros(Ci, device=DEV), Ci, 1, 1, 1, 0, False)
+    if res:
+        old = old + r.to(DEV)
+    assert torch.equal(got, old)

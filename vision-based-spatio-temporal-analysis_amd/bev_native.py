@@ -19,7 +19,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -34,6 +34,8 @@ _d = ctypes.c_double
 # name -> (restype, argtypes); must match include/bev_mi355x.h
 SIGNATURES = {
     "bev_abi_version": (_i, []),
+    "bev_place_strided_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "bev_conv2d_stem_x6_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
     "bev_build_source_hash": (ctypes.c_char_p, []),
     "bev_tune": (_i, [_i, _i]),
     "bev_linspace_f32": (_i, [_d, _d, _i, _vp]),
@@ -691,6 +693,25 @@ def conv2d_nhwc_x6(x, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, str
     return Split3(ys) if split_out else out
 
 
+def conv2d_stem_x6(x: torch.Tensor, packed: torch.Tensor, bias: torch.Tensor, Co: int, relu: bool,
+                   out: torch.Tensor = None) -> torch.Tensor:
+    """The ResNet stem (7x7 / s2 / p3 over NCHW [N,3,H,W] fp32 images) on the split arithmetic: packed = the split
+    panel of the [Co,3,7,7] weights (pack_conv_weight_x6) -> y [N,Ho,Wo,Co] NHWC fp32 (bev_conv2d_stem_x6_f32)."""
+    x = x.contiguous()
+    _require_gpu(x, bias)
+    N, Ci, H, W = x.shape
+    if Ci != 3 or not packed.is_cuda or packed.dtype != torch.bfloat16:
+        raise HipError("conv2d_stem_x6 takes NCHW 3-channel images and the split (bf16) weight panel on the device")
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    with _span("conv", x):
+        rc = lib().bev_conv2d_stem_x6_f32(_ptr(x), N, H, W, _ptr(packed), _ptr(bias.contiguous().float()), Co,
+                                          int(relu), _ptr(out), Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_stem_x6_f32")
+    return out
+
+
 def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
                 relu: bool, residual: torch.Tensor = None, in_nchw: bool = False, out: torch.Tensor = None,
                 ascale: torch.Tensor = None):
@@ -811,6 +832,21 @@ def conv_wgrad_h16_any(x: torch.Tensor, dz: torch.Tensor, KH: int, KW: int, stri
                                            int(dz.dtype == torch.float16), Ho, Wo, Co, KH, KW, stride, pad, dilation,
                                            _ptr(dW), _stream(x)), "bev_conv_wgrad_h16_ex_f32")
     return dW.permute(0, 3, 1, 2).contiguous()
+
+
+def place_strided(y: torch.Tensor, s: int, H: int, W: int, residual: torch.Tensor = None) -> torch.Tensor:
+    """y [N,Ho,Wo,C] fp32 -> out [N,H,W,C] = residual (or 0) + y at (s*oy, s*ox) (bev_place_strided_f32): the input
+    gradient of a 1x1 / stride-s / pad-0 conv from y = dz W."""
+    y = y.contiguous()
+    _require_gpu(y, residual)
+    N, Ho, Wo, C = y.shape
+    out = torch.empty(N, H, W, C, device=y.device, dtype=torch.float32)
+    if residual is not None:
+        residual = residual.contiguous().float()
+        assert residual.shape == out.shape
+    _check(lib().bev_place_strided_f32(_ptr(y), N, Ho, Wo, C, s, H, W, _ptr(residual), _ptr(out), _stream(y)),
+           "bev_place_strided_f32")
+    return out
 
 
 def dilate_nhwc_any(dz: torch.Tensor, s: int, top: int, left: int, Hd: int, Wd: int) -> torch.Tensor:

@@ -955,6 +955,200 @@ int dispatch_x6(const ConvX &a0, hipStream_t st) {
     return launch_x6<2, 2, 2, 2, DUAL>(a, st);
 }
 
+// ---------------------------------------------------------------------------
+// ResNet stem (7x7 / stride 2 / pad 3 over Ci = 3 NCHW images, Co <= 64) on the split arithmetic
+// ---------------------------------------------------------------------------
+// timm conv1 (cnn_encoder.py:26; first layer of CNNEncoder._encode_single) -- the same contract as bev_conv.hip's
+// exact-f32 k_stem, with the products of the other trunk layers: per 16-deep k slice six v_mfma_f32_32x32x16_bf16
+// (32 cycles each) instead of eight v_mfma_f32_32x32x2_f32 (64 cycles), 2.67x fewer matrix-core cycles.
+// Workgroup = 8 waves, tile = 8 output rows x 64 columns x 64 channels, wave w owns output row w (2 x 2 MFMA tiles
+// of 32 pixels x 32 channels).  The tile's input patch (3 ch x 21 rows x 133 cols) sits in LDS as fp32 even / odd
+// column planes exactly as k_stem keeps it (stride 2: tap kx of output column ox is plane kx & 1 at ox + kx / 2),
+// so each A element is a ds_read_b32 at a compile-time offset; a lane's 8 consecutive k (the split panel's order,
+// k = (ky * 7 + kx) * 3 + ci, 147 taps padded to 160) are read, split into h / m / l and fed as three bf16
+// fragments.  The weights' split panel (fragment order, the first two 32-column blocks: 60 KiB) is copied into LDS
+// once per workgroup, so B fragments are conflict-free ds_read_b128.  Persistent over tiles; the next tile's patch
+// is fetched into registers during the MFMAs.  fp32-tolerance equal to k_stem (summation order), as every split
+// conv is to its exact-f32 counterpart.
+namespace stem6 {
+constexpr int TW = 64, TH = 8, NTHR = 512;
+constexpr int PR = 2 * TH + 5;  // 21 input rows
+constexpr int PC = 2 * TW + 5;  // 133 input columns
+constexpr int PP = 80;          // plane pitch (67 used; = 16 mod 32 -> conflict-free stores)
+constexpr int RP = 2 * PP, CP = PR * RP, PATCH = 3 * CP;
+constexpr int NE = 3 * PR * PC;
+constexpr int PER_T = (NE + NTHR - 1) / NTHR;
+constexpr int NS = 10;            // 16-deep k slices (147 -> 160)
+constexpr int WB = 2 * NS * 3 * 512;  // bf16 of the panel's first two 32-column blocks
+// STEM6_PRESPLIT 1: the patch is split into h / m / l once, when it is written to LDS (a dword plane of (h, m) pairs
+// and a 16-bit plane of l): each input value serves ~12 (tap, pixel) products, so splitting per use (0: fp32 patch,
+// split3 on every A element) costs ~12x the conversions.
+// LDS float offset of panel k (k = (ky * 7 + kx) * 3 + ci) relative to (output row 0, output column 0) of the patch;
+// the padding k >= 147 reads tap 0 (its weight is zero)
+__host__ __device__ constexpr int koff(int k) {
+    return k >= 147 ? 0 : (k % 3) * CP + (k / 21) * RP + (((k / 3) % 7) & 1) * PP + (((k / 3) % 7) >> 1);
+}
+}  // namespace stem6
+
+#ifndef STEM6_PRESPLIT
+#define STEM6_PRESPLIT 1
+#endif
+
+struct StemX6Args {
+    const float *__restrict__ x;
+    const __bf16 *__restrict__ wp;
+    const float *__restrict__ bias;
+    float *__restrict__ y;
+    int H, W, Co, Ho, Wo, relu, nTx, nTy;
+    int64_t ntiles;
+};
+
+__device__ __forceinline__ void stem6_fetch(const StemX6Args &a, int64_t t, int tid, float (&pv)[stem6::PER_T]) {
+    using namespace stem6;
+    const int tx = (int)(t % a.nTx);
+    const int64_t r_ = t / a.nTx;
+    const int ty = (int)(r_ % a.nTy);
+    const int64_t img = r_ / a.nTy;
+    const int row0 = 2 * ty * TH - 3, col0 = 2 * tx * TW - 3;
+    const float *xi = a.x + img * 3 * (int64_t)a.H * a.W;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+        const int e = tid + NTHR * i;
+        const int cr = e / PC, c = e - cr * PC;
+        const int ci = cr / PR, r = cr - ci * PR;
+        const int gy = row0 + r, gx = col0 + c;
+        const bool in = e < NE && gy >= 0 && gy < a.H && gx >= 0 && gx < a.W;
+        pv[i] = *(in ? xi + ((int64_t)ci * a.H + gy) * a.W + gx : (const float *)g_xzero4);
+    }
+}
+
+__device__ __forceinline__ void stem6_put(float *pl, int tid, const float (&pv)[stem6::PER_T]) {
+    using namespace stem6;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+        const int e = tid + NTHR * i;
+        if (e < NE) {
+            const int cr = e / PC, c = e - cr * PC;
+            const int ci = cr / PR, r = cr - ci * PR;
+            const int o = ci * CP + r * RP + (c & 1) * PP + (c >> 1);
+            if (STEM6_PRESPLIT) {  // pl = the (h, m) dword plane, followed by the l plane (PATCH bf16)
+                __bf16 hh, mm, ll;
+                split3(pv[i], hh, mm, ll);
+                reinterpret_cast<unsigned *>(pl)[o] = (unsigned)__builtin_bit_cast(unsigned short, hh) |
+                                                      ((unsigned)__builtin_bit_cast(unsigned short, mm) << 16);
+                reinterpret_cast<__bf16 *>(pl + PATCH)[o] = ll;
+            } else {
+                pl[o] = pv[i];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(stem6::NTHR, 1) void k_stem_x6(StemX6Args a) {
+    using namespace stem6;
+    __shared__ __attribute__((aligned(16))) unsigned char lds_raw[WB * 2 + PATCH * (STEM6_PRESPLIT ? 6 : 4)];
+    __bf16 *wl = (__bf16 *)lds_raw;
+    float *pl = (float *)(lds_raw + WB * 2);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, r32 = lane & 31;
+    // the split panel's blocks 0 and 1 ([cb][slice][plane][64 lanes][8]) are its first WB bf16: a straight copy
+    for (int e = tid; e < WB / 8; e += NTHR) reinterpret_cast<u32x4 *>(wl)[e] = reinterpret_cast<const u32x4 *>(a.wp)[e];
+    float pv[PER_T];
+    int64_t t = blockIdx.x;
+    stem6_fetch(a, t < a.ntiles ? t : 0, tid, pv);
+    stem6_put(pl, tid, pv);
+    __syncthreads();
+
+    const float *P = pl + wave * 2 * RP + r32;  // output row `wave`, column r32 (+ 32 for the second M tile)
+    const __bf16 *PL = reinterpret_cast<const __bf16 *>(pl + PATCH) + wave * 2 * RP + r32;  // its l plane (PRESPLIT)
+    const float b0 = (r32 < a.Co) ? a.bias[r32] : 0.0f;
+    const float b1 = (32 + r32 < a.Co) ? a.bias[32 + r32] : 0.0f;
+    for (; t < a.ntiles; t += gridDim.x) {
+        const int64_t tn = t + gridDim.x;
+        stem6_fetch(a, tn < a.ntiles ? tn : t, tid, pv);  // in flight during the MFMAs
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){0};
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl) {
+            int hv = h;
+            asm volatile("" : "+v"(hv));  // per slice: the h selects stay cndmasks, not 160 hoisted lane offsets
+            const __bf16 *wlb = wl + lane * 8;
+            asm volatile("" : "+v"(wlb));  // per slice: the weight fragments are re-read, not held across tiles
+            bf16x8 fb[2][3];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    fb[j][p] = *(const bf16x8 *)(wlb + ((j * NS + sl) * 3 + p) * 512);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                bf16x8 fa[3];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int o0 = koff(16 * sl + e), o1 = koff(16 * sl + 8 + e);
+                    const int o = 32 * mt + (hv ? o1 : o0);
+                    if (STEM6_PRESPLIT) {
+                        const unsigned hm = reinterpret_cast<const unsigned *>(P)[o];
+                        fa[0][e] = __builtin_bit_cast(__bf16, (unsigned short)(hm & 0xffffu));
+                        fa[1][e] = __builtin_bit_cast(__bf16, (unsigned short)(hm >> 16));
+                        fa[2][e] = PL[o];
+                    } else {
+                        __bf16 hh, mm, ll;
+                        split3(P[o], hh, mm, ll);
+                        fa[0][e] = hh;
+                        fa[1][e] = mm;
+                        fa[2][e] = ll;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x16 &c = acc[mt][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][1], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[j][2], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[j][0], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[j][1], c, 0, 0, 0);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one slice of operands live at a time
+        }
+        // epilogue: D[row][col], col = channel r32 (+32), row = pixel (r & 3) + 8 (r >> 2) + 4 h (+32)
+        {
+            const int tx = (int)(t % a.nTx);
+            const int64_t r_ = t / a.nTx;
+            const int ty = (int)(r_ % a.nTy);
+            const int64_t img = r_ / a.nTy;
+            const int oy = ty * TH + wave;
+            const int oxb = tx * TW;
+            if (oy < a.Ho) {
+                float *yr = a.y + ((img * a.Ho + oy) * (int64_t)a.Wo) * a.Co;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int ox = oxb + 32 * mt + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        if (ox < a.Wo) {
+                            float v0 = acc[mt][0][r] + b0, v1 = acc[mt][1][r] + b1;
+                            if (a.relu) {
+                                v0 = v0 > 0.0f ? v0 : 0.0f;
+                                v1 = v1 > 0.0f ? v1 : 0.0f;
+                            }
+                            float *yp = yr + (int64_t)ox * a.Co;
+                            if (r32 < a.Co) yp[r32] = v0;
+                            if (32 + r32 < a.Co) yp[32 + r32] = v1;
+                        }
+                    }
+            }
+        }
+        __syncthreads();  // every wave is done reading the patch
+        stem6_put(pl, tid, pv);
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 namespace bev {
@@ -1129,6 +1323,34 @@ int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, co
     a.Co2 = Co2;
     a.act2 = act2;
     return launch_x6b<4, 1, 1, 2, false, 2>(a, (hipStream_t)stream);
+}
+
+
+int bev_conv2d_stem_x6_f32(const float *x, int N, int H, int W, const uint16_t *packed, const float *bias, int Co,
+                           int relu, float *y, int Ho, int Wo, void *stream) {
+    if (!x || !packed || !bias || !y || N <= 0 || H <= 0 || W <= 0 || Co <= 0 || Co > 64 ||
+        Ho != (H + 6 - 7) / 2 + 1 || Wo != (W + 6 - 7) / 2 + 1 || (((uintptr_t)packed) & 15) != 0)
+        return BEV_ERR_ARGS;
+    static int num_cu = 0;
+    if (num_cu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        num_cu = n;
+    }
+    StemX6Args a;
+    a.x = x;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.y = y;
+    a.H = H, a.W = W, a.Co = Co, a.Ho = Ho, a.Wo = Wo, a.relu = relu;
+    a.nTx = (Wo + stem6::TW - 1) / stem6::TW;
+    a.nTy = (Ho + stem6::TH - 1) / stem6::TH;
+    a.ntiles = (int64_t)N * a.nTx * a.nTy;
+    const int64_t grid = a.ntiles < num_cu ? a.ntiles : num_cu;
+    hipLaunchKernelGGL(k_stem_x6, dim3((unsigned)grid), dim3(stem6::NTHR), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

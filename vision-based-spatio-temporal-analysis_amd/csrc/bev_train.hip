@@ -64,6 +64,26 @@ __global__ __launch_bounds__(256) void k_dilate(const Q *__restrict__ dz, int N,
     }
 }
 
+// The input gradient of a 1x1 / stride-s / pad-0 conv without dilation: out [N][H][W][C] = residual (or 0) plus, at
+// (s*oy, s*ox), y[n][oy][ox] = dz W -- one pass over out (the dilated form wrote the zero-inserted 4x map and ran the
+// 1x1 conv over it).  Grid (pixel blocks, images), thread = (channel quad, pixel phase) as the streaming passes.
+__global__ __launch_bounds__(256) void k_place_strided(const float4 *__restrict__ y, int Ho, int Wo, int C4, int s,
+                                                       int H, int W, const float4 *__restrict__ res,
+                                                       float4 *__restrict__ out) {
+    const int n = blockIdx.y, tid = threadIdx.x, q = tid % C4, ph = tid / C4, nph = 256 / C4;
+    const int64_t p0 = (int64_t)blockIdx.x * 256, p1 = p0 + 256 < (int64_t)H * W ? p0 + 256 : (int64_t)H * W;
+    for (int64_t p = p0 + ph; p < p1; p += nph) {
+        const int yy = (int)(p / W), xx = (int)(p - (int64_t)yy * W);
+        const int64_t e = ((int64_t)n * H * W + p) * C4 + q;
+        float4 v = res ? res[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (yy % s == 0 && xx % s == 0 && yy / s < Ho && xx / s < Wo) {
+            const float4 u = y[(((int64_t)n * Ho + yy / s) * Wo + xx / s) * C4 + q];
+            v = res ? make_float4(v.x + u.x, v.y + u.y, v.z + u.z, v.w + u.w) : u;  // no residual: y itself (-0 kept)
+        }
+        out[e] = v;
+    }
+}
+
 // dW[co][k], k = (ky*KW + kx)*Ci + ci.  Workgroup = 64 (co) x 64 (k) outputs, 256 threads x (4 x 4);
 // loops over its slice of m in steps of 16 with both operands staged in LDS.
 constexpr int WG_T = 64, WG_M = 16;
@@ -799,6 +819,18 @@ int bev_dilate_nhwc_ex(const void *dz, int elem_bytes, int N, int Ho, int Wo, in
     else
         hipLaunchKernelGGL(k_dilate<uint2>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                            (const uint2 *)dz, N, Ho, Wo, C, s, top, left, Hd, Wd, (uint2 *)out);
+    return last();
+}
+
+int bev_place_strided_f32(const float *y, int N, int Ho, int Wo, int C, int s, int H, int W, const float *residual,
+                          float *out, void *stream) {
+    if (!y || !out || N <= 0 || N > 65535 || Ho <= 0 || Wo <= 0 || C <= 0 || C % 4 != 0 || 256 % (C / 4) != 0 ||
+        s <= 0 || s * (Ho - 1) >= H || s * (Wo - 1) >= W ||
+        (((uintptr_t)y | (uintptr_t)out | (uintptr_t)residual) & 15) != 0)
+        return BEV_ERR_ARGS;
+    const dim3 grid((unsigned)(((int64_t)H * W + 255) / 256), N);
+    hipLaunchKernelGGL(k_place_strided, grid, dim3(256), 0, (hipStream_t)stream, (const float4 *)y, Ho, Wo, C / 4, s,
+                       H, W, (const float4 *)residual, (float4 *)out);
     return last();
 }
 

@@ -1756,7 +1756,7 @@ int warp_tune(int knob, int value) {
 
 extern "C" {
 
-int bev_abi_version(void) { return 7; }
+int bev_abi_version(void) { return 8; }
 
 #if WARP_STAMP
 int bev_warp_stamp_read(unsigned long long *host, int n) {  // timing builds only

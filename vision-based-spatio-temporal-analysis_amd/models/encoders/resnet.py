@@ -75,6 +75,10 @@ class Bottleneck(nn.Module):
         return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, True), (self.conv3, self.bn3, True)]
 
 
+# The ResNet stem on the split arithmetic (FoldedConv.stem_x6); False keeps the exact-f32 stem kernel.
+STEM_X6 = True
+
+
 class FoldedConv:
     """conv (+ eval-mode BN) folded into a packed MFMA weight panel + bias, cached on device.
 
@@ -103,6 +107,14 @@ class FoldedConv:
                 and c.dilation == (1, 1)):
             return "bf16x6"
         return "f32"
+
+    def stem_x6(self) -> bool:
+        """The ResNet stem (7x7 / s2 / p3, Ci 3, Co <= 64) under the bf16x6 arithmetic takes the split-arithmetic
+        stem kernel (STEM_X6, default on; off: the exact-f32 stem, fp32-tolerance equal)."""
+        c = self.conv
+        return (STEM_X6 and self.split_ok and _nat.conv_arith() == "bf16x6" and c.in_channels == 3
+                and c.out_channels <= 64 and c.kernel_size == (7, 7) and c.stride == (2, 2) and c.padding == (3, 3)
+                and c.groups == 1 and c.dilation == (1, 1))
 
     def prepare(self, device, arith: str = None):
         arith = arith or self.arith()
@@ -135,9 +147,12 @@ class FoldedConv:
                  split_out: bool = False):
         """x: NHWC fp32 (NCHW with in_nchw) or, in the bf16x6 arithmetic, a bev_native.Split3; split_out (bf16x6
         only) returns the result as a Split3 -- the pre-split operand of the next conv."""
+        c = self.conv
+        if in_nchw and self.stem_x6():  # the stem on the split arithmetic (bev_conv2d_stem_x6_f32)
+            self.prepare(x.device, "bf16x6")
+            return _nat.conv2d_stem_x6(x, self.packed6, self.bias, c.out_channels, relu, out=out)
         arith = "f32" if (in_nchw or ascale is not None) else self.arith()
         self.prepare(x.device, arith)
-        c = self.conv
         if arith == "bf16x6":
             return _nat.conv2d_nhwc_x6(x, self.packed6, self.bias, c.out_channels, c.kernel_size[0],
                                        c.kernel_size[1], c.stride[0], c.padding[0], 1, int(relu), residual=residual,
