@@ -216,3 +216,28 @@ def test_wgrad_h16_fp16_gradient_vs_float64(shape, x_half):
     err = (dw.cpu().double() - ref).abs()
     assert dw.shape == (Co, Ci, K, K)
     assert float((err / (mag + 1e-12)).max()) < 2e-6
+
+
+@pytest.mark.parametrize("N,H,W,Ci,K,dil,Co,res", [(2, 19, 70, 64, 3, 1, 128, False), (1, 21, 96, 128, 3, 2, 64, True),
+                                                   (1, 9, 40, 64, 3, 1, 192, True)])
+def test_conv_h16_wide_rows_bit_identical(N, H, W, Ci, K, dil, Co, res):
+    """Row tiles spanning image rows (Wo 40-96, ragged last tile), dilation 2, a residual and ReLU: the 64-deep kernel
+    (k_conv_h16b, buffer staging) gives the bits of the 32-deep one (CONV_H16_KERNEL 1) with fp32 operands, and of
+    the fp16-stored operand path.  (Round 5 also measured 2-D 8 x 16 output tiles for these convs: slower on every
+    spatial shape, profiles/r05y_conv_h16_tile2d_ab.txt, not kept.)"""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(Ci + Co + W)
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
+    w = (torch.randn(Co, Ci, K, K, generator=g) / (Ci * K * K) ** 0.5).to(DEV)
+    b = torch.randn(Co, generator=g).to(DEV)
+    r = torch.randn(N, H, W, Co, generator=g).to(DEV) if res else None
+    with nat._half_mode(True):
+        packed = nat.pack_conv_weight(w)
+    pad = dil * (K // 2)
+    z2d = nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, 1, pad, dil, 1, residual=r)
+    with nat.tuned(CONV_H16_KERNEL=1):
+        z32 = nat.conv2d_nhwc_h16(x, packed, b, Co, K, K, 1, pad, dil, 1, residual=r)
+    zh = nat.conv2d_h16_any(x.half(), packed, Co, K, K, 1, pad, bias=b, residual=r, dilation=dil)
+    torch.cuda.synchronize()
+    assert torch.equal(z2d, z32)
+    assert torch.equal(torch.relu(zh), z2d)
