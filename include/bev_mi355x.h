@@ -573,8 +573,14 @@ int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale
 int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                                const float *residual, int act, void *y, int y_half, void *stream);
 
+/* device: bev_batchnorm_apply_f32 with act 1 (ReLU), also writing mask [M * C / 4] bytes: bit u of byte k is
+ * (y[4 k + u] > 0) -- the ReLU mask the backward's act 4 reads (1 B per 4 elements) instead of y; 256 % (C / 4) == 0.
+ * Replaces the residual-add + ReLU of timm's Bottleneck.forward (conv3 / bn3 + shortcut) in training. */
+int bev_batchnorm_apply_mask_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                                 const float *residual, float *y, uint8_t *mask, void *stream);
+
 /* device: backward of y = act(batchnorm(z) (+ residual)): act 1 (ReLU) takes its mask from the forward output
- * y, act 3 (ReLU of a layer WITHOUT residual; dres must be NULL, y is not read) recomputes it exactly as
+ * y, act 4 (ReLU) from the mask bytes of bev_batchnorm_apply_mask_f32 passed as y (bit-identical to act 1), act 3 (ReLU of a layer WITHOUT residual; dres must be NULL, y is not read) recomputes it exactly as
  * z * scale + shift > 0 (apply's rounding), act 2 (SiLU) recomputes u = z * scale + shift; frozen = 1 for running statistics (the mean / variance are
  * constants: dz = gamma * rstd * g).  dz [M][C], dres [M][C] (the gradient reaching the residual; may be NULL),
  * dgamma, dbeta [C], all OVERWRITTEN. */

@@ -516,6 +516,37 @@ def test_batchnorm_bwd_relu_mask_from_z():
         nat.batchnorm_bwd(dy, None, z, mean, rstd, gamma, True, nat.ACT_RELU_FROM_Z, scale, shift)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [64, 256, 512])
+def test_batchnorm_relu_mask_bytes(C):
+    """bev_batchnorm_apply_mask_f32 (ReLU with a residual, mask bytes: bit u of byte k = y[4k + u] > 0) writes the
+    y of bev_batchnorm_apply_f32 bit for bit and the mask of that y; the backward with act 4 (mask bytes passed as
+    y) == act 1 (mask from y) bit for bit in dz (fp32 and fp16 storage), the residual gradient, dgamma and dbeta --
+    including pre-activations at / around the ReLU kink."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(C)
+    N, H, W = 2, 13, 17
+    z = torch.randn(N, H, W, C, generator=g).to(DEV)
+    res = torch.randn(N, H, W, C, generator=g).to(DEV)
+    gamma, beta = (torch.rand(C, generator=g) + 0.5).to(DEV), (torch.randn(C, generator=g) * 0.3).to(DEV)
+    mean, rstd, scale, shift = nat.batchnorm_train_fwd(z, gamma, beta, None, None, 1e-5, 0.1)
+    z.view(-1, C)[::5] = -shift / scale
+    res.view(-1, C)[::5] = 0.0
+    dy = torch.randn(N, H, W, C, generator=g).to(DEV)
+    y = nat.batchnorm_apply(z, scale, shift, res, 1)
+    y2, mask = nat.batchnorm_apply_mask(z, scale, shift, res)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    bits = (y.view(-1, 4) > 0).to(torch.uint8)
+    ref_mask = bits[:, 0] | (bits[:, 1] << 1) | (bits[:, 2] << 2) | (bits[:, 3] << 3)
+    assert torch.equal(mask, ref_mask)
+    a = nat.batchnorm_bwd(dy, y, z, mean, rstd, gamma, True, 1, scale, shift)
+    b = nat.batchnorm_bwd_half(dy, mask, z, mean, rstd, gamma, True, nat.ACT_RELU_MASK, scale, shift)
+    c = nat.batchnorm_bwd_half(dy, y, z, mean, rstd, gamma, True, 1, scale, shift)
+    for u, v in zip((c[0], a[1], a[2], a[3]), (b[0], b[1], b[2], b[3])):
+        assert torch.equal(u, v)
+
+
 DW_CASES = [(2, 96, 17, 23, 3, 1), (1, 144, 20, 31, 3, 2), (2, 40, 13, 11, 5, 1), (1, 240, 18, 22, 5, 2),
             (1, 1152, 5, 7, 3, 1)]
 

@@ -235,8 +235,15 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
             head_masks.append((u > 0).permute(0, 3, 1, 2).double().cpu())
         return out
 
+    bn_apply_mask = nat.batchnorm_apply_mask
+
+    def rec_bn_mask(z, scale, shift, residual=None):  # block outputs: y and its ReLU mask bytes
+        out, mask = bn_apply_mask(z, scale, shift, residual)
+        trunk_masks.append((out > 0).permute(0, 3, 1, 2).double().cpu())
+        return out, mask
+
     nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = rec_bn, rec_bn_half, rec_gn
-    nat.groupnorm_apply_half = rec_gn_half
+    nat.groupnorm_apply_half, nat.batchnorm_apply_mask = rec_gn_half, rec_bn_mask
     scaler = torch.amp.GradScaler("cuda") if amp else None
     try:
         model.zero_grad(set_to_none=True)
@@ -251,7 +258,7 @@ def test_bevnet_r50_training_step_vs_float64_reference(amp):
             losses["total_loss"].backward()
     finally:
         nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = bn_apply, bn_apply_half, gn_apply
-        nat.groupnorm_apply_half = gn_apply_half
+        nat.groupnorm_apply_half, nat.batchnorm_apply_mask = gn_apply_half, bn_apply_mask
     if amp:
         opt = torch.optim.SGD(model.parameters(), lr=0.0)
         scaler.unscale_(opt)
@@ -638,8 +645,15 @@ def test_bevnet_r50_amp_step_full_geometry():
             head_masks.append((u > 0).permute(0, 3, 1, 2).cpu())
         return out
 
+    bn_apply_mask = nat.batchnorm_apply_mask
+
+    def rec_bn_mask(z, scale, shift, residual=None):  # block outputs: y and its ReLU mask bytes
+        out, mask = bn_apply_mask(z, scale, shift, residual)
+        trunk_masks.append((out > 0).permute(0, 3, 1, 2).cpu())
+        return out, mask
+
     nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = rec_bn, rec_bn_half, rec_gn
-    nat.groupnorm_apply_half = rec_gn_half
+    nat.groupnorm_apply_half, nat.batchnorm_apply_mask = rec_gn_half, rec_bn_mask
     scaler = torch.amp.GradScaler("cuda")
     try:
         model.zero_grad(set_to_none=True)
@@ -649,7 +663,7 @@ def test_bevnet_r50_amp_step_full_geometry():
         scaler.scale(losses["total_loss"]).backward()
     finally:
         nat.batchnorm_apply, nat.batchnorm_apply_half, nat.groupnorm_apply = bn_apply, bn_apply_half, gn_apply
-        nat.groupnorm_apply_half = gn_apply_half
+        nat.groupnorm_apply_half, nat.batchnorm_apply_mask = gn_apply_half, bn_apply_mask
     opt = torch.optim.SGD(model.parameters(), lr=0.0)
     scaler.unscale_(opt)
     torch.cuda.synchronize()

@@ -1,0 +1,14 @@
+# Round 5 pass z: the block output's ReLU mask as bytes (bn3 backward act 4) -- tests, then the AMP training step with
+# and without it (--no-mask-bytes), alternating, same process type, and the profile.
+set -u
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/$1; mkdir -p $O
+timeout -k 10 700 python -u -m pytest -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread tests/test_train.py tests/test_train_amp_gpu.py > $O/tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/tests.log; [ $rc -ne 0 ] && exit $rc
+for r in 1 2; do
+  timeout -k 10 200 python -u tools/train_step_bench.py --steps 5 --bevnet --amp > $O/train_mask_$r.log 2>&1 || exit $?
+  timeout -k 10 200 python -u tools/train_step_bench.py --steps 5 --bevnet --amp --no-mask-bytes > $O/train_nomask_$r.log 2>&1 || exit $?
+done
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tprof -o run -- python3 tools/train_step_bench.py --steps 3 --warmup 1 --bevnet --amp > $O/tprof.log 2>&1 || exit $?
+exit 0

@@ -33,9 +33,14 @@ def main():
     ap.add_argument("--proj-ch", type=int, default=128, help="BEVNet BEV_PROJ_CH (configs/wildtrack.yaml:14: 128)")
     ap.add_argument("--fp32-kernels", action="store_true")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V", help="bev_tune knob (A/B); repeatable")
+    ap.add_argument("--no-mask-bytes", action="store_true", help="A/B: bn3's backward re-reads the fp32 block output "
+                    "instead of the forward's ReLU mask bytes (trunk_grad.RELU_MASK_BYTES)")
     a = ap.parse_args()
     import bev_native
     bev_native.AMP_HALF_CONVS = not a.fp32_kernels
+    if a.no_mask_bytes:
+        from models.encoders import trunk_grad
+        trunk_grad.RELU_MASK_BYTES = False
     for kv in a.tune:
         name, v = kv.split("=")
         bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))

@@ -34,6 +34,7 @@ _d = ctypes.c_double
 # name -> (restype, argtypes); must match include/bev_mi355x.h
 SIGNATURES = {
     "bev_abi_version": (_i, []),
+    "bev_batchnorm_apply_mask_f32": (_i, [_vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_place_strided_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "bev_conv2d_stem_x6_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
     "bev_build_source_hash": (ctypes.c_char_p, []),
@@ -755,6 +756,7 @@ def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, K
 
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2  # `relu` argument of conv2d_nhwc / dwconv2d_nhwc
 ACT_RELU_FROM_Z = 3  # batchnorm_bwd only: ReLU of a layer without residual, mask recomputed from z (y not read)
+ACT_RELU_MASK = 4  # batchnorm_bwd only: ReLU, mask from batchnorm_apply_mask's bytes (passed as y; bit-identical to 1)
 H16_STAT_ROWS = 128  # rows per BatchNorm statistics tile of conv2d_nhwc_h16_bnstats
 
 
@@ -871,11 +873,33 @@ def batchnorm_apply_half(z: torch.Tensor, scale, shift, act: int = 0) -> torch.T
     return y
 
 
+def batchnorm_apply_mask(z: torch.Tensor, scale, shift, residual=None):
+    """y = relu(z * scale + shift (+ residual)) and its ReLU mask bytes (bit u of byte k: y[4k + u] > 0) for the
+    backward's ACT_RELU_MASK (bev_batchnorm_apply_mask_f32) -> (y fp32, mask uint8 [numel / 4])."""
+    _require_gpu(z, scale, shift, residual)
+    assert z.is_contiguous()
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == z.shape
+    C = z.shape[-1]
+    y = torch.empty_like(z)
+    mask = torch.empty(z.numel() // 4, device=z.device, dtype=torch.uint8)
+    _check(lib().bev_batchnorm_apply_mask_f32(_ptr(z), z.numel() // C, C, _ptr(scale), _ptr(shift), _ptr(residual),
+                                              _ptr(y), _ptr(mask), _stream(z)), "bev_batchnorm_apply_mask_f32")
+    return y, mask
+
+
 def batchnorm_bwd_half(dy: torch.Tensor, y, z: torch.Tensor, mean, rstd, gamma, want_dres: bool, act: int = 1,
                        scale=None, shift=None, frozen: bool = False):
-    """batchnorm_bwd with dz stored in fp16 (for a dz read only by the fp16-operand dgrad / weight gradient)."""
+    """batchnorm_bwd with dz stored in fp16 (for a dz read only by the fp16-operand dgrad / weight gradient).
+    act ACT_RELU_MASK: `y` is the forward's ReLU mask bytes (batchnorm_apply_mask)."""
     dy = dy.contiguous()
-    _require_gpu(dy, y, z, mean, rstd, gamma, scale, shift)
+    if act == ACT_RELU_MASK:
+        if y is None or not y.is_cuda or y.dtype != torch.uint8 or y.numel() * 4 != z.numel():
+            raise HipError("ACT_RELU_MASK needs the forward's uint8 mask (batchnorm_apply_mask)")
+        _require_gpu(dy, z, mean, rstd, gamma, scale, shift)
+    else:
+        _require_gpu(dy, y, z, mean, rstd, gamma, scale, shift)
     C = z.shape[-1]
     M = z.numel() // C
     dz = torch.empty(z.shape, device=z.device, dtype=torch.float16)

@@ -54,7 +54,9 @@ __device__ __forceinline__ float silu_grad(float u) {
 }
 
 // g = dy * act'(u) for the 4 channels c .. c+3 of element i (act 1: y > 0 from the saved output; act 3: ReLU of a
-// layer without residual, y > 0 recomputed from z so y is not read; act 2: u = z * scale + shift)
+// layer without residual, y > 0 recomputed from z so y is not read; act 4: ReLU, y > 0 from the forward's mask
+// bytes (k_bn_apply_q's `mask`: 1 B per 4 elements instead of re-reading the 4-B y twice); act 2: u = z * scale +
+// shift)
 __device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const float *y, const float4 v,
                                          const float *scale, const float *shift, int act, int64_t i, int c) {
     g[0] = d.x;
@@ -66,6 +68,10 @@ __device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const fl
         const float ov[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) g[u] = ov[u] > 0.f ? g[u] : 0.f;
+    } else if (act == 4) {  // ReLU, the forward's mask bytes (bit u of byte i / 4: y[i + u] > 0) instead of y
+        const unsigned m = reinterpret_cast<const uint8_t *>(y)[i >> 2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[u] = (m >> u) & 1u ? g[u] : 0.f;
     } else if (act == 3) {  // ReLU without residual: y > 0 <=> u > 0, u exactly as k_bn_apply computed it
         const float zv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -322,7 +328,8 @@ constexpr int BNQ_ROWS = 256;
 template <typename OT>
 __global__ __launch_bounds__(256) void k_bn_apply_q(const float *__restrict__ z, int64_t M, int C,
                                                     const float *__restrict__ scale, const float *__restrict__ shift,
-                                                    const float *__restrict__ res, int act, OT *__restrict__ y) {
+                                                    const float *__restrict__ res, int act, OT *__restrict__ y,
+                                                    uint8_t *__restrict__ mask) {
     const int tid = threadIdx.x, QP = C / 4, q = tid % QP, ph = tid / QP, nph = 256 / QP;
     const int64_t r0 = (int64_t)blockIdx.x * BNQ_ROWS, r1 = r0 + BNQ_ROWS < M ? r0 + BNQ_ROWS : M;
     const float4 s = *(const float4 *)(scale + 4 * q), h = *(const float4 *)(shift + 4 * q);
@@ -337,6 +344,8 @@ __global__ __launch_bounds__(256) void k_bn_apply_q(const float *__restrict__ z,
         if (act == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
         if (act == 2) o = make_float4(silu_hw(o.x), silu_hw(o.y), silu_hw(o.z), silu_hw(o.w));
         st4(y, e, o);
+        if (mask)  // act 1: bit u = (y[e + u] > 0), what the backward's act 4 reads instead of y
+            mask[e >> 2] = (uint8_t)((o.x > 0.f) | ((o.y > 0.f) << 1) | ((o.z > 0.f) << 2) | ((o.w > 0.f) << 3));
     }
 }
 
@@ -482,10 +491,10 @@ int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *sc
         const dim3 gq((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS));
         if (y_half)
             hipLaunchKernelGGL(k_bn_apply_q<_Float16>, gq, dim3(256), 0, st, z, M, C, scale, shift, residual, act,
-                               (_Float16 *)y);
+                               (_Float16 *)y, (uint8_t *)nullptr);
         else
             hipLaunchKernelGGL(k_bn_apply_q<float>, gq, dim3(256), 0, st, z, M, C, scale, shift, residual, act,
-                               (float *)y);
+                               (float *)y, (uint8_t *)nullptr);
         return (int)hipGetLastError();
     }
     const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
@@ -504,6 +513,14 @@ int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *sc
     return (int)hipGetLastError();
 }
 
+int bev_batchnorm_apply_mask_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
+                                 const float *residual, float *y, uint8_t *mask, void *stream) {
+    if (!z || !scale || !shift || !y || !mask || !bn_shape_ok(M, C) || 256 % (C / 4) != 0) return BEV_ERR_ARGS;
+    hipLaunchKernelGGL(k_bn_apply_q<float>, dim3((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS)), dim3(256), 0,
+                       (hipStream_t)stream, z, M, C, scale, shift, residual, 1, y, mask);
+    return (int)hipGetLastError();
+}
+
 int bev_batchnorm_apply_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                             const float *residual, int act, float *y, void *stream) {
     return bev_batchnorm_apply_ex_f32(z, M, C, scale, shift, residual, act, y, 0, stream);
@@ -514,7 +531,7 @@ int bev_batchnorm_bwd_ex_f32(const float *dy, const float *y, const float *z, in
                              int frozen, void *dz, int dz_half, float *dres, float *dgamma, float *dbeta,
                              void *workspace, void *stream) {
     if (!dy || !z || !mean || !rstd || !gamma || !dz || !dgamma || !dbeta || !workspace || !bn_shape_ok(M, C) ||
-        act < 0 || act > 3 || (act == 1 && !y) || ((act == 2 || act == 3) && (!scale || !shift)) ||
+        act < 0 || act > 4 || ((act == 1 || act == 4) && !y) || ((act == 2 || act == 3) && (!scale || !shift)) ||
         (act == 3 && dres))  // act 3: ReLU recomputed from z, only for a layer without residual
         return BEV_ERR_ARGS;
     hipStream_t st = (hipStream_t)stream;

@@ -480,8 +480,18 @@ __device__ __forceinline__ uint32_t out_range(size_t total_bytes, size_t base) {
 #define WARP_STAGE_ALL 0  // fused warp v2: all live views staged at once when they fit the pool (1, A/B: neutral) or per view (0)
 #endif
 // LDS bytes of an np-pixel footprint image (17-slot pixels); dma_block rounds to its 1-KiB instructions
+#ifndef WARP_CK
+#define WARP_CK 64  // fused warp v2 channels per workgroup: 64 (one workgroup per tile and frame) or 32 (A/B: two
+                    // workgroups per tile, each staging and sampling every other 32-channel group -- half the LDS image
+                    // and accumulator per workgroup, the taps computed twice)
+#endif
+static_assert(WARP_CK == 64 || WARP_CK == 32, "WARP_CK: 64 or 32");
+static_assert(WARP_CK == 64 || WARP_DMA_ROWS == 0, "the row DMA stages 64-channel pixels");
+constexpr int V2_SL = WARP_CK / 4 + 1;  // DMA slots of 16 B per staged pixel (WARP_CK channels + pad)
+constexpr int V2_SPLIT = 64 / WARP_CK;  // workgroups per (tile, frame)
+
 __device__ __forceinline__ int stage_bytes(int np) {
-    return WARP_DMA_ROWS ? np * 272 : ((np * 17 + 63) >> 6) * 1024;
+    return WARP_DMA_ROWS ? np * 272 : ((np * V2_SL + 63) >> 6) * 1024;
 }
 
 #ifndef WARP_STORE_AUX
@@ -896,7 +906,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                                                           const uint2 *__restrict__ boxes_in, int rpr) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
-    constexpr int SL = 17, PS = SL * 16;  // DMA slots / bytes per staged pixel (64 channels + pad)
+    constexpr int CK = WARP_CK, SL = V2_SL, PS = SL * 16;  // channels / DMA slots / bytes per staged pixel (+ pad)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int zp = pool;                                    // zero pixel (256 B)
     int *red = reinterpret_cast<int *>(smem + pool + 256);  // [4 * NW] exact-bbox exchange
@@ -920,7 +930,8 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     };
     const int i = tyb * TH + tr;
     const int j = txb * TW + tc;
-    const int b = blockIdx.y;
+    const int b = V2_SPLIT == 1 ? (int)blockIdx.y : (int)blockIdx.y / V2_SPLIT;
+    const int cfirst = V2_SPLIT == 1 ? 0 : ((int)blockIdx.y % V2_SPLIT) * CK;  // this workgroup's first channel
     const bool inside = (i < Hb) && (j < Wb);
     const float cx = xs[inside ? j : 0], cy = ys[inside ? i : 0];
     const size_t plane = (size_t)Hb * Wb;
@@ -929,10 +940,10 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     // checks the whole output is < 2 GiB), the (frame, channel) base and the channel plane stay uniform
     // (CHUNK only: the plain layout keeps the round-4 addressing -- no extra live registers in the default kernel)
     const size_t oplane = CHUNK ? (size_t)rpr * Wb : plane;
-    auto store_out = [&](int c0, const float (&acc)[64], const MeanDiv &md) {
+    auto store_out = [&](int c0, const float (&acc)[CK], const MeanDiv &md) {
         if (!CHUNK) {
             store_chunk(out + ((size_t)b * C + c0) * plane, plane, (i * Wb + j) * (int)sizeof(float), acc, MODE, md,
-                        (uint32_t)(plane * 64 * sizeof(float)));
+                        (uint32_t)(plane * CK * sizeof(float)));
             return;
         }
         const int ck = i / rpr;
@@ -1025,13 +1036,13 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     };
 
     {
-      for (int c0 = 0; c0 < C; c0 += 64) {
+      for (int c0 = cfirst; c0 < C; c0 += 64) {
         ccx = cx;
         ccy = cy;
         asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep taps per chunk (no hoisting + spills)
-        float acc[64];
+        float acc[CK];
 #pragma unroll
-        for (int q = 0; q < 64; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
+        for (int q = 0; q < CK; ++q) acc[q] = (MODE == BEV_FUSE_MAX) ? -__builtin_inff() : 0.0f;
         const float *fb = feats + (int64_t)(b * V) * sN + c0;
 
         // Views whose corner box is empty (the tile is outside that camera's feature map)
@@ -1082,7 +1093,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                     const int w = bx.x1 - bx.x0 + 1;
                     const Taps t = taps_of(u);
                     if (__ballot(t.valid != 0) != 0ull && (!WARP_LANESKIP || t.valid))
-                        sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, w, zp, zp);
+                        sample_view_pipe<MODE, CK, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, w, zp, zp);
                     else
                         zero_view<MODE>(acc, u);
                     off += stage_bytes(w * (bx.y1 - bx.y0 + 1));
@@ -1175,7 +1186,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         __syncthreads();
                         const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
                         const bool go = single ? wave_any : (__ballot(mine) != 0ull);
-                        if (go) sample_view<MODE, 1, 64>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                        if (go) sample_view<MODE, 1, CK>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
                         else if (single) zero_view<MODE>(acc, v);
                     }
                 done = true;
@@ -1210,12 +1221,12 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         // the next view's taps inside this view's sampling, by every lane (a lane without a valid tap
                         // reads the zero pixel: its sample is +0, i.e. acc + 0 == acc, or max(acc, +0) -- what the
                         // lane skip gives)
-                        sample_view_pipe<MODE, 64, WARP_PIPE != 0, WARP_TAPS_AHEAD - 2>(
+                        sample_view_pipe<MODE, CK, WARP_PIPE != 0, WARP_TAPS_AHEAD - 2>(
                             acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp, [&]() { tf = taps_of(vn); });
                         if (WARP_TAPS_AHEAD == 1) tf = taps_of(vn);  // after the sampling, before the DMA wait
                         have_f = true;
                     } else if (!WARP_LANESKIP || t.valid)
-                        sample_view_pipe<MODE, 64, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+                        sample_view_pipe<MODE, CK, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
                     else zero_view<MODE>(acc, v);
                 } else zero_view<MODE>(acc, v);
             } else if (empty) {
@@ -1655,11 +1666,11 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
                        int mode, float *out, hipStream_t st, int pool, uint2 *boxes, bool boxes_ready, int rpr) {
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
-    dim3 grid(ntiles, B), block(FT_NT);
+    dim3 grid(ntiles, B * V2_SPLIT), block(FT_NT);
     const size_t lds = (size_t)pool + V2_FIXED;
     if (!WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (LDS homographies)
     if (boxes && !boxes_ready) {  // else bev_ipm_warp_fuse_boxes_f32 wrote them (same geometry, pool and knobs)
-        const int maxpix = pool / (17 * 16) - 4;  // the kernel's own pool test
+        const int maxpix = pool / (V2_SL * 16) - 4;  // the kernel's own pool test
         hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                            st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes);
     }
@@ -1861,7 +1872,7 @@ int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float 
     if (B == 0 || Hb == 0 || Wb == 0) return 0;
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
-    const int maxpix = v2_pool_bytes(mode) / (17 * 16) - 4;  // k_warp_fuse_v2's own pool test
+    const int maxpix = v2_pool_bytes(mode) / (V2_SL * 16) - 4;  // k_warp_fuse_v2's own pool test
     hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                        (hipStream_t)stream, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH,
                        reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR));

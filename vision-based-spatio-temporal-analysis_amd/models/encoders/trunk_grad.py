@@ -299,6 +299,11 @@ def _dgrad_h16(dz: torch.Tensor, wf: torch.Tensor, H: int, W: int, stride: int, 
     return _nat.conv2d_h16_any(d, packed, Ci, K, K, 1, 0, residual=residual)
 
 
+# BottleneckTrainH16: keep the block output's ReLU mask as bytes for bn3's backward (default), or the fp32 output
+# itself (A/B: tools/train_step_bench.py --no-mask-bytes; bit-identical results)
+RELU_MASK_BYTES = True
+
+
 class BottleneckTrainH16(torch.autograd.Function):
     """One timm Bottleneck (conv1 1x1 -> BN -> ReLU -> conv2 3x3 -> BN -> ReLU -> conv3 1x1 -> BN, + shortcut, ReLU)
     in training with batch-statistics BN under autocast(float16), as ONE autograd node, so the tensors that live
@@ -309,7 +314,8 @@ class BottleneckTrainH16(torch.autograd.Function):
         (`batchnorm_bwd_half`);
     both are exactly the values the fp32-stored path rounds them to, so every result is bit-identical to the
     per-layer `ConvBNTrain` chain (`tests/test_train_amp_gpu.py::test_bottleneck_h16_block_bit_identical`), with
-    half the bytes on those tensors.  The statistics come from the conv epilogues, the ReLU masks of y1 / y2 from
+    half the bytes on those tensors; the block output's ReLU mask is kept as bytes (1 B per 4 elements) for bn3's
+    backward instead of re-reading the fp32 output twice.  The statistics come from the conv epilogues, the ReLU masks of y1 / y2 from
     z, and an identity shortcut's gradient is added in conv1's dgrad epilogue.  `sc`: the shortcut tensor (the
     downsample branch's output), or None for the identity (x).  `x_sink` (downsample blocks): the node's gradient of x
     is handed to the downsample conv's node (which consumes it as its dgrad epilogue's residual; that node's backward
@@ -333,12 +339,14 @@ class BottleneckTrainH16(torch.autograd.Function):
             mean, rstd, scale, shift, _ = _bn_affine(bn, z, g, b, tiles)
             if i < 2:
                 y = _nat.batchnorm_apply_half(z, scale, shift, 1)
+            elif RELU_MASK_BYTES:  # the block output, and its ReLU mask as bytes for the backward (not the 4-B y,
+                y, mask = _nat.batchnorm_apply_mask(z, scale, shift, x if sc is None else sc)  # read twice there)
             else:
-                y = _nat.batchnorm_apply(z, scale, shift, x if sc is None else sc, 1)
+                y = mask = _nat.batchnorm_apply(z, scale, shift, x if sc is None else sc, 1)
             saved += [h, z, wd, mean, rstd, g, scale, shift]
             meta.append((k, st, p))
             h = y
-        ctx.save_for_backward(*saved, h)
+        ctx.save_for_backward(*saved, mask)
         ctx.meta = (meta, sc is not None)
         return h
 
@@ -347,7 +355,7 @@ class BottleneckTrainH16(torch.autograd.Function):
     def backward(ctx, dy):
         t = ctx.saved_tensors
         meta, has_sc = ctx.meta
-        y3 = t[24]
+        mask3 = t[24]
         g = dy.contiguous().float()
         grads = [None] * 3
         dres = None
@@ -355,7 +363,8 @@ class BottleneckTrainH16(torch.autograd.Function):
             h, z, wd, mean, rstd, gamma, scale, shift = t[8 * i: 8 * i + 8]
             k, st, p = meta[i]
             if i == 2:
-                dz, dres, dgm, dbt = _nat.batchnorm_bwd_half(g, y3, z, mean, rstd, gamma, True, 1, scale, shift)
+                act = _nat.ACT_RELU_MASK if mask3.dtype == torch.uint8 else 1  # mask bytes, or y itself
+                dz, dres, dgm, dbt = _nat.batchnorm_bwd_half(g, mask3, z, mean, rstd, gamma, True, act, scale, shift)
             else:
                 dz, _, dgm, dbt = _nat.batchnorm_bwd_half(g, None, z, mean, rstd, gamma, False,
                                                           _nat.ACT_RELU_FROM_Z, scale, shift)
