@@ -84,6 +84,8 @@ def parse():
                          "exact-f32 MFMA kernels")
     ap.add_argument("--stem-f32", action="store_true", help="ResNet: the exact-f32 stem kernel instead of the "
                     "split-arithmetic one (A/B only; resnet.STEM_X6)")
+    ap.add_argument("--no-stem-pool", action="store_true", help="ResNet: the stem output written and max-pooled "
+                    "by its own launch instead of the fused stem + max-pool (A/B)")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V",
                     help="set a performance knob (include/bev_mi355x.h BEV_TUNE_<NAME>) before the run; repeatable")
     ap.add_argument("--warp-kernel", choices=("dma", "register", "rows"), default="dma",
@@ -434,9 +436,10 @@ def main():
     if hasattr(enc.backbone, "stream_groups"):
         if args.stream_groups is not None:
             enc.backbone.stream_groups = args.stream_groups
-        if args.stem_f32:
+        if args.stem_f32 or args.no_stem_pool:
             import models.encoders.resnet as _resnet
-            _resnet.STEM_X6 = False
+            _resnet.STEM_X6 = _resnet.STEM_X6 and not args.stem_f32
+            _resnet.STEM_POOL = _resnet.STEM_POOL and not args.no_stem_pool
         if args.stream_offset is not None:
             enc.backbone.stream_offset = args.stream_offset
     geom = GeometryTransformer(args.bev[0], args.bev[1], BOUNDS)

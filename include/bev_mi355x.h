@@ -297,6 +297,9 @@ int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, in
 /* device: layout conversions between NCHW and NHWC. */
 int bev_nchw_to_nhwc_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
 int bev_nhwc_to_nchw_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
+/* device: NCHW [N][C][H][W] with C <= 4 -> NHWC [N][H][W][4], channels >= C zero (y 16-B aligned): the training
+ * stem's input as the float4 operand of its weight gradient (trunk_grad.py ConvBNTrain). */
+int bev_nchw_to_nhwc4_f32(const float *x, int N, int C, int H, int W, float *y, void *stream);
 
 /* ---------------------------------------------------------------------------
  * EfficientNet trunk (timm efficientnet_b3 features_only, cnn_encoder.py:26,
@@ -478,6 +481,15 @@ int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, co
  * = act(conv + bias), act 0 / 1 (ReLU).  fp32-tolerance equal to the exact-f32 stem of bev_conv2d_f32. */
 int bev_conv2d_stem_x6_f32(const float *x, int N, int H, int W, const uint16_t *packed, const float *bias, int Co,
                            int relu, float *y, int Ho, int Wo, void *stream);
+
+/* device: the same stem (Co = 64, ReLU) followed by timm's stem max-pool (3x3, stride 2, pad 1; cnn_encoder.py:26,
+ * features_only's maxpool) in one pass: y NHWC [N][Hp][Wp][64], Hp = (Ho - 1) / 2 + 1 (Wp alike), bit-identical to
+ * bev_conv2d_stem_x6_f32 + bev_maxpool2d_nhwc_f32 without writing the stem output.  workspace (16-B aligned) holds
+ * the tile seams: at least bev_conv2d_stem_pool_x6_workspace(N, H, W) bytes. */
+int64_t bev_conv2d_stem_pool_x6_workspace(int N, int H, int W);
+int bev_conv2d_stem_pool_x6_f32(const float *x, int N, int H, int W, const uint16_t *packed, const float *bias,
+                                int Co, float *y, int Hp, int Wp, void *workspace, int64_t workspace_bytes,
+                                void *stream);
 
 /* device: split n fp32 values into planes [3][n] bf16 with x == h + m + l exactly (the operand format of
  * bev_conv2d_x6_f32's xs). */

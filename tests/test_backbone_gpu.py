@@ -225,6 +225,11 @@ def test_maxpool_and_layouts_exact():
     assert torch.equal(nat.nhwc_to_nchw(xn).cpu(), x)
     y = nat.maxpool_nhwc(xn, 3, 2, 1)
     assert torch.equal(y.permute(0, 3, 1, 2).cpu(), F.max_pool2d(x, 3, 2, 1))
+    for shape in ((3, 3, 36, 20), (2, 3, 7, 5)):  # 3-channel images: the 4-pixel kernel (H*W % 4 == 0) and the tiles
+        x3 = _rand(shape, 6)
+        assert torch.equal(nat.nchw_to_nhwc(x3.to(DEV)).cpu(), x3.permute(0, 2, 3, 1).contiguous())
+        x4 = nat.nchw_to_nhwc4(x3.to(DEV)).cpu()  # 4-channel pixels with a zero channel (the stem's wgrad operand)
+        assert torch.equal(x4[..., :3], x3.permute(0, 2, 3, 1)) and not x4[..., 3].any()
 
 
 def test_encoder_proj_streaming_loads_same_result():

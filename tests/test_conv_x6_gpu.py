@@ -217,3 +217,20 @@ def test_stem_x6_vs_float64_and_exact_stem(N, H, W, Co, relu):
     assert torch.isfinite(y6).all()
     assert e6.max().item() <= 1e-5 * scale, (e6.max().item(), scale)
     assert e6.max().item() <= 4 * ef.max().item() + 1e-7 * scale, (e6.max().item(), ef.max().item())
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 45, 140), (3, 37, 131), (1, 1080, 1920), (2, 8, 8)],
+                         ids=["ragged", "odd-sizes", "bench-frame", "one-tile"])
+def test_stem_pool_x6_bit_identical_to_stem_then_maxpool(N, H, W):
+    """The stem with timm's max-pool fused into its epilogue (bev_conv2d_stem_pool_x6_f32: tile seams exported and
+    folded in by k_stem_pool_seams) equals bev_conv2d_stem_x6_f32 (ReLU) + bev_maxpool2d_nhwc_f32(3, 2, 1) bit for bit
+    -- ragged and odd image sizes (pooled rows / columns past a tile, seams on both axes and their corners), several
+    images, one 1080p frame, an image smaller than one tile."""
+    x, w, b = _case(N, H, W, 3, 64, 7, 321 + H)
+    xd, bd = x.float().to(DEV), b.float().to(DEV)
+    packed = nat.pack_conv_weight_x6(w.float().to(DEV))
+    ref = nat.maxpool_nhwc(nat.conv2d_stem_x6(xd, packed, bd, 64, True), 3, 2, 1)
+    got = nat.conv2d_stem_pool_x6(xd, packed, bd)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), (got - ref).abs().max().item()

@@ -19,7 +19,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -37,6 +37,8 @@ SIGNATURES = {
     "bev_batchnorm_apply_mask_f32": (_i, [_vp, _i64, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     "bev_place_strided_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "bev_conv2d_stem_x6_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
+    "bev_conv2d_stem_pool_x6_workspace": (_i64, [_i, _i, _i]),
+    "bev_conv2d_stem_pool_x6_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _i64, _vp]),
     "bev_build_source_hash": (ctypes.c_char_p, []),
     "bev_tune": (_i, [_i, _i]),
     "bev_linspace_f32": (_i, [_d, _d, _i, _vp]),
@@ -81,6 +83,7 @@ SIGNATURES = {
                                        _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
     "bev_maxpool2d_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _vp]),
     "bev_nchw_to_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
+    "bev_nchw_to_nhwc4_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_nhwc_to_nchw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp]),
     "bev_dwconv_psum_blocks": (_i, [_i, _i, _i, _i]),
     "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
@@ -713,6 +716,27 @@ def conv2d_stem_x6(x: torch.Tensor, packed: torch.Tensor, bias: torch.Tensor, Co
     return out
 
 
+def conv2d_stem_pool_x6(x: torch.Tensor, packed: torch.Tensor, bias: torch.Tensor, Co: int = 64) -> torch.Tensor:
+    """conv2d_stem_x6 with ReLU followed by maxpool_nhwc(3, 2, 1) in one pass (bev_conv2d_stem_pool_x6_f32; Co = 64):
+    NCHW [N,3,H,W] images -> the pooled NHWC [N,Hp,Wp,64], bit-identical to the two calls."""
+    x = x.contiguous()
+    _require_gpu(x, bias)
+    N, Ci, H, W = x.shape
+    if Ci != 3 or Co != 64 or not packed.is_cuda or packed.dtype != torch.bfloat16:
+        raise HipError("conv2d_stem_pool_x6 takes NCHW 3-channel images, Co 64 and the split (bf16) weight panel")
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+    Hp, Wp = (Ho - 1) // 2 + 1, (Wo - 1) // 2 + 1
+    ws_bytes = int(lib().bev_conv2d_stem_pool_x6_workspace(N, H, W))
+    _check(min(ws_bytes, 0), "bev_conv2d_stem_pool_x6_workspace")
+    ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
+    out = torch.empty(N, Hp, Wp, 64, device=x.device, dtype=torch.float32)
+    with _span("conv", x):
+        rc = lib().bev_conv2d_stem_pool_x6_f32(_ptr(x), N, H, W, _ptr(packed), _ptr(bias.contiguous().float()), Co,
+                                               _ptr(out), Hp, Wp, _ptr(ws), ws_bytes, _stream(x))
+    _check(rc, "bev_conv2d_stem_pool_x6_f32")
+    return out
+
+
 def conv2d_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
                 relu: bool, residual: torch.Tensor = None, in_nchw: bool = False, out: torch.Tensor = None,
                 ascale: torch.Tensor = None):
@@ -1129,6 +1153,17 @@ def nchw_to_nhwc(x: torch.Tensor) -> torch.Tensor:
     N, C, H, W = x.shape
     y = torch.empty(N, H, W, C, device=x.device, dtype=torch.float32)
     _check(lib().bev_nchw_to_nhwc_f32(_ptr(x), N, C, H, W, _ptr(y), _stream(x)), "bev_nchw_to_nhwc_f32")
+    return y
+
+
+def nchw_to_nhwc4(x: torch.Tensor) -> torch.Tensor:
+    """[N,C,H,W] (C <= 4) -> [N,H,W,4] NHWC with zero channels past C (bev_nchw_to_nhwc4_f32): the stem's input as
+    its weight gradient's float4 operand."""
+    x = x.contiguous()
+    _require_gpu(x)
+    N, C, H, W = x.shape
+    y = torch.empty(N, H, W, 4, device=x.device, dtype=torch.float32)
+    _check(lib().bev_nchw_to_nhwc4_f32(_ptr(x), N, C, H, W, _ptr(y), _stream(x)), "bev_nchw_to_nhwc4_f32")
     return y
 
 

@@ -1837,10 +1837,53 @@ int bev_maxpool2d_nhwc_f32(const float *x, int N, int H, int W, int C, int k, in
     return last();
 }
 
+// 3-channel images (the stem's input, for its weight gradient): 4 pixels per thread, one float4 from each plane in,
+// three float4 of interleaved channels out (the 32 x 32 tiles of k_transpose would use 3 of their 32 rows)
+__global__ __launch_bounds__(256) void k_nchw3_to_nhwc(const float4 *__restrict__ x, int64_t S4, int64_t total,
+                                                       float4 *__restrict__ y) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= total) return;
+    const int64_t n = t / S4, q = t - n * S4;
+    const float4 *xn = x + n * 3 * S4 + q;
+    const float4 a = xn[0], b = xn[S4], c = xn[2 * S4];
+    float4 *yp = y + t * 3;
+    yp[0] = make_float4(a.x, b.x, c.x, a.y);
+    yp[1] = make_float4(b.y, c.y, a.z, b.z);
+    yp[2] = make_float4(c.z, a.w, b.w, c.w);
+}
+
+// C <= 4 channels to 4-channel pixels (zero padding): one float4 per pixel -- the stem's input as the float4 operand
+// of its weight gradient, without a separate zero-pad copy
+__global__ __launch_bounds__(256) void k_nchw_to_nhwc4(const float *__restrict__ x, int C, int64_t S, int64_t total,
+                                                       float4 *__restrict__ y) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= total) return;
+    const int64_t n = t / S, q = t - n * S;
+    const float *xn = x + n * C * S + q;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < C; ++c) v[c] = xn[c * S];
+    y[t] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+int bev_nchw_to_nhwc4_f32(const float *x, int N, int C, int H, int W, float *y, void *stream) {
+    if (!x || !y || N < 0 || C <= 0 || C > 4 || H <= 0 || W <= 0 || ((uintptr_t)y & 15) != 0) return BEV_ERR_ARGS;
+    const int64_t S = (int64_t)H * W, total = (int64_t)N * S;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_nchw_to_nhwc4, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, C,
+                       S, total, reinterpret_cast<float4 *>(y));
+    return last();
+}
+
 int bev_nchw_to_nhwc_f32(const float *x, int N, int C, int H, int W, float *y, void *stream) {
     if (!x || !y || N < 0 || C <= 0 || H <= 0 || W <= 0) return BEV_ERR_ARGS;
     if (N == 0) return 0;
     const int S = H * W;
+    if (C == 3 && S % 4 == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0) {
+        const int64_t total = (int64_t)N * (S / 4);
+        hipLaunchKernelGGL(k_nchw3_to_nhwc, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<const float4 *>(x), (int64_t)(S / 4), total, reinterpret_cast<float4 *>(y));
+        return last();
+    }
     hipLaunchKernelGGL(k_transpose, dim3((S + 31) / 32, (C + 31) / 32, N), dim3(32, 8), 0, (hipStream_t)stream, x, C,
                        S, y);
     return last();

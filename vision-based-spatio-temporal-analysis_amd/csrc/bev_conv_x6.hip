@@ -998,9 +998,13 @@ struct StemX6Args {
     const float *__restrict__ x;
     const __bf16 *__restrict__ wp;
     const float *__restrict__ bias;
-    float *__restrict__ y;
+    float *__restrict__ y;  // the stem output [N, Ho, Wo, Co], or (POOL) the max-pooled one [N, Hp, Wp, 64]
     int H, W, Co, Ho, Wo, relu, nTx, nTy;
     int64_t ntiles;
+    // POOL only: per tile, the horizontally pooled last stem row (the next tile row's pooled row 0 needs it:
+    // [ntiles][32][64]) and the last stem column's vertical window maxima for pooled rows 0..4 ([ntiles][5][64])
+    float *__restrict__ edge_b, *__restrict__ edge_r;
+    int Hp, Wp;
 };
 
 __device__ __forceinline__ void stem6_fetch(const StemX6Args &a, int64_t t, int tid, float (&pv)[stem6::PER_T]) {
@@ -1044,6 +1048,21 @@ __device__ __forceinline__ void stem6_put(float *pl, int tid, const float (&pv)[
     }
 }
 
+// the pooled maximum of relu'd stem values (>= +0, never NaN: the ReLU maps NaN to 0)
+__device__ __forceinline__ float pool_mx(float m, float v) { return __builtin_fmaxf(m, v); }
+
+// POOL: timm's stem max-pool (3x3 / s2 / p1, cnn_encoder.py:26 features_only) fused into the epilogue.  The stem
+// output is relu'd (>= +0), so a window's padding and the tile's rows / columns past the image may count as +0 without
+// changing any maximum: every pooled value is the max over a set of non-negative values, whatever the grouping --
+// bit-identical to k_maxpool_rows over the stem output.  Tile (ty, tx) = stem rows 8ty..8ty+7 x columns
+// 64tx..64tx+63 owns pooled rows 4ty..4ty+3 x columns 32tx..32tx+31; pooled row 4ty needs stem row 8ty-1 (tile ty-1)
+// and pooled column 32tx stem column 64tx-1 (tile tx-1): each tile stores its own part of those seam outputs and
+// exports its last row / column parts (edge_b / edge_r), which k_stem_pool_seams folds in afterwards.
+// Lane (h, r32) holds channel r32 (+32) of stem columns 32mt + 8b + 4h + u (u = 0..3): pooled columns 16mt + 4b + 2h
+// (+1) are 3-maxima of its own values and, for the even one, the other half-wave's u = 3 value of the preceding
+// group (a cross-half shuffle); wave w = stem row w: the odd waves hand their 34 row maxima to the even ones through
+// LDS, the even wave 2p combines rows 2p-1..2p+1 into pooled row p.
+template <bool POOL>
 __global__ __launch_bounds__(stem6::NTHR, 1) void k_stem_x6(StemX6Args a) {
     using namespace stem6;
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[WB * 2 + PATCH * (STEM6_PRESPLIT ? 6 : 4)];
@@ -1116,7 +1135,118 @@ __global__ __launch_bounds__(stem6::NTHR, 1) void k_stem_x6(StemX6Args a) {
             __builtin_amdgcn_sched_barrier(0);  // one slice of operands live at a time
         }
         // epilogue: D[row][col], col = channel r32 (+32), row = pixel (r & 3) + 8 (r >> 2) + 4 h (+32)
-        {
+        if constexpr (POOL) {
+            const int tx = (int)(t % a.nTx);
+            const int64_t r_ = t / a.nTx;
+            const int ty = (int)(r_ % a.nTy);
+            const int64_t img = r_ / a.nTy;
+            const int oy = ty * TH + wave;
+            const int oxb = tx * TW;
+            float hp[2][4][2][2];  // [mt][b][pc][j]: pooled column 16 mt + 4 b + 2 h + pc, channel r32 + 32 j
+            float pa3[2][2][4];    // the other half-wave's u = 3 value of group (mt, b)
+            float c63[2];          // stem column 63 (lanes h = 1)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        float v[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int ox = oxb + 32 * mt + 8 * b + 4 * h + u;
+                            const float z = acc[mt][j][4 * b + u] + (j ? b1 : b0);
+                            v[u] = oy < a.Ho && ox < a.Wo && z > 0.0f ? z : 0.0f;  // the stem's ReLU (NaN -> 0)
+                        }
+                        pa3[mt][j][b] = __shfl_xor(v[3], 32);
+                        hp[mt][b][1][j] = pool_mx(pool_mx(v[1], v[2]), v[3]);
+                        hp[mt][b][0][j] = pool_mx(v[0], v[1]);
+                        if (mt == 1 && b == 3) c63[j] = v[3];
+                    }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const float prev0 = b > 0 ? pa3[mt][j][b - 1] : (mt > 0 ? pa3[mt - 1][j][3] : 0.0f);
+                        hp[mt][b][0][j] = pool_mx(hp[mt][b][0][j], h ? pa3[mt][j][b] : prev0);
+                    }
+            __syncthreads();  // every wave is done reading the patch: its LDS holds the row exchange
+            float *xl = pl;   // [odd wave][34][64 lanes]
+            if (wave & 1) {
+                float *o = xl + (wave >> 1) * 34 * 64 + lane;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+#pragma unroll
+                        for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j) o[(((mt * 4 + b) * 2 + pc) * 2 + j) * 64] = hp[mt][b][pc][j];
+                o[32 * 64] = c63[0];
+                o[33 * 64] = c63[1];
+            }
+            __syncthreads();
+            const int64_t tile = t;
+            if (wave == TH - 1) {  // the last row: next tile row's pooled row 0, and column 63 alone (pooled row 4)
+                float *eb = a.edge_b + tile * (32 * 64);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+#pragma unroll
+                        for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j)
+                                eb[(16 * mt + 4 * b + 2 * h + pc) * 64 + r32 + 32 * j] = hp[mt][b][pc][j];
+                if (h) {
+                    a.edge_r[(tile * 5 + 4) * 64 + r32] = c63[0];
+                    a.edge_r[(tile * 5 + 4) * 64 + 32 + r32] = c63[1];
+                }
+            } else if (!(wave & 1)) {
+                const int p = wave >> 1;
+                const float *up = xl + (p - 1) * 34 * 64 + lane, *dn = xl + p * 34 * 64 + lane;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b)
+#pragma unroll
+                        for (int pc = 0; pc < 2; ++pc)
+#pragma unroll
+                            for (int j = 0; j < 2; ++j) {
+                                const int e = (((mt * 4 + b) * 2 + pc) * 2 + j) * 64;
+                                float m = pool_mx(hp[mt][b][pc][j], dn[e]);
+                                if (p > 0) m = pool_mx(m, up[e]);
+                                hp[mt][b][pc][j] = m;
+                            }
+                float e0 = pool_mx(c63[0], dn[32 * 64]), e1 = pool_mx(c63[1], dn[33 * 64]);
+                if (p > 0) {
+                    e0 = pool_mx(e0, up[32 * 64]);
+                    e1 = pool_mx(e1, up[33 * 64]);
+                }
+                if (h) {
+                    a.edge_r[(tile * 5 + p) * 64 + r32] = e0;
+                    a.edge_r[(tile * 5 + p) * 64 + 32 + r32] = e1;
+                }
+                const int prow = ty * (TH / 2) + p;
+                if (prow < a.Hp) {
+                    float *yr = a.y + ((img * a.Hp + prow) * (int64_t)a.Wp) * 64;
+#pragma unroll
+                    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+#pragma unroll
+                            for (int pc = 0; pc < 2; ++pc) {
+                                const int Q = tx * (TW / 2) + 16 * mt + 4 * b + 2 * h + pc;
+                                if (Q < a.Wp) {
+                                    yr[(int64_t)Q * 64 + r32] = hp[mt][b][pc][0];
+                                    yr[(int64_t)Q * 64 + 32 + r32] = hp[mt][b][pc][1];
+                                }
+                            }
+                }
+            }
+        } else {
             const int tx = (int)(t % a.nTx);
             const int64_t r_ = t / a.nTx;
             const int ty = (int)(r_ % a.nTy);
@@ -1147,6 +1277,37 @@ __global__ __launch_bounds__(stem6::NTHR, 1) void k_stem_x6(StemX6Args a) {
         stem6_put(pl, tid, pv);
         __syncthreads();
     }
+}
+
+// The seam outputs of the fused stem max-pool: pooled row 4ty of tile (ty, tx) takes edge_b of tile (ty-1, tx),
+// pooled column 32tx edge_r of tile (ty, tx-1), their corner edge_r row 4 of tile (ty-1, tx-1).  One thread per
+// (tile, seam output, 4 channels): 35 seam outputs (32 columns of row 0, rows 1..3 of column 0) x 16 float4.
+__global__ __launch_bounds__(256) void k_stem_pool_seams(float *__restrict__ y, const float *__restrict__ edge_b,
+                                                         const float *__restrict__ edge_r, int nTx, int nTy,
+                                                         int64_t ntiles, int Hp, int Wp) {
+    const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t tile = g / (35 * 16);
+    if (tile >= ntiles) return;
+    const int k = (int)(g - tile * (35 * 16)), s = k >> 4, c4 = k & 15;
+    const int tx = (int)(tile % nTx);
+    const int64_t r_ = tile / nTx;
+    const int ty = (int)(r_ % nTy);
+    const int64_t img = r_ / nTy;
+    const int p = s < 32 ? 0 : s - 31, q = s < 32 ? s : 0;
+    const int P = ty * (stem6::TH / 2) + p, Q = tx * (stem6::TW / 2) + q;
+    if (P >= Hp || Q >= Wp || (p == 0 && ty == 0 && (q > 0 || tx == 0))) return;  // no seam contribution
+    float4 *yp = reinterpret_cast<float4 *>(y + (((img * Hp + P) * (int64_t)Wp + Q) * 64)) + c4;
+    float4 m = *yp;
+    auto mx = [](float4 a, float4 b) {
+        return make_float4(pool_mx(a.x, b.x), pool_mx(a.y, b.y), pool_mx(a.z, b.z), pool_mx(a.w, b.w));
+    };
+    if (p == 0 && ty > 0) m = mx(m, reinterpret_cast<const float4 *>(edge_b + ((tile - nTx) * 32 + q) * 64)[c4]);
+    if (q == 0 && tx > 0) {
+        m = mx(m, reinterpret_cast<const float4 *>(edge_r + ((tile - 1) * 5 + p) * 64)[c4]);
+        if (p == 0 && ty > 0)
+            m = mx(m, reinterpret_cast<const float4 *>(edge_r + ((tile - nTx - 1) * 5 + 4) * 64)[c4]);
+    }
+    *yp = m;
 }
 
 }  // namespace
@@ -1348,8 +1509,54 @@ int bev_conv2d_stem_x6_f32(const float *x, int N, int H, int W, const uint16_t *
     a.nTx = (Wo + stem6::TW - 1) / stem6::TW;
     a.nTy = (Ho + stem6::TH - 1) / stem6::TH;
     a.ntiles = (int64_t)N * a.nTx * a.nTy;
+    a.edge_b = a.edge_r = nullptr;
+    a.Hp = a.Wp = 0;
     const int64_t grid = a.ntiles < num_cu ? a.ntiles : num_cu;
-    hipLaunchKernelGGL(k_stem_x6, dim3((unsigned)grid), dim3(stem6::NTHR), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(k_stem_x6<false>, dim3((unsigned)grid), dim3(stem6::NTHR), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+}
+
+int64_t bev_conv2d_stem_pool_x6_workspace(int N, int H, int W) {
+    if (N <= 0 || H <= 0 || W <= 0) return BEV_ERR_ARGS;
+    const int Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+    const int64_t nt = (int64_t)N * ((Wo + stem6::TW - 1) / stem6::TW) * ((Ho + stem6::TH - 1) / stem6::TH);
+    return nt * (32 + 5) * 64 * (int64_t)sizeof(float);
+}
+
+int bev_conv2d_stem_pool_x6_f32(const float *x, int N, int H, int W, const uint16_t *packed, const float *bias,
+                                int Co, float *y, int Hp, int Wp, void *workspace, int64_t workspace_bytes,
+                                void *stream) {
+    const int Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+    if (!x || !packed || !bias || !y || !workspace || N <= 0 || H <= 0 || W <= 0 || Co != 64 ||
+        Hp != (Ho + 2 - 3) / 2 + 1 || Wp != (Wo + 2 - 3) / 2 + 1 || (((uintptr_t)packed | (uintptr_t)y |
+                                                                       (uintptr_t)workspace) & 15) != 0)
+        return BEV_ERR_ARGS;
+    if (workspace_bytes < bev_conv2d_stem_pool_x6_workspace(N, H, W)) return BEV_ERR_ARGS;
+    static int num_cu = 0;
+    if (num_cu == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        num_cu = n;
+    }
+    StemX6Args a;
+    a.x = x;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.y = y;
+    a.H = H, a.W = W, a.Co = Co, a.Ho = Ho, a.Wo = Wo, a.relu = 1;
+    a.nTx = (Wo + stem6::TW - 1) / stem6::TW;
+    a.nTy = (Ho + stem6::TH - 1) / stem6::TH;
+    a.ntiles = (int64_t)N * a.nTx * a.nTy;
+    a.edge_b = (float *)workspace;
+    a.edge_r = a.edge_b + a.ntiles * 32 * 64;
+    a.Hp = Hp, a.Wp = Wp;
+    const int64_t grid = a.ntiles < num_cu ? a.ntiles : num_cu;
+    hipLaunchKernelGGL(k_stem_x6<true>, dim3((unsigned)grid), dim3(stem6::NTHR), 0, (hipStream_t)stream, a);
+    const int64_t nthr = a.ntiles * 35 * 16;
+    hipLaunchKernelGGL(k_stem_pool_seams, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y,
+                       a.edge_b, a.edge_r, a.nTx, a.nTy, a.ntiles, Hp, Wp);
     return (int)hipGetLastError();
 }
 

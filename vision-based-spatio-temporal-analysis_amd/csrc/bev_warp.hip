@@ -1767,7 +1767,7 @@ int warp_tune(int knob, int value) {
 
 extern "C" {
 
-int bev_abi_version(void) { return 8; }
+int bev_abi_version(void) { return 9; }
 
 #if WARP_STAMP
 int bev_warp_stamp_read(unsigned long long *host, int n) {  // timing builds only

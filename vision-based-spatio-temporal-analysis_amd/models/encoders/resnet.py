@@ -77,6 +77,9 @@ class Bottleneck(nn.Module):
 
 # The ResNet stem on the split arithmetic (FoldedConv.stem_x6); False keeps the exact-f32 stem kernel.
 STEM_X6 = True
+# ... and, in the eval chain, with the stem max-pool fused into its epilogue (bev_conv2d_stem_pool_x6_f32,
+# bit-identical; False: the stem output is written and max-pooled by its own launch)
+STEM_POOL = True
 
 
 class FoldedConv:
@@ -369,12 +372,19 @@ class ResNet(nn.Module):
         launch stage i (1 = stem, 2 = max-pool, 3.. = residual blocks)."""
         mark = mark or (lambda i: None)
         last_li = max(1, min(out_index, 4))
-        y = self._fc(self.conv1, self.bn1)(x, relu=True, in_nchw=True, out=out if out_index == 0 else None)
-        mark(1)
-        if out_index == 0:
-            return y
-        y = _nat.maxpool_nhwc(y, 3, 2, 1)
-        mark(2)
+        fc = self._fc(self.conv1, self.bn1)
+        if out_index > 0 and STEM_POOL and fc.stem_x6() and self.conv1.out_channels == 64:
+            fc.prepare(x.device, "bf16x6")
+            y = _nat.conv2d_stem_pool_x6(x, fc.packed6, fc.bias)  # stem + max-pool, one pass
+            mark(1)
+            mark(2)
+        else:
+            y = fc(x, relu=True, in_nchw=True, out=out if out_index == 0 else None)
+            mark(1)
+            if out_index == 0:
+                return y
+            y = _nat.maxpool_nhwc(y, 3, 2, 1)
+            mark(2)
         stage = 2
         layers = (self.layer1, self.layer2, self.layer3, self.layer4)
         for li, layer in enumerate(layers, start=1):

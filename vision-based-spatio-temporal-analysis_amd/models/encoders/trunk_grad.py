@@ -91,6 +91,12 @@ def _dgrad(dz: torch.Tensor, wf: torch.Tensor, H: int, W: int, stride: int, pad:
     return _nat.conv2d_nhwc(d, packed, zero, Ci, K, K, 1, 0, False)
 
 
+def _stem_operand(x: torch.Tensor) -> torch.Tensor:
+    """The NCHW input of an in_nchw conv (the stem) as the NHWC operand of its weight gradient: 3-channel images
+    straight to 4-channel pixels with a zero channel (the float4 kernel's operand; no separate pad copy)."""
+    return _nat.nchw_to_nhwc4(x) if x.shape[1] <= 4 else _nat.nchw_to_nhwc(x)
+
+
 class ConvBNAct(torch.autograd.Function):
     @staticmethod
     @_nat.amp_fwd
@@ -122,11 +128,13 @@ class ConvBNAct(torch.autograd.Function):
         res_in = None
         if sink_in is not None:
             res_in, sink_in.grad = sink_in.grad, None
-        xn = _nat.nchw_to_nhwc(x) if in_nchw else x
+        xn = _stem_operand(x) if in_nchw else x
         H, W = xn.shape[1], xn.shape[2]
         dx = _dgrad(dz, wf, H, W, st, p, residual=res_in) if (ctx.needs_input_grad[0] and not in_nchw) else (
             res_in if ctx.needs_input_grad[0] else None)
         dwf = _nat.conv_wgrad(xn, dz, k, k, st, p)
+        if dwf.shape[1] != wf.shape[1]:  # the zero channel of the 4-channel stem operand
+            dwf = dwf[:, :wf.shape[1]].contiguous()
         dbf = _nat.colsum(dz)
         dw = dwf * s.view(-1, 1, 1, 1)
         ds = (dwf * weight.detach().float()).sum((1, 2, 3)) - bn.running_mean.detach().float() * dbf
@@ -201,11 +209,13 @@ class ConvBNTrain(torch.autograd.Function):
         res_in = None
         if sink_in is not None:
             res_in, sink_in.grad = sink_in.grad, None
-        xn = _nat.nchw_to_nhwc(x) if in_nchw else x
+        xn = _stem_operand(x) if in_nchw else x
         H, W = xn.shape[1], xn.shape[2]
         dx = _dgrad(dz, w, H, W, st, p, residual=res_in) if (ctx.needs_input_grad[0] and not in_nchw) else (
             res_in if ctx.needs_input_grad[0] else None)
         dw = _nat.conv_wgrad(xn, dz, k, k, st, p)
+        if dw.shape[1] != w.shape[1]:  # the zero channel of the 4-channel stem operand
+            dw = dw[:, :w.shape[1]].contiguous()
         return dx, dw, dgamma, dbeta, None, None, None, None, dres, None, None
 
 
