@@ -380,6 +380,15 @@ int bev_maxpool2d_bwd_nhwc_f32(const float *x, const float *dy, int N, int H, in
 int bev_maxpool2d_bwd_ws_nhwc_f32(const float *x, const float *dy, int N, int H, int W, int C, int k, int stride,
                                   int pad, int Ho, int Wo, float *dx, uint8_t *argmax, void *stream);
 
+/* Training form of the same pair, split at the forward: the pooled y [N][Ho][Wo][C] (bev_maxpool2d_nhwc_f32's
+ * values) together with the window argmax bytes, so the backward needs neither x nor the argmax pass; the backward
+ * gathers exactly as bev_maxpool2d_bwd_ws_nhwc_f32 does (bit-identical dx).  C % 4 == 0, k * k <= 255, x / y / dy /
+ * dx 16-B aligned, argmax 4-B aligned. */
+int bev_maxpool2d_fwd_arg_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y,
+                                   uint8_t *argmax, int Ho, int Wo, void *stream);
+int bev_maxpool2d_bwd_arg_nhwc_f32(const uint8_t *argmax, const float *dy, int N, int H, int W, int C, int k,
+                                   int stride, int pad, int Ho, int Wo, float *dx, void *stream);
+
 /* ---------------------------------------------------------------------------
  * Mixed precision (train.py:238-247, configs/wildtrack.yaml:45 USE_AMP): the convolutions a training step
  * runs under torch.autocast(float16) -- fp16 operands (round to nearest even, as autocast's casts), fp32
@@ -671,6 +680,13 @@ int bev_image_normalize_u8_f32(const uint8_t *src, int N, int H, int W, const fl
 int bev_head_operand_f32(const float *s, const float *bias, const float *pos, int B, int P, int Hb, int Wb, int cp,
                          float *x, void *stream);
 int bev_head_operand_bwd_f32(const float *gx, int B, int P, int Hb, int Wb, int cp, float *gs, void *stream);
+/* The same backward with the BEV projection bias's gradient (the sum of gx[..., :P] over every cell: torch's
+ * reduction of the broadcast add's gradient, model_wrapper.py:69-75) from the same pass: per-block fp32 partials
+ * (`partials`, bev_head_operand_bwd_bias_partials(B, P, Hb, Wb) floats) added in double into gbias [P].  Needs the
+ * 16-B form (Wb % 4 == 0, cp % 4 == 0, 16-B aligned gx / gs). */
+int64_t bev_head_operand_bwd_bias_partials(int B, int P, int Hb, int Wb);
+int bev_head_operand_bwd_bias_f32(const float *gx, int B, int P, int Hb, int Wb, int cp, float *gs, float *gbias,
+                                  float *partials, void *stream);
 
 #ifdef __cplusplus
 }

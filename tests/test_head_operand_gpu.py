@@ -40,3 +40,13 @@ def test_head_operand_matches_torch(B, P, Hb, Wb, cp):
     gs = nat.head_operand_bwd(gx, P)
     torch.cuda.synchronize()
     assert torch.equal(gs, gx[..., :P].permute(0, 3, 1, 2).contiguous())
+    gs2, gb = nat.head_operand_bwd_bias(gx, P)  # with the bias gradient from the same pass (16-B form) or None
+    torch.cuda.synchronize()
+    assert torch.equal(gs2, gs)
+    if Wb % 4 == 0 and cp % 4 == 0:
+        ref = gx[..., :P].double().sum((0, 1, 2))
+        assert gb is not None and gb.shape == (P,)
+        # block partials in fp32 (64 cells each) added in double: within a few fp32 ulps of the exact sum
+        assert float((gb.double() - ref).abs().max()) <= 1e-6 * float(gx[..., :P].abs().sum((0, 1, 2)).max())
+    else:
+        assert gb is None

@@ -383,6 +383,34 @@ def test_maxpool_bwd_two_pass_bit_identical(N, C, H, W):
                                                 nat._ptr(one), nat._stream(xd)) == 0
     two = nat.maxpool_bwd_nhwc(xd, dyd, 3, 2, 1)
     assert torch.equal(one.view(torch.int32), two.view(torch.int32))
+    # the training form: argmax bytes kept by the forward pool (whose values equal maxpool_nhwc's), the row-grid gather
+    y, arg = nat.maxpool_fwd_arg_nhwc(xd, 3, 2, 1)
+    assert torch.equal(y.view(torch.int32), nat.maxpool_nhwc(xd, 3, 2, 1).view(torch.int32))
+    three = nat.maxpool_bwd_arg_nhwc(arg, dyd, H, W, 3, 2, 1)
+    assert torch.equal(one.view(torch.int32), three.view(torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,s,p", [(2, 3, 0), (3, 1, 1), (3, 2, 0), (5, 2, 2)])
+def test_maxpool_argmax_training_form_other_windows(k, s, p):
+    """The training max-pool pair (forward argmax bytes, then the gather) == the single-pass x-based backward for
+    windows the stem pool does not use: uncovered inputs (s > k), 3 windows per axis (the looped gather), no padding,
+    5 x 5."""
+    import bev_native as nat
+    g = torch.Generator().manual_seed(k * 10 + s)
+    N, C, H, W = 2, 8, 13, 11
+    x = torch.randint(-2, 3, (N, H, W, C), generator=g).float()
+    x.view(-1)[::53] = float("nan")
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, Ho, Wo, C, generator=g)
+    xd, dyd = x.to(DEV), dy.to(DEV)
+    one = torch.empty_like(xd)
+    assert nat.lib().bev_maxpool2d_bwd_nhwc_f32(nat._ptr(xd), nat._ptr(dyd), N, H, W, C, k, s, p, Ho, Wo,
+                                                nat._ptr(one), nat._stream(xd)) == 0
+    y, arg = nat.maxpool_fwd_arg_nhwc(xd, k, s, p)
+    assert torch.equal(y.view(torch.int32), nat.maxpool_nhwc(xd, k, s, p).view(torch.int32))
+    two = nat.maxpool_bwd_arg_nhwc(arg, dyd, H, W, k, s, p)
+    assert torch.equal(one.view(torch.int32), two.view(torch.int32))
 
 
 BN_CASES = [(2, 64, 13, 17, 1, True, False), (1, 384, 9, 11, 1, False, False), (3, 24, 7, 5, 0, False, False),

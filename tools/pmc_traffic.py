@@ -42,7 +42,7 @@ def main():
             tot[(fam, cnt)] += float(r["Counter_Value"]) * 1024.0
             if cnt == "FETCH_SIZE":
                 n[fam] += 1
-                steps += "k_stem" in r["Kernel_Name"]
+                steps += "k_stem" in r["Kernel_Name"] and "seams" not in r["Kernel_Name"]  # one stem per group
     res = {}
     steps //= groups
     for fam, per in (("conv", steps), ("warp", n["warp"])):

@@ -35,12 +35,17 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V", help="bev_tune knob (A/B); repeatable")
     ap.add_argument("--no-mask-bytes", action="store_true", help="A/B: bn3's backward re-reads the fp32 block output "
                     "instead of the forward's ReLU mask bytes (trunk_grad.RELU_MASK_BYTES)")
+    ap.add_argument("--no-pool-arg", action="store_true", help="A/B: the stem max-pool saves its input and the backward "
+                    "re-scans it for the argmax instead of taking the forward's argmax bytes (trunk_grad.MAXPOOL_ARG)")
     a = ap.parse_args()
     import bev_native
     bev_native.AMP_HALF_CONVS = not a.fp32_kernels
     if a.no_mask_bytes:
         from models.encoders import trunk_grad
         trunk_grad.RELU_MASK_BYTES = False
+    if a.no_pool_arg:
+        from models.encoders import trunk_grad
+        trunk_grad.MAXPOOL_ARG = False
     for kv in a.tune:
         name, v = kv.split("=")
         bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))

@@ -54,6 +54,8 @@ SIGNATURES = {
     "bev_ipm_warp_fuse_boxes_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _vp, _i64, _vp]),
     "bev_head_operand_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_head_operand_bwd_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    "bev_head_operand_bwd_bias_partials": (_i64, [_i, _i, _i, _i]),
+    "bev_head_operand_bwd_bias_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_ipm_warp_fuse_chunked_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
                                            _i, _i, _i, _vp, _vp, _i64, _i, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
@@ -76,6 +78,8 @@ SIGNATURES = {
     "bev_colsum_f32": (_i, [_vp, _i64, _i, _vp, _vp]),
     "bev_maxpool2d_bwd_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_maxpool2d_bwd_ws_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "bev_maxpool2d_fwd_arg_nhwc_f32": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp]),
+    "bev_maxpool2d_bwd_arg_nhwc_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_conv2d_dual_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_conv2d_chain_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
                                   _i, _i, _vp]),
@@ -517,6 +521,27 @@ def head_operand_bwd(gx: torch.Tensor, P: int) -> torch.Tensor:
     return gs
 
 
+def head_operand_bwd_bias(gx: torch.Tensor, P: int):
+    """(gs, gbias): head_operand_bwd's gs and the BEV projection bias's gradient sum(gx[..., :P]) over (b, h, w) from
+    the same pass (bev_head_operand_bwd_bias_f32; block partials added in double), or None for gbias when the 16-B
+    form does not apply (the caller reduces gs itself)."""
+    _require_gpu(gx)
+    gx = gx.contiguous()
+    B, Hb, Wb, cp = gx.shape
+    gs = torch.empty(B, P, Hb, Wb, device=gx.device, dtype=torch.float32)
+    if Wb % 4 != 0 or cp % 4 != 0 or gx.data_ptr() % 16 != 0 or B * Hb * Wb == 0:
+        _check(lib().bev_head_operand_bwd_f32(_ptr(gx), B, P, Hb, Wb, cp, _ptr(gs), _stream(gx)),
+               "bev_head_operand_bwd_f32")
+        return gs, None
+    n = int(lib().bev_head_operand_bwd_bias_partials(B, P, Hb, Wb))
+    _check(min(n, 0), "bev_head_operand_bwd_bias_partials")
+    part = torch.empty(n, device=gx.device, dtype=torch.float32)
+    gb = torch.empty(P, device=gx.device, dtype=torch.float32)
+    _check(lib().bev_head_operand_bwd_bias_f32(_ptr(gx), B, P, Hb, Wb, cp, _ptr(gs), _ptr(gb), _ptr(part),
+                                               _stream(gx)), "bev_head_operand_bwd_bias_f32")
+    return gs, gb
+
+
 def taps(H, xs, ys, Hf, Wf, img_hw):
     _require_gpu(H, xs, ys)
     N = H.shape[0]
@@ -819,9 +844,11 @@ def _require_gpu_h(*ts):
 
 
 def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: int, stride: int, pad: int,
-                   stats: bool = False, residual: torch.Tensor = None, bias: torch.Tensor = None, dilation: int = 1):
+                   stats: bool = False, residual: torch.Tensor = None, bias: torch.Tensor = None, dilation: int = 1,
+                   out: torch.Tensor = None):
     """The autocast fp16 conv with x [N,H,W,Ci] stored in fp32 or fp16 (Ci % 64 == 0 for fp16) -> z fp32
-    [N,Ho,Wo,Co] (+ residual), and with `stats` the BatchNorm tile partials (conv2d_nhwc_h16_bnstats)."""
+    [N,Ho,Wo,Co] (+ residual), and with `stats` the BatchNorm tile partials (conv2d_nhwc_h16_bnstats).  `out`: a
+    wider NHWC fp32 buffer [N,Ho,Wo,>=Co] whose first Co channels receive z (the rest are left as they are)."""
     x = x.contiguous()
     _require_gpu_h(x)
     _require_gpu(residual, bias)
@@ -830,7 +857,12 @@ def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: 
     N, H, W, Ci = x.shape
     Ho = (H + 2 * pad - dilation * (KH - 1) - 1) // stride + 1
     Wo = (W + 2 * pad - dilation * (KW - 1) - 1) // stride + 1
-    z = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    if out is not None:
+        assert (out.shape[:3] == (N, Ho, Wo) and out.shape[3] >= Co and out.is_contiguous() and out.is_cuda
+                and out.dtype == torch.float32 and residual is None and not stats)
+        z = out
+    else:
+        z = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
     tiles = None
     if stats:
         nt = lib().bev_conv_h16_stat_tiles(N * Ho * Wo)
@@ -840,8 +872,8 @@ def conv2d_h16_any(x: torch.Tensor, packed: torch.Tensor, Co: int, KH: int, KW: 
         residual = residual.contiguous()
     with _span("conv", x):
         rc = lib().bev_conv2d_h16_ex_f32(_ptr(x), int(x.dtype == torch.float16), N, H, W, Ci, _ptr(packed),
-                                         _ptr(bias), _ptr(residual), Co, KH, KW, stride, pad, dilation, 0, _ptr(z), Co,
-                                         Ho, Wo, _ptr(tiles), _stream(x))
+                                         _ptr(bias), _ptr(residual), Co, KH, KW, stride, pad, dilation, 0, _ptr(z),
+                                         z.shape[3], Ho, Wo, _ptr(tiles), _stream(x))
     _check(rc, "bev_conv2d_h16_ex_f32")
     return (z, tiles) if stats else z
 
@@ -1214,6 +1246,35 @@ def colsum(dz: torch.Tensor) -> torch.Tensor:
     db = torch.empty(C, device=dz.device, dtype=torch.float32)
     _check(lib().bev_colsum_f32(_ptr(dz), dz.numel() // C, C, _ptr(db), _stream(dz)), "bev_colsum_f32")
     return db
+
+
+def maxpool_fwd_arg_nhwc(x: torch.Tensor, k: int, stride: int, pad: int):
+    """Training max-pool: (y [N,Ho,Wo,C], argmax uint8 [N,Ho,Wo,C]) -- maxpool_nhwc's values and the window argmax
+    bytes maxpool_bwd_arg_nhwc consumes (C % 4 == 0, k * k <= 255)."""
+    x = x.contiguous()
+    _require_gpu(x)
+    N, H, W, C = x.shape
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    y = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.float32)
+    arg = torch.empty(N, Ho, Wo, C, device=x.device, dtype=torch.uint8)
+    _check(lib().bev_maxpool2d_fwd_arg_nhwc_f32(_ptr(x), N, H, W, C, k, stride, pad, _ptr(y), _ptr(arg), Ho, Wo,
+                                                _stream(x)), "bev_maxpool2d_fwd_arg_nhwc_f32")
+    return y, arg
+
+
+def maxpool_bwd_arg_nhwc(arg: torch.Tensor, dy: torch.Tensor, H: int, W: int, k: int, stride: int,
+                         pad: int) -> torch.Tensor:
+    """dx [N,H,W,C] of the max-pool from its forward's argmax bytes (maxpool_fwd_arg_nhwc): bit-identical to
+    maxpool_bwd_nhwc."""
+    dy = dy.contiguous()
+    _require_gpu(dy)
+    if not arg.is_cuda or arg.dtype != torch.uint8 or arg.shape != dy.shape:
+        raise HipError("maxpool_bwd_arg_nhwc needs the forward's uint8 argmax of dy's shape")
+    N, Ho, Wo, C = dy.shape
+    dx = torch.empty(N, H, W, C, device=dy.device, dtype=torch.float32)
+    _check(lib().bev_maxpool2d_bwd_arg_nhwc_f32(_ptr(arg), _ptr(dy), N, H, W, C, k, stride, pad, Ho, Wo, _ptr(dx),
+                                                _stream(dy)), "bev_maxpool2d_bwd_arg_nhwc_f32")
+    return dx
 
 
 def maxpool_bwd_nhwc(x: torch.Tensor, dy: torch.Tensor, k: int, stride: int, pad: int) -> torch.Tensor:

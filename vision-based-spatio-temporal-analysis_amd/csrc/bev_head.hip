@@ -410,8 +410,12 @@ __global__ __launch_bounds__(HO_T) void k_head_operand_v4(const float *__restric
     }
 }
 
+// BIAS: also the block's per-channel sums of its nw cells (fp32, in cell order) into bpart[block][P], which
+// k_head_bias_fin adds in double -- the BEV projection bias's gradient without a separate pass over gs
+template <bool BIAS = false>
 __global__ __launch_bounds__(HO_T) void k_head_operand_bwd_v4(const float *__restrict__ gx, int P, int Hb, int Wb,
-                                                              int cp, float *__restrict__ gs) {
+                                                              int cp, float *__restrict__ gs,
+                                                              float *__restrict__ bpart = nullptr) {
     extern __shared__ float tile[];  // [HO_RUN][P + 1]
     const int w0 = blockIdx.x * HO_RUN, h = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
     const int nw = min(HO_RUN, Wb - w0), nq = nw / 4, cq = cp / 4, pq = (P + 3) / 4;
@@ -434,6 +438,30 @@ __global__ __launch_bounds__(HO_T) void k_head_operand_bwd_v4(const float *__res
             *(float4 *)(gb + (size_t)c * plane + 4 * k4) = make_float4(t[0], t[P + 1], t[2 * (P + 1)], t[3 * (P + 1)]);
         }
     }
+    if constexpr (BIAS) {
+        const size_t blk = ((size_t)b * Hb + h) * gridDim.x + blockIdx.x;
+        for (int c = tid; c < P; c += HO_T) {
+            float acc = 0.0f;
+            for (int k = 0; k < nw; ++k) acc += tile[k * (P + 1) + c];
+            bpart[blk * P + c] = acc;
+        }
+    }
+}
+
+// gbias[c] = sum over the blocks' partials (double, fixed order: deterministic); one workgroup per channel
+__global__ __launch_bounds__(256) void k_head_bias_fin(const float *__restrict__ bpart, int64_t nblk, int P,
+                                                       float *__restrict__ gbias) {
+    __shared__ double red[256];
+    const int c = blockIdx.x, tid = threadIdx.x;
+    double acc = 0.0;
+    for (int64_t i = tid; i < nblk; i += 256) acc += (double)bpart[i * P + c];
+    red[tid] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    if (tid == 0) gbias[c] = (float)red[0];
 }
 
 }  // namespace
@@ -528,6 +556,26 @@ int bev_head_operand_f32(const float *s, const float *bias, const float *pos, in
     return (int)hipGetLastError();
 }
 
+int64_t bev_head_operand_bwd_bias_partials(int B, int P, int Hb, int Wb) {
+    if (B <= 0 || P <= 0 || Hb <= 0 || Wb <= 0) return BEV_ERR_ARGS;
+    return (int64_t)B * Hb * ((Wb + HO_RUN - 1) / HO_RUN) * P;
+}
+
+int bev_head_operand_bwd_bias_f32(const float *gx, int B, int P, int Hb, int Wb, int cp, float *gs, float *gbias,
+                                  float *partials, void *stream) {
+    if (!gx || !gs || !gbias || !partials || B <= 0 || P <= 0 || Hb <= 0 || Wb <= 0 || cp < P || B > 65535 ||
+        Hb > 65535 || P > 512)
+        return BEV_ERR_ARGS;
+    if (Wb % 4 != 0 || cp % 4 != 0 || (((uintptr_t)gx | (uintptr_t)gs) & 15) != 0) return BEV_ERR_ARGS;  // 16-B form
+    const size_t lds = (size_t)HO_RUN * (P + 1) * sizeof(float);
+    const dim3 grid((Wb + HO_RUN - 1) / HO_RUN, Hb, B);
+    hipLaunchKernelGGL(k_head_operand_bwd_v4<true>, grid, dim3(HO_T), lds, (hipStream_t)stream, gx, P, Hb, Wb, cp, gs,
+                       partials);
+    hipLaunchKernelGGL(k_head_bias_fin, dim3(P), dim3(256), 0, (hipStream_t)stream, partials,
+                       (int64_t)B * Hb * grid.x, P, gbias);
+    return (int)hipGetLastError();
+}
+
 int bev_head_operand_bwd_f32(const float *gx, int B, int P, int Hb, int Wb, int cp, float *gs, void *stream) {
     if (!gx || !gs || B < 0 || P <= 0 || Hb < 0 || Wb < 0 || cp < P || B > 65535 || Hb > 65535 || P > 512)
         return BEV_ERR_ARGS;
@@ -535,7 +583,8 @@ int bev_head_operand_bwd_f32(const float *gx, int B, int P, int Hb, int Wb, int 
     const size_t lds = (size_t)HO_RUN * (P + 1) * sizeof(float);
     const dim3 grid((Wb + HO_RUN - 1) / HO_RUN, Hb, B);
     if (Wb % 4 == 0 && cp % 4 == 0 && (((uintptr_t)gx | (uintptr_t)gs) & 15) == 0)
-        hipLaunchKernelGGL(k_head_operand_bwd_v4, grid, dim3(HO_T), lds, (hipStream_t)stream, gx, P, Hb, Wb, cp, gs);
+        hipLaunchKernelGGL(k_head_operand_bwd_v4<false>, grid, dim3(HO_T), lds, (hipStream_t)stream, gx, P, Hb, Wb, cp,
+                           gs, nullptr);
     else
         hipLaunchKernelGGL(k_head_operand_bwd, grid, dim3(HO_T), lds, (hipStream_t)stream, gx, P, Hb, Wb, cp, gs);
     return (int)hipGetLastError();

@@ -795,9 +795,143 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_idx_v4(const uchar4 *__rest
     }
 }
 
+// Training forward max-pool that also keeps the backward's window argmax bytes (C % 4 == 0): one float4 of channels
+// per thread on a (row piece, output row, image) grid with 32-bit indices; the pooled value by k_maxpool_rows' rule
+// and the winning tap by k_maxpool_argmax_v4's (the same comparisons: first valid tap, then v > best or v NaN), so
+// the backward's argmax pass over the input disappears.
+__global__ __launch_bounds__(256) void k_maxpool_fwd_arg_v4(const float4 *__restrict__ x, int H, int W, int CV, int k,
+                                                            int s, int p, float4 *__restrict__ y,
+                                                            uchar4 *__restrict__ arg, int Ho, int Wo) {
+    const int oy = blockIdx.y, n = blockIdx.z;
+    const int t = blockIdx.x * 256 + threadIdx.x;  // (ox, c4) within the output row
+    if (t >= Wo * CV) return;
+    const int ox = t / CV, c = t - ox * CV;
+    float best[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+    int bi[4] = {-1, -1, -1, -1};
+    const int iy0 = oy * s - p, ix0 = ox * s - p;
+    for (int ky = 0; ky < k; ++ky) {
+        const int iy = iy0 + ky;
+        if (iy < 0 || iy >= H) continue;
+        const float4 *row = x + ((size_t)n * H + iy) * (size_t)W * CV + c;
+        for (int kx = 0; kx < k; ++kx) {
+            const int ix = ix0 + kx;
+            if (ix < 0 || ix >= W) continue;
+            const float4 q = row[(size_t)ix * CV];
+            const float v[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (bi[u] < 0) bi[u] = ky * k + kx;
+                if (v[u] > best[u] || v[u] != v[u]) {
+                    best[u] = v[u];
+                    bi[u] = ky * k + kx;
+                }
+            }
+        }
+    }
+    const size_t o = ((size_t)n * Ho + oy) * (size_t)Wo * CV + t;
+    y[o] = make_float4(best[0], best[1], best[2], best[3]);
+    arg[o] = make_uchar4((unsigned char)bi[0], (unsigned char)bi[1], (unsigned char)bi[2], (unsigned char)bi[3]);
+}
+
+// k_maxpool_bwd_idx_v4 on an (input row piece, input row, image) grid with 32-bit indices; same windows in the
+// same (oy, ox) order: bit-identical.  W2 (windows per axis <= 2, e.g. 3x3 / 2): the up to 2 x 2 covering windows'
+// argmax bytes and dy are all loaded up front (dy unconditionally, from L2), so a thread waits for memory once
+// instead of twice per window (the looped form ran at ~2.3 TB/s, latency-bound).
+template <bool W2>
+__global__ __launch_bounds__(256) void k_maxpool_bwd_arg_v4(const uchar4 *__restrict__ arg,
+                                                            const float4 *__restrict__ dy, int H, int W, int CV, int k,
+                                                            int s, int p, int Ho, int Wo, float4 *__restrict__ dx) {
+    const int iy = blockIdx.y, n = blockIdx.z;
+    const int t = blockIdx.x * 256 + threadIdx.x;  // (ix, c4) within the input row
+    if (t >= W * CV) return;
+    const int ix = t / CV, c = t - ix * CV;
+    float g[4] = {0.f, 0.f, 0.f, 0.f};
+    const int oy_lo = max(0, (iy + p - k + s) / s), oy_hi = min(Ho - 1, (iy + p) / s);
+    const int ox_lo = max(0, (ix + p - k + s) / s), ox_hi = min(Wo - 1, (ix + p) / s);
+    if constexpr (W2) {
+        uchar4 a[2][2];
+        float4 d[2][2];
+        bool ok[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int oy = oy_lo + u, ox = ox_lo + v;
+                ok[u][v] = oy <= oy_hi && ox <= ox_hi;
+                const size_t o = ((size_t)n * Ho + (ok[u][v] ? oy : min(oy_lo, Ho - 1))) * (size_t)Wo * CV +
+                                 (size_t)(ok[u][v] ? ox : min(ox_lo, Wo - 1)) * CV + c;  // any in-range address
+                a[u][v] = arg[o];
+                d[u][v] = dy[o];
+            }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int me = (iy - ((oy_lo + u) * s - p)) * k + (ix - ((ox_lo + v) * s - p));
+                if (!ok[u][v]) continue;
+                if (a[u][v].x == me) g[0] += d[u][v].x;
+                if (a[u][v].y == me) g[1] += d[u][v].y;
+                if (a[u][v].z == me) g[2] += d[u][v].z;
+                if (a[u][v].w == me) g[3] += d[u][v].w;
+            }
+        dx[((size_t)n * H + iy) * (size_t)W * CV + t] = make_float4(g[0], g[1], g[2], g[3]);
+        return;
+    }
+    for (int oy = oy_lo; oy <= oy_hi; ++oy)
+        for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+            const int me = (iy - (oy * s - p)) * k + (ix - (ox * s - p));
+            const size_t o = ((size_t)n * Ho + oy) * (size_t)Wo * CV + (size_t)ox * CV + c;
+            const uchar4 a = arg[o];
+            const bool h0 = a.x == me, h1 = a.y == me, h2 = a.z == me, h3 = a.w == me;
+            if (h0 || h1 || h2 || h3) {
+                const float4 d = dy[o];
+                if (h0) g[0] += d.x;
+                if (h1) g[1] += d.y;
+                if (h2) g[2] += d.z;
+                if (h3) g[3] += d.w;
+            }
+        }
+    dx[((size_t)n * H + iy) * (size_t)W * CV + t] = make_float4(g[0], g[1], g[2], g[3]);
+}
+
 }  // namespace
 
 extern "C" {
+
+int bev_maxpool2d_fwd_arg_nhwc_f32(const float *x, int N, int H, int W, int C, int k, int stride, int pad, float *y,
+                                   uint8_t *argmax, int Ho, int Wo, void *stream) {
+    if (!x || !y || !argmax || N < 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || k <= 0 || k * k > 255 ||
+        stride <= 0 || pad < 0 || N >= 65536 || Ho >= 65536)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)y) & 15) != 0 || ((uintptr_t)argmax & 3) != 0) return BEV_ERR_ARGS;
+    if ((int64_t)Wo * (C / 4) >= (1ll << 30)) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    hipLaunchKernelGGL(k_maxpool_fwd_arg_v4, dim3((unsigned)(((int64_t)Wo * (C / 4) + 255) / 256), Ho, N), dim3(256), 0,
+                       (hipStream_t)stream, reinterpret_cast<const float4 *>(x), H, W, C / 4, k, stride, pad,
+                       reinterpret_cast<float4 *>(y), reinterpret_cast<uchar4 *>(argmax), Ho, Wo);
+    return last();
+}
+
+int bev_maxpool2d_bwd_arg_nhwc_f32(const uint8_t *argmax, const float *dy, int N, int H, int W, int C, int k,
+                                   int stride, int pad, int Ho, int Wo, float *dx, void *stream) {
+    if (!argmax || !dy || !dx || N < 0 || H <= 0 || W <= 0 || C <= 0 || C % 4 != 0 || k <= 0 || k * k > 255 ||
+        stride <= 0 || pad < 0 || N >= 65536 || H >= 65536)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - k) / stride + 1 || Wo != (W + 2 * pad - k) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    if ((((uintptr_t)dy | (uintptr_t)dx) & 15) != 0 || ((uintptr_t)argmax & 3) != 0) return BEV_ERR_ARGS;
+    if ((int64_t)W * (C / 4) >= (1ll << 30)) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    const bool w2 = (k + stride - 1) / stride <= 2;  // covering windows per axis
+    hipLaunchKernelGGL(w2 ? k_maxpool_bwd_arg_v4<true> : k_maxpool_bwd_arg_v4<false>,
+                       dim3((unsigned)(((int64_t)W * (C / 4) + 255) / 256), H, N), dim3(256), 0,
+                       (hipStream_t)stream, reinterpret_cast<const uchar4 *>(argmax),
+                       reinterpret_cast<const float4 *>(dy), H, W, C / 4, k, stride, pad, Ho, Wo,
+                       reinterpret_cast<float4 *>(dx));
+    return last();
+}
 
 int bev_relu_bwd_f32(const float *dy, const float *y, float *dz, int64_t n, void *stream) {
     if (!dy || !y || !dz || n < 0 || n % 4 != 0) return BEV_ERR_ARGS;

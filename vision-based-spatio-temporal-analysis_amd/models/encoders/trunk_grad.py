@@ -446,17 +446,35 @@ def conv_act(conv: nn.Conv2d, x, relu: bool, in_nchw: bool = False):
     return ConvAct.apply(x, conv.weight, conv.bias, conv.stride[0], conv.padding[0], relu, in_nchw)
 
 
+# MaxPool: the forward keeps the window argmax bytes for the backward (default), or saves x (A/B:
+# tools/train_step_bench.py --no-pool-arg; bit-identical results)
+MAXPOOL_ARG = True
+
+
 class MaxPool(torch.autograd.Function):
+    """Max-pool (timm's stem pool).  C % 4 == 0: the forward keeps the window argmax bytes (1 B per output instead
+    of the 4-B input per input element saved) and the backward gathers from them (bit-identical to the x-based
+    backward); else x is saved and the backward re-scans it."""
+
     @staticmethod
     @_nat.amp_fwd
     def forward(ctx, x, k: int, stride: int, pad: int):
+        ctx.meta = (k, stride, pad, x.shape[1], x.shape[2])
+        if MAXPOOL_ARG and x.shape[-1] % 4 == 0 and k * k <= 255:
+            y, arg = _nat.maxpool_fwd_arg_nhwc(x, k, stride, pad)
+            ctx.save_for_backward(arg)
+            ctx.arg = True
+            return y
         ctx.save_for_backward(x)
-        ctx.meta = (k, stride, pad)
+        ctx.arg = False
         return _nat.maxpool_nhwc(x, k, stride, pad)
 
     @staticmethod
     @_nat.amp_bwd
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
-        k, stride, pad = ctx.meta
-        return _nat.maxpool_bwd_nhwc(x, dy.contiguous().float(), k, stride, pad), None, None, None
+        (t,) = ctx.saved_tensors
+        k, stride, pad, H, W = ctx.meta
+        dy = dy.contiguous().float()
+        if ctx.arg:
+            return _nat.maxpool_bwd_arg_nhwc(t, dy, H, W, k, stride, pad), None, None, None
+        return _nat.maxpool_bwd_nhwc(t, dy, k, stride, pad), None, None, None

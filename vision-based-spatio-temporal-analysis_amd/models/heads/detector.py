@@ -152,6 +152,7 @@ class _HeadTrainH16(torch.autograd.Function):
         y = _nat.conv2d_h16_any(a, _nat.pack_conv_weight(w), w.shape[0], 3, 3, 1, 1, bias=bb)
         ctx.save_for_backward(*saved, a, w)
         ctx.meta = meta
+        ctx.grad_channels = min(head.grad_channels or head.in_channels, x.shape[-1])
         return y
 
     @staticmethod
@@ -175,9 +176,16 @@ class _HeadTrainH16(torch.autograd.Function):
             pad = dil * (K // 2)
             dz, dg, db = _nat.groupnorm_bwd_half(z, da, _GROUPS, mean, rstd, g, scale, shift, True)
             dw = _nat.conv_wgrad_h16_any(a, dz, K, K, 1, pad, dil)[:, :Ci]
-            if i > 0 or ctx.needs_input_grad[0]:
+            if i > 0:
                 wt = w.flip(2, 3).transpose(0, 1).contiguous()
                 da = _nat.conv2d_h16_any(dz, _nat.pack_conv_weight(wt), cpi, K, K, 1, pad, dilation=dil)
+            elif ctx.needs_input_grad[0]:
+                # the operand's gradient is read only in its first `gc` channels (the BEV features; the position
+                # encoding and the zero pad take none): the dgrad computes those alone, into a cp-wide buffer
+                gc = ctx.grad_channels
+                wt = w.flip(2, 3).transpose(0, 1)[:gc].contiguous()
+                da = torch.empty(dz.shape[0], dz.shape[1], dz.shape[2], cpi, device=dz.device, dtype=torch.float32)
+                _nat.conv2d_h16_any(dz, _nat.pack_conv_weight(wt), gc, K, K, 1, pad, dilation=dil, out=da)
             else:
                 da = None
             grads[i] = (dw, dg, db)
@@ -201,6 +209,10 @@ class BEVDetector(nn.Module):
             layers += [nn.Conv2d(cin, cout, kernel_size=3, padding=dil, dilation=dil, bias=False),
                        nn.GroupNorm(num_groups=_GROUPS, num_channels=cout), nn.ReLU(inplace=True)]
         self.stem = nn.Sequential(*layers)
+        # leading operand channels that need a gradient (BEVNet: the P BEV feature channels -- its position-encoding
+        # channels are a buffer); the AMP node's input gradient is computed for these alone, the rest of its
+        # channels are left unset (never read).  None: every input channel.
+        self.grad_channels = None
         self.heatmap_head = nn.Conv2d(128, 1, kernel_size=3, padding=1)
         self.offset_head = nn.Conv2d(128, 2, kernel_size=3, padding=1)
         self.size_head = nn.Conv2d(128, 2, kernel_size=3, padding=1)

@@ -54,8 +54,12 @@ class _HeadOperand(torch.autograd.Function):
     @staticmethod
     @_nat.amp_bwd
     def backward(ctx, gx):
-        gs = _nat.head_operand_bwd(gx, ctx.P)
-        gb = gs.sum((0, 2, 3)) if ctx.needs_input_grad[1] else None
+        if ctx.needs_input_grad[1]:  # the bias gradient from the same pass (block partials added in double)
+            gs, gb = _nat.head_operand_bwd_bias(gx, ctx.P)
+            if gb is None:
+                gb = gs.sum((0, 2, 3))
+        else:
+            gs, gb = _nat.head_operand_bwd(gx, ctx.P), None
         return gs, gb, None, None
 
 
@@ -198,6 +202,7 @@ class BEVNet(nn.Module):
         if self.detector is None:
             self.detector = BEVDetector(in_channels=P + 2, bev_bounds=self.bounds, bev_size=(self.bev_h, self.bev_w),
                                         default_box_wh=self.default_box_wh).to(main.device)
+        self.detector.grad_channels = P  # the position-encoding channels are a buffer: no gradient
         cp = self.detector.input_channels_padded
         if bias is not None and P <= 512 and main.is_cuda:
             x = _HeadOperand.apply(main, bias, self.pos_enc, cp)  # [B, Hb, Wb, cp] channels-last head operand
