@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V", help="bev_tune knob (A/B); repeatable")
     ap.add_argument("--no-mask-bytes", action="store_true", help="A/B: bn3's backward re-reads the fp32 block output "
                     "instead of the forward's ReLU mask bytes (trunk_grad.RELU_MASK_BYTES)")
+    ap.add_argument("--eager-decode", action="store_true", help="A/B: BEVNet.forward synchronises on its decode")
+    ap.add_argument("--device-targets", action="store_true", help="A/B: the targets already on the device (the "
+                    "reference's loop, train.py:228-243, leaves them in host memory)")
+    ap.add_argument("--no-loss-graph", action="store_true", help="A/B: BEVNet.loss launches its terms eagerly")
     ap.add_argument("--no-pool-arg", action="store_true", help="A/B: the stem max-pool saves its input and the backward "
                     "re-scans it for the argmax instead of taking the forward's argmax bytes (trunk_grad.MAXPOOL_ARG)")
     a = ap.parse_args()
@@ -46,6 +50,9 @@ def main():
     if a.no_pool_arg:
         from models.encoders import trunk_grad
         trunk_grad.MAXPOOL_ARG = False
+    import models.model_wrapper as _mw
+    _mw.LAZY_DECODE = not a.eager_decode
+    _mw.LOSS_GRAPHS = not a.no_loss_graph
     for kv in a.tune:
         name, v = kv.split("=")
         bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))
@@ -62,7 +69,10 @@ def main():
                "LOSS": {}, "EVAL": {"CONF_THRESH": 0.99}}
         model = BEVNet(cfg).to(dev)
         batch = {"images": images, "calib": {"intrinsic": Kd, "extrinsic": Rtd}}
-        targets = [{"boxes_world": torch.tensor([[1.0, 0.5, 0.6, 0.6], [-3.0, 2.0, 0.6, 0.6]], device=dev)}]
+        # the loader's targets stay in host memory, as in the reference's loop (train.py:228-243 moves only the
+        # images and the calibration)
+        targets = [{"boxes_world": torch.tensor([[1.0, 0.5, 0.6, 0.6], [-3.0, 2.0, 0.6, 0.6]],
+                                                device=dev if a.device_targets else "cpu")}]
         with torch.no_grad():
             model.eval()(batch)
         model.train()
@@ -116,6 +126,9 @@ def main():
                       "tune": a.tune, "bev": [480, 1440], "cameras": V, "img": [H, W], "feat_dim": 64,
                       "bev_proj_ch": a.proj_ch if a.bevnet else None,
                       "amp": a.amp, "half_convs": a.amp and not a.fp32_kernels,
+                      "decode": "eager" if a.eager_decode else "lazy",
+                      "loss_graph": not a.no_loss_graph,
+                      "targets": "device" if a.device_targets else "host",
                       "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
                       "loss": float(loss)}), flush=True)
 

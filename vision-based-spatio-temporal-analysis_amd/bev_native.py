@@ -8,6 +8,7 @@ kernels bind to -- one runtime, one set of streams.
 """
 from __future__ import annotations
 
+import collections.abc
 import contextlib
 import ctypes
 import functools
@@ -1296,12 +1297,45 @@ def maxpool_bwd_nhwc(x: torch.Tensor, dy: torch.Tensor, k: int, stride: int, pad
 # ---------------------------------------------------------------------------
 # decode (detector.py:64-125)
 # ---------------------------------------------------------------------------
+class _PendingDecode:
+    """A decode whose kernels are queued: the kept / candidate counts travel to pinned host memory behind an
+    event, and the host waits for them only when a result is first read (`get`)."""
+
+    def __init__(self, finish):
+        self._finish, self._val = finish, None
+
+    def get(self):
+        if self._val is None:
+            self._val, self._finish = self._finish(), None
+        return self._val
+
+
+class DetectionList(collections.abc.Sequence):
+    """Per-frame boxes (which 0) or scores (which 1) of a decode queued by decode(lazy=True): a read-only sequence
+    of device tensors, materialised -- one host synchronisation for the batch -- on first access.  A training step
+    that never reads the detections of its forward (train.py:238-243 reads only the loss) therefore never waits for
+    them, and the loss and backward launches queue behind the forward instead of after a drained GPU."""
+
+    def __init__(self, pending: _PendingDecode, which: int):
+        self._p, self._w = pending, which
+
+    def __getitem__(self, i):
+        return self._p.get()[self._w][i]
+
+    def __len__(self):
+        return len(self._p.get()[self._w])
+
+    def __repr__(self):
+        return repr(list(self))
+
+
 def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, bounds, conf_thresh: float,
-           nms_dist: float):
+           nms_dist: float, lazy: bool = False):
     """heatmap [B,1,H,W], offset / size [B,2,H,W] (device) -> (boxes list of [K,4], scores list of [K]).
     Like the reference there is no candidate limit: a frame with more candidates than the LDS sort holds
     (bev_decode_max_candidates) is finished by the global-memory sort + blocked NMS (bev_decode_nms_large_f32).
-    One host synchronisation per batch (two when some frame needs the large path)."""
+    One host synchronisation per batch (two when some frame needs the large path).  lazy: return two
+    DetectionList sequences instead; the synchronisation happens when one of them is first read."""
     heatmap, offset, size = heatmap.contiguous().float(), offset.contiguous().float(), size.contiguous().float()
     _require_gpu(heatmap, offset, size)
     B, _, H, W = heatmap.shape
@@ -1321,19 +1355,32 @@ def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, boun
     args = (float(x_min), float(y_min), float(res_x), float(res_y), float(nms_dist))
     _check(lib().bev_decode_nms_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, _ptr(offset), _ptr(size), H, W, *args,
                                     _ptr(boxes), _ptr(scores), _ptr(nk), st), "bev_decode_nms_f32")
-    kc = torch.stack([nk, cnt]).cpu()
-    kept, counts = kc[0].tolist(), kc[1].tolist()
-    if min(kept, default=0) < 0:
-        big = max(c for k, c in zip(kept, counts) if k < 0)
-        P = max(2 * DECODE_SORT_CHUNK, 1 << (big - 1).bit_length())
-        keys = torch.empty(B, P, device=dev, dtype=torch.int64)
-        _check(lib().bev_decode_nms_large_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, P, _ptr(offset), _ptr(size), H,
-                                              W, *args, _ptr(keys), _ptr(boxes), _ptr(scores), _ptr(nk), st),
-               "bev_decode_nms_large_f32")
-        kept = nk.cpu().tolist()
+    kc = torch.empty(2, B, dtype=torch.int32, pin_memory=True)
+    kc.copy_(torch.stack([nk, cnt]), non_blocking=True)
+    queued_on = torch.cuda.current_stream(dev)
+    ready = torch.cuda.Event()
+    ready.record(queued_on)
+
+    def finish():
+        ready.synchronize()
+        kept, counts = kc[0].tolist(), kc[1].tolist()
         if min(kept, default=0) < 0:
-            raise HipError("decode: large-candidate path left a frame unfinished")
-    return [boxes[b, :k] for b, k in enumerate(kept)], [scores[b, :k] for b, k in enumerate(kept)]
+            big = max(c for k, c in zip(kept, counts) if k < 0)
+            P = max(2 * DECODE_SORT_CHUNK, 1 << (big - 1).bit_length())
+            keys = torch.empty(B, P, device=dev, dtype=torch.int64)
+            with torch.cuda.stream(queued_on):  # the large path on the stream the decode was queued on
+                _check(lib().bev_decode_nms_large_f32(_ptr(idx), _ptr(sc), _ptr(cnt), B, cap, P, _ptr(offset),
+                                                      _ptr(size), H, W, *args, _ptr(keys), _ptr(boxes), _ptr(scores),
+                                                      _ptr(nk), st), "bev_decode_nms_large_f32")
+                kept = nk.cpu().tolist()
+            if min(kept, default=0) < 0:
+                raise HipError("decode: large-candidate path left a frame unfinished")
+        return [boxes[b, :k] for b, k in enumerate(kept)], [scores[b, :k] for b, k in enumerate(kept)]
+
+    if not lazy:
+        return finish()
+    pending = _PendingDecode(finish)
+    return DetectionList(pending, 0), DetectionList(pending, 1)
 
 
 DECODE_SORT_CHUNK = 8192  # keys per LDS chunk of the large-path sort (bev_decode.hip SORT_CHUNK)

@@ -297,11 +297,13 @@ class BEVDetector(nn.Module):
         peak = F.max_pool2d(x, kernel_size=kernel, stride=1, padding=kernel // 2)
         return x * (x == peak).float()
 
-    def decode(self, heatmap, offset, size_cells, conf_thresh: float = 0.4, nms_dist_m: float = 0.5):
+    def decode(self, heatmap, offset, size_cells, conf_thresh: float = 0.4, nms_dist_m: float = 0.5,
+               lazy: bool = False):
         """Peaks -> world boxes [cx, cy, w, h] + scores per frame (detector.py:71-125) on the device:
         bev_decode_peaks_f32 (3x3 peak test + threshold + compaction) and bev_decode_nms_f32 (sort by
-        score, box arithmetic, greedy centre-distance NMS).  One host sync per batch, not per pair."""
-        return _nat.decode(heatmap, offset, size_cells, self.bounds, conf_thresh, nms_dist_m)
+        score, box arithmetic, greedy centre-distance NMS).  One host sync per batch, not per pair; with `lazy`
+        the per-frame lists are bev_native.DetectionList sequences that take that sync when first read."""
+        return _nat.decode(heatmap, offset, size_cells, self.bounds, conf_thresh, nms_dist_m, lazy=lazy)
 
 
 class AnchorDetector(nn.Module):

@@ -21,7 +21,9 @@ The computation is reorganised for the GPU:
   splats are one scatter_reduce('amax') over every object's footprint.
 """
 import math
-from typing import Any, Dict, List, Tuple
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
 
 import torch
 import torch.nn as nn
@@ -36,6 +38,13 @@ from .heads.detector import BEVDetector, _ceil_to
 
 
 AMP_FWD_HALF_PANELS = True  # autocast: the projection's forward packs fp16 panels (its backward's arithmetic)
+
+
+# BEVNet.forward queues its decode and returns bev_native.DetectionList sequences that synchronise when first read
+# (A/B: tools/train_step_bench.py --eager-decode)
+LAZY_DECODE = True
+# BEVNet.loss on the GPU replays its loss terms as captured graphs (A/B: tools/train_step_bench.py --no-loss-graph)
+LOSS_GRAPHS = True
 
 
 class _HeadOperand(torch.autograd.Function):
@@ -215,8 +224,10 @@ class BEVNet(nn.Module):
                 parts.append(main.new_zeros(B, self.bev_h, self.bev_w, cp - P - 2))
             x = torch.cat(parts, dim=-1)  # [B, Hb, Wb, cp] channels-last head operand
         det = self.detector.forward_nhwc(x)
+        # the detections are queued, and the host waits for them only when they are read (a training step reads
+        # only the loss: its loss and backward launches then queue behind the forward instead of after a drain)
         boxes, scores = self.detector.decode(det["heatmap"], det["offset"], det["size"],
-                                             conf_thresh=self.conf_thresh, nms_dist_m=self.nms_dist_m)
+                                             conf_thresh=self.conf_thresh, nms_dist_m=self.nms_dist_m, lazy=LAZY_DECODE)
         return {"heatmap": det["heatmap"], "heatmap_logits": det["heatmap_logits"], "boxes": boxes, "scores": scores,
                 "offset": det["offset"], "offset_raw": det["offset_raw"], "size": det["size"],
                 "size_raw": det["size_raw"], "bev_feat": x[..., :P + 2].permute(0, 3, 1, 2)}
@@ -224,16 +235,50 @@ class BEVNet(nn.Module):
     # ---- training objective (model_wrapper.py:105-247) --------------------------
     def loss(self, preds: Dict, targets: List[Dict], loss_cfg: Dict[str, Any]) -> Dict[str, torch.Tensor]:
         t = self._build_training_targets(targets)
-        hm_loss = self._heatmap_focal_loss(preds["heatmap_logits"], t["heatmap"])
-        m = t["mask"].unsqueeze(-1)
-        n = m.sum() + 1e-4
-        off_loss = (self._gather_feat(preds["offset"], t["indices"]) - t["offset"]).mul(m).abs().sum() / n
-        size_loss = (self._gather_feat(preds["size_raw"], t["indices"]) - t["size_log"]).mul(m).abs().sum() / n
-        total = self.hm_weight * hm_loss + self.offset_weight * off_loss + self.size_weight * size_loss
+        args = (preds["heatmap_logits"], preds["offset"], preds["size_raw"], t["heatmap"], t["indices"], t["mask"],
+                t["offset"], t["size_log"])
+        if (LOSS_GRAPHS and args[0].is_cuda and torch.is_grad_enabled()
+                and all(a.is_cuda for a in args) and any(a.requires_grad for a in args[:3])):
+            # the graph's outputs live in its static buffers (overwritten by the next replay): one stack copies them
+            hm_loss, off_loss, size_loss, total = torch.stack(self._graphed_loss_terms(args)(*args)).unbind(0)
+        else:
+            hm_loss, off_loss, size_loss, total = self._loss_terms(*args)
         return {"heatmap_loss": hm_loss, "offset_loss": off_loss, "size_loss": size_loss, "total_loss": total}
 
-    def _target_boxes(self, targets: List[Dict], dev) -> Tuple[torch.Tensor, torch.Tensor]:
-        """All frames' boxes [N, 4] (cx, cy, w, h; centre-only targets get DEFAULT_BOX_WH) + frame index [N]."""
+    def _loss_terms(self, logits, offset, size_raw, hm, indices, mask, off_t, size_t):
+        """model_wrapper.py:105-124: the focal heatmap loss and the masked L1 offset / log-size losses."""
+        hm_loss = self._heatmap_focal_loss(logits, hm)
+        m = mask.unsqueeze(-1)
+        n = m.sum() + 1e-4
+        off_loss = (self._gather_feat(offset, indices) - off_t).mul(m).abs().sum() / n
+        size_loss = (self._gather_feat(size_raw, indices) - size_t).mul(m).abs().sum() / n
+        total = self.hm_weight * hm_loss + self.offset_weight * off_loss + self.size_weight * size_loss
+        return hm_loss, off_loss, size_loss, total
+
+    def _graphed_loss_terms(self, args):
+        """_loss_terms captured as a HIP graph pair (forward, backward) per input signature
+        (torch.cuda.make_graphed_callables): a training step replays ~100 small elementwise / reduction launches
+        as two graph launches plus the input copies, so the loss no longer leaves the GPU waiting on the host
+        between the forward and the backward.  The graphs run the same kernels on the same values: identical
+        results (tests/test_targets.py::test_graphed_loss_identical).  Captured with autocast off -- every input
+        is fp32 and every op of the loss runs in fp32 under autocast(float16) as well."""
+        key = tuple((tuple(a.shape), a.dtype, a.requires_grad, a.device) for a in args)
+        key += (self.hm_weight, self.offset_weight, self.size_weight, self.hm_alpha, self.hm_beta)
+        graphs = self.__dict__.setdefault("_loss_graphs", {})
+        fn = graphs.get(key)
+        if fn is None:
+            samples = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
+            with torch.autocast("cuda", enabled=False):
+                fn = torch.cuda.make_graphed_callables(self._loss_terms, samples, allow_unused_input=True)
+            graphs[key] = fn
+        return fn
+
+    def _target_boxes(self, targets: List[Dict], dev) -> Tuple[torch.Tensor, torch.Tensor, Optional[int]]:
+        """All frames' boxes [N, 4] (cx, cy, w, h; centre-only targets get DEFAULT_BOX_WH) + frame index [N] on
+        `dev`, and an upper bound of the objects' gaussian radii when it is known without waiting for the device.
+        The reference's loader hands the targets over in host memory (train.py:228-243 moves only the images and
+        calibration): then the boxes go over in one pinned, asynchronous copy and the bound comes from the host
+        values; boxes already on the device give None (the splat then reads its bound back, one sync)."""
         boxes, frame = [], []
         for b, tgt in enumerate(targets):
             bx = tgt.get("boxes_world", None)
@@ -241,30 +286,65 @@ class BEVNet(nn.Module):
                 c = tgt.get("centers_world", None)
                 bx = None
                 if c is not None and c.numel() > 0:
-                    c = c.to(dev, torch.float32).reshape(-1, 2)
+                    c = c.to(torch.float32).reshape(-1, 2)
                     bx = torch.cat([c, c.new_tensor(self.default_box_wh).expand(c.shape[0], 2)], dim=1)
             if bx is None:
                 continue
-            bx = bx.to(dev, torch.float32).reshape(-1, bx.shape[-1])
+            bx = bx.to(torch.float32).reshape(-1, bx.shape[-1])
             boxes.append(bx[:, :4])
-            frame.append(torch.full((bx.shape[0],), b, device=dev, dtype=torch.long))
+            frame.append(torch.full((bx.shape[0],), b, device=bx.device, dtype=torch.long))
         if not boxes:
-            return torch.zeros(0, 4, device=dev), torch.zeros(0, dtype=torch.long, device=dev)
-        return torch.cat(boxes), torch.cat(frame)
+            return torch.zeros(0, 4, device=dev), torch.zeros(0, dtype=torch.long, device=dev), None
+        if all(not t.is_cuda for t in boxes):
+            bh, fh = torch.cat(boxes), torch.cat(frame)
+            bound = self._radius_bound_host(bh)
+            if dev.type == "cuda":
+                bh, fh = bh.pin_memory(), fh.pin_memory()
+            return bh.to(dev, non_blocking=True), fh.to(dev, non_blocking=True), bound
+        return torch.cat([t.to(dev) for t in boxes]), torch.cat([t.to(dev) for t in frame]), None
+
+    def _radius_bound_host(self, boxes: torch.Tensor) -> Optional[int]:
+        """An integer >= every gaussian radius _gaussian_radius_tensor gives these (host) boxes: the same formula
+        in float64 on the host, floored, plus one (the device's float32 result differs from it by ~1e-7
+        relative, far below one cell).  None if a size is not finite."""
+        bx = boxes.double().numpy()
+        if not np.isfinite(bx).all():
+            return None
+        # only objects that can be in the grid draw (with a one-cell margin against float32 rounding)
+        x_min, _, y_min, _ = self.bounds
+        gx, gy = (bx[:, 0] - x_min) / self.res_x, (bx[:, 1] - y_min) / self.res_y
+        near = (gx >= -1) & (gx < self.bev_w + 1) & (gy >= -1) & (gy < self.bev_h + 1)
+        wh = bx[near, 2:4]
+        if wh.shape[0] == 0:
+            return 0
+        w = np.maximum(np.maximum(wh[:, 0] / self.res_x, 1e-3), 1.0)
+        h = np.maximum(np.maximum(wh[:, 1] / self.res_y, 1e-3), 1.0)
+        ov = self.gaussian_iou
+        r1 = (h + w + np.sqrt(np.maximum((h + w) ** 2 - 4 * w * h * (1 - ov) / (1 + ov), 0.0))) / 2
+        r2 = (2 * (h + w) + np.sqrt(np.maximum(4 * (h + w) ** 2 - 16 * (1 - ov) * w * h, 0.0))) / 8
+        r = np.minimum(r1, r2)
+        if ov != 0:
+            r3 = (-2 * ov * (h + w) + np.sqrt(np.maximum((2 * ov * (h + w)) ** 2 - 16 * ov * (ov - 1) * w * h,
+                                                         0.0))) / (8 * ov)
+            r = np.minimum(r, r3)
+        r = np.maximum(r, float(self.gaussian_min_radius))
+        return int(np.floor(r.max())) + 1
 
     def _build_training_targets(self, targets: List[Dict]) -> Dict[str, torch.Tensor]:
         """CenterNet targets (model_wrapper.py:127-203) for the whole batch at once: the first MAX_OBJECTS
-        in-grid objects of each frame fill its slots in order; heatmap = per-cell max of their gaussians."""
+        in-grid objects of each frame fill its slots in order; heatmap = per-cell max of their gaussians.
+        No host synchronisation when the targets come in host memory: nothing is compacted by a boolean mask
+        (objects outside the grid or past MAX_OBJECTS write a discarded slot M / a discarded heatmap cell), and
+        the splat's window comes from the host bound (_target_boxes)."""
         dev = next(self.parameters()).device
         B, M, Hb, Wb = len(targets), self.max_objects, self.bev_h, self.bev_w
-        hm = torch.zeros(B, 1, Hb, Wb, device=dev)
-        indices = torch.zeros(B, M, dtype=torch.long, device=dev)
-        mask = torch.zeros(B, M, device=dev)
-        offset = torch.zeros(B, M, 2, device=dev)
-        size_log = torch.zeros(B, M, 2, device=dev)
-        boxes, frame = self._target_boxes(targets, dev)
+        hm_ext = torch.zeros(B * Hb * Wb + 1, device=dev)  # + one discarded cell
+        hm = hm_ext[:-1].view(B, 1, Hb, Wb)
+        boxes, frame, bound = self._target_boxes(targets, dev)
         if boxes.shape[0] == 0:
-            return {"heatmap": hm, "indices": indices, "mask": mask, "offset": offset, "size_log": size_log}
+            z = torch.zeros
+            return {"heatmap": hm, "indices": z(B, M, dtype=torch.long, device=dev), "mask": z(B, M, device=dev),
+                    "offset": z(B, M, 2, device=dev), "size_log": z(B, M, 2, device=dev)}
         x_min, _, y_min, _ = self.bounds
         gx = (boxes[:, 0] - x_min) / self.res_x
         gy = (boxes[:, 1] - y_min) / self.res_y
@@ -275,38 +355,49 @@ class BEVNet(nn.Module):
         before = torch.where(first > 0, run[(first - 1).clamp(min=0)], torch.zeros_like(first))
         slot = run - 1 - before[frame]
         sel = inside & (slot < M)
-        b, s = frame[sel], slot[sel]
-        gx, gy, wh = gx[sel], gy[sel], boxes[sel, 2:4]
+        s = torch.where(sel, slot, torch.full_like(slot, M))  # slot M of each frame: discarded
+        wh = boxes[:, 2:4]
         cx, cy = torch.floor(gx), torch.floor(gy)
         w_cells = (wh[:, 0] / self.res_x).clamp(min=1e-3)
         h_cells = (wh[:, 1] / self.res_y).clamp(min=1e-3)
-        indices[b, s] = cy.long() * Wb + cx.long()
-        mask[b, s] = 1.0
-        offset[b, s] = torch.stack([gx - cx, gy - cy], dim=1)
-        size_log[b, s] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
-        self._splat_gaussians(hm, b, cx.long(), cy.long(), self._gaussian_radius_tensor(w_cells, h_cells))
-        return {"heatmap": hm, "indices": indices, "mask": mask, "offset": offset, "size_log": size_log}
+        cxl, cyl = cx.long(), cy.long()
+        indices = torch.zeros(B, M + 1, dtype=torch.long, device=dev)
+        mask = torch.zeros(B, M + 1, device=dev)
+        offset = torch.zeros(B, M + 1, 2, device=dev)
+        size_log = torch.zeros(B, M + 1, 2, device=dev)
+        indices[frame, s] = cyl * Wb + cxl
+        mask[frame, s] = 1.0
+        offset[frame, s] = torch.stack([gx - cx, gy - cy], dim=1)
+        size_log[frame, s] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
+        self._splat_gaussians(hm_ext, frame, cxl, cyl, self._gaussian_radius_tensor(w_cells, h_cells), sel, bound,
+                              (B, Hb, Wb))
+        return {"heatmap": hm, "indices": indices[:, :M], "mask": mask[:, :M], "offset": offset[:, :M],
+                "size_log": size_log[:, :M]}
 
     @staticmethod
-    def _splat_gaussians(hm: torch.Tensor, b, cx, cy, radius):
-        """hm[b, 0] = max(hm, exp(-(dx^2+dy^2) / (2 sigma^2))) over each object's clipped (2r+1)^2 window,
-        sigma = (2r+1)/6 (the splat of model_wrapper.py:250-276); radius <= 0 draws nothing."""
-        keep = radius > 0
-        if not bool(keep.any()):
+    def _splat_gaussians(hm_ext: torch.Tensor, b, cx, cy, radius, keep, bound: Optional[int], shape):
+        """hm[b, 0] = max(hm, exp(-(dx^2+dy^2) / (2 sigma^2))) over each kept object's clipped (2r+1)^2 window,
+        sigma = (2r+1)/6 (the splat of model_wrapper.py:250-276); radius <= 0 draws nothing.  hm_ext = the
+        flat heatmap [B*Hb*Wb] + one discarded cell that every masked-out window position writes; `bound` >= the
+        largest radius (None: read back from the device).  The maxima are order-free, so the result is the
+        same for any bound."""
+        B, Hb, Wb = shape
+        keep = keep & (radius > 0)
+        R = int(torch.where(keep, radius, torch.zeros_like(radius)).max()) if bound is None else bound
+        if R <= 0:
             return
-        b, cx, cy, radius = b[keep], cx[keep], cy[keep], radius[keep]
-        _, _, Hb, Wb = hm.shape
-        R = int(radius.max())
-        d = torch.arange(-R, R + 1, device=hm.device)
+        d = torch.arange(-R, R + 1, device=hm_ext.device)
         dy, dx = d.view(-1, 1).expand(-1, d.numel()).reshape(-1), d.repeat(d.numel())
         x = cx[:, None] + dx[None]
         y = cy[:, None] + dy[None]
         r = radius[:, None]
-        ok = (dx.abs()[None] <= r) & (dy.abs()[None] <= r) & (x >= 0) & (x < Wb) & (y >= 0) & (y < Hb)
+        ok = (keep[:, None] & (dx.abs()[None] <= r) & (dy.abs()[None] <= r) & (x >= 0) & (x < Wb) & (y >= 0)
+              & (y < Hb))
         two_s2 = ((2.0 * radius.double() + 1.0) / 6.0) ** 2 * 2.0  # the reference's python-float denominator
         val = torch.exp(-(dx * dx + dy * dy).float()[None] / two_s2.float()[:, None])
-        flat = (b[:, None] * Hb + y) * Wb + x
-        hm.view(-1).scatter_reduce_(0, flat[ok], val[ok], reduce="amax", include_self=True)
+        flat = torch.where(ok, (b[:, None] * Hb + y) * Wb + x, B * Hb * Wb)
+        hm_ext.scatter_reduce_(0, flat.reshape(-1), torch.where(ok, val, torch.zeros_like(val)).reshape(-1),
+                               reduce="amax", include_self=True)
 
     def _gaussian_radius_tensor(self, width_cells: torch.Tensor, height_cells: torch.Tensor) -> torch.Tensor:
         """CenterNet radius, same tensor arithmetic (and rounding) as model_wrapper.py:205-233."""
@@ -356,9 +447,11 @@ class BEVNet(nn.Module):
         H, W = heatmap.shape
         if int(radius) > 0 and 0 <= x < W and 0 <= y < H:
             dev = heatmap.device
-            self._splat_gaussians(heatmap.view(1, 1, H, W), torch.zeros(1, dtype=torch.long, device=dev),
-                                  torch.tensor([x], device=dev), torch.tensor([y], device=dev),
-                                  torch.tensor([int(radius)], device=dev))
+            ext = torch.cat([heatmap.reshape(-1), heatmap.new_zeros(1)])
+            self._splat_gaussians(ext, torch.zeros(1, dtype=torch.long, device=dev), torch.tensor([x], device=dev),
+                                  torch.tensor([y], device=dev), torch.tensor([int(radius)], device=dev),
+                                  torch.ones(1, dtype=torch.bool, device=dev), int(radius), (1, H, W))
+            heatmap.copy_(ext[:-1].view(H, W))
         return heatmap
 
     @staticmethod
