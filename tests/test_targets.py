@@ -74,8 +74,11 @@ def test_targets_match_reference_loop():
     for trial in range(60):
         tg = _random_targets(g, trial)
         got, ref = net._build_training_targets(tg), _loop_targets(net, tg)
+        # the graph path's padding: out-of-grid dummy boxes of the last frame change nothing
+        padded = net._targets_from_boxes(*net._target_boxes(tg, torch.device("cpu"), pad=True), len(tg))
         for k in ref:
             assert torch.equal(got[k], ref[k]), (trial, k)
+            assert torch.equal(padded[k], ref[k]), (trial, k)
 
 
 def test_radius_host_bound_covers_device_radii():
@@ -150,4 +153,4 @@ def test_graphed_loss_identical():
     for d, vals in kept:  # returned losses are not aliased to the graph's buffers
         for k in vals:
             assert torch.equal(d[k].detach(), vals[k])
-    assert len(net._loss_graphs) == 1
+    assert 2 <= len(net._loss_graphs) <= 4  # host targets: targets + terms; device targets: terms only
