@@ -6,7 +6,7 @@
 //                                  shift = beta - mean*scale; running_mean / running_var updated with
 //                                  the momentum rule and the unbiased variance (torch's train-mode BN)
 //             k_bn_apply           y = act(z*scale + shift (+ residual)), act = none / ReLU / SiLU (float4)
-//   backward  k_bn_partial<Grads>  per channel (sum g, sum g*xhat), g = dy * act'(u) (ReLU: y > 0 from the
+//   backward  k_bn_partial<GradsT> per channel (sum g, sum g*xhat), g = dy * act'(u) (ReLU: y > 0 from the
 //                                  saved output, or -- no residual -- u = z*scale + shift > 0 recomputed from
 //                                  z (act 3); SiLU: u recomputed), xhat = (z - mean) * rstd
 //             k_bn_bwd_finalize    k1 = sum g / M, k2 = sum g xhat / M, dbeta, dgamma
@@ -33,6 +33,7 @@ namespace {
 constexpr int BN_T = 256;
 constexpr int BN_ROWS = 1024;  // rows per block
 constexpr int BN_QB = 64;      // channel quads per block (256 channels)
+constexpr int BN_U = 4;        // rows per load batch of the streaming passes
 
 struct Stats {  // (z, z^2)
     const float *z;
@@ -83,13 +84,48 @@ __device__ __forceinline__ void act_grad(float (&g)[4], const float4 d, const fl
     }
 }
 
-struct Grads {  // (g, g * xhat)
+// act_grad with the activation as a template parameter (no per-element branch, so the batched row loops below keep
+// every load of a batch in flight): the same expressions, so the same values
+template <int ACT>
+__device__ __forceinline__ void act_side(const float *y, int64_t i, float4 &o, unsigned &m) {
+    if constexpr (ACT == 1) o = *(const float4 *)(y + i);
+    if constexpr (ACT == 4) m = reinterpret_cast<const uint8_t *>(y)[i >> 2];
+}
+template <int ACT>
+__device__ __forceinline__ void act_grad_t(float (&g)[4], const float4 d, const float4 o, const unsigned m,
+                                           const float4 v, const float *sc, const float *sh) {
+    g[0] = d.x;
+    g[1] = d.y;
+    g[2] = d.z;
+    g[3] = d.w;
+    const float ov[4] = {o.x, o.y, o.z, o.w}, zv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if constexpr (ACT == 1) g[u] = ov[u] > 0.f ? g[u] : 0.f;
+        if constexpr (ACT == 4) g[u] = (m >> u) & 1u ? g[u] : 0.f;
+        if constexpr (ACT == 3) g[u] = bn_u(zv[u], sc[u], sh[u]) > 0.f ? g[u] : 0.f;
+        if constexpr (ACT == 2) g[u] *= silu_grad(bn_u(zv[u], sc[u], sh[u]));
+    }
+}
+
+template <int ACT>
+struct GradsT {  // Grads with a compile-time activation
     const float *dy, *y, *z, *mean, *rstd, *scale, *shift;
-    int act;
     __device__ void at(int64_t i, int c, float4 &a, float4 &b) const {
         const float4 d = *(const float4 *)(dy + i), v = *(const float4 *)(z + i);
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        unsigned m = 0;
+        act_side<ACT>(y, i, o, m);
+        float sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (ACT == 2 || ACT == 3) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                sc[u] = scale[c + u];
+                sh[u] = shift[c + u];
+            }
+        }
         float g[4];
-        act_grad(g, d, y, v, scale, shift, act, i, c);
+        act_grad_t<ACT>(g, d, o, m, v, sc, sh);
         const float zv[4] = {v.x, v.y, v.z, v.w};
         float h[4];
 #pragma unroll
@@ -110,7 +146,20 @@ __device__ __forceinline__ void k_bn_partial_body(const F &f, int64_t M, int C, 
     const int64_t r0 = (int64_t)blk * BN_ROWS, r1 = r0 + BN_ROWS < M ? r0 + BN_ROWS : M;
     double s[4] = {0, 0, 0, 0}, t[4] = {0, 0, 0, 0};
     if (ph < nph && qg < C4) {
-        for (int64_t r = r0 + ph; r < r1; r += nph) {
+        // rows in batches of BN_U: the batch's loads all in flight before the first use (one row at a time left
+        // ~2 float4 loads per wave outstanding: latency-, not HBM-bound); the sums still run row by row, in order
+        int64_t r = r0 + ph;
+        for (; r + (BN_U - 1) * nph < r1; r += BN_U * nph) {
+            float4 a[BN_U], b[BN_U];
+#pragma unroll
+            for (int u = 0; u < BN_U; ++u) f.at((r + u * nph) * C + 4 * qg, 4 * qg, a[u], b[u]);
+#pragma unroll
+            for (int u = 0; u < BN_U; ++u) {
+                s[0] += a[u].x; s[1] += a[u].y; s[2] += a[u].z; s[3] += a[u].w;
+                t[0] += b[u].x; t[1] += b[u].y; t[2] += b[u].z; t[3] += b[u].w;
+            }
+        }
+        for (; r < r1; r += nph) {
             float4 a, b;
             f.at(r * C + 4 * qg, 4 * qg, a, b);
             s[0] += a.x; s[1] += a.y; s[2] += a.z; s[3] += a.w;
@@ -325,43 +374,70 @@ __global__ void k_bn_bwd_apply(const float *__restrict__ dy, const float *__rest
 // values per element.  Same arithmetic per element, so identical results.
 constexpr int BNQ_ROWS = 256;
 
-template <typename OT>
+template <typename OT, int ACT, bool RES>
+__device__ __forceinline__ void bn_apply_one(const float4 v, const float4 rr, const float4 s, const float4 h, OT *y,
+                                             uint8_t *mask, int64_t e) {
+    float4 o = make_float4(bn_u(v.x, s.x, h.x), bn_u(v.y, s.y, h.y), bn_u(v.z, s.z, h.z), bn_u(v.w, s.w, h.w));
+    if constexpr (RES) o = make_float4(o.x + rr.x, o.y + rr.y, o.z + rr.z, o.w + rr.w);
+    if constexpr (ACT == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
+    if constexpr (ACT == 2) o = make_float4(silu_hw(o.x), silu_hw(o.y), silu_hw(o.z), silu_hw(o.w));
+    st4(y, e, o);
+    if (mask)  // act 1: bit u = (y[e + u] > 0), what the backward's act 4 reads instead of y
+        mask[e >> 2] = (uint8_t)((o.x > 0.f) | ((o.y > 0.f) << 1) | ((o.z > 0.f) << 2) | ((o.w > 0.f) << 3));
+}
+
+template <typename OT, int ACT, bool RES>
 __global__ __launch_bounds__(256) void k_bn_apply_q(const float *__restrict__ z, int64_t M, int C,
                                                     const float *__restrict__ scale, const float *__restrict__ shift,
-                                                    const float *__restrict__ res, int act, OT *__restrict__ y,
+                                                    const float *__restrict__ res, OT *__restrict__ y,
                                                     uint8_t *__restrict__ mask) {
     const int tid = threadIdx.x, QP = C / 4, q = tid % QP, ph = tid / QP, nph = 256 / QP;
     const int64_t r0 = (int64_t)blockIdx.x * BNQ_ROWS, r1 = r0 + BNQ_ROWS < M ? r0 + BNQ_ROWS : M;
     const float4 s = *(const float4 *)(scale + 4 * q), h = *(const float4 *)(shift + 4 * q);
-    for (int64_t r = r0 + ph; r < r1; r += nph) {
-        const int64_t e = r * C + 4 * q;
-        const float4 v = *(const float4 *)(z + e);
-        float4 o = make_float4(bn_u(v.x, s.x, h.x), bn_u(v.y, s.y, h.y), bn_u(v.z, s.z, h.z), bn_u(v.w, s.w, h.w));
-        if (res) {
-            const float4 rr = *(const float4 *)(res + e);
-            o = make_float4(o.x + rr.x, o.y + rr.y, o.z + rr.z, o.w + rr.w);
+    const float4 zero = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t r = r0 + ph;
+    for (; r + (BN_U - 1) * nph < r1; r += BN_U * nph) {  // BN_U rows' loads in flight at once
+        float4 v[BN_U], rr[BN_U];
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u) {
+            const int64_t e = (r + u * nph) * C + 4 * q;
+            v[u] = *(const float4 *)(z + e);
+            rr[u] = RES ? *(const float4 *)(res + e) : zero;
         }
-        if (act == 1) o = make_float4(fmaxf(o.x, 0.f), fmaxf(o.y, 0.f), fmaxf(o.z, 0.f), fmaxf(o.w, 0.f));
-        if (act == 2) o = make_float4(silu_hw(o.x), silu_hw(o.y), silu_hw(o.z), silu_hw(o.w));
-        st4(y, e, o);
-        if (mask)  // act 1: bit u = (y[e + u] > 0), what the backward's act 4 reads instead of y
-            mask[e >> 2] = (uint8_t)((o.x > 0.f) | ((o.y > 0.f) << 1) | ((o.z > 0.f) << 2) | ((o.w > 0.f) << 3));
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u) bn_apply_one<OT, ACT, RES>(v[u], rr[u], s, h, y, mask, (r + u * nph) * C + 4 * q);
+    }
+    for (; r < r1; r += nph) {
+        const int64_t e = r * C + 4 * q;
+        bn_apply_one<OT, ACT, RES>(*(const float4 *)(z + e), RES ? *(const float4 *)(res + e) : zero, s, h, y, mask, e);
     }
 }
 
 template <typename OT>
+static void launch_bn_apply_q(dim3 g, hipStream_t st, const float *z, int64_t M, int C, const float *scale,
+                              const float *shift, const float *res, int act, OT *y, uint8_t *mask) {
+#define BN_APPLY_Q(A, R) hipLaunchKernelGGL((k_bn_apply_q<OT, A, R>), g, dim3(256), 0, st, z, M, C, scale, shift, res, y, mask)
+    if (res) {
+        if (act == 1) BN_APPLY_Q(1, true); else if (act == 2) BN_APPLY_Q(2, true); else BN_APPLY_Q(0, true);
+    } else {
+        if (act == 1) BN_APPLY_Q(1, false); else if (act == 2) BN_APPLY_Q(2, false); else BN_APPLY_Q(0, false);
+    }
+#undef BN_APPLY_Q
+}
+
+template <typename OT, int ACT>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_q(const float *__restrict__ dy, const float *__restrict__ y,
                                                         const float *__restrict__ z, int64_t M, int C,
                                                         const float *__restrict__ mean, const float *__restrict__ rstd,
                                                         const float *__restrict__ gamma,
                                                         const float *__restrict__ scale,
-                                                        const float *__restrict__ shift, int act,
+                                                        const float *__restrict__ shift,
                                                         const float *__restrict__ coef, OT *__restrict__ dz,
                                                         float *__restrict__ dres) {
     const int tid = threadIdx.x, QP = C / 4, q = tid % QP, ph = tid / QP, nph = 256 / QP;
     const int64_t r0 = (int64_t)blockIdx.x * BNQ_ROWS, r1 = r0 + BNQ_ROWS < M ? r0 + BNQ_ROWS : M;
     const int c0 = 4 * q;
-    float mu[4], rs[4], gr[4], k1[4], k2[4];
+    float mu[4], rs[4], gr[4], k1[4], k2[4], sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         mu[u] = mean[c0 + u];
@@ -369,22 +445,63 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_q(const float *__restrict_
         gr[u] = gamma[c0 + u] * rstd[c0 + u];
         k1[u] = coef[2 * (c0 + u)];
         k2[u] = coef[2 * (c0 + u) + 1];
+        if constexpr (ACT == 2 || ACT == 3) {
+            sc[u] = scale[c0 + u];
+            sh[u] = shift[c0 + u];
+        }
     }
-    for (int64_t r = r0 + ph; r < r1; r += nph) {
-        const int64_t e = r * C + c0;
-        const float4 d = *(const float4 *)(dy + e), v = *(const float4 *)(z + e);
+    auto one = [&](const float4 d, const float4 v, const float4 o, const unsigned m, const int64_t e) {
         float g[4];
-        act_grad(g, d, y, v, scale, shift, act, e, c0);
+        act_grad_t<ACT>(g, d, o, m, v, sc, sh);
         const float zv[4] = {v.x, v.y, v.z, v.w};
-        float o[4];
+        float out[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const float xh = (zv[u] - mu[u]) * rs[u];
-            o[u] = gr[u] * (g[u] - k1[u] - xh * k2[u]);
+            out[u] = gr[u] * (g[u] - k1[u] - xh * k2[u]);
         }
-        st4(dz, e, make_float4(o[0], o[1], o[2], o[3]));
+        st4(dz, e, make_float4(out[0], out[1], out[2], out[3]));
         if (dres) *(float4 *)(dres + e) = make_float4(g[0], g[1], g[2], g[3]);
+    };
+    int64_t r = r0 + ph;
+    for (; r + (BN_U - 1) * nph < r1; r += BN_U * nph) {  // BN_U rows' loads in flight at once
+        float4 d[BN_U], v[BN_U], o[BN_U];
+        unsigned m[BN_U];
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u) {
+            const int64_t e = (r + u * nph) * C + c0;
+            d[u] = *(const float4 *)(dy + e);
+            v[u] = *(const float4 *)(z + e);
+            o[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            m[u] = 0;
+            act_side<ACT>(y, e, o[u], m[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u) one(d[u], v[u], o[u], m[u], (r + u * nph) * C + c0);
     }
+    for (; r < r1; r += nph) {
+        const int64_t e = r * C + c0;
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        unsigned m = 0;
+        act_side<ACT>(y, e, o, m);
+        one(*(const float4 *)(dy + e), *(const float4 *)(z + e), o, m, e);
+    }
+}
+
+template <typename OT>
+static void launch_bn_bwd_apply_q(dim3 g, hipStream_t st, const float *dy, const float *y, const float *z, int64_t M,
+                                  int C, const float *mean, const float *rstd, const float *gamma, const float *scale,
+                                  const float *shift, int act, const float *coef, OT *dz, float *dres) {
+#define BN_BWD_Q(A) hipLaunchKernelGGL((k_bn_bwd_apply_q<OT, A>), g, dim3(256), 0, st, dy, y, z, M, C, mean, rstd, \
+                                       gamma, scale, shift, coef, dz, dres)
+    switch (act) {
+        case 1: BN_BWD_Q(1); break;
+        case 2: BN_BWD_Q(2); break;
+        case 3: BN_BWD_Q(3); break;
+        case 4: BN_BWD_Q(4); break;
+        default: BN_BWD_Q(0); break;
+    }
+#undef BN_BWD_Q
 }
 
 // ---- per-image channel sums and channel affine (SqueezeExcite training) -------------------------------
@@ -490,11 +607,9 @@ int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *sc
     if (256 % (C / 4) == 0) {
         const dim3 gq((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS));
         if (y_half)
-            hipLaunchKernelGGL(k_bn_apply_q<_Float16>, gq, dim3(256), 0, st, z, M, C, scale, shift, residual, act,
-                               (_Float16 *)y, (uint8_t *)nullptr);
+            launch_bn_apply_q<_Float16>(gq, st, z, M, C, scale, shift, residual, act, (_Float16 *)y, nullptr);
         else
-            hipLaunchKernelGGL(k_bn_apply_q<float>, gq, dim3(256), 0, st, z, M, C, scale, shift, residual, act,
-                               (float *)y, (uint8_t *)nullptr);
+            launch_bn_apply_q<float>(gq, st, z, M, C, scale, shift, residual, act, (float *)y, nullptr);
         return (int)hipGetLastError();
     }
     const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
@@ -516,8 +631,8 @@ int bev_batchnorm_apply_ex_f32(const float *z, int64_t M, int C, const float *sc
 int bev_batchnorm_apply_mask_f32(const float *z, int64_t M, int C, const float *scale, const float *shift,
                                  const float *residual, float *y, uint8_t *mask, void *stream) {
     if (!z || !scale || !shift || !y || !mask || !bn_shape_ok(M, C) || 256 % (C / 4) != 0) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL(k_bn_apply_q<float>, dim3((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS)), dim3(256), 0,
-                       (hipStream_t)stream, z, M, C, scale, shift, residual, 1, y, mask);
+    launch_bn_apply_q<float>(dim3((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS)), (hipStream_t)stream, z, M, C, scale,
+                             shift, residual, 1, y, mask);
     return (int)hipGetLastError();
 }
 
@@ -539,7 +654,16 @@ int bev_batchnorm_bwd_ex_f32(const float *dy, const float *y, const float *z, in
     double *part = (double *)workspace;
     float *coef = (float *)(part + (size_t)nb * C * 2);
     const dim3 grid(nb, (C / 4 + BN_QB - 1) / BN_QB);
-    hipLaunchKernelGGL(k_bn_partial<Grads>, grid, dim3(BN_T), 0, st, Grads{dy, y, z, mean, rstd, scale, shift, act}, M, C, part);
+#define BN_PART_G(A) hipLaunchKernelGGL(k_bn_partial<GradsT<A>>, grid, dim3(BN_T), 0, st, \
+                                      GradsT<A>{dy, y, z, mean, rstd, scale, shift}, M, C, part)
+    switch (act) {
+        case 1: BN_PART_G(1); break;
+        case 2: BN_PART_G(2); break;
+        case 3: BN_PART_G(3); break;
+        case 4: BN_PART_G(4); break;
+        default: BN_PART_G(0); break;
+    }
+#undef BN_PART_G
     hipLaunchKernelGGL(k_bn_bwd_finalize, dim3((C + FIN_C - 1) / FIN_C), dim3(FIN_C * FIN_P), 0, st, part, nb, M, C,
                        frozen, coef, dgamma, dbeta);
     const int64_t total4 = M * C / 4;
@@ -547,11 +671,11 @@ int bev_batchnorm_bwd_ex_f32(const float *dy, const float *y, const float *z, in
     if (256 % (C / 4) == 0) {
         const dim3 gq((unsigned)((M + BNQ_ROWS - 1) / BNQ_ROWS));
         if (dz_half)
-            hipLaunchKernelGGL(k_bn_bwd_apply_q<_Float16>, gq, dim3(256), 0, st, dy, y, z, M, C, mean, rstd, gamma,
-                               scale, shift, act, coef, (_Float16 *)dz, dres);
+            launch_bn_bwd_apply_q<_Float16>(gq, st, dy, y, z, M, C, mean, rstd, gamma, scale, shift, act, coef,
+                                            (_Float16 *)dz, dres);
         else
-            hipLaunchKernelGGL(k_bn_bwd_apply_q<float>, gq, dim3(256), 0, st, dy, y, z, M, C, mean, rstd, gamma,
-                               scale, shift, act, coef, (float *)dz, dres);
+            launch_bn_bwd_apply_q<float>(gq, st, dy, y, z, M, C, mean, rstd, gamma, scale, shift, act, coef,
+                                         (float *)dz, dres);
         return (int)hipGetLastError();
     }
     const bool small = total4 < ((int64_t)1 << 32) - 65536 * 256;
