@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--stream-offset", type=int, default=None, help="ResNet inference: stagger of the stream groups")
     ap.add_argument("--cpu-iters", type=int, default=3, help="frames timed for the CPU baseline (median; 0 = skip)")
     ap.add_argument("--warp-only", action="store_true", help="time only the fused warp (for profiling)")
+    ap.add_argument("--warp-nhwc", action="store_true", help="A/B: the fused warp writes its output channels-last "
+                    "(bev_ipm_warp_fuse_nhwc_f32) instead of the default NCHW storage")
     ap.add_argument("--conv-arith", choices=("bf16x6", "f32"), default="bf16x6",
                     help="trunk conv arithmetic: bf16x6 = fp32 through exact 3-way bf16 splits (default), f32 = the "
                          "exact-f32 MFMA kernels")
@@ -454,6 +456,7 @@ def main():
         nat.tune(getattr(nat, "TUNE_" + name.upper()), int(v))
     nat.set_conv_arith(args.conv_arith)
     stream = torch.cuda.current_stream(dev)
+    bev_format = torch.channels_last if args.warp_nhwc else torch.contiguous_format
     ev = []  # (t0, t1, t2) per timed step: backbone [t0,t1], geometry (+ exchange) [t1,t2]
 
     def step(record):
@@ -476,7 +479,7 @@ def main():
             if args.camera_shard:
                 bev = bev_dist.camera_sharded_forward(geom, feats, Kd, Rtd, (H, W), V, "mean")
             else:
-                bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean")
+                bev = geom.forward_fused(feats, Kd, Rtd, (H, W), "mean", memory_format=bev_format)
             if record:
                 e2.record(stream)
                 ev.append((e0, e1, e2))
@@ -600,6 +603,8 @@ def main():
                                         if B == 2 else "--batch"),
                        "frames_per_step": B if args.camera_shard else world * B, "cameras": V,
                        "cameras_per_gpu": VL, "bev": list(args.bev), "channels": C,
+                       "bev_memory_format": ("n/a" if args.camera_shard else
+                                             "channels_last (--warp-nhwc)" if args.warp_nhwc else "NCHW"),
                        "parallelism": (f"camera-sharded x{world} (reduce-scatter over BEV rows)" if args.camera_shard
                                        else f"frame-sharded x{world} (no collective)")},
             "roofline": roof_bb_hbm or roof_bb or roof_wp,

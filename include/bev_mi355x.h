@@ -159,6 +159,17 @@ int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_
                               const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy,
                               int Hb, int Wb, int mode, float *out, void *workspace, int64_t workspace_bytes,
                               void *stream);
+/* bev_ipm_warp_fuse_pre_f32 (boxes_ready != 0) or _ws_f32 (boxes_ready == 0) writing the fused map channels-last:
+ * out [B][Hb][Wb][C] (a [B][C][Hb][Wb] tensor in torch.channels_last memory format), the layout the reference's next
+ * consumer -- the BEV projection / detector convs (model_wrapper.py:72-84) -- reads best, and one a 16 x 16 tile writes
+ * as whole 128-B lines (1 KiB per store instruction) instead of 64-B row segments per channel plane.  Same values as the
+ * plain call.  Needs the LDS-DMA kernel's layout (NHWC features, C % 64 == 0, ...) and one frame's output < 2 GiB; else
+ * BEV_ERR_ARGS.  Replaces geometry.py:120-162 + fusion.py:17-22 (the fused inference path, GeometryTransformer
+ * .forward_fused). */
+int bev_ipm_warp_fuse_nhwc_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                               const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx,
+                               float sy, int Hb, int Wb, int mode, float *out, void *workspace,
+                               int64_t workspace_bytes, int boxes_ready, void *stream);
 /* bev_ipm_warp_fuse_pre_f32 (boxes_ready != 0) or _ws_f32 (boxes_ready == 0) writing the fused map in
  * rank-chunk-major row order for the camera-shard exchange: out [ceil(Hb / rows_per_chunk)][B][C][rows_per_chunk][Wb],
  * BEV row r of frame b at chunk r / rows_per_chunk, row r % rows_per_chunk -- the layout reduce_scatter over BEV rows

@@ -74,11 +74,8 @@ def test_targets_match_reference_loop():
     for trial in range(60):
         tg = _random_targets(g, trial)
         got, ref = net._build_training_targets(tg), _loop_targets(net, tg)
-        # the graph path's padding: out-of-grid dummy boxes of the last frame change nothing
-        padded = net._targets_from_boxes(*net._target_boxes(tg, torch.device("cpu"), pad=True), len(tg))
         for k in ref:
             assert torch.equal(got[k], ref[k]), (trial, k)
-            assert torch.equal(padded[k], ref[k]), (trial, k)
 
 
 def test_radius_host_bound_covers_device_radii():
@@ -118,39 +115,3 @@ def test_targets_host_and_device_boxes_identical_and_lazy_decode():
     for a, b in zip(list(lb) + list(ls), eb + es):
         assert torch.equal(a, b)
 
-
-@pytest.mark.gpu
-def test_graphed_loss_identical():
-    """BEVNet.loss through the captured graphs (LOSS_GRAPHS) vs the eager loss terms: the same values and input
-    gradients bit for bit, over several target sets replayed through one cached graph (host- and device-resident
-    targets), with the earlier call's losses left intact by the later replays."""
-    import models.model_wrapper as mw
-    dev = torch.device("cuda:0")
-    net = BEVNet(CFG).to(dev)
-    g = torch.Generator().manual_seed(8)
-    kept = []
-    for trial in range(6):
-        preds = {k: torch.randn(2, c, 60, 180, device=dev, requires_grad=True)
-                 for k, c in (("heatmap_logits", 1), ("offset", 2), ("size_raw", 2))}
-        tg = [{"boxes_world": torch.cat([torch.rand(4, 1, generator=g) * 40 - 20, torch.rand(4, 1, generator=g) * 12 - 6,
-                                         torch.rand(4, 2, generator=g) + 0.2], 1)} for _ in range(2)]
-        if trial % 2:
-            tg = [{k: v.to(dev) for k, v in t.items()} for t in tg]
-        out = {}
-        for graphs in (True, False):
-            mw.LOSS_GRAPHS = graphs
-            try:
-                d = net.loss(preds, tg, {})
-                grads = torch.autograd.grad(d["total_loss"], list(preds.values()))
-            finally:
-                mw.LOSS_GRAPHS = True
-            out[graphs] = ({k: v.detach().clone() for k, v in d.items()}, grads, d)
-        for k in out[True][0]:
-            assert torch.equal(out[True][0][k], out[False][0][k]), (trial, k)
-        for a, b in zip(out[True][1], out[False][1]):
-            assert torch.equal(a, b), trial
-        kept.append((out[True][2], out[True][0]))
-    for d, vals in kept:  # returned losses are not aliased to the graph's buffers
-        for k in vals:
-            assert torch.equal(d[k].detach(), vals[k])
-    assert 2 <= len(net._loss_graphs) <= 4  # host targets: targets + terms; device targets: terms only

@@ -32,6 +32,46 @@ __global__ __launch_bounds__(256) void k_store(float *__restrict__ out, int Hb, 
                                               (int)(uint32_t)(q * plane * sizeof(float)), AUX);
 }
 
+// NHWC ([B][Hb][Wb][64], channels-last): the 16 x 16 tile's 64 cells per wave = 4 rows of 16 cells, each row 4 KiB
+// contiguous.  LANE: lane = cell (k_warp_fuse_v2's cell mapping), its 256-B run as 16 float4 stores (per instruction
+// 64 x 16 B at a 256-B stride, merged in L2); COAL: instruction k writes row k / 4's bytes (k % 4) KiB .. + 1 KiB,
+// 16 B per lane, 1 KiB contiguous per instruction (the data would come through LDS).
+template <int AUX, bool COAL>
+__global__ __launch_bounds__(256) void k_store_nhwc(float *__restrict__ out, int Hb, int Wb) {
+    constexpr int TH = 16, TW = 16;
+    const int ntx = Wb / TW, nt = ntx * (Hb / TH);
+    int tile = blockIdx.x;
+    {
+        const int q = nt / 8, r = nt % 8, x = tile % 8;
+        tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    const int ty = tile / ntx, tx = tile - ty * ntx;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float *frame = out + (size_t)blockIdx.y * Hb * Wb * 64;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(frame, 0, (int)(uint32_t)((size_t)Hb * Wb * 64 * sizeof(float)), 0x00020000);
+    const float a = (float)(lane + tile);
+    if (COAL) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int row = ty * TH + wave * 4 + k / 4;
+            const int voff = ((row * Wb + tx * TW) * 64) * 4 + ((k % 4) * 64 + lane) * 16;
+            const float4 v = make_float4(a, a + 1.f, a + 2.f, (float)k);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int __attribute__((ext_vector_type(4))), v), rs,
+                                                   voff, 0, AUX);
+        }
+    } else {
+        const int i = ty * TH + wave * 4 + lane / 16, j = tx * TW + lane % 16;
+        const int voff = (i * Wb + j) * 256;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float4 v = make_float4(a, a + 1.f, a + 2.f, (float)q);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int __attribute__((ext_vector_type(4))), v), rs,
+                                                   voff, q * 16, AUX);
+        }
+    }
+}
+
 // reference: the same bytes as a plain float4 fill (every wave writes 1 KiB contiguous per instruction)
 __global__ __launch_bounds__(256) void k_fill4(float4 *__restrict__ out, size_t n4) {
     for (size_t k = (size_t)blockIdx.x * 256 + threadIdx.x; k < n4; k += (size_t)gridDim.x * 256)
@@ -57,6 +97,8 @@ int main() {
         {"8x32  raster   nt(2)", k_store<8, 2, 0>, 8},     {"8x32  xcd-8ths nt(2)", k_store<8, 2, 1>, 8},
         {"8x32  xcd-8ths aux0", k_store<8, 0, 1>, 8},      {"4x64  raster   nt(2)", k_store<4, 2, 0>, 4},
         {"4x64  xcd-8ths nt(2)", k_store<4, 2, 1>, 4},     {"4x64  xcd-8ths aux0", k_store<4, 0, 1>, 4},
+        {"NHWC 16x16 lane aux0", k_store_nhwc<0, false>, 16}, {"NHWC 16x16 lane nt(2)", k_store_nhwc<2, false>, 16},
+        {"NHWC 16x16 coal aux0", k_store_nhwc<0, true>, 16},  {"NHWC 16x16 coal nt(2)", k_store_nhwc<2, true>, 16},
     };
     for (int rnd = 0; rnd < 3; ++rnd) {
         for (auto &c : cases) {

@@ -38,7 +38,6 @@ def main():
     ap.add_argument("--eager-decode", action="store_true", help="A/B: BEVNet.forward synchronises on its decode")
     ap.add_argument("--device-targets", action="store_true", help="A/B: the targets already on the device (the "
                     "reference's loop, train.py:228-243, leaves them in host memory)")
-    ap.add_argument("--no-loss-graph", action="store_true", help="A/B: BEVNet.loss launches its terms eagerly")
     ap.add_argument("--no-pool-arg", action="store_true", help="A/B: the stem max-pool saves its input and the backward "
                     "re-scans it for the argmax instead of taking the forward's argmax bytes (trunk_grad.MAXPOOL_ARG)")
     a = ap.parse_args()
@@ -52,7 +51,6 @@ def main():
         trunk_grad.MAXPOOL_ARG = False
     import models.model_wrapper as _mw
     _mw.LAZY_DECODE = not a.eager_decode
-    _mw.LOSS_GRAPHS = not a.no_loss_graph
     for kv in a.tune:
         name, v = kv.split("=")
         bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))
@@ -127,7 +125,6 @@ def main():
                       "bev_proj_ch": a.proj_ch if a.bevnet else None,
                       "amp": a.amp, "half_convs": a.amp and not a.fp32_kernels,
                       "decode": "eager" if a.eager_decode else "lazy",
-                      "loss_graph": not a.no_loss_graph,
                       "targets": "device" if a.device_targets else "host",
                       "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
                       "loss": float(loss)}), flush=True)

@@ -57,6 +57,8 @@ SIGNATURES = {
     "bev_head_operand_bwd_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_head_operand_bwd_bias_partials": (_i64, [_i, _i, _i, _i]),
     "bev_head_operand_bwd_bias_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "bev_ipm_warp_fuse_nhwc_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
+                                        _i, _i, _vp, _vp, _i64, _i, _vp]),
     "bev_ipm_warp_fuse_chunked_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
                                            _i, _i, _i, _vp, _vp, _i64, _i, _vp]),
     "bev_ipm_taps_f32": (_i, [_vp, _vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _vp, _vp, _vp]),
@@ -441,13 +443,17 @@ def warp_fuse_boxes(H: torch.Tensor, xs, ys, B: int, V: int, Hf: int, Wf: int, i
 
 
 def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, out: torch.Tensor = None,
-              boxes: torch.Tensor = None, rows_per_chunk: int = None):
+              boxes: torch.Tensor = None, rows_per_chunk: int = None, channels_last: bool = False):
     """feats [B,V,C,Hf,Wf] (any strides within a map; maps b*V+v) -> out [B,C,Hb,Wb].  `boxes`: a workspace filled
     by `warp_fuse_boxes` for this geometry and mode (the pre-pass is then not launched again).
     `rows_per_chunk` (< Hb): the rank-chunk-major layout of bev_ipm_warp_fuse_chunked_f32 instead,
-    out [ceil(Hb / rpr), B, C, rpr, Wb] with the rows past Hb zero (the camera-shard reduce-scatter's input)."""
+    out [ceil(Hb / rpr), B, C, rpr, Wb] with the rows past Hb zero (the camera-shard reduce-scatter's input).
+    `channels_last`: bev_ipm_warp_fuse_nhwc_f32 -- the same [B,C,Hb,Wb] values in torch.channels_last memory format
+    (storage [B,Hb,Wb,C]); needs NHWC features with C % 64 == 0 (the LDS-DMA kernel), else HipError."""
     if rows_per_chunk is not None and rows_per_chunk < ys.numel():
         return _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, int(rows_per_chunk), boxes)
+    if channels_last:
+        return _warp_fuse_nhwc(feats, H, xs, ys, img_hw, mode, out, boxes)
     _require_gpu(feats, H, xs, ys)
     B, V, C, Hf, Wf = feats.shape
     if B * V > 0 and feats.stride(0) != V * feats.stride(1):
@@ -472,6 +478,36 @@ def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, o
         rc = fn(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V, C, Hf, Wf, sx, sy, Hb, Wb,
                 FUSE_MODES[mode], _ptr(out), _ptr(ws), nws, _stream(feats))
     _check(rc, "bev_ipm_warp_fuse")
+    return out
+
+
+def _warp_fuse_nhwc(feats, H, xs, ys, img_hw, mode, out=None, boxes=None):
+    _require_gpu(feats, H, xs, ys)
+    B, V, C, Hf, Wf = feats.shape
+    if B * V > 0 and feats.stride(0) != V * feats.stride(1):
+        feats = feats.contiguous()
+    Hb, Wb = ys.numel(), xs.numel()
+    sx, sy = _scales(Hf, Wf, img_hw)
+    if out is None:
+        out = torch.empty(B, Hb, Wb, C, device=feats.device, dtype=torch.float32).permute(0, 3, 1, 2)
+    assert out.shape == (B, C, Hb, Wb) and out.permute(0, 2, 3, 1).is_contiguous(), "channels-last [B,C,Hb,Wb] out"
+    s = feats.stride()
+    nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
+    ready = boxes is not None
+    if boxes is None and s[2] == 1 and C % 64 == 0 and V <= 64 and Hf < 16384 and Wf < 16384 and B * Hb * Wb > 0:
+        boxes, ready = warp_fuse_boxes(H, xs, ys, B, V, Hf, Wf, img_hw, mode), True
+    if boxes is not None:
+        assert boxes.numel() >= nws and boxes.device == feats.device, "boxes workspace for another geometry"
+    ws = boxes if boxes is not None else torch.empty(max(nws, 8), device=feats.device, dtype=torch.uint8)
+    with _span("warp_fuse", feats):
+        rc = lib().bev_ipm_warp_fuse_nhwc_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B, V,
+                                              C, Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], _ptr(out), _ptr(ws), nws,
+                                              int(ready), _stream(feats))
+    if rc == -1 and boxes is not None:  # a kernel choice without the channels-last store (BEV_TUNE_WARP_KERNEL 1 / a
+        # small WARP_POOL_KB, A/B knobs): the NCHW launch, then one layout copy on the device
+        out.copy_(warp_fuse(feats, H, xs, ys, img_hw, mode, boxes=boxes if ready else None))
+        return out
+    _check(rc, "bev_ipm_warp_fuse_nhwc_f32")
     return out
 
 

@@ -897,7 +897,7 @@ __device__ __forceinline__ void tile_cell(int lane, int wave, int &r, int &c) {
     }
 }
 
-template <int MODE, int OCC, int TH = 8, bool CHUNK = false>
+template <int MODE, int OCC, int TH = 8, bool CHUNK = false, bool NHWC = false>
 __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__restrict__ feats, int64_t sN, int64_t sH,
                                                           int64_t sW, const float *__restrict__ Hmat,
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
@@ -951,6 +951,52 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         const size_t orange = (size_t)((Hb + rpr - 1) / rpr) * B * C * oplane * sizeof(float);  // whole output
         store_chunk(out + ((size_t)b * C + c0) * oplane, oplane, ovoff, acc, MODE, md,
                     out_range(orange, ((size_t)b * C + c0) * oplane));
+    };
+    // NHWC: channels-last output [B][Hb][Wb][C] (bev_ipm_warp_fuse_nhwc_f32).  A cell's C values are one contiguous
+    // run, so a wave's 4 x 16 (TH 16) cells are 4 row runs of 16 x C floats: each lane parks its 32-channel half in
+    // the (free) pool, and the wave writes it back 16 B per lane, 8 cells x 128 B (whole cache lines) per store --
+    // 1 KiB per instruction instead of the NCHW layout's 64-B row segments per channel plane
+    // (tools/store_pattern_micro.hip: 65.5 vs 104.5 us for the 354 MB of a batch-2 launch).  Same values.
+    auto store_nhwc = [&](int c0, const float (&acc)[CK], const MeanDiv &md) {
+        constexpr int RW = TH / NW, NS = 36;  // rows per wave; floats per parked cell (32 + 4 pad)
+        __syncthreads();                      // every wave is done with the pool
+        float *stg = reinterpret_cast<float *>(smem) + wave * 64 * NS;
+        const int cl = (tr - wave * RW) * TW + tc;  // this lane's cell among the wave's 64
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            out + (size_t)b * plane * C, 0, (int)(uint32_t)(plane * C * sizeof(float)), 0x00020000);
+#pragma unroll
+        for (int hh = 0; hh < CK / 32; ++hh) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                // four divisions at a time, pinned after the previous group's LDS write (as store_chunk groups its
+                // divisions): no hoisted doubles for all 64 channels, no spills
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = acc[32 * hh + 4 * q + u];
+                asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])::"memory");
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (MODE == BEV_FUSE_MEAN && !(WARP_ABLATE & 1)) v[u] = mean_div(v[u], md);
+                *reinterpret_cast<float4 *>(stg + cl * NS + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int cc = 8 * k + (lane >> 3), pc = lane & 7;
+                const float4 v = *reinterpret_cast<const float4 *>(stg + cc * NS + 4 * pc);
+                const int gi = tyb * TH + wave * RW + cc / TW, gj = txb * TW + cc % TW;
+                if (gi < Hb && gj < Wb)
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(v4i_t, v), rs,
+                        (int)((((size_t)gi * Wb + gj) * C + c0 + 32 * hh) * sizeof(float)) + pc * 16, 0, WARP_STORE_AUX);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (c0 + CK < C) __syncthreads();  // the next chunk stages into the pool
     };
     const Grid grid = make_grid(Hf, Wf);
     const MeanDiv md = mean_div_of(V);  // mean: acc / V (exact)
@@ -1098,7 +1144,8 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         zero_view<MODE>(acc, u);
                     off += stage_bytes(w * (bx.y1 - bx.y0 + 1));
                 }
-                if (inside) store_out(c0, acc, md);
+                if constexpr (NHWC) store_nhwc(c0, acc, md);
+                else if (inside) store_out(c0, acc, md);
                 if (c0 + 64 < C) __syncthreads();  // the next chunk re-stages the pool
                 continue;
             }
@@ -1239,7 +1286,9 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             ++nview;
         }
         STAMP(3);
-        if (inside) {
+        if constexpr (NHWC) {
+            store_nhwc(c0, acc, md);
+        } else if (inside) {
             store_out(c0, acc, md);
         }
         STAMP(4);
@@ -1678,8 +1727,13 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
         hipLaunchKernelGGL(kern, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
                            out, pool, boxes, rpr);
     };
-    const bool ck = rpr < Hb;  // rank-chunk-major output (camera-shard partials)
-    if (mode == BEV_FUSE_SUM)
+    const bool nhwc = rpr == 0;          // channels-last output (bev_ipm_warp_fuse_nhwc_f32)
+    const bool ck = !nhwc && rpr < Hb;  // rank-chunk-major output (camera-shard partials)
+    if (nhwc) {
+        if (mode == BEV_FUSE_SUM) go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, false, true>);
+        else if (mode == BEV_FUSE_MEAN) go(k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, false, true>);
+        else go(k_warp_fuse_v2<BEV_FUSE_MAX, OCC, TH, false, true>);
+    } else if (mode == BEV_FUSE_SUM)
         ck ? go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, true>) : go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, false>);
     else if (mode == BEV_FUSE_MEAN)
         ck ? go(k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, true>) : go(k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, false>);
@@ -1852,6 +1906,14 @@ int bev_ipm_warp_fuse_pre_f32(const float *feats, int64_t sN, int64_t sC, int64_
                           workspace_bytes, stream, true, Hb);
 }
 
+int bev_ipm_warp_fuse_nhwc_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
+                               const float *xs, const float *ys, int B, int V, int C, int Hf, int Wf, float sx,
+                               float sy, int Hb, int Wb, int mode, float *out, void *workspace,
+                               int64_t workspace_bytes, int boxes_ready, void *stream) {
+    return warp_fuse_impl(feats, sN, sC, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb, mode, out, workspace,
+                          workspace_bytes, stream, boxes_ready != 0, 0);
+}
+
 int bev_ipm_warp_fuse_chunked_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW,
                                   const float *Hmat, const float *xs, const float *ys, int B, int V, int C, int Hf,
                                   int Wf, float sx, float sy, int Hb, int Wb, int mode, int rows_per_chunk, float *out,
@@ -1897,7 +1959,12 @@ int warp_fuse_impl(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
                         ((int64_t)Hf * sH < (1ll << 31)) && ((int64_t)Wf * sW < (1ll << 31)) &&
                         (((uintptr_t)feats & 15) == 0) && (sW % 4 == 0) && (sH % 4 == 0) && (sN % 4 == 0) &&
                         (int64_t)Hb * Wb * 64 * (int64_t)sizeof(float) < (1ll << 32);
-    if (rpr != Hb) {  // rank-chunk-major output: the LDS-DMA kernel only, whole output < 2 GiB (per-lane offsets)
+    if (rpr == 0) {  // channels-last output: the LDS-DMA kernel only, a frame's output < 2 GiB (per-lane offsets),
+                     // the parking area (4 waves x 64 cells x 144 B) inside the pool
+        if (!dma_ok || g_warp_kernel == 1 || (int64_t)Hb * Wb * C * (int64_t)sizeof(float) >= (1ll << 31) ||
+            v2_pool_bytes(mode) < 4 * 64 * 36 * (int)sizeof(float))
+            return BEV_ERR_ARGS;
+    } else if (rpr != Hb) {  // rank-chunk-major output: the LDS-DMA kernel only, whole output < 2 GiB (per-lane offsets)
         const int64_t nck = ((int64_t)Hb + rpr - 1) / rpr;
         if (!dma_ok || g_warp_kernel == 1 || nck * rpr * (int64_t)B * C * Wb * (int64_t)sizeof(float) >= (1ll << 31))
             return BEV_ERR_ARGS;

@@ -299,16 +299,26 @@ class GeometryTransformer(nn.Module):
         return out.view(B, V, C, self.bev_h, self.bev_w)
 
     def forward_fused(self, feats: torch.Tensor, intrinsics, extrinsics, img_size: Tuple[int, int] = (1080, 1920),
-                      mode: str = "mean", rows_per_chunk: Optional[int] = None) -> torch.Tensor:
-        """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev].
+                      mode: str = "mean", rows_per_chunk: Optional[int] = None,
+                      memory_format: torch.memory_format = torch.contiguous_format) -> torch.Tensor:
+        """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev] (NCHW storage,
+        as the reference's torch.mean over the stacked views gives).  memory_format=torch.channels_last (inference,
+        channels-last features with C % 64 == 0): the same values in [B,H_bev,W_bev,C] storage
+        (bev_ipm_warp_fuse_nhwc_f32), for a consumer that reads channels-last -- at the bench geometry the launch is
+        ~4 % slower than the NCHW one (profiles/r05as_warp_nhwc_ab.txt), so it is not the default.
         rows_per_chunk (< H_bev, inference only): the same values in rank-chunk-major row order,
         [ceil(H_bev / rows_per_chunk), B, C, rows_per_chunk, W_bev] (padding rows zero) -- the layout the camera-shard
         reduce-scatter over BEV rows consumes without a permute (bev_dist.camera_sharded_forward)."""
         H, xs, ys, hw = self._sampling(feats, intrinsics, extrinsics, img_size)
+        grad = torch.is_grad_enabled() and feats.requires_grad
         if rows_per_chunk is not None and rows_per_chunk < self.bev_h:
-            if torch.is_grad_enabled() and feats.requires_grad:
+            if grad:
                 raise RuntimeError("forward_fused(rows_per_chunk=...) is an inference layout (no autograd)")
             return _nat.warp_fuse(feats, H, xs, ys, hw, mode, rows_per_chunk=rows_per_chunk)
+        C = feats.shape[2]
+        if (not grad and memory_format == torch.channels_last and feats.is_cuda and C % 64 == 0
+                and feats.stride(2) == 1 and feats.shape[1] <= 64):
+            return _nat.warp_fuse(feats, H, xs, ys, hw, mode, channels_last=True)
         return _WarpFuseFn.apply(feats, H, xs, ys, hw, mode)
 
 

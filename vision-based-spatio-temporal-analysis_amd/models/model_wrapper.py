@@ -20,7 +20,6 @@ The computation is reorganised for the GPU:
 * Training targets are built for the whole batch at once (no per-object Python loop / host syncs): gaussian
   splats are one scatter_reduce('amax') over every object's footprint.
 """
-import functools
 import math
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -44,8 +43,6 @@ AMP_FWD_HALF_PANELS = True  # autocast: the projection's forward packs fp16 pane
 # BEVNet.forward queues its decode and returns bev_native.DetectionList sequences that synchronise when first read
 # (A/B: tools/train_step_bench.py --eager-decode)
 LAZY_DECODE = True
-# BEVNet.loss on the GPU replays its loss terms as captured graphs (A/B: tools/train_step_bench.py --no-loss-graph)
-LOSS_GRAPHS = True
 
 
 class _HeadOperand(torch.autograd.Function):
@@ -235,30 +232,11 @@ class BEVNet(nn.Module):
 
     # ---- training objective (model_wrapper.py:105-247) --------------------------
     def loss(self, preds: Dict, targets: List[Dict], loss_cfg: Dict[str, Any]) -> Dict[str, torch.Tensor]:
-        pr = (preds["heatmap_logits"], preds["offset"], preds["size_raw"])
-        if (LOSS_GRAPHS and all(a.is_cuda for a in pr) and torch.is_grad_enabled()
-                and any(a.requires_grad for a in pr)):
-            dev = next(self.parameters()).device
-            boxes, frame, bound = self._target_boxes(targets, dev, pad=True)
-            if bound is not None and boxes.shape[0] > 0:  # host targets: targets + loss terms as one graph pair
-                outs = self._graphed("boxes", (len(targets), bound), pr + (boxes, frame),
-                                     functools.partial(self._loss_from_boxes, B=len(targets), bound=bound))
-            else:
-                t = self._targets_from_boxes(boxes, frame, bound, len(targets))
-                args = pr + (t["heatmap"], t["indices"], t["mask"], t["offset"], t["size_log"])
-                outs = self._graphed("terms", (), args, self._loss_terms)
-            # the graph's outputs live in its static buffers (overwritten by the next replay): one stack copies them
-            hm_loss, off_loss, size_loss, total = torch.stack(outs).unbind(0)
-        else:
-            t = self._build_training_targets(targets)
-            hm_loss, off_loss, size_loss, total = self._loss_terms(
-                *pr, t["heatmap"], t["indices"], t["mask"], t["offset"], t["size_log"])
+        t = self._build_training_targets(targets)
+        hm_loss, off_loss, size_loss, total = self._loss_terms(
+            preds["heatmap_logits"], preds["offset"], preds["size_raw"], t["heatmap"], t["indices"], t["mask"],
+            t["offset"], t["size_log"])
         return {"heatmap_loss": hm_loss, "offset_loss": off_loss, "size_loss": size_loss, "total_loss": total}
-
-    def _loss_from_boxes(self, logits, offset, size_raw, boxes, frame, B: int, bound: int):
-        t = self._targets_from_boxes(boxes, frame, bound, B)
-        return self._loss_terms(logits, offset, size_raw, t["heatmap"], t["indices"], t["mask"], t["offset"],
-                                t["size_log"])
 
     def _loss_terms(self, logits, offset, size_raw, hm, indices, mask, off_t, size_t):
         """model_wrapper.py:105-124: the focal heatmap loss and the masked L1 offset / log-size losses."""
@@ -270,28 +248,7 @@ class BEVNet(nn.Module):
         total = self.hm_weight * hm_loss + self.offset_weight * off_loss + self.size_weight * size_loss
         return hm_loss, off_loss, size_loss, total
 
-    def _graphed(self, kind: str, extra: tuple, args, fn):
-        """`fn(*args)` captured as a HIP graph pair (forward, backward) per input signature
-        (torch.cuda.make_graphed_callables) and replayed: a training step runs the ~100 small elementwise /
-        reduction launches of the loss terms -- and, for targets handed over in host memory, the ~150 of the target
-        construction (boxes padded to a multiple of 16 by out-of-grid dummies, see _target_boxes) -- as two graph
-        launches plus the input copies, so the loss no longer leaves the GPU waiting on the host between the
-        forward and the backward.  The graphs run the same kernels on the same values: identical results
-        (tests/test_targets.py::test_graphed_loss_identical).  Captured with autocast off -- every input is fp32
-        and every op of the loss runs in fp32 under autocast(float16) as well."""
-        key = (kind, extra) + tuple((tuple(a.shape), a.dtype, a.requires_grad, a.device) for a in args)
-        key += (self.hm_weight, self.offset_weight, self.size_weight, self.hm_alpha, self.hm_beta, self.max_objects)
-        graphs = self.__dict__.setdefault("_loss_graphs", {})
-        g = graphs.get(key)
-        if g is None:
-            samples = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
-            with torch.autocast("cuda", enabled=False):
-                g = torch.cuda.make_graphed_callables(fn, samples, allow_unused_input=True)
-            graphs[key] = g
-        return g(*args)
-
-    def _target_boxes(self, targets: List[Dict], dev, pad: bool = False
-                      ) -> Tuple[torch.Tensor, torch.Tensor, Optional[int]]:
+    def _target_boxes(self, targets: List[Dict], dev) -> Tuple[torch.Tensor, torch.Tensor, Optional[int]]:
         """All frames' boxes [N, 4] (cx, cy, w, h; centre-only targets get DEFAULT_BOX_WH) + frame index [N] on
         `dev`, and an upper bound of the objects' gaussian radii when it is known without waiting for the device.
         The reference's loader hands the targets over in host memory (train.py:228-243 moves only the images and
@@ -316,12 +273,6 @@ class BEVNet(nn.Module):
         if all(not t.is_cuda for t in boxes):
             bh, fh = torch.cat(boxes), torch.cat(frame)
             bound = self._radius_bound_host(bh)
-            if pad and bh.shape[0] % 16:  # out-of-grid dummies of the last frame: no slot, no gaussian
-                x_min, _, y_min, _ = self.bounds
-                n = 16 - bh.shape[0] % 16
-                dummy = bh.new_tensor([x_min - 1e6 * self.res_x, y_min - 1e6 * self.res_y, self.res_x, self.res_y])
-                bh = torch.cat([bh, dummy.expand(n, 4)])
-                fh = torch.cat([fh, fh.new_full((n,), len(targets) - 1)])
             if dev.type == "cuda":
                 bh, fh = bh.pin_memory(), fh.pin_memory()
             return bh.to(dev, non_blocking=True), fh.to(dev, non_blocking=True), bound
@@ -393,7 +344,7 @@ class BEVNet(nn.Module):
         offset = torch.zeros(B, M + 1, 2, device=dev)
         size_log = torch.zeros(B, M + 1, 2, device=dev)
         indices[frame, s] = cyl * Wb + cxl
-        mask[frame, s] = torch.ones((), device=dev)  # a device value: no host-to-device copy (graph capture)
+        mask[frame, s] = 1.0
         offset[frame, s] = torch.stack([gx - cx, gy - cy], dim=1)
         size_log[frame, s] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
         self._splat_gaussians(hm_ext, frame, cxl, cyl, self._gaussian_radius_tensor(w_cells, h_cells), sel, bound,
