@@ -379,6 +379,16 @@ int bev_conv_wgrad_f32(const float *x, int N, int H, int W, int Ci, const float 
 
 /* db [C] (OVERWRITTEN) = sum over m of dz[m][c] (bias / BN-shift gradient). */
 int bev_colsum_f32(const float *dz, int64_t M, int C, float *db, void *stream);
+/* CenterNet penalty-reduced focal heatmap loss of model_wrapper.py:235-247 (BEVNet._heatmap_focal_loss) over n cells:
+ * p = clamp(sigmoid(logits), 1e-4, 1 - 1e-4), loss[0] = -(sum_{gt == 1} log p (1-p)^alpha + sum_{gt < 1} log(1-p)
+ * p^alpha (1-gt)^beta) / max(#{gt == 1}, 1) (fp32 terms, double sums), inv_norm[0] = 1 / max(#{gt == 1}, 1) for the
+ * backward; workspace >= bev_focal_loss_workspace_bytes(n).  Backward: dlogits = -grad_loss[0] * inv_norm[0] *
+ * d(terms)/dp * sigmoid', torch's clamp rule (no gradient where sigmoid(x) is outside [1e-4, 1 - 1e-4]). */
+int64_t bev_focal_loss_workspace_bytes(int64_t n);
+int bev_focal_loss_fwd_f32(const float *logits, const float *gt, int64_t n, float alpha, float beta, float *loss,
+                           float *inv_norm, void *workspace, int64_t workspace_bytes, void *stream);
+int bev_focal_loss_bwd_f32(const float *logits, const float *gt, int64_t n, float alpha, float beta,
+                           const float *grad_loss, const float *inv_norm, float *dlogits, void *stream);
 
 /* dx [N][H][W][C] (OVERWRITTEN): max-pool backward with ATen's window argmax rule
  * (first maximum in scan order, NaN wins). */

@@ -115,3 +115,36 @@ def test_targets_host_and_device_boxes_identical_and_lazy_decode():
     for a, b in zip(list(lb) + list(ls), eb + es):
         assert torch.equal(a, b)
 
+
+
+@pytest.mark.gpu
+def test_native_focal_loss_vs_float64_torch():
+    """The native focal heatmap loss (bev_focal_loss_fwd_f32 / _bwd_f32, BEVNet._heatmap_focal_loss on the GPU) vs
+    the torch composition (model_wrapper.py:235-247) in float64: the loss and the logits' gradient, with saturated
+    logits on both sides of the clamp (no gradient there, torch's clamp rule)."""
+    import models.model_wrapper as mw
+    dev = torch.device("cuda:0")
+    net = BEVNet(CFG).to(dev)
+    g = torch.Generator().manual_seed(9)
+    tg = _random_targets(g, 0)
+    while not any("boxes_world" in t for t in tg):
+        tg = _random_targets(g, 0)
+    hm = net._build_training_targets(tg)["heatmap"]
+    logits = torch.randn(hm.shape, generator=g) * 3
+    logits.view(-1)[:40] = 20.0
+    logits.view(-1)[40:80] = -20.0
+    x = logits.to(dev).requires_grad_(True)
+    x64 = logits.double().requires_grad_(True)
+    try:
+        mw.NATIVE_FOCAL = True
+        ln = net._heatmap_focal_loss(x, hm)
+        (gn,) = torch.autograd.grad(ln * 1.7, x)
+        mw.NATIVE_FOCAL = False
+        lr = net._heatmap_focal_loss(x64, hm.double().cpu())
+        (gr,) = torch.autograd.grad(lr * 1.7, x64)
+    finally:
+        mw.NATIVE_FOCAL = True
+    assert abs(float(ln) - float(lr)) <= 1e-5 * abs(float(lr)), (float(ln), float(lr))
+    gn = gn.double().cpu()
+    assert float(gn.view(-1)[:80].abs().max()) == 0.0
+    torch.testing.assert_close(gn, gr, rtol=1e-4, atol=1e-5 * float(gr.abs().max()))

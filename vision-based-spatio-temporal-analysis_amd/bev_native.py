@@ -57,6 +57,9 @@ SIGNATURES = {
     "bev_head_operand_bwd_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_head_operand_bwd_bias_partials": (_i64, [_i, _i, _i, _i]),
     "bev_head_operand_bwd_bias_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "bev_focal_loss_workspace_bytes": (_i64, [_i64]),
+    "bev_focal_loss_fwd_f32": (_i, [_vp, _vp, _i64, _f, _f, _vp, _vp, _vp, _i64, _vp]),
+    "bev_focal_loss_bwd_f32": (_i, [_vp, _vp, _i64, _f, _f, _vp, _vp, _vp, _vp]),
     "bev_ipm_warp_fuse_nhwc_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
                                         _i, _i, _vp, _vp, _i64, _i, _vp]),
     "bev_ipm_warp_fuse_chunked_f32": (_i, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i, _i, _i, _i, _i, _f, _f, _i,
@@ -1417,6 +1420,31 @@ def decode(heatmap: torch.Tensor, offset: torch.Tensor, size: torch.Tensor, boun
         return finish()
     pending = _PendingDecode(finish)
     return DetectionList(pending, 0), DetectionList(pending, 1)
+
+
+def focal_loss(logits: torch.Tensor, gt: torch.Tensor, alpha: float, beta: float):
+    """CenterNet focal heatmap loss (model_wrapper.py:235-247) over same-shaped fp32 logits / gt on the device ->
+    (loss [] fp32, inv_norm [1] = 1 / max(#peaks, 1) for focal_loss_bwd)."""
+    logits, gt = logits.contiguous(), gt.contiguous()
+    _require_gpu(logits, gt)
+    if logits.dtype != torch.float32 or gt.dtype != torch.float32 or logits.shape != gt.shape:
+        raise HipError("focal_loss: fp32 logits / gt of one shape")
+    n = logits.numel()
+    ws = torch.empty(lib().bev_focal_loss_workspace_bytes(n), device=logits.device, dtype=torch.uint8)
+    loss = torch.empty((), device=logits.device, dtype=torch.float32)
+    inv = torch.empty(1, device=logits.device, dtype=torch.float32)
+    _check(lib().bev_focal_loss_fwd_f32(_ptr(logits), _ptr(gt), n, float(alpha), float(beta), _ptr(loss), _ptr(inv),
+                                        _ptr(ws), ws.numel(), _stream(logits)), "bev_focal_loss_fwd_f32")
+    return loss, inv
+
+
+def focal_loss_bwd(logits, gt, alpha: float, beta: float, grad_loss: torch.Tensor, inv: torch.Tensor) -> torch.Tensor:
+    logits, gt, grad_loss = logits.contiguous(), gt.contiguous(), grad_loss.contiguous().float()
+    _require_gpu(logits, gt, grad_loss, inv)
+    dx = torch.empty_like(logits)
+    _check(lib().bev_focal_loss_bwd_f32(_ptr(logits), _ptr(gt), logits.numel(), float(alpha), float(beta),
+                                        _ptr(grad_loss), _ptr(inv), _ptr(dx), _stream(logits)), "bev_focal_loss_bwd_f32")
+    return dx
 
 
 DECODE_SORT_CHUNK = 8192  # keys per LDS chunk of the large-path sort (bev_decode.hip SORT_CHUNK)

@@ -591,3 +591,126 @@ int bev_head_operand_bwd_f32(const float *gx, int B, int P, int Hb, int Wb, int 
 }
 
 }  // extern "C"
+
+// ---- CenterNet focal heatmap loss (model_wrapper.py:235-247) -------------------------------------------------------
+// p = clamp(sigmoid(x), 1e-4, 1 - 1e-4); pos = log p (1 - p)^a where gt == 1, neg = log(1 - p) p^a (1 - gt)^b where
+// gt < 1; loss = -(sum pos + sum neg) / max(#(gt == 1), 1).  Forward: per-block partial sums in double, one finalize
+// block (loss, and 1 / max(npos, 1) kept on the device for the backward); backward: dx = -g inv d(pos + neg)/dp dp/dx
+// with torch's clamp rule (gradient where 1e-4 <= sigmoid(x) <= 1 - 1e-4) and sigmoid'(x) = s (1 - s).  Two launches
+// forward and one backward instead of torch's ~60 elementwise / reduction launches for the same loss (a training step
+// runs them at the host's launch pace, between the head's forward and its backward).
+namespace {
+constexpr int FL_T = 256, FL_MAXB = 1024;
+
+__device__ __forceinline__ float fl_p(float x, float &s) {
+    s = 1.0f / (1.0f + expf(-x));
+    const float lo = (float)1e-4, hi = (float)(1.0 - 1e-4);
+    return fminf(fmaxf(s, lo), hi);
+}
+
+__device__ __forceinline__ double fl_block_sum(double v, double *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(FL_T) void k_focal_partial(const float *__restrict__ x, const float *__restrict__ gt,
+                                                        int64_t n, float alpha, float beta, double *__restrict__ part) {
+    __shared__ double red[4];
+    double sp = 0.0, sn = 0.0, np = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * FL_T + threadIdx.x; i < n; i += (int64_t)gridDim.x * FL_T) {
+        float s;
+        const float p = fl_p(x[i], s), g = gt[i];
+        if (g == 1.0f) {
+            sp += (double)(logf(p) * powf(1.0f - p, alpha));
+            np += 1.0;
+        }
+        if (g < 1.0f) sn += (double)(logf(1.0f - p) * powf(p, alpha) * powf(1.0f - g, beta));
+    }
+    sp = fl_block_sum(sp, red);
+    sn = fl_block_sum(sn, red);
+    np = fl_block_sum(np, red);
+    if (threadIdx.x == 0) {
+        part[3 * blockIdx.x] = sp;
+        part[3 * blockIdx.x + 1] = sn;
+        part[3 * blockIdx.x + 2] = np;
+    }
+}
+
+__global__ __launch_bounds__(FL_T) void k_focal_finalize(const double *__restrict__ part, int nb, float *__restrict__ loss,
+                                                         float *__restrict__ inv) {
+    __shared__ double red[4];
+    double sp = 0.0, sn = 0.0, np = 0.0;
+    for (int b = threadIdx.x; b < nb; b += FL_T) {
+        sp += part[3 * b];
+        sn += part[3 * b + 1];
+        np += part[3 * b + 2];
+    }
+    sp = fl_block_sum(sp, red);
+    sn = fl_block_sum(sn, red);
+    np = fl_block_sum(np, red);
+    if (threadIdx.x == 0) {
+        const double den = np > 1.0 ? np : 1.0;
+        loss[0] = (float)(-(sp + sn) / den);
+        inv[0] = (float)(1.0 / den);
+    }
+}
+
+__global__ __launch_bounds__(FL_T) void k_focal_bwd(const float *__restrict__ x, const float *__restrict__ gt, int64_t n,
+                                                    float alpha, float beta, const float *__restrict__ gout,
+                                                    const float *__restrict__ inv, float *__restrict__ dx) {
+    const float scale = -gout[0] * inv[0];
+    const float lo = (float)1e-4, hi = (float)(1.0 - 1e-4);
+    for (int64_t i = (int64_t)blockIdx.x * FL_T + threadIdx.x; i < n; i += (int64_t)gridDim.x * FL_T) {
+        float s;
+        const float p = fl_p(x[i], s), g = gt[i];
+        float d = 0.0f;
+        if (g == 1.0f) d += powf(1.0f - p, alpha) / p - alpha * logf(p) * powf(1.0f - p, alpha - 1.0f);
+        if (g < 1.0f) {
+            const float w = powf(1.0f - g, beta);
+            d += -powf(p, alpha) * w / (1.0f - p) + alpha * logf(1.0f - p) * powf(p, alpha - 1.0f) * w;
+        }
+        const float dp = (s >= lo && s <= hi) ? s * (1.0f - s) : 0.0f;
+        dx[i] = scale * d * dp;
+    }
+}
+
+inline int fl_blocks(int64_t n) {
+    const int64_t b = (n + FL_T - 1) / FL_T;
+    return (int)(b < FL_MAXB ? (b > 0 ? b : 1) : FL_MAXB);
+}
+}  // namespace
+
+extern "C" {
+
+int64_t bev_focal_loss_workspace_bytes(int64_t n) {
+    if (n < 0) return BEV_ERR_ARGS;
+    return (int64_t)fl_blocks(n) * 3 * (int64_t)sizeof(double);
+}
+
+int bev_focal_loss_fwd_f32(const float *logits, const float *gt, int64_t n, float alpha, float beta, float *loss,
+                           float *inv_norm, void *workspace, int64_t workspace_bytes, void *stream) {
+    if (!logits || !gt || !loss || !inv_norm || !workspace || n < 0 ||
+        workspace_bytes < bev_focal_loss_workspace_bytes(n))
+        return BEV_ERR_ARGS;
+    const int nb = fl_blocks(n);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_focal_partial, dim3(nb), dim3(FL_T), 0, st, logits, gt, n, alpha, beta, (double *)workspace);
+    hipLaunchKernelGGL(k_focal_finalize, dim3(1), dim3(FL_T), 0, st, (const double *)workspace, nb, loss, inv_norm);
+    return (int)hipGetLastError();
+}
+
+int bev_focal_loss_bwd_f32(const float *logits, const float *gt, int64_t n, float alpha, float beta,
+                           const float *grad_loss, const float *inv_norm, float *dlogits, void *stream) {
+    if (!logits || !gt || !grad_loss || !inv_norm || !dlogits || n < 0) return BEV_ERR_ARGS;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_focal_bwd, dim3(fl_blocks(n)), dim3(FL_T), 0, (hipStream_t)stream, logits, gt, n, alpha, beta,
+                       grad_loss, inv_norm, dlogits);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

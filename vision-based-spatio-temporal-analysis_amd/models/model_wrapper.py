@@ -45,6 +45,29 @@ AMP_FWD_HALF_PANELS = True  # autocast: the projection's forward packs fp16 pane
 LAZY_DECODE = True
 
 
+# BEVNet._heatmap_focal_loss on the GPU runs the native loss (A/B: tools/train_step_bench.py --torch-focal)
+NATIVE_FOCAL = True
+
+
+class _FocalLoss(torch.autograd.Function):
+    """The focal heatmap loss (model_wrapper.py:235-247) on the native kernels; gradient for the logits only (the
+    heatmap targets carry none)."""
+
+    @staticmethod
+    @_nat.amp_fwd
+    def forward(ctx, logits, gt, alpha: float, beta: float):
+        loss, inv = _nat.focal_loss(logits, gt, alpha, beta)
+        ctx.save_for_backward(logits, gt, inv)
+        ctx.ab = (alpha, beta)
+        return loss
+
+    @staticmethod
+    @_nat.amp_bwd
+    def backward(ctx, g):
+        logits, gt, inv = ctx.saved_tensors
+        return _nat.focal_loss_bwd(logits, gt, *ctx.ab, g.reshape(1), inv), None, None, None
+
+
 class _HeadOperand(torch.autograd.Function):
     """x [B,Hb,Wb,cp] channels-last head operand = (s + bias, pos_enc, zeros) per cell (model_wrapper.py:69-75: the
     BEV projection's bias add and the pos-enc concat), s [B,P,Hb,Wb] the fused warp-sum of the projected views: one
@@ -398,7 +421,11 @@ class BEVNet(nn.Module):
         return torch.floor(r).to(torch.long)
 
     def _heatmap_focal_loss(self, pred_logits: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
-        """Penalty-reduced focal loss (model_wrapper.py:235-247), normalised by the number of gt peaks."""
+        """Penalty-reduced focal loss (model_wrapper.py:235-247), normalised by the number of gt peaks.  On the GPU:
+        bev_focal_loss_fwd_f32 / _bwd_f32 (three launches for forward + backward instead of ~60 small torch ones;
+        fp32 terms, double sums, so within fp32 rounding of the torch composition)."""
+        if NATIVE_FOCAL and pred_logits.is_cuda and gt.is_cuda:
+            return _FocalLoss.apply(pred_logits.float(), gt.float(), float(self.hm_alpha), float(self.hm_beta))
         p = torch.sigmoid(pred_logits).clamp(1e-4, 1 - 1e-4)
         peak = gt == 1.0
         pos = torch.where(peak, p.log() * (1 - p).pow(self.hm_alpha), torch.zeros_like(p))
