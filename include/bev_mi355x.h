@@ -384,6 +384,18 @@ int bev_colsum_f32(const float *dz, int64_t M, int C, float *db, void *stream);
  * p^alpha (1-gt)^beta) / max(#{gt == 1}, 1) (fp32 terms, double sums), inv_norm[0] = 1 / max(#{gt == 1}, 1) for the
  * backward; workspace >= bev_focal_loss_workspace_bytes(n).  Backward: dlogits = -grad_loss[0] * inv_norm[0] *
  * d(terms)/dp * sigmoid', torch's clamp rule (no gradient where sigmoid(x) is outside [1e-4, 1 - 1e-4]). */
+/* CenterNet masked L1 losses of model_wrapper.py:109-116 (BEVNet.loss): offset / size [B][2][HW] fp32 (NCHW maps),
+ * indices [B][ld] int64 cell ids, mask [B][ld], off_t / size_t [B][ld][2] (the first M slots of rows of ld):
+ * out[0] = sum |offset[b][c][idx] - off_t| m / n, out[1] = the same on size / size_t, out[2] = 1 / n,
+ * n = sum m + 1e-4 (fp32 terms, double sums).  Backward: d_offset / d_size (zeroed by the caller) += g sign(x) m / n
+ * at the gathered cells (torch's abs rule), grad_losses = the two losses' gradients. */
+int bev_l1_losses_fwd_f32(const float *offset, const float *size, int B, int64_t HW, const int64_t *indices,
+                          const float *mask, const float *off_t, const float *size_t_, int M, int ld, float *out,
+                          void *stream);
+int bev_l1_losses_bwd_f32(const float *offset, const float *size, int B, int64_t HW, const int64_t *indices,
+                          const float *mask, const float *off_t, const float *size_t_, int M, int ld,
+                          const float *grad_losses, const float *fwd_out, float *d_offset, float *d_size,
+                          void *stream);
 int64_t bev_focal_loss_workspace_bytes(int64_t n);
 int bev_focal_loss_fwd_f32(const float *logits, const float *gt, int64_t n, float alpha, float beta, float *loss,
                            float *inv_norm, void *workspace, int64_t workspace_bytes, void *stream);

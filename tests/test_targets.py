@@ -136,15 +136,49 @@ def test_native_focal_loss_vs_float64_torch():
     x = logits.to(dev).requires_grad_(True)
     x64 = logits.double().requires_grad_(True)
     try:
-        mw.NATIVE_FOCAL = True
+        mw.NATIVE_LOSS = True
         ln = net._heatmap_focal_loss(x, hm)
         (gn,) = torch.autograd.grad(ln * 1.7, x)
-        mw.NATIVE_FOCAL = False
+        mw.NATIVE_LOSS = False
         lr = net._heatmap_focal_loss(x64, hm.double().cpu())
         (gr,) = torch.autograd.grad(lr * 1.7, x64)
     finally:
-        mw.NATIVE_FOCAL = True
+        mw.NATIVE_LOSS = True
     assert abs(float(ln) - float(lr)) <= 1e-5 * abs(float(lr)), (float(ln), float(lr))
     gn = gn.double().cpu()
     assert float(gn.view(-1)[:80].abs().max()) == 0.0
     torch.testing.assert_close(gn, gr, rtol=1e-4, atol=1e-5 * float(gr.abs().max()))
+
+
+@pytest.mark.gpu
+def test_native_l1_losses_vs_float64_torch():
+    """The native masked L1 offset / log-size losses (bev_l1_losses_fwd_f32 / _bwd_f32, BEVNet._loss_terms on the
+    GPU) vs the torch composition (model_wrapper.py:109-116) in float64: both losses and the gradients of the offset
+    and size maps, with two objects in one cell (their gradients add) and empty slots."""
+    import models.model_wrapper as mw
+    dev = torch.device("cuda:0")
+    net = BEVNet(CFG).to(dev)
+    g = torch.Generator().manual_seed(11)
+    tg = [{"boxes_world": torch.tensor([[1.0, 0.5, 0.6, 0.6], [1.0, 0.5, 0.9, 0.7], [-3.0, 2.0, 0.6, 0.6]])},
+          {"boxes_world": torch.tensor([[5.0, -1.0, 1.2, 0.4]])}]
+    t = net._build_training_targets(tg)
+    off = torch.rand(2, 2, 60, 180, generator=g)
+    size = torch.randn(2, 2, 60, 180, generator=g)
+    res = {}
+    for native in (True, False):
+        o = (off.to(dev) if native else off.double()).requires_grad_(True)
+        s = (size.to(dev) if native else size.double()).requires_grad_(True)
+        tt = t if native else {k: (v.cpu().double() if v.is_floating_point() else v.cpu()) for k, v in t.items()}
+        try:
+            mw.NATIVE_LOSS = native
+            _, lo, ls, _ = net._loss_terms(torch.zeros_like(o[:, :1]), o, s, torch.zeros_like(o[:, :1]),
+                                           tt["indices"], tt["mask"], tt["offset"], tt["size_log"])
+            go, gs = torch.autograd.grad(1.3 * lo + 0.7 * ls, (o, s))
+        finally:
+            mw.NATIVE_LOSS = True
+        res[native] = (float(lo), float(ls), go.double().cpu(), gs.double().cpu())
+    for a, b in zip(res[True][:2], res[False][:2]):
+        assert abs(a - b) <= 1e-5 * abs(b), (a, b)
+    for a, b in zip(res[True][2:], res[False][2:]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+    assert float(res[True][2].abs().sum()) > 0

@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=V", help="bev_tune knob (A/B); repeatable")
     ap.add_argument("--no-mask-bytes", action="store_true", help="A/B: bn3's backward re-reads the fp32 block output "
                     "instead of the forward's ReLU mask bytes (trunk_grad.RELU_MASK_BYTES)")
-    ap.add_argument("--torch-focal", action="store_true", help="A/B: the focal loss as torch ops")
+    ap.add_argument("--torch-loss", action="store_true", help="A/B: the focal and L1 losses as torch ops")
     ap.add_argument("--eager-decode", action="store_true", help="A/B: BEVNet.forward synchronises on its decode")
     ap.add_argument("--device-targets", action="store_true", help="A/B: the targets already on the device (the "
                     "reference's loop, train.py:228-243, leaves them in host memory)")
@@ -52,7 +52,7 @@ def main():
         trunk_grad.MAXPOOL_ARG = False
     import models.model_wrapper as _mw
     _mw.LAZY_DECODE = not a.eager_decode
-    _mw.NATIVE_FOCAL = not a.torch_focal
+    _mw.NATIVE_LOSS = not a.torch_loss
     for kv in a.tune:
         name, v = kv.split("=")
         bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))
@@ -126,7 +126,7 @@ def main():
                       "tune": a.tune, "bev": [480, 1440], "cameras": V, "img": [H, W], "feat_dim": 64,
                       "bev_proj_ch": a.proj_ch if a.bevnet else None,
                       "amp": a.amp, "half_convs": a.amp and not a.fp32_kernels,
-                      "decode": "eager" if a.eager_decode else "lazy", "focal": "torch" if a.torch_focal else "native",
+                      "decode": "eager" if a.eager_decode else "lazy", "loss_impl": "torch" if a.torch_loss else "native",
                       "targets": "device" if a.device_targets else "host",
                       "ms_per_step": round(dt * 1e3, 2), "frames_per_s": round(1.0 / dt, 3),
                       "loss": float(loss)}), flush=True)

@@ -57,6 +57,8 @@ SIGNATURES = {
     "bev_head_operand_bwd_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "bev_head_operand_bwd_bias_partials": (_i64, [_i, _i, _i, _i]),
     "bev_head_operand_bwd_bias_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "bev_l1_losses_fwd_f32": (_i, [_vp, _vp, _i, _i64, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
+    "bev_l1_losses_bwd_f32": (_i, [_vp, _vp, _i, _i64, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "bev_focal_loss_workspace_bytes": (_i64, [_i64]),
     "bev_focal_loss_fwd_f32": (_i, [_vp, _vp, _i64, _f, _f, _vp, _vp, _vp, _i64, _vp]),
     "bev_focal_loss_bwd_f32": (_i, [_vp, _vp, _i64, _f, _f, _vp, _vp, _vp, _vp]),
@@ -1445,6 +1447,46 @@ def focal_loss_bwd(logits, gt, alpha: float, beta: float, grad_loss: torch.Tenso
     _check(lib().bev_focal_loss_bwd_f32(_ptr(logits), _ptr(gt), logits.numel(), float(alpha), float(beta),
                                         _ptr(grad_loss), _ptr(inv), _ptr(dx), _stream(logits)), "bev_focal_loss_bwd_f32")
     return dx
+
+
+def _l1_operands(offset, size, indices, mask, off_t, size_t):
+    """The L1 losses' slot operands as rows of a common length ld (the targets' [B, M + 1] buffers viewed [:, :M])."""
+    B, M = indices.shape
+    ld = indices.stride(0)
+    ok = (indices.stride(1) == 1 and mask.stride() == (ld, 1) and off_t.stride() == (2 * ld, 2, 1)
+          and size_t.stride() == (2 * ld, 2, 1) and indices.dtype == torch.int64 and mask.dtype == torch.float32
+          and off_t.dtype == torch.float32 and size_t.dtype == torch.float32)
+    if not ok:
+        indices, mask = indices.contiguous().long(), mask.contiguous().float()
+        off_t, size_t, ld = off_t.contiguous().float(), size_t.contiguous().float(), M
+    offset, size = offset.contiguous().float(), size.contiguous().float()
+    _require_gpu(offset, size, mask, off_t, size_t)
+    if not indices.is_cuda or indices.device != offset.device:
+        raise HipError("l1_losses: indices must be an int64 tensor on the maps' device")
+    if offset.shape != size.shape or offset.shape[:2] != (B, 2):
+        raise HipError("l1_losses: offset / size [B, 2, H, W]")
+    return offset, size, indices, mask, off_t, size_t, B, M, ld, offset.shape[2] * offset.shape[3]
+
+
+def l1_losses(offset, size, indices, mask, off_t, size_t) -> torch.Tensor:
+    """model_wrapper.py:109-116's masked L1 offset / log-size losses on the device -> [3] = (offset loss, size loss,
+    1 / n) (bev_l1_losses_fwd_f32)."""
+    o, sz, idx, m, ot, st, B, M, ld, HW = _l1_operands(offset, size, indices, mask, off_t, size_t)
+    out = torch.empty(3, device=o.device, dtype=torch.float32)
+    _check(lib().bev_l1_losses_fwd_f32(_ptr(o), _ptr(sz), B, HW, _ptr(idx), _ptr(m), _ptr(ot), _ptr(st), M, ld,
+                                       _ptr(out), _stream(o)), "bev_l1_losses_fwd_f32")
+    return out
+
+
+def l1_losses_bwd(offset, size, indices, mask, off_t, size_t, grad_losses, fwd_out):
+    o, sz, idx, m, ot, st, B, M, ld, HW = _l1_operands(offset, size, indices, mask, off_t, size_t)
+    d_off, d_sz = torch.zeros_like(o), torch.zeros_like(sz)
+    g = grad_losses.contiguous().float()
+    _require_gpu(g, fwd_out)
+    _check(lib().bev_l1_losses_bwd_f32(_ptr(o), _ptr(sz), B, HW, _ptr(idx), _ptr(m), _ptr(ot), _ptr(st), M, ld,
+                                       _ptr(g), _ptr(fwd_out), _ptr(d_off), _ptr(d_sz), _stream(o)),
+           "bev_l1_losses_bwd_f32")
+    return d_off, d_sz
 
 
 DECODE_SORT_CHUNK = 8192  # keys per LDS chunk of the large-path sort (bev_decode.hip SORT_CHUNK)

@@ -714,3 +714,86 @@ int bev_focal_loss_bwd_f32(const float *logits, const float *gt, int64_t n, floa
 }
 
 }  // extern "C"
+
+// ---- CenterNet L1 offset / log-size losses (model_wrapper.py:109-116) ---------------------------------------------
+// off = sum_{b,k,c} |offset[b][c][idx[b][k]] - off_t[b][k][c]| m[b][k] / n, size likewise on size_raw / size_t,
+// n = sum m + 1e-4 (fp32 terms, double sums): one workgroup over the B x M slots.  Backward: the gathers' gradients
+// scattered back, g sign(x) m / n (torch's abs rule, sign(0) = 0), added per cell (two objects may share one).
+namespace {
+__global__ __launch_bounds__(FL_T) void k_l1_fwd(const float *__restrict__ off, const float *__restrict__ sz, int64_t HW,
+                                                 const int64_t *__restrict__ idx, const float *__restrict__ m,
+                                                 const float *__restrict__ offt, const float *__restrict__ szt, int B,
+                                                 int M, int ldi, float *__restrict__ out) {
+    __shared__ double red[4];
+    double so = 0.0, ss = 0.0, sm = 0.0;
+    for (int e = threadIdx.x; e < B * M; e += FL_T) {
+        const int b = e / M, k = e - b * M;
+        const float mk = m[(int64_t)b * ldi + k];
+        const int64_t i = idx[(int64_t)b * ldi + k];
+        sm += (double)mk;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int64_t t = ((int64_t)b * ldi + k) * 2 + c;
+            so += (double)fabsf((off[((int64_t)b * 2 + c) * HW + i] - offt[t]) * mk);
+            ss += (double)fabsf((sz[((int64_t)b * 2 + c) * HW + i] - szt[t]) * mk);
+        }
+    }
+    so = fl_block_sum(so, red);
+    ss = fl_block_sum(ss, red);
+    sm = fl_block_sum(sm, red);
+    if (threadIdx.x == 0) {
+        const float n = (float)sm + 1e-4f;  // torch: m.sum() (fp32) + 1e-4
+        out[0] = (float)(so / (double)n);
+        out[1] = (float)(ss / (double)n);
+        out[2] = 1.0f / n;
+    }
+}
+
+__global__ __launch_bounds__(FL_T) void k_l1_bwd(const float *__restrict__ off, const float *__restrict__ sz, int64_t HW,
+                                                 const int64_t *__restrict__ idx, const float *__restrict__ m,
+                                                 const float *__restrict__ offt, const float *__restrict__ szt, int B,
+                                                 int M, int ldi, const float *__restrict__ gl,
+                                                 const float *__restrict__ fwd, float *__restrict__ doff,
+                                                 float *__restrict__ dsz) {
+    const float go = gl[0] * fwd[2], gs = gl[1] * fwd[2];
+    for (int e = blockIdx.x * FL_T + threadIdx.x; e < B * M * 2; e += gridDim.x * FL_T) {
+        const int c = e & 1, bk = e >> 1, b = bk / M, k = bk - b * M;
+        const float mk = m[(int64_t)b * ldi + k];
+        if (mk == 0.0f) continue;
+        const int64_t i = idx[(int64_t)b * ldi + k];
+        const int64_t t = ((int64_t)b * ldi + k) * 2 + c, o = ((int64_t)b * 2 + c) * HW + i;
+        const float xo = (off[o] - offt[t]) * mk, xs = (sz[o] - szt[t]) * mk;
+        const float so = xo > 0.0f ? 1.0f : (xo < 0.0f ? -1.0f : 0.0f), ss = xs > 0.0f ? 1.0f : (xs < 0.0f ? -1.0f : 0.0f);
+        atomicAdd(doff + o, go * so * mk);
+        atomicAdd(dsz + o, gs * ss * mk);
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int bev_l1_losses_fwd_f32(const float *offset, const float *size, int B, int64_t HW, const int64_t *indices,
+                          const float *mask, const float *off_t, const float *size_t_, int M, int ld, float *out,
+                          void *stream) {
+    if (!offset || !size || !indices || !mask || !off_t || !size_t_ || !out || B < 0 || M < 0 || ld < M || HW <= 0)
+        return BEV_ERR_ARGS;
+    hipLaunchKernelGGL(k_l1_fwd, dim3(1), dim3(FL_T), 0, (hipStream_t)stream, offset, size, HW, indices, mask, off_t,
+                       size_t_, B, M, ld, out);
+    return (int)hipGetLastError();
+}
+
+int bev_l1_losses_bwd_f32(const float *offset, const float *size, int B, int64_t HW, const int64_t *indices,
+                          const float *mask, const float *off_t, const float *size_t_, int M, int ld,
+                          const float *grad_losses, const float *fwd_out, float *d_offset, float *d_size,
+                          void *stream) {
+    if (!offset || !size || !indices || !mask || !off_t || !size_t_ || !grad_losses || !fwd_out || !d_offset ||
+        !d_size || B < 0 || M < 0 || ld < M || HW <= 0)
+        return BEV_ERR_ARGS;
+    const int n = B * M * 2;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_l1_bwd, dim3((n + FL_T - 1) / FL_T), dim3(FL_T), 0, (hipStream_t)stream, offset, size, HW,
+                       indices, mask, off_t, size_t_, B, M, ld, grad_losses, fwd_out, d_offset, d_size);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -45,8 +45,9 @@ AMP_FWD_HALF_PANELS = True  # autocast: the projection's forward packs fp16 pane
 LAZY_DECODE = True
 
 
-# BEVNet._heatmap_focal_loss on the GPU runs the native loss (A/B: tools/train_step_bench.py --torch-focal)
-NATIVE_FOCAL = True
+# BEVNet's focal heatmap and L1 offset / size losses on the GPU run on the native kernels (A/B:
+# tools/train_step_bench.py --torch-loss)
+NATIVE_LOSS = True
 
 
 class _FocalLoss(torch.autograd.Function):
@@ -66,6 +67,25 @@ class _FocalLoss(torch.autograd.Function):
     def backward(ctx, g):
         logits, gt, inv = ctx.saved_tensors
         return _nat.focal_loss_bwd(logits, gt, *ctx.ab, g.reshape(1), inv), None, None, None
+
+
+class _L1Losses(torch.autograd.Function):
+    """model_wrapper.py:109-116's masked L1 offset and log-size losses on the native kernels -> [2]; gradients for the
+    offset / size maps only."""
+
+    @staticmethod
+    @_nat.amp_fwd
+    def forward(ctx, offset, size, indices, mask, off_t, size_t):
+        out = _nat.l1_losses(offset, size, indices, mask, off_t, size_t)
+        ctx.save_for_backward(offset, size, indices, mask, off_t, size_t, out)
+        return out[:2].clone()
+
+    @staticmethod
+    @_nat.amp_bwd
+    def backward(ctx, g):
+        offset, size, indices, mask, off_t, size_t, out = ctx.saved_tensors
+        d_off, d_size = _nat.l1_losses_bwd(offset, size, indices, mask, off_t, size_t, g, out)
+        return d_off, d_size, None, None, None, None
 
 
 class _HeadOperand(torch.autograd.Function):
@@ -264,10 +284,13 @@ class BEVNet(nn.Module):
     def _loss_terms(self, logits, offset, size_raw, hm, indices, mask, off_t, size_t):
         """model_wrapper.py:105-124: the focal heatmap loss and the masked L1 offset / log-size losses."""
         hm_loss = self._heatmap_focal_loss(logits, hm)
-        m = mask.unsqueeze(-1)
-        n = m.sum() + 1e-4
-        off_loss = (self._gather_feat(offset, indices) - off_t).mul(m).abs().sum() / n
-        size_loss = (self._gather_feat(size_raw, indices) - size_t).mul(m).abs().sum() / n
+        if NATIVE_LOSS and offset.is_cuda and size_raw.is_cuda and indices.is_cuda:
+            off_loss, size_loss = _L1Losses.apply(offset, size_raw, indices, mask, off_t, size_t).unbind(0)
+        else:
+            m = mask.unsqueeze(-1)
+            n = m.sum() + 1e-4
+            off_loss = (self._gather_feat(offset, indices) - off_t).mul(m).abs().sum() / n
+            size_loss = (self._gather_feat(size_raw, indices) - size_t).mul(m).abs().sum() / n
         total = self.hm_weight * hm_loss + self.offset_weight * off_loss + self.size_weight * size_loss
         return hm_loss, off_loss, size_loss, total
 
@@ -424,7 +447,7 @@ class BEVNet(nn.Module):
         """Penalty-reduced focal loss (model_wrapper.py:235-247), normalised by the number of gt peaks.  On the GPU:
         bev_focal_loss_fwd_f32 / _bwd_f32 (three launches for forward + backward instead of ~60 small torch ones;
         fp32 terms, double sums, so within fp32 rounding of the torch composition)."""
-        if NATIVE_FOCAL and pred_logits.is_cuda and gt.is_cuda:
+        if NATIVE_LOSS and pred_logits.is_cuda and gt.is_cuda:
             return _FocalLoss.apply(pred_logits.float(), gt.float(), float(self.hm_alpha), float(self.hm_beta))
         p = torch.sigmoid(pred_logits).clamp(1e-4, 1 - 1e-4)
         peak = gt == 1.0
