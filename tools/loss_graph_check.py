@@ -1,5 +1,7 @@
 """Diagnostic: the AMP BEVNet training step of tools/train_step_bench.py with the graphed loss, each step's losses
-compared with the eager loss terms on the same predictions (and the same targets), printed per step."""
+compared with the eager loss terms on the same predictions (and the same targets), printed per step.
+Needs the graphed loss (models.model_wrapper.LOSS_GRAPHS) of commit 69d574d, removed after this check found wrong
+replays (profiles/r05ar_loss_graph_check.txt); kept as the reproducer for that investigation."""
 import os
 import sys
 import time
