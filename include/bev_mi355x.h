@@ -396,6 +396,13 @@ int bev_l1_losses_bwd_f32(const float *offset, const float *size, int B, int64_t
                           const float *mask, const float *off_t, const float *size_t_, int M, int ld,
                           const float *grad_losses, const float *fwd_out, float *d_offset, float *d_size,
                           void *stream);
+/* CenterNet gaussian radius of model_wrapper.py:205-233 per object (BEVNet._gaussian_radius_tensor, as torch's
+ * float32 ops compute it on the device): width / height in cells -> radius[i] (int64).  The Python-scalar operands
+ * come as torch casts them: f_1mov = (float)(1 - ov), rcp_1pov = 1.0f / (float)(1 + ov), f_4ov = (float)(4 ov),
+ * f_m2ov = (float)(-2 ov), f_ovm1 = (float)(ov - 1); ov_zero: the r3 root is +inf (ov == 0). */
+int bev_gaussian_radius_f32(const float *width_cells, const float *height_cells, int n, float f_1mov,
+                            float rcp_1pov, float f_4ov, float f_m2ov, float f_ovm1, int ov_zero, float min_radius,
+                            int64_t *radius, void *stream);
 int64_t bev_focal_loss_workspace_bytes(int64_t n);
 int bev_focal_loss_fwd_f32(const float *logits, const float *gt, int64_t n, float alpha, float beta, float *loss,
                            float *inv_norm, void *workspace, int64_t workspace_bytes, void *stream);

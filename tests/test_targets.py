@@ -182,3 +182,22 @@ def test_native_l1_losses_vs_float64_torch():
     for a, b in zip(res[True][2:], res[False][2:]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
     assert float(res[True][2].abs().sum()) > 0
+
+
+@pytest.mark.gpu
+def test_native_gaussian_radius_bit_identical_to_torch_ops():
+    """bev_gaussian_radius_f32 vs BEVNet._gaussian_radius_tensor's torch ops on the device: equal radii for 2^20 random
+    sizes (sub-cell to 10^4 cells, the integer edges included) and the configured overlaps, ov = 0 among them."""
+    import bev_native as nat
+    dev = torch.device("cuda:0")
+    net = BEVNet(CFG).to(dev)
+    g = torch.Generator().manual_seed(12)
+    n = 1 << 20
+    w = torch.exp(torch.rand(n, generator=g) * 11 - 2).to(dev)
+    h = torch.exp(torch.rand(n, generator=g) * 11 - 2).to(dev)
+    w[:1000] = torch.arange(1000, device=dev, dtype=torch.float32) / 7
+    for ov in (0.7, 0.5, 0.0, 0.3):
+        net.gaussian_iou = ov
+        ref = net._gaussian_radius_tensor(w, h)
+        got = nat.gaussian_radius(w, h, ov, net.gaussian_min_radius)
+        assert torch.equal(got, ref), (ov, int((got != ref).sum()))

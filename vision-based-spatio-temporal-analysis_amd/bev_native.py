@@ -59,6 +59,7 @@ SIGNATURES = {
     "bev_head_operand_bwd_bias_f32": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "bev_l1_losses_fwd_f32": (_i, [_vp, _vp, _i, _i64, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
     "bev_l1_losses_bwd_f32": (_i, [_vp, _vp, _i, _i64, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "bev_gaussian_radius_f32": (_i, [_vp, _vp, _i, _f, _f, _f, _f, _f, _i, _f, _vp, _vp]),
     "bev_focal_loss_workspace_bytes": (_i64, [_i64]),
     "bev_focal_loss_fwd_f32": (_i, [_vp, _vp, _i64, _f, _f, _vp, _vp, _vp, _i64, _vp]),
     "bev_focal_loss_bwd_f32": (_i, [_vp, _vp, _i64, _f, _f, _vp, _vp, _vp, _vp]),
@@ -1487,6 +1488,21 @@ def l1_losses_bwd(offset, size, indices, mask, off_t, size_t, grad_losses, fwd_o
                                        _ptr(g), _ptr(fwd_out), _ptr(d_off), _ptr(d_sz), _stream(o)),
            "bev_l1_losses_bwd_f32")
     return d_off, d_sz
+
+
+def gaussian_radius(width_cells: torch.Tensor, height_cells: torch.Tensor, overlap: float, min_radius: int):
+    """BEVNet._gaussian_radius_tensor (model_wrapper.py:205-233) in one launch, the same float32 values as torch's ops
+    on the device -> int64 radii."""
+    import numpy as np
+    w, h = width_cells.contiguous(), height_cells.contiguous()
+    _require_gpu(w, h)
+    out = torch.empty(w.shape, device=w.device, dtype=torch.int64)
+    f32 = np.float32
+    _check(lib().bev_gaussian_radius_f32(_ptr(w), _ptr(h), w.numel(), float(f32(1 - overlap)),
+                                         float(f32(1.0) / f32(1 + overlap)), float(f32(4 * overlap)),
+                                         float(f32(-2 * overlap)), float(f32(overlap - 1)), int(overlap == 0),
+                                         float(min_radius), _ptr(out), _stream(w)), "bev_gaussian_radius_f32")
+    return out
 
 
 DECODE_SORT_CHUNK = 8192  # keys per LDS chunk of the large-path sort (bev_decode.hip SORT_CHUNK)

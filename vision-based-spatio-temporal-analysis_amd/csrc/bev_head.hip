@@ -797,3 +797,46 @@ int bev_l1_losses_bwd_f32(const float *offset, const float *size, int B, int64_t
 }
 
 }  // extern "C"
+
+// ---- CenterNet gaussian radius (model_wrapper.py:205-233, BEVNet._gaussian_radius_tensor) --------------------------
+// The torch float32 op sequence replayed op by op in one launch instead of ~45 (the library builds with
+// -ffp-contract=off: no fused multiply-adds): a tensor times a Python scalar is x * (float)s, a tensor over a Python
+// scalar x * (1.0f / (float)s) (torch's CUDA division by a CPU scalar; the caller passes that reciprocal), tensor over
+// tensor a true division, x ** 2 a product, clamp / min propagate NaN like torch's.
+namespace {
+__device__ __forceinline__ float gr_clamp_min(float x, float lo) { return x < lo ? lo : x; }  // NaN stays NaN
+__device__ __forceinline__ float gr_min(float a, float b) { return a != a ? a : (b != b ? b : (b < a ? b : a)); }
+__device__ __forceinline__ float gr_root(float a, float b, float c) {
+    const float t = gr_clamp_min(b * b - (a * 4.0f) * c, 0.0f);  // b ** 2 - 4 * a * c, clamp(min=0)
+    return b + sqrtf(t);
+}
+__global__ void k_gauss_radius(const float *__restrict__ wc, const float *__restrict__ hc, int n, float f_1mov,
+                               float rcp_1pov, float f_4ov, float f_m2ov, float f_ovm1, int ov_zero, float minr,
+                               int64_t *__restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float w = gr_clamp_min(wc[i], 1.0f), h = gr_clamp_min(hc[i], 1.0f);
+    const float r1 = gr_root(1.0f, h + w, ((w * h) * f_1mov) * rcp_1pov) * 0.5f;
+    const float a2 = 4.0f;
+    const float r2 = gr_root(a2, (h + w) * 2.0f, (w * f_1mov) * h) / (a2 * 2.0f);
+    float r = gr_min(r1, r2);
+    if (!ov_zero) {
+        const float a3 = f_4ov;
+        const float r3 = gr_root(a3, (h + w) * f_m2ov, (w * f_ovm1) * h) / (a3 * 2.0f);
+        r = gr_min(r, r3);
+    }
+    out[i] = (int64_t)floorf(gr_clamp_min(r, minr));
+}
+}  // namespace
+
+extern "C" {
+int bev_gaussian_radius_f32(const float *width_cells, const float *height_cells, int n, float f_1mov,
+                            float rcp_1pov, float f_4ov, float f_m2ov, float f_ovm1, int ov_zero, float min_radius,
+                            int64_t *radius, void *stream) {
+    if (!width_cells || !height_cells || !radius || n < 0) return BEV_ERR_ARGS;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_gauss_radius, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, width_cells,
+                       height_cells, n, f_1mov, rcp_1pov, f_4ov, f_m2ov, f_ovm1, ov_zero, min_radius, radius);
+    return (int)hipGetLastError();
+}
+}  // extern "C"

@@ -393,7 +393,11 @@ class BEVNet(nn.Module):
         mask[frame, s] = 1.0
         offset[frame, s] = torch.stack([gx - cx, gy - cy], dim=1)
         size_log[frame, s] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
-        self._splat_gaussians(hm_ext, frame, cxl, cyl, self._gaussian_radius_tensor(w_cells, h_cells), sel, bound,
+        if NATIVE_LOSS and w_cells.is_cuda:  # the same float32 op sequence in one launch
+            radius = _nat.gaussian_radius(w_cells, h_cells, self.gaussian_iou, self.gaussian_min_radius)
+        else:
+            radius = self._gaussian_radius_tensor(w_cells, h_cells)
+        self._splat_gaussians(hm_ext, frame, cxl, cyl, radius, sel, bound,
                               (B, Hb, Wb))
         return {"heatmap": hm, "indices": indices[:, :M], "mask": mask[:, :M], "offset": offset[:, :M],
                 "size_log": size_log[:, :M]}
