@@ -510,19 +510,22 @@ int bev_conv2d_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, i
 
 /* device: bev_conv2d_chain_f32 (bottleneck conv2 -> conv3 + identity residual in one launch, the conv2 output kept
  * in LDS) in the split arithmetic: packed / packed2 are the split panels of conv2 [Co][Ci][KH][KW] and conv3
- * [Co2][Co][1][1]; NHWC x, Ci % 32 == 0, Co in {64, 128}, Co2 % 64 == 0; residual [N][Ho][Wo][Co2] (or NULL). */
-int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
-                            int Co, int KH, int KW, int stride, int pad, int act, const uint16_t *packed2,
-                            const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
-                            void *stream);
+ * [Co2][Co][1][1]; NHWC x, Ci % 32 == 0, Co in {64, 128}, Co2 % 64 == 0; residual [N][Ho][Wo][Co2] (or NULL).
+ * Exactly one of x / xs: xs = conv2's operand already split ([3][N][H][W][Ci] bf16 planes, as the conv1 launch's
+ * split output ys writes them; 16-B aligned) -- staged by LDS-DMA, bit-identical to the fp32 x. */
+int bev_conv2d_chain_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, int Ci,
+                            const uint16_t *packed, const float *bias, int Co, int KH, int KW, int stride, int pad,
+                            int act, const uint16_t *packed2, const float *bias2, int Co2, const float *residual,
+                            int act2, float *y, int Ho, int Wo, void *stream);
 
 /* device: bev_conv2d_chain_dual_f32 (block 0 of a stage: conv2 -> [conv3 | 1x1/s2 downsample of x2] in one launch)
  * in the split arithmetic; packed2 = the split panel of [W3 | Wds] as [Co2][Co + Ci2][1][1]; Co == Ci2 == 64 (the
- * layer1 shape), Ci % 32 == 0, Co2 % 64 == 0. */
-int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed,
-                                 const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
-                                 const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
-                                 const float *bias2, int Co2, int act2, float *y, int Ho, int Wo, void *stream);
+ * layer1 shape), Ci % 32 == 0, Co2 % 64 == 0.  x / xs as bev_conv2d_chain_x6_f32 (x2 stays fp32). */
+int bev_conv2d_chain_dual_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, int Ci,
+                                 const uint16_t *packed, const float *bias, int Co, int KH, int KW, int stride,
+                                 int pad, int act, const float *x2, int H2, int W2, int Ci2, int stride2,
+                                 const uint16_t *packed2, const float *bias2, int Co2, int act2, float *y, int Ho,
+                                 int Wo, void *stream);
 
 /* device: the ResNet stem (timm conv1: 7x7, stride 2, pad 3, Ci = 3; cnn_encoder.py:26, the first layer of
  * CNNEncoder._encode_single) in the split arithmetic: x NCHW [N][3][H][W] fp32 images, packed = the split panel of

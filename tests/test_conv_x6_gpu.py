@@ -182,6 +182,62 @@ def test_x6_chain_dual_bit_identical_to_two_launches():
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("Ci,Co,Co2,stride,N,H,W", [(64, 64, 256, 1, 2, 25, 37), (128, 128, 512, 1, 2, 25, 37),
+                                                    (64, 64, 256, 2, 1, 31, 20), (64, 64, 256, 1, 3, 7, 130)])
+def test_x6_chain_pre_split_operand_bit_identical(Ci, Co, Co2, stride, N, H, W):
+    """The chain with conv2's operand handed over split (conv1's ys planes -> LDS-DMA staging, k_conv_x6s CHAIN)
+    == the chain splitting the fp32 operand per tap (k_conv_x6b CHAIN), bit for bit; ragged M (the last tile's
+    rows past M), W past one 128-row tile, stride 2."""
+    g = torch.Generator().manual_seed(5 * Ci + Co2 + H)
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
+    w2 = (torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5).to(DEV)
+    w3 = (torch.randn(Co2, Co, 1, 1, generator=g) / Co ** 0.5).to(DEV)
+    b2, b3 = (torch.randn(Co, generator=g) * 0.1).to(DEV), (torch.randn(Co2, generator=g) * 0.1).to(DEV)
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    res = torch.randn(N, Ho, Wo, Co2, generator=g).to(DEV)
+    p2, p3 = nat.pack_conv_weight_x6(w2), nat.pack_conv_weight_x6(w3)
+    ref = nat.conv2d_chain_nhwc(x, p2, b2, Co, 3, 3, stride, 1, 1, p3, b3, Co2, 1, residual=res)
+    got = nat.conv2d_chain_nhwc(nat.split3(x), p2, b2, Co, 3, 3, stride, 1, 1, p3, b3, Co2, 1, residual=res)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
+def test_x6_chain_dual_pre_split_operand_bit_identical():
+    """bev_conv2d_chain_dual_x6_f32 with conv2's operand pre-split == with it fp32 (layer1 block 0 shape)."""
+    g = torch.Generator().manual_seed(31)
+    N, H, W, Ci, Co, Co2 = 2, 27, 45, 64, 64, 256
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
+    xb = torch.randn(N, H, W, 64, generator=g).to(DEV)
+    w2 = (torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5).to(DEV)
+    w3 = (torch.randn(Co2, Co + 64, 1, 1, generator=g) / (Co + 64) ** 0.5).to(DEV)
+    b2, b3 = (torch.randn(Co, generator=g) * 0.1).to(DEV), (torch.randn(Co2, generator=g) * 0.1).to(DEV)
+    p2, p3 = nat.pack_conv_weight_x6(w2), nat.pack_conv_weight_x6(w3)
+    ref = nat.conv2d_chain_dual_nhwc(x, p2, b2, Co, 3, 3, 1, 1, 1, xb, 1, p3, b3, Co2, 1)
+    got = nat.conv2d_chain_dual_nhwc(nat.split3(x), p2, b2, Co, 3, 3, 1, 1, 1, xb, 1, p3, b3, Co2, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
+def test_x6_resnet50_encoder_split_chain_bit_identical():
+    """The ResNet-50 encoder with conv1 -> chain edges pre-split (resnet.SPLIT_CHAIN, the default) == with them fp32."""
+    from models.encoders import resnet
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(1)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(DEV)
+    imgs = torch.randn(1, 3, 3, 96, 160, device=DEV)
+    old = resnet.SPLIT_CHAIN
+    try:
+        with torch.no_grad(), nat.conv_arith_mode("bf16x6"):
+            resnet.SPLIT_CHAIN = False
+            ref = enc(imgs).float().clone()
+            resnet.SPLIT_CHAIN = True
+            got = enc(imgs).float().clone()
+    finally:
+        resnet.SPLIT_CHAIN = old
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 def test_x6_resnet50_encoder_matches_f32_path():
     """The ResNet-50 CNNEncoder (the bench's trunk) in the split-bf16 arithmetic vs the exact-f32 MFMA chains."""
     from models.encoders.cnn_encoder import CNNEncoder

@@ -158,3 +158,34 @@ def test_fused_warp_rank_chunk_major_layout():
                     assert torch.equal(flat[:, :, :g.bev_h].view(torch.int32), plain.view(torch.int32)), (mode, rpr)
                     assert not flat[:, :, g.bev_h:].any(), (mode, rpr)
     assert nat.lib().bev_abi_version() == nat.ABI_VERSION
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("Hb,world,C,nhwc", [(120, 16, 64, True), (9, 4, 64, True), (120, 16, 20, False),
+                                             (97, 3, 64, False)])
+def test_fused_warp_chunked_world_chunks_and_any_layout(Hb, world, C, nhwc):
+    """camera_sharded_forward's partial: exactly `world` chunks of rows_per_rank(Hb, world) rows even when
+    ceil(Hb / rpr) < world (Hb 120 at world 16: 15 map chunks + 1 zero chunk; Hb 9 at world 4: 3 + 1), and for
+    feature layouts the chunk-major LDS-DMA kernel does not take (NCHW storage, C % 64 != 0), which run the plain
+    fused launch + a rearranging copy -- all bit-equal to the plain map, the rows / chunks past it zero."""
+    import bev_rig
+    from bev_dist import rows_per_rank
+    from models.fusion.geometry import GeometryTransformer
+    g = GeometryTransformer(Hb, 3 * Hb + 5, (-24.0, 24.0, -7.2, 7.2))
+    B, V, Hf, Wf = 2, 5, 34, 60
+    K, Rt = bev_rig.rig(V, 270, 480, B)
+    K, Rt = torch.from_numpy(K).to(DEV), torch.from_numpy(Rt).to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(Hb + C)
+    if nhwc:
+        f = torch.randn(B, V, Hf, Wf, C, device=DEV, generator=gen).permute(0, 1, 4, 2, 3)
+    else:
+        f = torch.randn(B, V, C, Hf, Wf, device=DEV, generator=gen)
+    rpr = rows_per_rank(Hb, world)
+    with torch.no_grad():
+        for mode in ("sum", "max"):
+            plain = g.forward_fused(f, K, Rt, (270, 480), mode)
+            ck = g.forward_fused(f, K, Rt, (270, 480), mode, rows_per_chunk=rpr, num_chunks=world)
+            assert tuple(ck.shape) == (world, B, C, rpr, g.bev_w)
+            flat = ck.permute(1, 2, 0, 3, 4).reshape(B, C, world * rpr, g.bev_w)
+            assert torch.equal(flat[:, :, :Hb].view(torch.int32), plain.view(torch.int32)), mode
+            assert not flat[:, :, Hb:].any(), mode

@@ -117,12 +117,14 @@ def camera_sharded_forward(geom, feats_local: torch.Tensor, K_local, Rt_local, i
     chunked = world > 1 and feats_local.is_cuda and dist.get_backend(group) != "gloo" and not (
         torch.is_grad_enabled() and feats_local.requires_grad)
     if chunked:
+        # exactly `world` chunks of rows_per_rank rows (ceil(Hb / rpr) can be < world, e.g. Hb 120 at world 16:
+        # 15 map chunks + one all-zero chunk); layouts the chunk-major kernel does not take are rearranged by
+        # warp_fuse itself, so the reduce-scatter always receives [world, B, C, rpr, Wb]
         rpr = rows_per_rank(geom.bev_h, world)
-        partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode, rows_per_chunk=rpr)
-        if partial.dim() == 5:
-            return reduce_partial_bev(partial, num_views, mode, group, gather, bev_h=geom.bev_h)
-    else:
-        partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
+        partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode, rows_per_chunk=rpr,
+                                     num_chunks=world)
+        return reduce_partial_bev(partial, num_views, mode, group, gather, bev_h=geom.bev_h)
+    partial = geom.forward_fused(feats_local, K_local, Rt_local, img_size, part_mode)
     return reduce_partial_bev(partial, num_views, mode, group, gather)
 
 

@@ -20,7 +20,8 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
+BEV_ERR_ARGS = -1  # include/bev_mi355x.h: an argument the kernel cannot take
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
 
@@ -147,10 +148,10 @@ SIGNATURES = {
     "bev_conv2d_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _i, _i,
                                _vp]),
     "bev_split3_f32": (_i, [_vp, _i64, _vp, _vp]),
-    "bev_conv2d_chain_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp,
-                                          _vp, _i, _i, _vp, _i, _i, _vp]),
-    "bev_conv2d_chain_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp,
-                                     _i, _i, _vp]),
+    "bev_conv2d_chain_dual_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i,
+                                          _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
+    "bev_conv2d_chain_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i,
+                                     _vp, _i, _i, _vp]),
     "bev_conv2d_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
 }
 
@@ -449,15 +450,19 @@ def warp_fuse_boxes(H: torch.Tensor, xs, ys, B: int, V: int, Hf: int, Wf: int, i
 
 
 def warp_fuse(feats: torch.Tensor, H: torch.Tensor, xs, ys, img_hw, mode: str, out: torch.Tensor = None,
-              boxes: torch.Tensor = None, rows_per_chunk: int = None, channels_last: bool = False):
+              boxes: torch.Tensor = None, rows_per_chunk: int = None, channels_last: bool = False,
+              num_chunks: int = None):
     """feats [B,V,C,Hf,Wf] (any strides within a map; maps b*V+v) -> out [B,C,Hb,Wb].  `boxes`: a workspace filled
     by `warp_fuse_boxes` for this geometry and mode (the pre-pass is then not launched again).
     `rows_per_chunk` (< Hb): the rank-chunk-major layout of bev_ipm_warp_fuse_chunked_f32 instead,
-    out [ceil(Hb / rpr), B, C, rpr, Wb] with the rows past Hb zero (the camera-shard reduce-scatter's input).
+    out [ceil(Hb / rpr), B, C, rpr, Wb] with the rows past Hb zero (the camera-shard reduce-scatter's input), or
+    [num_chunks, B, C, rpr, Wb] when `num_chunks` (>= ceil(Hb / rpr), the world size) is given: the chunks past the
+    map are all zero.  Layouts the chunk-major kernel does not take (not channels-last, C % 64 != 0, ...) run the
+    plain fused launch and one rearranging copy on the device, with the same values.
     `channels_last`: bev_ipm_warp_fuse_nhwc_f32 -- the same [B,C,Hb,Wb] values in torch.channels_last memory format
     (storage [B,Hb,Wb,C]); needs NHWC features with C % 64 == 0 (the LDS-DMA kernel), else HipError."""
-    if rows_per_chunk is not None and rows_per_chunk < ys.numel():
-        return _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, int(rows_per_chunk), boxes)
+    if rows_per_chunk is not None and (rows_per_chunk < ys.numel() or num_chunks):
+        return _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, int(rows_per_chunk), boxes, num_chunks)
     if channels_last:
         return _warp_fuse_nhwc(feats, H, xs, ys, img_hw, mode, out, boxes)
     _require_gpu(feats, H, xs, ys)
@@ -517,17 +522,24 @@ def _warp_fuse_nhwc(feats, H, xs, ys, img_hw, mode, out=None, boxes=None):
     return out
 
 
-def _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, rpr, boxes=None):
+def _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, rpr, boxes=None, num_chunks=None):
     _require_gpu(feats, H, xs, ys)
     B, V, C, Hf, Wf = feats.shape
     if B * V > 0 and feats.stride(0) != V * feats.stride(1):
         feats = feats.contiguous()
     Hb, Wb = ys.numel(), xs.numel()
     sx, sy = _scales(Hf, Wf, img_hw)
-    nck = -(-Hb // rpr)
+    if rpr <= 0:
+        raise ValueError("rows_per_chunk must be positive")
+    nmap = -(-Hb // rpr)  # chunks that hold map rows
+    nck = nmap if num_chunks is None else int(num_chunks)
+    if nck < nmap:
+        raise ValueError(f"num_chunks {nck} < ceil(Hb / rows_per_chunk) = {nmap}")
     out = torch.empty(nck, B, C, rpr, Wb, device=feats.device, dtype=torch.float32)
-    if nck * rpr > Hb:
-        out[-1, :, :, Hb - (nck - 1) * rpr:].zero_()  # padding rows: no cell writes them
+    if nmap * rpr > Hb:
+        out[nmap - 1, :, :, Hb - (nmap - 1) * rpr:].zero_()  # padding rows: no cell writes them
+    if nck > nmap:
+        out[nmap:].zero_()  # whole chunks past the map (a world larger than ceil(Hb / rpr))
     s = feats.stride()
     nws = lib().bev_ipm_warp_fuse_workspace_bytes(B, V, Hb, Wb)
     ready = boxes is not None
@@ -538,6 +550,14 @@ def _warp_fuse_chunked(feats, H, xs, ys, img_hw, mode, rpr, boxes=None):
         rc = lib().bev_ipm_warp_fuse_chunked_f32(_ptr(feats), s[1], s[2], s[3], s[4], _ptr(H), _ptr(xs), _ptr(ys), B,
                                                  V, C, Hf, Wf, sx, sy, Hb, Wb, FUSE_MODES[mode], rpr, _ptr(out),
                                                  _ptr(ws), nws, int(ready), _stream(feats))
+    if rc == BEV_ERR_ARGS:
+        # a layout the chunk-major LDS-DMA kernel does not take (NCHW or C % 64 != 0 features, V > 64, an A/B knob):
+        # the plain fused launch, then its rows copied into chunk order on the device (same values)
+        plain = warp_fuse(feats, H, xs, ys, img_hw, mode, boxes=boxes if ready else None)
+        padded = torch.zeros(B, C, nmap * rpr, Wb, device=feats.device, dtype=torch.float32)
+        padded[:, :, :Hb] = plain
+        out[:nmap] = padded.view(B, C, nmap, rpr, Wb).permute(2, 0, 1, 3, 4)
+        return out
     _check(rc, "bev_ipm_warp_fuse_chunked_f32")
     return out
 
@@ -1155,9 +1175,19 @@ def conv2d_dual_nhwc(x: torch.Tensor, x2: torch.Tensor, stride2: int, packed: to
 def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
                       relu: int, packed2: torch.Tensor, bias2, Co2: int, relu2: int, residual: torch.Tensor = None,
                       out: torch.Tensor = None):
-    """act2(act(conv(x) + bias) (*) W2 + bias2 + residual) in one launch; x [N,H,W,Ci] NHWC -> [N,Ho,Wo,Co2]."""
-    x = x.contiguous()
-    _require_gpu(x, bias, bias2, residual, *([packed, packed2] if packed.dtype != torch.bfloat16 else []))
+    """act2(act(conv(x) + bias) (*) W2 + bias2 + residual) in one launch; x [N,H,W,Ci] NHWC -> [N,Ho,Wo,Co2].  In the
+    split arithmetic x may be a Split3 (conv1's split output): conv2's operand is then staged by LDS-DMA with no
+    split in the kernel (bit-identical to the fp32 x it holds)."""
+    xs = x if isinstance(x, Split3) else None
+    if xs is not None and packed.dtype != torch.bfloat16:
+        raise HipError("a pre-split operand needs the split-bf16 panels")
+    if xs is None:
+        x = x.contiguous()
+    src = xs.planes if xs is not None else x
+    _require_gpu(x if xs is None else None, bias, bias2, residual,
+                 *([packed, packed2] if packed.dtype != torch.bfloat16 else []))
+    if xs is not None and not src.is_cuda:
+        raise HipError("the pre-split operand must be on the device")
     if not (packed.is_cuda and packed2.is_cuda and packed.dtype == packed2.dtype):
         raise HipError("conv2d_chain_nhwc needs both weight panels on the device, in one arithmetic")
     N, H, W, Ci = x.shape
@@ -1168,10 +1198,11 @@ def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: 
         residual = residual.contiguous()
         assert residual.shape == out.shape
     if packed.dtype == torch.bfloat16:  # split-bf16 arithmetic (both panels from pack_conv_weight_x6)
-        with _span("conv", x):
-            rc = lib().bev_conv2d_chain_x6_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad,
-                                               int(relu), _ptr(packed2), _ptr(bias2), Co2, _ptr(residual), int(relu2),
-                                               _ptr(out), Ho, Wo, _stream(x))
+        with _span("conv", src):
+            rc = lib().bev_conv2d_chain_x6_f32(None if xs is not None else _ptr(x), _ptr(xs.planes) if xs is not None
+                                               else None, N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride,
+                                               pad, int(relu), _ptr(packed2), _ptr(bias2), Co2, _ptr(residual),
+                                               int(relu2), _ptr(out), Ho, Wo, _stream(src))
         _check(rc, "bev_conv2d_chain_x6_f32")
         return out
     with _span("conv", x):
@@ -1185,10 +1216,19 @@ def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: 
 def conv2d_chain_dual_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int,
                            pad: int, relu: int, x2: torch.Tensor, stride2: int, packed2: torch.Tensor, bias2, Co2: int,
                            relu2: int, out: torch.Tensor = None):
-    """act2([act(conv(x) + bias) | x2[:, ::s2, ::s2]] (*) W2 + bias2) in one launch (bottleneck with downsample)."""
-    x = x.contiguous()
+    """act2([act(conv(x) + bias) | x2[:, ::s2, ::s2]] (*) W2 + bias2) in one launch (bottleneck with downsample).
+    x may be a Split3 in the split arithmetic, as for conv2d_chain_nhwc."""
+    xs = x if isinstance(x, Split3) else None
+    if xs is not None and packed.dtype != torch.bfloat16:
+        raise HipError("a pre-split operand needs the split-bf16 panels")
+    if xs is None:
+        x = x.contiguous()
+    src = xs.planes if xs is not None else x
     x2 = x2.contiguous()
-    _require_gpu(x, bias, x2, bias2, *([packed, packed2] if packed.dtype != torch.bfloat16 else []))
+    _require_gpu(x if xs is None else None, bias, x2, bias2,
+                 *([packed, packed2] if packed.dtype != torch.bfloat16 else []))
+    if xs is not None and not src.is_cuda:
+        raise HipError("the pre-split operand must be on the device")
     if not (packed.is_cuda and packed2.is_cuda and packed.dtype == packed2.dtype):
         raise HipError("conv2d_chain_dual_nhwc needs both weight panels on the device, in one arithmetic")
     N, H, W, Ci = x.shape
@@ -1197,10 +1237,12 @@ def conv2d_chain_dual_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int,
     if out is None:
         out = torch.empty(N, Ho, Wo, Co2, device=x.device, dtype=torch.float32)
     if packed.dtype == torch.bfloat16:  # split-bf16 arithmetic
-        with _span("conv", x):
-            rc = lib().bev_conv2d_chain_dual_x6_f32(_ptr(x), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride,
-                                                    pad, int(relu), _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed2),
-                                                    _ptr(bias2), Co2, int(relu2), _ptr(out), Ho, Wo, _stream(x))
+        with _span("conv", src):
+            rc = lib().bev_conv2d_chain_dual_x6_f32(None if xs is not None else _ptr(x),
+                                                    _ptr(xs.planes) if xs is not None else None, N, H, W, Ci,
+                                                    _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad, int(relu),
+                                                    _ptr(x2), H2, W2, Ci2, stride2, _ptr(packed2), _ptr(bias2), Co2,
+                                                    int(relu2), _ptr(out), Ho, Wo, _stream(src))
         _check(rc, "bev_conv2d_chain_dual_x6_f32")
         return out
     with _span("conv", x):

@@ -761,16 +761,26 @@ __device__ __forceinline__ void dma16(const void *src, unsigned dst_any) {
         : "memory");
 }
 
-template <int WM, int WN, int TM, int TN>
-__global__ __launch_bounds__(256, 3) void k_conv_x6s(ConvX a) {
+// CHAIN (bev_conv2d_chain_x6_f32 / _dual_ with a pre-split xs): the mainloop above, then x6_chain_epilogue exactly
+// as k_conv_x6b's chain runs it -- the layer1 / layer2 bottleneck bodies take conv1's split output, so conv2 (the
+// 3x3, whose fp32 operand the register-staged kernel splits once per tap) stages by DMA alone.
+// BLDS (the chains): B goes through LDS too -- the K step's BN / 32 x 2 slices x 3 planes of the fragment-order panel
+// are 1-KiB runs, one DMA instruction each, read back as conflict-free ds_read_b128 (lane l at 16 l) -- so every
+// vector-memory operation of the loop is a DMA issued one K step ahead and waited for at the step's end.  (With B
+// in registers hipcc re-issued the fragment loads next to their MFMAs and waited on each: L2 latency per slice.)
+template <int WM, int WN, int TM, int TN, int CHAIN = 0, bool BLDS = (CHAIN > 0)>
+__global__ __launch_bounds__(256, CHAIN ? 2 : 3) void k_conv_x6s(ConvX a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int APL = BM * 32;     // bf16 per A plane per stage (64-B rows)
-    constexpr int STAGE = 3 * APL;   // bf16 per stage
+    constexpr int BST = BLDS ? BN / 32 * 6 * 512 : 0;  // bf16 of B per stage: [cb][slice][plane][64 lanes][8]
+    constexpr int STAGE = 3 * APL + BST;  // bf16 per stage
     constexpr int RW = BM / 4;       // rows staged by each wave
     constexpr int RG = RW / 16;      // 16-row DMA groups per wave and plane
-    constexpr int EPIB = x6_epi_bytes<TN>();
+    constexpr int BPW = BLDS ? BN / 32 * 6 / 4 : 0;  // B pieces (1 KiB) per wave and K step
+    constexpr int EPIB = CHAIN ? 3 * BM * (BN + 8) * 2 : x6_epi_bytes<TN>();
     constexpr int LDSB = (2 * STAGE * 2 > EPIB) ? 2 * STAGE * 2 : EPIB;
     static_assert(RW % 16 == 0, "whole DMA groups per wave");
+    static_assert(!BLDS || (BN / 32 * 6) % 4 == 0, "whole B pieces per wave");
     __shared__ __attribute__((aligned(16))) unsigned char lds_raw[LDSB];
     const __bf16 *lds = (const __bf16 *)lds_raw;
 
@@ -807,8 +817,20 @@ __global__ __launch_bounds__(256, 3) void k_conv_x6s(ConvX a) {
         abase[g] = ((n * a.H + aiy[g]) * a.W + aix[g]) * a.Ci + 8 * lc;
     }
     const unsigned lbase = (unsigned)__builtin_amdgcn_readfirstlane((int)lds_addr(lds_raw));
-    int ky = 0, kx = 0, ci0 = 0;
+    const int S = a.Kp / XBK;  // 16-deep slices
+    int ky = 0, kx = 0, ci0 = 0, kstep = 0;
+    const __bf16 *bsrc = a.wp + (int64_t)(n0 >> 5) * S * 1536 + lane * 8;  // the block's first column block
     auto issue = [&](int buf) {
+        if constexpr (BLDS) {  // piece q = (cb, slice, plane) of this K step: panel run ((cb S + 2 ks + sl) 3 + p)
+            const unsigned db = lbase + (unsigned)(buf * STAGE * 2 + 3 * APL * 2);
+#pragma unroll
+            for (int i = 0; i < BPW; ++i) {
+                const int q = wave + 4 * i, cbl = q / 6, r = q % 6;
+                dma16(bsrc + ((int64_t)cbl * S + 2 * kstep + r / 3) * 1536 + (r % 3) * 512,
+                      db + (unsigned)(q * 1024));
+            }
+            ++kstep;
+        }
         const int64_t toff = ((int64_t)ky * a.dil * a.W + kx * a.dil) * a.Ci + ci0;
         const unsigned d0 = lbase + (unsigned)(buf * STAGE * 2) + (unsigned)(wave * RW * 64);
 #pragma unroll
@@ -831,7 +853,6 @@ __global__ __launch_bounds__(256, 3) void k_conv_x6s(ConvX a) {
         }
     };
 
-    const int S = a.Kp / XBK;  // 16-deep slices
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<__bf16 *>(a.wp), 0, (int)(uint32_t)(copad_x(a.Co) / 32 * (int64_t)S * 3072), 0x00020000);
     const int cb0 = (n0 + wn * TN * 32) >> 5;
@@ -872,32 +893,59 @@ __global__ __launch_bounds__(256, 3) void k_conv_x6s(ConvX a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){0};
     const int nk = a.Kp / YBK;
-    X6S_BLOAD(bs0, 0);
-    issue(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-        const int cur = ks & 1;
-        if (ks + 1 < nk) issue(cur ^ 1);
-        const __bf16 *As = lds + cur * STAGE;
-        X6S_BLOAD(bs1, 2 * ks + 1);
-        X6S_SLICE(As, 0, bs0);
-        X6S_BLOAD(bs0, 2 * ks + 2);
-        X6S_SLICE(As, 1, bs1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step ks + 1 landed
-        __syncthreads();                                   // all of it; buffer cur is free again
+    if constexpr (BLDS) {
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int ks = 0; ks < nk; ++ks) {
+            const int cur = ks & 1;
+            if (ks + 1 < nk) issue(cur ^ 1);
+            const __bf16 *As = lds + cur * STAGE;
+            const __bf16 *Bs = As + 3 * APL + lane * 8;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                bf16x8 fb[TN][3];
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) fb[j][p] = *(const bf16x8 *)(Bs + (((wn * TN + j) * 2 + kk) * 3 + p) * 512);
+                X6S_SLICE(As, kk, fb);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs of step ks + 1 landed
+            __syncthreads();                                   // everyone's; buffer cur is free again
+        }
+    } else {
+        X6S_BLOAD(bs0, 0);
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int ks = 0; ks < nk; ++ks) {
+            const int cur = ks & 1;
+            if (ks + 1 < nk) issue(cur ^ 1);
+            const __bf16 *As = lds + cur * STAGE;
+            X6S_BLOAD(bs1, 2 * ks + 1);
+            X6S_SLICE(As, 0, bs0);
+            X6S_BLOAD(bs0, 2 * ks + 2);
+            X6S_SLICE(As, 1, bs1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step ks + 1 landed
+            __syncthreads();                                   // all of it; buffer cur is free again
+        }
     }
 #undef X6S_SLICE
 #undef X6S_BLOAD
+    if constexpr (CHAIN > 0) {
+        x6_chain_epilogue<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0>(a, lds_raw, acc, wave, lane, wm, wn, m0);
+        return;
+    }
     x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
 }
 
-template <int WM, int WN, int TM, int TN>
+template <int WM, int WN, int TM, int TN, int CHAIN = 0>
 int launch_x6s(const ConvX &a, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL((k_conv_x6s<WM, WN, TM, TN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_conv_x6s<WM, WN, TM, TN, CHAIN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
     return (int)hipGetLastError();
 }
 
@@ -1412,15 +1460,15 @@ int bev_conv2d_dual_x6_f32(const float *x, int N, int Ho, int Wo, int Ci, const 
     return dispatch_x6<true>(a, (hipStream_t)stream);
 }
 
-int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed, const float *bias,
-                            int Co, int KH, int KW, int stride, int pad, int act, const uint16_t *packed2,
-                            const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
-                            void *stream) {
-    if (!x || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
-        pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2)
+int bev_conv2d_chain_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, int Ci,
+                            const uint16_t *packed, const float *bias, int Co, int KH, int KW, int stride, int pad,
+                            int act, const uint16_t *packed2, const float *bias2, int Co2, const float *residual,
+                            int act2, float *y, int Ho, int Wo, void *stream) {
+    if ((!x == !xs) || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 ||
+        stride <= 0 || pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2)
         return BEV_ERR_ARGS;
     if (Ci % YBK != 0 || (Co != 64 && Co != 128) || Co2 <= 0 || Co2 % 64 != 0 ||
-        (((uintptr_t)x | (uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
+        (((uintptr_t)x | (uintptr_t)xs | (uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
         return BEV_ERR_ARGS;
     if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
         return BEV_ERR_ARGS;
@@ -1437,28 +1485,34 @@ int bev_conv2d_chain_x6_f32(const float *x, int N, int H, int W, int Ci, const u
     a.M = (int64_t)N * Ho * Wo;
     a.x2 = nullptr;
     a.Ci2 = a.H2 = a.W2 = a.stride2 = 0;
-    a.xs = nullptr;
+    a.xs = (const __bf16 *)xs;
     a.ys = nullptr;
-    a.xps = a.yps = 0;
+    a.xps = (int64_t)N * H * W * Ci;
+    a.yps = 0;
     a.wp2 = (const __bf16 *)packed2;
     a.bias2 = bias2;
     a.Co2 = Co2;
     a.act2 = act2;
+    if (Co != 64 && Co2 % 128 != 0) return BEV_ERR_ARGS;  // two waves share each 32-row band of the 64-row tile
+    if (xs) {  // conv1 handed over its output split: conv2's operand by LDS-DMA (k_conv_x6s), same K order
+        if (Co == 64) return launch_x6s<4, 1, 1, 2, 1>(a, (hipStream_t)stream);
+        return launch_x6s<2, 2, 1, 2, 1>(a, (hipStream_t)stream);
+    }
     if (Co == 64) return launch_x6b<4, 1, 1, 2, false, 1>(a, (hipStream_t)stream);
-    if (Co2 % 128 != 0) return BEV_ERR_ARGS;  // two waves share each 32-row band of the 64-row tile
     return launch_x6b<2, 2, 1, 2, false, 1>(a, (hipStream_t)stream);  // 64 x 128: h2 planes 52 KiB of LDS
 }
 
-int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, const uint16_t *packed,
-                                 const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
-                                 const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
-                                 const float *bias2, int Co2, int act2, float *y, int Ho, int Wo, void *stream) {
-    if (!x || !x2 || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
-        pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2 || stride2 <= 0 || H2 <= 0 || W2 <= 0)
+int bev_conv2d_chain_dual_x6_f32(const float *x, const uint16_t *xs, int N, int H, int W, int Ci,
+                                 const uint16_t *packed, const float *bias, int Co, int KH, int KW, int stride,
+                                 int pad, int act, const float *x2, int H2, int W2, int Ci2, int stride2,
+                                 const uint16_t *packed2, const float *bias2, int Co2, int act2, float *y, int Ho,
+                                 int Wo, void *stream) {
+    if ((!x == !xs) || !x2 || !packed || !packed2 || !y || N < 0 || H <= 0 || W <= 0 || KH <= 0 || KW <= 0 ||
+        stride <= 0 || pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2 || stride2 <= 0 || H2 <= 0 || W2 <= 0)
         return BEV_ERR_ARGS;
     // the layer1 block-0 shape: 64-channel h2 and a 64-channel shortcut operand (4 slices kept in registers)
     if (Ci % YBK != 0 || Co != 64 || Ci2 != 64 || Co2 <= 0 || Co2 % 64 != 0 ||
-        (((uintptr_t)x | (uintptr_t)x2 | (uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
+        (((uintptr_t)x | (uintptr_t)xs | (uintptr_t)x2 | (uintptr_t)packed | (uintptr_t)packed2) & 15) != 0)
         return BEV_ERR_ARGS;
     if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0 ||
         Ho != (H2 - 1) / stride2 + 1 || Wo != (W2 - 1) / stride2 + 1)
@@ -1476,13 +1530,15 @@ int bev_conv2d_chain_dual_x6_f32(const float *x, int N, int H, int W, int Ci, co
     a.M = (int64_t)N * Ho * Wo;
     a.x2 = x2;
     a.Ci2 = Ci2, a.H2 = H2, a.W2 = W2, a.stride2 = stride2;
-    a.xs = nullptr;
+    a.xs = (const __bf16 *)xs;
     a.ys = nullptr;
-    a.xps = a.yps = 0;
+    a.xps = (int64_t)N * H * W * Ci;
+    a.yps = 0;
     a.wp2 = (const __bf16 *)packed2;
     a.bias2 = bias2;
     a.Co2 = Co2;
     a.act2 = act2;
+    if (xs) return launch_x6s<4, 1, 1, 2, 2>(a, (hipStream_t)stream);
     return launch_x6b<4, 1, 1, 2, false, 2>(a, (hipStream_t)stream);
 }
 

@@ -80,6 +80,10 @@ STEM_X6 = True
 # ... and, in the eval chain, with the stem max-pool fused into its epilogue (bev_conv2d_stem_pool_x6_f32,
 # bit-identical; False: the stem output is written and max-pooled by its own launch)
 STEM_POOL = True
+# The chained bottleneck bodies (chain6 / chaintail6) take conv1's output pre-split: conv1 writes h / m / l bf16 planes
+# (bev_conv2d_x6_f32 ys) and the chain stages conv2's operand by LDS-DMA with no split in its mainloop (k_conv_x6s
+# CHAIN).  Bit-identical either way; False: conv1 writes fp32 and the chain splits it once per tap (k_conv_x6b).
+SPLIT_CHAIN = True
 
 
 class FoldedConv:
@@ -556,7 +560,8 @@ class ResNet(nn.Module):
             h = fs[0](x, relu=True)
             return fs[1](h, x, out=out)
         if kind in ("chain6", "chaintail6"):
-            h = fs[0](x, relu=True)
+            split = SPLIT_CHAIN and fs[0].arith() == "bf16x6" and fs[0].conv.out_channels % 32 == 0
+            h = fs[0](x, relu=True, split_out=split)
             return fs[1](h, x, out=out, arith="bf16x6")
         if kind == "tail":
             h = fs[0](x, relu=True, split_out=self._split_edge(fs[0], fs[1]))

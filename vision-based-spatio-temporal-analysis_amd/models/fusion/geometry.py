@@ -300,7 +300,8 @@ class GeometryTransformer(nn.Module):
 
     def forward_fused(self, feats: torch.Tensor, intrinsics, extrinsics, img_size: Tuple[int, int] = (1080, 1920),
                       mode: str = "mean", rows_per_chunk: Optional[int] = None,
-                      memory_format: torch.memory_format = torch.contiguous_format) -> torch.Tensor:
+                      memory_format: torch.memory_format = torch.contiguous_format,
+                      num_chunks: Optional[int] = None) -> torch.Tensor:
         """SimpleFusion(mode)(self.forward(...)) in one kernel: [B,V,C,Hf,Wf] -> [B,C,H_bev,W_bev] (NCHW storage,
         as the reference's torch.mean over the stacked views gives).  memory_format=torch.channels_last (inference,
         channels-last features with C % 64 == 0): the same values in [B,H_bev,W_bev,C] storage
@@ -308,13 +309,14 @@ class GeometryTransformer(nn.Module):
         ~4 % slower than the NCHW one (profiles/r05as_warp_nhwc_ab.txt), so it is not the default.
         rows_per_chunk (< H_bev, inference only): the same values in rank-chunk-major row order,
         [ceil(H_bev / rows_per_chunk), B, C, rows_per_chunk, W_bev] (padding rows zero) -- the layout the camera-shard
-        reduce-scatter over BEV rows consumes without a permute (bev_dist.camera_sharded_forward)."""
+        reduce-scatter over BEV rows consumes without a permute (bev_dist.camera_sharded_forward); `num_chunks` (the
+        world size, >= that count) pads the layout with all-zero chunks to exactly that many."""
         H, xs, ys, hw = self._sampling(feats, intrinsics, extrinsics, img_size)
         grad = torch.is_grad_enabled() and feats.requires_grad
-        if rows_per_chunk is not None and rows_per_chunk < self.bev_h:
+        if rows_per_chunk is not None and (rows_per_chunk < self.bev_h or num_chunks):
             if grad:
                 raise RuntimeError("forward_fused(rows_per_chunk=...) is an inference layout (no autograd)")
-            return _nat.warp_fuse(feats, H, xs, ys, hw, mode, rows_per_chunk=rows_per_chunk)
+            return _nat.warp_fuse(feats, H, xs, ys, hw, mode, rows_per_chunk=rows_per_chunk, num_chunks=num_chunks)
         C = feats.shape[2]
         if (not grad and memory_format == torch.channels_last and feats.is_cuda and C % 64 == 0
                 and feats.stride(2) == 1 and feats.shape[1] <= 64):

@@ -185,6 +185,8 @@ class _HeadTrainH16(torch.autograd.Function):
                 gc = ctx.grad_channels
                 wt = w.flip(2, 3).transpose(0, 1)[:gc].contiguous()
                 da = torch.empty(dz.shape[0], dz.shape[1], dz.shape[2], cpi, device=dz.device, dtype=torch.float32)
+                if gc < cpi:  # the channels past gc are defined (zero), so a hook / anomaly check sees no garbage
+                    da[..., gc:].zero_()
                 _nat.conv2d_h16_any(dz, _nat.pack_conv_weight(wt), gc, K, K, 1, pad, dilation=dil, out=da)
             else:
                 da = None
@@ -211,7 +213,8 @@ class BEVDetector(nn.Module):
         self.stem = nn.Sequential(*layers)
         # leading operand channels that need a gradient (BEVNet: the P BEV feature channels -- its position-encoding
         # channels are a buffer); the AMP node's input gradient is computed for these alone, the rest of its
-        # channels are left unset (never read).  None: every input channel.
+        # channels are zero.  None: every input channel.  Owned by BEVNet (model_wrapper.py sets it when it builds
+        # the head); a standalone BEVDetector leaves it None.
         self.grad_channels = None
         self.heatmap_head = nn.Conv2d(128, 1, kernel_size=3, padding=1)
         self.offset_head = nn.Conv2d(128, 2, kernel_size=3, padding=1)
