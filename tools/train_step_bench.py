@@ -37,6 +37,8 @@ def main():
                     "instead of the forward's ReLU mask bytes (trunk_grad.RELU_MASK_BYTES)")
     ap.add_argument("--torch-loss", action="store_true", help="A/B: the focal and L1 losses as torch ops")
     ap.add_argument("--eager-decode", action="store_true", help="A/B: BEVNet.forward synchronises on its decode")
+    ap.add_argument("--loss-graph", action="store_true", help="A/B: BEVNet.loss as a replayed graph pair "
+                    "(model_wrapper.LOSS_GRAPHS)")
     ap.add_argument("--device-targets", action="store_true", help="A/B: the targets already on the device (the "
                     "reference's loop, train.py:228-243, leaves them in host memory)")
     ap.add_argument("--no-pool-arg", action="store_true", help="A/B: the stem max-pool saves its input and the backward "
@@ -53,6 +55,7 @@ def main():
     import models.model_wrapper as _mw
     _mw.LAZY_DECODE = not a.eager_decode
     _mw.NATIVE_LOSS = not a.torch_loss
+    _mw.LOSS_GRAPHS = a.loss_graph
     for kv in a.tune:
         name, v = kv.split("=")
         bev_native.tune(getattr(bev_native, "TUNE_" + name.upper()), int(v))

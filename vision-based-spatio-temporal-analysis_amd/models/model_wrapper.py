@@ -49,6 +49,16 @@ LAZY_DECODE = True
 # tools/train_step_bench.py --torch-loss)
 NATIVE_LOSS = True
 
+# BEVNet.loss in a training step replays the target construction + loss terms as one captured graph pair
+# (torch.cuda.make_graphed_callables): ~50 small launches become two graph launches, so the loss no longer waits on
+# the host between the forward and the backward.  Only with NATIVE_LOSS: in this PyTorch / ROCm build a torch
+# reduction over more than one workgroup (x.sum() over the 691 k heatmap cells) gives wrong results when replayed
+# from a HIP graph -- from the second replay on in isolation (tools/graph_reduce_check.py), the fifth inside the
+# round-5 loss graph, whose torch-op focal loss returned -375 (profiles/r06e_loss_graph_cause.txt) -- while the
+# native loss kernels (per-workgroup double partials, no cross-workgroup semaphore) replay bit-identically.
+# A/B: tools/train_step_bench.py --loss-graph.
+LOSS_GRAPHS = False  # measured neutral with the native losses (r06f: 52.3-52.4 vs 52.3-52.5 ms), kept as an A/B
+
 
 class _FocalLoss(torch.autograd.Function):
     """The focal heatmap loss (model_wrapper.py:235-247) on the native kernels; gradient for the logits only (the
@@ -275,11 +285,46 @@ class BEVNet(nn.Module):
 
     # ---- training objective (model_wrapper.py:105-247) --------------------------
     def loss(self, preds: Dict, targets: List[Dict], loss_cfg: Dict[str, Any]) -> Dict[str, torch.Tensor]:
-        t = self._build_training_targets(targets)
+        pr = (preds["heatmap_logits"], preds["offset"], preds["size_raw"])
+        if (LOSS_GRAPHS and NATIVE_LOSS and all(a.is_cuda for a in pr) and torch.is_grad_enabled()
+                and any(a.requires_grad for a in pr)):
+            boxes, frame, bound = self._target_boxes(targets, pr[0].device, pad=16)
+            if bound is not None and boxes.shape[0] > 0:  # host targets: targets + loss terms as one graph pair
+                B = len(targets)
+                outs = self._graphed((B, bound), pr + (boxes, frame),
+                                     lambda *a: self._loss_from_boxes(*a, B=B, bound=bound))
+                # the graph's outputs live in its static buffers (overwritten by the next replay): one stack copies
+                hm_loss, off_loss, size_loss, total = torch.stack(outs).unbind(0)
+                return {"heatmap_loss": hm_loss, "offset_loss": off_loss, "size_loss": size_loss, "total_loss": total}
+            t = self._targets_from_boxes(boxes, frame, bound, len(targets))
+        else:
+            t = self._build_training_targets(targets)
         hm_loss, off_loss, size_loss, total = self._loss_terms(
-            preds["heatmap_logits"], preds["offset"], preds["size_raw"], t["heatmap"], t["indices"], t["mask"],
-            t["offset"], t["size_log"])
+            *pr, t["heatmap"], t["indices"], t["mask"], t["offset"], t["size_log"])
         return {"heatmap_loss": hm_loss, "offset_loss": off_loss, "size_loss": size_loss, "total_loss": total}
+
+    def _loss_from_boxes(self, logits, offset, size_raw, boxes, frame, B: int, bound: int):
+        t = self._targets_from_boxes(boxes, frame, bound, B)
+        return self._loss_terms(logits, offset, size_raw, t["heatmap"], t["indices"], t["mask"], t["offset"],
+                                t["size_log"])
+
+    def _graphed(self, extra: tuple, args, fn):
+        """fn(*args) captured as a HIP graph pair (forward, backward) per input signature
+        (torch.cuda.make_graphed_callables) and replayed -- the same kernels on the same values, bit-identical to the
+        eager loss (tests/test_targets.py::test_graphed_loss_replays_bit_identical).  Captured with autocast off:
+        every loss input is fp32 and the native loss kernels compute in fp32 under autocast(float16) as well."""
+        key = extra + tuple((tuple(a.shape), a.dtype, a.requires_grad, a.device) for a in args)
+        key += (self.hm_weight, self.offset_weight, self.size_weight, self.hm_alpha, self.hm_beta, self.max_objects)
+        graphs = self.__dict__.setdefault("_loss_graphs", {})
+        g = graphs.get(key)
+        if g is None and len(graphs) >= 8:  # many target signatures (radius bounds, box counts): stay eager
+            return fn(*args)
+        if g is None:
+            samples = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
+            with torch.autocast("cuda", enabled=False):
+                g = torch.cuda.make_graphed_callables(fn, samples, allow_unused_input=True)
+            graphs[key] = g
+        return g(*args)
 
     def _loss_terms(self, logits, offset, size_raw, hm, indices, mask, off_t, size_t):
         """model_wrapper.py:105-124: the focal heatmap loss and the masked L1 offset / log-size losses."""
@@ -294,12 +339,15 @@ class BEVNet(nn.Module):
         total = self.hm_weight * hm_loss + self.offset_weight * off_loss + self.size_weight * size_loss
         return hm_loss, off_loss, size_loss, total
 
-    def _target_boxes(self, targets: List[Dict], dev) -> Tuple[torch.Tensor, torch.Tensor, Optional[int]]:
+    def _target_boxes(self, targets: List[Dict], dev, pad: int = 0
+                      ) -> Tuple[torch.Tensor, torch.Tensor, Optional[int]]:
         """All frames' boxes [N, 4] (cx, cy, w, h; centre-only targets get DEFAULT_BOX_WH) + frame index [N] on
         `dev`, and an upper bound of the objects' gaussian radii when it is known without waiting for the device.
         The reference's loader hands the targets over in host memory (train.py:228-243 moves only the images and
         calibration): then the boxes go over in one pinned, asynchronous copy and the bound comes from the host
-        values; boxes already on the device give None (the splat then reads its bound back, one sync)."""
+        values; boxes already on the device give None (the splat then reads its bound back, one sync).  `pad`: host
+        boxes are padded to a multiple of it by out-of-grid dummies of the last frame (no slot, no gaussian: the
+        targets are unchanged), so a captured loss graph serves every box count up to that multiple."""
         boxes, frame = [], []
         for b, tgt in enumerate(targets):
             bx = tgt.get("boxes_world", None)
@@ -319,6 +367,12 @@ class BEVNet(nn.Module):
         if all(not t.is_cuda for t in boxes):
             bh, fh = torch.cat(boxes), torch.cat(frame)
             bound = self._radius_bound_host(bh)
+            if pad and bh.shape[0] % pad:
+                x_min, _, y_min, _ = self.bounds
+                n = pad - bh.shape[0] % pad
+                dummy = bh.new_tensor([x_min - 1e6 * self.res_x, y_min - 1e6 * self.res_y, self.res_x, self.res_y])
+                bh = torch.cat([bh, dummy.expand(n, 4)])
+                fh = torch.cat([fh, fh.new_full((n,), len(targets) - 1)])
             if dev.type == "cuda":
                 bh, fh = bh.pin_memory(), fh.pin_memory()
             return bh.to(dev, non_blocking=True), fh.to(dev, non_blocking=True), bound
@@ -390,7 +444,7 @@ class BEVNet(nn.Module):
         offset = torch.zeros(B, M + 1, 2, device=dev)
         size_log = torch.zeros(B, M + 1, 2, device=dev)
         indices[frame, s] = cyl * Wb + cxl
-        mask[frame, s] = 1.0
+        mask[frame, s] = torch.ones((), device=dev)  # a device scalar: no host-to-device copy (graph capture)
         offset[frame, s] = torch.stack([gx - cx, gy - cy], dim=1)
         size_log[frame, s] = torch.stack([w_cells.log(), h_cells.log()], dim=1)
         if NATIVE_LOSS and w_cells.is_cuda:  # the same float32 op sequence in one launch
