@@ -25,12 +25,15 @@ import backbone_ref
 from oracle import reference_grid_cpu
 
 
-def head_forward(det, x, masks=None):
-    """detector.py:47-62 with det's parameters (any dtype / device of det)."""
+def head_forward(det, x, masks=None, check=None):
+    """detector.py:47-62 with det's parameters (any dtype / device of det).  `check(pre_activation, mask)`, when given,
+    sees each injected ReLU mask beside the reference's own pre-activation (tests compare their signs)."""
     a = x
     for j, (i, d) in enumerate(((0, 1), (3, 2), (6, 1))):
         a = F.conv2d(a, det.stem[i].weight, padding=d, dilation=d)
         a = F.group_norm(a, 32, det.stem[i + 1].weight, det.stem[i + 1].bias, det.stem[i + 1].eps)
+        if masks is not None and check is not None:
+            check(a, masks[j])
         a = torch.relu(a) if masks is None else a * masks[j]
     hm = F.conv2d(a, det.heatmap_head.weight, det.heatmap_head.bias, padding=1)
     off = F.conv2d(a, det.offset_head.weight, det.offset_head.bias, padding=1)
@@ -39,7 +42,7 @@ def head_forward(det, x, masks=None):
             "size": torch.exp(size), "size_raw": size}
 
 
-def bevnet_train_forward(net, images, K, Rt, trunk_act=None, head_masks=None):
+def bevnet_train_forward(net, images, K, Rt, trunk_act=None, head_masks=None, head_check=None):
     """net: a float64 CPU BEVNet (lazy modules materialised, timm ResNet trunk); images [B,V,3,H,W] f64;
     K [B,V,3,3], Rt [B,V,4,4] fp32 (the grid is built in fp32 like the reference).  Returns the prediction
     dict of BEVNet.forward without the decoded boxes."""
@@ -55,6 +58,6 @@ def bevnet_train_forward(net, images, K, Rt, trunk_act=None, head_masks=None):
     cat = warped.reshape(B, V * C, net.bev_h, net.bev_w)
     main = F.conv2d(cat, net.proj.weight, net.proj.bias)
     bev = torch.cat([main, net.pos_enc.to(main.dtype).unsqueeze(0).expand(B, -1, -1, -1)], dim=1)
-    out = head_forward(net.detector, bev, head_masks)
+    out = head_forward(net.detector, bev, head_masks, head_check)
     out["bev_feat"] = bev
     return out

@@ -551,16 +551,35 @@ def test_bevnet_r50_ddp_world2_trainable_trunk_amp():
     assert res[0][5] == res[1][5] and res[0][5] in (65536.0, 32768.0, 16384.0)
 
 
-K3_TRAINABLE_REF = ("encoder.backbone.layer2.3.", "encoder.proj.", "proj.", "detector.")
+# the parameters whose gradients the full-geometry test compares: the head, the BEV / encoder projections, the last
+# trunk block, the first layer1 block and the stem -- so the reference's autograd runs through the whole trunk
+K3_TRAINABLE_REF = ("encoder.backbone.layer2.3.", "encoder.backbone.layer1.0.", "encoder.backbone.conv1.",
+                    "encoder.backbone.bn1.", "encoder.proj.", "proj.", "detector.")
 
 
-def k3_reference_step(model_cpu_state, cfg, imgs, K, Rt, t_ref, boxes, trunk_masks, head_masks, scale, half):
+def _mask_sign_check(stats, name, rel_band=1e-4):
+    """check(pre_activation, mask) for the reference forward: the native run's ReLU decision (mask) against the sign of
+    the reference's own pre-activation.  Records per layer (name, elements, disagreements, disagreements outside the
+    band |pre| <= rel_band max|pre|, largest |pre| of a disagreement relative to max|pre|)."""
+    def check(t, m):
+        t = t.detach()
+        band = rel_band * float(t.abs().max())
+        dis = (t > 0) != (m > 0)
+        out = dis & (t.abs() > band)
+        worst = float(t.abs()[dis].max()) / max(band / rel_band, 1e-300) if bool(dis.any()) else 0.0
+        stats.append((f"{name}{len(stats)}", t.numel(), int(dis.sum()), int(out.sum()), worst))
+    return check
+
+
+def k3_reference_step(model_cpu_state, cfg, imgs, K, Rt, t_ref, boxes, trunk_masks, head_masks, scale, half,
+                      sign_stats=None, sign_band=1e-4):
     """The reference graph of one K3 training step at full geometry, in float64 and float32 on the CPU, with the
     native run's ReLU decisions (bool masks, in execution order) and, under AMP, the native fp16 operand
     roundings (_H16Conv).  Only the parameters the full-geometry test compares take gradients -- the head, the BEV
-    projection, the encoder projection and the last trunk block (K3_TRAINABLE_REF) -- so autograd stops at
-    layer2's last block and the float64 trunk runs forward only below it.  Returns {dtype: (outputs, losses,
-    {name: grad})}."""
+    projection, the encoder projection, the last trunk block, layer1's first block and the stem
+    (K3_TRAINABLE_REF).  `sign_stats` (a list): the float64 pass records, per ReLU, how the injected native mask
+    agrees with the sign of the reference's own pre-activation (_mask_sign_check).  Returns {dtype: (outputs,
+    losses, {name: grad})}."""
     import bevnet_ref
     res = {}
     if half:
@@ -574,8 +593,17 @@ def k3_reference_step(model_cpu_state, cfg, imgs, K, Rt, t_ref, boxes, trunk_mas
                 p.requires_grad_(k.startswith(K3_TRAINABLE_REF))
             net._build_training_targets = lambda _t: t_ref
             it = iter(trunk_masks)
-            out = bevnet_ref.bevnet_train_forward(net, imgs.to(dt), K, Rt, trunk_act=lambda t: t * next(it).to(dt),
-                                                  head_masks=[m.to(dt) for m in head_masks])
+            rec = sign_stats is not None and dt == torch.float64
+            tcheck = _mask_sign_check(sign_stats, "trunk", sign_band) if rec else None
+            hcheck = _mask_sign_check(sign_stats, "head", sign_band) if rec else None
+
+            def trunk_act(t):
+                m = next(it).to(dt)
+                if tcheck is not None:
+                    tcheck(t, m)
+                return t * m
+            out = bevnet_ref.bevnet_train_forward(net, imgs.to(dt), K, Rt, trunk_act=trunk_act,
+                                                  head_masks=[m.to(dt) for m in head_masks], head_check=hcheck)
             ls = net.loss(out, [{"boxes_world": b.to(dt)} for b in boxes], cfg["LOSS"])
             ls["total_loss"].backward()
             print(f"k3_reference_step: {dt} forward + backward done", flush=True)  # progress (pytest -s)
@@ -595,8 +623,11 @@ def test_bevnet_r50_amp_step_full_geometry():
     shape: B = 1 frame, 7 cameras x 3 x 1080 x 1920, ResNet-50 trunk trainable with batch-statistics BN, FEAT_DIM
     64, BEV 480 x 1440, BEV_PROJ_CH 128 = configs/wildtrack.yaml:14; autocast float16 + GradScaler, train.py:238-247)
     vs the float64 / float32 torch restatement of the reference graph: the outputs, the four losses and the
-    gradients of the head, the BEV projection, the encoder projection and the last trunk block, with
-    test_bevnet_r50_training_step_vs_float64_reference's bar (error <= 4 x the fp32 reference's own error + floor).
+    gradients of the head, the BEV projection, the encoder projection, the last trunk block, layer1's first block and
+    the stem, with test_bevnet_r50_training_step_vs_float64_reference's bar (error <= 4 x the fp32 reference's own
+    error + floor).  The reference is driven by the native run's ReLU decisions; every one of them is checked against
+    the sign of the reference's own pre-activation (outside a band of 2e-3 of the layer's max under AMP, and at most
+    1e-3 of a layer's elements inside it), so a native kernel that wrongly zeroed activations cannot pass.
     Covers at full size what the reduced-size test cannot: the fp16 conv tiles and the BatchNorm epilogue-statistics
     partial counts over 7 x 270 x 480 pixels, the 512-channel head over 691 k cells, the fused-warp backward on
     the bench rig."""
@@ -684,9 +715,31 @@ def test_bevnet_r50_amp_step_full_geometry():
         m.load_state_dict(state, strict=True)
         return m
 
+    signs = []
+    # band of the sign check: 1e-4 of the layer's max |pre-activation| for fp32 kernels; under AMP 2e-3 (4 fp16 ulps)
+    # -- the fp16 operand roundings are emulated in the reference, but an operand that sits on an fp16 rounding
+    # boundary can round to the other neighbour after fp32 accumulation-order differences (2^-11 = 4.9e-4 relative)
+    # and the shifts cascade through the trunk (r06g: disagreements up to 1.4e-4 of the max in layer1, 1.0e-3 in
+    # layer2)
+    sign_band = 2e-3 if half else 1e-4
+    # ... and the share of elements that may flip inside the band: every element closer to 0 than the native-vs-
+    # reference noise is a coin flip -- r06g: 1.6e-4 of layer1.2's 3x3 ReLU (9,387 of 58 M), 4.5e-4 of a layer2 ReLU
+    # (13,161 of 29 M); 1e-3 bounds that (fp32 kernels: 1e-4)
+    sign_frac = 1e-3 if half else 1e-4
     res = k3_reference_step(ref_copy, cfg, imgs, K, Rt, t_ref, boxes, trunk_masks, head_masks,
-                            float(scaler.get_scale()), half)
+                            float(scaler.get_scale()), half, sign_stats=signs, sign_band=sign_band)
     (o64, l64, g64), (o32, l32, g32) = res[torch.float64], res[torch.float32]
+    import resource
+    print(f"full-geometry K3: peak host RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20:.1f} GiB",
+          flush=True)
+    # the native ReLU decisions the reference was driven by agree with the reference's own pre-activation signs:
+    # everywhere outside |pre| <= sign_band max|pre|, and in at most sign_frac of a layer's elements overall (a native
+    # bug that zeroed activations would be copied into the reference otherwise)
+    assert len(signs) == len(trunk_masks) + len(head_masks), (len(signs), len(trunk_masks), len(head_masks))
+    for name, n, dis, out_band, rel in signs:
+        assert out_band == 0 and dis <= sign_frac * n, (name, n, dis, out_band, rel)
+    print("ReLU sign agreement (layer, elements, disagreements, outside band, worst |pre| / max):",
+          sorted(signs, key=lambda s: -s[2])[:4])
     worst = []
 
     def bounded(native, r64, r32, what, floor=1e-5):
