@@ -73,7 +73,7 @@ def run_dual(name, iters):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     flops = 2 * N * Ho * Wo * Co * (Ci + Ci2)
-    byts = 4 * (h.numel() + N * Ho * Wo * Ci2 + out.numel())
+    byts = 4 * (N * H * W * Ci + N * Ho * Wo * Ci2 + out.numel())
     print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
 
 
@@ -97,8 +97,11 @@ def run_chain_dual(name, iters):
     g = torch.Generator(device=dev).manual_seed(0)
     h = torch.randn(N, H, W, Ci, device=dev, generator=g)
     x = torch.randn(N, H, W, Ci2, device=dev, generator=g)
-    p1 = nat.pack_conv_weight(torch.randn(Co, Ci, 3, 3, device=dev, generator=g) * (2.0 / (Ci * 9)) ** 0.5)
-    p2 = nat.pack_conv_weight(torch.randn(Co2, Co + Ci2, 1, 1, device=dev, generator=g) * (2.0 / (Co + Ci2)) ** 0.5)
+    pk = nat.pack_conv_weight_x6 if ARITH == "bf16x6" else nat.pack_conv_weight
+    p1 = pk(torch.randn(Co, Ci, 3, 3, device=dev, generator=g) * (2.0 / (Ci * 9)) ** 0.5)
+    p2 = pk(torch.randn(Co2, Co + Ci2, 1, 1, device=dev, generator=g) * (2.0 / (Co + Ci2)) ** 0.5)
+    if SPLIT_IN and ARITH == "bf16x6":
+        h = nat.split3(h)  # conv1's split output (k_conv_x6s CHAIN)
     b1, b2 = torch.randn(Co, device=dev, generator=g), torch.randn(Co2, device=dev, generator=g)
     out = torch.empty(N, Ho, Wo, Co2, device=dev)
     for _ in range(3):
@@ -111,7 +114,7 @@ def run_chain_dual(name, iters):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     flops = 2 * N * Ho * Wo * (Co * Ci * 9 + Co2 * (Co + Ci2))
-    byts = 4 * (h.numel() + N * Ho * Wo * Ci2 + out.numel())
+    byts = 4 * (N * H * W * Ci + N * Ho * Wo * Ci2 + out.numel())
     print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
 
 
@@ -121,8 +124,11 @@ def run_chain(name, iters):
     g = torch.Generator(device=dev).manual_seed(0)
     h = torch.randn(N, H, W, Ci, device=dev, generator=g)
     x = torch.randn(N, H, W, Co2, device=dev, generator=g)
-    p1 = nat.pack_conv_weight(torch.randn(Co, Ci, 3, 3, device=dev, generator=g) * (2.0 / (Ci * 9)) ** 0.5)
-    p2 = nat.pack_conv_weight(torch.randn(Co2, Co, 1, 1, device=dev, generator=g) * (2.0 / Co) ** 0.5)
+    pk = nat.pack_conv_weight_x6 if ARITH == "bf16x6" else nat.pack_conv_weight
+    p1 = pk(torch.randn(Co, Ci, 3, 3, device=dev, generator=g) * (2.0 / (Ci * 9)) ** 0.5)
+    p2 = pk(torch.randn(Co2, Co, 1, 1, device=dev, generator=g) * (2.0 / Co) ** 0.5)
+    if SPLIT_IN and ARITH == "bf16x6":
+        h = nat.split3(h)  # conv1's split output (k_conv_x6s CHAIN)
     b1, b2 = torch.randn(Co, device=dev, generator=g), torch.randn(Co2, device=dev, generator=g)
     out = torch.empty(N, H, W, Co2, device=dev)
     for _ in range(3):
@@ -135,7 +141,7 @@ def run_chain(name, iters):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
     flops = 2 * N * H * W * Co * (Ci * 9 + Co2)
-    byts = 4 * (h.numel() + x.numel() + out.numel())
+    byts = 4 * (N * H * W * Ci + x.numel() + out.numel())
     print(f"{name:8s} {ms * 1e3:8.1f} us  {flops / ms / 1e9:6.1f} TF  {byts / ms / 1e6:7.1f} GB/s(io)", flush=True)
 
 

@@ -41,6 +41,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
+#ifndef X6S_ABLATE
+#define X6S_ABLATE 0  // timing builds only (chains) (wrong results): 1 no chain epilogue, 2 no mainloop MFMAs, 4 no operand DMA
+#endif
 constexpr int XBK = 16;   // K step
 constexpr int XROW = 24;  // bf16 per LDS row (48 B)
 
@@ -730,6 +733,15 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
 #undef X6B_SWRITE
 #undef X6B_GLOAD
     if constexpr (CHAIN > 0) {
+        if (X6S_ABLATE & 1) {  // timing only: one store per lane keeps the mainloop live
+            float s_ = 0.0f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) s_ += acc[i][j][0] + acc[i][j][15];
+            if (m0 + tid < a.M) a.y[(m0 + tid) * a.Co2] = s_;
+            return;
+        }
         x6_chain_epilogue<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0>(a, lds_raw, acc, wave, lane, wm, wn, m0);
         return;
     }
@@ -821,6 +833,7 @@ __global__ __launch_bounds__(256, CHAIN ? 2 : 3) void k_conv_x6s(ConvX a) {
     int ky = 0, kx = 0, ci0 = 0, kstep = 0;
     const __bf16 *bsrc = a.wp + (int64_t)(n0 >> 5) * S * 1536 + lane * 8;  // the block's first column block
     auto issue = [&](int buf) {
+        if (X6S_ABLATE & 4) return;
         if constexpr (BLDS) {  // piece q = (cb, slice, plane) of this K step: panel run ((cb S + 2 ks + sl) 3 + p)
             const unsigned db = lbase + (unsigned)(buf * STAGE * 2 + 3 * APL * 2);
 #pragma unroll
@@ -875,6 +888,12 @@ __global__ __launch_bounds__(256, CHAIN ? 2 : 3) void k_conv_x6s(ConvX a) {
             const int ph = (2 * (KK) + h) ^ ((R >> 2) & 3);                                                \
             _Pragma("unroll") for (int p = 0; p < 3; ++p)                                                  \
                 fa[i][p] = *(const bf16x8 *)(AS + p * APL + R * 32 + ph * 8);                              \
+        }                                                                                                  \
+        if (X6S_ABLATE & 2) {                                                                              \
+            _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                 \
+                _Pragma("unroll") for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fa[i][0]), "v"(fa[i][1]), \
+                                                                  "v"(fa[i][2]), "v"(BC[j][0]), "v"(BC[j][1]), "v"(BC[j][2])); \
+            break;                                                                                         \
         }                                                                                                  \
         _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                     \
             _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                               \
@@ -934,6 +953,15 @@ __global__ __launch_bounds__(256, CHAIN ? 2 : 3) void k_conv_x6s(ConvX a) {
 #undef X6S_SLICE
 #undef X6S_BLOAD
     if constexpr (CHAIN > 0) {
+        if (X6S_ABLATE & 1) {  // timing only: one store per lane keeps the mainloop live
+            float s_ = 0.0f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) s_ += acc[i][j][0] + acc[i][j][15];
+            if (m0 + tid < a.M) a.y[(m0 + tid) * a.Co2] = s_;
+            return;
+        }
         x6_chain_epilogue<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0>(a, lds_raw, acc, wave, lane, wm, wn, m0);
         return;
     }
