@@ -527,6 +527,21 @@ int bev_conv2d_chain_dual_x6_f32(const float *x, const uint16_t *xs, int N, int 
                                  const uint16_t *packed2, const float *bias2, int Co2, int act2, float *y, int Ho,
                                  int Wo, void *stream);
 
+/* device: a pre-split chained bottleneck body (bev_conv2d_chain_x6_f32 with xs, identity residual) that also runs
+ * the NEXT block's 1x1 conv on the block output it has just computed: y = the block output [N][Ho][Wo][Co2] fp32 as
+ * before, and h3 = act3(y (*) W3 + bias3) with packed3 the split panel of [Co3][Co2][1][1], written split (ys3
+ * [3][N][Ho][Wo][Co3] bf16, 8-B aligned) or fp32 (y3 [N][Ho][Wo][Co3]) -- exactly one of them.  h3 equals
+ * bev_conv2d_x6_f32 over y (same K order); y never makes the HBM round trip the separate 1x1 launch would read it by
+ * (timm Bottleneck.conv1 of block k + 1, cnn_encoder.py:26).  Co == 64 (the 128-row tile), Co3 in {64, 128},
+ * Co2 % 64 == 0, 16-B aligned operands.  x2 (the dual block-0 form) is reserved: non-NULL returns BEV_ERR_ARGS
+ * (its kernel was not repeatable at the bench size). */
+int bev_conv2d_chain_next_x6_f32(const uint16_t *xs, int N, int H, int W, int Ci, const uint16_t *packed,
+                                 const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
+                                 const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
+                                 const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
+                                 const uint16_t *packed3, const float *bias3, int Co3, int act3, float *y3,
+                                 uint16_t *ys3, void *stream);
+
 /* device: the ResNet stem (timm conv1: 7x7, stride 2, pad 3, Ci = 3; cnn_encoder.py:26, the first layer of
  * CNNEncoder._encode_single) in the split arithmetic: x NCHW [N][3][H][W] fp32 images, packed = the split panel of
  * the (BN-folded) [Co][3][7][7] weights (bev_conv_pack_weights_x6, 16-B aligned), Co <= 64; y NHWC [N][Ho][Wo][Co]

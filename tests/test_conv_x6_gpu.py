@@ -218,6 +218,63 @@ def test_x6_chain_dual_pre_split_operand_bit_identical():
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("Co3,dual,split_out,N,H,W", [(64, False, True, 2, 25, 37), (128, False, False, 1, 31, 70),
+                                                      (64, True, True, 2, 27, 45), (128, False, True, 3, 7, 130)])
+def test_x6_chain_next_conv_bit_identical(Co3, dual, split_out, N, H, W):
+    """bev_conv2d_chain_next_x6_f32 (a pre-split chain that also runs the next block's 1x1 conv in its epilogue, conv3
+    computed transposed): y == the pre-split chain's y, and h3 == bev_conv2d_x6_f32 over y (split or fp32 output),
+    bit for bit -- ragged M, 7-pixel-row images.  The dual (block 0) form is refused (BEV_ERR_ARGS)."""
+    g = torch.Generator().manual_seed(Co3 + 3 * H + dual)
+    Ci, Co, Co2 = 64, 64, 256
+    x = torch.randn(N, H, W, Ci, generator=g).to(DEV)
+    w2 = (torch.randn(Co, Ci, 3, 3, generator=g) / (9 * Ci) ** 0.5).to(DEV)
+    w3 = (torch.randn(Co2, Co + (64 if dual else 0), 1, 1, generator=g) / Co ** 0.5).to(DEV)
+    wn = (torch.randn(Co3, Co2, 1, 1, generator=g) / Co2 ** 0.5).to(DEV)
+    b2, b3 = (torch.randn(Co, generator=g) * 0.1).to(DEV), (torch.randn(Co2, generator=g) * 0.1).to(DEV)
+    bn = (torch.randn(Co3, generator=g) * 0.1).to(DEV)
+    p2, p3, pn = nat.pack_conv_weight_x6(w2), nat.pack_conv_weight_x6(w3), nat.pack_conv_weight_x6(wn)
+    xs = nat.split3(x)
+    if dual:
+        xb = torch.randn(N, H, W, 64, generator=g).to(DEV)
+        with pytest.raises(nat.HipError):
+            nat.conv2d_chain_next_nhwc(xs, p2, b2, Co, 3, 3, 1, 1, 1, p3, b3, Co2, 1, pn, bn, Co3, 1, x2=xb,
+                                       split3_out=split_out)
+        return
+    else:
+        res = torch.randn(N, H, W, Co2, generator=g).to(DEV)
+        ref = nat.conv2d_chain_nhwc(xs, p2, b2, Co, 3, 3, 1, 1, 1, p3, b3, Co2, 1, residual=res)
+        y, h3 = nat.conv2d_chain_next_nhwc(xs, p2, b2, Co, 3, 3, 1, 1, 1, p3, b3, Co2, 1, pn, bn, Co3, 1, residual=res,
+                                           split3_out=split_out)
+    ref3 = nat.conv2d_nhwc_x6(ref, pn, bn, Co3, 1, 1, 1, 0, 1, 1, split_out=split_out)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    if split_out:
+        assert torch.equal(h3.planes, ref3.planes)
+    else:
+        assert torch.equal(h3, ref3)
+
+
+def test_x6_resnet50_encoder_fused_next_conv1_bit_identical():
+    """The ResNet-50 encoder with the layer1 chains running the next block's conv1 (resnet.FUSE_NEXT_CONV1, default)
+    == with every conv1 its own launch, bit for bit."""
+    from models.encoders import resnet
+    from models.encoders.cnn_encoder import CNNEncoder
+    torch.manual_seed(2)
+    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(DEV)
+    imgs = torch.randn(2, 3, 3, 120, 200, device=DEV)
+    old = resnet.FUSE_NEXT_CONV1
+    try:
+        with torch.no_grad(), nat.conv_arith_mode("bf16x6"):
+            resnet.FUSE_NEXT_CONV1 = False
+            ref = enc(imgs).float().clone()
+            resnet.FUSE_NEXT_CONV1 = True
+            got = enc(imgs).float().clone()
+    finally:
+        resnet.FUSE_NEXT_CONV1 = old
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 def test_x6_resnet50_encoder_split_chain_bit_identical():
     """The ResNet-50 encoder with conv1 -> chain edges pre-split (resnet.SPLIT_CHAIN, the default) == with them fp32."""
     from models.encoders import resnet

@@ -23,9 +23,12 @@ from models.encoders.cnn_encoder import CNNEncoder  # noqa: E402
 
 def apply(name, rn):
     resnet.SPLIT_CHAIN = True
+    resnet.FUSE_NEXT_CONV1 = False
     rn.split_edges = False
     if name == "nosplitchain":
         resnet.SPLIT_CHAIN = False
+    elif name == "fuse":
+        resnet.FUSE_NEXT_CONV1 = True
     elif name == "splitedges":
         rn.split_edges = True
     elif name != "base":

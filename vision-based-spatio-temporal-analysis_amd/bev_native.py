@@ -153,6 +153,8 @@ SIGNATURES = {
     "bev_conv2d_chain_x6_f32": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i,
                                      _vp, _i, _i, _vp]),
     "bev_conv2d_dual_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp]),
+    "bev_conv2d_chain_next_x6_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _i, _i, _i, _i,
+                                          _vp, _vp, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp]),
 }
 
 
@@ -1211,6 +1213,45 @@ def conv2d_chain_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: 
                                         _ptr(out), Ho, Wo, _stream(x))
     _check(rc, "bev_conv2d_chain_f32")
     return out
+
+
+def conv2d_chain_next_nhwc(xs: "Split3", packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int, pad: int,
+                           relu: int, packed2: torch.Tensor, bias2, Co2: int, relu2: int, packed3: torch.Tensor, bias3,
+                           Co3: int, relu3: int, residual: torch.Tensor = None, x2: torch.Tensor = None,
+                           stride2: int = 1, out: torch.Tensor = None, split3_out: bool = True):
+    """A pre-split chained bottleneck body (conv2d_chain_nhwc with a Split3 x; with x2 the dual form of
+    conv2d_chain_dual_nhwc) that also runs the next block's 1x1 conv on the block output it computes
+    (bev_conv2d_chain_next_x6_f32): returns (y [N,Ho,Wo,Co2] fp32, h3) with h3 = act3(y (*) W3 + bias3) as a Split3
+    (split3_out) or fp32 [N,Ho,Wo,Co3] -- bit-identical to conv2d_nhwc_x6 over y, without reading y back."""
+    if not isinstance(xs, Split3) or not (packed.dtype == packed2.dtype == packed3.dtype == torch.bfloat16):
+        raise HipError("conv2d_chain_next_nhwc takes a Split3 operand and split-bf16 panels")
+    if not xs.planes.is_cuda:
+        raise HipError("the pre-split operand must be on the device")
+    _require_gpu(bias, bias2, bias3, residual, x2)
+    N, H, W, Ci = xs.shape
+    Ho, Wo = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    dev = xs.device
+    if out is None:
+        out = torch.empty(N, Ho, Wo, Co2, device=dev, dtype=torch.float32)
+    assert out.shape == (N, Ho, Wo, Co2) and out.is_contiguous()
+    if residual is not None:
+        residual = residual.contiguous()
+        assert residual.shape == out.shape
+    H2 = W2 = Ci2 = 0
+    if x2 is not None:
+        x2 = x2.contiguous()
+        _, H2, W2, Ci2 = x2.shape
+    if split3_out:
+        ys3, y3 = torch.empty(3, N, Ho, Wo, Co3, device=dev, dtype=torch.bfloat16), None
+    else:
+        ys3, y3 = None, torch.empty(N, Ho, Wo, Co3, device=dev, dtype=torch.float32)
+    with _span("conv", xs.planes):
+        rc = lib().bev_conv2d_chain_next_x6_f32(
+            _ptr(xs.planes), N, H, W, Ci, _ptr(packed), _ptr(bias), Co, KH, KW, stride, pad, int(relu), _ptr(x2), H2,
+            W2, Ci2, stride2, _ptr(packed2), _ptr(bias2), Co2, _ptr(residual), int(relu2), _ptr(out), Ho, Wo,
+            _ptr(packed3), _ptr(bias3), Co3, int(relu3), _ptr(y3), _ptr(ys3), _stream(xs.planes))
+    _check(rc, "bev_conv2d_chain_next_x6_f32")
+    return out, (Split3(ys3) if split3_out else y3)
 
 
 def conv2d_chain_dual_nhwc(x: torch.Tensor, packed: torch.Tensor, bias, Co: int, KH: int, KW: int, stride: int,

@@ -41,6 +41,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
+// pre-split chains without a fused next conv: 1 = conv3 transposed (x6_chain_epilogue_t), 0 = x6_chain_epilogue.
+// r06m A/B (7 x 1080p ResNet-50 encoder): the transposed epilogue's per-pixel float4 residual loads / y stores (32
+// rows x 32 B per instruction) cost ~0.1 ms per launch over the row-contiguous dword form, so only the chains that
+// run the next conv (NT3 > 0, which needs the transposed layout) take it.
+#ifndef X6S_T_EPI
+#define X6S_T_EPI 0
+#endif
 #ifndef X6S_ABLATE
 #define X6S_ABLATE 0  // timing builds only (chains) (wrong results): 1 no chain epilogue, 2 no mainloop MFMAs, 4 no operand DMA
 #endif
@@ -107,6 +114,13 @@ struct ConvX {
     const float *__restrict__ bias2;
     int Co2, act2;
     int nta = 0;  // 1: A (activation) loads non-temporal (BEV_TUNE_CONV_X6_NT, the last layer of a trunk)
+    // the next block's 1x1 conv fused into a chain's epilogue (x6_chain_epilogue_t NT3 > 0): h3 = act3(y (*) W3 + b3)
+    // from the block output y the chain just computed, written split (ys3 [3][M][Co3] bf16) or fp32 (y3 [M][Co3])
+    const __bf16 *__restrict__ wp3 = nullptr;
+    const float *__restrict__ bias3 = nullptr;
+    __bf16 *__restrict__ ys3 = nullptr;
+    float *__restrict__ y3 = nullptr;
+    int Co3 = 0, act3 = 0;
 };
 
 __device__ __forceinline__ float act_x(float t, int act) {
@@ -541,6 +555,231 @@ __device__ __forceinline__ void x6_chain_epilogue(const ConvX &a, unsigned char 
 }
 
 // ---------------------------------------------------------------------------
+// The chain epilogue with conv3 computed TRANSPOSED (x6_chain_epilogue_t, the pre-split chains of k_conv_x6s):
+// D^T = W3^T h2^T -- the same fragments as x6_chain_epilogue with the MFMA operands swapped (A = the W3 panel
+// fragment, rows = output channels; B = the h2 fragment, columns = the band's 32 pixels) and the six products issued
+// in the same order, so every output element accumulates the same products in the same sequence.  Lane (p, hh)
+// then holds pixel band + p, channels c0 + 32 j + 8 g + 4 hh + u (g, u = 0..3) of the chunk: the residual and the
+// output move as float4 (four per tile and lane instead of sixteen dwords), and -- NT3 > 0 -- the block output y is
+// already the B operand of the NEXT block's 1x1 conv (h3 = act3(y (*) W3' + b3), Co3 = 32 NT3 output channels):
+// per 16-deep slice a lane keeps one 4-channel group of each plane and trades the other with lane p + 32 (one
+// __shfl_xor per plane and dword), so the next conv runs on y straight from registers -- its launch, its HBM read of
+// y (1 KiB per pixel in layer1) and its operand split per N tile disappear.  h3 leaves split (ys3) or fp32 (y3).
+// Same K order per output as the stand-alone conv (slices ascending, six products per slice).  Needs every Co2 chunk
+// of a band in one wave (WPB == 1: the 128-row tiles).
+template <int WM, int WN, int TM, int TN, int X2S = 0, int NT3 = 0>
+__device__ __forceinline__ void x6_chain_epilogue_t(const ConvX &a, unsigned char *lds_raw,
+                                                    const f32x16 (&acc)[TM][TN], int wave, int lane, int wm, int wn,
+                                                    int64_t m0) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32, HR = BN + 8, HPL = BM * HR;
+    constexpr int NB = BM / 32, WPB = 4 / NB;
+    static_assert(NB * WPB == 4, "chain epilogue: 4 waves over the 32-row bands");
+    static_assert(NT3 == 0 || WPB == 1, "the fused next conv needs all of a band's Co2 chunks in one wave");
+    __bf16 *H = (__bf16 *)lds_raw;
+    const int r32 = lane & 31, hh = lane >> 5;
+    const int band = (wave % NB) * 32, part = wave / NB;
+    const int64_t rows = (a.M - m0 < BM) ? a.M - m0 : BM;
+    const int64_t base = m0 * a.Co2;
+    const __amdgpu_buffer_rsrc_t rr = x6_rsrc(a.res ? a.res + base : a.y + base, rows * a.Co2 * 4);
+    const int vrow = (band + r32) * a.Co2 * 4 + 16 * hh;  // this lane's pixel row + its 4-channel half (bytes)
+    const int nch = a.Co2 / 64 / WPB;
+    f32x4 rvn[2][4];
+    auto res_load = [&](int c0) {
+        if (!a.res) return;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                rvn[j][g] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, vrow + 32 * g,
+                                                                                           (c0 + 32 * j) * 4, 0));
+    };
+    res_load(64 * part * nch);
+    __syncthreads();  // every wave is done with the staging buffers
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = wn * TN * 32 + j * 32 + r32;
+            const float bj = a.bias ? a.bias[col] : 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                __bf16 h_, m_, l_;
+                split3(act_x(acc[i][j][r] + bj, a.act), h_, m_, l_);
+                const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                H[row * HR + col] = h_;
+                H[HPL + row * HR + col] = m_;
+                H[2 * HPL + row * HR + col] = l_;
+            }
+        }
+    __syncthreads();
+    constexpr int S2 = BN / 16;
+    constexpr int ST = S2 + X2S;
+    bf16x8 fx[X2S > 0 ? X2S : 1][3];
+    if constexpr (X2S > 0) {
+        int64_t m = m0 + band + r32;
+        const bool ok = m < a.M;
+        m = ok ? m : 0;
+        const int ox = (int)(m % a.Wo);
+        const int64_t q = m / a.Wo;
+        const int oy = (int)(q % a.Ho);
+        const int64_t n = q / a.Ho;
+        const float *xp = a.x2 + ((n * a.H2 + (int64_t)oy * a.stride2) * a.W2 + (int64_t)ox * a.stride2) * a.Ci2 + 8 * hh;
+#pragma unroll
+        for (int t = 0; t < X2S; ++t) {
+            f32x4 v0 = ok ? *(const f32x4 *)(xp + 16 * t) : (f32x4){0.f, 0.f, 0.f, 0.f};
+            f32x4 v1 = ok ? *(const f32x4 *)(xp + 16 * t + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __bf16 h_, m_, l_;
+                split3(e < 4 ? v0[e] : v1[e - 4], h_, m_, l_);
+                fx[t][0][e] = h_, fx[t][1][e] = m_, fx[t][2][e] = l_;
+            }
+        }
+    }
+    const __bf16 *ap = H + (band + r32) * HR + 8 * hh;
+    const __amdgpu_buffer_rsrc_t ry = x6_rsrc(a.y + base, rows * a.Co2 * 4);
+    const __amdgpu_buffer_rsrc_t rw = x6_rsrc(a.wp2, copad_x(a.Co2) / 32 * (int64_t)ST * 3072);
+    const int vl = lane * 16;
+    constexpr int N3 = NT3 > 0 ? NT3 : 1;
+    const int S3 = a.Co2 / 16;  // 16-deep slices of the fused conv's K (= Co2)
+    const __amdgpu_buffer_rsrc_t rw3 = x6_rsrc(NT3 > 0 ? a.wp3 : a.wp2, NT3 > 0 ? copad_x(a.Co3) / 32 * (int64_t)S3 * 3072 : 0);
+    f32x16 acc3[N3];
+#pragma unroll
+    for (int q = 0; q < N3; ++q) acc3[q] = (f32x16){0};
+    for (int nc = part * nch; nc < (part + 1) * nch; ++nc) {
+        const int c0 = 64 * nc;
+        f32x4 rv[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) rv[j][g] = rvn[j][g];
+        if (nc + 1 < (part + 1) * nch) res_load(c0 + 64);  // the next chunk's residual, during these MFMAs
+        f32x16 acc2[2] = {(f32x16){0}, (f32x16){0}};
+#pragma unroll
+        for (int t = 0; t < ST; ++t) {
+            bf16x8 fh[3], fw[2][3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+                if constexpr (X2S > 0) fh[p] = t < S2 ? *(const bf16x8 *)(ap + p * HPL + 16 * (t < S2 ? t : 0))
+                                                      : fx[t >= S2 ? t - S2 : 0][p];
+                else fh[p] = *(const bf16x8 *)(ap + p * HPL + 16 * t);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int p = 0; p < 3; ++p)
+                    fw[j][p] = __builtin_bit_cast(
+                        bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw, vl, (((c0 >> 5) + j) * ST + t) * 3072 + p * 1024, 0));
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {  // x6_chain_epilogue's products, operands swapped
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j][0], fh[0], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j][1], fh[0], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j][0], fh[1], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j][2], fh[0], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j][0], fh[2], acc2[j], 0, 0, 0);
+                acc2[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j][1], fh[1], acc2[j], 0, 0, 0);
+            }
+        }
+        // y = act2(acc2 + b2 + res): channel c0 + 32 j + 8 g + 4 hh + u of this lane's pixel
+        unsigned ys[NT3 > 0 ? 2 : 1][4][3][2];  // NT3: y split, [j][g][plane][2 packed bf16 pairs]
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int c = c0 + 32 * j + 8 * g + 4 * hh;
+                const f32x4 bv = a.bias2 ? *(const f32x4 *)(a.bias2 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                f32x4 o;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float t_ = acc2[j][4 * g + u] + bv[u];
+                    if (a.res) t_ += rv[j][g][u];
+                    o[u] = act_x(t_, a.act2);
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ry, vrow + 32 * g,
+                                                       (c0 + 32 * j) * 4, 0);
+                if constexpr (NT3 > 0) {
+                    __bf16 hv[4], mv[4], lv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) split3(o[u], hv[u], mv[u], lv[u]);
+                    auto pk = [](__bf16 x0, __bf16 x1) {
+                        return (unsigned)__builtin_bit_cast(unsigned short, x0) |
+                               ((unsigned)__builtin_bit_cast(unsigned short, x1) << 16);
+                    };
+                    ys[j][g][0][0] = pk(hv[0], hv[1]), ys[j][g][0][1] = pk(hv[2], hv[3]);
+                    ys[j][g][1][0] = pk(mv[0], mv[1]), ys[j][g][1][1] = pk(mv[2], mv[3]);
+                    ys[j][g][2][0] = pk(lv[0], lv[1]), ys[j][g][2][1] = pk(lv[2], lv[3]);
+                }
+            }
+        if constexpr (NT3 > 0) {
+            // the next conv's K slices of this chunk: (j, sl), channels c0 + 32 j + 16 sl .. + 15.  Lane hh = 0 needs
+            // channels 0-7 of the slice (its own group g = 2 sl, the partner's 4-7), hh = 1 needs 8-15 (the partner's
+            // group 2 sl + 1, its own 12-15): each lane sends the group it does not keep
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int sl = 0; sl < 2; ++sl) {
+                    bf16x8 fy[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p) {
+                        const unsigned k0 = ys[j][2 * sl][p][0], k1 = ys[j][2 * sl][p][1];
+                        const unsigned q0 = ys[j][2 * sl + 1][p][0], q1 = ys[j][2 * sl + 1][p][1];
+                        const unsigned s0 = hh ? k0 : q0, s1 = hh ? k1 : q1;  // the group the partner keeps
+                        const unsigned r0 = (unsigned)__shfl_xor((int)s0, 32), r1 = (unsigned)__shfl_xor((int)s1, 32);
+                        const u32x4 f = hh ? (u32x4){r0, r1, q0, q1} : (u32x4){k0, k1, r0, r1};
+                        fy[p] = __builtin_bit_cast(bf16x8, f);
+                    }
+                    const int ks = (c0 + 32 * j + 16 * sl) >> 4;  // slice of the next conv's K
+#pragma unroll
+                    for (int q = 0; q < NT3; ++q) {
+                        bf16x8 fw3[3];
+#pragma unroll
+                        for (int p = 0; p < 3; ++p)
+                            fw3[p] = __builtin_bit_cast(
+                                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rw3, vl, (q * S3 + ks) * 3072 + p * 1024, 0));
+                        acc3[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw3[0], fy[0], acc3[q], 0, 0, 0);
+                        acc3[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw3[1], fy[0], acc3[q], 0, 0, 0);
+                        acc3[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw3[0], fy[1], acc3[q], 0, 0, 0);
+                        acc3[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw3[2], fy[0], acc3[q], 0, 0, 0);
+                        acc3[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw3[0], fy[2], acc3[q], 0, 0, 0);
+                        acc3[q] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw3[1], fy[1], acc3[q], 0, 0, 0);
+                    }
+                }
+        }
+    }
+    if constexpr (NT3 > 0) {  // h3 = act3(acc3 + b3) of this lane's pixel, channels 32 q + 8 g + 4 hh + u
+        const int64_t prow = m0 + band + r32;
+        if (prow < a.M) {
+#pragma unroll
+            for (int q = 0; q < NT3; ++q)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c = 32 * q + 8 * g + 4 * hh;
+                    const f32x4 bv = a.bias3 ? *(const f32x4 *)(a.bias3 + c) : (f32x4){0.f, 0.f, 0.f, 0.f};
+                    f32x4 o;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) o[u] = act_x(acc3[q][4 * g + u] + bv[u], a.act3);
+                    if (a.ys3) {
+                        bf16x4 hv, mv, lv;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            __bf16 h_, m_, l_;
+                            split3(o[u], h_, m_, l_);
+                            hv[u] = h_, mv[u] = m_, lv[u] = l_;
+                        }
+                        __bf16 *yp = a.ys3 + prow * a.Co3 + c;
+                        const int64_t pl = a.M * a.Co3;
+                        *(bf16x4 *)yp = hv;
+                        *(bf16x4 *)(yp + pl) = mv;
+                        *(bf16x4 *)(yp + 2 * pl) = lv;
+                    } else {
+                        *(f32x4 *)(a.y3 + prow * a.Co3 + c) = o;
+                    }
+                }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_conv_x6b: Ci % 32 == 0 (every ResNet trunk layer).  K step 32 (two 16-deep slices, 48 MFMAs per wave and
 // step for a 64 x 64 wave tile: twice the work per barrier of k_conv_x6).  Only A goes through LDS (three bf16
 // planes, rows of 40 bf16 = 80 B = 5 odd 16-B slots: conflict-free fragment groups); the B fragments are read
@@ -780,7 +1019,7 @@ __device__ __forceinline__ void dma16(const void *src, unsigned dst_any) {
 // are 1-KiB runs, one DMA instruction each, read back as conflict-free ds_read_b128 (lane l at 16 l) -- so every
 // vector-memory operation of the loop is a DMA issued one K step ahead and waited for at the step's end.  (With B
 // in registers hipcc re-issued the fragment loads next to their MFMAs and waited on each: L2 latency per slice.)
-template <int WM, int WN, int TM, int TN, int CHAIN = 0, bool BLDS = (CHAIN > 0)>
+template <int WM, int WN, int TM, int TN, int CHAIN = 0, bool BLDS = (CHAIN > 0), int NT3 = 0>
 __global__ __launch_bounds__(256, CHAIN ? 2 : 3) void k_conv_x6s(ConvX a) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     constexpr int APL = BM * 32;     // bf16 per A plane per stage (64-B rows)
@@ -962,18 +1201,20 @@ __global__ __launch_bounds__(256, CHAIN ? 2 : 3) void k_conv_x6s(ConvX a) {
             if (m0 + tid < a.M) a.y[(m0 + tid) * a.Co2] = s_;
             return;
         }
-        x6_chain_epilogue<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0>(a, lds_raw, acc, wave, lane, wm, wn, m0);
+        if (X6S_T_EPI || NT3 > 0) x6_chain_epilogue_t<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0, NT3>(a, lds_raw, acc, wave, lane, wm, wn, m0);
+        else x6_chain_epilogue<WM, WN, TM, TN, CHAIN == 2 ? 4 : 0>(a, lds_raw, acc, wave, lane, wm, wn, m0);
         return;
     }
     x6_epilogue<TM, TN>(a, (float *)lds_raw, acc, wave, lane, wn, wm, m0, n0);
 }
 
-template <int WM, int WN, int TM, int TN, int CHAIN = 0>
+template <int WM, int WN, int TM, int TN, int CHAIN = 0, int NT3 = 0>
 int launch_x6s(const ConvX &a, hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const int64_t blocks = ((a.M + BM - 1) / BM) * ((a.Co + BN - 1) / BN);
     if (blocks >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
-    hipLaunchKernelGGL((k_conv_x6s<WM, WN, TM, TN, CHAIN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_conv_x6s<WM, WN, TM, TN, CHAIN, (CHAIN > 0), NT3>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       a);
     return (int)hipGetLastError();
 }
 
@@ -1570,6 +1811,58 @@ int bev_conv2d_chain_dual_x6_f32(const float *x, const uint16_t *xs, int N, int 
     return launch_x6b<4, 1, 1, 2, false, 2>(a, (hipStream_t)stream);
 }
 
+int bev_conv2d_chain_next_x6_f32(const uint16_t *xs, int N, int H, int W, int Ci, const uint16_t *packed,
+                                 const float *bias, int Co, int KH, int KW, int stride, int pad, int act,
+                                 const float *x2, int H2, int W2, int Ci2, int stride2, const uint16_t *packed2,
+                                 const float *bias2, int Co2, const float *residual, int act2, float *y, int Ho, int Wo,
+                                 const uint16_t *packed3, const float *bias3, int Co3, int act3, float *y3,
+                                 uint16_t *ys3, void *stream) {
+    if (!xs || !packed || !packed2 || !packed3 || !y || (!y3 == !ys3) || N < 0 || H <= 0 || W <= 0 || KH <= 0 ||
+        KW <= 0 || stride <= 0 || pad < 0 || act < 0 || act > 2 || act2 < 0 || act2 > 2 || act3 < 0 || act3 > 2)
+        return BEV_ERR_ARGS;
+    // the 128-row tile (every Co2 chunk of a band in one wave), conv2 64 channels; the next conv Co3 in {64, 128}
+    if (Ci % YBK != 0 || Co != 64 || Co2 <= 0 || Co2 % 64 != 0 || (Co3 != 64 && Co3 != 128) ||
+        (((uintptr_t)xs | (uintptr_t)packed | (uintptr_t)packed2 | (uintptr_t)packed3 | (uintptr_t)y |
+          (uintptr_t)y3 | (uintptr_t)residual | (uintptr_t)bias2 | (uintptr_t)bias3) & 15) != 0 ||
+        ((uintptr_t)ys3 & 7) != 0)
+        return BEV_ERR_ARGS;
+    if (Ho != (H + 2 * pad - KH) / stride + 1 || Wo != (W + 2 * pad - KW) / stride + 1 || Ho <= 0 || Wo <= 0)
+        return BEV_ERR_ARGS;
+    // The dual (block 0) form is not offered: its instantiation (k_conv_x6s<4,1,1,2,2,1,2>, 256 VGPRs) wrote y
+    // channels 24-31 of each 32 wrongly for lanes 12-15 of every 16, differently from run to run, at the bench size
+    // (r06o tools/chain_next_determinism.py; every other form repeatable) -- x2 is refused until that is understood.
+    if (x2) return BEV_ERR_ARGS;
+    (void)H2, (void)W2, (void)Ci2, (void)stride2;
+    if (N == 0) return 0;
+    ConvX a;
+    a.x = nullptr;
+    a.wp = (const __bf16 *)packed;
+    a.bias = bias;
+    a.res = residual;
+    a.y = y;
+    a.N = N, a.H = H, a.W = W, a.Ci = Ci, a.Co = Co, a.KH = KH, a.KW = KW, a.stride = stride, a.pad = pad;
+    a.dil = 1, a.Ho = Ho, a.Wo = Wo, a.act = act, a.ldy = Co2;
+    a.Kp = (int)kpad_x(Ci * KH * KW);
+    a.M = (int64_t)N * Ho * Wo;
+    a.x2 = x2;
+    a.Ci2 = x2 ? Ci2 : 0, a.H2 = x2 ? H2 : 0, a.W2 = x2 ? W2 : 0, a.stride2 = x2 ? stride2 : 0;
+    a.xs = (const __bf16 *)xs;
+    a.ys = nullptr;
+    a.xps = (int64_t)N * H * W * Ci;
+    a.yps = 0;
+    a.wp2 = (const __bf16 *)packed2;
+    a.bias2 = bias2;
+    a.Co2 = Co2;
+    a.act2 = act2;
+    a.wp3 = (const __bf16 *)packed3;
+    a.bias3 = bias3;
+    a.Co3 = Co3;
+    a.act3 = act3;
+    a.y3 = y3;
+    a.ys3 = (__bf16 *)ys3;
+    const hipStream_t st = (hipStream_t)stream;
+    return Co3 == 64 ? launch_x6s<4, 1, 1, 2, 1, 2>(a, st) : launch_x6s<4, 1, 1, 2, 1, 4>(a, st);
+}
 
 int bev_conv2d_stem_x6_f32(const float *x, int N, int H, int W, const uint16_t *packed, const float *bias, int Co,
                            int relu, float *y, int Ho, int Wo, void *stream) {

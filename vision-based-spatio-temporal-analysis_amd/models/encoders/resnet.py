@@ -84,6 +84,12 @@ STEM_POOL = True
 # (bev_conv2d_x6_f32 ys) and the chain stages conv2's operand by LDS-DMA with no split in its mainloop (k_conv_x6s
 # CHAIN).  Bit-identical either way; False: conv1 writes fp32 and the chain splits it once per tap (k_conv_x6b).
 SPLIT_CHAIN = True
+# ... and such a chain over a 64-channel conv2 (the 128-row tile: layer1) also runs the NEXT block's 1x1 conv1 on the
+# block output it computes (bev_conv2d_chain_next_x6_f32: the next conv1's launch and its HBM read of the block output
+# disappear; bit-identical).  False: the next block runs its conv1 itself.  Off: the fusion needs conv3 in the
+# transposed epilogue layout, whose per-pixel stores cost what the saved launch gains (r06p A/B, encoder ms per 2-frame
+# step: fused 15.82, separate conv1 15.76, no pre-split chains 16.00).
+FUSE_NEXT_CONV1 = False
 
 
 class FoldedConv:
@@ -254,6 +260,18 @@ class FoldedChain:
                                       _nat.ACT_RELU, self.c3.packed6 if x6 else self.c3.packed, self.c3.bias,
                                       self.c3.conv.out_channels, _nat.ACT_RELU, residual=x, out=out)
 
+    def fused(self, h, x, nxt: "FoldedConv", out=None, split_out: bool = True):
+        """The split-arithmetic chain that also runs the next block's 1x1 conv1 `nxt` on its output
+        (bev_conv2d_chain_next_x6_f32): returns (y, h1 of the next block)."""
+        self.prepare(h.device, "bf16x6")
+        nxt.prepare(h.device, "bf16x6")
+        c2 = self.c2.conv
+        return _nat.conv2d_chain_next_nhwc(h, self.c2.packed6, self.c2.bias, c2.out_channels, c2.kernel_size[0],
+                                           c2.kernel_size[1], c2.stride[0], c2.padding[0], _nat.ACT_RELU,
+                                           self.c3.packed6, self.c3.bias, self.c3.conv.out_channels, _nat.ACT_RELU,
+                                           nxt.packed6, nxt.bias, nxt.conv.out_channels, _nat.ACT_RELU, residual=x,
+                                           out=out, split3_out=split_out)
+
 
 class FoldedChainTail:
     """Bottleneck conv2/bn2/act2 -> [conv3/bn3 + downsample conv/bn] -> act3 as ONE launch (block 0).
@@ -391,12 +409,16 @@ class ResNet(nn.Module):
             mark(2)
         stage = 2
         layers = (self.layer1, self.layer2, self.layer3, self.layer4)
-        for li, layer in enumerate(layers, start=1):
-            for bi, blk in enumerate(layer):
-                y = self._block(blk, y, out=out if (li == last_li and bi == len(layer) - 1) else None)
-                stage += 1
-                mark(stage)
-            if li == out_index:
+        seq = [(li, bi, blk) for li, layer in enumerate(layers, start=1) if li <= max(out_index, 1)
+               for bi, blk in enumerate(layer)]
+        h1 = None  # the next block's conv1 output, computed by the previous chain's epilogue (FUSE_NEXT_CONV1)
+        for k, (li, bi, blk) in enumerate(seq):
+            last = li == last_li and bi == len(layers[li - 1]) - 1
+            nxt = seq[k + 1][2] if k + 1 < len(seq) else None
+            y, h1 = self._block(blk, y, out=out if last else None, h1=h1, nxt=nxt)
+            stage += 1
+            mark(stage)
+            if li == out_index and bi == len(layers[li - 1]) - 1:
                 return y
         return y
 
@@ -554,19 +576,40 @@ class ResNet(nn.Module):
         return (self.split_edges and f1.arith() == "bf16x6" and f2.arith() == "bf16x6" and f2.conv.kernel_size[0] > 1
                 and f2.conv.in_channels % 32 == 0 and f1.conv.out_channels % 4 == 0)
 
-    def _block(self, blk, x, out=None):
+    def _next_conv1(self, fs, nxt):
+        """The next block's conv1 that this split chain (fs = its plan) may run in its epilogue, with whether the
+        next block wants that output split (a chain) or fp32 (the tail plan's stride-2 conv2); (None, _) if not.
+        Identity-shortcut chains only: the library refuses the dual (block 0) form (bev_mi355x.h)."""
+        if not (FUSE_NEXT_CONV1 and SPLIT_CHAIN and nxt is not None and isinstance(fs[1], FoldedChain)
+                and fs[1].c2.conv.out_channels == 64):
+            return None, False
+        kind, nf = self._block_plan(nxt)
+        if kind not in ("chain6", "chaintail6", "tail"):
+            return None, False
+        c1 = nf[0]
+        cv = c1.conv
+        ok = (c1.arith() == "bf16x6" and cv.kernel_size == (1, 1) and cv.stride == (1, 1) and cv.padding == (0, 0)
+              and cv.in_channels == fs[1].c3.conv.out_channels and cv.out_channels in (64, 128))
+        return (c1, kind != "tail") if ok else (None, False)
+
+    def _block(self, blk, x, out=None, h1=None, nxt=None):
+        """One residual block of the eval chain -> (y, h1 of the next block if this block's chain computed it)."""
         kind, fs = self._block_plan(blk)
         if kind in ("chain", "chaintail"):
             h = fs[0](x, relu=True)
-            return fs[1](h, x, out=out)
+            return fs[1](h, x, out=out), None
         if kind in ("chain6", "chaintail6"):
             split = SPLIT_CHAIN and fs[0].arith() == "bf16x6" and fs[0].conv.out_channels % 32 == 0
-            h = fs[0](x, relu=True, split_out=split)
-            return fs[1](h, x, out=out, arith="bf16x6")
+            h = h1 if h1 is not None else fs[0](x, relu=True, split_out=split)
+            if isinstance(h, _nat.Split3):
+                c1n, split_n = self._next_conv1(fs, nxt)
+                if c1n is not None:
+                    return fs[1].fused(h, x, c1n, out=out, split_out=split_n)
+            return fs[1](h, x, out=out, arith="bf16x6"), None
         if kind == "tail":
-            h = fs[0](x, relu=True, split_out=self._split_edge(fs[0], fs[1]))
+            h = h1 if h1 is not None else fs[0](x, relu=True, split_out=self._split_edge(fs[0], fs[1]))
             h = fs[1](h, relu=True)
-            return fs[2](h, x, out=out)
+            return fs[2](h, x, out=out), None
         sc = fs[0](x, relu=False) if fs[0] is not None else x
         chain = blk.convs()
         fl = fs[1:]
@@ -575,7 +618,7 @@ class ResNet(nn.Module):
             last = idx == len(chain) - 1
             split = not last and self._split_edge(f, fl[idx + 1])
             y = f(y, relu=relu, residual=sc if last else None, out=out if last else None, split_out=split)
-        return y
+        return y, None
 
 
 def resnet18():
