@@ -3,7 +3,8 @@
 # steps:
 #   tests            every GPU test                      tests=<file or -k expr>  a subset (file path or -k expression)
 #   smoke            __graft_entry__.smoke()
-#   bench            bench.py default line               bench:<extra bench.py args, comma-separated>
+#   bench            bench.py default line               bench:<extra bench.py args, comma-separated> (K5:
+#                    bench:--camera-shard,--steps,10,--cpu-iters,0  K4: bench:--backbone,efficientnet_b3,--cpu-iters,0)
 #   prof             rocprofv3 kernel trace + stats of the default bench (20 steps)
 #   encab:<v,v,...>  tools/encoder_ab.py variants        train  the AMP BEVNet training step line
 #   encprof:<v>      kernel trace of tools/encoder_ab.py <v> (1 round, 5 iterations)
@@ -29,7 +30,8 @@ for step in "$@"; do
         --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -3 $O/tests.log ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?
       tail -2 $O/smoke.log ;;
-    bench) timeout -k 10 600 python -u bench.py ${arg//,/ } > $O/bench.log 2>&1; rc=$?; tail -1 $O/bench.log ;;
+    bench) b=bench${arg:+_${arg//[^A-Za-z0-9]/_}}
+      timeout -k 10 600 python -u bench.py ${arg//,/ } > $O/$b.log 2>&1; rc=$?; tail -1 $O/$b.log ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
         python3 bench.py --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1; rc=$? ;;
     encab) timeout -k 10 600 python -u tools/encoder_ab.py ${arg//,/ } > $O/encab.log 2>&1; rc=$?
