@@ -78,7 +78,10 @@ const char *bev_build_source_hash(void);
  *   per bev_dwconv_psum_blocks, which follows the knob.
  * BEV_TUNE_CONV_X6_NT: 1 = non-temporal (streaming) activation loads in the split-arithmetic 1x1 / 3x3 convs with
  *   Co <= 64 tiles, 0 (default) = cached loads.  For the LAST reader of a large tensor: CNNEncoder sets it around its
- *   projection so the feature maps that conv writes stay in the Infinity Cache for the warp.  Same results. */
+ *   projection so the feature maps that conv writes stay in the Infinity Cache for the warp.  Same results.
+ * BEV_TUNE_STEM3_STAGE: bev_conv2d_stem3_f32 output stores: staged in LDS and written as whole NHWC row runs (1 KiB
+ *   per instruction), 64 pixels per wave and pass (1) or 32 (2, default: half the LDS, more resident workgroups);
+ *   0 = straight from registers (16 B per lane at a pixel stride).  Same results. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -93,6 +96,7 @@ const char *bev_build_source_hash(void);
 #define BEV_TUNE_CONV_PW_SMALL 13
 #define BEV_TUNE_DW_RUN 14
 #define BEV_TUNE_CONV_X6_NT 16
+#define BEV_TUNE_STEM3_STAGE 17
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------
@@ -333,6 +337,14 @@ int bev_dwconv_psum_blocks(int Ho, int Wo, int C, int stride);
  * every other shape and stride the per-pixel kernel. */
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
                      int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);
+
+/* device: the EfficientNet stem (timm conv_stem -> bn1 -> SiLU, cnn_encoder.py:26: 3x3, stride 2, pad 1, 3 input
+ * channels), BN folded, from NCHW images to NHWC:
+ *   y[n,oy,ox,c] = act( sum_{ci,ky,kx ascending} x[n, ci, 2 oy - 1 + ky, 2 ox - 1 + kx] * wt[(ci*3+ky)*3+kx][c] + bias[c] )
+ * x [N][3][H][W] fp32, wt tap-major [27][Co], Co in {32, 40, 48, 64} (timm B0-B5 stems), y [N][Ho][Wo][Co] 16-B
+ * aligned, Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1; act as bev_conv2d_f32.  fp32 FMAs on the vector ALU. */
+int bev_conv2d_stem3_f32(const float *x, int N, int H, int W, const float *wt, const float *bias, int Co, int act,
+                         float *y, int Ho, int Wo, void *stream);
 
 /* device: depthwise conv weight gradient (training): dW [K*K][C] (tap-major, like wt) =
  * sum over n, output pixels of dz[n][p][c] * x[n][tap t of p][c]; OVERWRITTEN (float atomics inside). */

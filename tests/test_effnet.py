@@ -150,6 +150,35 @@ def test_conv_silu_epilogue():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Co,N,H,W", [(40, 2, 37, 70), (32, 1, 16, 128), (48, 1, 9, 250), (64, 3, 30, 3)])
+def test_stem3_vs_float64_and_generic_conv(Co, N, H, W):
+    """bev_conv2d_stem3_f32 (the EfficientNet stem on the vector ALU) == torch's conv_stem -> bn1 -> SiLU in float64
+    within 2e-6 of max|ref| (27-term fp32 FMA chain + the hardware SiLU), and the generic implicit-GEMM path it
+    replaces within the same bound -- ragged tiles (rows % 8, columns % 64), tiny widths, every supported Co."""
+    import bev_native as nat
+    from models.encoders.resnet import FoldedConv
+    torch.manual_seed(Co + H)
+    conv, bn = torch.nn.Conv2d(3, Co, 3, 2, 1, bias=False), torch.nn.BatchNorm2d(Co)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5), bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.2, 0.2), bn.running_var.uniform_(0.5, 2.0)
+    bn.eval()
+    x = _rand((N, 3, H, W), Co)
+    with torch.no_grad():
+        ref = F.silu(bn.double()(F.conv2d(x.double(), conv.weight.double(), stride=2, padding=1)))
+    fc = FoldedConv(conv.to(DEV), bn.float().to(DEV))
+    w, b = fc.folded(DEV)
+    got = nat.conv2d_stem3(x.to(DEV), w.permute(1, 2, 3, 0).reshape(27, Co).contiguous(), b, nat.ACT_SILU)
+    gen = fc(x.to(DEV), relu=nat.ACT_SILU, in_nchw=True)
+    torch.cuda.synchronize()
+    ref = ref.permute(0, 2, 3, 1)
+    scale = ref.abs().max().item()
+    assert got.shape == ref.shape
+    assert (got.double().cpu() - ref).abs().max().item() <= 2e-6 * scale
+    assert (got - gen).abs().max().item() <= 2e-6 * scale
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,out_index", [("efficientnet_b3", 0), ("efficientnet_b3", 2), ("efficientnet_b3", 3),
                                             ("efficientnet_b0", 2)])
 def test_effnet_encoder_vs_torch_fp32(name, out_index):

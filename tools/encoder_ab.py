@@ -22,6 +22,13 @@ from models.encoders.cnn_encoder import CNNEncoder  # noqa: E402
 
 
 def apply(name, rn):
+    if hasattr(rn, "x6_expand"):  # EfficientNet (--backbone efficientnet_b3): base / x6expand / nostem3
+        if name not in ("base", "x6expand", "nostem3", "nopwstream"):
+            raise SystemExit(f"unknown EfficientNet variant {name}")
+        rn.x6_expand = name == "x6expand"
+        rn.stem3 = name != "nostem3"
+        rn.pw_stream = name != "nopwstream"
+        return
     resnet.SPLIT_CHAIN = True
     resnet.FUSE_NEXT_CONV1 = False
     rn.split_edges = False
@@ -41,14 +48,16 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--frames", type=int, default=2)
+    ap.add_argument("--backbone", default="resnet50")
     ap.add_argument("--stream-groups", type=int, default=2, help="1: launches attributable per layer (profiling)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    enc = CNNEncoder(out_channels=64, backbone="resnet50", pretrained=False).eval().to(dev)
+    enc = CNNEncoder(out_channels=64, backbone=a.backbone, pretrained=False).eval().to(dev)
     imgs = torch.randn(a.frames, 7, 3, 1080, 1920, device=dev)
     rn = enc.backbone
-    rn.stream_groups = a.stream_groups
+    if hasattr(rn, "stream_groups"):
+        rn.stream_groups = a.stream_groups
     res = {n: [] for n in a.variants}
     first = None
     with torch.no_grad():

@@ -10,7 +10,7 @@
 #   encprof:<v>      kernel trace of tools/encoder_ab.py <v> (1 round, 5 iterations)
 #   encpmc:<v>:<c,c> one --pmc pass over tools/encoder_ab.py <v> (1 iteration, one stream group)
 #   trainprof        kernel trace of 3 AMP training steps
-#   pmc:<counters>   one rocprofv3 --pmc pass over a 3-step bench (counters comma-separated)
+#   pmc:<counters>[:<bench args>]  one rocprofv3 --pmc pass over a 3-step bench (both comma-separated)
 #   py:<script,args> any python tool under tools/ (args comma-separated)
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -34,6 +34,9 @@ for step in "$@"; do
       timeout -k 10 600 python -u bench.py ${arg//,/ } > $O/$b.log 2>&1; rc=$?; tail -1 $O/$b.log ;;
     prof) timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
         python3 bench.py --steps 20 --warmup 3 --cpu-iters 0 > $O/prof.log 2>&1; rc=$? ;;
+    bprof) d=$O/bprof${arg:+_${arg//[^A-Za-z0-9]/_}}  # kernel trace of a bench variant: bprof:<bench args>
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- \
+        python3 bench.py --steps 10 --warmup 2 --cpu-iters 0 ${arg//,/ } > $O/bprof.log 2>&1; rc=$? ;;
     encab) timeout -k 10 600 python -u tools/encoder_ab.py ${arg//,/ } > $O/encab.log 2>&1; rc=$?
       grep median $O/encab.log; grep MISMATCH $O/encab.log ;;
     encprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/encprof_$arg -o run -- \
@@ -45,8 +48,10 @@ for step in "$@"; do
       tail -1 $O/train.log ;;
     trainprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tprof -o run -- \
         python3 tools/train_step_bench.py --steps 3 --warmup 1 --bevnet --amp > $O/tprof.log 2>&1; rc=$? ;;
-    pmc) timeout -s KILL 120 rocprofv3 --pmc ${arg//,/ } --output-format csv -d $O/pmc_${arg//,/_} -o run -- \
-        python3 bench.py --steps 3 --warmup 1 --cpu-iters 0 > $O/pmc.log 2>&1; rc=$? ;;
+    pmc) c=${arg%%:*}; ba=""; case "$arg" in *:*) ba=${arg#*:};; esac
+      d=$O/pmc_${c//,/_}${ba:+_${ba//[^A-Za-z0-9]/_}}
+      timeout -s KILL 180 rocprofv3 --pmc ${c//,/ } --output-format csv -d $d -o run -- \
+        python3 bench.py --steps 3 --warmup 1 --cpu-iters 0 ${ba//,/ } > $O/pmc.log 2>&1; rc=$? ;;
     py) set -- ${arg//,/ }; s=$1; shift
       timeout -k 10 600 python -u tools/$s "$@" > $O/$(basename $s .py).log 2>&1; rc=$?
       tail -5 $O/$(basename $s .py).log ;;

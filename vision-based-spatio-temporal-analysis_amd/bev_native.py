@@ -20,7 +20,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 BEV_ERR_ARGS = -1  # include/bev_mi355x.h: an argument the kernel cannot take
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
@@ -102,6 +102,7 @@ SIGNATURES = {
     "bev_dwconv_psum_blocks": (_i, [_i, _i, _i, _i]),
     "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_se_gate_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
+    "bev_conv2d_stem3_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
     "bev_channel_scale_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp]),
     "bev_decode_peaks_f32": (_i, [_vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "bev_decode_nms_f32": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _f, _f, _f, _f, _f, _vp, _vp, _vp, _vp]),
@@ -258,6 +259,7 @@ TUNE_CONV_H16_KERNEL = 12
 TUNE_CONV_PW_SMALL = 13
 TUNE_DW_RUN = 14
 TUNE_CONV_X6_NT = 16
+TUNE_STEM3_STAGE = 17
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 
@@ -1124,6 +1126,24 @@ def dwconv2d_nhwc(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, K: int,
                                     Wo, _ptr(psum), _stream(x))
     _check(rc, "bev_dwconv2d_f32")
     return y, psum
+
+
+def conv2d_stem3(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, act: int) -> torch.Tensor:
+    """EfficientNet stem (3x3 / s2 / p1, 3 input channels, BN folded) on the vector ALU: x [N,3,H,W] NCHW fp32,
+    wt [27, Co] tap-major ((ci*3+ky)*3+kx), bias [Co] -> y [N,Ho,Wo,Co] NHWC (bev_conv2d_stem3_f32)."""
+    x = x.contiguous()
+    _require_gpu(x, wt, bias)
+    N, Ci, H, W = x.shape
+    Co = wt.shape[1]
+    if Ci != 3 or wt.shape[0] != 27:
+        raise HipError("conv2d_stem3 takes 3-channel images and a [27, Co] weight")
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    y = torch.empty(N, Ho, Wo, Co, device=x.device, dtype=torch.float32)
+    with _span("conv", x):
+        rc = lib().bev_conv2d_stem3_f32(_ptr(x), N, H, W, _ptr(wt.contiguous()), _ptr(bias.contiguous()), Co, int(act),
+                                        _ptr(y), Ho, Wo, _stream(x))
+    _check(rc, "bev_conv2d_stem3_f32")
+    return y
 
 
 def se_gate(psum: torch.Tensor, hw: int, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor):

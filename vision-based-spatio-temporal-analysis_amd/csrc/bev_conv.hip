@@ -1535,6 +1535,7 @@ int bev_tune(int knob, int value) {
         return bev::conv_x6_tune(knob, value);
     if (knob == BEV_TUNE_CONV_H16_KERNEL) return bev::conv_h16_tune(value);
     if (knob == BEV_TUNE_DW_RUN) return bev::dw_tune(value);
+    if (knob == BEV_TUNE_STEM3_STAGE) return bev::stem3_tune(value);
     if (knob == BEV_TUNE_CONV_PW_SMALL) {
         if (value < 0 || value > 4) return BEV_ERR_ARGS;
         const int old = g_conv_pw_small;

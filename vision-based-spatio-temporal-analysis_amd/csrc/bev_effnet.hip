@@ -475,6 +475,119 @@ __global__ __launch_bounds__(DW_NT) void k_dw_wgrad(const float *__restrict__ x,
     }
 }
 
+// k_stem3: the EfficientNet stem (timm conv_stem, cnn_encoder.py:26: 3x3, stride 2, pad 1, 3 input channels; BN
+// folded, SiLU) from the NCHW fp32 images straight to NHWC, on the vector ALU.  K = 27 is far too short for the MFMA
+// implicit GEMM (the generic k_conv ran it at 2.1 ms per 14 x 1080p images, 0.7 TB/s); here a workgroup stages the
+// 3 x 17 x 129 input window of an 8 x 64 output tile in LDS (coalesced rows, zero padding), each lane computes two
+// output pixels (rows 2w and 2w + 1 of its wave, one column) as 27 x CO fp32 FMAs with the weights as scalar
+// operands (wave-uniform: s_load, no LDS or VGPR traffic), and each wave writes its 64-pixel row runs back as whole
+// NHWC runs (the CO values of a pixel staged at an odd LDS stride, then 16 B per lane, 1 KiB per instruction).
+// Per output: sum over (ci, ky, kx) ascending of fmaf(x, w), from +0, then + bias, then the activation.
+constexpr int S3_TR = 8, S3_TC = 64;                          // output tile rows / columns
+constexpr int S3_IR = 2 * S3_TR + 1, S3_IC = 2 * S3_TC + 1;  // its input window (stride 2, 3 taps)
+constexpr int S3_ICP = S3_IC + 3;                             // padded window row (floats)
+
+int g_stem3_stage = 2;  // BEV_TUNE_STEM3_STAGE (r06u micro, 14 x 1080p B3 stem: 64-pixel passes 545 us, 32-pixel 481, registers 3483)
+
+template <int CO, int SP>  // SP: output pixels staged per wave and pass (64 / 32), 0 = stores from registers
+__global__ __launch_bounds__(256) void k_stem3(const float *__restrict__ x, int H, int W, const float *__restrict__ wt,
+                                               const float *__restrict__ bias, int act, float *__restrict__ y, int Ho,
+                                               int Wo, int tiles_x) {
+    constexpr int CP = CO + 1;                 // staged pixel stride (odd: conflict-free dword writes)
+    constexpr int IN_F = 3 * S3_IR * S3_ICP;   // input window floats
+    constexpr int ST_F = 4 * SP * CP;          // output staging floats (4 waves x SP pixels)
+    __shared__ float lds[IN_F > ST_F ? IN_F : ST_F];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n = blockIdx.y;
+    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+    const int r0 = ty * S3_TR, c0 = tx * S3_TC;
+    const int iy0 = 2 * r0 - 1, ix0 = 2 * c0 - 1;
+    const float *xn = x + (int64_t)n * 3 * H * W;
+    constexpr int NE = 3 * S3_IR * S3_IC, NL = (NE + 255) / 256;  // window elements, loads per thread
+    float win[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {  // every load in flight before the first LDS write
+        const int e = tid + 256 * k;
+        const int ci = e / (S3_IR * S3_IC), rem = e - ci * (S3_IR * S3_IC);
+        const int rr = rem / S3_IC, cc = rem - rr * S3_IC;
+        const int iy = iy0 + rr, ix = ix0 + cc;
+        const bool in = e < NE && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+        win[k] = in ? xn[((int64_t)ci * H + iy) * W + ix] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int e = tid + 256 * k;
+        const int ci = e / (S3_IR * S3_IC), rem = e - ci * (S3_IR * S3_IC);
+        const int rr = rem / S3_IC, cc = rem - rr * S3_IC;
+        if (e < NE) lds[(ci * S3_IR + rr) * S3_ICP + cc] = win[k];
+    }
+    __syncthreads();
+    float acc0[CO], acc1[CO];
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc0[c] = acc1[c] = 0.0f;
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const int t = (ci * 3 + ky) * 3 + kx;
+                const float v0 = lds[(ci * S3_IR + 4 * wave + ky) * S3_ICP + 2 * lane + kx];
+                const float v1 = lds[(ci * S3_IR + 4 * wave + 2 + ky) * S3_ICP + 2 * lane + kx];
+#pragma unroll
+                for (int c = 0; c < CO; ++c) {
+                    acc0[c] = __builtin_fmaf(v0, wt[t * CO + c], acc0[c]);
+                    acc1[c] = __builtin_fmaf(v1, wt[t * CO + c], acc1[c]);
+                }
+            }
+    if constexpr (SP == 0) {  // straight from registers: 16 B per lane, lanes a pixel (CO floats) apart
+        const int c = c0 + lane;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int r = r0 + 2 * wave + i;
+            if (r >= Ho || c >= Wo) continue;
+            float *dst = y + (((int64_t)n * Ho + r) * Wo + c) * CO;
+#pragma unroll
+            for (int q = 0; q < CO / 4; ++q) {
+                float o[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o[u] = act_f((i ? acc1[4 * q + u] : acc0[4 * q + u]) + bias[4 * q + u], act);
+                *(float4 *)(dst + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
+            }
+        }
+        return;
+    }
+    __syncthreads();  // the window is no longer read: the staging reuses the LDS
+    float *stg = lds + wave * SP * CP;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = r0 + 2 * wave + i;
+#pragma unroll
+        for (int hb = 0; hb < 64 / SP; ++hb) {  // pixels hb SP .. hb SP + SP - 1 of the row run
+            if (lane / SP == hb) {
+#pragma unroll
+                for (int c = 0; c < CO; ++c)
+                    stg[(lane - hb * SP) * CP + c] = act_f((i ? acc1[c] : acc0[c]) + bias[c], act);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const int np = min(SP, Wo - c0 - hb * SP);  // pixels of this run piece
+            if (r < Ho && np > 0) {
+                float *dst = y + (((int64_t)n * Ho + r) * Wo + c0 + hb * SP) * CO;
+                for (int f = lane * 4; f < np * CO; f += 256) {  // CO % 4 == 0: a quad never straddles two pixels
+                    const int p = f / CO, c = f - p * CO;
+                    const float *s = stg + p * CP + c;
+                    *(float4 *)(dst + f) = make_float4(s[0], s[1], s[2], s[3]);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+}
+
 inline int last() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -509,6 +622,12 @@ inline int dw_run_blocks(int Ho, int Wo, int C, int stride) {
 }  // namespace
 
 namespace bev {
+int stem3_tune(int value) {
+    if (value < 0 || value > 2) return BEV_ERR_ARGS;
+    const int old = g_stem3_stage;
+    g_stem3_stage = value;
+    return old;
+}
 int dw_tune(int value) {
     if (value < 0 || value > 3) return BEV_ERR_ARGS;
     const int old = g_dw_run;
@@ -585,6 +704,34 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
     else if (K == 3) launch_dwconv_t<3, 2>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     else if (stride == 1) launch_dwconv_t<5, 1>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     else launch_dwconv_t<5, 2>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    return last();
+}
+
+int bev_conv2d_stem3_f32(const float *x, int N, int H, int W, const float *wt, const float *bias, int Co, int act,
+                         float *y, int Ho, int Wo, void *stream) {
+    if (!x || !wt || !bias || !y || N < 0 || H <= 0 || W <= 0 || act < 0 || act > 2 ||
+        (Co != 32 && Co != 40 && Co != 48 && Co != 64))
+        return BEV_ERR_ARGS;
+    if (Ho != (H - 1) / 2 + 1 || Wo != (W - 1) / 2 + 1 || (((uintptr_t)y) & 15) != 0) return BEV_ERR_ARGS;
+    if ((int64_t)3 * H * W >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    const int tiles_x = (Wo + S3_TC - 1) / S3_TC, tiles = ((Ho + S3_TR - 1) / S3_TR) * tiles_x;
+    const dim3 grid(tiles, N);
+    hipStream_t st = (hipStream_t)stream;
+#define STEM3_LAUNCH(CO)                                                                                          \
+    do {                                                                                                         \
+        if (g_stem3_stage == 1)                                                                                  \
+            hipLaunchKernelGGL((k_stem3<CO, 64>), grid, dim3(256), 0, st, x, H, W, wt, bias, act, y, Ho, Wo, tiles_x);  \
+        else if (g_stem3_stage == 2)                                                                             \
+            hipLaunchKernelGGL((k_stem3<CO, 32>), grid, dim3(256), 0, st, x, H, W, wt, bias, act, y, Ho, Wo, tiles_x);  \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_stem3<CO, 0>), grid, dim3(256), 0, st, x, H, W, wt, bias, act, y, Ho, Wo, tiles_x);   \
+    } while (0)
+    if (Co == 32) STEM3_LAUNCH(32);
+    else if (Co == 40) STEM3_LAUNCH(40);
+    else if (Co == 48) STEM3_LAUNCH(48);
+    else STEM3_LAUNCH(64);
+#undef STEM3_LAUNCH
     return last();
 }
 

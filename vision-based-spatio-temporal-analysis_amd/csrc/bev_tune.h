@@ -22,5 +22,6 @@ int conv_h16_tune(int value);
 
 // BEV_TUNE_DW_RUN (bev_effnet.hip).
 int dw_tune(int value);
+int stem3_tune(int value);
 
 }  // namespace bev

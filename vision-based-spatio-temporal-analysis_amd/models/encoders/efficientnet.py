@@ -140,6 +140,12 @@ class EfficientNet(nn.Module):
                                  if isinstance(self.blocks[FEATURE_STAGE[i]][-1], DepthwiseSeparableConv)
                                  else self.blocks[FEATURE_STAGE[i]][-1].bn3.num_features for i in range(5)]
         self._folded = {}
+        # the expansion 1x1 convs on the split-bf16 kernels: measured slower (r06q A/B, B3 encoder ms per 2-frame step:
+        # split 13.81, exact-f32 13.67), so off
+        self.x6_expand = False
+        self.stem3 = True  # the stem on its vector-ALU kernel (bev_conv2d_stem3_f32) instead of the implicit GEMM
+        self.pw_stream = True  # eval: the wide tiny-K expansions on k_pw_mfma too (see forward_features_nhwc)
+        self._stem3_key = None
 
     def _fc(self, conv, bn):
         """Pointwise / stem convs: exact-f32 kernels.  The trunk is HBM-bound; its Ci % 16 == 0 pointwise convs on the
@@ -147,6 +153,33 @@ class EfficientNet(nn.Module):
         k = id(conv)
         if k not in self._folded:
             self._folded[k] = FoldedConv(conv, bn)
+        return self._folded[k]
+
+    def _stem(self, x):
+        """conv_stem -> bn1 -> SiLU: the vector-ALU stem kernel (bev_conv2d_stem3_f32) for the timm 3x3 / s2 / p1
+        shape when `stem3`, else the generic implicit GEMM (in_nchw)."""
+        c = self.conv_stem
+        fc = self._fc(c, self.bn1)
+        if not (self.stem3 and c.in_channels == 3 and c.kernel_size == (3, 3) and c.stride == (2, 2)
+                and c.padding == (1, 1) and c.groups == 1 and c.dilation == (1, 1)
+                and c.out_channels in (32, 40, 48, 64)):
+            return fc(x, relu=_nat.ACT_SILU, in_nchw=True)
+        key = tuple((t.data_ptr(), t._version) for t in fc._tensors()) + (str(x.device),)
+        if self._stem3_key != key:
+            w, b = fc.folded(x.device)
+            self._stem3_w = w.permute(1, 2, 3, 0).reshape(27, c.out_channels).contiguous()  # [(ci, ky, kx)][Co]
+            self._stem3_b = b.contiguous().float()
+            self._stem3_key = key
+        return _nat.conv2d_stem3(x, self._stem3_w, self._stem3_b, _nat.ACT_SILU)
+
+    def _fc_expand(self, conv, bn):
+        """The inverted-residual expansion (1x1, Ci -> 6 Ci, SiLU): on the split-bf16 kernels (bev_conv2d_x6_f32, fp32
+        class) when `x6_expand` and the arithmetic is bf16x6 and Ci % 16 == 0, else as _fc."""
+        if not self.x6_expand:
+            return self._fc(conv, bn)
+        k = ("x6", id(conv))
+        if k not in self._folded:
+            self._folded[k] = FoldedConv(conv, bn, split_ok=True)
         return self._folded[k]
 
     def _fdw(self, conv, bn):
@@ -173,7 +206,7 @@ class EfficientNet(nn.Module):
         if isinstance(blk, DepthwiseSeparableConv):
             y, ps = self._fdw(blk.conv_dw, blk.bn1)(x, want_psum=True)
             return self._project(blk.conv_pw, blk.bn2, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
-        h = self._fc(blk.conv_pw, blk.bn1)(x, relu=_nat.ACT_SILU)
+        h = self._fc_expand(blk.conv_pw, blk.bn1)(x, relu=_nat.ACT_SILU)
         y, ps = self._fdw(blk.conv_dw, blk.bn2)(h, want_psum=True)
         return self._project(blk.conv_pwl, blk.bn3, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
 
@@ -190,8 +223,11 @@ class EfficientNet(nn.Module):
             raise IndexError(f"efficientnet feature index {out_index} out of range 0..4")
         if self.training:  # torch semantics: train-mode BN uses batch statistics, with or without autograd
             return self._forward_train(x, out_index)
-        y = self._fc(self.conv_stem, self.bn1)(x, relu=_nat.ACT_SILU, in_nchw=True)
-        with torch.no_grad():
+        y = self._stem(x)
+        # inference: every tiny-K (Ci 24-48) 1x1 conv on the wave-streaming k_pw_mfma (BEV_TUNE_CONV_PW_SMALL 3), the
+        # wide expansions included; training keeps the default (2: narrow outputs only), whose k order the float64
+        # gradient bounds were set on (bev_conv.hip try_pw_mfma)
+        with torch.no_grad(), _nat.tuned(CONV_PW_SMALL=3 if self.pw_stream else 2):
             for si in range(FEATURE_STAGE[out_index] + 1):
                 for blk in self.blocks[si]:
                     y = self._block(blk, y)
