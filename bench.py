@@ -182,7 +182,8 @@ def stem_flops(enc, H, W):
 def backbone_bytes(enc, H, W):
     """Algorithmic HBM bytes of one image through the EfficientNet trunk + proj as the launches run it: every
     launch reads its input once and writes its output once (+ the residual it adds), fp32 NHWC; the SE
-    excitation is applied in the projection conv's operand load (no extra pass).  Weights are negligible."""
+    excitation is applied in the projection conv's operand load (no extra pass); a fused inverted residual
+    (bev_ir_expand_dw_f32) reads its input and writes the depthwise output only.  Weights are negligible."""
     from models.encoders.efficientnet import FEATURE_STAGE, DepthwiseSeparableConv
     net = enc.backbone
 
@@ -196,11 +197,14 @@ def backbone_bytes(enc, H, W):
         for blk in net.blocks[si]:
             cin = blk.conv_dw.in_channels if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pw.in_channels
             x_bytes = 4 * h * w * cin
-            if not isinstance(blk, DepthwiseSeparableConv):
-                total += x_bytes + 4 * h * w * blk.conv_pw.out_channels  # expand 1x1
             cdw = blk.conv_dw.in_channels
             h2, w2 = out_hw(blk.conv_dw, h, w)
-            total += 4 * (h * w * cdw + h2 * w2 * cdw)  # depthwise
+            if net.ir_fused_block(blk, cin):  # expansion + depthwise in one pass: the expanded tensor never moves
+                total += x_bytes + 4 * h2 * w2 * cdw
+            else:
+                if not isinstance(blk, DepthwiseSeparableConv):
+                    total += x_bytes + 4 * h * w * blk.conv_pw.out_channels  # expand 1x1
+                total += 4 * (h * w * cdw + h2 * w2 * cdw)  # depthwise
             last = blk.conv_pw if isinstance(blk, DepthwiseSeparableConv) else blk.conv_pwl
             total += 4 * (h2 * w2 * cdw + h2 * w2 * last.out_channels)  # projection (+ excitation)
             if blk.has_skip:
@@ -314,9 +318,13 @@ def pmc_traffic(args, world: int = 1) -> dict:
     # cam_write -> tools/pmc_traffic.py -> profiles/r*_pmc_traffic_k5.json)
     k5 = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.backbone, args.camera_shard,
           args.warp_kernel, world) == (16, 64, (2160, 3840), (480, 1440), "resnet50", True, "dma", 1)
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_traffic_k5.json" if k5 else
-                                          "r*_pmc_traffic.json")))
-    if not (default or k5) or not files:
+    # the EfficientNet-B3 line (BASELINE configs[3]): its own passes (tools/pmc_traffic.py ... k4 ->
+    # profiles/r*_pmc_traffic_k4.json); "conv" = every encoder launch of a step
+    k4 = (args.views, args.channels, tuple(args.img), tuple(args.bev), args.batch, args.backbone, args.camera_shard,
+          args.warp_kernel) == (7, 64, (1080, 1920), (480, 1440), 2, "efficientnet_b3", False, "dma")
+    pat = "r*_pmc_traffic_k5.json" if k5 else "r*_pmc_traffic_k4.json" if k4 else "r*_pmc_traffic.json"
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", pat)))
+    if not (default or k5 or k4) or not files:
         return {}
     d = json.load(open(files[-1]))
     if d.get("conv_arith", "f32") != args.conv_arith:  # profiled under the other conv arithmetic
@@ -584,7 +592,7 @@ def main():
             ach_bb = nbytes / (bb_ms * 1e-3) / 1e9
             roof_bb_hbm = {"kernel": "k_conv + k_dwconv(_t) + k_se_gate (EfficientNet trunk + proj, every launch of "
                                      "one step)", "bound": "hbm", "achieved": round(ach_bb, 1), "peak": PEAK_HBM_GBS,
-                           "unit": "GB/s", "frac": round(ach_bb / PEAK_HBM_GBS, 4), "traffic": None,
+                           "unit": "GB/s", "frac": round(ach_bb / PEAK_HBM_GBS, 4), "traffic": pmc.get("conv"),
                            "alg_bytes_per_step": nbytes, "encoder_stage_ms": round(bb_ms, 4),
                            "timing": "HIP events on the caller stream around the whole encoder stage",
                            "bytes": "each launch reads its input once and writes its output once (+ residual), "

@@ -81,7 +81,10 @@ const char *bev_build_source_hash(void);
  *   projection so the feature maps that conv writes stay in the Infinity Cache for the warp.  Same results.
  * BEV_TUNE_STEM3_STAGE: bev_conv2d_stem3_f32 output stores: staged in LDS and written as whole NHWC row runs (1 KiB
  *   per instruction), 64 pixels per wave and pass (1) or 32 (2, default: half the LDS, more resident workgroups);
- *   0 = straight from registers (16 B per lane at a pixel stride).  Same results. */
+ *   0 = straight from registers (16 B per lane at a pixel stride).  Same results.
+ * BEV_TUNE_WARP_PERSIST: fused warp sum / mean with C == 64, NCHW or rank-chunk-major output and a footprint-box
+ *   workspace: 0 (default) = one workgroup per (tile, frame); 1 / 2 = the persistent work-queue kernel with 8 queues
+ *   (one per XCD) / one queue (A/B options, measured slower).  Same results. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -97,6 +100,7 @@ const char *bev_build_source_hash(void);
 #define BEV_TUNE_DW_RUN 14
 #define BEV_TUNE_CONV_X6_NT 16
 #define BEV_TUNE_STEM3_STAGE 17
+#define BEV_TUNE_WARP_PERSIST 18
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------
@@ -337,6 +341,18 @@ int bev_dwconv_psum_blocks(int Ho, int Wo, int C, int stride);
  * every other shape and stride the per-pixel kernel. */
 int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt, const float *bias, int K, int stride,
                      int pad, int act, float *y, int Ho, int Wo, float *psum, void *stream);
+
+/* device: an EfficientNet inverted residual's expansion and depthwise conv in one pass (timm InvertedResidual
+ * conv_pw -> bn1 -> SiLU -> conv_dw -> bn2 -> SiLU, cnn_encoder.py:26), BN folded:
+ *   h[n,iy,ix,c] = SiLU( sum_k x[n,iy,ix,k] * we[c][k] + be[c] )   (0 outside the image: the conv_dw zero padding)
+ *   y[n,oy,ox,c] = SiLU( bd[c] + sum_{ky,kx} h[n, oy*s-pad+ky, ox*s-pad+kx, c] * wd[ky*K+kx][c] ),  pad = K / 2
+ * and, as bev_dwconv2d_f32's psum, the channel sums of y per workgroup: psum [N][nb][Cm], nb =
+ * bev_ir_expand_dw_blocks(Ho, Wo, K, stride).  h is never stored.  x [N][H][W][Ci] NHWC fp32 with Ci in {16, 24, 32,
+ * 40, 48}, Cm % 48 == 0, K in {3, 5}, stride in {1, 2}; x, bd, y, psum 16-B aligned. */
+int bev_ir_expand_dw_blocks(int Ho, int Wo, int K, int stride);
+int bev_ir_expand_dw_f32(const float *x, int N, int H, int W, int Ci, const float *we, const float *be, int Cm,
+                         const float *wd, const float *bd, int K, int stride, float *y, int Ho, int Wo, float *psum,
+                         void *stream);
 
 /* device: the EfficientNet stem (timm conv_stem -> bn1 -> SiLU, cnn_encoder.py:26: 3x3, stride 2, pad 1, 3 input
  * channels), BN folded, from NCHW images to NHWC:

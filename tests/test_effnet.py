@@ -150,6 +150,48 @@ def test_conv_silu_epilogue():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Ci,Cm,K,S,N,H,W", [(24, 144, 3, 2, 2, 37, 70), (32, 192, 3, 1, 1, 33, 61),
+                                             (32, 192, 5, 2, 1, 40, 47), (48, 288, 5, 1, 2, 19, 35),
+                                             (16, 96, 3, 1, 1, 5, 3), (40, 240, 5, 2, 1, 17, 100)])
+def test_ir_expand_dw_fused_vs_float64_and_separate(Ci, Cm, K, S, N, H, W):
+    """bev_ir_expand_dw_f32 (an inverted residual's expansion + depthwise conv in one pass, h never stored) against
+    float64 torch of conv_pw -> bn1 -> SiLU -> conv_dw -> bn2 -> SiLU (<= 1e-5 of max|ref|) and against the separate
+    native launches (1x1 conv + bev_dwconv2d_f32, same bound), plus the SE squeeze: the partial sums add up to the
+    channel sums of y -- ragged strips / row segments, tiny maps, every (K, stride) and Ci."""
+    import bev_native as nat
+    from models.encoders.efficientnet import FoldedDW
+    from models.encoders.resnet import FoldedConv
+    torch.manual_seed(Ci + K + S + H)
+    pw, bn1 = torch.nn.Conv2d(Ci, Cm, 1, bias=False), torch.nn.BatchNorm2d(Cm)
+    dw, bn2 = torch.nn.Conv2d(Cm, Cm, K, S, K // 2, groups=Cm, bias=False), torch.nn.BatchNorm2d(Cm)
+    with torch.no_grad():
+        for bn in (bn1, bn2):
+            bn.weight.uniform_(0.5, 1.5), bn.bias.uniform_(-0.5, 0.5)
+            bn.running_mean.uniform_(-0.2, 0.2), bn.running_var.uniform_(0.5, 2.0)
+    for m in (bn1, bn2):
+        m.eval()
+    x = _rand((N, Ci, H, W), Ci + H)
+    with torch.no_grad():
+        h = F.silu(bn1.double()(F.conv2d(x.double(), pw.weight.double())))
+        ref = F.silu(bn2.double()(F.conv2d(h, dw.weight.double(), stride=S, padding=K // 2, groups=Cm)))
+    fc = FoldedConv(pw.to(DEV), bn1.float().to(DEV))
+    fdw = FoldedDW(dw.to(DEV), bn2.float().to(DEV))
+    fdw.prepare(DEV)
+    w, b = fc.folded(DEV)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    y, ps = nat.ir_expand_dw(xn, w.reshape(Cm, Ci).contiguous(), b, fdw.wt, fdw.bias, K, S)
+    y2, _ = fdw(fc(xn, relu=nat.ACT_SILU), want_psum=True)
+    torch.cuda.synchronize()
+    ref = ref.permute(0, 2, 3, 1)
+    scale = ref.abs().max().item()
+    assert y.shape == ref.shape
+    assert (y.double().cpu() - ref).abs().max().item() <= 1e-5 * scale
+    assert (y - y2).abs().max().item() <= 1e-5 * scale
+    sums = y.double().sum(dim=(1, 2))
+    assert (ps.double().sum(1) - sums).abs().max().item() <= 1e-5 * max(1.0, sums.abs().max().item())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("Co,N,H,W", [(40, 2, 37, 70), (32, 1, 16, 128), (48, 1, 9, 250), (64, 3, 30, 3)])
 def test_stem3_vs_float64_and_generic_conv(Co, N, H, W):
     """bev_conv2d_stem3_f32 (the EfficientNet stem on the vector ALU) == torch's conv_stem -> bn1 -> SiLU in float64

@@ -23,8 +23,9 @@ from models.encoders.cnn_encoder import CNNEncoder  # noqa: E402
 
 def apply(name, rn):
     if hasattr(rn, "x6_expand"):  # EfficientNet (--backbone efficientnet_b3): base / x6expand / nostem3
-        if name not in ("base", "x6expand", "nostem3", "nopwstream"):
+        if name not in ("base", "x6expand", "nostem3", "nopwstream", "noirfuse"):
             raise SystemExit(f"unknown EfficientNet variant {name}")
+        rn.ir_fuse = name != "noirfuse"
         rn.x6_expand = name == "x6expand"
         rn.stem3 = name != "nostem3"
         rn.pw_stream = name != "nopwstream"

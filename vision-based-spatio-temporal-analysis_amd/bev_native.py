@@ -103,6 +103,8 @@ SIGNATURES = {
     "bev_dwconv2d_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_se_gate_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp]),
     "bev_conv2d_stem3_f32": (_i, [_vp, _i, _i, _i, _vp, _vp, _i, _i, _vp, _i, _i, _vp]),
+    "bev_ir_expand_dw_blocks": (_i, [_i, _i, _i, _i]),
+    "bev_ir_expand_dw_f32": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _i, _i, _vp, _i, _i, _vp, _vp]),
     "bev_channel_scale_f32": (_i, [_vp, _i, _i64, _i, _vp, _vp]),
     "bev_decode_peaks_f32": (_i, [_vp, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "bev_decode_nms_f32": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _f, _f, _f, _f, _f, _vp, _vp, _vp, _vp]),
@@ -260,6 +262,7 @@ TUNE_CONV_PW_SMALL = 13
 TUNE_DW_RUN = 14
 TUNE_CONV_X6_NT = 16
 TUNE_STEM3_STAGE = 17
+TUNE_WARP_PERSIST = 18
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 
@@ -1144,6 +1147,30 @@ def conv2d_stem3(x: torch.Tensor, wt: torch.Tensor, bias: torch.Tensor, act: int
                                         _ptr(y), Ho, Wo, _stream(x))
     _check(rc, "bev_conv2d_stem3_f32")
     return y
+
+
+def ir_expand_dw(x: torch.Tensor, we: torch.Tensor, be: torch.Tensor, wd: torch.Tensor, bd: torch.Tensor, K: int,
+                 stride: int):
+    """An inverted residual's expansion (1x1, BN folded, SiLU) and depthwise KxK / stride conv (BN folded, SiLU,
+    pad K // 2) in one pass (bev_ir_expand_dw_f32): x [N,H,W,Ci] NHWC, we [Cm, Ci], be [Cm], wd [K*K, Cm] tap-major,
+    bd [Cm] -> (y [N,Ho,Wo,Cm] NHWC, SE partial sums [N, nb, Cm]) like dwconv2d_nhwc(want_psum=True) over the
+    expanded tensor, which is never stored."""
+    x = x.contiguous()
+    _require_gpu(x, we, be, wd, bd)
+    N, H, W, Ci = x.shape
+    Cm = we.shape[0]
+    pad = K // 2
+    Ho, Wo = (H + 2 * pad - K) // stride + 1, (W + 2 * pad - K) // stride + 1
+    nb = lib().bev_ir_expand_dw_blocks(Ho, Wo, K, stride)
+    _check(0 if nb > 0 else nb, "bev_ir_expand_dw_blocks")
+    y = torch.empty(N, Ho, Wo, Cm, device=x.device, dtype=torch.float32)
+    psum = torch.empty(N, nb, Cm, device=x.device, dtype=torch.float32)
+    with _span("dwconv", x):
+        rc = lib().bev_ir_expand_dw_f32(_ptr(x), N, H, W, Ci, _ptr(we.contiguous()), _ptr(be.contiguous()), Cm,
+                                        _ptr(wd.contiguous()), _ptr(bd.contiguous()), K, stride, _ptr(y), Ho, Wo,
+                                        _ptr(psum), _stream(x))
+    _check(rc, "bev_ir_expand_dw_f32")
+    return y, psum
 
 
 def se_gate(psum: torch.Tensor, hw: int, w1: torch.Tensor, b1: torch.Tensor, w2: torch.Tensor, b2: torch.Tensor):

@@ -588,6 +588,122 @@ __global__ __launch_bounds__(256) void k_stem3(const float *__restrict__ x, int 
     }
 }
 
+// k_irdw: an EfficientNet inverted residual's expansion and depthwise conv as ONE pass (timm InvertedResidual
+// conv_pw -> bn1 -> SiLU -> conv_dw -> bn2 -> SiLU, cnn_encoder.py:26), plus the SE squeeze partial sums.  The
+// expanded tensor h (Cm = 6 Ci channels at the block's input resolution: 4.2 GB per B3 bench step in blocks.1.0
+// alone) never reaches HBM: a workgroup owns a strip of TC output columns x IR_RSEG output rows x 48 channels (3
+// waves x 16) and walks down its rows; each input row the strip needs is staged once (IR_IC = 32 pixels x CI, zero
+// outside the image), expanded by each wave on the fp32 matrix cores (v_mfma_f32_16x16x4_f32: 16 pixels x 16
+// channels, K = CI; BN folded, SiLU; h = 0 outside the image -- the depthwise conv's zero padding) into the wave's
+// ring of the last K rows in LDS, and every output row is then the K x K taps of that ring (float4 per lane: 16
+// pixels x 4 channel quads), + bias, SiLU, stored NHWC and summed into the squeeze partials.
+// Numerics: h = SiLU(fp32 dot over CI + bias) (k order of the MFMA: fp32-tolerance equal to the 1x1 conv kernels);
+// the depthwise taps in k_dwconv's order from the bias (ky-major, kx-minor; zero taps exact).  psum[n][blk][c] over
+// the workgroup's outputs (blk = strip + strips * segment).
+constexpr int IR_W = 3;       // waves per workgroup (16 expanded channels each: 48 per workgroup)
+constexpr int IR_IC = 32;     // input columns per strip: two 16-pixel MFMA groups
+constexpr int IR_RSEG = 16;   // output rows per workgroup
+constexpr int IR_HS = 20;     // ring pixel stride (floats): conflict-free h writes, 16-B aligned quads
+template <int K, int S> constexpr int ir_tc() { return (IR_IC - K) / S + 1; }  // output columns per strip
+
+typedef float irf4 __attribute__((ext_vector_type(4)));
+
+template <int K, int S, int CI>
+__global__ __launch_bounds__(64 * IR_W) void k_irdw(const float *__restrict__ x, int H, int W,
+                                                    const float *__restrict__ we, const float *__restrict__ be,
+                                                    const float *__restrict__ wd, const float *__restrict__ bd, int Cm,
+                                                    float *__restrict__ y, int Ho, int Wo, float *__restrict__ psum,
+                                                    int strips, int segs) {
+    constexpr int TC = ir_tc<K, S>(), PAD = K / 2, CQ = CI / 4, XS = CI + 1;
+    static_assert(CI % 4 == 0 && CI <= 64, "CI");
+    __shared__ float xs[IR_IC * XS];                                          // one staged input row
+    __shared__ __attribute__((aligned(16))) float ring[IR_W][K][IR_IC * IR_HS];  // the last K expanded rows per wave
+    __shared__ __attribute__((aligned(16))) float wds[K * K][16 * IR_W];      // depthwise weights of the 48 channels
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int blk = blockIdx.x, sxi = blk % strips, syi = blk / strips, n = blockIdx.y;
+    const int chw = blockIdx.z * 16 * IR_W, ch0 = chw + wave * 16;
+    const int c0 = sxi * TC, r0 = syi * IR_RSEG;
+    const int ix0 = c0 * S - PAD;
+    const int rows_out = min(IR_RSEG, Ho - r0);
+    // expansion B operand (k = lane / 16 + 4 step, channel ch0 + lane % 16) and bias
+    float bw[CQ];
+#pragma unroll
+    for (int st = 0; st < CQ; ++st) bw[st] = we[(int64_t)(ch0 + (lane & 15)) * CI + 4 * st + (lane >> 4)];
+    const float bexp = be[ch0 + (lane & 15)];
+    for (int e = tid; e < K * K * 16 * IR_W; e += 64 * IR_W) {
+        const int t = e / (16 * IR_W), c = e - t * (16 * IR_W);
+        wds[t][c] = wd[(int64_t)t * Cm + chw + c];
+    }
+    const int p = lane >> 2, q = lane & 3;  // depthwise: output pixel p (+16 per pass), channel quad q
+    const irf4 bdw = *(const irf4 *)(bd + ch0 + 4 * q);
+    irf4 ssum = {0.f, 0.f, 0.f, 0.f};
+    const float *xn = x + (int64_t)n * H * W * CI;
+    float *hr = &ring[wave][0][0];
+    auto expand_row = [&](int iy) {  // stage + expand input row iy into ring slot iy mod K (iy may be outside)
+        __syncthreads();  // the previous row's staged pixels are no longer read
+        const bool rin = (unsigned)iy < (unsigned)H;
+        for (int e = tid; e < IR_IC * CQ; e += 64 * IR_W) {
+            const int px = e / CQ, cq = e - px * CQ, ix = ix0 + px;
+            irf4 v = {0.f, 0.f, 0.f, 0.f};
+            if (rin && (unsigned)ix < (unsigned)W) v = *(const irf4 *)(xn + ((int64_t)iy * W + ix) * CI + 4 * cq);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) xs[px * XS + 4 * cq + u] = v[u];
+        }
+        __syncthreads();
+        const int slot = ((iy % K) + K) % K;
+#pragma unroll
+        for (int g = 0; g < IR_IC / 16; ++g) {
+            irf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int st = 0; st < CQ; ++st)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[(g * 16 + (lane & 15)) * XS + 4 * st + (lane >> 4)], bw[st],
+                                                           acc, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int px = g * 16 + 4 * (lane >> 4) + r, ix = ix0 + px;
+                const bool in = rin && (unsigned)ix < (unsigned)W;
+                hr[slot * IR_IC * IR_HS + px * IR_HS + (lane & 15)] = in ? silu_hw(acc[r] + bexp) : 0.0f;
+            }
+        }
+    };
+    int iy_next = r0 * S - PAD;
+    for (int ro = 0; ro < rows_out; ++ro) {
+        const int r = r0 + ro, iy_top = r * S - PAD;
+        while (iy_next < iy_top + K) expand_row(iy_next++);
+        // this wave's ring writes precede its reads (LDS is in order within a wave)
+#pragma unroll
+        for (int pp = 0; pp < (TC + 15) / 16; ++pp) {
+            const int px = pp * 16 + p, c = c0 + px;
+            if (px < TC && c < Wo) {
+                irf4 acc = bdw;
+#pragma unroll
+                for (int ky = 0; ky < K; ++ky) {
+                    const int slot = (((iy_top + ky) % K) + K) % K;
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) {
+                        const irf4 h = *(const irf4 *)(hr + slot * IR_IC * IR_HS + (px * S + kx) * IR_HS + 4 * q);
+                        const irf4 w = *(const irf4 *)(&wds[ky * K + kx][wave * 16 + 4 * q]);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) acc[u] = __builtin_fmaf(h[u], w[u], acc[u]);
+                    }
+                }
+                irf4 o;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o[u] = silu_hw(acc[u]);
+                *(irf4 *)(y + (((int64_t)n * Ho + r) * Wo + c) * Cm + ch0 + 4 * q) = o;
+                ssum += o;
+            }
+        }
+    }
+    // squeeze partials: the 16 pixel lanes of each channel quad, fixed order
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ssum[u] += __shfl_xor(ssum[u], o);
+    }
+    if (p == 0) *(irf4 *)(psum + ((int64_t)n * strips * segs + blk) * Cm + ch0 + 4 * q) = ssum;
+}
+
 inline int last() {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -704,6 +820,47 @@ int bev_dwconv2d_f32(const float *x, int N, int H, int W, int C, const float *wt
     else if (K == 3) launch_dwconv_t<3, 2>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     else if (stride == 1) launch_dwconv_t<5, 1>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
     else launch_dwconv_t<5, 2>(dq, grid, st, x, H, W, C, wt, bias, pad, act, y, Ho, Wo, psum, nb);
+    return last();
+}
+
+int bev_ir_expand_dw_blocks(int Ho, int Wo, int K, int stride) {
+    if (Ho <= 0 || Wo <= 0 || (K != 3 && K != 5) || (stride != 1 && stride != 2)) return BEV_ERR_ARGS;
+    const int tc = (IR_IC - K) / stride + 1;
+    return ((Wo + tc - 1) / tc) * ((Ho + IR_RSEG - 1) / IR_RSEG);
+}
+
+int bev_ir_expand_dw_f32(const float *x, int N, int H, int W, int Ci, const float *we, const float *be, int Cm,
+                         const float *wd, const float *bd, int K, int stride, float *y, int Ho, int Wo, float *psum,
+                         void *stream) {
+    if (!x || !we || !be || !wd || !bd || !y || !psum || N < 0 || H <= 0 || W <= 0 || Cm <= 0 || Cm % 48 != 0)
+        return BEV_ERR_ARGS;
+    if ((Ci != 16 && Ci != 24 && Ci != 32 && Ci != 40 && Ci != 48) || (K != 3 && K != 5) || (stride != 1 && stride != 2))
+        return BEV_ERR_ARGS;
+    const int pad = K / 2;
+    if (Ho != (H + 2 * pad - K) / stride + 1 || Wo != (W + 2 * pad - K) / stride + 1) return BEV_ERR_ARGS;
+    if ((((uintptr_t)x | (uintptr_t)bd | (uintptr_t)y | (uintptr_t)psum) & 15) != 0) return BEV_ERR_ARGS;
+    if ((int64_t)H * W * Ci >= ((int64_t)1 << 31) || (int64_t)Ho * Wo * Cm >= ((int64_t)1 << 31)) return BEV_ERR_ARGS;
+    if (N == 0) return 0;
+    const int tc = (IR_IC - K) / stride + 1, strips = (Wo + tc - 1) / tc, segs = (Ho + IR_RSEG - 1) / IR_RSEG;
+    const dim3 grid(strips * segs, N, Cm / 48), block(64 * IR_W);
+    hipStream_t st = (hipStream_t)stream;
+#define IRDW(KK, SS, CC)                                                                                           \
+    hipLaunchKernelGGL((k_irdw<KK, SS, CC>), grid, block, 0, st, x, H, W, we, be, wd, bd, Cm, y, Ho, Wo, psum, strips, \
+                       segs)
+#define IRDW_CI(KK, SS)                                                                                            \
+    do {                                                                                                           \
+        if (Ci == 16) IRDW(KK, SS, 16);                                                                            \
+        else if (Ci == 24) IRDW(KK, SS, 24);                                                                       \
+        else if (Ci == 32) IRDW(KK, SS, 32);                                                                       \
+        else if (Ci == 40) IRDW(KK, SS, 40);                                                                       \
+        else IRDW(KK, SS, 48);                                                                                     \
+    } while (0)
+    if (K == 3 && stride == 1) IRDW_CI(3, 1);
+    else if (K == 3) IRDW_CI(3, 2);
+    else if (stride == 1) IRDW_CI(5, 1);
+    else IRDW_CI(5, 2);
+#undef IRDW_CI
+#undef IRDW
     return last();
 }
 

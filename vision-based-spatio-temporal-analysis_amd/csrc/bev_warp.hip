@@ -1296,16 +1296,291 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     }
 }
 
+// -------------------------------------------------------------------------
+// fused warp + sum / mean, persistent (k_warp_fuse_p; BEV_TUNE_WARP_PERSIST 1 / 2, an A/B option: measured SLOWER)
+// -------------------------------------------------------------------------
+// Measured (r06w-r06y, tools/warp_persist_ab.py, interleaved, us per launch): bench 7 cams B = 2 per-tile 135-137,
+// persistent 8 queues 150-154, 1 queue 144-146 (8 queues + stealing from the next queue at the tail: 194);
+// K5 16 cams 4K 218-224 vs 245-252.  Bit-identical in every form (test_fused_persistent_equals_per_tile_kernel).
+// Why it loses: the in-order vmcnt hides the first DMA behind the previous item's stores (vmcnt(63)), but EVERY
+// later DMA wait of the item (the end of each view) also waits for those 64 stores, so their drain lands on the
+// item's first view; a workgroup of v2 simply ends after its stores and the drain overlaps its successor's start.
+// k_warp_fuse_v2's per-item work (one frame x 16 x 16 BEV tile, 64 channels: taps, footprint DMA one view ahead,
+// LDS sampling, view order from +0, the mean by the same division) in CUs x OCC resident workgroups that pull items
+// from work queues instead of one workgroup per item.  What the loop buys (v2's s_memtime timeline: per workgroup
+// ~34 k cycles = prologue 1.6 k + first view's DMA 4.2 k + views 25.2 k + stores 3.1 k, and 2 k from a workgroup's
+// end to its successor's start): the next item's boxes and first-view DMA are issued BEFORE this item's output
+// stores, so that DMA lands while the 64 store instructions issue and the next item's taps are computed; the wait
+// before its first sampling is `vmcnt(63)` (every vector-memory op counts in issue order, MI355X_MICROARCH.md
+// §vmcnt: with >= 64 stores younger than the DMA, <= 63 outstanding means the DMA is done, the stores need not be),
+// and the barrier after it a raw s_barrier (no fence drain of the stores).  No workgroup launch gap.
+// Queues: q = blockIdx % 8 (the XCD under round-robin dispatch) owns the contiguous item range
+// [total q / 8, total (q + 1) / 8) (item = frame x tiles + tile): an XCD walks neighbouring tiles, whose footprints
+// share source pixels in its L2.  A workgroup's first item is static (lo + blockIdx / 8), the next ones a ticket
+// (atomicAdd on the queue word, fetched at the start of the current item and read after its views).  The queue
+// words live after the boxes in the workspace: zeroed by k_warp_boxes and reset by the last workgroup to finish
+// (a finished-count word), so every launch starts from zero.  Each workgroup exits once its queue is drained --
+// no inter-workgroup waits, so residency is not needed for progress.
+// Same per-cell arithmetic and view order as v2 => bit-identical output.
+constexpr int WQ_WORDS = 16;  // queue words after the boxes: [0..7] tickets per queue, [8] finished workgroups
+
+template <int MODE, int OCC, bool CHUNK>
+__global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_p(const float *__restrict__ feats, int64_t sN, int64_t sH,
+                                                         int64_t sW, const float *__restrict__ Hmat,
+                                                         const float *__restrict__ xs, const float *__restrict__ ys,
+                                                         int B, int V, int C, int Hf, int Wf, float sx, float sy,
+                                                         int Hb, int Wb, float *__restrict__ out, int pool,
+                                                         const uint2 *__restrict__ boxes_in, int rpr,
+                                                         unsigned *__restrict__ queue, int nqs) {
+    static_assert(MODE != BEV_FUSE_MAX, "sum / mean");
+    constexpr int NW = FT_NT / 64, TH = 16, TW = FT_NT / TH, CK = 64, SL = V2_SL, PS = SL * 16;
+    static_assert(WARP_CK == 64, "one workgroup per (tile, frame)");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int zp = pool;
+    int *red = reinterpret_cast<int *>(smem + pool + 256);
+    int *slot = reinterpret_cast<int *>(smem + pool + 256 + 4 * NW * sizeof(int));  // the next ticket (htab area)
+    const int maxpix = pool / PS - 4;
+    const int ntx = (Wb + TW - 1) / TW, nty = (Hb + TH - 1) / TH, nt = ntx * nty;
+    const int total = nt * B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int tr, tc;
+    tile_cell<TH>(lane, wave, tr, tc);
+    const int qi = (int)(blockIdx.x % (unsigned)nqs);
+    const int nq = (int)(gridDim.x / (unsigned)nqs);  // workgroups per queue (gridDim.x % nqs == 0)
+    const int lo = (int)((int64_t)total * qi / nqs), hi = (int)((int64_t)total * (qi + 1) / nqs);
+    bool hdr_ok = false;
+    {
+        const uint4 hd = reinterpret_cast<const uint4 *>(boxes_in)[-1];
+        hdr_ok = hd.x == BOX_MAGIC && (int)hd.y == maxpix && (int)hd.z == V && (int)hd.w == TH;
+    }
+    const Grid grid = make_grid(Hf, Wf);
+    const MeanDiv md = mean_div_of(V);
+    if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+    const size_t plane = (size_t)Hb * Wb;
+    const size_t oplane = CHUNK ? (size_t)rpr * Wb : plane;
+    auto dma = [&](const float *fp, int x0, int y0, int w, int h, int o) {
+        dma_block<SL>(fp, (int)sH, (int)sW, x0, y0, w, w * h, smem, o, wave, lane, NW);
+    };
+
+    // the item being set up: frame, tile origin, this lane's cell, its centre, the boxes of its views
+    int b = 0, tyb = 0, txb = 0, ci = 0, cj = 0;
+    bool inside = false;
+    float cx = 0.f, cy = 0.f;
+    unsigned lba = 0, lbb = 0;
+    auto load_item = [&](int it) {
+        b = it / nt;
+        const int tile = it - b * nt;
+        tyb = tile / ntx;
+        txb = tile - tyb * ntx;
+        ci = tyb * TH + tr;
+        cj = txb * TW + tc;
+        inside = (ci < Hb) && (cj < Wb);
+        cx = xs[inside ? cj : 0];
+        cy = ys[inside ? ci : 0];
+        if (hdr_ok) {
+            const uint2 bx = lane < V ? boxes_in[((int64_t)b * nt + tile) * V + lane] : make_uint2(0u, 0u);
+            lba = bx.x;
+            lbb = bx.y;
+        } else {  // boxes made for another pool / V / tiling: every view by the exact per-cell reduction
+            lba = lane < V ? 0x80000000u : 0u;
+            lbb = 0u;
+        }
+    };
+    auto box_of = [&](int v) {
+        const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
+        const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
+        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
+    };
+    auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
+    auto live = [&](int u) { return !ok_of(u) || box_of(u).x1 >= 0; };
+    auto next_live = [&](int u) {  // sum / mean: views with an empty box contribute +0 -- skipped exactly
+        ++u;
+        while (u < V && !live(u)) ++u;
+        return u;
+    };
+    float ccx = 0.f, ccy = 0.f;
+    auto taps_of = [&](int v, bool in) {
+        float h[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) h[k] = Hmat[__builtin_amdgcn_readfirstlane((b * V + v) * 9) + k];
+        float ix, iy;
+        cell_ixy(h, ccx, ccy, grid, sx, sy, ix, iy);
+        Taps t = taps_from_ixy(ix, iy, grid);
+        if (!in) t.valid = 0;
+        return t;
+    };
+    // the first live view of the item just loaded, its DMA issued now (offn = 0) when its corner box fits the pool
+    int v_first = V, offn = -1;
+    Box bn{0, 0, -1, -1};
+    auto first_dma = [&]() {
+        v_first = next_live(-1);
+        bn = box_of(v_first < V ? v_first : 0);
+        offn = -1;
+        if (v_first < V) {
+            const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+            if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
+                offn = 0;
+                dma(feats + (int64_t)(b * V + v_first) * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, 0);
+            }
+        }
+    };
+
+    int item = lo + (int)(blockIdx.x / (unsigned)nqs);
+    if (item < hi) {
+        load_item(item);
+        first_dma();
+    }
+    bool stores_out = false;  // this wave issued the previous item's 64 output stores after the current first DMA
+    while (item < hi) {
+        int tkt = 0;
+        if (tid == 0) tkt = (int)atomicAdd(&queue[qi], 1u);  // the next ticket, read after this item's views
+        const int bi = b, ii = ci, jj = cj;
+        const bool in = inside;
+        ccx = cx;
+        ccy = cy;
+        asm volatile("" : "+v"(ccx), "+v"(ccy));  // keep the taps per item (no hoisting + spills)
+        float acc[CK];
+#pragma unroll
+        for (int k = 0; k < CK; ++k) acc[k] = 0.0f;
+        const float *fb = feats + (int64_t)(bi * V) * sN;
+        Taps tf;
+        bool have_f = false;
+        if (v_first < V && ok_of(v_first)) {
+            tf = taps_of(v_first, in);
+            have_f = true;
+        }
+        // the first live view's image (and the zero pixel); the previous item's stores may still be in flight
+        if (stores_out) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        for (int v = v_first, vn; v < V; v = vn) {
+            vn = next_live(v);
+            Box bx = bn;
+            const int off = offn;
+            const float *f = fb + (int64_t)v * sN;
+            Taps t;
+            bool have_t = false;
+            if (have_f) {
+                t = tf;
+                have_t = true;
+                have_f = false;
+            }
+            if (!ok_of(v)) {  // exact footprint by per-cell reduction (horizon tiles); staged synchronously
+                t = taps_of(v, in);
+                have_t = true;
+                put_box<NW>(red, wave_box(t), wave, lane);
+                __syncthreads();
+                bx = get_box<NW>(red);
+            }
+            const bool empty = bx.x1 < 0;
+            const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
+            bool done = empty;
+            if (!done && off < 0) {  // synchronous staging, overlapping blocks if larger than the pool (as v2)
+                int wb = bw, hb = bh, nbx = 1, nby = 1;
+                if (bw * bh > maxpix) {
+                    wb = (2 * bw <= maxpix) ? bw : maxpix / 2;
+                    hb = min(bh, maxpix / wb);
+                    nbx = (wb >= bw) ? 1 : (bw - 2) / (wb - 1) + 1;
+                    nby = (hb >= bh) ? 1 : (bh - 2) / (hb - 1) + 1;
+                }
+                const bool single = (nbx == 1) && (nby == 1);
+                if (single) dma(f, bx.x0, bx.y0, bw, bh, 0);
+                if (!have_t) {
+                    t = taps_of(v, in);
+                    have_t = true;
+                }
+                int mkx = 0, mky = 0;
+                if (!single && t.valid) {
+                    const int xlo = (t.valid & 5) ? t.x0 : t.x0 + 1, ylo = (t.valid & 3) ? t.y0 : t.y0 + 1;
+                    mkx = (nbx == 1) ? 0 : min((xlo - bx.x0) / (wb - 1), nbx - 1);
+                    mky = (nby == 1) ? 0 : min((ylo - bx.y0) / (hb - 1), nby - 1);
+                }
+                const bool wave_any = __ballot(t.valid != 0) != 0ull;
+                for (int ky = 0; ky < nby; ++ky)
+                    for (int kx = 0; kx < nbx; ++kx) {
+                        const int sx0 = bx.x0 + kx * (wb - 1), sy0 = bx.y0 + ky * (hb - 1);
+                        const int sbw = min(wb, bx.x1 - sx0 + 1), sbh = min(hb, bx.y1 - sy0 + 1);
+                        if (!single) {
+                            __syncthreads();
+                            dma(f, sx0, sy0, sbw, sbh, 0);
+                        }
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __syncthreads();
+                        const bool mine = single ? true : (t.valid != 0 && mkx == kx && mky == ky);
+                        const bool go = single ? wave_any : (__ballot(mine) != 0ull);
+                        if (go) sample_view<MODE, 1, CK>(acc, t, mine, v, smem, 0, sx0, sy0, sbw, zp);
+                    }
+                done = true;
+                __syncthreads();
+            }
+            if (vn < V) {  // look ahead: DMA of the next live view beside the live image of view v
+                bn = box_of(vn);
+                offn = -1;
+                const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
+                if (ok_of(vn) && bn.x1 >= 0 && npix <= maxpix) {
+                    const int need = ((npix * SL + 63) >> 6) * 1024;
+                    if (done || off < 0) offn = 0;
+                    else if (off == 0) {
+                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
+                    } else if (need <= off) offn = 0;
+                    if (offn >= 0) dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, offn);
+                }
+            }
+            if (!done) {
+                if (!have_t) t = taps_of(v, in);
+                if (__ballot(t.valid != 0) != 0ull && (!WARP_LANESKIP || t.valid))
+                    sample_view_pipe<MODE, CK, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
+            __syncthreads();  // all of it landed; image of view v and red[] are free
+        }
+        // the next item: its ticket, boxes and first-view DMA before this item's stores (the pool is free: every
+        // view of this item ended with a barrier after its last LDS read)
+        if (tid == 0) *slot = tkt;
+        __syncthreads();
+        const int nxt = lo + nq + __builtin_amdgcn_readfirstlane(*slot);
+        if (nxt < hi) {
+            load_item(nxt);
+            first_dma();
+        }
+        item = nxt;
+        if (in) {
+            if (!CHUNK) {
+                store_chunk(out + (size_t)bi * C * plane, plane, (ii * Wb + jj) * (int)sizeof(float), acc, MODE, md,
+                            (uint32_t)(plane * CK * sizeof(float)));
+            } else {
+                const int ck = ii / rpr;
+                const int ovoff = (int)(((size_t)ck * B * C * oplane + (size_t)(ii - ck * rpr) * Wb + jj) * sizeof(float));
+                const size_t orange = (size_t)((Hb + rpr - 1) / rpr) * B * C * oplane * sizeof(float);
+                store_chunk(out + (size_t)bi * C * oplane, oplane, ovoff, acc, MODE, md,
+                            out_range(orange, (size_t)bi * C * oplane));
+            }
+        }
+        stores_out = __ballot(in) != 0ull;
+    }
+    // queue bookkeeping: the last workgroup to finish resets the words for the next launch
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned d = atomicAdd(&queue[8], 1u);
+        if (d == gridDim.x - 1) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) atomicExch(&queue[k], 0u);
+        }
+    }
+}
+
 template <int TH, int TW = FT_NT / TH>
 __global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hmat, const float *__restrict__ xs,
                                                     const float *__restrict__ ys, int V, int Hf, int Wf, float sx,
                                                     float sy, int Hb, int Wb, int maxpix, int nty,
-                                                    uint2 *__restrict__ boxes) {
+                                                    uint2 *__restrict__ boxes, unsigned *__restrict__ queue) {
     const int ntx = (Wb + TW - 1) / TW, nt = ntx * nty;  // nty >= ceil(Hb / TH) box-tile rows (extra rows: empty)
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int b = blockIdx.y;
     if (t == 0 && b == 0)
         reinterpret_cast<uint4 *>(boxes)[-1] = make_uint4(BOX_MAGIC, (unsigned)maxpix, (unsigned)V, (unsigned)TH);
+    if (queue != nullptr && b == 0 && t < WQ_WORDS) queue[t] = 0u;  // k_warp_fuse_p's work queues start at zero
     if (t >= (int64_t)nt * V) return;
     const int tile = (int)(t / V), v = (int)(t - (int64_t)tile * V);
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
@@ -1649,6 +1924,10 @@ int g_warp_pool_kb = 0;  // BEV_TUNE_WARP_POOL_KB: LDS image pool / ring per wor
 int g_warp_kernel = 0;   // BEV_TUNE_WARP_KERNEL: 0 default (= 2), 1 register-staged k_warp_fuse, 2 per-view LDS-DMA
                          // k_warp_fuse_v2, 3 DPP-row k_warp_fuse_v3 (sum / mean with a workspace)
 int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats, 0 = WARP_BWD_POOL_MAX
+// BEV_TUNE_WARP_PERSIST: 0 (default) = k_warp_fuse_v2; 1 = k_warp_fuse_p with 8 work queues, 2 = with one queue.
+// r06x A/B (tools/warp_persist_ab.py, us per launch, bench / K5): per-tile 136.2 / 220.0, persistent 8 queues
+// 150.2 / 247.6, 1 queue 145.6 / 245.7 -- slower: see k_warp_fuse_p (the store drain the next DMA waits behind).
+int g_warp_persist = 0;
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
 
@@ -1718,17 +1997,31 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
     dim3 grid(ntiles, B * V2_SPLIT), block(FT_NT);
     const size_t lds = (size_t)pool + V2_FIXED;
     if (!WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (LDS homographies)
+    unsigned *queue = boxes ? reinterpret_cast<unsigned *>(boxes + (int64_t)B * ntiles * V) : nullptr;
     if (boxes && !boxes_ready) {  // else bev_ipm_warp_fuse_boxes_f32 wrote them (same geometry, pool and knobs)
         const int maxpix = pool / (V2_SL * 16) - 4;  // the kernel's own pool test
         hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
-                           st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes);
+                           st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes, queue);
+    }
+    const bool nhwc = rpr == 0;          // channels-last output (bev_ipm_warp_fuse_nhwc_f32)
+    const bool ck = !nhwc && rpr < Hb;  // rank-chunk-major output (camera-shard partials)
+    if (g_warp_persist && boxes && !nhwc && C == 64 && mode != BEV_FUSE_MAX && TH == 16 && WARP_CK == 64 &&
+        !WARP_STAGE_ALL && !WARP_TAPS_AHEAD) {
+        // persistent: OCC resident workgroups per CU, a multiple of 8 (one work queue per XCD)
+        const int nq = (cu_count() * OCC + 7) / 8;
+        const dim3 pgrid((unsigned)(8 * nq)), pblock(FT_NT);
+        auto gop = [&](auto kern) {
+            hipLaunchKernelGGL(kern, pgrid, pblock, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy,
+                               Hb, Wb, out, pool, boxes, rpr, queue, g_warp_persist == 2 ? 1 : 8);
+        };
+        if (mode == BEV_FUSE_SUM) ck ? gop(k_warp_fuse_p<BEV_FUSE_SUM, OCC, true>) : gop(k_warp_fuse_p<BEV_FUSE_SUM, OCC, false>);
+        else ck ? gop(k_warp_fuse_p<BEV_FUSE_MEAN, OCC, true>) : gop(k_warp_fuse_p<BEV_FUSE_MEAN, OCC, false>);
+        return last();
     }
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
                            out, pool, boxes, rpr);
     };
-    const bool nhwc = rpr == 0;          // channels-last output (bev_ipm_warp_fuse_nhwc_f32)
-    const bool ck = !nhwc && rpr < Hb;  // rank-chunk-major output (camera-shard partials)
     if (nhwc) {
         if (mode == BEV_FUSE_SUM) go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, false, true>);
         else if (mode == BEV_FUSE_MEAN) go(k_warp_fuse_v2<BEV_FUSE_MEAN, OCC, TH, false, true>);
@@ -1753,7 +2046,7 @@ int launch_fuse_v3(const float *feats, int64_t sN, int64_t sH, int64_t sW, const
     // 3 workgroups per CU: pool + zero pixel <= 160 KiB / 3
     const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : ((163840 / 3 - 256 - 64) & ~1023);
     hipLaunchKernelGGL((k_warp_boxes<16, 16>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
-                       st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, pool / W3_PIX, nty, boxes);
+                       st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, pool / W3_PIX, nty, boxes, nullptr);
     const int fastdiv = (V >= 1 && V <= 64 && ((W3_FASTDIV_V >> (V - 1)) & 1)) ? 1 : 0;
     const size_t lds = (size_t)pool + 256;
     if (mode == BEV_FUSE_SUM)
@@ -1808,6 +2101,10 @@ int warp_tune(int knob, int value) {
         case BEV_TUNE_WARP_BWD_POOL:
             slot = &g_warp_bwd_pool;
             ok = value >= 0 && value <= WARP_BWD_POOL_MAX;
+            break;
+        case BEV_TUNE_WARP_PERSIST:
+            slot = &g_warp_persist;
+            ok = value >= 0 && value <= 2;
             break;
         default:
             return BEV_ERR_ARGS;
@@ -1880,7 +2177,7 @@ int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb) {
     // many)
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int64_t nt = (((int64_t)Wb + TW - 1) / TW) * (((int64_t)Hb + TH - 1) / TH);
-    return BOX_HDR + (int64_t)B * nt * V * (int64_t)sizeof(uint2);
+    return BOX_HDR + (int64_t)B * nt * V * (int64_t)sizeof(uint2) + WQ_WORDS * (int64_t)sizeof(unsigned);
 }
 
 int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
@@ -1937,7 +2234,9 @@ int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float 
     const int maxpix = v2_pool_bytes(mode) / (V2_SL * 16) - 4;  // k_warp_fuse_v2's own pool test
     hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                        (hipStream_t)stream, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH,
-                       reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR));
+                       reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR),
+                       reinterpret_cast<unsigned *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR +
+                                                    (int64_t)B * ntiles * V * (int64_t)sizeof(uint2)));
     return last();
 }
 

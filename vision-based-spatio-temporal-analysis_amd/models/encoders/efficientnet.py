@@ -145,6 +145,7 @@ class EfficientNet(nn.Module):
         self.x6_expand = False
         self.stem3 = True  # the stem on its vector-ALU kernel (bev_conv2d_stem3_f32) instead of the implicit GEMM
         self.pw_stream = True  # eval: the wide tiny-K expansions on k_pw_mfma too (see forward_features_nhwc)
+        self.ir_fuse = True  # eval: expansion + depthwise conv of an inverted residual as one kernel (_ir_fused)
         self._stem3_key = None
 
     def _fc(self, conv, bn):
@@ -171,6 +172,34 @@ class EfficientNet(nn.Module):
             self._stem3_b = b.contiguous().float()
             self._stem3_key = key
         return _nat.conv2d_stem3(x, self._stem3_w, self._stem3_b, _nat.ACT_SILU)
+
+    def _ir_fusable(self, blk, x) -> bool:
+        return self.ir_fused_block(blk, x.shape[-1])
+
+    def ir_fused_block(self, blk, cin: int) -> bool:
+        """The inverted residual's expansion + depthwise conv take the fused kernel (bev_ir_expand_dw_f32) for a
+        `cin`-channel input (eval path)?"""
+        if not isinstance(blk, InvertedResidual):
+            return False
+        pw, dw = blk.conv_pw, blk.conv_dw
+        return (self.ir_fuse and not self.x6_expand and cin in (16, 24, 32, 40, 48)
+                and pw.out_channels % 48 == 0 and pw.kernel_size == (1, 1) and pw.stride == (1, 1)
+                and dw.kernel_size[0] == dw.kernel_size[1] and dw.kernel_size[0] in (3, 5) and dw.stride[0] in (1, 2)
+                and dw.stride[0] == dw.stride[1] and dw.padding == (dw.kernel_size[0] // 2,) * 2
+                and dw.groups == dw.in_channels == pw.out_channels and dw.dilation == (1, 1))
+
+    def _ir_fused(self, blk, x):
+        fc, fdw = self._fc(blk.conv_pw, blk.bn1), self._fdw(blk.conv_dw, blk.bn2)
+        fdw.prepare(x.device)
+        key = ("irw", id(blk.conv_pw))
+        tkey = tuple((t.data_ptr(), t._version) for t in fc._tensors()) + (str(x.device),)
+        ent = self._folded.get(key)
+        if ent is None or ent[0] != tkey:
+            w, b = fc.folded(x.device)
+            ent = (tkey, w.reshape(w.shape[0], -1).contiguous(), b.contiguous().float())
+            self._folded[key] = ent
+        dw = blk.conv_dw
+        return _nat.ir_expand_dw(x, ent[1], ent[2], fdw.wt, fdw.bias, dw.kernel_size[0], dw.stride[0])
 
     def _fc_expand(self, conv, bn):
         """The inverted-residual expansion (1x1, Ci -> 6 Ci, SiLU): on the split-bf16 kernels (bev_conv2d_x6_f32, fp32
@@ -206,8 +235,10 @@ class EfficientNet(nn.Module):
         if isinstance(blk, DepthwiseSeparableConv):
             y, ps = self._fdw(blk.conv_dw, blk.bn1)(x, want_psum=True)
             return self._project(blk.conv_pw, blk.bn2, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
-        h = self._fc_expand(blk.conv_pw, blk.bn1)(x, relu=_nat.ACT_SILU)
-        y, ps = self._fdw(blk.conv_dw, blk.bn2)(h, want_psum=True)
+        y, ps = self._ir_fused(blk, x) if self._ir_fusable(blk, x) else (None, None)
+        if y is None:
+            h = self._fc_expand(blk.conv_pw, blk.bn1)(x, relu=_nat.ACT_SILU)
+            y, ps = self._fdw(blk.conv_dw, blk.bn2)(h, want_psum=True)
         return self._project(blk.conv_pwl, blk.bn3, y, self._gate(blk.se, y, ps), x if blk.has_skip else None)
 
     def unexecuted_parameter_names(self, out_index: int):
