@@ -921,12 +921,13 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], BC[j][1], acc[i][j], 0, 0, 0); \
             }                                                                                              \
     } while (0)
-    // MFMAs of K step KS from LDS buffer BUF: slice 2 KS (B in bs0, slice 2 KS + 1 loaded meanwhile into bs1),
-    // slice 2 KS + 1 (B in bs1, the next step's slice 0 loaded into bs0)
+    // MFMAs of K step KS from LDS buffer BUF: slice 2 KS (B in bs0), slice 2 KS + 1 (B in bs1, loaded by the caller
+    // BEFORE the step's A prefetch), the next step's slice 0 loaded into bs0 in between.  Order matters: vmcnt
+    // retires loads in issue order, so a B fragment loaded after an A prefetch would make its first use wait for
+    // that prefetch too (half a K step of cover instead of a whole one).
 #define X6B_MFMA(BUF, KS)                                                                                  \
     do {                                                                                                   \
         const __bf16 *As = lds + (BUF) * STAGE;                                                            \
-        X6B_BLOAD(bs1, 2 * (KS) + 1);                                                                      \
         X6B_SLICE(As, 0, bs0);                                                                             \
         X6B_BLOAD(bs0, 2 * (KS) + 2);                                                                      \
         X6B_SLICE(As, 1, bs1);                                                                             \
@@ -940,30 +941,38 @@ __global__ __launch_bounds__(256, 2) void k_conv_x6b(ConvX a) {
     __syncthreads();
     int ks = 0;
     for (; ks + 3 < nk; ks += 2) {
+        X6B_BLOAD(bs1, 2 * ks + 1);
         X6B_GLOAD(va0);  // step ks + 2
         X6B_MFMA(0, ks);
         X6B_SWRITE(1, va1);  // step ks + 1
         __syncthreads();
+        X6B_BLOAD(bs1, 2 * ks + 3);
         X6B_GLOAD(va1);  // step ks + 3
         X6B_MFMA(1, ks + 1);
         X6B_SWRITE(0, va0);  // step ks + 2
         __syncthreads();
     }
     if (ks + 2 < nk) {
+        X6B_BLOAD(bs1, 2 * ks + 1);
         X6B_GLOAD(va0);
         X6B_MFMA(0, ks);
         X6B_SWRITE(1, va1);
         __syncthreads();
+        X6B_BLOAD(bs1, 2 * ks + 3);
         X6B_MFMA(1, ks + 1);
         X6B_SWRITE(0, va0);
         __syncthreads();
+        X6B_BLOAD(bs1, 2 * ks + 5);
         X6B_MFMA(0, ks + 2);
     } else if (ks + 1 < nk) {
+        X6B_BLOAD(bs1, 2 * ks + 1);
         X6B_MFMA(0, ks);
         X6B_SWRITE(1, va1);
         __syncthreads();
+        X6B_BLOAD(bs1, 2 * ks + 3);
         X6B_MFMA(1, ks + 1);
     } else {
+        X6B_BLOAD(bs1, 2 * ks + 1);
         X6B_MFMA(0, ks);
     }
 #undef X6B_MFMA
