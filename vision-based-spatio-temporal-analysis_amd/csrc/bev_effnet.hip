@@ -639,16 +639,35 @@ __global__ __launch_bounds__(64 * IR_W) void k_irdw(const float *__restrict__ x,
     irf4 ssum = {0.f, 0.f, 0.f, 0.f};
     const float *xn = x + (int64_t)n * H * W * CI;
     float *hr = &ring[wave][0][0];
+    // input rows are loaded one row ahead into registers (the next row's loads fly during this row's expansion and
+    // the output rows it completes), then written to xs at the next expand_row
+    constexpr int NPF = (IR_IC * CQ + 64 * IR_W - 1) / (64 * IR_W);
+    irf4 pre[NPF];
+    auto load_row = [&](int iy) {
+        const bool rin = (unsigned)iy < (unsigned)H;
+#pragma unroll
+        for (int k = 0; k < NPF; ++k) {
+            const int e = tid + 64 * IR_W * k;
+            const int px = e / CQ, cq = e - px * CQ, ix = ix0 + px;
+            irf4 v = {0.f, 0.f, 0.f, 0.f};
+            if (e < IR_IC * CQ && rin && (unsigned)ix < (unsigned)W)
+                v = *(const irf4 *)(xn + ((int64_t)iy * W + ix) * CI + 4 * cq);
+            pre[k] = v;
+        }
+    };
     auto expand_row = [&](int iy) {  // stage + expand input row iy into ring slot iy mod K (iy may be outside)
         __syncthreads();  // the previous row's staged pixels are no longer read
         const bool rin = (unsigned)iy < (unsigned)H;
-        for (int e = tid; e < IR_IC * CQ; e += 64 * IR_W) {
-            const int px = e / CQ, cq = e - px * CQ, ix = ix0 + px;
-            irf4 v = {0.f, 0.f, 0.f, 0.f};
-            if (rin && (unsigned)ix < (unsigned)W) v = *(const irf4 *)(xn + ((int64_t)iy * W + ix) * CI + 4 * cq);
 #pragma unroll
-            for (int u = 0; u < 4; ++u) xs[px * XS + 4 * cq + u] = v[u];
+        for (int k = 0; k < NPF; ++k) {
+            const int e = tid + 64 * IR_W * k;
+            const int px = e / CQ, cq = e - px * CQ;
+            if (e < IR_IC * CQ) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) xs[px * XS + 4 * cq + u] = pre[k][u];
+            }
         }
+        load_row(iy + 1);
         __syncthreads();
         const int slot = ((iy % K) + K) % K;
 #pragma unroll
@@ -667,6 +686,7 @@ __global__ __launch_bounds__(64 * IR_W) void k_irdw(const float *__restrict__ x,
         }
     };
     int iy_next = r0 * S - PAD;
+    load_row(iy_next);
     for (int ro = 0; ro < rows_out; ++ro) {
         const int r = r0 + ro, iy_top = r * S - PAD;
         while (iy_next < iy_top + K) expand_row(iy_next++);
