@@ -84,7 +84,11 @@ const char *bev_build_source_hash(void);
  *   0 = straight from registers (16 B per lane at a pixel stride).  Same results.
  * BEV_TUNE_WARP_PERSIST: fused warp sum / mean with C == 64, NCHW or rank-chunk-major output and a footprint-box
  *   workspace: 0 (default) = one workgroup per (tile, frame); 1 / 2 = the persistent work-queue kernel with 8 queues
- *   (one per XCD) / one queue (A/B options, measured slower).  Same results. */
+ *   (one per XCD) / one queue (A/B options, measured slower).  Same results.
+ * BEV_TUNE_WARP_SPAN: fused warp with a footprint-box workspace: span staging (each box row's tap span only) for
+ *   footprints of <= 32 rows -- always where the box does not fit the LDS pool but the spans do, and where it fits
+ *   when the spans need at most `value` percent of its pixels (1..100; default 50); 0 = box staging only (A/B).
+ *   Same results. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -101,6 +105,7 @@ const char *bev_build_source_hash(void);
 #define BEV_TUNE_CONV_X6_NT 16
 #define BEV_TUNE_STEM3_STAGE 17
 #define BEV_TUNE_WARP_PERSIST 18
+#define BEV_TUNE_WARP_SPAN 19
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

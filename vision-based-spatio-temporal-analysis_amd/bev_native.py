@@ -20,7 +20,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libbev_mi355x.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 BEV_ERR_ARGS = -1  # include/bev_mi355x.h: an argument the kernel cannot take
 
 FUSE_MODES = {"sum": 0, "mean": 1, "max": 2}
@@ -263,6 +263,7 @@ TUNE_DW_RUN = 14
 TUNE_CONV_X6_NT = 16
 TUNE_STEM3_STAGE = 17
 TUNE_WARP_PERSIST = 18
+TUNE_WARP_SPAN = 19
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 

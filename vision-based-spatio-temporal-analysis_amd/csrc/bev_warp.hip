@@ -466,6 +466,48 @@ __device__ __forceinline__ void dma_rows(const float *__restrict__ f, int sH, in
     }
 }
 
+// Span staging (see row_span): a footprint staged row by row, row r = the `len` pixels from column `sx` of box row r,
+// rows back to back from LDS byte offset `off` (pixel exc_r + k of the image = column sx_r + k of row r; exc = the
+// exclusive prefix sum of len over the rows).  Lane r of len / sx / exc holds row r's values (r < nrows <= 32).  The
+// same instruction form as dma_rows (3 pixels of one row per LDS-DMA instruction, scalar source base and M0); the
+// instructions of all rows are dealt round-robin over the waves.
+__device__ __forceinline__ void dma_spans(const float *__restrict__ f, int sH, int sW, int sy0, int nrows, int len,
+                                          int sxr, int exc, unsigned char *smem, int off, int wave, int lane,
+                                          int nwaves = FT_NT / 64) {
+    if (WARP_ABLATE & 2) return;
+    const int lp = (lane * 241) >> 12;  // lane / 17 for lane < 64
+    const int ls = lane - 17 * lp;
+    const bool slot_ok = lp < 3 && ls < 16;
+    const unsigned voff = (unsigned)((lp * sW + ls * 4) * (int)sizeof(float));
+    const unsigned lds0 = (unsigned)__builtin_amdgcn_readfirstlane((int)(lds_base(smem) + (unsigned)off));
+    int r = 0, i = __builtin_amdgcn_readfirstlane(wave);
+    int rl = __builtin_amdgcn_readlane(len, 0), per = (rl + 2) / 3;
+    while (r < nrows) {
+        if (i < per) {
+            const int rsx = __builtin_amdgcn_readlane(sxr, r), rex = __builtin_amdgcn_readlane(exc, r);
+            const float *src = f + (sy0 + r) * sH + (rsx + 3 * i) * sW;
+            const unsigned dst = lds0 + (unsigned)((rex + 3 * i) * 272);
+            if (slot_ok && lp < rl - 3 * i) {
+                unsigned keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                    "global_load_lds_dwordx4 %1, %3" WARP_DMA_POLICY "\n\ts_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "v"(voff), "s"(dst), "s"(src)
+                    : "memory");
+            }
+            i += nwaves;
+        } else {
+            i -= per;
+            ++r;
+            if (r < nrows) {
+                rl = __builtin_amdgcn_readlane(len, r);
+                per = (rl + 2) / 3;
+            }
+        }
+    }
+}
+
 // bytes of the output from element `base` on, as a buffer bound (clamped to 32 bits: a chunk of 64 planes is < 4 GiB)
 __device__ __forceinline__ uint32_t out_range(size_t total_bytes, size_t base) {
     const size_t r = total_bytes - base * sizeof(float);
@@ -731,11 +773,27 @@ constexpr double EPS32 = 5.9604644775390625e-08;  // 2^-24
 constexpr unsigned BOX_MAGIC = 0x42455642u;  // "BVEB"
 constexpr int BOX_HDR = 16;                   // header bytes before the boxes
 constexpr int V2_MAXV = 64;                         // one view per lane
+constexpr int WQ_WORDS = 16;  // queue words after the boxes: [0..7] tickets per queue, [8] finished workgroups
+// Span tables after the queue words ([frame][tile][view][SPAN_ROWS] words, written for the views flagged span-staged:
+// box word a, bit 30).  Header word w = TH | SPAN_FLAG when k_warp_boxes made them.
+constexpr int SPAN_ROWS = 32;          // span staging applies to boxes of at most this many rows
+constexpr int SPAN_HDR = 144;          // LDS bytes before a span-staged image: the row bases of rows -1 .. 32 (34 ints)
+constexpr unsigned SPAN_FLAG = 0x100u;
+#ifndef WARP_SPAN_PCT
+#define WARP_SPAN_PCT 50  // fused warp v2: a footprint that fits the pool as a box is span-staged when its spans need at
+                          // most this percentage of the box's pixels (0: span staging off; oversized boxes always)
+#endif
+
+// The projected corners of the BEV rectangle (image coordinates, order: c & 1 -> xb, c & 2 -> yb) and the fp32
+// margins of the tap recipe, for the per-row spans (row_spans).
+struct Quad {
+    double x[4], y[4], mx, my;
+};
 
 // Conservative tap bbox of the BEV rectangle [xa, xb] x [ya, yb] (cell
 // centres) for homography h; ok = false when the corner bound does not apply.
 __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float yb, float sx, float sy, int Wf, int Hf,
-                          bool &ok) {
+                          bool &ok, Quad *quad = nullptr) {
     double h[9];
 #pragma unroll
     for (int q = 0; q < 9; ++q) h[q] = (double)hf[q];
@@ -763,6 +821,10 @@ __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float y
         vmax = fmax(vmax, fabs(Vv));
         aix = fmax(aix, fabs(ix));
         aiy = fmax(aiy, fabs(iy));
+        if (quad) {
+            quad->x[c] = ix;
+            quad->y[c] = iy;
+        }
         ixmin = fmin(ixmin, ix);
         ixmax = fmax(ixmax, ix);
         iymin = fmin(iymin, iy);
@@ -776,6 +838,10 @@ __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float y
                              16.0 * EPS32 * (aix + (double)Wf + 1.0)) + 1e-3;
     const double my = 4.0 * ((double)sy * 3.0 * EPS32 * (svmax + vmax * swmax) / wmin +
                              16.0 * EPS32 * (aiy + (double)Hf + 1.0)) + 1e-3;
+    if (quad) {
+        quad->mx = mx;
+        quad->my = my;
+    }
     const double lox = fmin(fmax(ixmin - mx, -4.0), (double)Wf + 4.0);
     const double hix = fmin(fmax(ixmax + mx, -4.0), (double)Wf + 4.0);
     const double loy = fmin(fmax(iymin - my, -4.0), (double)Hf + 4.0);
@@ -784,6 +850,45 @@ __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float y
     const int y0 = max((int)floor(loy), 0), y1 = min((int)floor(hiy) + 1, Hf - 1);
     if (x0 <= x1 && y0 <= y1) b = Box{x0, y0, x1, y1};
     return b;
+}
+
+// Span of image row y of box bx (span table word: x0 | len << 16; 0: no tap of the tile on that row).
+// A cell puts taps on row y iff its fp32 iy is in [y - 1, y + 1), so its exact iy (a point of the quad) is in the
+// band [y - 1 - my, y + 1 + my]; the exact ix of such cells lies in the x extent [lo, hi] of the quad's part inside
+// that band (a convex polygon: its vertices inside the band and its edges' crossings of the band's lines), so their
+// fp32 ix is in [lo - mx, hi + mx] and their tap columns in [floor(lo - mx), floor(hi + mx) + 1] -- clipped to the
+// (conservative) box.  Every valid tap of the tile on row y lies in the span.
+__device__ __forceinline__ unsigned row_span(const Quad &q, const Box &bx, int y) {
+    const double lo = (double)y - 1.0 - q.my - 1e-6, hi = (double)y + 1.0 + q.my + 1e-6;
+    double xl = __builtin_inf(), xh = -__builtin_inf();
+    constexpr int ord[4] = {0, 1, 3, 2};  // the corners in polygon order
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const double px = q.x[ord[e]], py = q.y[ord[e]], qx = q.x[ord[(e + 1) & 3]], qy = q.y[ord[(e + 1) & 3]];
+        if (py >= lo && py <= hi) {
+            xl = fmin(xl, px);
+            xh = fmax(xh, px);
+        }
+        if (py != qy) {
+            const double s = (qx - px) / (qy - py);
+            if ((lo - py) * (lo - qy) <= 0.0) {
+                const double x = px + (lo - py) * s;
+                xl = fmin(xl, x);
+                xh = fmax(xh, x);
+            }
+            if ((hi - py) * (hi - qy) <= 0.0) {
+                const double x = px + (hi - py) * s;
+                xl = fmin(xl, x);
+                xh = fmax(xh, x);
+            }
+        }
+    }
+    if (!(xl <= xh)) return 0u;
+    const double m = q.mx + 1e-6;
+    const double l = fmin(fmax(xl - m, (double)bx.x0 - 1.0), (double)bx.x1 + 2.0);
+    const double h = fmax(fmin(xh + m, (double)bx.x1 + 1.0), (double)bx.x0 - 2.0);
+    const int x0 = max((int)floor(l), bx.x0), x1 = min((int)floor(h) + 1, bx.x1);
+    return x0 <= x1 ? (unsigned)x0 | ((unsigned)(x1 - x0 + 1) << 16) : 0u;
 }
 
 // bilerp (bev_geometry.h) of 4 channels as two independent packed chains,
@@ -827,15 +932,15 @@ struct NoMid {
     __device__ __forceinline__ void operator()() const {}
 };
 // `mid` runs between LDS groups MID_G and MID_G + 1 (the next view's taps while this view's reads are in flight)
+// (the taps' LDS pixels: (x0, y0) at byte pb, (x0, y0 + 1) at byte pbs, each row's x0 + 1 one pixel further)
 template <int MODE, int N, bool PIPE = true, int MID_G = -1, class Mid = NoMid>
-__device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t, const unsigned char *smem, int ib,
-                                                 int sx0, int sy0, int sbw, int zp, int zp0, Mid mid = Mid()) {
+__device__ __forceinline__ void sample_pipe_at(float (&acc)[N], const Taps &t, const unsigned char *smem, int pb,
+                                               int pbs, int zp, int zp0, Mid mid = Mid()) {
     constexpr int PS = (N / 4 + 1) * 16, NG = N / 4;
-    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * PS;
     const unsigned char *a0 = smem + ((t.valid & 1) ? pb : zp0);
     const unsigned char *a1 = smem + ((t.valid & 2) ? pb + PS : zp);
-    const unsigned char *a2 = smem + ((t.valid & 4) ? pb + sbw * PS : zp);
-    const unsigned char *a3 = smem + ((t.valid & 8) ? pb + (sbw + 1) * PS : zp);
+    const unsigned char *a2 = smem + ((t.valid & 4) ? pbs : zp);
+    const unsigned char *a3 = smem + ((t.valid & 8) ? pbs + PS : zp);
     if (!PIPE) {
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
@@ -875,6 +980,15 @@ __device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t,
             c3 = n3;
         }
     }
+}
+
+// ... from a box image at LDS byte `ib` (origin sx0, sy0, width sbw)
+template <int MODE, int N, bool PIPE = true, int MID_G = -1, class Mid = NoMid>
+__device__ __forceinline__ void sample_view_pipe(float (&acc)[N], const Taps &t, const unsigned char *smem, int ib,
+                                                 int sx0, int sy0, int sbw, int zp, int zp0, Mid mid = Mid()) {
+    constexpr int PS = (N / 4 + 1) * 16;
+    const int pb = ib + ((t.y0 - sy0) * sbw + (t.x0 - sx0)) * PS;
+    sample_pipe_at<MODE, N, PIPE, MID_G, Mid>(acc, t, smem, pb, pb + sbw * PS, zp, zp0, mid);
 }
 
 // Tile shapes of k_warp_fuse_v2 (TH rows x TW cells, 256 lanes, one cell per lane):
@@ -1003,11 +1117,15 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     if (tid < 16) *(float4 *)(smem + zp + tid * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
     unsigned *btab = reinterpret_cast<unsigned *>(htab + V2_MAXV * 9);  // [V][2] corner boxes
     bool box_hdr_ok = false;  // boxes made for this kernel's fit test and tiling? (else: computed here)
+    bool span_ok = false;     // ... and span tables for the views flagged span-staged
     if (boxes_in != nullptr) {
         const uint4 hd = reinterpret_cast<const uint4 *>(boxes_in)[-1];
-        box_hdr_ok = hd.x == BOX_MAGIC && (int)hd.y == maxpix && (int)hd.z == V && (int)hd.w == TH;
+        box_hdr_ok = hd.x == BOX_MAGIC && (int)hd.y == maxpix && (int)hd.z == V && (int)(hd.w & ~SPAN_FLAG) == TH;
+        span_ok = box_hdr_ok && (hd.w & SPAN_FLAG) && CK == 64 && WARP_HSCALAR && !WARP_STAGE_ALL;
     }
     const uint2 *__restrict__ boxes = box_hdr_ok ? boxes_in : nullptr;
+    const unsigned *__restrict__ spans =
+        span_ok ? reinterpret_cast<const unsigned *>(boxes_in + (int64_t)B * nt * V) + WQ_WORDS : nullptr;
 
     // corner boxes of this tile for frame bb, lane v <-> view v, packed in two VGPRs (wave 0 computes them in
     // double, the others read them): lba = x0 | y0 << 16 | (!ok) << 31,  lbb = (x1 + 1) | (y1 + 1) << 16
@@ -1050,9 +1168,45 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     auto box_of = [&](int v) {
         const unsigned a = (unsigned)__builtin_amdgcn_readlane((int)lba, v);
         const unsigned c = (unsigned)__builtin_amdgcn_readlane((int)lbb, v);
-        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x7fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
+        return Box{(int)(a & 0xffffu), (int)((a >> 16) & 0x3fffu), (int)(c & 0xffffu) - 1, (int)(c >> 16) - 1};
     };
     auto ok_of = [&](int v) { return ((unsigned)__builtin_amdgcn_readlane((int)lba, v) >> 31) == 0u; };
+    auto span_of = [&](int v) {
+        return spans != nullptr && ((unsigned)__builtin_amdgcn_readlane((int)lba, v) & 0x40000000u) != 0u;
+    };
+    // span table of view v (lane r < SPAN_ROWS: row r's word) -- a plain load, consumed (and so waited for by the
+    // compiler) only after an explicit vmcnt(0), so its wait never covers LDS-DMA still in flight
+    auto load_span = [&](int v) -> unsigned {
+        return lane < SPAN_ROWS ? spans[(((int64_t)b * nt + tile) * V + v) * SPAN_ROWS + lane] : 0u;
+    };
+    // span staging of a view (box rows y0 .. y0 + nrows - 1, table spw) at LDS byte o: the row bases first (wave 0:
+    // int [34] for rows -1 .. 32, absolute LDS pixel-0 offsets, read by the sampling after the end-of-view barrier),
+    // then the rows' pixels from o + SPAN_HDR.  span_bytes: the LDS bytes it takes.
+    auto span_scan = [&](unsigned spw, int nrows, int &len, int &sxr, int &exc) {
+        len = lane < nrows ? (int)(spw >> 16) : 0;
+        sxr = (int)(spw & 0xffffu);
+        int inc = len;
+#pragma unroll
+        for (int d = 1; d < SPAN_ROWS; d <<= 1) {
+            const int u = __shfl_up(inc, d);
+            if (lane >= d) inc += u;
+        }
+        exc = inc - len;
+        return SPAN_HDR + __builtin_amdgcn_readlane(inc, SPAN_ROWS - 1) * PS;
+    };
+    auto stage_span = [&](const float *fp, int y0, int nrows, int len, int sxr, int exc, int o) {
+        const int rb = __shfl(exc - sxr, lane > 0 ? lane - 1 : 0);  // lane l: row l - 1's pixel of column 0
+        if (wave == 0 && lane < SPAN_ROWS + 2)
+            reinterpret_cast<int *>(smem + o)[lane] = o + SPAN_HDR + ((lane >= 1 && lane <= nrows) ? rb * PS : 0);
+        dma_spans(fp, (int)sH, (int)sW, y0, nrows, len, sxr, exc, smem, o + SPAN_HDR, wave, lane, NW);
+    };
+    // the taps' LDS pixels (sample_pipe_at) in a span image at o (box origin row y0) or a box image (origin, width)
+    auto span_addr = [&](const Taps &t, int o, int y0, int &pb, int &pbs) {
+        const int *hdr = reinterpret_cast<const int *>(smem + o);
+        const int r0 = min(max(t.y0 - y0 + 1, 0), SPAN_ROWS + 1), r1 = min(r0 + 1, SPAN_ROWS + 1);
+        pb = hdr[r0] + t.x0 * PS;
+        pbs = hdr[r1] + t.x0 * PS;
+    };
 
     float ccx = cx, ccy = cy;  // made opaque per chunk (see the chunk loop)
     const int hbase = b * V;   // homography row of view 0 of this frame
@@ -1109,7 +1263,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             // per tile (instead of one per view) -- same taps, same view order, same arithmetic
             int need = 0;  // lane v < V: view v's image bytes (0: empty view; huge: the corner box does not apply)
             if (lane < V) {
-                const int x0 = (int)(lba & 0xffffu), y0 = (int)((lba >> 16) & 0x7fffu);
+                const int x0 = (int)(lba & 0xffffu), y0 = (int)((lba >> 16) & 0x3fffu);
                 const int x1 = (int)(lbb & 0xffffu) - 1, y1 = (int)(lbb >> 16) - 1;
                 const int np = (x1 - x0 + 1) * (y1 - y0 + 1);
                 need = (lba >> 31) ? (1 << 26) : (x1 < 0 ? 0 : stage_bytes(np));
@@ -1151,15 +1305,35 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             }
         }
         const int v_first = next_live(-1);
-        // prologue: DMA of the first live view (if its corner box applies and fits)
+        auto peek_live = [&](int u) {  // next_live without the skipped views' max(acc, 0)
+            ++u;
+            while (u < V && !live(u)) ++u;
+            return u;
+        };
+        // prologue: DMA of the first live view (if its corner box applies and fits, or its spans do).  Span tables:
+        // spc = the current view's, spn = the next live view's (loaded during the view before, consumed after the
+        // end-of-view wait), both 0 for views without one.
         Box bn = box_of(v_first < V ? v_first : 0);
-        int offn = -1;
+        int offn = -1, bytesn = 0;  // the next image's LDS byte offset (-1: not staged ahead) and size
+        bool spsn = false;          // ... staged by spans
+        unsigned spc = 0u, spn = 0u;
         if (v_first < V) {
             const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-            if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
+            if (span_of(v_first)) {
+                spc = load_span(v_first);
+                asm volatile("" : "+v"(spc));  // its wait: nothing else in flight
+                int len, sxr, exc;
+                bytesn = span_scan(spc, bn.y1 - bn.y0 + 1, len, sxr, exc);
+                stage_span(fb + (int64_t)v_first * sN, bn.y0, bn.y1 - bn.y0 + 1, len, sxr, exc, 0);
                 offn = 0;
+                spsn = true;
+            } else if (ok_of(v_first) && bn.x1 >= 0 && npix <= maxpix) {
+                offn = 0;
+                bytesn = ((npix * SL + 63) >> 6) * 1024;
                 dma(fb + (int64_t)v_first * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, 0);
             }
+            const int vs = peek_live(v_first);
+            if (vs < V && span_of(vs)) spn = load_span(vs);
         }
         // the first live view's taps while its footprint lands (exact-bbox views reduce their taps first)
         Taps tf;
@@ -1170,13 +1344,15 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // zero pixel + image of the first live view
+        asm volatile("" : "+v"(spn));
         STAMP(2);
 
         int nview = 0;  // live views done (timing stamps)
         for (int v = v_first, vn; v < V; v = vn) {
             vn = next_live(v);
             Box bx = bn;
-            const int off = offn;
+            const int off = offn, bytesc = bytesn;
+            const bool spsc = spsn;
             const float *f = fb + (int64_t)v * sN;
             Taps t;
             bool have_t = false;
@@ -1196,6 +1372,26 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             const bool empty = bx.x1 < 0;
             const int bw = bx.x1 - bx.x0 + 1, bh = bx.y1 - bx.y0 + 1;
             bool done = empty;
+            if (!done && off < 0 && span_of(v)) {
+                // ---- synchronous span staging (no room was left beside the previous image) ----
+                int len, sxr, exc;
+                span_scan(spc, bh, len, sxr, exc);
+                stage_span(f, bx.y0, bh, len, sxr, exc, 0);
+                if (!have_t) {
+                    t = taps_of(v);
+                    have_t = true;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (__ballot(t.valid != 0) != 0ull && (!WARP_LANESKIP || t.valid)) {
+                    int pb, pbs;
+                    span_addr(t, 0, bx.y0, pb, pbs);
+                    sample_pipe_at<MODE, CK, WARP_PIPE != 0>(acc, t, smem, pb, pbs, zp, zp);
+                } else
+                    zero_view<MODE>(acc, v);
+                done = true;
+                __syncthreads();  // the pool is free again
+            }
             if (!done && off < 0) {
                 // ---- synchronous staging, overlapping blocks if larger than the pool ----
                 int wb = bw, hb = bh, nbx = 1, nby = 1;
@@ -1240,26 +1436,44 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                 __syncthreads();  // every wave is done with the staged blocks before DMA(v+1) reuses the pool
             }
             // ---- look ahead: DMA of the next live view beside the live image of view v ----
+            unsigned spnn = 0u;  // the span table of the live view after vn
             if (vn < V) {
                 bn = box_of(vn);
                 offn = -1;
+                spsn = false;
                 const int npix = (bn.x1 - bn.x0 + 1) * (bn.y1 - bn.y0 + 1);
-                if (ok_of(vn) && bn.x1 >= 0 && npix <= maxpix) {
+                const bool sp = span_of(vn);
+                if (ok_of(vn) && bn.x1 >= 0 && (sp || npix <= maxpix)) {
                     // consecutive images anchor at opposite ends of the pool: they coexist
                     // whenever their sizes add up to at most the pool
-                    const int need = ((npix * SL + 63) >> 6) * 1024;
+                    int len = 0, sxr = 0, exc = 0;
+                    const int need = sp ? span_scan(spn, bn.y1 - bn.y0 + 1, len, sxr, exc)
+                                        : ((npix * SL + 63) >> 6) * 1024;
                     if (done || off < 0) offn = 0;
                     else if (off == 0) {
-                        if (((bw * bh * SL + 63) >> 6) * 1024 + need <= pool) offn = pool - need;
+                        if (bytesc + need <= pool) offn = pool - need;
                     } else if (need <= off) offn = 0;
-                    if (offn >= 0)
-                        dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, offn);
+                    if (offn >= 0) {
+                        if (sp) stage_span(fb + (int64_t)vn * sN, bn.y0, bn.y1 - bn.y0 + 1, len, sxr, exc, offn);
+                        else dma(fb + (int64_t)vn * sN, bn.x0, bn.y0, bn.x1 - bn.x0 + 1, bn.y1 - bn.y0 + 1, offn);
+                        bytesn = need;
+                        spsn = sp;
+                    }
                 }
+                const int vnn = peek_live(vn);
+                if (vnn < V && span_of(vnn)) spnn = load_span(vnn);
             }
             // ---- sample view v from its prefetched image ------------------------------
             if (!done) {
                 if (!have_t) t = taps_of(v);
                 STAMP_VIEW(nview, 0);
+                int pb, pbs;  // the taps' LDS pixels
+                if (spsc) {
+                    span_addr(t, off, bx.y0, pb, pbs);
+                } else {
+                    pb = off + ((t.y0 - bx.y0) * bw + (t.x0 - bx.x0)) * PS;
+                    pbs = pb + bw * PS;
+                }
                 if (WARP_ABLATE & 4) acc[0] += t.w[0] * t.w[3] + (float)(t.x0 + t.y0 + (int)t.valid);
                 else if (__ballot(t.valid != 0) != 0ull) {
                     // WARP_LANESKIP: lanes without a valid tap leave the LDS reads to the others (their sample is
@@ -1268,12 +1482,12 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                         // the next view's taps inside this view's sampling, by every lane (a lane without a valid tap
                         // reads the zero pixel: its sample is +0, i.e. acc + 0 == acc, or max(acc, +0) -- what the
                         // lane skip gives)
-                        sample_view_pipe<MODE, CK, WARP_PIPE != 0, WARP_TAPS_AHEAD - 2>(
-                            acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp, [&]() { tf = taps_of(vn); });
+                        sample_pipe_at<MODE, CK, WARP_PIPE != 0, WARP_TAPS_AHEAD - 2>(
+                            acc, t, smem, pb, pbs, zp, zp, [&]() { tf = taps_of(vn); });
                         if (WARP_TAPS_AHEAD == 1) tf = taps_of(vn);  // after the sampling, before the DMA wait
                         have_f = true;
                     } else if (!WARP_LANESKIP || t.valid)
-                        sample_view_pipe<MODE, CK, WARP_PIPE != 0>(acc, t, smem, off, bx.x0, bx.y0, bw, zp, zp);
+                        sample_pipe_at<MODE, CK, WARP_PIPE != 0>(acc, t, smem, pb, pbs, zp, zp);
                     else zero_view<MODE>(acc, v);
                 } else zero_view<MODE>(acc, v);
             } else if (empty) {
@@ -1282,6 +1496,9 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
             STAMP_VIEW(nview, 1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of view v+1 landed
             __syncthreads();  // all of it landed; image of view v and red[] are free
+            spc = spn;
+            spn = spnn;
+            asm volatile("" : "+v"(spn));  // landed with the DMA
             STAMP_VIEW(nview, 2);
             ++nview;
         }
@@ -1322,7 +1539,6 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
 // (a finished-count word), so every launch starts from zero.  Each workgroup exits once its queue is drained --
 // no inter-workgroup waits, so residency is not needed for progress.
 // Same per-cell arithmetic and view order as v2 => bit-identical output.
-constexpr int WQ_WORDS = 16;  // queue words after the boxes: [0..7] tickets per queue, [8] finished workgroups
 
 template <int MODE, int OCC, bool CHUNK>
 __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_p(const float *__restrict__ feats, int64_t sN, int64_t sH,
@@ -1574,29 +1790,46 @@ template <int TH, int TW = FT_NT / TH>
 __global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hmat, const float *__restrict__ xs,
                                                     const float *__restrict__ ys, int V, int Hf, int Wf, float sx,
                                                     float sy, int Hb, int Wb, int maxpix, int nty,
-                                                    uint2 *__restrict__ boxes, unsigned *__restrict__ queue) {
+                                                    uint2 *__restrict__ boxes, unsigned *__restrict__ queue,
+                                                    unsigned *__restrict__ spans, int span_pct) {
     const int ntx = (Wb + TW - 1) / TW, nt = ntx * nty;  // nty >= ceil(Hb / TH) box-tile rows (extra rows: empty)
     const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int b = blockIdx.y;
     if (t == 0 && b == 0)
-        reinterpret_cast<uint4 *>(boxes)[-1] = make_uint4(BOX_MAGIC, (unsigned)maxpix, (unsigned)V, (unsigned)TH);
+        reinterpret_cast<uint4 *>(boxes)[-1] =
+            make_uint4(BOX_MAGIC, (unsigned)maxpix, (unsigned)V, (unsigned)TH | (spans ? SPAN_FLAG : 0u));
     if (queue != nullptr && b == 0 && t < WQ_WORDS) queue[t] = 0u;  // k_warp_fuse_p's work queues start at zero
     if (t >= (int64_t)nt * V) return;
     const int tile = (int)(t / V), v = (int)(t - (int64_t)tile * V);
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
     const int ia = tyb * TH, ib = min(ia + TH - 1, Hb - 1);
     const int ja = txb * TW, jb = min(ja + TW - 1, Wb - 1);
-    bool ok = true;
+    bool ok = true, span = false;
     Box cb{0x7fffffff, 0x7fffffff, -1, -1};
+    Quad q;
     if (ia < Hb) {
         float hv[9];
         load_h(Hmat, b * V + v, hv);
-        cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok);
+        cb = corner_box(hv, xs[ja], xs[jb], ys[ia], ys[ib], sx, sy, Wf, Hf, ok, spans ? &q : nullptr);
     }
-    if (ok && cb.x1 >= 0 && (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1) > maxpix) ok = false;
+    if (ok && cb.x1 >= 0) {
+        const int bpix = (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1), nrows = cb.y1 - cb.y0 + 1;
+        if (spans && nrows <= SPAN_ROWS) {
+            // span staging: when the box does not fit the pool but its rows' spans do, or when they save enough
+            int tot = 1;  // + the row-base header (144 B < one pixel)
+            for (int r = 0; r < nrows; ++r) tot += (int)(row_span(q, cb, cb.y0 + r) >> 16);
+            span = bpix > maxpix ? tot <= maxpix : tot * 100 <= bpix * span_pct;
+            if (span) {
+                unsigned *o = spans + (((int64_t)b * nt + tile) * V + v) * SPAN_ROWS;
+                for (int r = 0; r < nrows; ++r) o[r] = row_span(q, cb, cb.y0 + r);
+            }
+        }
+        if (!span && bpix > maxpix) ok = false;
+    }
     const bool emp = cb.x1 < 0;
     boxes[((int64_t)b * nt + tile) * V + v] =
-        make_uint2((emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u),
+        make_uint2((emp ? 0u : (unsigned)cb.x0 | ((unsigned)cb.y0 << 16)) | (ok ? 0u : 0x80000000u) |
+                       (span ? 0x40000000u : 0u),
                    emp ? 0u : (unsigned)(cb.x1 + 1) | ((unsigned)(cb.y1 + 1) << 16));
 }
 
@@ -1928,6 +2161,7 @@ int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats
 // r06x A/B (tools/warp_persist_ab.py, us per launch, bench / K5): per-tile 136.2 / 220.0, persistent 8 queues
 // 150.2 / 247.6, 1 queue 145.6 / 245.7 -- slower: see k_warp_fuse_p (the store drain the next DMA waits behind).
 int g_warp_persist = 0;
+int g_warp_span_pct = WARP_SPAN_PCT;  // BEV_TUNE_WARP_SPAN: span staging threshold in percent, 0 = off
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
 
@@ -1988,6 +2222,14 @@ int launch_fuse_ck(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64
 constexpr int V2_FIXED = 256 + 4 * (FT_NT / 64) * (int)sizeof(int) + V2_MAXV * 9 * (int)sizeof(float) +
                          (2 * V2_MAXV + 4) * (int)sizeof(unsigned);  // zero pixel, red, htab, btab
 
+// k_warp_boxes' span tables (after the queue words), or none: span staging off (knob 0), or boxes for a kernel that
+// does not read them (the persistent kernel; v2 builds with 32-channel workgroups, staging everything up front or
+// the LDS homography prologue)
+inline unsigned *span_tables(unsigned *queue, bool persist) {
+    if (!queue || persist || g_warp_span_pct <= 0 || WARP_CK != 64 || WARP_STAGE_ALL || !WARP_HSCALAR) return nullptr;
+    return queue + WQ_WORDS;
+}
+
 template <int OCC>
 int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, const float *Hmat, const float *xs,
                        const float *ys, int B, int V, int C, int Hf, int Wf, float sx, float sy, int Hb, int Wb,
@@ -1998,15 +2240,17 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
     const size_t lds = (size_t)pool + V2_FIXED;
     if (!WARP_HSCALAR) boxes = nullptr;  // the in-kernel prologue (LDS homographies)
     unsigned *queue = boxes ? reinterpret_cast<unsigned *>(boxes + (int64_t)B * ntiles * V) : nullptr;
+    const bool nhwc = rpr == 0;          // channels-last output (bev_ipm_warp_fuse_nhwc_f32)
+    const bool ck = !nhwc && rpr < Hb;  // rank-chunk-major output (camera-shard partials)
+    const bool persist = g_warp_persist && boxes && !nhwc && C == 64 && mode != BEV_FUSE_MAX && TH == 16 &&
+                         WARP_CK == 64 && !WARP_STAGE_ALL && !WARP_TAPS_AHEAD;
     if (boxes && !boxes_ready) {  // else bev_ipm_warp_fuse_boxes_f32 wrote them (same geometry, pool and knobs)
         const int maxpix = pool / (V2_SL * 16) - 4;  // the kernel's own pool test
         hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
-                           st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes, queue);
+                           st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH, boxes, queue,
+                           span_tables(queue, persist), g_warp_span_pct);
     }
-    const bool nhwc = rpr == 0;          // channels-last output (bev_ipm_warp_fuse_nhwc_f32)
-    const bool ck = !nhwc && rpr < Hb;  // rank-chunk-major output (camera-shard partials)
-    if (g_warp_persist && boxes && !nhwc && C == 64 && mode != BEV_FUSE_MAX && TH == 16 && WARP_CK == 64 &&
-        !WARP_STAGE_ALL && !WARP_TAPS_AHEAD) {
+    if (persist) {
         // persistent: OCC resident workgroups per CU, a multiple of 8 (one work queue per XCD)
         const int nq = (cu_count() * OCC + 7) / 8;
         const dim3 pgrid((unsigned)(8 * nq)), pblock(FT_NT);
@@ -2046,7 +2290,7 @@ int launch_fuse_v3(const float *feats, int64_t sN, int64_t sH, int64_t sW, const
     // 3 workgroups per CU: pool + zero pixel <= 160 KiB / 3
     const int pool = g_warp_pool_kb ? g_warp_pool_kb * 1024 : ((163840 / 3 - 256 - 64) & ~1023);
     hipLaunchKernelGGL((k_warp_boxes<16, 16>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
-                       st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, pool / W3_PIX, nty, boxes, nullptr);
+                       st, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, pool / W3_PIX, nty, boxes, nullptr, nullptr, 0);
     const int fastdiv = (V >= 1 && V <= 64 && ((W3_FASTDIV_V >> (V - 1)) & 1)) ? 1 : 0;
     const size_t lds = (size_t)pool + 256;
     if (mode == BEV_FUSE_SUM)
@@ -2106,6 +2350,10 @@ int warp_tune(int knob, int value) {
             slot = &g_warp_persist;
             ok = value >= 0 && value <= 2;
             break;
+        case BEV_TUNE_WARP_SPAN:
+            slot = &g_warp_span_pct;
+            ok = value >= 0 && value <= 100;
+            break;
         default:
             return BEV_ERR_ARGS;
     }
@@ -2118,7 +2366,7 @@ int warp_tune(int knob, int value) {
 
 extern "C" {
 
-int bev_abi_version(void) { return 11; }
+int bev_abi_version(void) { return 12; }
 
 #if WARP_STAMP
 int bev_warp_stamp_read(unsigned long long *host, int n) {  // timing builds only
@@ -2174,10 +2422,11 @@ int bev_ipm_warp_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int
 int64_t bev_ipm_warp_fuse_workspace_bytes(int B, int V, int Hb, int Wb) {
     if (B < 0 || V <= 0 || Hb < 0 || Wb < 0) return BEV_ERR_ARGS;
     // per-(frame, tile, view) footprint boxes (16 x 16 tiles, v2 and v3; A/B builds of v2 with 8 x 32 tiles have as
-    // many)
+    // many), the work-queue words and the span tables
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int64_t nt = (((int64_t)Wb + TW - 1) / TW) * (((int64_t)Hb + TH - 1) / TH);
-    return BOX_HDR + (int64_t)B * nt * V * (int64_t)sizeof(uint2) + WQ_WORDS * (int64_t)sizeof(unsigned);
+    return BOX_HDR + (int64_t)B * nt * V * (int64_t)sizeof(uint2) + WQ_WORDS * (int64_t)sizeof(unsigned) +
+           (int64_t)B * nt * V * SPAN_ROWS * (int64_t)sizeof(unsigned);
 }
 
 int bev_ipm_warp_fuse_f32(const float *feats, int64_t sN, int64_t sC, int64_t sH, int64_t sW, const float *Hmat,
@@ -2232,11 +2481,12 @@ int bev_ipm_warp_fuse_boxes_f32(const float *Hmat, const float *xs, const float 
     constexpr int TH = WARP_TILE_H, TW = FT_NT / TH;
     const int ntiles = ((Wb + TW - 1) / TW) * ((Hb + TH - 1) / TH);
     const int maxpix = v2_pool_bytes(mode) / (V2_SL * 16) - 4;  // k_warp_fuse_v2's own pool test
+    unsigned *queue = reinterpret_cast<unsigned *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR +
+                                                   (int64_t)B * ntiles * V * (int64_t)sizeof(uint2));
     hipLaunchKernelGGL((k_warp_boxes<TH>), dim3((unsigned)(((int64_t)ntiles * V + 255) / 256), B), dim3(256), 0,
                        (hipStream_t)stream, Hmat, xs, ys, V, Hf, Wf, sx, sy, Hb, Wb, maxpix, (Hb + TH - 1) / TH,
-                       reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR),
-                       reinterpret_cast<unsigned *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR +
-                                                    (int64_t)B * ntiles * V * (int64_t)sizeof(uint2)));
+                       reinterpret_cast<uint2 *>(reinterpret_cast<unsigned char *>(workspace) + BOX_HDR), queue,
+                       span_tables(queue, g_warp_persist != 0), g_warp_span_pct);
     return last();
 }
 
