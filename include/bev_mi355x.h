@@ -87,8 +87,9 @@ const char *bev_build_source_hash(void);
  *   (one per XCD) / one queue (A/B options, measured slower).  Same results.
  * BEV_TUNE_WARP_SPAN: fused warp with a footprint-box workspace: span staging (each box row's tap span only) for
  *   footprints of <= 32 rows -- always where the box does not fit the LDS pool but the spans do, and where it fits
- *   when the spans need at most `value` percent of its pixels (1..100; default 50); 0 = box staging only (A/B).
- *   Same results. */
+ *   when the spans need at most `value` percent of its pixels (1..100, e.g. 50); 0 (default) = box staging only.
+ *   An A/B option: at 50 the fused kernel is ~3 % faster on the 16-camera 4K rig, but the span pass adds 5-8 us to
+ *   the box pre-pass, so the geometry stage is unchanged there and slower on the bench rig.  Same results. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3

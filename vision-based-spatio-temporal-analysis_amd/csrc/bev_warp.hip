@@ -780,15 +780,27 @@ constexpr int SPAN_ROWS = 32;          // span staging applies to boxes of at mo
 constexpr int SPAN_HDR = 144;          // LDS bytes before a span-staged image: the row bases of rows -1 .. 32 (34 ints)
 constexpr unsigned SPAN_FLAG = 0x100u;
 #ifndef WARP_SPAN_PCT
-#define WARP_SPAN_PCT 50  // fused warp v2: a footprint that fits the pool as a box is span-staged when its spans need at
-                          // most this percentage of the box's pixels (0: span staging off; oversized boxes always)
+#define WARP_SPAN_PCT 0  // fused warp v2, BEV_TUNE_WARP_SPAN's default: a footprint that fits the pool as a box is
+                         // span-staged when its spans need at most this percentage of the box's pixels (oversized boxes
+                         // always); 0 = span staging off (default: the span pass costs k_warp_boxes 5-8 us per
+                         // launch, as much as it saves the fused kernel on K5 -- profiles/r06at_warp_span_staging.txt)
 #endif
 
 // The projected corners of the BEV rectangle (image coordinates, order: c & 1 -> xb, c & 2 -> yb) and the fp32
 // margins of the tap recipe, for the per-row spans (row_spans).
 struct Quad {
     double x[4], y[4], mx, my;
+    double s[4];  // dx / dy of polygon edge e (corner ord[e] -> ord[e + 1]; 0 for a horizontal edge): quad_slopes
 };
+constexpr int QUAD_ORD[4] = {0, 1, 3, 2};  // the corners in polygon order
+
+__device__ __forceinline__ void quad_slopes(Quad &q) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int a = QUAD_ORD[e], c = QUAD_ORD[(e + 1) & 3];
+        q.s[e] = q.y[a] != q.y[c] ? (q.x[c] - q.x[a]) / (q.y[c] - q.y[a]) : 0.0;
+    }
+}
 
 // Conservative tap bbox of the BEV rectangle [xa, xb] x [ya, yb] (cell
 // centres) for homography h; ok = false when the corner bound does not apply.
@@ -852,43 +864,64 @@ __device__ Box corner_box(const float *hf, float xa, float xb, float ya, float y
     return b;
 }
 
-// Span of image row y of box bx (span table word: x0 | len << 16; 0: no tap of the tile on that row).
+// Span of box row r (image row bx.y0 + r) of box bx (span table word: x0 | len << 16; 0: no tap of the tile there).
 // A cell puts taps on row y iff its fp32 iy is in [y - 1, y + 1), so its exact iy (a point of the quad) is in the
 // band [y - 1 - my, y + 1 + my]; the exact ix of such cells lies in the x extent [lo, hi] of the quad's part inside
 // that band (a convex polygon: its vertices inside the band and its edges' crossings of the band's lines), so their
 // fp32 ix is in [lo - mx, hi + mx] and their tap columns in [floor(lo - mx), floor(hi + mx) + 1] -- clipped to the
-// (conservative) box.  Every valid tap of the tile on row y lies in the span.
-__device__ __forceinline__ unsigned row_span(const Quad &q, const Box &bx, int y) {
-    const double lo = (double)y - 1.0 - q.my - 1e-6, hi = (double)y + 1.0 + q.my + 1e-6;
-    double xl = __builtin_inf(), xh = -__builtin_inf();
-    constexpr int ord[4] = {0, 1, 3, 2};  // the corners in polygon order
+// (conservative) box.  Every valid tap of the tile on row y lies in the span.  Evaluated in fp32 relative to the box
+// origin (QuadF): the corners, slopes and margins are rounded once, and the margins widened by 1e-2 pixel plus a
+// bound on fp32 rounding at the corners' magnitude -- far above the error of the few fp32 operations per row.
+struct QuadF {
+    float x[4], y[4], s[4], mx, my;
+};
+__device__ __forceinline__ QuadF quad_f(const Quad &q, const Box &bx) {
+    QuadF f;
+    double amax = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double x = q.x[c] - (double)bx.x0, y = q.y[c] - (double)bx.y0;
+        f.x[c] = (float)x;
+        f.y[c] = (float)y;
+        amax = fmax(amax, fmax(fabs(x), fabs(y)));
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f.s[e] = (float)q.s[e];
+    const double extra = 1e-2 + 1e-6 * amax;
+    f.mx = (float)(q.mx + extra);
+    f.my = (float)(q.my + extra);
+    return f;
+}
+__device__ __forceinline__ unsigned row_span(const QuadF &q, const Box &bx, int r) {
+    const float lo = (float)r - 1.0f - q.my, hi = (float)r + 1.0f + q.my;
+    float xl = __builtin_inff(), xh = -__builtin_inff();
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-        const double px = q.x[ord[e]], py = q.y[ord[e]], qx = q.x[ord[(e + 1) & 3]], qy = q.y[ord[(e + 1) & 3]];
+        const float px = q.x[QUAD_ORD[e]], py = q.y[QUAD_ORD[e]], qy = q.y[QUAD_ORD[(e + 1) & 3]];
         if (py >= lo && py <= hi) {
-            xl = fmin(xl, px);
-            xh = fmax(xh, px);
+            xl = fminf(xl, px);
+            xh = fmaxf(xh, px);
         }
         if (py != qy) {
-            const double s = (qx - px) / (qy - py);
-            if ((lo - py) * (lo - qy) <= 0.0) {
-                const double x = px + (lo - py) * s;
-                xl = fmin(xl, x);
-                xh = fmax(xh, x);
+            const float s = q.s[e];
+            if ((lo - py) * (lo - qy) <= 0.0f) {
+                const float x = px + (lo - py) * s;
+                xl = fminf(xl, x);
+                xh = fmaxf(xh, x);
             }
-            if ((hi - py) * (hi - qy) <= 0.0) {
-                const double x = px + (hi - py) * s;
-                xl = fmin(xl, x);
-                xh = fmax(xh, x);
+            if ((hi - py) * (hi - qy) <= 0.0f) {
+                const float x = px + (hi - py) * s;
+                xl = fminf(xl, x);
+                xh = fmaxf(xh, x);
             }
         }
     }
     if (!(xl <= xh)) return 0u;
-    const double m = q.mx + 1e-6;
-    const double l = fmin(fmax(xl - m, (double)bx.x0 - 1.0), (double)bx.x1 + 2.0);
-    const double h = fmax(fmin(xh + m, (double)bx.x1 + 1.0), (double)bx.x0 - 2.0);
-    const int x0 = max((int)floor(l), bx.x0), x1 = min((int)floor(h) + 1, bx.x1);
-    return x0 <= x1 ? (unsigned)x0 | ((unsigned)(x1 - x0 + 1) << 16) : 0u;
+    const int bw = bx.x1 - bx.x0;  // relative box columns 0 .. bw
+    const float l = fminf(fmaxf(xl - q.mx, -1.0f), (float)bw + 2.0f);
+    const float h = fmaxf(fminf(xh + q.mx, (float)bw + 1.0f), -2.0f);
+    const int x0 = max((int)floorf(l), 0), x1 = min((int)floorf(h) + 1, bw);
+    return x0 <= x1 ? (unsigned)(x0 + bx.x0) | ((unsigned)(x1 - x0 + 1) << 16) : 0u;
 }
 
 // bilerp (bev_geometry.h) of 4 channels as two independent packed chains,
@@ -1814,15 +1847,32 @@ __global__ __launch_bounds__(256) void k_warp_boxes(const float *__restrict__ Hm
     }
     if (ok && cb.x1 >= 0) {
         const int bpix = (cb.x1 - cb.x0 + 1) * (cb.y1 - cb.y0 + 1), nrows = cb.y1 - cb.y0 + 1;
-        if (spans && nrows <= SPAN_ROWS) {
-            // span staging: when the box does not fit the pool but its rows' spans do, or when they save enough
-            int tot = 1;  // + the row-base header (144 B < one pixel)
-            for (int r = 0; r < nrows; ++r) tot += (int)(row_span(q, cb, cb.y0 + r) >> 16);
-            span = bpix > maxpix ? tot <= maxpix : tot * 100 <= bpix * span_pct;
-            if (span) {
-                unsigned *o = spans + (((int64_t)b * nt + tile) * V + v) * SPAN_ROWS;
-                for (int r = 0; r < nrows; ++r) o[r] = row_span(q, cb, cb.y0 + r);
+        // the spans of a row band of height 2 hold at least the quad's width across it, and every point of the quad
+        // lies in two bands: the spans total at least the quad's area -- a box that fits and is less than
+        // 100 / span_pct times that area cannot qualify (no row pass)
+        double area = 0.0;
+        if (spans) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int a = QUAD_ORD[e], c = QUAD_ORD[(e + 1) & 3];
+                area += q.x[a] * q.y[c] - q.x[c] * q.y[a];
             }
+            area = 0.5 * fabs(area);
+        }
+        if (spans && nrows <= SPAN_ROWS && (bpix > maxpix || area * 100.0 <= (double)bpix * span_pct)) {
+            // span staging: when the box does not fit the pool but its rows' spans do, or when they save enough
+            // one pass: the table is written whether or not the view ends up flagged (the fused kernel reads only
+            // flagged views' tables)
+            quad_slopes(q);
+            const QuadF qf = quad_f(q, cb);
+            unsigned *o = spans + (((int64_t)b * nt + tile) * V + v) * SPAN_ROWS;
+            int tot = 1;  // + the row-base header (144 B < one pixel)
+            for (int r = 0; r < nrows; ++r) {
+                const unsigned w = row_span(qf, cb, r);
+                o[r] = w;
+                tot += (int)(w >> 16);
+            }
+            span = bpix > maxpix ? tot <= maxpix : tot * 100 <= bpix * span_pct;
         }
         if (!span && bpix > maxpix) ok = false;
     }
