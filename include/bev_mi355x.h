@@ -89,7 +89,11 @@ const char *bev_build_source_hash(void);
  *   footprints of <= 32 rows -- always where the box does not fit the LDS pool but the spans do, and where it fits
  *   when the spans need at most `value` percent of its pixels (1..100, e.g. 50); 0 (default) = box staging only.
  *   An A/B option: at 50 the fused kernel is ~3 % faster on the 16-camera 4K rig, but the span pass adds 5-8 us to
- *   the box pre-pass, so the geometry stage is unchanged there and slower on the bench rig.  Same results. */
+ *   the box pre-pass, so the geometry stage is unchanged there and slower on the bench rig.  Same results.
+ * BEV_TUNE_WARP_TILE_BAND: fused warp (per-tile kernel) tile order inside each XCD's contiguous range: 1 = row-major
+ *   tiles, n (2..64) = bands of n tile rows walked column by column, so vertically neighbouring tiles (which share
+ *   source pixels) are resident together and share that XCD's L2; 0 (default) = bands of 4 for >= 12 views,
+ *   row-major otherwise (measured: 16-camera 4K rig -3.7 %, 7-camera rig +2.2 % with bands of 4).  Same results. */
 #define BEV_TUNE_CONV_TILE 1
 #define BEV_TUNE_WARP_POOL_KB 2
 #define BEV_TUNE_WARP_KERNEL 3
@@ -107,6 +111,7 @@ const char *bev_build_source_hash(void);
 #define BEV_TUNE_STEM3_STAGE 17
 #define BEV_TUNE_WARP_PERSIST 18
 #define BEV_TUNE_WARP_SPAN 19
+#define BEV_TUNE_WARP_TILE_BAND 20
 int bev_tune(int knob, int value);
 
 /* ---------------------------------------------------------------------------

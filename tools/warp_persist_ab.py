@@ -3,7 +3,7 @@ one-workgroup-per-tile kernel (0, k_warp_fuse_v2): bench geometry (7 cams, C = 6
 480 x 1440, B = 2, mean) or the K5 rig (--k5: 16 cams 4K, 270 x 480 maps, sum); footprint boxes computed once,
 HIP events around the fused launches alone; us per launch, HBM fraction of the algorithmic bytes, and a bit check.
 
-    python tools/warp_persist_ab.py [--k5] [--iters 20] [--rounds 4] [--pools 0:40] [--spans 0:80:100]
+    python tools/warp_persist_ab.py [--k5] [--iters 20] [--rounds 4] [--pools 0:40] [--spans 0:80:100] [--bands 1:2:4]
 """
 import argparse
 import os
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--pools", default="", help="WARP_POOL_KB values, comma- or colon-separated: A/B the per-tile kernel's pool")
     ap.add_argument("--spans", default="", help="WARP_SPAN values (colon-separated): A/B the span-staging threshold")
+    ap.add_argument("--bands", default="", help="WARP_TILE_BAND values (colon-separated): A/B the tile order")
     a = ap.parse_args()
     dev = torch.device("cuda")
     g = GeometryTransformer(480, 1440, (-24.0, 24.0, -7.2, 7.2))
@@ -48,11 +49,13 @@ def main():
         variants = [("pool", int(x)) for x in a.pools.replace(":", ",").split(",")]
     if a.spans:
         variants = [("span", int(x)) for x in a.spans.replace(":", ",").split(",")]
+    if a.bands:
+        variants = [("band", int(x)) for x in a.bands.replace(":", ",").split(",")]
     res = {v: [] for v in variants}
     ref = None
     for _ in range(a.rounds):
         for var in variants:
-            knobs = {{"persist": "WARP_PERSIST", "pool": "WARP_POOL_KB", "span": "WARP_SPAN"}[var[0]]: var[1]}
+            knobs = {{"persist": "WARP_PERSIST", "pool": "WARP_POOL_KB", "span": "WARP_SPAN", "band": "WARP_TILE_BAND"}[var[0]]: var[1]}
             with nat.tuned(**knobs):
                 bx = boxes if var[0] == "persist" else nat.warp_fuse_boxes(Hm, xs, ys, B, V, Hf, Wf, hw, mode)
                 out = nat.warp_fuse(f, Hm, xs, ys, hw, mode, boxes=bx)
@@ -71,7 +74,8 @@ def main():
     for var, v in res.items():
         us = statistics.median(v)
         name = (["per-tile", "persistent 8 queues", "persistent 1 queue"][var[1]] if var[0] == "persist"
-                else f"pool {var[1]} KiB" if var[0] == "pool" else f"span {var[1]} %")
+                else f"pool {var[1]} KiB" if var[0] == "pool" else f"span {var[1]} %" if var[0] == "span"
+                else f"tile band {var[1]}")
         print(f"{name:20s} {us:8.2f} us  frac {alg / (us * 1e-6) / 8e12:.4f}  "
               f"(all: {', '.join(f'{x:.1f}' for x in v)})", flush=True)
 

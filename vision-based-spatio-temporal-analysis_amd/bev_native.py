@@ -264,6 +264,7 @@ TUNE_CONV_X6_NT = 16
 TUNE_STEM3_STAGE = 17
 TUNE_WARP_PERSIST = 18
 TUNE_WARP_SPAN = 19
+TUNE_WARP_TILE_BAND = 20
 WARP_KERNEL_DMA, WARP_KERNEL_REGISTER = 0, 1
 
 

@@ -1050,7 +1050,7 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
                                                           const float *__restrict__ xs, const float *__restrict__ ys,
                                                           int B, int V, int C, int Hf, int Wf, float sx, float sy,
                                                           int Hb, int Wb, float *__restrict__ out, int pool,
-                                                          const uint2 *__restrict__ boxes_in, int rpr) {
+                                                          const uint2 *__restrict__ boxes_in, int rpr, int tband) {
     constexpr int NW = FT_NT / 64;  // 4 waves
     constexpr int TW = FT_NT / TH;  // tile width in cells
     constexpr int CK = WARP_CK, SL = V2_SL, PS = SL * 16;  // channels / DMA slots / bytes per staged pixel (+ pad)
@@ -1065,6 +1065,11 @@ __global__ __launch_bounds__(FT_NT, OCC) void k_warp_fuse_v2(const float *__rest
     {
         const int q = nt / 8, r = nt % 8, x = tile % 8;
         tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + tile / 8;
+    }
+    if (tband > 1) {  // order index -> tile: bands of tband tile rows walked column by column (BEV_TUNE_WARP_TILE_BAND)
+        const int band = tile / (tband * ntx), k = tile - band * (tband * ntx);
+        const int bh = min(tband, nty - band * tband);
+        tile = (band * tband + k % bh) * ntx + k / bh;
     }
     const int tyb = tile / ntx, txb = tile - tyb * ntx;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2212,6 +2217,11 @@ int g_warp_bwd_pool = 0; // BEV_TUNE_WARP_BWD_POOL: backward LDS image in floats
 // 150.2 / 247.6, 1 queue 145.6 / 245.7 -- slower: see k_warp_fuse_p (the store drain the next DMA waits behind).
 int g_warp_persist = 0;
 int g_warp_span_pct = WARP_SPAN_PCT;  // BEV_TUNE_WARP_SPAN: span staging threshold in percent, 0 = off
+// BEV_TUNE_WARP_TILE_BAND: fused warp v2 tile order, 1 = row-major, n = bands of n tile rows walked column by column,
+// 0 = automatic: bands of 4 for >= 12 views (read-heavy: the 16-camera 4K rig's warp 228.9 -> 220.5 us and its reads
+// 479 -> 366 MB per launch), row-major otherwise (store-heavy: the 7-camera bench rig's output rows stay contiguous
+// across the resident tiles; bands of 4 there 134.5 -> 137.4 us) -- profiles/r06bf_warp_tile_band_ab.txt
+int g_warp_tile_band = 0;
 
 constexpr int FUSE_LDS_BYTES = 60 * 1024;  // register-staged kernel's footprint image
 
@@ -2314,7 +2324,7 @@ int launch_fuse_v2_occ(const float *feats, int64_t sN, int64_t sH, int64_t sW, c
     }
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, lds, st, feats, sN, sH, sW, Hmat, xs, ys, B, V, C, Hf, Wf, sx, sy, Hb, Wb,
-                           out, pool, boxes, rpr);
+                           out, pool, boxes, rpr, g_warp_tile_band > 0 ? g_warp_tile_band : (V >= 12 ? 4 : 1));
     };
     if (nhwc) {
         if (mode == BEV_FUSE_SUM) go(k_warp_fuse_v2<BEV_FUSE_SUM, OCC, TH, false, true>);
@@ -2403,6 +2413,10 @@ int warp_tune(int knob, int value) {
         case BEV_TUNE_WARP_SPAN:
             slot = &g_warp_span_pct;
             ok = value >= 0 && value <= 100;
+            break;
+        case BEV_TUNE_WARP_TILE_BAND:
+            slot = &g_warp_tile_band;
+            ok = value >= 0 && value <= 64;
             break;
         default:
             return BEV_ERR_ARGS;
