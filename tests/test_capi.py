@@ -92,7 +92,9 @@ def test_tune_knobs_host_only(lib):
                             (nat.TUNE_WGRAD_MFMA, 0, 3), (nat.TUNE_CONV_X6_TILE, 2, 3),
                             (nat.TUNE_CONV_X6_KERNEL, 1, 3), (nat.TUNE_CONV_H16_KERNEL, 1, 4),
                             (nat.TUNE_CONV_PW_SMALL, 0, 5),
-                            (nat.TUNE_DW_RUN, 1, 4), (nat.TUNE_CONV_X6_NT, 1, 2)):
+                            (nat.TUNE_DW_RUN, 1, 4), (nat.TUNE_CONV_X6_NT, 1, 2),
+                            (nat.TUNE_STEM3_STAGE, 1, 3), (nat.TUNE_WARP_PERSIST, 2, 3),
+                            (nat.TUNE_WARP_SPAN, 50, 101), (nat.TUNE_WARP_TILE_BAND, 4, 65)):
         old = lib.bev_tune(knob, good)
         assert old >= 0
         assert lib.bev_tune(knob, bad) == -1
@@ -100,6 +102,10 @@ def test_tune_knobs_host_only(lib):
     with nat.tuned(WARP_KERNEL=1, WARP_POOL_KB=8):
         assert lib.bev_tune(nat.TUNE_WARP_KERNEL, 1) == 1
     assert lib.bev_tune(nat.TUNE_WARP_KERNEL, 0) == 0  # the default kernel stays selected
+    # the round-6 warp knobs' defaults: span staging off, automatic tile bands, the per-tile kernel
+    assert lib.bev_tune(nat.TUNE_WARP_SPAN, 0) == 0
+    assert lib.bev_tune(nat.TUNE_WARP_TILE_BAND, 0) == 0
+    assert lib.bev_tune(nat.TUNE_WARP_PERSIST, 0) == 0
 
 
 def test_no_environment_knobs_in_library():
